@@ -1,0 +1,1190 @@
+/*
+ * bb_oracle.c -- CPU fp64 restatement of the reference's hot path:
+ *   `mujoco.mj_step(model, data)` for ballbot_gym/models/ballbot.xml with the
+ *   tools/mujoco_fix.patch contact frame, and the BBotSimulation.step glue.
+ *
+ * TEST INFRASTRUCTURE ONLY (see bb_oracle.h).  This is the parity checker;
+ * the shipped HIP path lives in openballbot-rl_amd/csrc and never calls it.
+ *
+ * Physics parity vs. real MuJoCo: UNPINNED (MuJoCo is not in /root/reference
+ * and cannot be built or imported here).  The algorithms
+ * below follow MuJoCo's published pipeline and are deliberately written in
+ * MuJoCo's *general* form (tree loops, com-based spatial vectors, dense J,
+ * dense Newton) so that they are independent of the specialised GPU kernel:
+ *   kinematics        mj_kinematics            (engine_core_smooth.c)
+ *   com/cinert/cdof   mj_comPos
+ *   mass matrix       sum_b J_b' I_b J_b (== mj_crb result)
+ *   cvel/cdof_dot     mj_comVel
+ *   bias              mj_rne(flg_acc=0)
+ *   passive/actuator  hinge damping (ballbot.xml:58), motor gear 1 (:84-86)
+ *   collision         mjraw_SphereCapsule + mujoco_fix.patch:11-16 frame,
+ *                     mju_makeFrame, mjc_ConvexHField prism decomposition
+ *   constraint        mj_instantiateContact / mj_makeImpedance (elliptic)
+ *   solver            Newton on the primal cost (mj_solNewton); the minimiser
+ *                     is unique (M > 0), so any convergent method reproduces it
+ *   integrator        mj_RungeKutta(N=4) + mj_advance + mj_integratePos
+ *   env glue          ballbot_env.py:897-1036 (obs A10, reward A12, term A13)
+ */
+#include "bb_oracle.h"
+
+#include <math.h>
+#include <string.h>
+#include <float.h>
+#include <stdlib.h>
+#include <stdio.h>
+
+#define NQ BBO_NQ
+#define NV BBO_NV
+#define NB BBO_NBODY
+#define MJMINVAL 1e-15
+#define MJMINIMP 0.0001
+#define MJMAXIMP 0.9999
+
+static const double PI = 3.14159265358979323846;
+
+/* ------------------------------------------------------------------ options */
+static int g_flags = 0;
+static int g_maxiter = 100;          /* MuJoCo default opt.iterations */
+static double g_tol = 1e-10;         /* tighter than MuJoCo's 1e-8 (oracle) */
+
+int bbo_abi_version(void) { return 3; }
+void bbo_set_flags(int flags) { g_flags = flags; }
+int bbo_get_flags(void) { return g_flags; }
+void bbo_set_solver(int maxiter, double tol) { g_maxiter = maxiter; g_tol = tol; }
+
+/* ------------------------------------------------------------- small maths */
+static void v3copy(double* r, const double* a) { r[0] = a[0]; r[1] = a[1]; r[2] = a[2]; }
+static void v3add(double* r, const double* a, const double* b) { for (int i = 0; i < 3; i++) r[i] = a[i] + b[i]; }
+static void v3sub(double* r, const double* a, const double* b) { for (int i = 0; i < 3; i++) r[i] = a[i] - b[i]; }
+static void v3scl(double* r, const double* a, double s) { for (int i = 0; i < 3; i++) r[i] = a[i] * s; }
+static double v3dot(const double* a, const double* b) { return a[0] * b[0] + a[1] * b[1] + a[2] * b[2]; }
+static double v3norm(const double* a) { return sqrt(v3dot(a, a)); }
+static void v3cross(double* r, const double* a, const double* b) {
+  double t[3] = {a[1] * b[2] - a[2] * b[1], a[2] * b[0] - a[0] * b[2], a[0] * b[1] - a[1] * b[0]};
+  v3copy(r, t);
+}
+static double v3normalize(double* a) {
+  double n = v3norm(a);
+  if (n < MJMINVAL) { a[0] = 1; a[1] = 0; a[2] = 0; return 0; }
+  v3scl(a, a, 1.0 / n);
+  return n;
+}
+/* 3x3 row-major */
+static void m3v(double* r, const double* m, const double* v) {
+  double t[3];
+  for (int i = 0; i < 3; i++) t[i] = m[3 * i] * v[0] + m[3 * i + 1] * v[1] + m[3 * i + 2] * v[2];
+  v3copy(r, t);
+}
+static inline void m3tv(double* r, const double* m, const double* v) {
+  double t[3];
+  for (int i = 0; i < 3; i++) t[i] = m[i] * v[0] + m[3 + i] * v[1] + m[6 + i] * v[2];
+  v3copy(r, t);
+}
+static void m3mul(double* r, const double* a, const double* b) {
+  double t[9];
+  for (int i = 0; i < 3; i++)
+    for (int j = 0; j < 3; j++) t[3 * i + j] = a[3 * i] * b[j] + a[3 * i + 1] * b[3 + j] + a[3 * i + 2] * b[6 + j];
+  memcpy(r, t, sizeof t);
+}
+static void m3mulT(double* r, const double* a, const double* b) { /* a * b' */
+  double t[9];
+  for (int i = 0; i < 3; i++)
+    for (int j = 0; j < 3; j++) t[3 * i + j] = a[3 * i] * b[3 * j] + a[3 * i + 1] * b[3 * j + 1] + a[3 * i + 2] * b[3 * j + 2];
+  memcpy(r, t, sizeof t);
+}
+/* quaternions (w,x,y,z) */
+static void qmul(double* r, const double* a, const double* b) {
+  double t[4] = {a[0] * b[0] - a[1] * b[1] - a[2] * b[2] - a[3] * b[3],
+                 a[0] * b[1] + a[1] * b[0] + a[2] * b[3] - a[3] * b[2],
+                 a[0] * b[2] - a[1] * b[3] + a[2] * b[0] + a[3] * b[1],
+                 a[0] * b[3] + a[1] * b[2] - a[2] * b[1] + a[3] * b[0]};
+  memcpy(r, t, sizeof t);
+}
+static void qnormalize(double* q) {
+  double n = sqrt(q[0] * q[0] + q[1] * q[1] + q[2] * q[2] + q[3] * q[3]);
+  if (n < MJMINVAL) { q[0] = 1; q[1] = q[2] = q[3] = 0; return; }
+  for (int i = 0; i < 4; i++) q[i] /= n;
+}
+static void q2mat(double* m, const double* q) { /* mju_quat2Mat */
+  if (q[0] == 1 && q[1] == 0 && q[2] == 0 && q[3] == 0) {
+    memset(m, 0, 9 * sizeof(double)); m[0] = m[4] = m[8] = 1; return;
+  }
+  double q00 = q[0] * q[0], q01 = q[0] * q[1], q02 = q[0] * q[2], q03 = q[0] * q[3];
+  double q11 = q[1] * q[1], q12 = q[1] * q[2], q13 = q[1] * q[3];
+  double q22 = q[2] * q[2], q23 = q[2] * q[3], q33 = q[3] * q[3];
+  m[0] = q00 + q11 - q22 - q33; m[4] = q00 - q11 + q22 - q33; m[8] = q00 - q11 - q22 + q33;
+  m[1] = 2 * (q12 - q03); m[2] = 2 * (q13 + q02); m[3] = 2 * (q12 + q03);
+  m[5] = 2 * (q23 - q01); m[6] = 2 * (q13 - q02); m[7] = 2 * (q23 + q01);
+}
+static void axisangle2quat(double* q, const double* axis, double angle) {
+  if (angle == 0) { q[0] = 1; q[1] = q[2] = q[3] = 0; return; }
+  double s = sin(angle * 0.5);
+  q[0] = cos(angle * 0.5); q[1] = axis[0] * s; q[2] = axis[1] * s; q[3] = axis[2] * s;
+}
+/* MJCF euler, degrees, default eulerseq "xyz" (intrinsic): q = qx*qy*qz */
+static void euler2quat(double* q, double ax, double ay, double az) {
+  double e[3] = {ax * PI / 180, ay * PI / 180, az * PI / 180};
+  q[0] = 1; q[1] = q[2] = q[3] = 0;
+  for (int i = 0; i < 3; i++) {
+    double r[4] = {cos(e[i] / 2), 0, 0, 0};
+    r[1 + i] = sin(e[i] / 2);
+    qmul(q, q, r);
+  }
+}
+/* mju_quatIntegrate: q <- normalize(q) * exp(vel*scale/2) */
+static void quat_integrate(double* q, const double* vel, double scale) {
+  double axis[3] = {vel[0], vel[1], vel[2]};
+  double angle = scale * v3normalize(axis);
+  double qrot[4];
+  axisangle2quat(qrot, axis, angle);
+  qnormalize(q);
+  qmul(q, q, qrot);
+}
+
+/* ------------------------------------------------------------ model table */
+/* ballbot.xml:38-79.  Body 0 world, 1 base, 2 cam_0_body, 3 cam_1_body,
+ * 4..6 wheel_0..2, 7 ball. */
+static const int body_parent[NB] = {-1, 0, 1, 1, 1, 1, 1, 0};
+static const int body_root[NB] = {0, 1, 1, 1, 1, 1, 1, 7};
+static const double HINGE_AXIS[3] = {-0.15316554764123935, -0.6903189805903613, -0.7071067953657663};
+static const double HINGE_POS[3] = {0, 0, 0.0293};           /* ballbot.xml:58 */
+static const double HINGE_ARMATURE = 0.005, HINGE_DAMPING = 0.8;
+static const double BALL_R = 0.09, BALL_RHO = 55.0;           /* ballbot.xml:78 */
+static const double BALL_GPOS[3] = {0, 0, -0.14};
+static const double WHEEL_R = 0.025, WHEEL_HH = 0.02, WHEEL_RHO = 620.0; /* :57 */
+static const double WHEEL_GPOS[3] = {-0.018, -0.08, -0.053};
+static const double HF_SIZE[4] = {5, 5, 2.0, 0.1};            /* ballbot.xml:23 */
+static const double TIMESTEP = 0.002;                         /* ballbot.xml:3 */
+static const double GRAVITY = 9.81;                           /* MuJoCo default */
+
+typedef struct {
+  int compiled;
+  double body_pos[NB][3], body_quat[NB][4];
+  double mass[NB], ipos[NB][3], inertia[NB][9]; /* full tensor about COM, body frame */
+  double jnt_axis[3];                            /* normalised hinge axis */
+  double wheel_gquat[4], wheel_gmat[9];          /* wheel capsule orientation in wheel frame */
+  double qpos0[NQ];
+  double invweight_tran[NB], invweight_rot[NB];
+  double meaninertia;
+  double ball_mass;
+} Model;
+static Model M_;
+
+static void add_geom_inertia(int b, double m, const double* pos, const double* gmat, const double* Idiag,
+                             double* msum, double* mcom, double* Isum_origin) {
+  /* accumulate mass, first moment and inertia about the BODY ORIGIN */
+  double Ig[9], tmp[9], D[9] = {Idiag[0], 0, 0, 0, Idiag[1], 0, 0, 0, Idiag[2]};
+  m3mul(tmp, gmat, D); m3mulT(Ig, tmp, gmat);
+  double p2 = v3dot(pos, pos);
+  for (int i = 0; i < 3; i++)
+    for (int j = 0; j < 3; j++) Isum_origin[3 * i + j] += Ig[3 * i + j] + m * ((i == j ? p2 : 0) - pos[i] * pos[j]);
+  *msum += m;
+  for (int i = 0; i < 3; i++) mcom[i] += m * pos[i];
+  (void)b;
+}
+
+static void capsule_inertia(double rho, double r, double hh, double* m, double* I) {
+  double h = 2 * hh;
+  double ms = rho * 4.0 / 3.0 * PI * r * r * r, mc = rho * PI * r * r * h;
+  *m = ms + mc;
+  I[0] = I[1] = mc * (3 * r * r + h * h) / 12 + ms * (0.4 * r * r + 0.25 * h * h + 0.375 * h * r);
+  I[2] = mc * r * r / 2 + ms * 0.4 * r * r;
+}
+
+static void z2mat(double* R, const double* vec) { /* mjuu_z2quat then quat2mat */
+  double z[3] = {0, 0, 1}, axis[3], v[3] = {vec[0], vec[1], vec[2]}, q[4];
+  v3normalize(v);
+  v3cross(axis, z, v);
+  double s = v3normalize(axis);
+  if (s < 1e-10) { axis[0] = 1; axis[1] = 0; axis[2] = 0; }
+  double ang = atan2(s, v[2]);
+  axisangle2quat(q, axis, ang);
+  q2mat(R, q);
+}
+
+static void finish_body(int b, double msum, const double* mcom, const double* Iorig) {
+  Model* m = &M_;
+  m->mass[b] = msum;
+  if (msum <= 0) { memset(m->ipos[b], 0, 3 * sizeof(double)); memset(m->inertia[b], 0, 9 * sizeof(double)); return; }
+  double c[3]; v3scl(c, mcom, 1.0 / msum);
+  v3copy(m->ipos[b], c);
+  double c2 = v3dot(c, c);
+  for (int i = 0; i < 3; i++)
+    for (int j = 0; j < 3; j++) m->inertia[b][3 * i + j] = Iorig[3 * i + j] - msum * ((i == j ? c2 : 0) - c[i] * c[j]);
+}
+
+static void kinematics_all(const double* qpos, double xpos[NB][3], double xquat[NB][4], double xmat[NB][9],
+                           double xipos[NB][3], double xI[NB][9], double xanchor[3][3], double xaxis[3][3]);
+static void build_M(const double xmat[NB][9], const double xpos[NB][3], const double xipos[NB][3],
+                    const double xI[NB][9], const double xanchor[3][3], const double xaxis[3][3],
+                    double subtree_com[NB][3], double cinert[NB][36], double cdof[NV][6], double* Mout);
+static int chol(double* A, int n);
+static void chol_solve(const double* L, int n, double* x);
+
+static void compile_model(void) {
+  Model* m = &M_;
+  if (m->compiled) return;
+  memset(m, 0, sizeof *m);
+  double I3[9] = {1, 0, 0, 0, 1, 0, 0, 0, 1};
+  /* body frames (ballbot.xml:38,44,50,56,61,67,76) */
+  for (int b = 0; b < NB; b++) { m->body_quat[b][0] = 1; }
+  m->body_pos[1][2] = 0.24;
+  m->body_pos[2][0] = 0.17; m->body_pos[2][1] = -0.01; m->body_pos[2][2] = -0.06;
+  euler2quat(m->body_quat[2], 180, -30, 0);
+  m->body_pos[3][0] = -0.17; m->body_pos[3][1] = -0.01; m->body_pos[3][2] = -0.06;
+  euler2quat(m->body_quat[3], 180, 30, 0);
+  for (int k = 0; k < 3; k++) {
+    m->body_pos[4 + k][2] = -0.001;
+    euler2quat(m->body_quat[4 + k], 0, 0, 120.0 * k);
+  }
+  m->body_pos[7][2] = 0.26;
+  v3copy(m->jnt_axis, HINGE_AXIS);
+  v3normalize(m->jnt_axis);
+  euler2quat(m->wheel_gquat, -45, 9, 0);
+  q2mat(m->wheel_gmat, m->wheel_gquat);
+
+  /* inertia from geoms (mjCBody inertia from geoms; compiler inertiagrouprange 0..5) */
+  {
+    /* base: tower cylinder (:41) + ballast box (:42, contype 0 but has mass) */
+    double ms = 0, mc[3] = {0}, Io[9] = {0};
+    double r = 0.11, hh = 0.14, rho = 23.6;
+    double mcyl = rho * PI * r * r * 2 * hh;
+    double Icyl[3] = {mcyl * (3 * r * r + 4 * hh * hh) / 12, mcyl * (3 * r * r + 4 * hh * hh) / 12, mcyl * r * r / 2};
+    double p1[3] = {0, 0, 0.2};
+    add_geom_inertia(1, mcyl, p1, I3, Icyl, &ms, mc, Io);
+    double a = 0.1, mb = 400.0 * 8 * a * a * a;
+    double Ibox[3] = {mb * (a * a + a * a) / 3, mb * (a * a + a * a) / 3, mb * (a * a + a * a) / 3};
+    double p2[3] = {0, 0, 0.002};
+    add_geom_inertia(1, mb, p2, I3, Ibox, &ms, mc, Io);
+    finish_body(1, ms, mc, Io);
+  }
+  for (int c = 0; c < 2; c++) {
+    /* cam_k_stick capsule fromto (0,0,0)->(-+0.2,0,0), r 0.01, density 1000 (:46,:52).
+     * cam_k_geom is a mesh whose asset (meshes/cone.stl) is absent from the
+     * reference (.gitignore:178): treated as massless, non-colliding. */
+    double ms = 0, mc[3] = {0}, Io[9] = {0};
+    double to[3] = {c == 0 ? -0.2 : 0.2, 0, 0};
+    double pos[3] = {to[0] / 2, 0, 0}, R[9], mcap, Icap[3];
+    z2mat(R, to);
+    capsule_inertia(1000.0, 0.01, 0.1, &mcap, Icap);
+    add_geom_inertia(2 + c, mcap, pos, R, Icap, &ms, mc, Io);
+    finish_body(2 + c, ms, mc, Io);
+  }
+  for (int k = 0; k < 3; k++) {
+    double ms = 0, mc[3] = {0}, Io[9] = {0}, mw, Iw[3];
+    capsule_inertia(WHEEL_RHO, WHEEL_R, WHEEL_HH, &mw, Iw);
+    add_geom_inertia(4 + k, mw, WHEEL_GPOS, m->wheel_gmat, Iw, &ms, mc, Io);
+    finish_body(4 + k, ms, mc, Io);
+  }
+  {
+    double ms = 0, mc[3] = {0}, Io[9] = {0};
+    double mball = BALL_RHO * 4.0 / 3.0 * PI * BALL_R * BALL_R * BALL_R;
+    double Ib[3] = {0.4 * mball * BALL_R * BALL_R, 0.4 * mball * BALL_R * BALL_R, 0.4 * mball * BALL_R * BALL_R};
+    add_geom_inertia(7, mball, BALL_GPOS, I3, Ib, &ms, mc, Io);
+    finish_body(7, ms, mc, Io);
+    m->ball_mass = mball;
+  }
+  /* qpos0 */
+  memset(m->qpos0, 0, sizeof m->qpos0);
+  m->qpos0[2] = 0.24; m->qpos0[3] = 1;
+  m->qpos0[12] = 0.26; m->qpos0[13] = 1;
+
+  /* set0: invweight0 and meaninertia at qpos0 (mj_setConst) */
+  double xpos[NB][3], xquat[NB][4], xmat[NB][9], xipos[NB][3], xI[NB][9], xanc[3][3], xax[3][3];
+  double scom[NB][3], cin[NB][36], cdof[NV][6], Mm[NV * NV];
+  m->compiled = 1; /* kinematics uses the tables above */
+  kinematics_all(m->qpos0, xpos, xquat, xmat, xipos, xI, xanc, xax);
+  build_M(xmat, xpos, xipos, xI, xanc, xax, scom, cin, cdof, Mm);
+  double tr = 0;
+  for (int i = 0; i < NV; i++) tr += Mm[i * NV + i];
+  m->meaninertia = tr / NV;
+  double L[NV * NV];
+  memcpy(L, Mm, sizeof L);
+  chol(L, NV);
+  for (int b = 1; b < NB; b++) {
+    /* jacobian at body COM: jacp = cdof_lin + cdof_ang x (xipos - subtree_com[root]) */
+    double jac[6][NV];
+    memset(jac, 0, sizeof jac);
+    for (int d = 0; d < NV; d++) {
+      int in_chain = 0;
+      if (d < 6) in_chain = (b >= 1 && b <= 6);
+      else if (d < 9) in_chain = (b == 4 + (d - 6));
+      else in_chain = (b == 7);
+      if (!in_chain) continue;
+      double off[3], w[3];
+      v3sub(off, xipos[b], scom[body_root[b]]);
+      v3cross(w, cdof[d], off);
+      for (int i = 0; i < 3; i++) { jac[i][d] = cdof[d][3 + i] + w[i]; jac[3 + i][d] = cdof[d][i]; }
+    }
+    double A[6] = {0};
+    for (int i = 0; i < 6; i++) {
+      double x[NV];
+      for (int d = 0; d < NV; d++) x[d] = jac[i][d];
+      chol_solve(L, NV, x);
+      double s = 0;
+      for (int d = 0; d < NV; d++) s += jac[i][d] * x[d];
+      A[i] = s;
+    }
+    m->invweight_tran[b] = (A[0] + A[1] + A[2]) / 3;
+    m->invweight_rot[b] = (A[3] + A[4] + A[5]) / 3;
+  }
+}
+
+void bbo_model_info(double* out) {
+  compile_model();
+  Model* m = &M_;
+  /* [0..7] masses, [8..15] invweight_tran, [16..23] invweight_rot, [24] meaninertia,
+   * [25..41] qpos0, [42..44] wheel0 ipos, [45..53] base inertia */
+  for (int b = 0; b < NB; b++) { out[b] = m->mass[b]; out[8 + b] = m->invweight_tran[b]; out[16 + b] = m->invweight_rot[b]; }
+  out[24] = m->meaninertia;
+  for (int i = 0; i < NQ; i++) out[25 + i] = m->qpos0[i];
+  for (int i = 0; i < 3; i++) out[42 + i] = m->ipos[4][i];
+  for (int i = 0; i < 9; i++) out[45 + i] = m->inertia[1][i];
+}
+
+/* ---------------------------------------------------------- mj_kinematics */
+static void kinematics_all(const double* qpos, double xpos[NB][3], double xquat[NB][4], double xmat[NB][9],
+                           double xipos[NB][3], double xI[NB][9], double xanchor[3][3], double xaxis[3][3]) {
+  Model* m = &M_;
+  memset(xpos[0], 0, 3 * sizeof(double));
+  xquat[0][0] = 1; xquat[0][1] = xquat[0][2] = xquat[0][3] = 0;
+  q2mat(xmat[0], xquat[0]);
+  for (int b = 1; b < NB; b++) {
+    int p = body_parent[b];
+    if (b == 1 || b == 7) { /* free joint */
+      int a = (b == 1) ? 0 : 10;
+      v3copy(xpos[b], qpos + a);
+      memcpy(xquat[b], qpos + a + 3, 4 * sizeof(double));
+      qnormalize(xquat[b]);
+    } else {
+      double t[3];
+      m3v(t, xmat[p], m->body_pos[b]);
+      v3add(xpos[b], xpos[p], t);
+      qmul(xquat[b], xquat[p], m->body_quat[b]);
+      if (b >= 4) { /* hinge */
+        int k = b - 4;
+        double R[9];
+        q2mat(R, xquat[b]);
+        m3v(t, R, HINGE_POS);
+        v3add(xanchor[k], xpos[b], t);
+        m3v(xaxis[k], R, m->jnt_axis);
+        double ql[4];
+        axisangle2quat(ql, m->jnt_axis, qpos[7 + k] - m->qpos0[7 + k]);
+        qmul(xquat[b], xquat[b], ql);
+        q2mat(R, xquat[b]);
+        m3v(t, R, HINGE_POS);
+        v3sub(xpos[b], xanchor[k], t);
+      }
+      qnormalize(xquat[b]);
+    }
+    q2mat(xmat[b], xquat[b]);
+    double t[3], tmp[9];
+    m3v(t, xmat[b], m->ipos[b]);
+    v3add(xipos[b], xpos[b], t);
+    m3mul(tmp, xmat[b], m->inertia[b]);
+    m3mulT(xI[b], tmp, xmat[b]);
+  }
+}
+
+/* body chain membership of dof d */
+static int dof_in_chain(int d, int b) {
+  if (d < 6) return b >= 1 && b <= 6;
+  if (d < 9) return b == 4 + (d - 6);
+  return b == 7;
+}
+static int dof_body(int d) { return d < 6 ? 1 : (d < 9 ? 4 + (d - 6) : 7); }
+
+/* mj_comPos (subtree_com, cinert, cdof) + M = sum_b J_b' cinert_b J_b + armature */
+static void build_M(const double xmat[NB][9], const double xpos[NB][3], const double xipos[NB][3],
+                    const double xI[NB][9], const double xanchor[3][3], const double xaxis[3][3],
+                    double subtree_com[NB][3], double cinert[NB][36], double cdof[NV][6], double* Mout) {
+  Model* m = &M_;
+  /* subtree com per tree root */
+  for (int r = 0; r < NB; r++) { subtree_com[r][0] = subtree_com[r][1] = subtree_com[r][2] = 0; }
+  double msum1 = 0;
+  double c1[3] = {0, 0, 0};
+  for (int b = 1; b <= 6; b++) { msum1 += m->mass[b]; for (int i = 0; i < 3; i++) c1[i] += m->mass[b] * xipos[b][i]; }
+  for (int i = 0; i < 3; i++) c1[i] /= msum1;
+  for (int b = 1; b <= 6; b++) v3copy(subtree_com[b], c1); /* per-body subtree com (only root's is used) */
+  /* true per-body subtree com for the base is c1; store root values */
+  v3copy(subtree_com[1], c1);
+  v3copy(subtree_com[7], xipos[7]);
+  /* cinert: spatial inertia at subtree_com[root], ordering (ang; lin) */
+  for (int b = 1; b < NB; b++) {
+    double* I6 = cinert[b];
+    memset(I6, 0, 36 * sizeof(double));
+    double r[3];
+    v3sub(r, xipos[b], subtree_com[body_root[b]]);
+    double mm = m->mass[b];
+    double rx[9] = {0, -r[2], r[1], r[2], 0, -r[0], -r[1], r[0], 0};
+    double rr = v3dot(r, r);
+    for (int i = 0; i < 3; i++)
+      for (int j = 0; j < 3; j++) {
+        I6[6 * i + j] = xI[b][3 * i + j] + mm * ((i == j ? rr : 0) - r[i] * r[j]);
+        I6[6 * i + 3 + j] = mm * rx[3 * i + j];
+        I6[6 * (3 + i) + j] = mm * rx[3 * j + i];
+        I6[6 * (3 + i) + 3 + j] = (i == j) ? mm : 0;
+      }
+  }
+  /* cdof */
+  for (int d = 0; d < NV; d++) memset(cdof[d], 0, 6 * sizeof(double));
+  for (int t = 0; t < 2; t++) {
+    int b = t == 0 ? 1 : 7, da = t == 0 ? 0 : 9;
+    for (int i = 0; i < 3; i++) cdof[da + i][3 + i] = 1;
+    double off[3];
+    v3sub(off, subtree_com[b], xpos[b]);
+    for (int i = 0; i < 3; i++) {
+      double ax[3] = {xmat[b][i], xmat[b][3 + i], xmat[b][6 + i]};
+      v3copy(cdof[da + 3 + i], ax);
+      v3cross(cdof[da + 3 + i] + 3, ax, off);
+    }
+  }
+  for (int k = 0; k < 3; k++) {
+    double off[3];
+    v3sub(off, subtree_com[1], xanchor[k]);
+    v3copy(cdof[6 + k], xaxis[k]);
+    v3cross(cdof[6 + k] + 3, xaxis[k], off);
+  }
+  /* M */
+  memset(Mout, 0, NV * NV * sizeof(double));
+  for (int b = 1; b < NB; b++) {
+    double IS[NV][6];
+    for (int d = 0; d < NV; d++) {
+      if (!dof_in_chain(d, b)) continue;
+      for (int i = 0; i < 6; i++) {
+        double s = 0;
+        for (int j = 0; j < 6; j++) s += cinert[b][6 * i + j] * cdof[d][j];
+        IS[d][i] = s;
+      }
+    }
+    for (int d1 = 0; d1 < NV; d1++) {
+      if (!dof_in_chain(d1, b)) continue;
+      for (int d2 = 0; d2 < NV; d2++) {
+        if (!dof_in_chain(d2, b)) continue;
+        double s = 0;
+        for (int i = 0; i < 6; i++) s += cdof[d1][i] * IS[d2][i];
+        Mout[d1 * NV + d2] += s;
+      }
+    }
+  }
+  for (int k = 0; k < 3; k++) Mout[(6 + k) * NV + 6 + k] += HINGE_ARMATURE;
+}
+
+/* ------------------------------------------------------------ dense linalg */
+static int chol(double* A, int n) { /* in place, lower */
+  for (int j = 0; j < n; j++) {
+    double s = A[j * n + j];
+    for (int k = 0; k < j; k++) s -= A[j * n + k] * A[j * n + k];
+    if (s <= 0) return -1;
+    double d = sqrt(s);
+    A[j * n + j] = d;
+    for (int i = j + 1; i < n; i++) {
+      double t = A[i * n + j];
+      for (int k = 0; k < j; k++) t -= A[i * n + k] * A[j * n + k];
+      A[i * n + j] = t / d;
+    }
+  }
+  return 0;
+}
+static void chol_solve(const double* L, int n, double* x) {
+  for (int i = 0; i < n; i++) {
+    double s = x[i];
+    for (int k = 0; k < i; k++) s -= L[i * n + k] * x[k];
+    x[i] = s / L[i * n + i];
+  }
+  for (int i = n - 1; i >= 0; i--) {
+    double s = x[i];
+    for (int k = i + 1; k < n; k++) s -= L[k * n + i] * x[k];
+    x[i] = s / L[i * n + i];
+  }
+}
+
+/* ---------------------------------------------------------- spatial algebra */
+static void cross_motion(double* r, const double* v, const double* u) { /* v xm u */
+  double t[6], a[3], b[3];
+  v3cross(t, v, u);
+  v3cross(a, v, u + 3);
+  v3cross(b, v + 3, u);
+  v3add(t + 3, a, b);
+  memcpy(r, t, sizeof t);
+}
+static void cross_force(double* r, const double* v, const double* f) { /* v xf f */
+  double t[6], a[3], b[3];
+  v3cross(a, v, f);
+  v3cross(b, v + 3, f + 3);
+  v3add(t, a, b);
+  v3cross(t + 3, v, f + 3);
+  memcpy(r, t, sizeof t);
+}
+static void mul6(double* r, const double* I6, const double* v) {
+  double t[6];
+  for (int i = 0; i < 6; i++) { double s = 0; for (int j = 0; j < 6; j++) s += I6[6 * i + j] * v[j]; t[i] = s; }
+  memcpy(r, t, sizeof t);
+}
+
+/* ------------------------------------------------------------- collision */
+typedef struct {
+  double dist, pos[3], frame[9];
+  int body2;   /* 4..6 wheel (geom1 = ball), 7 = ball (geom1 = hfield) */
+  double mu, fr[2];
+} Contact;
+
+/* mju_makeFrame: normalise x, default/orthogonalise y, z = x cross y */
+static void make_frame(double* f) {
+  v3normalize(f);
+  if (v3norm(f + 3) < 0.5) {
+    f[3] = f[4] = f[5] = 0;
+    if (fabs(f[1]) < 0.5) f[4] = 1; else f[5] = 1;
+  }
+  double t[3];
+  v3scl(t, f, v3dot(f, f + 3));
+  v3sub(f + 3, f + 3, t);
+  v3normalize(f + 3);
+  v3cross(f + 6, f, f + 3);
+}
+
+/* closest point on triangle abc to p (Ericson, Real-Time Collision Detection 5.1.5) */
+static void closest_pt_triangle(double* res, const double* p, const double* a, const double* b, const double* c) {
+  double ab[3], ac[3], ap[3], bp[3], cp[3];
+  v3sub(ab, b, a); v3sub(ac, c, a); v3sub(ap, p, a);
+  double d1 = v3dot(ab, ap), d2 = v3dot(ac, ap);
+  if (d1 <= 0 && d2 <= 0) { v3copy(res, a); return; }
+  v3sub(bp, p, b);
+  double d3 = v3dot(ab, bp), d4 = v3dot(ac, bp);
+  if (d3 >= 0 && d4 <= d3) { v3copy(res, b); return; }
+  double vc = d1 * d4 - d3 * d2;
+  if (vc <= 0 && d1 >= 0 && d3 <= 0) { double v = d1 / (d1 - d3); for (int i = 0; i < 3; i++) res[i] = a[i] + v * ab[i]; return; }
+  v3sub(cp, p, c);
+  double d5 = v3dot(ab, cp), d6 = v3dot(ac, cp);
+  if (d6 >= 0 && d5 <= d6) { v3copy(res, c); return; }
+  double vb = d5 * d2 - d1 * d6;
+  if (vb <= 0 && d2 >= 0 && d6 <= 0) { double w = d2 / (d2 - d6); for (int i = 0; i < 3; i++) res[i] = a[i] + w * ac[i]; return; }
+  double va = d3 * d6 - d5 * d4;
+  if (va <= 0 && (d4 - d3) >= 0 && (d5 - d6) >= 0) {
+    double w = (d4 - d3) / ((d4 - d3) + (d5 - d6));
+    for (int i = 0; i < 3; i++) res[i] = b[i] + w * (c[i] - b[i]);
+    return;
+  }
+  double denom = 1.0 / (va + vb + vc), v = vb * denom, w = vc * denom;
+  for (int i = 0; i < 3; i++) res[i] = a[i] + ab[i] * v + ac[i] * w;
+}
+
+/* Exact sphere (center c, radius r) vs triangular prism (top vertices T[3],
+ * bottom plane z=zb) penetration: the minimum-translation result that the
+ * convex penetration solver of mjc_ConvexHField converges to.
+ * Returns 1 on contact with dist <= 0; fills dist, normal (prism -> sphere), pos. */
+static int sphere_prism(const double* c, double r, double T[3][3], double zb, double* dist, double* n, double* pos) {
+  double B[3][3];
+  for (int i = 0; i < 3; i++) { B[i][0] = T[i][0]; B[i][1] = T[i][1]; B[i][2] = zb; }
+  /* inside test: xy in triangle, above bottom, below top plane */
+  double e1[3], e2[3], nt[3];
+  v3sub(e1, T[1], T[0]); v3sub(e2, T[2], T[0]);
+  v3cross(nt, e1, e2);
+  if (nt[2] < 0) v3scl(nt, nt, -1);
+  v3normalize(nt); /* top face outward normal (z >= 0) */
+  /* 2D barycentric sign test */
+  double area = (T[1][0] - T[0][0]) * (T[2][1] - T[0][1]) - (T[2][0] - T[0][0]) * (T[1][1] - T[0][1]);
+  int inside_xy = 1;
+  double sgn = area > 0 ? 1 : -1;
+  double eout[3][3]; double edist[3];
+  for (int i = 0; i < 3; i++) {
+    const double* P = T[i]; const double* Q = T[(i + 1) % 3];
+    double ex = Q[0] - P[0], ey = Q[1] - P[1];
+    double cr = ex * (c[1] - P[1]) - ey * (c[0] - P[0]);
+    if (cr * sgn < 0) inside_xy = 0;
+    /* outward 2D normal of edge */
+    double nx = ey * sgn, ny = -ex * sgn, nl = sqrt(nx * nx + ny * ny);
+    eout[i][0] = nx / nl; eout[i][1] = ny / nl; eout[i][2] = 0;
+    edist[i] = fabs(cr) / nl; /* distance of c to edge line (inside) */
+  }
+  double dtop = v3dot(nt, T[0]) - v3dot(nt, c); /* >0 when c below top plane */
+  if (inside_xy && c[2] >= zb && dtop >= 0) {
+    /* c inside prism: exit through nearest face */
+    double best = dtop; double nb[3]; v3copy(nb, nt);
+    if (c[2] - zb < best) { best = c[2] - zb; nb[0] = 0; nb[1] = 0; nb[2] = -1; }
+    for (int i = 0; i < 3; i++) if (edist[i] < best) { best = edist[i]; v3copy(nb, eout[i]); }
+    *dist = -best - r;
+    v3copy(n, nb);
+    for (int i = 0; i < 3; i++) pos[i] = c[i] - n[i] * (r + *dist / 2);
+    return 1;
+  }
+  /* outside: closest point over the 5 faces (8 triangles) */
+  double best = 1e300, q[3], qb[3];
+  const double* tri[8][3] = {
+      {T[0], T[1], T[2]}, {B[0], B[1], B[2]},
+      {T[0], T[1], B[1]}, {T[0], B[1], B[0]},
+      {T[1], T[2], B[2]}, {T[1], B[2], B[1]},
+      {T[2], T[0], B[0]}, {T[2], B[0], B[2]}};
+  for (int f = 0; f < 8; f++) {
+    closest_pt_triangle(q, c, tri[f][0], tri[f][1], tri[f][2]);
+    double dd[3]; v3sub(dd, c, q);
+    double d2 = v3dot(dd, dd);
+    if (d2 < best) { best = d2; v3copy(qb, q); }
+  }
+  double d = sqrt(best);
+  if (d > r) return 0;
+  if (d > 1e-12) { v3sub(n, c, qb); v3scl(n, n, 1.0 / d); }
+  else { v3copy(n, nt); }
+  *dist = d - r;
+  for (int i = 0; i < 3; i++) pos[i] = c[i] - n[i] * (r + *dist / 2);
+  return 1;
+}
+
+static int collide(const double xpos[NB][3], const double xmat[NB][9], const float* hf, double size_z,
+                   Contact* con, int* nground_out, int* overflow) {
+  Model* m = &M_;
+  int n = 0;
+  double c[3], t[3];
+  m3v(t, xmat[7], BALL_GPOS);
+  v3add(c, xpos[7], t);
+  /* explicit pairs ballbot.xml:90-92: the_ball x wheel_mesh_k, condim 3,
+   * friction (0.001, 1.0).  mjraw_SphereCapsule (+ mujoco_fix.patch). */
+  for (int k = 0; k < 3; k++) {
+    int b = 4 + k;
+    double gp[3], gm[9];
+    m3v(t, xmat[b], WHEEL_GPOS);
+    v3add(gp, xpos[b], t);
+    m3mul(gm, xmat[b], m->wheel_gmat);
+    double axis[3] = {gm[2], gm[5], gm[8]};
+    double vec[3];
+    v3sub(vec, c, gp);
+    double x = v3dot(axis, vec);
+    if (x > WHEEL_HH) x = WHEEL_HH;
+    if (x < -WHEEL_HH) x = -WHEEL_HH;
+    double near[3];
+    for (int i = 0; i < 3; i++) near[i] = gp[i] + axis[i] * x;
+    double dif[3];
+    v3sub(dif, near, c);
+    double cdist = v3norm(dif);
+    double dist = cdist - BALL_R - WHEEL_R;
+    if (dist > 0) continue;
+    Contact* cc = &con[n++];
+    memset(cc, 0, sizeof *cc);
+    cc->dist = dist;
+    if (cdist > 0) v3scl(cc->frame, dif, 1.0 / cdist);
+    else { cc->frame[0] = 1; }
+    v3copy(cc->frame + 3, axis); /* mujoco_fix.patch:15 */
+    make_frame(cc->frame);
+    for (int i = 0; i < 3; i++) cc->pos[i] = c[i] + cc->frame[i] * (BALL_R + dist / 2);
+    cc->body2 = b;
+    cc->fr[0] = 0.001; cc->fr[1] = 1.0;
+  }
+  int nground = 0;
+  *overflow = 0;
+  if (hf) {
+    /* mjc_ConvexHField: hfield geom at origin, identity frame (ballbot.xml:35) */
+    double xmin = c[0] - BALL_R, xmax = c[0] + BALL_R, ymin = c[1] - BALL_R, ymax = c[1] + BALL_R;
+    double zmin = c[2] - BALL_R, zmax = c[2] + BALL_R;
+    const double sx = HF_SIZE[0], sy = HF_SIZE[1], zb = HF_SIZE[3];
+    const int nrow = BBO_HF_N, ncol = BBO_HF_N;
+    if (!(xmin > sx || xmax < -sx || ymin > sy || ymax < -sy || zmin > size_z || zmax < -zb)) {
+      int cmin = (int)floor((xmin + sx) / (2 * sx) * (ncol - 1));
+      int cmax = (int)ceil((xmax + sx) / (2 * sx) * (ncol - 1));
+      int rmin = (int)floor((ymin + sy) / (2 * sy) * (nrow - 1));
+      int rmax = (int)ceil((ymax + sy) / (2 * sy) * (nrow - 1));
+      if (cmin < 0) cmin = 0;
+      if (cmax > ncol - 1) cmax = ncol - 1;
+      if (rmin < 0) rmin = 0;
+      if (rmax > nrow - 1) rmax = nrow - 1;
+      double dx = 2 * sx / (ncol - 1), dy = 2 * sy / (nrow - 1);
+      for (int r = rmin; r < rmax; r++) {
+        double win[3][3] = {{0}};
+        int nvert = 0;
+        for (int cc = cmin; cc <= cmax; cc++) {
+          for (int i = 0; i < 2; i++) {
+            win[0][0] = win[1][0]; win[0][1] = win[1][1]; win[0][2] = win[1][2];
+            win[1][0] = win[2][0]; win[1][1] = win[2][1]; win[1][2] = win[2][2];
+            win[2][0] = dx * cc - sx;
+            win[2][1] = dy * (r + i) - sy;
+            win[2][2] = (double)hf[(r + i) * ncol + cc] * size_z;
+            nvert++;
+            if (nvert <= 2) continue;
+            if (win[0][2] < zmin && win[1][2] < zmin && win[2][2] < zmin) continue;
+            double dist, nn[3], pos[3];
+            if (!sphere_prism(c, BALL_R, win, -zb, &dist, nn, pos)) continue;
+            if (nground >= BBO_MAXGROUND) { *overflow = 1; continue; }
+            Contact* g = &con[n++];
+            memset(g, 0, sizeof *g);
+            g->dist = dist;
+            v3copy(g->frame, nn);
+            make_frame(g->frame);
+            v3copy(g->pos, pos);
+            g->body2 = 7;
+            g->fr[0] = 1.0; g->fr[1] = 1.0; /* max(geom friction) = (1,1,0.005,..) */
+            nground++;
+          }
+        }
+      }
+    }
+  }
+  *nground_out = nground;
+  return n;
+}
+
+/* ----------------------------------------------------------- constraints */
+static double impedance(double pos) { /* getImpedance with solimp (0.9,0.95,0.001,0.5,2) */
+  const double s0 = 0.9, s1 = 0.95, w = 0.001, mid = 0.5, pw = 2;
+  double x = pos / w;
+  if (x < 0) x = -x;
+  if (x >= 1 || x <= 0) return x >= 1 ? s1 : s0;
+  double y;
+  if (x <= mid) y = pow(x, pw) / pow(mid, pw - 1);
+  else y = 1 - pow(1 - x, pw) / pow(1 - mid, pw - 1);
+  return s0 + y * (s1 - s0);
+}
+
+typedef struct {
+  int nc;
+  double J[BBO_MAXCON * 3][NV];
+  double aref[BBO_MAXCON * 3], D[BBO_MAXCON * 3];
+  double mu[BBO_MAXCON], fr[BBO_MAXCON][2];
+} Efc;
+
+/* contact cost/force/hessian for one elliptic condim-3 contact (mj_constraintUpdate) */
+static double cone_eval(const double* jar, double mu, const double* fr, const double* D, double* force, double H[3][3]) {
+  double U0 = jar[0] * mu, U1 = jar[1] * fr[0], U2 = jar[2] * fr[1];
+  double N = U0, T = sqrt(U1 * U1 + U2 * U2);
+  double cost = 0;
+  if (H) memset(H, 0, 9 * sizeof(double));
+  if (N >= mu * T || (T <= 0 && N >= 0)) { /* top zone */
+    force[0] = force[1] = force[2] = 0;
+  } else if (mu * N + T <= 0 || (T <= 0 && N < 0)) { /* bottom zone */
+    for (int j = 0; j < 3; j++) { force[j] = -D[j] * jar[j]; cost += 0.5 * D[j] * jar[j] * jar[j]; if (H) H[j][j] = D[j]; }
+  } else { /* middle zone */
+    double Dm = D[0] / (mu * mu * (1 + mu * mu));
+    double g = N - mu * T;
+    cost = 0.5 * Dm * g * g;
+    double Ut[2] = {U1, U2};
+    double grad[3] = {mu, -mu * fr[0] * U1 / T, -mu * fr[1] * U2 / T};
+    for (int j = 0; j < 3; j++) force[j] = -Dm * g * grad[j];
+    if (H) {
+      for (int a = 0; a < 3; a++)
+        for (int b = 0; b < 3; b++) H[a][b] = Dm * grad[a] * grad[b];
+      for (int a = 0; a < 2; a++)
+        for (int b = 0; b < 2; b++) {
+          double h2 = -mu * fr[a] * fr[b] * ((a == b ? 1.0 / T : 0) - Ut[a] * Ut[b] / (T * T * T));
+          H[1 + a][1 + b] += Dm * g * h2;
+        }
+    }
+  }
+  return cost;
+}
+
+static double total_cost(const Efc* e, const double* jar, double* force, double* Hrows /*nullable*/) {
+  double cost = 0;
+  for (int c = 0; c < e->nc; c++) {
+    double H[3][3];
+    cost += cone_eval(jar + 3 * c, e->mu[c], e->fr[c], e->D + 3 * c, force + 3 * c, Hrows ? H : NULL);
+    if (Hrows) memcpy(Hrows + 9 * c, H, sizeof H);
+  }
+  return cost;
+}
+
+/* Newton solve of min 0.5(a-a0)'M(a-a0) + s(Ja - aref) (mj_solNewton) */
+static int newton(const Efc* e, const double* Mm, const double* a0, double* a, double scale) {
+  int nr = 3 * e->nc, it;
+  double jar[BBO_MAXCON * 3], force[BBO_MAXCON * 3], Hc[BBO_MAXCON * 9];
+  for (it = 0; it < g_maxiter; it++) {
+    for (int r = 0; r < nr; r++) { double s = -e->aref[r]; for (int d = 0; d < NV; d++) s += e->J[r][d] * a[d]; jar[r] = s; }
+    total_cost(e, jar, force, Hc);
+    double grad[NV], dq[NV];
+    for (int d = 0; d < NV; d++) dq[d] = a[d] - a0[d];
+    for (int i = 0; i < NV; i++) {
+      double s = 0;
+      for (int j = 0; j < NV; j++) s += Mm[i * NV + j] * dq[j];
+      for (int r = 0; r < nr; r++) s -= e->J[r][i] * force[r];
+      grad[i] = s;
+    }
+    double gn = 0;
+    for (int i = 0; i < NV; i++) gn += grad[i] * grad[i];
+    if (g_flags & 256) fprintf(stderr, "it %d gn %.3e\n", it, scale * sqrt(gn));
+    if (scale * sqrt(gn) < g_tol) break;
+    double H[NV * NV];
+    memcpy(H, Mm, sizeof H);
+    for (int c = 0; c < e->nc; c++) {
+      const double* C = Hc + 9 * c;
+      for (int p = 0; p < 3; p++)
+        for (int q = 0; q < 3; q++) {
+          double w = C[3 * p + q];
+          if (w == 0) continue;
+          for (int i = 0; i < NV; i++) {
+            double ji = e->J[3 * c + p][i];
+            if (ji == 0) continue;
+            for (int j = 0; j < NV; j++) H[i * NV + j] += ji * w * e->J[3 * c + q][j];
+          }
+        }
+    }
+    if (chol(H, NV)) break;
+    double s[NV];
+    for (int i = 0; i < NV; i++) s[i] = -grad[i];
+    chol_solve(H, NV, s);
+    /* exact line search on phi(alpha) */
+    double Ms[NV], sMs = 0, sMdq = 0, Js[BBO_MAXCON * 3];
+    for (int i = 0; i < NV; i++) { double t = 0; for (int j = 0; j < NV; j++) t += Mm[i * NV + j] * s[j]; Ms[i] = t; }
+    for (int i = 0; i < NV; i++) { sMs += s[i] * Ms[i]; sMdq += Ms[i] * dq[i]; }
+    for (int r = 0; r < nr; r++) { double t = 0; for (int d = 0; d < NV; d++) t += e->J[r][d] * s[d]; Js[r] = t; }
+    double lo = 0, hi = -1, alpha = 1, d0 = 0;
+    double jt[BBO_MAXCON * 3], ft[BBO_MAXCON * 3], Ht[BBO_MAXCON * 9];
+    for (int r = 0; r < nr; r++) d0 -= force[r] * Js[r];
+    d0 += sMdq;
+    if (d0 >= 0) break; /* not a descent direction: converged to roundoff */
+    for (int ls = 0; ls < 200; ls++) {
+      for (int r = 0; r < nr; r++) jt[r] = jar[r] + alpha * Js[r];
+      total_cost(e, jt, ft, Ht);
+      double d1 = sMdq + alpha * sMs, d2 = sMs;
+      for (int c = 0; c < e->nc; c++) {
+        for (int p = 0; p < 3; p++) {
+          d1 -= ft[3 * c + p] * Js[3 * c + p];
+          for (int q = 0; q < 3; q++) d2 += Js[3 * c + p] * Ht[9 * c + 3 * p + q] * Js[3 * c + q];
+        }
+      }
+      if (fabs(d1) <= 1e-15 * fabs(d0)) break;
+      if (d1 < 0) lo = alpha; else hi = alpha;
+      double an = alpha - d1 / d2;
+      if (hi < 0) { if (an <= lo) an = 2 * alpha; }
+      else if (!(an > lo && an < hi)) an = 0.5 * (lo + hi);
+      if (hi >= 0 && hi - lo <= 1e-16 * hi) break;
+      alpha = an;
+    }
+    if (g_flags & 256) fprintf(stderr, "   alpha %.6e d0 %.3e\n", alpha, d0);
+    double snorm = 0, anorm = 0;
+    for (int i = 0; i < NV; i++) { a[i] += alpha * s[i]; snorm += (alpha * s[i]) * (alpha * s[i]); anorm += a[i] * a[i]; }
+    /* roundoff floor: the step no longer moves qacc */
+    if (sqrt(snorm) <= 1e-15 * (1 + sqrt(anorm))) { it++; break; }
+  }
+  return it;
+}
+
+/* -------------------------------------------------------------- forward */
+typedef struct {
+  double xpos[NB][3], xquat[NB][4], xmat[NB][9], xipos[NB][3], xI[NB][9];
+  double xanchor[3][3], xaxis[3][3];
+  double scom[NB][3], cinert[NB][36], cdof[NV][6], cdof_dot[NV][6], cvel[NB][6];
+  double M[NV * NV];
+} Work;
+
+static void forward_impl(const double* qpos, const double* qvel, const double* ctrl, double* warm_io,
+                         const float* hf, double size_z, bbo_forward_out* out) {
+  compile_model();
+  Model* m = &M_;
+  static __thread Work W_;
+  Work* w = &W_;
+  kinematics_all(qpos, w->xpos, w->xquat, w->xmat, w->xipos, w->xI, w->xanchor, w->xaxis);
+  build_M(w->xmat, w->xpos, w->xipos, w->xI, w->xanchor, w->xaxis, w->scom, w->cinert, w->cdof, w->M);
+
+  /* mj_comVel: cvel, cdof_dot */
+  memset(w->cvel, 0, sizeof w->cvel);
+  for (int b = 1; b < NB; b++) {
+    int p = body_parent[b];
+    double cv[6];
+    memcpy(cv, w->cvel[p], sizeof cv);
+    if (b == 1 || b == 7) {
+      int da = (b == 1) ? 0 : 9;
+      for (int i = 0; i < 3; i++) { memset(w->cdof_dot[da + i], 0, 6 * sizeof(double)); }
+      for (int i = 0; i < 3; i++) for (int j = 0; j < 6; j++) cv[j] += w->cdof[da + i][j] * qvel[da + i];
+      for (int i = 3; i < 6; i++) cross_motion(w->cdof_dot[da + i], cv, w->cdof[da + i]);
+      for (int i = 3; i < 6; i++) for (int j = 0; j < 6; j++) cv[j] += w->cdof[da + i][j] * qvel[da + i];
+    } else if (b >= 4) {
+      int d = 6 + (b - 4);
+      cross_motion(w->cdof_dot[d], cv, w->cdof[d]);
+      for (int j = 0; j < 6; j++) cv[j] += w->cdof[d][j] * qvel[d];
+    }
+    memcpy(w->cvel[b], cv, sizeof cv);
+  }
+
+  /* mj_rne(flg_acc = 0): qfrc_bias */
+  double cacc[NB][6], cfrc[NB][6];
+  memset(cacc, 0, sizeof cacc);
+  if (!(g_flags & BBO_DISABLE_GRAVITY)) cacc[0][5] = GRAVITY;
+  for (int b = 1; b < NB; b++) {
+    int p = body_parent[b];
+    memcpy(cacc[b], cacc[p], 6 * sizeof(double));
+    for (int d = 0; d < NV; d++)
+      if (dof_body(d) == b)
+        for (int j = 0; j < 6; j++) cacc[b][j] += w->cdof_dot[d][j] * qvel[d];
+    double Iv[6], t1[6], t2[6];
+    mul6(t1, w->cinert[b], cacc[b]);
+    mul6(Iv, w->cinert[b], w->cvel[b]);
+    cross_force(t2, w->cvel[b], Iv);
+    for (int j = 0; j < 6; j++) cfrc[b][j] = t1[j] + t2[j];
+  }
+  for (int b = NB - 1; b >= 1; b--) {
+    int p = body_parent[b];
+    if (p > 0) for (int j = 0; j < 6; j++) cfrc[p][j] += cfrc[b][j];
+  }
+  double bias[NV], fsmooth[NV], a0[NV];
+  for (int d = 0; d < NV; d++) {
+    int b = dof_body(d);
+    double s = 0;
+    for (int j = 0; j < 6; j++) s += w->cdof[d][j] * cfrc[b][j];
+    bias[d] = s;
+  }
+  for (int d = 0; d < NV; d++) fsmooth[d] = -bias[d];
+  for (int k = 0; k < 3; k++) {
+    if (!(g_flags & BBO_DISABLE_DAMPING)) fsmooth[6 + k] -= HINGE_DAMPING * qvel[6 + k];
+    fsmooth[6 + k] += ctrl ? ctrl[k] : 0;
+  }
+  double L[NV * NV];
+  memcpy(L, w->M, sizeof L);
+  chol(L, NV);
+  memcpy(a0, fsmooth, sizeof a0);
+  chol_solve(L, NV, a0);
+
+  /* collision + constraints */
+  Contact con[BBO_MAXCON];
+  int nground = 0, overflow = 0;
+  int nc = 0;
+  if (!(g_flags & BBO_DISABLE_CONTACT)) nc = collide(w->xpos, w->xmat, hf, size_z, con, &nground, &overflow);
+  static __thread Efc E;
+  E.nc = nc;
+  const double dmax = 0.95, tc = fmax(0.02, 2 * TIMESTEP), dr = 1.0;
+  const double K = 1 / fmax(MJMINVAL, dmax * dmax * tc * tc * dr * dr), Bd = 2 / fmax(MJMINVAL, dmax * tc);
+  for (int c = 0; c < nc; c++) {
+    Contact* cc = &con[c];
+    /* jacdif = jac(body2, pos) - jac(body1, pos); body1 = ball for wheel pairs, world for hfield */
+    double jd[3][NV];
+    memset(jd, 0, sizeof jd);
+    int b2 = cc->body2, b1 = (b2 == 7) ? 0 : 7;
+    for (int side = 0; side < 2; side++) {
+      int b = side == 0 ? b2 : b1;
+      double sg = side == 0 ? 1 : -1;
+      if (b == 0) continue;
+      for (int d = 0; d < NV; d++) {
+        if (!dof_in_chain(d, b)) continue;
+        double off[3], x[3];
+        v3sub(off, cc->pos, w->scom[body_root[b]]);
+        v3cross(x, w->cdof[d], off);
+        for (int i = 0; i < 3; i++) jd[i][d] += sg * (w->cdof[d][3 + i] + x[i]);
+      }
+    }
+    for (int rr = 0; rr < 3; rr++)
+      for (int d = 0; d < NV; d++) E.J[3 * c + rr][d] = cc->frame[3 * rr] * jd[0][d] + cc->frame[3 * rr + 1] * jd[1][d] + cc->frame[3 * rr + 2] * jd[2][d];
+    double tran = m->invweight_tran[b1] + m->invweight_tran[b2];
+    double imp = impedance(cc->dist);
+    if (imp < MJMINIMP) imp = MJMINIMP;
+    if (imp > MJMAXIMP) imp = MJMAXIMP;
+    double R0 = fmax(MJMINVAL, (1 - imp) * tran / imp);
+    double R1 = R0 / 1.0; /* impratio = 1 */
+    double mu = cc->fr[0] * sqrt(R1 / R0);
+    double R2 = R1 * cc->fr[0] * cc->fr[0] / (cc->fr[1] * cc->fr[1]);
+    E.D[3 * c] = 1 / R0; E.D[3 * c + 1] = 1 / R1; E.D[3 * c + 2] = 1 / R2;
+    E.mu[c] = mu; E.fr[c][0] = cc->fr[0]; E.fr[c][1] = cc->fr[1];
+    for (int rr = 0; rr < 3; rr++) {
+      double vel = 0;
+      for (int d = 0; d < NV; d++) vel += E.J[3 * c + rr][d] * qvel[d];
+      double pos = rr == 0 ? cc->dist : 0;
+      E.aref[3 * c + rr] = -Bd * vel - K * imp * pos;
+    }
+  }
+  double a[NV];
+  int niter = 0;
+  if (nc == 0) memcpy(a, a0, sizeof a);
+  else {
+    if (warm_io) memcpy(a, warm_io, sizeof a); else memcpy(a, a0, sizeof a);
+    for (int i = 0; i < NV; i++) if (!isfinite(a[i])) { memcpy(a, a0, sizeof a); break; }
+    niter = newton(&E, w->M, a0, a, 1.0 / (m->meaninertia * NV));
+  }
+  if (warm_io) memcpy(warm_io, a, sizeof a);
+
+  if (out) {
+    memcpy(out->qacc, a, sizeof a);
+    memcpy(out->qacc_smooth, a0, sizeof a0);
+    memcpy(out->qfrc_bias, bias, sizeof bias);
+    memcpy(out->M, w->M, sizeof w->M);
+    v3copy(out->xpos_base, w->xpos[1]);
+    memcpy(out->xquat_base, w->xquat[1], 4 * sizeof(double));
+    memcpy(out->cvel_base, w->cvel[1], 6 * sizeof(double));
+    v3copy(out->subtree_com_base, w->scom[1]);
+    out->ncon = nc; out->nground = nground; out->niter = niter; out->ground_overflow = overflow;
+    for (int c = 0; c < nc && c < BBO_MAXCON; c++) {
+      out->con_dist[c] = con[c].dist;
+      memcpy(out->con_pos + 3 * c, con[c].pos, 3 * sizeof(double));
+      memcpy(out->con_frame + 9 * c, con[c].frame, 9 * sizeof(double));
+      out->con_body2[c] = con[c].body2;
+    }
+    double ek = 0;
+    for (int i = 0; i < NV; i++) for (int j = 0; j < NV; j++) ek += 0.5 * qvel[i] * w->M[i * NV + j] * qvel[j];
+    double ep = 0;
+    for (int b = 1; b < NB; b++) ep += m->mass[b] * GRAVITY * w->xipos[b][2];
+    out->energy_kin = ek; out->energy_pot = ep;
+  }
+}
+
+void bbo_forward(const double* qpos, const double* qvel, const double* ctrl, const double* warm,
+                 const float* hfield, double size_z, bbo_forward_out* out) {
+  double w[NV];
+  if (warm) memcpy(w, warm, sizeof w);
+  forward_impl(qpos, qvel, ctrl, warm ? w : NULL, hfield, size_z, out);
+}
+
+/* mj_integratePos */
+static void integrate_pos(double* qpos, const double* v, double h) {
+  for (int t = 0; t < 2; t++) {
+    int qa = t == 0 ? 0 : 10, da = t == 0 ? 0 : 9;
+    for (int i = 0; i < 3; i++) qpos[qa + i] += h * v[da + i];
+    quat_integrate(qpos + qa + 3, v + da + 3, h);
+  }
+  for (int k = 0; k < 3; k++) qpos[7 + k] += h * v[6 + k];
+}
+
+/* mj_step with integrator RK4: mj_forward, then mj_RungeKutta(m, d, 4) */
+void bbo_mj_step(double* qpos, double* qvel, double* warm, const double* ctrl,
+                 const float* hfield, double size_z, bbo_forward_out* stage4) {
+  static const double A[3] = {0.5, 0.5, 1.0}; /* RK4 A (sub)diagonal */
+  static const double B[4] = {1.0 / 6, 1.0 / 3, 1.0 / 3, 1.0 / 6};
+  const double h = TIMESTEP;
+  double q0[NQ], v0[NV], X[4][NV], F[4][NV];
+  memcpy(q0, qpos, sizeof q0);
+  memcpy(v0, qvel, sizeof v0);
+  bbo_forward_out tmp;
+  bbo_forward_out* o = stage4 ? stage4 : &tmp;
+  forward_impl(q0, v0, ctrl, warm, hfield, size_z, o);
+  memcpy(X[0], v0, sizeof v0);
+  memcpy(F[0], o->qacc, sizeof F[0]);
+  for (int i = 1; i < 4; i++) {
+    double dxv[NV], dxa[NV], q[NQ], v[NV];
+    for (int d = 0; d < NV; d++) { dxv[d] = A[i - 1] * X[i - 1][d]; dxa[d] = A[i - 1] * F[i - 1][d]; }
+    memcpy(q, q0, sizeof q);
+    integrate_pos(q, dxv, h);
+    for (int d = 0; d < NV; d++) v[d] = v0[d] + h * dxa[d];
+    forward_impl(q, v, ctrl, warm, hfield, size_z, o);
+    memcpy(X[i], v, sizeof v);
+    memcpy(F[i], o->qacc, sizeof F[i]);
+  }
+  double dv[NV], da[NV];
+  for (int d = 0; d < NV; d++) {
+    dv[d] = B[0] * X[0][d] + B[1] * X[1][d] + B[2] * X[2][d] + B[3] * X[3][d];
+    da[d] = B[0] * F[0][d] + B[1] * F[1][d] + B[2] * F[2][d] + B[3] * F[3][d];
+  }
+  /* mj_advance: qvel += h*qacc_rk, integratePos(qpos, v_rk, h) */
+  for (int d = 0; d < NV; d++) qvel[d] = v0[d] + h * da[d];
+  memcpy(qpos, q0, sizeof q0);
+  integrate_pos(qpos, dv, h);
+}
+
+/* ---------------------------------------------------------------- env glue */
+void bbo_quat_to_rotvec(const double* q, double* rv) {
+  /* numpy-quaternion: as_rotation_vector(q) = 2 * log(q).vec ; quaternion_log */
+  const double EPS = 1e-14;
+  double b = sqrt(q[1] * q[1] + q[2] * q[2] + q[3] * q[3]);
+  if (fabs(b) <= EPS * fabs(q[0])) {
+    if (q[0] < 0) { rv[0] = 2 * PI; rv[1] = rv[2] = 0; }
+    else { rv[0] = rv[1] = rv[2] = 0; }
+    return;
+  }
+  double v = atan2(b, q[0]), f = v / b;
+  rv[0] = 2 * f * q[1]; rv[1] = 2 * f * q[2]; rv[2] = 2 * f * q[3];
+}
+
+static float clipf(float x, float lo, float hi) { return x < lo ? lo : (x > hi ? hi : x); }
+
+void bbo_reset_state(double offset, double* qpos, double* qvel, double* warm) {
+  compile_model();
+  memcpy(qpos, M_.qpos0, NQ * sizeof(double));
+  qpos[2] += offset;   /* ballbot_env.py:616 */
+  qpos[12] += offset;  /* ballbot_env.py:617 */
+  memset(qvel, 0, NV * sizeof(double));
+  if (warm) memset(warm, 0, NV * sizeof(double));
+}
+
+double bbo_init_offset(const float* hf, double size_z) {
+  /* ballbot_env.py:527-565 with the ball geom at (0,0,0.12) after mj_forward(qpos0) */
+  const int n = BBO_HF_N;
+  double sz = HF_SIZE[0];
+  double cell = sz / n;          /* quirk: size/nrows, not 2*size/(nrows-1) */
+  int center = n / 2;
+  double amin[2] = {-BALL_R, -BALL_R}, amax[2] = {BALL_R, BALL_R};
+  int x0 = center - abs((int)floor(amin[0] / cell));
+  int x1 = center + (int)floor(amax[0] / cell) + 1;
+  int y0 = center - abs((int)floor(amin[1] / cell));
+  int y1 = center + (int)floor(amax[1] / cell) + 1;
+  double mx = -1e300;
+  for (int i = x0; i < x1; i++)
+    for (int j = y0; j < y1; j++) { double v = hf ? (double)hf[i * n + j] : 0.0; if (v > mx) mx = v; }
+  return mx * size_z + 0.01;
+}
+
+static int state_bad(const double* qpos, const double* qvel) {
+  for (int i = 0; i < NQ; i++) if (!isfinite(qpos[i]) || fabs(qpos[i]) > 1e10) return 1;
+  for (int i = 0; i < NV; i++) if (!isfinite(qvel[i]) || fabs(qvel[i]) > 1e10) return 1;
+  return 0;
+}
+
+int bbo_env_step(const bbo_env_cfg* cfg, double* qpos, double* qvel, double* warm, int* step_counter,
+                 const float* action, const float* hfield, double size_z, float* obs15, float* reward,
+                 float* pos2d, double* tilt_deg) {
+  /* action -> ctrl (ballbot_env.py:903-907): f32 math, then negated into f64 ctrl */
+  float mwv = (float)cfg->max_wheel_velocity;
+  double ctrl[3];
+  for (int k = 0; k < 3; k++) {
+    float c = action[k] * mwv;
+    c = clipf(c, -mwv, mwv);
+    ctrl[k] = -(double)c;
+  }
+  bbo_forward_out s4;
+  bbo_mj_step(qpos, qvel, warm, ctrl, hfield, size_z, &s4);
+  int diverged = state_bad(qpos, qvel);
+
+  /* _get_obs (ballbot_env.py:771-811) from stage-4 xquat/cvel and final qvel */
+  double rv[3];
+  bbo_quat_to_rotvec(s4.xquat_base, rv);
+  float orient[3] = {(float)rv[0], (float)rv[1], (float)rv[2]};
+  float motor[3];
+  for (int k = 0; k < 3; k++) { /* qvel[joint id k+1]: base dofs 1,2,3 */
+    float v = (float)qvel[1 + k];
+    v = v / mwv;
+    motor[k] = clipf(v, -2.0f, 2.0f);
+  }
+  float vel[3], angv[3];
+  for (int i = 0; i < 3; i++) {
+    vel[i] = clipf((float)s4.cvel_base[i], -2.0f, 2.0f);
+    angv[i] = clipf((float)s4.cvel_base[3 + i], -2.0f, 2.0f);
+  }
+  /* sorted keys: actions, angular_vel, motor_state, orientation, vel */
+  for (int i = 0; i < 3; i++) {
+    obs15[i] = action[i]; obs15[3 + i] = angv[i]; obs15[6 + i] = motor[i];
+    obs15[9 + i] = orient[i]; obs15[12 + i] = vel[i];
+  }
+  if (pos2d) { pos2d[0] = (float)s4.xpos_base[0]; pos2d[1] = (float)s4.xpos_base[1]; }
+
+  /* reward (ballbot_env.py:929-937 + DirectionalReward) in float32 */
+  float dir = vel[0] * cfg->target_dir[0] + vel[1] * cfg->target_dir[1];
+  float r = dir * cfg->reward_scale;
+  float nrm = sqrtf(action[0] * action[0] + action[1] * action[1] + action[2] * action[2]);
+  float reg = cfg->action_reg_coef * (nrm * nrm);
+  r = r + reg;
+  *step_counter += 1;
+  int terminated = (*step_counter >= cfg->max_ep_steps);
+  /* tilt (ballbot_env.py:989-1008): R from f32 rotvec (f64 math) -> arccos(R22) */
+  double rx = orient[0], ry = orient[1], rz = orient[2];
+  double th = sqrt(rx * rx + ry * ry + rz * rz) / 2;
+  double qw = cos(th), sf = th > 0 ? sin(th) / th : 1.0;
+  double qx = sf * rx / 2, qy = sf * ry / 2, qz = sf * rz / 2;
+  double nn = qw * qw + qx * qx + qy * qy + qz * qz;
+  double R22 = 1 - 2 * (qx * qx + qy * qy) / nn;
+  double ang = acos(R22) * 180 / PI;
+  if (tilt_deg) *tilt_deg = ang;
+  int failure = ang > cfg->max_allowed_tilt;
+  if (failure) terminated = 1;
+  else r = r + cfg->survival_bonus;
+  *reward = r;
+  return (terminated ? 1 : 0) | (failure ? 2 : 0) | (diverged ? 4 : 0);
+}
+
+int bbo_env_step_batch(const bbo_env_cfg* cfg, int n, double* qpos, double* qvel, double* warm,
+                       int* step_counter, const float* actions, const float* hfield, double size_z,
+                       float* obs, float* reward, unsigned char* done, double offset) {
+  int nd = 0;
+  for (int e = 0; e < n; e++) {
+    double* q = qpos + e * NQ; double* v = qvel + e * NV; double* w = warm + e * NV;
+    int f = bbo_env_step(cfg, q, v, w, step_counter + e, actions + 3 * e, hfield, size_z, obs + 15 * e,
+                         reward + e, NULL, NULL);
+    done[e] = (unsigned char)(f & 7);
+    if (f & 5) { /* terminated or diverged -> auto-reset */
+      bbo_reset_state(offset, q, v, w);
+      step_counter[e] = 0;
+      nd++;
+    }
+  }
+  return nd;
+}

@@ -1,0 +1,116 @@
+/*
+ * bb_oracle.h -- CPU fp64 restatement of the reference's `mj_step` hot path for
+ * ballbot.xml, plus the env step glue of ballbot_gym/envs/ballbot_env.py.
+ *
+ * TEST INFRASTRUCTURE ONLY.  Only tests/, __graft_entry__.smoke() and the
+ * cpu_baseline leg of bench.py may load this library, and only as the checker.
+ * The product path (openballbot-rl_amd/csrc) never links or calls it.
+ *
+ * Parity status
+ *   - physics (A3..A9 of SURVEY.md §8): UNPINNED against real MuJoCo.  MuJoCo
+ *     (git 99490163 + tools/mujoco_fix.patch) is not vendored in the reference
+ *     and cannot be built or imported here.  This file restates MuJoCo's
+ *     published algorithms for this one model; it is validated by physical
+ *     invariants (tests/test_oracle_invariants.py).
+ *   - glue (A10..A15): pinned by golden vectors generated from the reference's
+ *     importable Python modules (tests/golden/, tools/gen_goldens.py).
+ *
+ * All state is MuJoCo layout: qpos[17] = base(x,y,z,qw,qx,qy,qz), wheel0..2,
+ * ball(x,y,z,qw,qx,qy,qz); qvel[15] = base(v_world[3], w_local[3]),
+ * wheel0..2 rates, ball(v_world[3], w_local[3]).
+ */
+#ifndef BB_ORACLE_H
+#define BB_ORACLE_H
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define BBO_NQ 17
+#define BBO_NV 15
+#define BBO_NU 3
+#define BBO_NBODY 8
+#define BBO_HF_N 293          /* ballbot.xml:23 nrow = ncol = 293 */
+#define BBO_MAXGROUND 24      /* cap on ball-hfield contacts (MuJoCo: mjMAXCONPAIR=50; max observed 20) */
+#define BBO_MAXCON (3 + BBO_MAXGROUND)
+
+/* option flags for invariant tests (0 = reference behaviour) */
+#define BBO_DISABLE_CONTACT 1
+#define BBO_DISABLE_GRAVITY 2
+#define BBO_DISABLE_DAMPING 4
+
+/* Per-forward diagnostic outputs (stage-level view of mjData). */
+typedef struct {
+  double qacc[BBO_NV];
+  double qacc_smooth[BBO_NV];
+  double qfrc_bias[BBO_NV];
+  double M[BBO_NV * BBO_NV];
+  double xpos_base[3], xquat_base[4];
+  double cvel_base[6];          /* MuJoCo cvel[base]: [w_world; v at subtree_com] */
+  double subtree_com_base[3];
+  int ncon, nground, niter;
+  double con_dist[BBO_MAXCON];
+  double con_pos[BBO_MAXCON * 3];
+  double con_frame[BBO_MAXCON * 9];
+  int con_body2[BBO_MAXCON];    /* 4..6 = wheel (ball is geom1), 7 = ball vs hfield */
+  double energy_kin, energy_pot;
+  int ground_overflow;
+} bbo_forward_out;
+
+/* Env configuration mirroring BBotSimulation.__init__ (ballbot_env.py:157-231). */
+typedef struct {
+  int max_ep_steps;             /* default 4000 */
+  double max_allowed_tilt;      /* degrees, default 20 */
+  double max_wheel_velocity;    /* default 10 */
+  float reward_scale;           /* 0.01 */
+  float action_reg_coef;        /* -1e-4 */
+  float survival_bonus;         /* 0.02 */
+  float target_dir[2];          /* DirectionalReward target (0, 1) */
+} bbo_env_cfg;
+
+/* Model/options.  size_z: hfield size[2] (ballbot.xml:23, 2.0; ramp/gradient rescale). */
+int  bbo_abi_version(void);
+void bbo_set_flags(int flags);
+int  bbo_get_flags(void);
+void bbo_set_solver(int maxiter, double tol);
+void bbo_model_info(double* out);   /* masses, invweight0, meaninertia, qpos0 ... (see .c) */
+
+/* mj_forward at (qpos, qvel) with ctrl; warm = qacc_warmstart (may be NULL). */
+void bbo_forward(const double* qpos, const double* qvel, const double* ctrl,
+                 const double* warm, const float* hfield, double size_z,
+                 bbo_forward_out* out);
+
+/* mj_step with RK4: advances qpos/qvel/warm in place.  stage4 (may be NULL)
+ * receives the forward outputs of the last RK stage (what mjData holds after
+ * mj_step: xquat/cvel/xpos come from RK stage 4). */
+void bbo_mj_step(double* qpos, double* qvel, double* warm, const double* ctrl,
+                 const float* hfield, double size_z, bbo_forward_out* stage4);
+
+/* Full env step (ballbot_env.py:854-1036) for one env.
+ * obs15 layout = sorted keys: actions, angular_vel, motor_state, orientation, vel.
+ * Returns flags: bit0 terminated, bit1 failure (tilt), bit2 diverged. */
+int bbo_env_step(const bbo_env_cfg* cfg, double* qpos, double* qvel, double* warm,
+                 int* step_counter, const float* action, const float* hfield,
+                 double size_z, float* obs15, float* reward, float* pos2d,
+                 double* tilt_deg);
+
+/* Reset state (ballbot_env.py:612-620): qpos0 with height offset, zero vel. */
+void bbo_reset_state(double offset, double* qpos, double* qvel, double* warm);
+
+/* init height offset of _reset_terrain (ballbot_env.py:527-565), incl. its
+ * cell_size = size/nrows quirk. */
+double bbo_init_offset(const float* hfield, double size_z);
+
+/* numpy-quaternion as_rotation_vector restatement (quaternion_log). */
+void bbo_quat_to_rotvec(const double* q, double* rv);
+
+/* Batch helper: n envs stepped sequentially on one thread (CPU baseline). */
+int bbo_env_step_batch(const bbo_env_cfg* cfg, int n, double* qpos, double* qvel,
+                       double* warm, int* step_counter, const float* actions,
+                       const float* hfield, double size_z, float* obs,
+                       float* reward, unsigned char* done, double offset);
+
+#ifdef __cplusplus
+}
+#endif
+#endif
