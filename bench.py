@@ -1,0 +1,177 @@
+"""bench.py -- env-steps/sec of the batched ballbot hot path on MI355X.
+
+One "step" = one env.step of every env (one fused HIP launch: RK4 mj_step +
+obs + reward + termination + auto-reset) over a batch of synthetic random
+actions already resident in HBM.  Workload = BASELINE.json configs[1]:
+4096 envs per GPU, flat terrain, random actions.  Multi-GPU: one process per
+GPU (torchrun), envs sharded with no data-path collective (weak scaling);
+the MAX elapsed time over ranks is used.
+
+Prints ONE JSON line (rank 0).
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import platform
+import sys
+import time
+from pathlib import Path
+
+ROOT = Path(__file__).resolve().parent
+for _p in (ROOT / "openballbot-rl_amd", ROOT / "tests"):
+    if str(_p) not in sys.path:
+        sys.path.insert(0, str(_p))
+
+HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
+
+
+def algorithmic_bytes(precision: str) -> int:
+    """HBM bytes one env-step must move (state in and out, action, outputs)."""
+    es = 8 if precision == "fp64" else 4
+    state = (17 + 15 + 15) * es      # qpos, qvel, qacc_warmstart
+    return 2 * state + 12 + 60 + 4 + 1 + 8 + 4  # r/w state, action, obs, reward, done, step r/w, terrain id
+
+
+def cpu_baseline(seconds: float = 12.0) -> dict:
+    """The fp64 oracle (a port of the reference step semantics, not MuJoCo) on
+    one host core, 32 envs with random actions, flat terrain."""
+    import numpy as np
+
+    import oracle_lib as O
+
+    O.build()
+    n = 32
+    cfg = O.default_cfg()
+    hf = O.flat_hfield()
+    off = O.init_offset(hf)
+    q = np.zeros((n, 17)); v = np.zeros((n, 15)); w = np.zeros((n, 15))
+    for e in range(n):
+        q[e], v[e], w[e] = O.reset_state(off)
+    steps = np.zeros(n, np.int32)
+    rng = np.random.default_rng(0)
+    done_steps = 0
+    t0 = time.perf_counter()
+    while time.perf_counter() - t0 < seconds:
+        a = rng.uniform(-1, 1, (n, 3)).astype(np.float32)
+        O.env_step_batch(cfg, q, v, w, steps, a, hf, 2.0, off)
+        done_steps += n
+    dt = time.perf_counter() - t0
+    cpu = platform.processor() or platform.machine()
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                cpu = line.split(":", 1)[1].strip()
+                break
+    except OSError:
+        pass
+    return {"value": done_steps / dt, "unit": "env-steps/s", "cores": 1, "kind": "port",
+            "sample": f"{n} envs x {done_steps // n} steps, flat, random actions, 1 thread on '{cpu}' "
+                      f"(fp64 oracle restating the reference step; MuJoCo itself is not available)"}
+
+
+def main() -> None:
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=300)
+    ap.add_argument("--warmup", type=int, default=30)
+    ap.add_argument("--envs", type=int, default=4096, help="envs per GPU")
+    ap.add_argument("--precision", default="fp32", choices=["fp32", "fp64"])
+    ap.add_argument("--terrain", default="flat")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-seconds", type=float, default=12.0)
+    ap.add_argument("--traffic-json", default=str(ROOT / "profiles" / "traffic.json"))
+    args = ap.parse_args()
+
+    import torch
+    import torch.distributed as dist
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        os.environ.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    dev = torch.device("cuda", local)
+    torch.cuda.set_device(dev)
+
+    from ballbot_gym.envs import BallbotVecEnv
+
+    n = args.envs
+    env = BallbotVecEnv(n, device=dev, precision=args.precision, seed=1000 + rank,
+                        terrain_config={"type": args.terrain, "config": {}})
+    g = torch.Generator(device=dev).manual_seed(1234 + rank)
+    pool = torch.rand(64, n, 3, generator=g, device=dev) * 2 - 1  # random actions resident in HBM
+    for i in range(args.warmup):
+        env.step_async_raw(pool[i % 64])
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    t0 = time.perf_counter()
+    ev0.record()
+    for i in range(args.steps):
+        env.step_async_raw(pool[i % 64])
+    ev1.record()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    elapsed = time.perf_counter() - t0
+    kern_ms = ev0.elapsed_time(ev1) / args.steps  # one step kernel per step, on the env's stream
+    t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+    if world > 1:
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    elapsed = float(t.item())
+    stats = env.stats()
+
+    if rank == 0:
+        total_steps = n * world * args.steps
+        value = total_steps / elapsed
+        abytes = algorithmic_bytes(args.precision) * n
+        achieved = abytes / (kern_ms * 1e-3) / 1e9
+        traffic = None
+        tj = Path(args.traffic_json)
+        if tj.exists():
+            try:
+                tr = json.loads(tj.read_text())
+                if tr.get("precision") == args.precision and tr.get("envs") == n:
+                    traffic = tr.get("bytes_per_launch")
+            except Exception:
+                traffic = None
+        line = {
+            "metric": "env-steps/sec at 4096 envs per GPU (flat terrain, random actions)",
+            "value": value,
+            "unit": "env-steps/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": elapsed / args.steps * 1e3,
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "f64" if args.precision == "fp64" else "f32",
+            "data": "synthetic (uniform random actions in [-1,1], resident in HBM)",
+            "config": {"workload": f"{n} envs/GPU, {args.terrain} terrain, random actions (BASELINE configs[1])",
+                       "envs_per_gpu": n, "total_envs": n * world, "precision": args.precision,
+                       "parallelism": f"env-sharded x{world} (no collective on the step path)"},
+            "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                         "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
+                         "note": "latency/VALU-bound per-lane physics; HBM bytes = algorithmic state I/O "
+                                 f"({algorithmic_bytes(args.precision)} B/env-step)",
+                         "kernel_ms": kern_ms},
+            "stats": stats,
+        }
+        if world == 1 and not args.no_cpu_baseline:
+            line["cpu_baseline"] = cpu_baseline(args.cpu_seconds)
+        print(json.dumps(line), flush=True)
+    env.close()
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

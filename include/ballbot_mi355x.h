@@ -1,0 +1,112 @@
+/*
+ * ballbot_mi355x.h -- C-ABI drop-in boundary for the batched ballbot hot path.
+ *
+ * Replaces, for N envs at once on one MI355X, what the reference does per env
+ * through MuJoCo's pybind11 API inside BBotSimulation:
+ *   bb_create        mujoco.MjModel.from_xml_path + MjData      ballbot_env.py:261-262
+ *   bb_set_hfield    model.hfield_data = terrain_gen(n, seed)   ballbot_env.py:513
+ *                    (+ hfield_size[2] rescale                  ballbot_env.py:486-495)
+ *                    (+ init height offset                      ballbot_env.py:527-565)
+ *   bb_assign_terrain   choice of terrain per env at reset      ballbot_env.py:501-513
+ *   bb_reset         mj_resetData + height offset + mj_forward  ballbot_env.py:612-620
+ *   bb_step          ctrl = -clip(10a); mj_step; _get_obs;      ballbot_env.py:903-1036
+ *                    reward plugin; termination
+ *   bb_forward       mujoco.mj_forward (diagnostic)             ballbot_env.py:525,620
+ *   bb_get_state/    read/write qpos/qvel/qacc_warmstart        ballbot_env.py:616-617
+ *   bb_set_state     (MjData.qpos / qvel)
+ *
+ * Conventions
+ *   - every function returns int: 0 ok, <0 error (bb_last_error has the text);
+ *     per-env physics divergence is NOT an error, it is reported in done[]
+ *     (bit 2) and the env is auto-reset, mirroring mj_checkPos/Vel/Acc.
+ *   - device pointers belong to the caller (e.g. torch tensors); the library
+ *     never frees them.  Work is enqueued on the caller's stream (hipStream_t
+ *     passed as void*); bb_step/bb_reset are graph-capturable.
+ *   - one handle per device; a handle is not thread-safe.
+ *   - state layout (get/set): qpos[n][17], qvel[n][15], warm[n][15] in MuJoCo
+ *     order (free joints: pos, quat(w,x,y,z); lin vel world, ang vel local).
+ *   - obs layout [n][15]: sorted keys actions(3) angular_vel(3) motor_state(3)
+ *     orientation(3) vel(3), the order the reference policy consumes.
+ */
+#ifndef BALLBOT_MI355X_H
+#define BALLBOT_MI355X_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define BB_ABI_VERSION 1
+#define BB_NQ 17
+#define BB_NV 15
+#define BB_OBS 15
+#define BB_HF_N 293
+
+/* done[] bits */
+#define BB_DONE_TERMINATED 1
+#define BB_DONE_FAILURE 2
+#define BB_DONE_DIVERGED 4
+#define BB_DONE_OVERFLOW 8
+
+/* reward kinds (built-in reward plugins, ballbot_gym/rewards) */
+#define BB_REWARD_DIRECTIONAL 0 /* rewards/directional.py:33-54 */
+#define BB_REWARD_DISTANCE 1    /* rewards/distance.py:33-50 (pos2d-based) */
+#define BB_REWARD_NONE 2        /* custom plugin evaluated host-side */
+
+typedef struct bb_handle bb_handle;
+
+/* BBotSimulation.__init__ settings (ballbot_env.py:157-231) */
+typedef struct {
+  int max_ep_steps;            /* 4000 */
+  float max_allowed_tilt;      /* 20 degrees */
+  float max_wheel_velocity;    /* 10 */
+  float reward_scale;          /* 0.01 */
+  float action_reg_coef;       /* -1e-4 */
+  float survival_bonus;        /* 0.02 */
+  float target_dir[2];         /* directional target (0, 1) */
+  int reward_kind;             /* BB_REWARD_* */
+  float goal[2];               /* distance reward goal */
+  float goal_scale;            /* distance reward scale */
+  int n_terrains;              /* terrain bank size (>= 1) */
+  uint64_t seed;               /* per-env terrain draws at auto-reset */
+  int fp64;                    /* 0: fp32 arithmetic, 1: fp64 arithmetic */
+  int solver_maxiter;          /* 0 = default */
+  double solver_tol;           /* 0 = default */
+} bb_params;
+
+int bb_abi_version(void);
+int bb_last_error(char* buf, int len);
+void bb_default_params(bb_params* p);
+
+int bb_create(int n_envs, int device, const bb_params* p, bb_handle** out);
+int bb_destroy(bb_handle* h);
+
+/* upload one terrain (host float32[293*293], row-major, values in [0,1]) */
+int bb_set_hfield(bb_handle* h, int terrain_id, const float* data_host, float size_z);
+/* per-env terrain ids (device int32[n]) applied at the next reset */
+int bb_assign_terrain(bb_handle* h, const int32_t* ids_dev, void* stream);
+
+/* reset envs where mask_dev[i] != 0 (mask NULL = all); writes reset obs */
+int bb_reset(bb_handle* h, const uint8_t* mask_dev, float* obs_dev, void* stream);
+
+/* one env.step for all envs.  actions_dev float[n][3]; obs_dev float[n][15];
+ * reward_dev float[n]; done_dev uint8[n]; terminal_obs_dev float[n][15] and
+ * pos2d_dev float[n][2] may be NULL.  auto_reset != 0: done envs are reset in
+ * the same launch and obs holds the reset observation (SB3 VecEnv). */
+int bb_step(bb_handle* h, const float* actions_dev, float* obs_dev, float* reward_dev, uint8_t* done_dev,
+            float* terminal_obs_dev, float* pos2d_dev, int auto_reset, void* stream);
+
+/* diagnostics / parity (synchronous, host arrays) */
+int bb_get_state(bb_handle* h, double* qpos, double* qvel, double* warm, int32_t* steps);
+int bb_set_state(bb_handle* h, const double* qpos, const double* qvel, const double* warm, const int32_t* steps);
+int bb_forward(bb_handle* h, const double* ctrl, double* qacc, int32_t* ncontact);
+/* counters since create: [resets, diverged, overflow, steps, solver_iters_lo, solver_iters_hi] */
+int bb_get_stats(bb_handle* h, int64_t* out6);
+/* init height offset per terrain (ballbot_env.py:546-563) */
+int bb_get_offsets(bb_handle* h, float* out);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

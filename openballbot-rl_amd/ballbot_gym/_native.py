@@ -1,0 +1,122 @@
+"""ctypes binding of the C-ABI library (include/ballbot_mi355x.h).
+
+The HIP library is the only compute path: there is no CPU fallback.  If the
+shared object is missing or fails to load, `lib()` raises NativeLibraryError.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+from pathlib import Path
+
+PKG = Path(__file__).resolve().parent
+LIB_PATH = PKG / "_lib" / "libbb_mi355x.so"
+CSRC = PKG.parent / "csrc"
+INCLUDE = PKG.parent.parent / "include"
+
+NQ, NV, NOBS, HF_N = 17, 15, 15, 293
+DONE_TERMINATED, DONE_FAILURE, DONE_DIVERGED, DONE_OVERFLOW = 1, 2, 4, 8
+REWARD_DIRECTIONAL, REWARD_DISTANCE, REWARD_NONE = 0, 1, 2
+
+
+class NativeLibraryError(RuntimeError):
+    pass
+
+
+class BBParams(C.Structure):
+    _fields_ = [
+        ("max_ep_steps", C.c_int),
+        ("max_allowed_tilt", C.c_float),
+        ("max_wheel_velocity", C.c_float),
+        ("reward_scale", C.c_float),
+        ("action_reg_coef", C.c_float),
+        ("survival_bonus", C.c_float),
+        ("target_dir", C.c_float * 2),
+        ("reward_kind", C.c_int),
+        ("goal", C.c_float * 2),
+        ("goal_scale", C.c_float),
+        ("n_terrains", C.c_int),
+        ("seed", C.c_uint64),
+        ("fp64", C.c_int),
+        ("solver_maxiter", C.c_int),
+        ("solver_tol", C.c_double),
+    ]
+
+
+EXPORTS = [
+    "bb_abi_version", "bb_last_error", "bb_default_params", "bb_create", "bb_destroy", "bb_set_hfield",
+    "bb_assign_terrain", "bb_reset", "bb_step", "bb_get_state", "bb_set_state", "bb_forward", "bb_get_stats",
+    "bb_get_offsets",
+]
+
+_lib = None
+
+
+def build(force: bool = False, verbose: bool = False) -> Path:
+    """Compile csrc/bb_kernels.hip for gfx950 into _lib/libbb_mi355x.so."""
+    import subprocess
+
+    srcs = list(CSRC.glob("*.h")) + list(CSRC.glob("*.hip")) + list(INCLUDE.glob("*.h"))
+    if LIB_PATH.exists() and not force and all(LIB_PATH.stat().st_mtime >= s.stat().st_mtime for s in srcs):
+        return LIB_PATH
+    LIB_PATH.parent.mkdir(parents=True, exist_ok=True)
+    tmp = LIB_PATH.with_suffix(".so.tmp")
+    cmd = ["hipcc", "--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC", "-shared",
+           "-o", str(tmp), str(CSRC / "bb_kernels.hip")]
+    if verbose:
+        print(" ".join(cmd))
+    subprocess.run(cmd, check=True)
+    os.replace(tmp, LIB_PATH)
+    return LIB_PATH
+
+
+def lib():
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not LIB_PATH.exists():
+        raise NativeLibraryError(
+            f"HIP library {LIB_PATH} not found; run __graft_entry__.build() (hipcc --offload-arch=gfx950)")
+    try:
+        L = C.CDLL(str(LIB_PATH))
+    except OSError as e:  # pragma: no cover - depends on the box
+        raise NativeLibraryError(f"cannot load {LIB_PATH}: {e}") from e
+    vp, fp, dp = C.c_void_p, C.POINTER(C.c_float), C.POINTER(C.c_double)
+    L.bb_abi_version.restype = C.c_int
+    L.bb_last_error.argtypes = [C.c_char_p, C.c_int]
+    L.bb_default_params.argtypes = [C.POINTER(BBParams)]
+    L.bb_default_params.restype = None
+    L.bb_create.argtypes = [C.c_int, C.c_int, C.POINTER(BBParams), C.POINTER(vp)]
+    L.bb_destroy.argtypes = [vp]
+    L.bb_set_hfield.argtypes = [vp, C.c_int, fp, C.c_float]
+    L.bb_assign_terrain.argtypes = [vp, vp, vp]
+    L.bb_reset.argtypes = [vp, vp, vp, vp]
+    L.bb_step.argtypes = [vp, vp, vp, vp, vp, vp, vp, C.c_int, vp]
+    L.bb_get_state.argtypes = [vp, dp, dp, dp, C.POINTER(C.c_int32)]
+    L.bb_set_state.argtypes = [vp, dp, dp, dp, C.POINTER(C.c_int32)]
+    L.bb_forward.argtypes = [vp, dp, dp, C.POINTER(C.c_int32)]
+    L.bb_get_stats.argtypes = [vp, C.POINTER(C.c_int64)]
+    L.bb_get_offsets.argtypes = [vp, fp]
+    for name in [n for n in EXPORTS if n not in ("bb_default_params", "bb_abi_version")]:
+        getattr(L, name).restype = C.c_int
+    if L.bb_abi_version() != 1:
+        raise NativeLibraryError("ABI version mismatch")
+    _lib = L
+    return L
+
+
+def last_error() -> str:
+    buf = C.create_string_buffer(512)
+    lib().bb_last_error(buf, 512)
+    return buf.value.decode()
+
+
+def check(rc: int, what: str) -> None:
+    if rc != 0:
+        raise RuntimeError(f"{what} failed: {last_error()}")
+
+
+def default_params() -> BBParams:
+    p = BBParams()
+    lib().bb_default_params(C.byref(p))
+    return p

@@ -1,0 +1,241 @@
+"""BallbotVecEnv: N ballbot envs stepped by one HIP launch per env.step.
+
+Batched replacement for `BBotSimulation` (ballbot_gym/envs/ballbot_env.py:60)
+as driven by SB3's VecEnv (ballbot_rl/training/train.py:60-120): the physics
+(`mujoco.mj_step`, ballbot_env.py:912), observation packing (:771-811), the
+reward plugin (:929-937) and termination (:982-1017) all run in the fused
+step kernel behind the C-ABI (include/ballbot_mi355x.h).  Tensors live on the
+GPU; `step` takes and returns torch tensors on `device`.
+"""
+from __future__ import annotations
+
+import ctypes as C
+from typing import Any, Dict, Optional
+
+import numpy as np
+import torch
+
+from .. import _native as N
+
+OBS_KEYS = ("actions", "angular_vel", "motor_state", "orientation", "vel")  # sorted, as the policy reads them
+
+
+def _ptr(t: Optional[torch.Tensor]):
+    return None if t is None else C.c_void_p(t.data_ptr())
+
+
+class BallbotVecEnv:
+    """Vectorised ballbot env on one GPU.
+
+    Args mirror BBotSimulation (ballbot_env.py:157-231) plus `num_envs`,
+    `device`, `precision` ("fp32" | "fp64") and the terrain bank size.
+    """
+
+    metadata = {"render_modes": []}
+
+    def __init__(
+        self,
+        num_envs: int,
+        device: str | torch.device = "cuda:0",
+        reward_config: Optional[Dict[str, Any]] = None,
+        terrain_config: Optional[Dict[str, Any]] = None,
+        env_config: Optional[Dict[str, Any]] = None,
+        max_ep_steps: Optional[int] = None,
+        seed: int = 0,
+        precision: str = "fp32",
+        n_terrains: Optional[int] = None,
+        auto_reset: bool = True,
+    ):
+        from ..core.factories import create_reward
+        from ..rewards.directional import DirectionalReward
+        from ..rewards.distance import DistanceReward
+
+        if not torch.cuda.is_available():
+            raise RuntimeError("BallbotVecEnv needs a ROCm GPU (torch.cuda.is_available() is False)")
+        self.device = torch.device(device)
+        if self.device.type != "cuda":
+            raise ValueError(f"BallbotVecEnv runs on a GPU device, got {self.device}")
+        self.num_envs = int(num_envs)
+        self.auto_reset = bool(auto_reset)
+        self.terrain_config = terrain_config or {"type": "flat", "config": {}}
+        self.reward_config = reward_config or {"type": "directional", "config": {"target_direction": [0.0, 1.0]}}
+        env_settings = (env_config or {}).get("env", {})
+        self.max_ep_steps = int(env_settings.get("max_ep_steps", max_ep_steps if max_ep_steps is not None else 4000))
+        rcfg = self.reward_config.get("config", {})
+
+        p = N.default_params()
+        p.max_ep_steps = self.max_ep_steps
+        p.max_allowed_tilt = float(env_settings.get("max_allowed_tilt", 20.0))
+        p.max_wheel_velocity = float(env_settings.get("max_wheel_velocity", 10.0))
+        p.reward_scale = float(rcfg.get("scale", 0.01))
+        p.action_reg_coef = float(rcfg.get("action_reg_coef", -0.0001))
+        p.survival_bonus = float(rcfg.get("survival_bonus", 0.02))
+        # reward plugin -> fused kernel id, or host-side evaluation for custom plugins
+        self.reward_obj = create_reward(self.reward_config)
+        self._host_reward = None
+        if type(self.reward_obj) is DirectionalReward:
+            td = np.asarray(self.reward_obj.target_direction, dtype=np.float32)
+            p.reward_kind = N.REWARD_DIRECTIONAL
+            p.target_dir[0], p.target_dir[1] = float(td[0]), float(td[1])
+        elif type(self.reward_obj) is DistanceReward:
+            p.reward_kind = N.REWARD_DISTANCE
+            p.goal[0], p.goal[1] = float(self.reward_obj.goal_position[0]), float(self.reward_obj.goal_position[1])
+            p.goal_scale = float(self.reward_obj.scale)
+        else:
+            p.reward_kind = N.REWARD_NONE
+            self._host_reward = self.reward_obj
+
+        bank = self._build_terrain_bank(n_terrains, seed)
+        p.n_terrains = len(bank)
+        p.seed = int(seed) & 0xFFFFFFFFFFFFFFFF
+        p.fp64 = 1 if precision == "fp64" else 0
+        self.precision = "fp64" if p.fp64 else "fp32"
+        self._params = p
+        L = N.lib()
+        h = C.c_void_p()
+        N.check(L.bb_create(self.num_envs, self.device.index or 0, C.byref(p), C.byref(h)), "bb_create")
+        self._h = h
+        for i, (data, size_z) in enumerate(bank):
+            arr = np.ascontiguousarray(data, dtype=np.float32)
+            N.check(L.bb_set_hfield(h, i, arr.ctypes.data_as(C.POINTER(C.c_float)), float(size_z)), "bb_set_hfield")
+        self.n_terrains = len(bank)
+        n, dev = self.num_envs, self.device
+        self.obs = torch.zeros(n, N.NOBS, dtype=torch.float32, device=dev)
+        self.terminal_obs = torch.zeros(n, N.NOBS, dtype=torch.float32, device=dev)
+        self.reward = torch.zeros(n, dtype=torch.float32, device=dev)
+        self.done = torch.zeros(n, dtype=torch.uint8, device=dev)
+        self.pos2d = torch.zeros(n, 2, dtype=torch.float32, device=dev)
+        if self.n_terrains > 1:
+            g = torch.Generator(device="cpu").manual_seed(int(seed))
+            ids = torch.randint(0, self.n_terrains, (n,), generator=g, dtype=torch.int32).to(dev)
+            N.check(L.bb_assign_terrain(h, _ptr(ids), self._stream()), "bb_assign_terrain")
+        self.reset()
+
+    # ------------------------------------------------------------------ terrain
+    def _build_terrain_bank(self, n_terrains, seed):
+        """Generate heightfields host-side with the registered terrain plugin
+        (ballbot_env.py:501-513) and the ramp/gradient z-rescale (:486-495)."""
+        from ..core.factories import create_terrain
+
+        ttype = self.terrain_config.get("type", "flat")
+        tcfg = self.terrain_config.get("config", {})
+        size_z = 2.0
+        if ttype == "ramp":
+            size_z = float(2 * 5.0 * np.tan(np.radians(tcfg.get("ramp_angle", 15.0))))
+        elif ttype == "gradient":
+            size_z = float(2 * 5.0 * np.tan(np.radians(tcfg.get("max_slope", 20.0))))
+        gen = create_terrain(self.terrain_config)
+        if ttype == "flat":
+            return [(np.asarray(gen(N.HF_N), dtype=np.float32), size_z)]
+        if tcfg.get("seed") is not None:
+            return [(np.asarray(gen(N.HF_N), dtype=np.float32), size_z)]
+        k = int(n_terrains or 16)
+        rng = np.random.default_rng(seed)
+        seeds = rng.integers(0, 10000, size=k)  # reference draws seeds from [0, 10000)
+        return [(np.asarray(gen(N.HF_N, seed=int(s)), dtype=np.float32), size_z) for s in seeds]
+
+    # --------------------------------------------------------------------- api
+    def _stream(self):
+        return C.c_void_p(torch.cuda.current_stream(self.device).cuda_stream)
+
+    def reset(self, mask: Optional[torch.Tensor] = None):
+        m = None if mask is None else mask.to(device=self.device, dtype=torch.uint8).contiguous()
+        N.check(N.lib().bb_reset(self._h, _ptr(m), _ptr(self.obs), self._stream()), "bb_reset")
+        return self.obs, {}
+
+    def step(self, actions: torch.Tensor):
+        """One env.step for all envs: returns (obs[N,15], reward[N], terminated[N], truncated[N], info)."""
+        if actions.device != self.device or actions.dtype != torch.float32 or not actions.is_contiguous():
+            actions = actions.to(device=self.device, dtype=torch.float32).contiguous()
+        if actions.shape != (self.num_envs, 3):
+            raise ValueError(f"actions must have shape ({self.num_envs}, 3), got {tuple(actions.shape)}")
+        N.check(N.lib().bb_step(self._h, _ptr(actions), _ptr(self.obs), _ptr(self.reward), _ptr(self.done),
+                                _ptr(self.terminal_obs), _ptr(self.pos2d), int(self.auto_reset), self._stream()),
+                "bb_step")
+        terminated = (self.done & N.DONE_TERMINATED) != 0
+        info = {"done_flags": self.done, "terminal_observation": self.terminal_obs, "pos2d": self.pos2d,
+                "failure": (self.done & N.DONE_FAILURE) != 0}
+        reward = self.reward
+        if self._host_reward is not None:
+            reward = reward + self._host_reward_batch()
+        return self.obs, reward, terminated, torch.zeros_like(terminated), info
+
+    def step_async_raw(self, actions: torch.Tensor) -> None:
+        """Launch-only step (graph capture / benchmarking): no derived tensors."""
+        N.lib().bb_step(self._h, _ptr(actions), _ptr(self.obs), _ptr(self.reward), _ptr(self.done),
+                        None, None, int(self.auto_reset), self._stream())
+
+    def _host_reward_batch(self) -> torch.Tensor:
+        """Custom reward plugins (BaseReward.__call__(state) -> float) evaluated
+        per env on the host from the terminal observation dict."""
+        obs = self.terminal_obs.cpu().numpy()
+        pos = self.pos2d.cpu().numpy()
+        out = np.zeros(self.num_envs, dtype=np.float32)
+        for i in range(self.num_envs):
+            state = split_obs(obs[i])
+            state["pos2d"] = pos[i]
+            out[i] = np.float32(self._host_reward(state)) * np.float32(self._params.reward_scale)
+        return torch.from_numpy(out).to(self.device)
+
+    def obs_dict(self, obs: Optional[torch.Tensor] = None) -> Dict[str, torch.Tensor]:
+        o = self.obs if obs is None else obs
+        return {k: o[:, 3 * i:3 * i + 3] for i, k in enumerate(OBS_KEYS)}
+
+    # ------------------------------------------------------------ parity/state
+    def get_state(self):
+        n = self.num_envs
+        q, v, w = np.zeros((n, N.NQ)), np.zeros((n, N.NV)), np.zeros((n, N.NV))
+        s = np.zeros(n, dtype=np.int32)
+        dp = C.POINTER(C.c_double)
+        N.check(N.lib().bb_get_state(self._h, q.ctypes.data_as(dp), v.ctypes.data_as(dp), w.ctypes.data_as(dp),
+                                     s.ctypes.data_as(C.POINTER(C.c_int32))), "bb_get_state")
+        return q, v, w, s
+
+    def set_state(self, qpos, qvel, warm=None, steps=None):
+        n = self.num_envs
+        q = np.ascontiguousarray(np.broadcast_to(qpos, (n, N.NQ)), dtype=np.float64)
+        v = np.ascontiguousarray(np.broadcast_to(qvel, (n, N.NV)), dtype=np.float64)
+        w = np.zeros((n, N.NV)) if warm is None else np.ascontiguousarray(np.broadcast_to(warm, (n, N.NV)),
+                                                                           dtype=np.float64)
+        s = np.zeros(n, np.int32) if steps is None else np.ascontiguousarray(np.broadcast_to(steps, (n,)),
+                                                                              dtype=np.int32)
+        dp = C.POINTER(C.c_double)
+        N.check(N.lib().bb_set_state(self._h, q.ctypes.data_as(dp), v.ctypes.data_as(dp), w.ctypes.data_as(dp),
+                                     s.ctypes.data_as(C.POINTER(C.c_int32))), "bb_set_state")
+
+    def forward(self, ctrl):
+        """mj_forward at the current state (diagnostic): returns qacc [N,15], ground contacts [N]."""
+        n = self.num_envs
+        c = np.ascontiguousarray(np.broadcast_to(ctrl, (n, 3)), dtype=np.float64)
+        qacc = np.zeros((n, N.NV))
+        ncon = np.zeros(n, np.int32)
+        dp = C.POINTER(C.c_double)
+        N.check(N.lib().bb_forward(self._h, c.ctypes.data_as(dp), qacc.ctypes.data_as(dp),
+                                   ncon.ctypes.data_as(C.POINTER(C.c_int32))), "bb_forward")
+        return qacc, ncon
+
+    def stats(self) -> Dict[str, int]:
+        out = (C.c_int64 * 6)()
+        N.check(N.lib().bb_get_stats(self._h, out), "bb_get_stats")
+        return {"resets": out[0], "diverged": out[1], "overflow": out[2],
+                "solver_iters": out[4] + (out[5] << 32)}
+
+    def offsets(self) -> np.ndarray:
+        o = np.zeros(self.n_terrains, np.float32)
+        N.check(N.lib().bb_get_offsets(self._h, o.ctypes.data_as(C.POINTER(C.c_float))), "bb_get_offsets")
+        return o
+
+    def close(self):
+        if getattr(self, "_h", None):
+            N.lib().bb_destroy(self._h)
+            self._h = None
+
+    def __del__(self):  # pragma: no cover
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+def split_obs(obs15) -> Dict[str, Any]:
+    return {k: obs15[3 * i:3 * i + 3] for i, k in enumerate(OBS_KEYS)}

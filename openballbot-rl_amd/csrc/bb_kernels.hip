@@ -1,0 +1,454 @@
+// bb_kernels.hip -- gfx950 kernels and the C-ABI boundary (include/ballbot_mi355x.h).
+//
+// Layout in HBM (per handle, n envs, T = float or double):
+//   qpos  T[17][n]   qvel T[15][n]   warm T[15][n]     SoA: lane e reads
+//   steps int[n]     terrain int[n]  episodes int[n]   element i at [i*n + e]
+//   bank  float[n_terrains][293*293], size_z float[nt], offset float[nt]
+// One env per lane, one 64-lane wave per workgroup; ball-terrain contacts
+// are kept in LDS, lane-interleaved ([slot*NGF + field][64]).
+#include <hip/hip_runtime.h>
+
+#include <stdarg.h>
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+#include <vector>
+
+#include "../../include/ballbot_mi355x.h"
+#include "bb_model.h"
+#include "bb_step.h"
+
+using namespace bb;
+
+namespace {
+
+constexpr int WAVE = 64;
+char g_err[512] = "";
+
+int fail(const char* fmt, ...) {
+  va_list ap;
+  va_start(ap, fmt);
+  vsnprintf(g_err, sizeof g_err, fmt, ap);
+  va_end(ap);
+  return -1;
+}
+#define HIPCHK(x)                                                                   \
+  do {                                                                              \
+    hipError_t e_ = (x);                                                            \
+    if (e_ != hipSuccess) return fail("%s: %s", #x, hipGetErrorString(e_));         \
+  } while (0)
+
+template <typename T>
+size_t lds_bytes() { return size_t(MAXG) * NGF * WAVE * sizeof(T); }
+
+BB_HD uint32_t hash3(uint64_t seed, uint32_t a, uint32_t b) {  // splitmix-style counter hash
+  uint64_t z = seed + 0x9E3779B97F4A7C15ull * (uint64_t(a) * 0x100000001ull + b + 1);
+  z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+  z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+  return uint32_t(z ^ (z >> 31));
+}
+
+struct Dev {
+  int n;
+  void* qpos;
+  void* qvel;
+  void* warm;
+  int* steps;
+  int* terrain;
+  int* pending_terrain;
+  int* episodes;
+  const float* bank;
+  const float* size_z;
+  const float* offset;
+  int n_terrains;
+  uint64_t seed;
+  unsigned long long* stats;  // resets, diverged, overflow, steps, iters
+};
+
+template <typename T>
+__device__ __forceinline__ void load_state(const Dev& d, int e, T* q, T* v, T* w, int& step) {
+  const T* Q = (const T*)d.qpos;
+  const T* V = (const T*)d.qvel;
+  const T* W = (const T*)d.warm;
+#pragma unroll
+  for (int i = 0; i < NQ; i++) q[i] = Q[i * d.n + e];
+#pragma unroll
+  for (int i = 0; i < NV; i++) { v[i] = V[i * d.n + e]; w[i] = W[i * d.n + e]; }
+  step = d.steps[e];
+}
+template <typename T>
+__device__ __forceinline__ void store_state(const Dev& d, int e, const T* q, const T* v, const T* w, int step) {
+  T* Q = (T*)d.qpos;
+  T* V = (T*)d.qvel;
+  T* W = (T*)d.warm;
+#pragma unroll
+  for (int i = 0; i < NQ; i++) Q[i * d.n + e] = q[i];
+#pragma unroll
+  for (int i = 0; i < NV; i++) { V[i * d.n + e] = v[i]; W[i * d.n + e] = w[i]; }
+  d.steps[e] = step;
+}
+
+template <typename T>
+__device__ __forceinline__ void reset_lane(const ModelT<T>& m, const Dev& d, int e, T* q, T* v, T* w, int& step) {
+  int tid = d.pending_terrain[e];
+  d.terrain[e] = tid;
+  reset_state(m, T(d.offset[tid]), q, v, w);
+  step = 0;
+}
+
+template <typename T>
+__global__ __launch_bounds__(64) void step_kernel(ModelT<T> m, EnvCfg cfg, Dev d, const float* __restrict__ act,
+                                                  float* __restrict__ obs, float* __restrict__ rew,
+                                                  uint8_t* __restrict__ done, float* __restrict__ tobs,
+                                                  float* __restrict__ pos2d, int auto_reset) {
+  extern __shared__ __align__(16) unsigned char smem[];
+  const int lane = threadIdx.x;
+  const int e = blockIdx.x * WAVE + lane;
+  if (e >= d.n) return;
+  GStore<T> st{reinterpret_cast<T*>(smem) + lane, WAVE};
+  T q[NQ], v[NV], w[NV];
+  int step;
+  load_state(d, e, q, v, w, step);
+  float a[3] = {act[3 * e], act[3 * e + 1], act[3 * e + 2]};
+  const int tid = d.terrain[e];
+  const float* hf = d.bank + size_t(tid) * (HF_N * HF_N);
+  float o[15], r, p2[2];
+  int iters = 0;
+  int fl = env_step(m, cfg, q, v, w, step, a, hf, T(d.size_z[tid]), st, o, r, p2, &iters);
+  if (tobs) {
+#pragma unroll
+    for (int i = 0; i < 15; i++) tobs[15 * e + i] = o[i];
+  }
+  if (pos2d) { pos2d[2 * e] = p2[0]; pos2d[2 * e + 1] = p2[1]; }
+  const bool reset = auto_reset && (fl & (F_TERMINATED | F_DIVERGED));
+  if (reset) {
+    // next terrain for this env: counter-based draw from the bank
+    int ep = d.episodes[e] + 1;
+    d.episodes[e] = ep;
+    if (d.n_terrains > 1) d.pending_terrain[e] = int(hash3(d.seed, uint32_t(e), uint32_t(ep)) % uint32_t(d.n_terrains));
+    reset_lane(m, d, e, q, v, w, step);
+#pragma unroll
+    for (int i = 0; i < 15; i++) o[i] = 0.f;  // reset obs: identity quat, zero velocities, zero action
+  }
+#pragma unroll
+  for (int i = 0; i < 15; i++) obs[15 * e + i] = o[i];
+  rew[e] = r;
+  done[e] = uint8_t(fl);
+  store_state(d, e, q, v, w, step);
+  // counters (wave-aggregated by the compiler)
+  if (reset) atomicAdd(&d.stats[0], 1ull);
+  if (fl & F_DIVERGED) atomicAdd(&d.stats[1], 1ull);
+  if (fl & F_OVERFLOW) atomicAdd(&d.stats[2], 1ull);
+  atomicAdd(&d.stats[4], (unsigned long long)iters);
+}
+
+template <typename T>
+__global__ __launch_bounds__(64) void reset_kernel(ModelT<T> m, Dev d, const uint8_t* mask, float* obs) {
+  const int e = blockIdx.x * WAVE + threadIdx.x;
+  if (e >= d.n) return;
+  if (mask && !mask[e]) return;
+  T q[NQ], v[NV], w[NV];
+  int step;
+  reset_lane(m, d, e, q, v, w, step);
+  store_state(d, e, q, v, w, step);
+  if (obs) {
+#pragma unroll
+    for (int i = 0; i < 15; i++) obs[15 * e + i] = 0.f;
+  }
+}
+
+template <typename T>
+__global__ __launch_bounds__(64) void forward_kernel(ModelT<T> m, Dev d, const double* ctrl, double* qacc, int* ncon) {
+  extern __shared__ __align__(16) unsigned char smem[];
+  const int lane = threadIdx.x;
+  const int e = blockIdx.x * WAVE + lane;
+  if (e >= d.n) return;
+  GStore<T> st{reinterpret_cast<T*>(smem) + lane, WAVE};
+  T q[NQ], v[NV], w[NV], c[3];
+  int step;
+  load_state(d, e, q, v, w, step);
+  for (int i = 0; i < 3; i++) c[i] = T(ctrl[3 * e + i]);
+  const int tid = d.terrain[e];
+  StageOut<T> so;
+  forward(m, q, v, c, w, d.bank + size_t(tid) * (HF_N * HF_N), T(d.size_z[tid]), st, &so);
+  for (int i = 0; i < NV; i++) qacc[NV * e + i] = double(w[i]);
+  if (ncon) ncon[e] = so.ng;
+}
+
+__global__ void assign_kernel(Dev d, const int32_t* ids) {
+  const int e = blockIdx.x * blockDim.x + threadIdx.x;
+  if (e >= d.n) return;
+  int t = ids[e];
+  d.pending_terrain[e] = (t >= 0 && t < d.n_terrains) ? t : 0;
+}
+
+}  // namespace
+
+struct bb_handle {
+  int n, device, fp64;
+  bb_params p;
+  EnvCfg cfg;
+  ModelT<float> mf;
+  ModelT<double> md;
+  Dev d;
+  float* bank;
+  float* size_z;
+  float* offset;
+  std::vector<float> h_offset;
+};
+
+template <typename T> const ModelT<T>& model_of(const bb_handle* h);
+template <> const ModelT<float>& model_of<float>(const bb_handle* h) { return h->mf; }
+template <> const ModelT<double>& model_of<double>(const bb_handle* h) { return h->md; }
+
+namespace {
+// init height offset (ballbot_env.py:546-563), incl. cell_size = size/nrows
+float init_offset(const float* hf, float size_z) {
+  const int n = HF_N;
+  const double sz = 5.0, cell = sz / n, r = 0.09;
+  const int center = n / 2;
+  int x0 = center - abs((int)floor(-r / cell)), x1 = center + (int)floor(r / cell) + 1;
+  int y0 = center - abs((int)floor(-r / cell)), y1 = center + (int)floor(r / cell) + 1;
+  double mx = -1e300;
+  for (int i = x0; i < x1; i++)
+    for (int j = y0; j < y1; j++) mx = fmax(mx, (double)hf[i * n + j]);
+  return float(mx * size_z + 0.01);
+}
+
+template <typename T>
+int launch_step(bb_handle* h, const float* a, float* o, float* r, uint8_t* dn, float* t, float* p2, int ar,
+                hipStream_t s) {
+  const ModelT<T>& m = model_of<T>(h);
+  int blocks = (h->n + WAVE - 1) / WAVE;
+  hipLaunchKernelGGL(step_kernel<T>, dim3(blocks), dim3(WAVE), lds_bytes<T>(), s, m, h->cfg, h->d, a, o, r, dn, t,
+                     p2, ar);
+  HIPCHK(hipGetLastError());
+  return 0;
+}
+}  // namespace
+
+extern "C" {
+
+int bb_abi_version(void) { return BB_ABI_VERSION; }
+
+int bb_last_error(char* buf, int len) {
+  if (buf && len > 0) { strncpy(buf, g_err, len - 1); buf[len - 1] = 0; }
+  return (int)strlen(g_err);
+}
+
+void bb_default_params(bb_params* p) {
+  memset(p, 0, sizeof *p);
+  p->max_ep_steps = 4000;
+  p->max_allowed_tilt = 20.f;
+  p->max_wheel_velocity = 10.f;
+  p->reward_scale = 0.01f;
+  p->action_reg_coef = -0.0001f;
+  p->survival_bonus = 0.02f;
+  p->target_dir[0] = 0.f; p->target_dir[1] = 1.f;
+  p->reward_kind = BB_REWARD_DIRECTIONAL;
+  p->goal_scale = 1.f;
+  p->n_terrains = 1;
+  p->seed = 0;
+  p->fp64 = 0;
+}
+
+int bb_create(int n_envs, int device, const bb_params* p, bb_handle** out) {
+  if (!out) return fail("bb_create: out is NULL");
+  *out = nullptr;
+  if (n_envs <= 0) return fail("bb_create: n_envs must be > 0 (got %d)", n_envs);
+  bb_params pp;
+  if (p) pp = *p; else bb_default_params(&pp);
+  if (pp.n_terrains < 1) return fail("bb_create: n_terrains must be >= 1");
+  int ndev = 0;
+  HIPCHK(hipGetDeviceCount(&ndev));
+  if (device < 0 || device >= ndev) return fail("bb_create: device %d out of range (%d devices)", device, ndev);
+  HIPCHK(hipSetDevice(device));
+  bb_handle* h = new bb_handle();
+  h->n = n_envs; h->device = device; h->fp64 = pp.fp64 ? 1 : 0; h->p = pp;
+  EnvCfg& c = h->cfg;
+  c.max_ep_steps = pp.max_ep_steps; c.max_allowed_tilt = pp.max_allowed_tilt;
+  c.max_wheel_velocity = pp.max_wheel_velocity; c.reward_scale = pp.reward_scale;
+  c.action_reg_coef = pp.action_reg_coef; c.survival_bonus = pp.survival_bonus;
+  c.target[0] = pp.target_dir[0]; c.target[1] = pp.target_dir[1];
+  c.reward_kind = pp.reward_kind; c.goal[0] = pp.goal[0]; c.goal[1] = pp.goal[1]; c.goal_scale = pp.goal_scale;
+  SolverCfg sc = default_solver(h->fp64);
+  if (pp.solver_maxiter > 0) sc.maxiter = pp.solver_maxiter;
+  if (pp.solver_tol > 0) sc.tol = pp.solver_tol;
+  h->md = compile_model(sc);
+  h->mf = cast_model<float>(h->md);
+  const size_t es = h->fp64 ? sizeof(double) : sizeof(float);
+  const size_t n = n_envs, nt = pp.n_terrains;
+  Dev& d = h->d;
+  memset(&d, 0, sizeof d);
+  d.n = n_envs; d.n_terrains = pp.n_terrains; d.seed = pp.seed;
+  HIPCHK(hipMalloc(&d.qpos, es * NQ * n));
+  HIPCHK(hipMalloc(&d.qvel, es * NV * n));
+  HIPCHK(hipMalloc(&d.warm, es * NV * n));
+  HIPCHK(hipMalloc((void**)&d.steps, sizeof(int) * n));
+  HIPCHK(hipMalloc((void**)&d.terrain, sizeof(int) * n));
+  HIPCHK(hipMalloc((void**)&d.pending_terrain, sizeof(int) * n));
+  HIPCHK(hipMalloc((void**)&d.episodes, sizeof(int) * n));
+  HIPCHK(hipMalloc((void**)&h->bank, sizeof(float) * nt * HF_N * HF_N));
+  HIPCHK(hipMalloc((void**)&h->size_z, sizeof(float) * nt));
+  HIPCHK(hipMalloc((void**)&h->offset, sizeof(float) * nt));
+  HIPCHK(hipMalloc((void**)&d.stats, sizeof(unsigned long long) * 8));
+  HIPCHK(hipMemset(d.steps, 0, sizeof(int) * n));
+  HIPCHK(hipMemset(d.terrain, 0, sizeof(int) * n));
+  HIPCHK(hipMemset(d.pending_terrain, 0, sizeof(int) * n));
+  HIPCHK(hipMemset(d.episodes, 0, sizeof(int) * n));
+  HIPCHK(hipMemset(h->bank, 0, sizeof(float) * nt * HF_N * HF_N));
+  HIPCHK(hipMemset(d.stats, 0, sizeof(unsigned long long) * 8));
+  // default: every terrain flat (terrain/__init__.py:32-34), size_z 2.0 (ballbot.xml:23)
+  std::vector<float> sz(nt, 2.0f);
+  h->h_offset.assign(nt, 0.01f);
+  HIPCHK(hipMemcpy(h->size_z, sz.data(), sizeof(float) * nt, hipMemcpyHostToDevice));
+  HIPCHK(hipMemcpy(h->offset, h->h_offset.data(), sizeof(float) * nt, hipMemcpyHostToDevice));
+  d.bank = h->bank; d.size_z = h->size_z; d.offset = h->offset;
+  // LDS for the ground-contact store (f64: 120 KiB, above the 64 KiB default)
+  HIPCHK(hipFuncSetAttribute((const void*)step_kernel<float>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                             (int)lds_bytes<float>()));
+  HIPCHK(hipFuncSetAttribute((const void*)step_kernel<double>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                             (int)lds_bytes<double>()));
+  HIPCHK(hipFuncSetAttribute((const void*)forward_kernel<float>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                             (int)lds_bytes<float>()));
+  HIPCHK(hipFuncSetAttribute((const void*)forward_kernel<double>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                             (int)lds_bytes<double>()));
+  *out = h;
+  int rc = bb_reset(h, nullptr, nullptr, nullptr);
+  if (rc) return rc;
+  HIPCHK(hipDeviceSynchronize());
+  return 0;
+}
+
+int bb_destroy(bb_handle* h) {
+  if (!h) return 0;
+  hipSetDevice(h->device);
+  hipFree(h->d.qpos); hipFree(h->d.qvel); hipFree(h->d.warm);
+  hipFree(h->d.steps); hipFree(h->d.terrain); hipFree(h->d.pending_terrain); hipFree(h->d.episodes);
+  hipFree(h->bank); hipFree(h->size_z); hipFree(h->offset); hipFree(h->d.stats);
+  delete h;
+  return 0;
+}
+
+int bb_set_hfield(bb_handle* h, int terrain_id, const float* data, float size_z) {
+  if (!h) return fail("bb_set_hfield: NULL handle");
+  if (terrain_id < 0 || terrain_id >= h->p.n_terrains)
+    return fail("bb_set_hfield: terrain_id %d out of range [0,%d)", terrain_id, h->p.n_terrains);
+  if (!data) return fail("bb_set_hfield: NULL data");
+  if (!(size_z > 0)) return fail("bb_set_hfield: size_z must be > 0");
+  HIPCHK(hipSetDevice(h->device));
+  HIPCHK(hipMemcpy(h->bank + size_t(terrain_id) * HF_N * HF_N, data, sizeof(float) * HF_N * HF_N,
+                   hipMemcpyHostToDevice));
+  float off = init_offset(data, size_z);
+  h->h_offset[terrain_id] = off;
+  HIPCHK(hipMemcpy(h->size_z + terrain_id, &size_z, sizeof(float), hipMemcpyHostToDevice));
+  HIPCHK(hipMemcpy(h->offset + terrain_id, &off, sizeof(float), hipMemcpyHostToDevice));
+  return 0;
+}
+
+int bb_assign_terrain(bb_handle* h, const int32_t* ids, void* stream) {
+  if (!h || !ids) return fail("bb_assign_terrain: NULL argument");
+  HIPCHK(hipSetDevice(h->device));
+  hipLaunchKernelGGL(assign_kernel, dim3((h->n + 255) / 256), dim3(256), 0, (hipStream_t)stream, h->d, ids);
+  HIPCHK(hipGetLastError());
+  return 0;
+}
+
+int bb_reset(bb_handle* h, const uint8_t* mask, float* obs, void* stream) {
+  if (!h) return fail("bb_reset: NULL handle");
+  int blocks = (h->n + WAVE - 1) / WAVE;
+  if (h->fp64)
+    hipLaunchKernelGGL(reset_kernel<double>, dim3(blocks), dim3(WAVE), 0, (hipStream_t)stream, h->md, h->d, mask, obs);
+  else
+    hipLaunchKernelGGL(reset_kernel<float>, dim3(blocks), dim3(WAVE), 0, (hipStream_t)stream, h->mf, h->d, mask, obs);
+  HIPCHK(hipGetLastError());
+  return 0;
+}
+
+int bb_step(bb_handle* h, const float* a, float* o, float* r, uint8_t* dn, float* t, float* p2, int ar, void* s) {
+  if (!h) return fail("bb_step: NULL handle");
+  if (!a || !o || !r || !dn) return fail("bb_step: actions/obs/reward/done must be non-NULL");
+  return h->fp64 ? launch_step<double>(h, a, o, r, dn, t, p2, ar, (hipStream_t)s)
+                 : launch_step<float>(h, a, o, r, dn, t, p2, ar, (hipStream_t)s);
+}
+
+int bb_get_state(bb_handle* h, double* qpos, double* qvel, double* warm, int32_t* steps) {
+  if (!h) return fail("bb_get_state: NULL handle");
+  HIPCHK(hipSetDevice(h->device));
+  HIPCHK(hipDeviceSynchronize());
+  const size_t n = h->n, es = h->fp64 ? 8 : 4;
+  std::vector<unsigned char> buf(es * NQ * n);
+  auto conv = [&](void* dsrc, int nf, double* dst) -> int {
+    if (!dst) return 0;
+    HIPCHK(hipMemcpy(buf.data(), dsrc, es * nf * n, hipMemcpyDeviceToHost));
+    for (size_t e = 0; e < n; e++)
+      for (int i = 0; i < nf; i++)
+        dst[e * nf + i] = h->fp64 ? ((double*)buf.data())[i * n + e] : (double)((float*)buf.data())[i * n + e];
+    return 0;
+  };
+  if (conv(h->d.qpos, NQ, qpos) || conv(h->d.qvel, NV, qvel) || conv(h->d.warm, NV, warm)) return -1;
+  if (steps) HIPCHK(hipMemcpy(steps, h->d.steps, sizeof(int) * n, hipMemcpyDeviceToHost));
+  return 0;
+}
+
+int bb_set_state(bb_handle* h, const double* qpos, const double* qvel, const double* warm, const int32_t* steps) {
+  if (!h) return fail("bb_set_state: NULL handle");
+  HIPCHK(hipSetDevice(h->device));
+  HIPCHK(hipDeviceSynchronize());
+  const size_t n = h->n, es = h->fp64 ? 8 : 4;
+  std::vector<unsigned char> buf(es * NQ * n);
+  auto conv = [&](void* ddst, int nf, const double* src) -> int {
+    if (!src) return 0;
+    for (size_t e = 0; e < n; e++)
+      for (int i = 0; i < nf; i++) {
+        if (h->fp64) ((double*)buf.data())[i * n + e] = src[e * nf + i];
+        else ((float*)buf.data())[i * n + e] = (float)src[e * nf + i];
+      }
+    HIPCHK(hipMemcpy(ddst, buf.data(), es * nf * n, hipMemcpyHostToDevice));
+    return 0;
+  };
+  if (conv(h->d.qpos, NQ, qpos) || conv(h->d.qvel, NV, qvel) || conv(h->d.warm, NV, warm)) return -1;
+  if (steps) HIPCHK(hipMemcpy(h->d.steps, steps, sizeof(int) * n, hipMemcpyHostToDevice));
+  return 0;
+}
+
+int bb_forward(bb_handle* h, const double* ctrl, double* qacc, int32_t* ncon) {
+  if (!h || !ctrl || !qacc) return fail("bb_forward: NULL argument");
+  HIPCHK(hipSetDevice(h->device));
+  const size_t n = h->n;
+  double *dc = nullptr, *dq = nullptr;
+  int* dn = nullptr;
+  HIPCHK(hipMalloc(&dc, sizeof(double) * 3 * n));
+  HIPCHK(hipMalloc(&dq, sizeof(double) * NV * n));
+  HIPCHK(hipMalloc(&dn, sizeof(int) * n));
+  HIPCHK(hipMemcpy(dc, ctrl, sizeof(double) * 3 * n, hipMemcpyHostToDevice));
+  int blocks = (h->n + WAVE - 1) / WAVE;
+  if (h->fp64)
+    hipLaunchKernelGGL(forward_kernel<double>, dim3(blocks), dim3(WAVE), lds_bytes<double>(), 0, h->md, h->d, dc, dq, dn);
+  else
+    hipLaunchKernelGGL(forward_kernel<float>, dim3(blocks), dim3(WAVE), lds_bytes<float>(), 0, h->mf, h->d, dc, dq, dn);
+  HIPCHK(hipGetLastError());
+  HIPCHK(hipDeviceSynchronize());
+  HIPCHK(hipMemcpy(qacc, dq, sizeof(double) * NV * n, hipMemcpyDeviceToHost));
+  if (ncon) HIPCHK(hipMemcpy(ncon, dn, sizeof(int) * n, hipMemcpyDeviceToHost));
+  hipFree(dc); hipFree(dq); hipFree(dn);
+  return 0;
+}
+
+int bb_get_stats(bb_handle* h, int64_t* out6) {
+  if (!h || !out6) return fail("bb_get_stats: NULL argument");
+  HIPCHK(hipSetDevice(h->device));
+  unsigned long long s[8];
+  HIPCHK(hipMemcpy(s, h->d.stats, sizeof s, hipMemcpyDeviceToHost));
+  out6[0] = (int64_t)s[0]; out6[1] = (int64_t)s[1]; out6[2] = (int64_t)s[2];
+  out6[3] = (int64_t)s[3]; out6[4] = (int64_t)(s[4] & 0xffffffffull); out6[5] = (int64_t)(s[4] >> 32);
+  return 0;
+}
+
+int bb_get_offsets(bb_handle* h, float* out) {
+  if (!h || !out) return fail("bb_get_offsets: NULL argument");
+  memcpy(out, h->h_offset.data(), sizeof(float) * h->h_offset.size());
+  return 0;
+}
+
+}  // extern "C"

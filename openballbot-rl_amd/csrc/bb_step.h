@@ -1,0 +1,215 @@
+// bb_step.h -- one env step = one BBotSimulation.step (ballbot_env.py:854-1036):
+//   action -> ctrl (:903-907), mj_step with RK4 (:912), _get_obs (:771-811),
+//   DirectionalReward + action penalty + survival bonus (:929-937, :1019),
+//   termination (:982-1017).  Per lane, templated on T (see bb_physics.h).
+#pragma once
+
+#include "bb_physics.h"
+
+namespace bb {
+
+// Env configuration (BBotSimulation.__init__, ballbot_env.py:221-231).
+struct EnvCfg {
+  int max_ep_steps;        // 4000
+  float max_allowed_tilt;  // 20 deg
+  float max_wheel_velocity;  // 10
+  float reward_scale;      // 0.01
+  float action_reg_coef;   // -1e-4
+  float survival_bonus;    // 0.02
+  float target[2];         // DirectionalReward target_direction
+  int reward_kind;         // 0 directional, 1 distance (needs pos2d; raises in ref), 2 none (host plugin)
+  float goal[2], goal_scale;
+};
+
+// What mjData holds after the last forward of mj_step (RK stage 4).
+template <typename T>
+struct StageOut {
+  T quat_b[4];   // xquat[base] (normalised)
+  T w_world[3];  // cvel[base][0:3]
+  T v_com[3];    // cvel[base][3:6] (linear velocity at subtree_com[base])
+  T pb[3];       // xpos[base]
+  int ng, iters, overflow;
+};
+
+// mj_forward for this model: returns qacc in acc (acc holds the warm start on entry).
+template <typename T>
+BB_HD int forward(const ModelT<T>& m, const T* q, const T* v, const T* ctrl, T* acc, const float* hf, T size_z,
+                  const GStore<T>& st, StageOut<T>* so) {
+  Kin<T> k;
+  kinematics(m, q, k);
+  Mass<T> M;
+  build_mass(m, k, M);
+  T qfs[NV];
+  bias_forces(m, k, M, v, qfs);
+#pragma unroll
+  for (int i = 0; i < NV; i++) qfs[i] = -qfs[i];
+#pragma unroll
+  for (int w = 0; w < 3; w++) qfs[6 + w] += -m.damping * v[6 + w] + ctrl[w];
+  WheelCon<T> WC[3];
+#pragma unroll
+  for (int w = 0; w < 3; w++) wheel_contact(m, k, v, w, WC[w]);
+  int overflow = 0;
+  int ng = hf ? collide_ground(m, k, v, hf, size_z, st, &overflow) : 0;
+  bool ok = true;
+#pragma unroll
+  for (int i = 0; i < NV; i++) ok = ok && isfinite(acc[i]);
+  if (!ok) {
+#pragma unroll
+    for (int i = 0; i < NV; i++) acc[i] = 0;
+  }
+  int it = solve(m, k, M, qfs, WC, ng, st, acc);
+  if (so) {
+    T qb[4] = {q[3], q[4], q[5], q[6]};
+    qnormalize(qb);
+    so->quat_b[0] = qb[0]; so->quat_b[1] = qb[1]; so->quat_b[2] = qb[2]; so->quat_b[3] = qb[3];
+    mv3(so->w_world, k.Rb, v + 3);
+    // subtree_com[base] - xpos[base] = Rb * mr / mt
+    T cl[3] = {M.mr[0] / M.mt, M.mr[1] / M.mt, M.mr[2] / M.mt}, cw[3], t[3];
+    mv3(cw, k.Rb, cl);
+    cross3(t, so->w_world, cw);
+    so->v_com[0] = v[0] + t[0]; so->v_com[1] = v[1] + t[1]; so->v_com[2] = v[2] + t[2];
+    so->pb[0] = q[0]; so->pb[1] = q[1]; so->pb[2] = q[2];
+    so->ng = ng; so->iters = it; so->overflow = overflow;
+  }
+  return it;
+}
+
+// mj_step with integrator RK4 = mj_forward + mj_RungeKutta(N=4) + mj_advance.
+// warm: qacc_warmstart (each stage's constraint solve saves its qacc).
+template <typename T>
+BB_HD int rk4_step(const ModelT<T>& m, T* q, T* v, T* warm, const T* ctrl, const float* hf, T size_z,
+                   const GStore<T>& st, StageOut<T>& so) {
+  const T h = m.h;
+  T q0[NQ], v0[NV], vs[NV], as[NV], vp[NV];
+#pragma unroll
+  for (int i = 0; i < NQ; i++) q0[i] = q[i];
+#pragma unroll
+  for (int i = 0; i < NV; i++) v0[i] = v[i];
+  int iters = forward(m, q0, v0, ctrl, warm, hf, size_z, st, (StageOut<T>*)nullptr);
+#pragma unroll
+  for (int i = 0; i < NV; i++) { vs[i] = v0[i] * T(1.0 / 6); as[i] = warm[i] * T(1.0 / 6); vp[i] = v0[i]; }
+  for (int stage = 1; stage < 4; stage++) {
+    const T a = stage < 3 ? T(0.5) : T(1);       // RK4 Butcher A (sub-diagonal)
+    const T b = stage < 3 ? T(1.0 / 3) : T(1.0 / 6);
+    T qi[NQ], vi[NV], dv[NV];
+#pragma unroll
+    for (int i = 0; i < NQ; i++) qi[i] = q0[i];
+#pragma unroll
+    for (int i = 0; i < NV; i++) { dv[i] = a * vp[i]; vi[i] = v0[i] + h * a * warm[i]; }
+    integrate_pos(qi, dv, h);
+    iters += forward(m, qi, vi, ctrl, warm, hf, size_z, st, stage == 3 ? &so : (StageOut<T>*)nullptr);
+#pragma unroll
+    for (int i = 0; i < NV; i++) { vs[i] += b * vi[i]; as[i] += b * warm[i]; vp[i] = vi[i]; }
+  }
+  // mj_advance: qvel = v0 + h*qacc_rk ; qpos = q0 (+) h*v_rk
+#pragma unroll
+  for (int i = 0; i < NV; i++) v[i] = v0[i] + h * as[i];
+#pragma unroll
+  for (int i = 0; i < NQ; i++) q[i] = q0[i];
+  integrate_pos(q, vs, h);
+  return iters;
+}
+
+// numpy-quaternion as_rotation_vector (quaternion_log, eps 1e-14): no w>=0
+// canonicalisation.
+template <typename T>
+BB_HD void quat_to_rotvec(const T* q, T* rv) {
+  T b = sqrt(q[1] * q[1] + q[2] * q[2] + q[3] * q[3]);
+  if (fabs(b) <= T(1e-14) * fabs(q[0])) {
+    rv[0] = q[0] < 0 ? T(2 * 3.14159265358979323846) : T(0);
+    rv[1] = rv[2] = 0;
+    return;
+  }
+  T f = 2 * atan2(b, q[0]) / b;
+  rv[0] = f * q[1]; rv[1] = f * q[2]; rv[2] = f * q[3];
+}
+
+BB_HD float clipf(float x, float lo, float hi) { return x < lo ? lo : (x > hi ? hi : x); }
+
+template <typename T>
+BB_HD bool state_bad(const T* q, const T* v) {
+  bool bad = false;
+#pragma unroll
+  for (int i = 0; i < NQ; i++) bad = bad || !(fabs(q[i]) <= T(1e10));
+#pragma unroll
+  for (int i = 0; i < NV; i++) bad = bad || !(fabs(v[i]) <= T(1e10));
+  return bad;
+}
+
+// flags returned by env_step
+constexpr int F_TERMINATED = 1, F_FAILURE = 2, F_DIVERGED = 4, F_OVERFLOW = 8;
+
+// One BBotSimulation.step.  obs15 = sorted keys (actions, angular_vel,
+// motor_state, orientation, vel), the order the policy's Extractor consumes.
+template <typename T>
+BB_HD int env_step(const ModelT<T>& m, const EnvCfg& cfg, T* q, T* v, T* warm, int& step, const float* action,
+                   const float* hf, T size_z, const GStore<T>& st, float* obs15, float& reward, float* pos2d,
+                   int* iters) {
+  const float mwv = cfg.max_wheel_velocity;
+  T ctrl[3];
+#pragma unroll
+  for (int i = 0; i < 3; i++) ctrl[i] = -T(clipf(action[i] * mwv, -mwv, mwv));  // data.ctrl[:] = -ctrl
+  StageOut<T> so;
+  int it = rk4_step(m, q, v, warm, ctrl, hf, size_z, st, so);
+  if (iters) *iters = it;
+  int flags = state_bad(q, v) ? F_DIVERGED : 0;
+  if (so.overflow) flags |= F_OVERFLOW;
+  // _get_obs
+  T rv[3];
+  quat_to_rotvec(so.quat_b, rv);
+  float orient[3] = {float(rv[0]), float(rv[1]), float(rv[2])};
+  float vel[3], angv[3], motor[3];
+#pragma unroll
+  for (int i = 0; i < 3; i++) {
+    vel[i] = clipf(float(so.w_world[i]), -2.f, 2.f);     // "vel" = cvel[0:3] (angular)
+    angv[i] = clipf(float(so.v_com[i]), -2.f, 2.f);      // "angular_vel" = cvel[3:6] (linear)
+    motor[i] = clipf(float(v[1 + i]) / mwv, -2.f, 2.f);  // qvel[joint id 1..3]
+  }
+#pragma unroll
+  for (int i = 0; i < 3; i++) {
+    obs15[i] = action[i]; obs15[3 + i] = angv[i]; obs15[6 + i] = motor[i];
+    obs15[9 + i] = orient[i]; obs15[12 + i] = vel[i];
+  }
+  pos2d[0] = float(so.pb[0]);
+  pos2d[1] = float(so.pb[1]);
+  // reward terms in float32 (numpy float32 chain under NumPy 2)
+  float r;
+  if (cfg.reward_kind == 0) {
+    r = (vel[0] * cfg.target[0] + vel[1] * cfg.target[1]) * cfg.reward_scale;
+  } else if (cfg.reward_kind == 1) {
+    float dx = cfg.goal[0] - pos2d[0], dy = cfg.goal[1] - pos2d[1];
+    r = (-cfg.goal_scale * sqrtf(dx * dx + dy * dy)) * cfg.reward_scale;
+  } else {
+    r = 0.f;
+  }
+  float nrm = sqrtf(action[0] * action[0] + action[1] * action[1] + action[2] * action[2]);
+  r = r + cfg.action_reg_coef * (nrm * nrm);
+  step += 1;
+  if (step >= cfg.max_ep_steps) flags |= F_TERMINATED;
+  // tilt: R(from_rotation_vector(f32 rotvec))[2,2]
+  T rx = orient[0], ry = orient[1], rz = orient[2];
+  T th = sqrt(rx * rx + ry * ry + rz * rz) * T(0.5);
+  T sf = th > T(1e-14) ? sin(th) / th : T(1);
+  T qw = th > T(1e-14) ? cos(th) : T(1);
+  T qx = sf * rx * T(0.5), qy = sf * ry * T(0.5), qz = sf * rz * T(0.5);
+  T nn = qw * qw + qx * qx + qy * qy + qz * qz;
+  T R22 = T(1) - 2 * (qx * qx + qy * qy) / nn;
+  T ang = acos(clampT(R22, T(-1), T(1))) * T(180 / 3.14159265358979323846);
+  if (ang > T(cfg.max_allowed_tilt)) flags |= F_FAILURE | F_TERMINATED;
+  else r = r + cfg.survival_bonus;
+  reward = r;
+  return flags;
+}
+
+// mj_resetData + height offset (ballbot_env.py:612-620)
+template <typename T>
+BB_HD void reset_state(const ModelT<T>& m, T offset, T* q, T* v, T* warm) {
+#pragma unroll
+  for (int i = 0; i < NQ; i++) q[i] = m.qpos0[i];
+  q[2] += offset;
+  q[12] += offset;
+#pragma unroll
+  for (int i = 0; i < NV; i++) { v[i] = 0; warm[i] = 0; }
+}
+
+}  // namespace bb

@@ -1,0 +1,88 @@
+"""ctypes binding of the test-only host build of the product templates."""
+import ctypes as C
+import subprocess
+from pathlib import Path
+
+import numpy as np
+
+ROOT = Path(__file__).resolve().parent.parent
+LIB = ROOT / "tests" / "_build" / "libbb_hostcheck.so"
+SRC = ROOT / "tests" / "hostcheck" / "bb_hostcheck.cpp"
+CSRC = ROOT / "openballbot-rl_amd" / "csrc"
+
+
+class EnvCfg(C.Structure):
+    _fields_ = [("max_ep_steps", C.c_int), ("max_allowed_tilt", C.c_float), ("max_wheel_velocity", C.c_float),
+                ("reward_scale", C.c_float), ("action_reg_coef", C.c_float), ("survival_bonus", C.c_float),
+                ("target", C.c_float * 2), ("reward_kind", C.c_int), ("goal", C.c_float * 2),
+                ("goal_scale", C.c_float)]
+
+
+def default_cfg(max_ep_steps=4000, target=(0.0, 1.0)):
+    c = EnvCfg()
+    c.max_ep_steps = max_ep_steps
+    c.max_allowed_tilt = 20.0
+    c.max_wheel_velocity = 10.0
+    c.reward_scale = 0.01
+    c.action_reg_coef = -0.0001
+    c.survival_bonus = 0.02
+    c.target[0], c.target[1] = target
+    c.reward_kind = 0
+    return c
+
+
+_lib = None
+
+
+def build():
+    LIB.parent.mkdir(parents=True, exist_ok=True)
+    srcs = [SRC] + sorted(CSRC.glob("*.h"))
+    if LIB.exists() and all(LIB.stat().st_mtime >= s.stat().st_mtime for s in srcs):
+        return
+    subprocess.run(["hipcc", "-O2", "-fPIC", "-shared", "--offload-arch=gfx950", "-std=c++17", f"-I{CSRC}",
+                    "-o", str(LIB), str(SRC)], check=True)
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        build()
+        L = C.CDLL(str(LIB))
+        dp, fp, ip = C.POINTER(C.c_double), C.POINTER(C.c_float), C.POINTER(C.c_int)
+        L.hc_forward.argtypes = [dp, dp, dp, dp, fp, C.c_double, C.c_int, dp]
+        L.hc_env_step.argtypes = [C.POINTER(EnvCfg), dp, dp, dp, ip, fp, fp, C.c_double, fp, fp, fp, C.c_int]
+        L.hc_model.argtypes = [dp]
+        _lib = L
+    return _lib
+
+
+def _d(a):
+    return a.ctypes.data_as(C.POINTER(C.c_double))
+
+
+def _f(a):
+    return None if a is None else a.ctypes.data_as(C.POINTER(C.c_float))
+
+
+def model():
+    out = np.zeros(16)
+    lib().hc_model(_d(out))
+    return out
+
+
+def forward(q, v, ctrl, warm, hf, size_z=2.0, fp64=True):
+    q = np.ascontiguousarray(q, np.float64); v = np.ascontiguousarray(v, np.float64)
+    c = np.ascontiguousarray(ctrl, np.float64); acc = np.array(warm, np.float64)
+    extra = np.zeros(16)
+    hfa = None if hf is None else np.ascontiguousarray(hf, np.float32)
+    it = lib().hc_forward(_d(q), _d(v), _d(c), _d(acc), _f(hfa), size_z, int(fp64), _d(extra))
+    return acc, it, extra
+
+
+def env_step(cfg, q, v, w, step, action, hf, size_z=2.0, fp64=True):
+    obs = np.zeros(15, np.float32); rew = np.zeros(1, np.float32); p2 = np.zeros(2, np.float32)
+    a = np.ascontiguousarray(action, np.float32)
+    hfa = np.ascontiguousarray(hf, np.float32)
+    fl = lib().hc_env_step(C.byref(cfg), _d(q), _d(v), _d(w), step.ctypes.data_as(C.POINTER(C.c_int)), _f(a),
+                           _f(hfa), size_z, _f(obs), _f(rew), _f(p2), int(fp64))
+    return obs, float(rew[0]), fl & 0xff, p2, fl >> 8
