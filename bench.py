@@ -77,7 +77,7 @@ def main() -> None:
     ap.add_argument("--steps", type=int, default=300)
     ap.add_argument("--warmup", type=int, default=30)
     ap.add_argument("--envs", type=int, default=4096, help="envs per GPU")
-    ap.add_argument("--precision", default="fp32", choices=["fp32", "fp64"])
+    ap.add_argument("--precision", default="fp64", choices=["fp32", "fp64"])
     ap.add_argument("--terrain", default="flat")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
@@ -157,7 +157,8 @@ def main() -> None:
             "data": "synthetic (uniform random actions in [-1,1], resident in HBM)",
             "config": {"workload": f"{n} envs/GPU, {args.terrain} terrain, random actions (BASELINE configs[1])",
                        "envs_per_gpu": n, "total_envs": n * world, "precision": args.precision,
-                       "parallelism": f"env-sharded x{world} (no collective on the step path)"},
+                       "parallelism": f"env-sharded x{world} (no collective on the step path)",
+                       "envs_per_wave": os.environ.get("BB_EPW", "auto")},
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
                          "note": "latency/VALU-bound per-lane physics; HBM bytes = algorithmic state I/O "

@@ -42,7 +42,7 @@ class BallbotVecEnv:
         env_config: Optional[Dict[str, Any]] = None,
         max_ep_steps: Optional[int] = None,
         seed: int = 0,
-        precision: str = "fp32",
+        precision: str = "fp64",
         n_terrains: Optional[int] = None,
         auto_reset: bool = True,
     ):

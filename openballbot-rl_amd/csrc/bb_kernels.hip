@@ -39,7 +39,7 @@ int fail(const char* fmt, ...) {
   } while (0)
 
 template <typename T>
-size_t lds_bytes() { return size_t(MAXG) * NGF * WAVE * sizeof(T); }
+size_t lds_bytes(int epw) { return size_t(MAXG) * NGF * epw * sizeof(T); }
 
 BB_HD uint32_t hash3(uint64_t seed, uint32_t a, uint32_t b) {  // splitmix-style counter hash
   uint64_t z = seed + 0x9E3779B97F4A7C15ull * (uint64_t(a) * 0x100000001ull + b + 1);
@@ -100,12 +100,15 @@ template <typename T>
 __global__ __launch_bounds__(64) void step_kernel(ModelT<T> m, EnvCfg cfg, Dev d, const float* __restrict__ act,
                                                   float* __restrict__ obs, float* __restrict__ rew,
                                                   uint8_t* __restrict__ done, float* __restrict__ tobs,
-                                                  float* __restrict__ pos2d, int auto_reset) {
+                                                  float* __restrict__ pos2d, int auto_reset, int epw) {
+  // epw envs per 64-lane wave (lanes >= epw idle): spreads small batches over
+  // all 1024 SIMDs instead of a few fully-populated waves.
   extern __shared__ __align__(16) unsigned char smem[];
   const int lane = threadIdx.x;
-  const int e = blockIdx.x * WAVE + lane;
+  if (lane >= epw) return;
+  const int e = blockIdx.x * epw + lane;
   if (e >= d.n) return;
-  GStore<T> st{reinterpret_cast<T*>(smem) + lane, WAVE};
+  GStore<T> st{reinterpret_cast<T*>(smem) + lane, epw};
   T q[NQ], v[NV], w[NV];
   int step;
   load_state(d, e, q, v, w, step);
@@ -163,7 +166,7 @@ __global__ __launch_bounds__(64) void forward_kernel(ModelT<T> m, Dev d, const d
   const int lane = threadIdx.x;
   const int e = blockIdx.x * WAVE + lane;
   if (e >= d.n) return;
-  GStore<T> st{reinterpret_cast<T*>(smem) + lane, WAVE};
+  GStore<T> st{reinterpret_cast<T*>(smem) + lane, WAVE};  // diagnostic: full waves
   T q[NQ], v[NV], w[NV], c[3];
   int step;
   load_state(d, e, q, v, w, step);
@@ -185,7 +188,7 @@ __global__ void assign_kernel(Dev d, const int32_t* ids) {
 }  // namespace
 
 struct bb_handle {
-  int n, device, fp64;
+  int n, device, fp64, epw;
   bb_params p;
   EnvCfg cfg;
   ModelT<float> mf;
@@ -219,9 +222,10 @@ template <typename T>
 int launch_step(bb_handle* h, const float* a, float* o, float* r, uint8_t* dn, float* t, float* p2, int ar,
                 hipStream_t s) {
   const ModelT<T>& m = model_of<T>(h);
-  int blocks = (h->n + WAVE - 1) / WAVE;
-  hipLaunchKernelGGL(step_kernel<T>, dim3(blocks), dim3(WAVE), lds_bytes<T>(), s, m, h->cfg, h->d, a, o, r, dn, t,
-                     p2, ar);
+  const int epw = h->epw;
+  int blocks = (h->n + epw - 1) / epw;
+  hipLaunchKernelGGL(step_kernel<T>, dim3(blocks), dim3(WAVE), lds_bytes<T>(epw), s, m, h->cfg, h->d, a, o, r, dn,
+                     t, p2, ar, epw);
   HIPCHK(hipGetLastError());
   return 0;
 }
@@ -274,6 +278,17 @@ int bb_create(int n_envs, int device, const bb_params* p, bb_handle** out) {
   SolverCfg sc = default_solver(h->fp64);
   if (pp.solver_maxiter > 0) sc.maxiter = pp.solver_maxiter;
   if (pp.solver_tol > 0) sc.tol = pp.solver_tol;
+  // envs per wave: aim for one wave per SIMD (4 per CU) across the whole chip
+  {
+    hipDeviceProp_t prop;
+    HIPCHK(hipGetDeviceProperties(&prop, device));
+    const int simds = prop.multiProcessorCount * 4;
+    int epw = 1;
+    while (epw < WAVE && (long)epw * simds < (long)n_envs) epw *= 2;
+    const char* ov = getenv("BB_EPW");
+    if (ov && atoi(ov) > 0) epw = atoi(ov) > WAVE ? WAVE : atoi(ov);
+    h->epw = epw;
+  }
   h->md = compile_model(sc);
   h->mf = cast_model<float>(h->md);
   const size_t es = h->fp64 ? sizeof(double) : sizeof(float);
@@ -306,13 +321,13 @@ int bb_create(int n_envs, int device, const bb_params* p, bb_handle** out) {
   d.bank = h->bank; d.size_z = h->size_z; d.offset = h->offset;
   // LDS for the ground-contact store (f64: 120 KiB, above the 64 KiB default)
   HIPCHK(hipFuncSetAttribute((const void*)step_kernel<float>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                             (int)lds_bytes<float>()));
+                             (int)lds_bytes<float>(WAVE)));
   HIPCHK(hipFuncSetAttribute((const void*)step_kernel<double>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                             (int)lds_bytes<double>()));
+                             (int)lds_bytes<double>(WAVE)));
   HIPCHK(hipFuncSetAttribute((const void*)forward_kernel<float>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                             (int)lds_bytes<float>()));
+                             (int)lds_bytes<float>(WAVE)));
   HIPCHK(hipFuncSetAttribute((const void*)forward_kernel<double>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                             (int)lds_bytes<double>()));
+                             (int)lds_bytes<double>(WAVE)));
   *out = h;
   int rc = bb_reset(h, nullptr, nullptr, nullptr);
   if (rc) return rc;
@@ -424,9 +439,9 @@ int bb_forward(bb_handle* h, const double* ctrl, double* qacc, int32_t* ncon) {
   HIPCHK(hipMemcpy(dc, ctrl, sizeof(double) * 3 * n, hipMemcpyHostToDevice));
   int blocks = (h->n + WAVE - 1) / WAVE;
   if (h->fp64)
-    hipLaunchKernelGGL(forward_kernel<double>, dim3(blocks), dim3(WAVE), lds_bytes<double>(), 0, h->md, h->d, dc, dq, dn);
+    hipLaunchKernelGGL(forward_kernel<double>, dim3(blocks), dim3(WAVE), lds_bytes<double>(WAVE), 0, h->md, h->d, dc, dq, dn);
   else
-    hipLaunchKernelGGL(forward_kernel<float>, dim3(blocks), dim3(WAVE), lds_bytes<float>(), 0, h->mf, h->d, dc, dq, dn);
+    hipLaunchKernelGGL(forward_kernel<float>, dim3(blocks), dim3(WAVE), lds_bytes<float>(WAVE), 0, h->mf, h->d, dc, dq, dn);
   HIPCHK(hipGetLastError());
   HIPCHK(hipDeviceSynchronize());
   HIPCHK(hipMemcpy(qacc, dq, sizeof(double) * NV * n, hipMemcpyDeviceToHost));

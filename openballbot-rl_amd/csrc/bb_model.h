@@ -49,15 +49,15 @@ inline void capsule(double rho, double r, double hh, double& m, double* I) {
 }  // namespace detail
 
 struct SolverCfg {
-  double tol, ls_tol;
+  double tol, ls_tol, step_rel;
   int maxiter, ls_maxiter;
 };
 
 inline SolverCfg default_solver(bool fp64) {
   // MuJoCo: tolerance 1e-8, iterations 100, ls_iterations 50.  The minimiser is
   // unique, so the fp32 build stops at its roundoff floor instead.
-  if (fp64) return SolverCfg{1e-10, 1e-8, 40, 40};
-  return SolverCfg{2e-6, 1e-3, 16, 16};
+  if (fp64) return SolverCfg{1e-10, 1e-8, 1e-14, 40, 40};
+  return SolverCfg{2e-6, 1e-3, 3e-7, 16, 16};
 }
 
 // Compile ballbot.xml (values cited per line) into a double-precision model.
@@ -146,7 +146,8 @@ inline ModelT<double> compile_model(const SolverCfg& sc) {
   for (int i = 0; i < NQ; i++) m.qpos0[i] = 0;
   m.qpos0[2] = 0.24; m.qpos0[3] = 1;   // base pos (ballbot.xml:38)
   m.qpos0[12] = 0.26; m.qpos0[13] = 1; // ball pos (ballbot.xml:76)
-  m.tol = sc.tol; m.ls_tol = sc.ls_tol; m.maxiter = sc.maxiter; m.ls_maxiter = sc.ls_maxiter;
+  m.tol = sc.tol; m.ls_tol = sc.ls_tol; m.step_rel2 = sc.step_rel * sc.step_rel;
+  m.maxiter = sc.maxiter; m.ls_maxiter = sc.ls_maxiter;
 
   // ---- mj_setConst at qpos0: meaninertia, body_invweight0
   Kin<double> k;
@@ -219,7 +220,7 @@ inline ModelT<T> cast_model(const ModelT<double>& d) {
   BBC(wheel_r); BBC(wheel_hh); BBC(armature); BBC(damping);
   BBC(mB); BBC(IB); BBC(ball_r); BBC(dz);
   BBC(iw_ball); BBA(iw_wheel, 3); BBC(K); BBC(Bd); BBA(solimp, 5); BBA(fr_wheel, 2);
-  BBC(h); BBC(grav); BBC(hf_sx); BBC(hf_sy); BBC(hf_bottom); BBC(scale); BBC(tol); BBC(ls_tol);
+  BBC(h); BBC(grav); BBC(hf_sx); BBC(hf_sy); BBC(hf_bottom); BBC(scale); BBC(tol); BBC(ls_tol); BBC(step_rel2);
   m.maxiter = d.maxiter; m.ls_maxiter = d.ls_maxiter;
   BBA(qpos0, NQ);
 #undef BBC

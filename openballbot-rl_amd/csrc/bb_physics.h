@@ -61,7 +61,7 @@ struct ModelT {
   // options / solver
   T h, grav;
   T hf_sx, hf_sy, hf_bottom;
-  T scale, tol, ls_tol;
+  T scale, tol, ls_tol, step_rel2;  // step_rel2: stop when |alpha s|^2 <= step_rel2 (1 + |a|^2)
   int maxiter, ls_maxiter;
   T qpos0[NQ];
 };
@@ -110,9 +110,6 @@ template <typename T> BB_HD void sym_rot(T* out, const T* R, const T* S) {  // R
     for (int j = 0; j < 3; j++) B[3 * i + j] = A[3 * i] * R[3 * j] + A[3 * i + 1] * R[3 * j + 1] + A[3 * i + 2] * R[3 * j + 2];
   out[0] = B[0]; out[1] = B[4]; out[2] = B[8]; out[3] = B[1]; out[4] = B[2]; out[5] = B[5];
 }
-template <typename T> BB_HD T sq_eps();
-template <> BB_HD float sq_eps<float>() { return 1e-13f; }
-template <> BB_HD double sq_eps<double>() { return 1e-28; }
 template <typename T> BB_HD T clampT(T x, T lo, T hi) { return x < lo ? lo : (x > hi ? hi : x); }
 template <typename T> BB_HD T maxT(T a, T b) { return a > b ? a : b; }
 template <typename T> BB_HD T minT(T a, T b) { return a < b ? a : b; }
@@ -757,14 +754,26 @@ BB_HD int collide_ground(const ModelT<T>& m, const Kin<T>& k, const T* v, const 
 }
 
 // ------------------------------------------------------------ Newton solve
+template <typename T> BB_HD T eps_of();
+template <> BB_HD float eps_of<float>() { return 1.1920929e-7f; }
+template <> BB_HD double eps_of<double>() { return 2.220446049250313e-16; }
+template <typename T> BB_HD T pivot_eps();
+template <> BB_HD float pivot_eps<float>() { return 1e-6f; }
+template <> BB_HD double pivot_eps<double>() { return 1e-14; }
+
+// In-place packed Cholesky.  A pivot that roundoff drives below eps*H_jj
+// (fp32 with the 1e6x stiffer drive-direction rows) is floored relative to
+// the diagonal, so the Newton direction stays finite; descent is then
+// enforced by the line search.
 template <typename T>
 BB_HD void chol_packed(T* H) {
 #pragma unroll
   for (int j = 0; j < NV; j++) {
     T s = H[hidx(j, j)];
+    const T floor_j = pivot_eps<T>() * maxT(H[hidx(j, j)], T(1e-30));
 #pragma unroll
     for (int k = 0; k < j; k++) s -= H[hidx(j, k)] * H[hidx(j, k)];
-    s = maxT(s, T(1e-30));
+    s = s > floor_j ? s : floor_j;
     T d = sqrt(s), id = T(1) / d;
     H[hidx(j, j)] = d;
 #pragma unroll
@@ -919,13 +928,31 @@ BB_HD int solve(const ModelT<T>& m, const Kin<T>& k, const Mass<T>& M, const T* 
     T gn = 0;
 #pragma unroll
     for (int i = 0; i < NV; i++) gn += g[i] * g[i];
+#ifdef BB_TRACE
+    printf("it %d gn %.4e\n", it, double(m.scale * sqrt(gn)));
+#endif
     if (m.scale * sqrt(gn) < m.tol) break;
     // ---- Newton direction
+    T hd[NV];
+#pragma unroll
+    for (int i = 0; i < NV; i++) hd[i] = H[hidx(i, i)];
     chol_packed(H);
     T s[NV];
 #pragma unroll
     for (int i = 0; i < NV; i++) s[i] = -g[i];
     chol_solve_packed(H, s);
+    {
+      // a roundoff-indefinite Hessian (fp32, stiff drive rows) can give a
+      // non-descent or non-finite direction: fall back to diagonal Newton
+      bool fin = true;
+      T dd = 0;
+#pragma unroll
+      for (int i = 0; i < NV; i++) { fin = fin && isfinite(s[i]); dd += s[i] * g[i]; }
+      if (!fin || !(dd < 0)) {
+#pragma unroll
+        for (int i = 0; i < NV; i++) s[i] = -g[i] / maxT(hd[i], T(1e-30));
+      }
+    }
     // ---- exact line search on phi(alpha) = f(a + alpha s)
     T Ms[NV];
     mass_mul(M, s, Ms);
@@ -944,9 +971,14 @@ BB_HD int solve(const ModelT<T>& m, const Kin<T>& k, const Mass<T>& M, const T* 
     T wa[3], ws[3];
     mv3(wa, k.RB, a + 12);
     mv3(ws, k.RB, s + 12);
-    T lo = 0, hi = -1, alpha = 1;
-    for (int ls = 0; ls < m.ls_maxiter; ls++) {
+    // 1-D Newton on phi'(alpha) from the full Newton step alpha = 1,
+    // safeguarded by false position on the bracket [lo, hi] (phi' is
+    // continuous and nondecreasing: the cost is convex and C1).
+    T lo = 0, dlo = d0, hi = -1, dhi = 0, alpha = 1;
+    bool ls_ok = false;
+    for (int ls = 1; ls <= m.ls_maxiter; ls++) {
       T d1 = gs + alpha * sMs, d2 = sMs;
+      T dmag = fabs(gs) + fabs(alpha * sMs);  // magnitude of the summed terms: roundoff floor of d1
 #pragma unroll
       for (int w = 0; w < 3; w++) {
         T jr[3] = {ja[w][0] + alpha * js[w][0], ja[w][1] + alpha * js[w][1], ja[w][2] + alpha * js[w][2]};
@@ -954,6 +986,7 @@ BB_HD int solve(const ModelT<T>& m, const Kin<T>& k, const Mass<T>& M, const T* 
         cone_eval(jr, mu_w, f1w, f2w, WC[w].D, f, Cc);
         const T* x = js[w];
         d1 -= f[0] * x[0] + f[1] * x[1] + f[2] * x[2];
+        dmag += fabs(f[0] * x[0]) + fabs(f[1] * x[1]) + fabs(f[2] * x[2]);
         d2 += Cc[0] * x[0] * x[0] + Cc[1] * x[1] * x[1] + Cc[2] * x[2] * x[2] +
               2 * (Cc[3] * x[0] * x[1] + Cc[4] * x[0] * x[2] + Cc[5] * x[1] * x[2]);
       }
@@ -973,20 +1006,36 @@ BB_HD int solve(const ModelT<T>& m, const Kin<T>& k, const Mass<T>& M, const T* 
         T Dv[3] = {D, D, D}, f[3], Cc[6];
         cone_eval(jr, T(1), T(1), T(1), Dv, f, Cc);
         d1 -= f[0] * x[0] + f[1] * x[1] + f[2] * x[2];
+        dmag += fabs(f[0] * x[0]) + fabs(f[1] * x[1]) + fabs(f[2] * x[2]);
         d2 += Cc[0] * x[0] * x[0] + Cc[1] * x[1] * x[1] + Cc[2] * x[2] * x[2] +
               2 * (Cc[3] * x[0] * x[1] + Cc[4] * x[0] * x[2] + Cc[5] * x[1] * x[2]);
       }
-      if (fabs(d1) <= m.ls_tol * fabs(d0)) break;
-      if (d1 < 0) lo = alpha; else hi = alpha;
+      if (ls > 0) {
+        // converged: relative to phi'(0), or at the arithmetic's roundoff floor
+        if (fabs(d1) <= m.ls_tol * fabs(d0) || fabs(d1) <= T(32) * eps_of<T>() * dmag) { ls_ok = true; break; }
+        if (!(d1 == d1)) break;
+        if (d1 < 0) { lo = alpha; dlo = d1; } else { hi = alpha; dhi = d1; }
+      }
       T an = alpha - d1 / maxT(d2, T(1e-30));
-      if (hi < 0) { if (!(an > lo)) an = 2 * alpha; }
-      else if (!(an > lo && an < hi)) an = T(0.5) * (lo + hi);
+      if (hi < 0) {
+        if (!(an > lo)) an = lo > 0 ? 2 * lo : T(1);
+      } else if (!(an > lo && an < hi)) {
+        T fp = lo - dlo * (hi - lo) / (dhi - dlo);
+        an = (fp > lo && fp < hi) ? fp : T(0.5) * (lo + hi);
+      }
       alpha = an;
     }
+    // unconverged search: fall back to the last point with phi' < 0, which
+    // (phi convex) is guaranteed to lower the cost
+    if (!ls_ok) alpha = lo > 0 ? lo : (hi > 0 ? hi * dlo / (dlo - dhi) : T(0));
+    if (!(alpha > 0)) break;
+#ifdef BB_TRACE
+    printf("   alpha %.4e lo %.3e hi %.3e d0 %.3e sMs %.3e |s| %.3e\n", double(alpha), double(lo), double(hi), double(d0), double(sMs), double(sqrt(s[0]*s[0]+s[9]*s[9]+s[12]*s[12])));
+#endif
     T sn = 0, an2 = 0;
 #pragma unroll
     for (int i = 0; i < NV; i++) { a[i] += alpha * s[i]; sn += s[i] * s[i]; an2 += a[i] * a[i]; }
-    if (alpha * alpha * sn <= T(1e-30) + sq_eps<T>() * (1 + an2)) { it++; break; }
+    if (alpha * alpha * sn <= T(1e-30) + m.step_rel2 * (1 + an2)) { it++; break; }
   }
   return it;
 }

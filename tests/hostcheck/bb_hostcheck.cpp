@@ -7,12 +7,15 @@
 
 using namespace bb;
 
+#include <stdlib.h>
 template <typename T>
 static ModelT<T> model_for(int fp64) {
-  static bool init = false;
-  static ModelT<double> md;
-  if (!init) { md = compile_model(default_solver(fp64 != 0)); init = true; }
-  ModelT<double> d = compile_model(default_solver(fp64 != 0));
+  SolverCfg sc = default_solver(fp64 != 0);
+  if (getenv("BB_TOL")) sc.tol = atof(getenv("BB_TOL"));
+  if (getenv("BB_STEPREL")) sc.step_rel = atof(getenv("BB_STEPREL"));
+  if (getenv("BB_LSTOL")) sc.ls_tol = atof(getenv("BB_LSTOL"));
+  if (getenv("BB_MAXIT")) sc.maxiter = atoi(getenv("BB_MAXIT"));
+  ModelT<double> d = compile_model(sc);
   return cast_model<T>(d);
 }
 
