@@ -127,6 +127,7 @@ def main() -> None:
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
     elapsed = float(t.item())
     stats = env.stats()
+    launch = env.launch_config()
 
     if rank == 0:
         total_steps = n * world * args.steps
@@ -158,7 +159,7 @@ def main() -> None:
             "config": {"workload": f"{n} envs/GPU, {args.terrain} terrain, random actions (BASELINE configs[1])",
                        "envs_per_gpu": n, "total_envs": n * world, "precision": args.precision,
                        "parallelism": f"env-sharded x{world} (no collective on the step path)",
-                       "envs_per_wave": os.environ.get("BB_EPW", "auto")},
+                       "launch": launch},
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
                          "note": "latency/VALU-bound per-lane physics; HBM bytes = algorithmic state I/O "

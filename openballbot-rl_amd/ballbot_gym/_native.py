@@ -46,7 +46,7 @@ class BBParams(C.Structure):
 EXPORTS = [
     "bb_abi_version", "bb_last_error", "bb_default_params", "bb_create", "bb_destroy", "bb_set_hfield",
     "bb_assign_terrain", "bb_reset", "bb_step", "bb_get_state", "bb_set_state", "bb_forward", "bb_get_stats",
-    "bb_get_offsets",
+    "bb_get_offsets", "bb_get_config",
 ]
 
 _lib = None
@@ -97,6 +97,7 @@ def lib():
     L.bb_forward.argtypes = [vp, dp, dp, C.POINTER(C.c_int32)]
     L.bb_get_stats.argtypes = [vp, C.POINTER(C.c_int64)]
     L.bb_get_offsets.argtypes = [vp, fp]
+    L.bb_get_config.argtypes = [vp, C.POINTER(C.c_int32)]
     for name in [n for n in EXPORTS if n not in ("bb_default_params", "bb_abi_version")]:
         getattr(L, name).restype = C.c_int
     if L.bb_abi_version() != 1:

@@ -220,6 +220,11 @@ class BallbotVecEnv:
         return {"resets": out[0], "diverged": out[1], "overflow": out[2],
                 "solver_iters": out[4] + (out[5] << 32)}
 
+    def launch_config(self) -> Dict[str, int]:
+        out = (C.c_int32 * 4)()
+        N.check(N.lib().bb_get_config(self._h, out), "bb_get_config")
+        return {"num_envs": out[0], "envs_per_wave": out[1], "fp64": out[2], "lds_bytes_per_workgroup": out[3]}
+
     def offsets(self) -> np.ndarray:
         o = np.zeros(self.n_terrains, np.float32)
         N.check(N.lib().bb_get_offsets(self._h, o.ctypes.data_as(C.POINTER(C.c_float))), "bb_get_offsets")

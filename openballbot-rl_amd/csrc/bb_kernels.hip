@@ -38,8 +38,16 @@ int fail(const char* fmt, ...) {
     if (e_ != hipSuccess) return fail("%s: %s", #x, hipGetErrorString(e_));         \
   } while (0)
 
+// per-lane EnvWork stride in LDS: 8 mod 16 bytes so that 8-byte accesses of
+// consecutive lanes fall on distinct bank pairs
 template <typename T>
-size_t lds_bytes(int epw) { return size_t(MAXG) * NGF * epw * sizeof(T); }
+__host__ __device__ constexpr size_t work_stride() { return (sizeof(EnvWork<T>) + 15) / 16 * 16 + 8; }
+template <typename T>
+size_t lds_bytes(int epw) { return work_stride<T>() * epw; }
+template <typename T>
+__device__ __forceinline__ EnvWork<T>& lane_work(unsigned char* smem, int lane) {
+  return *reinterpret_cast<EnvWork<T>*>(smem + size_t(lane) * work_stride<T>());
+}
 
 BB_HD uint32_t hash3(uint64_t seed, uint32_t a, uint32_t b) {  // splitmix-style counter hash
   uint64_t z = seed + 0x9E3779B97F4A7C15ull * (uint64_t(a) * 0x100000001ull + b + 1);
@@ -97,18 +105,24 @@ __device__ __forceinline__ void reset_lane(const ModelT<T>& m, const Dev& d, int
 }
 
 template <typename T>
-__global__ __launch_bounds__(64) void step_kernel(ModelT<T> m, EnvCfg cfg, Dev d, const float* __restrict__ act,
+__global__ __launch_bounds__(64) void step_kernel(ModelT<T> mg, EnvCfg cfg, Dev d, const float* __restrict__ act,
                                                   float* __restrict__ obs, float* __restrict__ rew,
                                                   uint8_t* __restrict__ done, float* __restrict__ tobs,
                                                   float* __restrict__ pos2d, int auto_reset, int epw) {
   // epw envs per 64-lane wave (lanes >= epw idle): spreads small batches over
   // all 1024 SIMDs instead of a few fully-populated waves.
   extern __shared__ __align__(16) unsigned char smem[];
+  // model constants staged in LDS once per workgroup: uniform-address LDS
+  // reads broadcast, and ~150 uniform doubles no longer overflow the SGPRs
+  __shared__ ModelT<T> ms;
+  if (threadIdx.x == 0) ms = mg;
+  __syncthreads();
+  const ModelT<T>& m = ms;
   const int lane = threadIdx.x;
   if (lane >= epw) return;
   const int e = blockIdx.x * epw + lane;
   if (e >= d.n) return;
-  GStore<T> st{reinterpret_cast<T*>(smem) + lane, epw};
+  EnvWork<T>& W = lane_work<T>(smem, lane);
   T q[NQ], v[NV], w[NV];
   int step;
   load_state(d, e, q, v, w, step);
@@ -117,7 +131,7 @@ __global__ __launch_bounds__(64) void step_kernel(ModelT<T> m, EnvCfg cfg, Dev d
   const float* hf = d.bank + size_t(tid) * (HF_N * HF_N);
   float o[15], r, p2[2];
   int iters = 0;
-  int fl = env_step(m, cfg, q, v, w, step, a, hf, T(d.size_z[tid]), st, o, r, p2, &iters);
+  int fl = env_step(m, cfg, q, v, w, step, a, hf, T(d.size_z[tid]), W, o, r, p2, &iters);
   if (tobs) {
 #pragma unroll
     for (int i = 0; i < 15; i++) tobs[15 * e + i] = o[i];
@@ -161,19 +175,24 @@ __global__ __launch_bounds__(64) void reset_kernel(ModelT<T> m, Dev d, const uin
 }
 
 template <typename T>
-__global__ __launch_bounds__(64) void forward_kernel(ModelT<T> m, Dev d, const double* ctrl, double* qacc, int* ncon) {
+__global__ __launch_bounds__(64) void forward_kernel(ModelT<T> mg, Dev d, const double* ctrl, double* qacc, int* ncon, int epw) {
   extern __shared__ __align__(16) unsigned char smem[];
+  __shared__ ModelT<T> ms;
+  if (threadIdx.x == 0) ms = mg;
+  __syncthreads();
+  const ModelT<T>& m = ms;
   const int lane = threadIdx.x;
-  const int e = blockIdx.x * WAVE + lane;
+  if (lane >= epw) return;
+  const int e = blockIdx.x * epw + lane;
   if (e >= d.n) return;
-  GStore<T> st{reinterpret_cast<T*>(smem) + lane, WAVE};  // diagnostic: full waves
+  EnvWork<T>& W = lane_work<T>(smem, lane);
   T q[NQ], v[NV], w[NV], c[3];
   int step;
   load_state(d, e, q, v, w, step);
   for (int i = 0; i < 3; i++) c[i] = T(ctrl[3 * e + i]);
   const int tid = d.terrain[e];
   StageOut<T> so;
-  forward(m, q, v, c, w, d.bank + size_t(tid) * (HF_N * HF_N), T(d.size_z[tid]), st, &so);
+  forward(m, q, v, c, w, d.bank + size_t(tid) * (HF_N * HF_N), T(d.size_z[tid]), W, &so);
   for (int i = 0; i < NV; i++) qacc[NV * e + i] = double(w[i]);
   if (ncon) ncon[e] = so.ng;
 }
@@ -283,10 +302,15 @@ int bb_create(int n_envs, int device, const bb_params* p, bb_handle** out) {
     hipDeviceProp_t prop;
     HIPCHK(hipGetDeviceProperties(&prop, device));
     const int simds = prop.multiProcessorCount * 4;
+    // LDS caps envs per wave: one EnvWork per lane + the staged model
+    const size_t lds_max = 160 * 1024 - 2048;
+    const int cap = (int)(lds_max / (h->fp64 ? work_stride<double>() : work_stride<float>()));
     int epw = 1;
     while (epw < WAVE && (long)epw * simds < (long)n_envs) epw *= 2;
     const char* ov = getenv("BB_EPW");
-    if (ov && atoi(ov) > 0) epw = atoi(ov) > WAVE ? WAVE : atoi(ov);
+    if (ov && atoi(ov) > 0) epw = atoi(ov);
+    if (epw > WAVE) epw = WAVE;
+    if (epw > cap) epw = cap;
     h->epw = epw;
   }
   h->md = compile_model(sc);
@@ -320,14 +344,13 @@ int bb_create(int n_envs, int device, const bb_params* p, bb_handle** out) {
   HIPCHK(hipMemcpy(h->offset, h->h_offset.data(), sizeof(float) * nt, hipMemcpyHostToDevice));
   d.bank = h->bank; d.size_z = h->size_z; d.offset = h->offset;
   // LDS for the ground-contact store (f64: 120 KiB, above the 64 KiB default)
-  HIPCHK(hipFuncSetAttribute((const void*)step_kernel<float>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                             (int)lds_bytes<float>(WAVE)));
-  HIPCHK(hipFuncSetAttribute((const void*)step_kernel<double>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                             (int)lds_bytes<double>(WAVE)));
-  HIPCHK(hipFuncSetAttribute((const void*)forward_kernel<float>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                             (int)lds_bytes<float>(WAVE)));
-  HIPCHK(hipFuncSetAttribute((const void*)forward_kernel<double>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                             (int)lds_bytes<double>(WAVE)));
+  {
+    const int lb = (int)(h->fp64 ? lds_bytes<double>(h->epw) : lds_bytes<float>(h->epw));
+    const void* sk = h->fp64 ? (const void*)step_kernel<double> : (const void*)step_kernel<float>;
+    const void* fk = h->fp64 ? (const void*)forward_kernel<double> : (const void*)forward_kernel<float>;
+    HIPCHK(hipFuncSetAttribute(sk, hipFuncAttributeMaxDynamicSharedMemorySize, lb));
+    HIPCHK(hipFuncSetAttribute(fk, hipFuncAttributeMaxDynamicSharedMemorySize, lb));
+  }
   *out = h;
   int rc = bb_reset(h, nullptr, nullptr, nullptr);
   if (rc) return rc;
@@ -437,11 +460,14 @@ int bb_forward(bb_handle* h, const double* ctrl, double* qacc, int32_t* ncon) {
   HIPCHK(hipMalloc(&dq, sizeof(double) * NV * n));
   HIPCHK(hipMalloc(&dn, sizeof(int) * n));
   HIPCHK(hipMemcpy(dc, ctrl, sizeof(double) * 3 * n, hipMemcpyHostToDevice));
-  int blocks = (h->n + WAVE - 1) / WAVE;
+  const int epw = h->epw;
+  int blocks = (h->n + epw - 1) / epw;
   if (h->fp64)
-    hipLaunchKernelGGL(forward_kernel<double>, dim3(blocks), dim3(WAVE), lds_bytes<double>(WAVE), 0, h->md, h->d, dc, dq, dn);
+    hipLaunchKernelGGL(forward_kernel<double>, dim3(blocks), dim3(WAVE), lds_bytes<double>(epw), 0, h->md, h->d, dc, dq,
+                       dn, epw);
   else
-    hipLaunchKernelGGL(forward_kernel<float>, dim3(blocks), dim3(WAVE), lds_bytes<float>(WAVE), 0, h->mf, h->d, dc, dq, dn);
+    hipLaunchKernelGGL(forward_kernel<float>, dim3(blocks), dim3(WAVE), lds_bytes<float>(epw), 0, h->mf, h->d, dc, dq,
+                       dn, epw);
   HIPCHK(hipGetLastError());
   HIPCHK(hipDeviceSynchronize());
   HIPCHK(hipMemcpy(qacc, dq, sizeof(double) * NV * n, hipMemcpyDeviceToHost));
@@ -457,6 +483,13 @@ int bb_get_stats(bb_handle* h, int64_t* out6) {
   HIPCHK(hipMemcpy(s, h->d.stats, sizeof s, hipMemcpyDeviceToHost));
   out6[0] = (int64_t)s[0]; out6[1] = (int64_t)s[1]; out6[2] = (int64_t)s[2];
   out6[3] = (int64_t)s[3]; out6[4] = (int64_t)(s[4] & 0xffffffffull); out6[5] = (int64_t)(s[4] >> 32);
+  return 0;
+}
+
+int bb_get_config(bb_handle* h, int32_t* out4) {
+  if (!h || !out4) return fail("bb_get_config: NULL argument");
+  out4[0] = h->n; out4[1] = h->epw; out4[2] = h->fp64;
+  out4[3] = (int32_t)(h->fp64 ? lds_bytes<double>(h->epw) : lds_bytes<float>(h->epw));
   return 0;
 }
 

@@ -56,7 +56,7 @@ struct SolverCfg {
 inline SolverCfg default_solver(bool fp64) {
   // MuJoCo: tolerance 1e-8, iterations 100, ls_iterations 50.  The minimiser is
   // unique, so the fp32 build stops at its roundoff floor instead.
-  if (fp64) return SolverCfg{1e-10, 1e-8, 1e-14, 40, 40};
+  if (fp64) return SolverCfg{1e-8, 1e-2, 1e-14, 40, 40};  // MuJoCo tolerance / ls_tolerance
   return SolverCfg{2e-6, 1e-3, 3e-7, 16, 16};
 }
 
@@ -153,8 +153,9 @@ inline ModelT<double> compile_model(const SolverCfg& sc) {
   Kin<double> k;
   kinematics(m, m.qpos0, k);
   Mass<double> M;
-  build_mass(m, k, M);
-  double H[NH];
+  double Iw_[3][6];
+  build_mass(m, k, M, Iw_);
+  static double H[NH];
   mass_dense(M, H);
   double tr = 0;
   for (int i = 0; i < NV; i++) tr += H[hidx(i, i)];

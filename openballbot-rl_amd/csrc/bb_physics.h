@@ -33,7 +33,11 @@ constexpr int NQ = 17, NV = 15, NU = 3;
 constexpr int HF_N = 293;        // ballbot.xml:23 nrow = ncol
 constexpr int MAXG = 24;         // ball-hfield contact cap (== oracle BBO_MAXGROUND)
 constexpr int NH = NV * (NV + 1) / 2;
-constexpr int NGF = 10;          // fields per stored ground contact: n[3] r[3] aref[3] D
+constexpr int NGF = 28;          // fields per stored ground contact (see GF_* below)
+// ground-contact store fields: three Jacobian rows over the ball dofs
+// (world-linear[3], local-angular[3]), aref[3], D, and the line-search cache
+// jar(alpha=0)[3], J*s[3]
+constexpr int GF_J = 0, GF_AREF = 18, GF_D = 21, GF_JAR = 22, GF_JS = 25;
 
 // ------------------------------------------------------------------ model
 // Compiled constants (bb_model.cpp computes them in double from the MJCF
@@ -217,25 +221,24 @@ struct Mass {
   T mB;
   T MBtr[9];       // ball trans x ball rot
   T MBrr[3];       // ball rot diagonal (constant)
-  T Iw[3][6];      // wheel inertia about COM (base-local), reused by the RNE
 };
 
 template <typename T>
-BB_HD void build_mass(const ModelT<T>& m, const Kin<T>& k, Mass<T>& M) {
+BB_HD void build_mass(const ModelT<T>& m, const Kin<T>& k, Mass<T>& M, T (&Iw)[3][6]) {
   T mr[3] = {m.h0[0], m.h0[1], m.h0[2]};
   T IO[6] = {m.I0O[0], m.I0O[1], m.I0O[2], m.I0O[3], m.I0O[4], m.I0O[5]};
 #pragma unroll
   for (int w = 0; w < 3; w++) {
     const T* c = k.wc[w];
-    sym_rot(M.Iw[w], k.Rw[w], m.Iw);
+    sym_rot(Iw[w], k.Rw[w], m.Iw);
     mr[0] += m.mw * c[0]; mr[1] += m.mw * c[1]; mr[2] += m.mw * c[2];
     T cc = dot3(c, c);
-    IO[0] += M.Iw[w][0] + m.mw * (cc - c[0] * c[0]);
-    IO[1] += M.Iw[w][1] + m.mw * (cc - c[1] * c[1]);
-    IO[2] += M.Iw[w][2] + m.mw * (cc - c[2] * c[2]);
-    IO[3] += M.Iw[w][3] - m.mw * c[0] * c[1];
-    IO[4] += M.Iw[w][4] - m.mw * c[0] * c[2];
-    IO[5] += M.Iw[w][5] - m.mw * c[1] * c[2];
+    IO[0] += Iw[w][0] + m.mw * (cc - c[0] * c[0]);
+    IO[1] += Iw[w][1] + m.mw * (cc - c[1] * c[1]);
+    IO[2] += Iw[w][2] + m.mw * (cc - c[2] * c[2]);
+    IO[3] += Iw[w][3] - m.mw * c[0] * c[1];
+    IO[4] += Iw[w][4] - m.mw * c[0] * c[2];
+    IO[5] += Iw[w][5] - m.mw * c[1] * c[2];
     // hinge motion subspace S = (u; anchor x u) about the base origin
     const T* u = m.u[w];
     T ca[3] = {c[0] - m.anchor[0], c[1] - m.anchor[1], c[2] - m.anchor[2]};
@@ -243,7 +246,7 @@ BB_HD void build_mass(const ModelT<T>& m, const Kin<T>& k, Mass<T>& M) {
     cross3(vc, u, ca);                       // wheel COM velocity per unit rate
     T p[3] = {m.mw * vc[0], m.mw * vc[1], m.mw * vc[2]};
     T L[3], t[3];
-    symv(L, M.Iw[w], u);
+    symv(L, Iw[w], u);
     T uIu = dot3(u, L);
     cross3(t, c, p);
     L[0] += t[0]; L[1] += t[1]; L[2] += t[2];  // angular momentum about base origin
@@ -347,7 +350,7 @@ BB_HD void body_force(T m, const T* c, const T* Ic, const T* Aw, const T* Av, co
 
 // qfrc_bias = C(q,v) v + gravity  (mj_rne with flg_acc = 0)
 template <typename T>
-BB_HD void bias_forces(const ModelT<T>& m, const Kin<T>& k, const Mass<T>& M, const T* v, T* bias) {
+BB_HD void bias_forces(const ModelT<T>& m, const Kin<T>& k, const T (&Iw)[3][6], const T* v, T* bias) {
   // ---- tree 1, base-local coordinates about the base origin
   T w0[3] = {v[3], v[4], v[5]};
   T vl[3];
@@ -384,7 +387,7 @@ BB_HD void bias_forces(const ModelT<T>& m, const Kin<T>& k, const Mass<T>& M, co
     T Aw[3] = {qd * x1[0], qd * x1[1], qd * x1[2]};
     T Av[3] = {a0[0] + qd * (x2[0] + x3[0]), a0[1] + qd * (x2[1] + x3[1]), a0[2] + qd * (x2[2] + x3[2])};
     T fa[3], fl[3];
-    body_force(m.mw, k.wc[w], M.Iw[w], Aw, Av, Vw, Vv, fa, fl);
+    body_force(m.mw, k.wc[w], Iw[w], Aw, Av, Vw, Vv, fa, fl);
     bias[6 + w] = dot3(u, fa) + dot3(au, fl);
     Fa[0] += fa[0]; Fa[1] += fa[1]; Fa[2] += fa[2];
     Fl[0] += fl[0]; Fl[1] += fl[1]; Fl[2] += fl[2];
@@ -464,18 +467,19 @@ BB_HD void cone_eval(const T* jar, T mu, T f1, T f2, const T* D, T* force, T* C)
   }
 }
 
-// One ball-wheel contact (explicit pair, condim 3), Jacobian rows compressed
-// to their 13 structural non-zeros: base trans = d, ball trans = -d.
+// One ball-wheel contact (explicit pair, condim 3).  Jacobian rows over the
+// 13 structural columns: base trans (3), base rot (3), hinge w, ball trans (3),
+// ball rot (3) -- see wheel_col().
 template <typename T>
 struct WheelCon {
-  T act;          // 1 active, 0 inactive (D zeroed)
-  T d[3][3];      // frame rows (normal, axle tangent, drive tangent)
-  T br[3][3];     // base rot columns
-  T hk[3];        // hinge column
-  T Br[3][3];     // ball rot columns (sign included)
+  T J[3][13];     // rows: normal, axle tangent (patch), drive tangent
   T aref[3], D[3];
   T dist;
+  T ja[3], js[3];   // line-search cache: J a - aref, J s
 };
+
+// global dof index of wheel-contact column i for wheel w
+BB_HD constexpr int wheel_col(int i, int w) { return i < 6 ? i : (i == 6 ? 6 + w : i + 2); }
 
 // ground-contact store: element (slot s, field f) at base[(s*NGF + f)*stride]
 template <typename T>
@@ -483,6 +487,21 @@ struct GStore {
   T* base;
   int stride;
   BB_HD T& at(int s, int f) const { return base[(s * NGF + f) * stride]; }
+};
+
+// Per-env working set of one forward/RK step.  On the GPU one EnvWork per
+// lane lives in LDS (bb_kernels.hip), so only the solver vectors and the
+// packed Hessian occupy registers.
+template <typename T>
+struct EnvWork {
+  T g[MAXG * NGF];          // ball-terrain contacts
+  WheelCon<T> wc[3];        // ball-wheel contacts
+  Mass<T> M;                // mass-matrix blocks
+  Kin<T> k;                 // kinematics of the current stage
+  T Iw[3][6];               // wheel inertias (base-local) of the current stage
+  T H[NH];                  // Newton Hessian / its Cholesky factor (packed lower)
+  T q0[NQ], v0[NV], vs[NV], as[NV], vp[NV];  // RK4 stage context
+  T qi[NQ], vi[NV];                          // current stage state
 };
 
 // patched mjraw_SphereCapsule (tools/mujoco_fix.patch:11-16) + mju_makeFrame
@@ -499,7 +518,7 @@ BB_HD void wheel_contact(const ModelT<T>& m, const Kin<T>& k, const T* v, int w,
   T cd = sqrt(dot3(dif, dif));
   T dist = cd - m.ball_r - m.wheel_r;
   C.dist = dist;
-  C.act = dist <= 0 ? T(1) : T(0);
+  const T act = dist <= 0 ? T(1) : T(0);
   T n[3];
   if (cd > 0) { T ic = T(1) / cd; n[0] = dif[0] * ic; n[1] = dif[1] * ic; n[2] = dif[2] * ic; }
   else { n[0] = 1; n[1] = 0; n[2] = 0; }
@@ -522,15 +541,17 @@ BB_HD void wheel_contact(const ModelT<T>& m, const Kin<T>& k, const T* v, int w,
 #pragma unroll
   for (int r = 0; r < 3; r++) {
     const T* d = r == 0 ? n : (r == 1 ? t1 : t2);
-    C.d[r][0] = d[0]; C.d[r][1] = d[1]; C.d[r][2] = d[2];
-    T x1[3];
+    T x1[3], br[3];
+    C.J[r][0] = d[0]; C.J[r][1] = d[1]; C.J[r][2] = d[2];
     cross3(x1, lb, d);
-    mtv3(C.br[r], k.Rb, x1);
+    mtv3(br, k.Rb, x1);
+    C.J[r][3] = br[0]; C.J[r][4] = br[1]; C.J[r][5] = br[2];
     cross3(x1, la, d);
-    C.hk[r] = dot3(uw, x1);
+    C.J[r][6] = dot3(uw, x1);
+    C.J[r][7] = -d[0]; C.J[r][8] = -d[1]; C.J[r][9] = -d[2];
     cross3(x1, lB, d);
     mtv3(t, k.RB, x1);
-    C.Br[r][0] = -t[0]; C.Br[r][1] = -t[1]; C.Br[r][2] = -t[2];
+    C.J[r][10] = -t[0]; C.J[r][11] = -t[1]; C.J[r][12] = -t[2];
   }
   // impedance, R, D (elliptic, impratio = 1) and aref
   T imp = clampT(impedance(m, dist), T(0.0001), T(0.9999));
@@ -538,19 +559,23 @@ BB_HD void wheel_contact(const ModelT<T>& m, const Kin<T>& k, const T* v, int w,
   T R0 = maxT(T(1e-15), (1 - imp) * tran / imp);
   T rr = m.fr_wheel[0] / m.fr_wheel[1];
   T R2 = R0 * rr * rr;
-  C.D[0] = C.act / R0; C.D[1] = C.act / R0; C.D[2] = C.act / R2;
+  C.D[0] = act / R0; C.D[1] = act / R0; C.D[2] = act / R2;
 #pragma unroll
   for (int r = 0; r < 3; r++) {
-    T vel = dot3(C.d[r], v) + dot3(C.br[r], v + 3) + C.hk[r] * v[6 + w] - dot3(C.d[r], v + 9) +
-            dot3(C.Br[r], v + 12);
-    C.aref[r] = C.act * (-m.Bd * vel - (r == 0 ? m.K * imp * dist : T(0)));
+    T vel = 0;
+#pragma unroll
+    for (int i = 0; i < 13; i++) vel += C.J[r][i] * v[wheel_col(i, w)];
+    C.aref[r] = (C.D[0] > 0 ? T(1) : T(0)) * (-m.Bd * vel - (r == 0 ? m.K * imp * dist : T(0)));
   }
 }
 
 // J x for one wheel contact row
 template <typename T>
 BB_HD T wheel_row_mul(const WheelCon<T>& C, int w, int r, const T* x) {
-  return dot3(C.d[r], x) + dot3(C.br[r], x + 3) + C.hk[r] * x[6 + w] - dot3(C.d[r], x + 9) + dot3(C.Br[r], x + 12);
+  T acc = 0;
+#pragma unroll
+  for (int i = 0; i < 13; i++) acc += C.J[r][i] * x[wheel_col(i, w)];
+  return acc;
 }
 
 // closest point on triangle (Ericson, RTCD 5.1.5) -- used for the top face
@@ -740,12 +765,19 @@ BB_HD int collide_ground(const ModelT<T>& m, const Kin<T>& k, const T* v, const 
         T pv[3], tt[3];
         cross3(tt, wB, lv);
         pv[0] = v[9] + tt[0]; pv[1] = v[10] + tt[1]; pv[2] = v[11] + tt[2];
-        st.at(ng, 0) = nn[0]; st.at(ng, 1) = nn[1]; st.at(ng, 2) = nn[2];
-        st.at(ng, 3) = lv[0]; st.at(ng, 4) = lv[1]; st.at(ng, 5) = lv[2];
-        st.at(ng, 6) = -m.Bd * dot3(nn, pv) - m.K * imp * dist;
-        st.at(ng, 7) = -m.Bd * dot3(t1, pv);
-        st.at(ng, 8) = -m.Bd * dot3(t2, pv);
-        st.at(ng, 9) = T(1) / R0;
+        const T* F[3] = {nn, t1, t2};
+#pragma unroll
+        for (int r = 0; r < 3; r++) {
+          T x1[3], x2[3];
+          cross3(x1, lv, F[r]);
+          mtv3(x2, k.RB, x1);
+#pragma unroll
+          for (int i = 0; i < 3; i++) { st.at(ng, GF_J + 6 * r + i) = F[r][i]; st.at(ng, GF_J + 6 * r + 3 + i) = x2[i]; }
+        }
+        st.at(ng, GF_AREF + 0) = -m.Bd * dot3(nn, pv) - m.K * imp * dist;
+        st.at(ng, GF_AREF + 1) = -m.Bd * dot3(t1, pv);
+        st.at(ng, GF_AREF + 2) = -m.Bd * dot3(t2, pv);
+        st.at(ng, GF_D) = T(1) / R0;
         ng++;
       }
     }
@@ -767,26 +799,25 @@ template <> BB_HD double pivot_eps<double>() { return 1e-14; }
 // enforced by the line search.
 template <typename T>
 BB_HD void chol_packed(T* H) {
-#pragma unroll
   for (int j = 0; j < NV; j++) {
-    T s = H[hidx(j, j)];
-    const T floor_j = pivot_eps<T>() * maxT(H[hidx(j, j)], T(1e-30));
-#pragma unroll
-    for (int k = 0; k < j; k++) s -= H[hidx(j, k)] * H[hidx(j, k)];
+    const int rj = j * (j + 1) / 2;
+    T s = H[rj + j];
+    const T floor_j = pivot_eps<T>() * maxT(s, T(1e-30));
+    for (int k = 0; k < j; k++) s -= H[rj + k] * H[rj + k];
     s = s > floor_j ? s : floor_j;
-    T d = sqrt(s), id = T(1) / d;
-    H[hidx(j, j)] = d;
-#pragma unroll
+    const T d = sqrt(s), id = T(1) / d;
+    H[rj + j] = d;
     for (int i = j + 1; i < NV; i++) {
-      T t = H[hidx(i, j)];
-#pragma unroll
-      for (int k = 0; k < j; k++) t -= H[hidx(i, k)] * H[hidx(j, k)];
-      H[hidx(i, j)] = t * id;
+      const int ri = i * (i + 1) / 2;
+      T t = H[ri + j];
+      for (int k = 0; k < j; k++) t -= H[ri + k] * H[rj + k];
+      H[ri + j] = t * id;
     }
   }
 }
 template <typename T>
 BB_HD void chol_solve_packed(const T* L, T* x) {
+  // x lives in registers: unrolled over i, rolled over nothing dynamic
 #pragma unroll
   for (int i = 0; i < NV; i++) {
     T s = x[i];
@@ -803,24 +834,23 @@ BB_HD void chol_solve_packed(const T* L, T* x) {
   }
 }
 
-// ground contact: frame rows and point acceleration at the lever
+// J_r . x over the ball dofs for a stored ground contact
 template <typename T>
-BB_HD void ground_load(const GStore<T>& st, int s, T* n, T* lv, T* aref, T& D) {
-  n[0] = st.at(s, 0); n[1] = st.at(s, 1); n[2] = st.at(s, 2);
-  lv[0] = st.at(s, 3); lv[1] = st.at(s, 4); lv[2] = st.at(s, 5);
-  aref[0] = st.at(s, 6); aref[1] = st.at(s, 7); aref[2] = st.at(s, 8);
-  D = st.at(s, 9);
+BB_HD T ground_row_mul(const GStore<T>& st, int c, int r, const T* x) {
+  const int b = GF_J + 6 * r;
+  return st.at(c, b) * x[9] + st.at(c, b + 1) * x[10] + st.at(c, b + 2) * x[11] + st.at(c, b + 3) * x[12] +
+         st.at(c, b + 4) * x[13] + st.at(c, b + 5) * x[14];
 }
 
 // Newton on  0.5 a'Ma - a'qfs + sum_c cost_c(J_c a - aref_c)   (mj_solNewton).
 // The minimiser is unique (M > 0); returns iterations used.
 template <typename T>
-BB_HD int solve(const ModelT<T>& m, const Kin<T>& k, const Mass<T>& M, const T* qfs, const WheelCon<T>* WC,
-                int ng, const GStore<T>& st, T* a) {
+BB_HD int solve(const ModelT<T>& m, const Mass<T>& M, const T* qfs, WheelCon<T>* WC, int ng, const GStore<T>& st,
+                T* H, T* a) {
   const T mu_w = m.fr_wheel[0], f1w = m.fr_wheel[0], f2w = m.fr_wheel[1];
   int it = 0;
   for (; it < m.maxiter; it++) {
-    T g[NV], H[NH], Ma[NV];
+    T g[NV], Ma[NV];
     mass_mul(M, a, Ma);
 #pragma unroll
     for (int i = 0; i < NV; i++) g[i] = Ma[i] - qfs[i];
@@ -833,97 +863,58 @@ BB_HD int solve(const ModelT<T>& m, const Kin<T>& k, const Mass<T>& M, const T* 
 #pragma unroll
       for (int r = 0; r < 3; r++) jar[r] = wheel_row_mul(C, w, r, a) - C.aref[r];
       cone_eval(jar, mu_w, f1w, f2w, C.D, f, Cc);
-      // J rows over the 13 structural columns
-      T J[3][13];
+      // gradient over the 13 structural columns
 #pragma unroll
-      for (int r = 0; r < 3; r++) {
-        J[r][0] = C.d[r][0]; J[r][1] = C.d[r][1]; J[r][2] = C.d[r][2];
-        J[r][3] = C.br[r][0]; J[r][4] = C.br[r][1]; J[r][5] = C.br[r][2];
-        J[r][6] = C.hk[r];
-        J[r][7] = -C.d[r][0]; J[r][8] = -C.d[r][1]; J[r][9] = -C.d[r][2];
-        J[r][10] = C.Br[r][0]; J[r][11] = C.Br[r][1]; J[r][12] = C.Br[r][2];
+      for (int j = 0; j < 13; j++) g[wheel_col(j, w)] -= C.J[0][j] * f[0] + C.J[1][j] * f[1] + C.J[2][j] * f[2];
+      // H += J' C J, rolled over (i, j) with J and H in the LDS workspace
+      for (int i = 0; i < 13; i++) {
+        const T j0 = C.J[0][i], j1 = C.J[1][i], j2 = C.J[2][i];
+        const T u0 = Cc[0] * j0 + Cc[3] * j1 + Cc[4] * j2;
+        const T u1 = Cc[3] * j0 + Cc[1] * j1 + Cc[5] * j2;
+        const T u2 = Cc[4] * j0 + Cc[5] * j1 + Cc[2] * j2;
+        const int ci = wheel_col(i, w);
+        T* Hrow = H + ci * (ci + 1) / 2;
+        for (int j = 0; j <= i; j++) Hrow[wheel_col(j, w)] += C.J[0][j] * u0 + C.J[1][j] * u1 + C.J[2][j] * u2;
       }
-      const int col[13] = {0, 1, 2, 3, 4, 5, 6 + w, 9, 10, 11, 12, 13, 14};
-#pragma unroll
-      for (int j = 0; j < 13; j++) g[col[j]] -= J[0][j] * f[0] + J[1][j] * f[1] + J[2][j] * f[2];
-      T CJ[3][13];
-#pragma unroll
-      for (int j = 0; j < 13; j++) {
-        CJ[0][j] = Cc[0] * J[0][j] + Cc[3] * J[1][j] + Cc[4] * J[2][j];
-        CJ[1][j] = Cc[3] * J[0][j] + Cc[1] * J[1][j] + Cc[5] * J[2][j];
-        CJ[2][j] = Cc[4] * J[0][j] + Cc[5] * J[1][j] + Cc[2] * J[2][j];
-      }
-#pragma unroll
-      for (int i = 0; i < 13; i++)
-#pragma unroll
-        for (int j = 0; j <= i; j++)
-          H[hidx(col[i], col[j])] += J[0][i] * CJ[0][j] + J[1][i] * CJ[1][j] + J[2][i] * CJ[2][j];
     }
-    // ---- ground contacts: ball-only columns, accumulated in world form
+    // ---- ground contacts: ball-only columns (6), rows cached in the store
     {
-      T wa[3];
-      mv3(wa, k.RB, a + 12);
-      T fsum[3] = {0, 0, 0}, tsum[3] = {0, 0, 0};
-      T Att[6] = {0, 0, 0, 0, 0, 0};
-      T Atr[9] = {0, 0, 0, 0, 0, 0, 0, 0, 0};
-      T Arr[6] = {0, 0, 0, 0, 0, 0};
-      for (int s = 0; s < ng; s++) {
-        T n[3], lv[3], aref[3], D;
-        ground_load(st, s, n, lv, aref, D);
-        T t1[3], t2[3];
-        frame_from_normal(n, t1, t2);
-        T pa[3], tt[3];
-        cross3(tt, wa, lv);
-        pa[0] = a[9] + tt[0]; pa[1] = a[10] + tt[1]; pa[2] = a[11] + tt[2];
-        T jar[3] = {dot3(n, pa) - aref[0], dot3(t1, pa) - aref[1], dot3(t2, pa) - aref[2]};
+      T Hb[21];
+#pragma unroll
+      for (int i = 0; i < 21; i++) Hb[i] = 0;
+      for (int c = 0; c < ng; c++) {
+        T J[3][6];
+#pragma unroll
+        for (int r = 0; r < 3; r++)
+#pragma unroll
+          for (int i = 0; i < 6; i++) J[r][i] = st.at(c, GF_J + 6 * r + i);
+        T jar[3];
+#pragma unroll
+        for (int r = 0; r < 3; r++) {
+          jar[r] = J[r][0] * a[9] + J[r][1] * a[10] + J[r][2] * a[11] + J[r][3] * a[12] + J[r][4] * a[13] +
+                   J[r][5] * a[14] - st.at(c, GF_AREF + r);
+          st.at(c, GF_JAR + r) = jar[r];
+        }
+        const T D = st.at(c, GF_D);
         T Dv[3] = {D, D, D}, f[3], Cc[6];
         cone_eval(jar, T(1), T(1), T(1), Dv, f, Cc);
-        T fw[3];
+        T w[3][6];
 #pragma unroll
-        for (int i = 0; i < 3; i++) fw[i] = f[0] * n[i] + f[1] * t1[i] + f[2] * t2[i];
-        fsum[0] += fw[0]; fsum[1] += fw[1]; fsum[2] += fw[2];
-        cross3(tt, lv, fw);
-        tsum[0] += tt[0]; tsum[1] += tt[1]; tsum[2] += tt[2];
-        // G = F' C F (world), F rows = n, t1, t2
-        T F[9] = {n[0], n[1], n[2], t1[0], t1[1], t1[2], t2[0], t2[1], t2[2]};
-        T Cf[9] = {Cc[0], Cc[3], Cc[4], Cc[3], Cc[1], Cc[5], Cc[4], Cc[5], Cc[2]};
-        T CF[9], G[9];
-        mm3(CF, Cf, F);
+        for (int i = 0; i < 6; i++) {
+          g[9 + i] -= J[0][i] * f[0] + J[1][i] * f[1] + J[2][i] * f[2];
+          w[0][i] = Cc[0] * J[0][i] + Cc[3] * J[1][i] + Cc[4] * J[2][i];
+          w[1][i] = Cc[3] * J[0][i] + Cc[1] * J[1][i] + Cc[5] * J[2][i];
+          w[2][i] = Cc[4] * J[0][i] + Cc[5] * J[1][i] + Cc[2] * J[2][i];
+        }
 #pragma unroll
-        for (int i = 0; i < 3; i++)
+        for (int i = 0; i < 6; i++)
 #pragma unroll
-          for (int j = 0; j < 3; j++) G[3 * i + j] = F[i] * CF[j] + F[3 + i] * CF[3 + j] + F[6 + i] * CF[6 + j];
-        Att[0] += G[0]; Att[1] += G[4]; Att[2] += G[8]; Att[3] += G[1]; Att[4] += G[2]; Att[5] += G[5];
-        // X = G [l]x ; Atr -= X ; Arr += [l]x' G [l]x = -[l]x X
-        T Lx[9] = {0, -lv[2], lv[1], lv[2], 0, -lv[0], -lv[1], lv[0], 0};
-        T X[9], Y[9];
-        mm3(X, G, Lx);
-#pragma unroll
-        for (int i = 0; i < 9; i++) Atr[i] -= X[i];
-        mm3(Y, Lx, X);
-        Arr[0] -= Y[0]; Arr[1] -= Y[4]; Arr[2] -= Y[8]; Arr[3] -= Y[1]; Arr[4] -= Y[2]; Arr[5] -= Y[5];
+          for (int j = 0; j <= i; j++) Hb[i * (i + 1) / 2 + j] += J[0][i] * w[0][j] + J[1][i] * w[1][j] + J[2][i] * w[2][j];
       }
-      if (ng > 0) {
-        // gradient: ball trans -= fsum ; ball rot -= RB' tsum
-        T tl[3];
-        mtv3(tl, k.RB, tsum);
-        g[9] -= fsum[0]; g[10] -= fsum[1]; g[11] -= fsum[2];
-        g[12] -= tl[0]; g[13] -= tl[1]; g[14] -= tl[2];
-        // H: tt += Att ; tr += Atr RB ; rr += RB' Arr RB
-        H[hidx(9, 9)] += Att[0]; H[hidx(10, 10)] += Att[1]; H[hidx(11, 11)] += Att[2];
-        H[hidx(10, 9)] += Att[3]; H[hidx(11, 9)] += Att[4]; H[hidx(11, 10)] += Att[5];
-        T P[9];
-        mm3(P, Atr, k.RB);  // rows: trans i, cols: rot j
 #pragma unroll
-        for (int i = 0; i < 3; i++)
+      for (int i = 0; i < 6; i++)
 #pragma unroll
-          for (int j = 0; j < 3; j++) H[hidx(12 + j, 9 + i)] += P[3 * i + j];
-        T RT[9] = {k.RB[0], k.RB[3], k.RB[6], k.RB[1], k.RB[4], k.RB[7], k.RB[2], k.RB[5], k.RB[8]};
-        T Q[6];
-        sym_rot(Q, RT, Arr);
-        H[hidx(12, 12)] += Q[0]; H[hidx(13, 13)] += Q[1]; H[hidx(14, 14)] += Q[2];
-        H[hidx(13, 12)] += Q[3]; H[hidx(14, 12)] += Q[4]; H[hidx(14, 13)] += Q[5];
-      }
+        for (int j = 0; j <= i; j++) H[hidx(9 + i, 9 + j)] += Hb[i * (i + 1) / 2 + j];
     }
     T gn = 0;
 #pragma unroll
@@ -960,17 +951,16 @@ BB_HD int solve(const ModelT<T>& m, const Kin<T>& k, const Mass<T>& M, const T* 
 #pragma unroll
     for (int i = 0; i < NV; i++) { sMs += s[i] * Ms[i]; gs += s[i] * (Ma[i] - qfs[i]); d0 += s[i] * g[i]; }
     if (!(d0 < 0)) break;
-    T ja[3][3], js[3][3];
 #pragma unroll
     for (int w = 0; w < 3; w++)
 #pragma unroll
       for (int r = 0; r < 3; r++) {
-        ja[w][r] = wheel_row_mul(WC[w], w, r, a) - WC[w].aref[r];
-        js[w][r] = wheel_row_mul(WC[w], w, r, s);
+        WC[w].ja[r] = wheel_row_mul(WC[w], w, r, a) - WC[w].aref[r];
+        WC[w].js[r] = wheel_row_mul(WC[w], w, r, s);
       }
-    T wa[3], ws[3];
-    mv3(wa, k.RB, a + 12);
-    mv3(ws, k.RB, s + 12);
+    for (int c = 0; c < ng; c++)
+#pragma unroll
+      for (int r = 0; r < 3; r++) st.at(c, GF_JS + r) = ground_row_mul(st, c, r, s);
     // 1-D Newton on phi'(alpha) from the full Newton step alpha = 1,
     // safeguarded by false position on the bracket [lo, hi] (phi' is
     // continuous and nondecreasing: the cost is convex and C1).
@@ -981,28 +971,21 @@ BB_HD int solve(const ModelT<T>& m, const Kin<T>& k, const Mass<T>& M, const T* 
       T dmag = fabs(gs) + fabs(alpha * sMs);  // magnitude of the summed terms: roundoff floor of d1
 #pragma unroll
       for (int w = 0; w < 3; w++) {
-        T jr[3] = {ja[w][0] + alpha * js[w][0], ja[w][1] + alpha * js[w][1], ja[w][2] + alpha * js[w][2]};
+        const T x[3] = {WC[w].js[0], WC[w].js[1], WC[w].js[2]};
+        T jr[3] = {WC[w].ja[0] + alpha * x[0], WC[w].ja[1] + alpha * x[1], WC[w].ja[2] + alpha * x[2]};
+        T Dw[3] = {WC[w].D[0], WC[w].D[1], WC[w].D[2]};
         T f[3], Cc[6];
-        cone_eval(jr, mu_w, f1w, f2w, WC[w].D, f, Cc);
-        const T* x = js[w];
+        cone_eval(jr, mu_w, f1w, f2w, Dw, f, Cc);
         d1 -= f[0] * x[0] + f[1] * x[1] + f[2] * x[2];
         dmag += fabs(f[0] * x[0]) + fabs(f[1] * x[1]) + fabs(f[2] * x[2]);
         d2 += Cc[0] * x[0] * x[0] + Cc[1] * x[1] * x[1] + Cc[2] * x[2] * x[2] +
               2 * (Cc[3] * x[0] * x[1] + Cc[4] * x[0] * x[2] + Cc[5] * x[1] * x[2]);
       }
-      for (int sg = 0; sg < ng; sg++) {
-        T n[3], lv[3], aref[3], D;
-        ground_load(st, sg, n, lv, aref, D);
-        T t1[3], t2[3];
-        frame_from_normal(n, t1, t2);
-        T pa[3], ps[3], tt[3];
-        cross3(tt, wa, lv);
-        pa[0] = a[9] + tt[0]; pa[1] = a[10] + tt[1]; pa[2] = a[11] + tt[2];
-        cross3(tt, ws, lv);
-        ps[0] = s[9] + tt[0]; ps[1] = s[10] + tt[1]; ps[2] = s[11] + tt[2];
-        T x[3] = {dot3(n, ps), dot3(t1, ps), dot3(t2, ps)};
-        T jr[3] = {dot3(n, pa) - aref[0] + alpha * x[0], dot3(t1, pa) - aref[1] + alpha * x[1],
-                   dot3(t2, pa) - aref[2] + alpha * x[2]};
+      for (int c = 0; c < ng; c++) {
+        T x[3] = {st.at(c, GF_JS), st.at(c, GF_JS + 1), st.at(c, GF_JS + 2)};
+        T jr[3] = {st.at(c, GF_JAR) + alpha * x[0], st.at(c, GF_JAR + 1) + alpha * x[1],
+                   st.at(c, GF_JAR + 2) + alpha * x[2]};
+        const T D = st.at(c, GF_D);
         T Dv[3] = {D, D, D}, f[3], Cc[6];
         cone_eval(jr, T(1), T(1), T(1), Dv, f, Cc);
         d1 -= f[0] * x[0] + f[1] * x[1] + f[2] * x[2];

@@ -34,20 +34,21 @@ struct StageOut {
 // mj_forward for this model: returns qacc in acc (acc holds the warm start on entry).
 template <typename T>
 BB_HD int forward(const ModelT<T>& m, const T* q, const T* v, const T* ctrl, T* acc, const float* hf, T size_z,
-                  const GStore<T>& st, StageOut<T>* so) {
-  Kin<T> k;
+                  EnvWork<T>& W, StageOut<T>* so) {
+  Kin<T>& k = W.k;
   kinematics(m, q, k);
-  Mass<T> M;
-  build_mass(m, k, M);
+  Mass<T>& M = W.M;
+  build_mass(m, k, M, W.Iw);
   T qfs[NV];
-  bias_forces(m, k, M, v, qfs);
+  bias_forces(m, k, W.Iw, v, qfs);
 #pragma unroll
   for (int i = 0; i < NV; i++) qfs[i] = -qfs[i];
 #pragma unroll
   for (int w = 0; w < 3; w++) qfs[6 + w] += -m.damping * v[6 + w] + ctrl[w];
-  WheelCon<T> WC[3];
+  WheelCon<T>* WC = W.wc;
 #pragma unroll
   for (int w = 0; w < 3; w++) wheel_contact(m, k, v, w, WC[w]);
+  const GStore<T> st{W.g, 1};
   int overflow = 0;
   int ng = hf ? collide_ground(m, k, v, hf, size_z, st, &overflow) : 0;
   bool ok = true;
@@ -57,7 +58,7 @@ BB_HD int forward(const ModelT<T>& m, const T* q, const T* v, const T* ctrl, T* 
 #pragma unroll
     for (int i = 0; i < NV; i++) acc[i] = 0;
   }
-  int it = solve(m, k, M, qfs, WC, ng, st, acc);
+  int it = solve(m, M, qfs, WC, ng, st, W.H, acc);
   if (so) {
     T qb[4] = {q[3], q[4], q[5], q[6]};
     qnormalize(qb);
@@ -78,28 +79,51 @@ BB_HD int forward(const ModelT<T>& m, const T* q, const T* v, const T* ctrl, T* 
 // warm: qacc_warmstart (each stage's constraint solve saves its qacc).
 template <typename T>
 BB_HD int rk4_step(const ModelT<T>& m, T* q, T* v, T* warm, const T* ctrl, const float* hf, T size_z,
-                   const GStore<T>& st, StageOut<T>& so) {
+                   EnvWork<T>& W, StageOut<T>& so) {
   const T h = m.h;
-  T q0[NQ], v0[NV], vs[NV], as[NV], vp[NV];
+  T* q0 = W.q0;
+  T* v0 = W.v0;
+  T* vs = W.vs;
+  T* as = W.as;
+  T* vp = W.vp;
 #pragma unroll
   for (int i = 0; i < NQ; i++) q0[i] = q[i];
 #pragma unroll
   for (int i = 0; i < NV; i++) v0[i] = v[i];
-  int iters = forward(m, q0, v0, ctrl, warm, hf, size_z, st, (StageOut<T>*)nullptr);
+  (void)vp;
+  // one call site for forward (keeps a single inlined copy of the solver);
+  // the stage state lives in the workspace so nothing but the warm start is
+  // register-resident across the solve
+  T* qi = W.qi;
+  T* vi = W.vi;
+  int iters = 0;
+#pragma unroll 1
+  for (int stage = 0; stage < 4; stage++) {
+    const T a = stage == 3 ? T(1) : T(0.5);                            // RK4 Butcher A (sub-diagonal)
+    if (stage == 0) {
 #pragma unroll
-  for (int i = 0; i < NV; i++) { vs[i] = v0[i] * T(1.0 / 6); as[i] = warm[i] * T(1.0 / 6); vp[i] = v0[i]; }
-  for (int stage = 1; stage < 4; stage++) {
-    const T a = stage < 3 ? T(0.5) : T(1);       // RK4 Butcher A (sub-diagonal)
-    const T b = stage < 3 ? T(1.0 / 3) : T(1.0 / 6);
-    T qi[NQ], vi[NV], dv[NV];
+      for (int i = 0; i < NQ; i++) qi[i] = q0[i];
 #pragma unroll
-    for (int i = 0; i < NQ; i++) qi[i] = q0[i];
+      for (int i = 0; i < NV; i++) vi[i] = v0[i];
+    } else {
+      T qq[NQ], dv[NV];
 #pragma unroll
-    for (int i = 0; i < NV; i++) { dv[i] = a * vp[i]; vi[i] = v0[i] + h * a * warm[i]; }
-    integrate_pos(qi, dv, h);
-    iters += forward(m, qi, vi, ctrl, warm, hf, size_z, st, stage == 3 ? &so : (StageOut<T>*)nullptr);
+      for (int i = 0; i < NQ; i++) qq[i] = q0[i];
 #pragma unroll
-    for (int i = 0; i < NV; i++) { vs[i] += b * vi[i]; as[i] += b * warm[i]; vp[i] = vi[i]; }
+      for (int i = 0; i < NV; i++) { dv[i] = a * vp[i]; vi[i] = v0[i] + h * a * warm[i]; }
+      integrate_pos(qq, dv, h);
+#pragma unroll
+      for (int i = 0; i < NQ; i++) qi[i] = qq[i];
+    }
+    iters += forward(m, qi, vi, ctrl, warm, hf, size_z, W, stage == 3 ? &so : (StageOut<T>*)nullptr);
+    const T b = (stage == 0 || stage == 3) ? T(1.0 / 6) : T(1.0 / 3);  // RK4 weights B
+    if (stage == 0) {
+#pragma unroll
+      for (int i = 0; i < NV; i++) { vs[i] = b * vi[i]; as[i] = b * warm[i]; vp[i] = vi[i]; }
+    } else {
+#pragma unroll
+      for (int i = 0; i < NV; i++) { vs[i] += b * vi[i]; as[i] += b * warm[i]; vp[i] = vi[i]; }
+    }
   }
   // mj_advance: qvel = v0 + h*qacc_rk ; qpos = q0 (+) h*v_rk
 #pragma unroll
@@ -143,14 +167,14 @@ constexpr int F_TERMINATED = 1, F_FAILURE = 2, F_DIVERGED = 4, F_OVERFLOW = 8;
 // motor_state, orientation, vel), the order the policy's Extractor consumes.
 template <typename T>
 BB_HD int env_step(const ModelT<T>& m, const EnvCfg& cfg, T* q, T* v, T* warm, int& step, const float* action,
-                   const float* hf, T size_z, const GStore<T>& st, float* obs15, float& reward, float* pos2d,
+                   const float* hf, T size_z, EnvWork<T>& W, float* obs15, float& reward, float* pos2d,
                    int* iters) {
   const float mwv = cfg.max_wheel_velocity;
   T ctrl[3];
 #pragma unroll
   for (int i = 0; i < 3; i++) ctrl[i] = -T(clipf(action[i] * mwv, -mwv, mwv));  // data.ctrl[:] = -ctrl
   StageOut<T> so;
-  int it = rk4_step(m, q, v, warm, ctrl, hf, size_z, st, so);
+  int it = rk4_step(m, q, v, warm, ctrl, hf, size_z, W, so);
   if (iters) *iters = it;
   int flags = state_bad(q, v) ? F_DIVERGED : 0;
   if (so.overflow) flags |= F_OVERFLOW;
