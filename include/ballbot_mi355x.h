@@ -37,7 +37,7 @@
 extern "C" {
 #endif
 
-#define BB_ABI_VERSION 1
+#define BB_ABI_VERSION 2
 #define BB_NQ 17
 #define BB_NV 15
 #define BB_OBS 15
@@ -103,8 +103,9 @@ int bb_set_state(bb_handle* h, const double* qpos, const double* qvel, const dou
 int bb_forward(bb_handle* h, const double* ctrl, double* qacc, int32_t* ncontact);
 /* counters since create: [resets, diverged, overflow, steps, solver_iters_lo, solver_iters_hi] */
 int bb_get_stats(bb_handle* h, int64_t* out6);
-/* launch configuration: [n_envs, envs_per_wave, fp64, lds_bytes_per_workgroup] */
-int bb_get_config(bb_handle* h, int32_t* out4);
+/* launch configuration: [n_envs, envs_per_wave, fp64, lds_bytes_per_workgroup,
+ * lanes_per_env] */
+int bb_get_config(bb_handle* h, int32_t* out5);
 /* init height offset per terrain (ballbot_env.py:546-563) */
 int bb_get_offsets(bb_handle* h, float* out);
 

@@ -49,6 +49,8 @@ EXPORTS = [
     "bb_get_offsets", "bb_get_config",
 ]
 
+ABI_VERSION = 2  # include/ballbot_mi355x.h BB_ABI_VERSION
+
 _lib = None
 
 
@@ -100,7 +102,7 @@ def lib():
     L.bb_get_config.argtypes = [vp, C.POINTER(C.c_int32)]
     for name in [n for n in EXPORTS if n not in ("bb_default_params", "bb_abi_version")]:
         getattr(L, name).restype = C.c_int
-    if L.bb_abi_version() != 1:
+    if L.bb_abi_version() != ABI_VERSION:
         raise NativeLibraryError("ABI version mismatch")
     _lib = L
     return L

@@ -221,9 +221,10 @@ class BallbotVecEnv:
                 "solver_iters": out[4] + (out[5] << 32)}
 
     def launch_config(self) -> Dict[str, int]:
-        out = (C.c_int32 * 4)()
+        out = (C.c_int32 * 5)()
         N.check(N.lib().bb_get_config(self._h, out), "bb_get_config")
-        return {"num_envs": out[0], "envs_per_wave": out[1], "fp64": out[2], "lds_bytes_per_workgroup": out[3]}
+        return {"num_envs": out[0], "envs_per_wave": out[1], "fp64": out[2], "lds_bytes_per_workgroup": out[3],
+                "lanes_per_env": out[4]}
 
     def offsets(self) -> np.ndarray:
         o = np.zeros(self.n_terrains, np.float32)

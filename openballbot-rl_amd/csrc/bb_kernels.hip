@@ -4,8 +4,12 @@
 //   qpos  T[17][n]   qvel T[15][n]   warm T[15][n]     SoA: lane e reads
 //   steps int[n]     terrain int[n]  episodes int[n]   element i at [i*n + e]
 //   bank  float[n_terrains][293*293], size_z float[nt], offset float[nt]
-// One env per lane, one 64-lane wave per workgroup; ball-terrain contacts
-// are kept in LDS, lane-interleaved ([slot*NGF + field][64]).
+// One env per TEAM of L lanes (L = 16 by default: 4 envs per 64-lane wave,
+// one wave per workgroup, 4096 envs -> 1024 waves = one per SIMD).  Each team
+// owns an EnvWork (bb_solve.h) in LDS holding the mass blocks, contact
+// Jacobians, ground-contact store, Hessian/Cholesky factor and phase-local
+// scratch; the constraint solve is team-parallel, the per-env state is
+// replicated in the team's registers and stored by the team's lane 0.
 #include <hip/hip_runtime.h>
 
 #include <stdarg.h>
@@ -38,15 +42,14 @@ int fail(const char* fmt, ...) {
     if (e_ != hipSuccess) return fail("%s: %s", #x, hipGetErrorString(e_));         \
   } while (0)
 
-// per-lane EnvWork stride in LDS: 8 mod 16 bytes so that 8-byte accesses of
-// consecutive lanes fall on distinct bank pairs
+// per-team EnvWork stride in LDS (16-byte aligned)
 template <typename T>
-__host__ __device__ constexpr size_t work_stride() { return (sizeof(EnvWork<T>) + 15) / 16 * 16 + 8; }
+__host__ __device__ constexpr size_t work_stride() { return (sizeof(EnvWork<T>) + 15) / 16 * 16; }
 template <typename T>
 size_t lds_bytes(int epw) { return work_stride<T>() * epw; }
 template <typename T>
-__device__ __forceinline__ EnvWork<T>& lane_work(unsigned char* smem, int lane) {
-  return *reinterpret_cast<EnvWork<T>*>(smem + size_t(lane) * work_stride<T>());
+__device__ __forceinline__ EnvWork<T>& team_work(unsigned char* smem, int team) {
+  return *reinterpret_cast<EnvWork<T>*>(smem + size_t(team) * work_stride<T>());
 }
 
 BB_HD uint32_t hash3(uint64_t seed, uint32_t a, uint32_t b) {  // splitmix-style counter hash
@@ -108,9 +111,8 @@ template <typename T>
 __global__ __launch_bounds__(64) void step_kernel(ModelT<T> mg, EnvCfg cfg, Dev d, const float* __restrict__ act,
                                                   float* __restrict__ obs, float* __restrict__ rew,
                                                   uint8_t* __restrict__ done, float* __restrict__ tobs,
-                                                  float* __restrict__ pos2d, int auto_reset, int epw) {
-  // epw envs per 64-lane wave (lanes >= epw idle): spreads small batches over
-  // all 1024 SIMDs instead of a few fully-populated waves.
+                                                  float* __restrict__ pos2d, int auto_reset, int L, int epw) {
+  // epw teams of L lanes per 64-lane wave (teams >= epw idle)
   extern __shared__ __align__(16) unsigned char smem[];
   // model constants staged in LDS once per workgroup: uniform-address LDS
   // reads broadcast, and ~150 uniform doubles no longer overflow the SGPRs
@@ -118,11 +120,13 @@ __global__ __launch_bounds__(64) void step_kernel(ModelT<T> mg, EnvCfg cfg, Dev 
   if (threadIdx.x == 0) ms = mg;
   __syncthreads();
   const ModelT<T>& m = ms;
-  const int lane = threadIdx.x;
-  if (lane >= epw) return;
-  const int e = blockIdx.x * epw + lane;
+  const Team tm{L, int(threadIdx.x) & (L - 1)};
+  const int team = threadIdx.x / L;
+  if (team >= epw) return;
+  const int e = blockIdx.x * epw + team;
   if (e >= d.n) return;
-  EnvWork<T>& W = lane_work<T>(smem, lane);
+  const bool lead = tm.tl == 0;
+  EnvWork<T>& W = team_work<T>(smem, team);
   T q[NQ], v[NV], w[NV];
   int step;
   load_state(d, e, q, v, w, step);
@@ -131,7 +135,8 @@ __global__ __launch_bounds__(64) void step_kernel(ModelT<T> mg, EnvCfg cfg, Dev 
   const float* hf = d.bank + size_t(tid) * (HF_N * HF_N);
   float o[15], r, p2[2];
   int iters = 0;
-  int fl = env_step(m, cfg, q, v, w, step, a, hf, T(d.size_z[tid]), W, o, r, p2, &iters);
+  int fl = env_step(m, cfg, q, v, w, step, a, hf, T(d.size_z[tid]), W, o, r, p2, &iters, tm);
+  if (!lead) return;
   if (tobs) {
 #pragma unroll
     for (int i = 0; i < 15; i++) tobs[15 * e + i] = o[i];
@@ -175,24 +180,27 @@ __global__ __launch_bounds__(64) void reset_kernel(ModelT<T> m, Dev d, const uin
 }
 
 template <typename T>
-__global__ __launch_bounds__(64) void forward_kernel(ModelT<T> mg, Dev d, const double* ctrl, double* qacc, int* ncon, int epw) {
+__global__ __launch_bounds__(64) void forward_kernel(ModelT<T> mg, Dev d, const double* ctrl, double* qacc, int* ncon,
+                                                     int L, int epw) {
   extern __shared__ __align__(16) unsigned char smem[];
   __shared__ ModelT<T> ms;
   if (threadIdx.x == 0) ms = mg;
   __syncthreads();
   const ModelT<T>& m = ms;
-  const int lane = threadIdx.x;
-  if (lane >= epw) return;
-  const int e = blockIdx.x * epw + lane;
+  const Team tm{L, int(threadIdx.x) & (L - 1)};
+  const int team = threadIdx.x / L;
+  if (team >= epw) return;
+  const int e = blockIdx.x * epw + team;
   if (e >= d.n) return;
-  EnvWork<T>& W = lane_work<T>(smem, lane);
+  EnvWork<T>& W = team_work<T>(smem, team);
   T q[NQ], v[NV], w[NV], c[3];
   int step;
   load_state(d, e, q, v, w, step);
   for (int i = 0; i < 3; i++) c[i] = T(ctrl[3 * e + i]);
   const int tid = d.terrain[e];
   StageOut<T> so;
-  forward(m, q, v, c, w, d.bank + size_t(tid) * (HF_N * HF_N), T(d.size_z[tid]), W, &so);
+  forward(m, q, v, c, w, d.bank + size_t(tid) * (HF_N * HF_N), T(d.size_z[tid]), W, &so, tm);
+  if (tm.tl != 0) return;
   for (int i = 0; i < NV; i++) qacc[NV * e + i] = double(w[i]);
   if (ncon) ncon[e] = so.ng;
 }
@@ -207,7 +215,7 @@ __global__ void assign_kernel(Dev d, const int32_t* ids) {
 }  // namespace
 
 struct bb_handle {
-  int n, device, fp64, epw;
+  int n, device, fp64, team, epw;
   bb_params p;
   EnvCfg cfg;
   ModelT<float> mf;
@@ -244,7 +252,7 @@ int launch_step(bb_handle* h, const float* a, float* o, float* r, uint8_t* dn, f
   const int epw = h->epw;
   int blocks = (h->n + epw - 1) / epw;
   hipLaunchKernelGGL(step_kernel<T>, dim3(blocks), dim3(WAVE), lds_bytes<T>(epw), s, m, h->cfg, h->d, a, o, r, dn,
-                     t, p2, ar, epw);
+                     t, p2, ar, h->team, epw);
   HIPCHK(hipGetLastError());
   return 0;
 }
@@ -297,20 +305,26 @@ int bb_create(int n_envs, int device, const bb_params* p, bb_handle** out) {
   SolverCfg sc = default_solver(h->fp64);
   if (pp.solver_maxiter > 0) sc.maxiter = pp.solver_maxiter;
   if (pp.solver_tol > 0) sc.tol = pp.solver_tol;
-  // envs per wave: aim for one wave per SIMD (4 per CU) across the whole chip
+  // team size L (lanes per env) and envs per wave: aim for at least one wave
+  // per SIMD (4 per CU) across the whole chip
   {
     hipDeviceProp_t prop;
     HIPCHK(hipGetDeviceProperties(&prop, device));
     const int simds = prop.multiProcessorCount * 4;
-    // LDS caps envs per wave: one EnvWork per lane + the staged model
+    int L = 16;
+    const char* tv = getenv("BB_TEAM");
+    if (tv && atoi(tv) > 0) L = atoi(tv);
+    if (L > WAVE || (L & (L - 1))) { delete h; return fail("bb_create: BB_TEAM must be a power of two <= 64 (got %d)", L); }
+    // LDS caps envs per wave: one EnvWork per team + the staged model
     const size_t lds_max = 160 * 1024 - 2048;
     const int cap = (int)(lds_max / (h->fp64 ? work_stride<double>() : work_stride<float>()));
     int epw = 1;
-    while (epw < WAVE && (long)epw * simds < (long)n_envs) epw *= 2;
+    while (epw < WAVE / L && (long)epw * simds < (long)n_envs) epw *= 2;
     const char* ov = getenv("BB_EPW");
     if (ov && atoi(ov) > 0) epw = atoi(ov);
-    if (epw > WAVE) epw = WAVE;
+    if (epw > WAVE / L) epw = WAVE / L;
     if (epw > cap) epw = cap;
+    h->team = L;
     h->epw = epw;
   }
   h->md = compile_model(sc);
@@ -360,10 +374,10 @@ int bb_create(int n_envs, int device, const bb_params* p, bb_handle** out) {
 
 int bb_destroy(bb_handle* h) {
   if (!h) return 0;
-  hipSetDevice(h->device);
-  hipFree(h->d.qpos); hipFree(h->d.qvel); hipFree(h->d.warm);
-  hipFree(h->d.steps); hipFree(h->d.terrain); hipFree(h->d.pending_terrain); hipFree(h->d.episodes);
-  hipFree(h->bank); hipFree(h->size_z); hipFree(h->offset); hipFree(h->d.stats);
+  (void)hipSetDevice(h->device);
+  (void)hipFree(h->d.qpos); (void)hipFree(h->d.qvel); (void)hipFree(h->d.warm);
+  (void)hipFree(h->d.steps); (void)hipFree(h->d.terrain); (void)hipFree(h->d.pending_terrain); (void)hipFree(h->d.episodes);
+  (void)hipFree(h->bank); (void)hipFree(h->size_z); (void)hipFree(h->offset); (void)hipFree(h->d.stats);
   delete h;
   return 0;
 }
@@ -464,15 +478,15 @@ int bb_forward(bb_handle* h, const double* ctrl, double* qacc, int32_t* ncon) {
   int blocks = (h->n + epw - 1) / epw;
   if (h->fp64)
     hipLaunchKernelGGL(forward_kernel<double>, dim3(blocks), dim3(WAVE), lds_bytes<double>(epw), 0, h->md, h->d, dc, dq,
-                       dn, epw);
+                       dn, h->team, epw);
   else
     hipLaunchKernelGGL(forward_kernel<float>, dim3(blocks), dim3(WAVE), lds_bytes<float>(epw), 0, h->mf, h->d, dc, dq,
-                       dn, epw);
+                       dn, h->team, epw);
   HIPCHK(hipGetLastError());
   HIPCHK(hipDeviceSynchronize());
   HIPCHK(hipMemcpy(qacc, dq, sizeof(double) * NV * n, hipMemcpyDeviceToHost));
   if (ncon) HIPCHK(hipMemcpy(ncon, dn, sizeof(int) * n, hipMemcpyDeviceToHost));
-  hipFree(dc); hipFree(dq); hipFree(dn);
+  (void)hipFree(dc); (void)hipFree(dq); (void)hipFree(dn);
   return 0;
 }
 
@@ -486,10 +500,11 @@ int bb_get_stats(bb_handle* h, int64_t* out6) {
   return 0;
 }
 
-int bb_get_config(bb_handle* h, int32_t* out4) {
-  if (!h || !out4) return fail("bb_get_config: NULL argument");
-  out4[0] = h->n; out4[1] = h->epw; out4[2] = h->fp64;
-  out4[3] = (int32_t)(h->fp64 ? lds_bytes<double>(h->epw) : lds_bytes<float>(h->epw));
+int bb_get_config(bb_handle* h, int32_t* out5) {
+  if (!h || !out5) return fail("bb_get_config: NULL argument");
+  out5[0] = h->n; out5[1] = h->epw; out5[2] = h->fp64;
+  out5[3] = (int32_t)(h->fp64 ? lds_bytes<double>(h->epw) : lds_bytes<float>(h->epw));
+  out5[4] = h->team;
   return 0;
 }
 

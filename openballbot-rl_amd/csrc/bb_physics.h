@@ -33,11 +33,10 @@ constexpr int NQ = 17, NV = 15, NU = 3;
 constexpr int HF_N = 293;        // ballbot.xml:23 nrow = ncol
 constexpr int MAXG = 24;         // ball-hfield contact cap (== oracle BBO_MAXGROUND)
 constexpr int NH = NV * (NV + 1) / 2;
-constexpr int NGF = 28;          // fields per stored ground contact (see GF_* below)
+constexpr int NGF = 22;          // fields per stored ground contact (see GF_* below)
 // ground-contact store fields: three Jacobian rows over the ball dofs
-// (world-linear[3], local-angular[3]), aref[3], D, and the line-search cache
-// jar(alpha=0)[3], J*s[3]
-constexpr int GF_J = 0, GF_AREF = 18, GF_D = 21, GF_JAR = 22, GF_JS = 25;
+// (world-linear[3], local-angular[3]), aref[3], D
+constexpr int GF_J = 0, GF_AREF = 18, GF_D = 21;
 
 // ------------------------------------------------------------------ model
 // Compiled constants (bb_model.cpp computes them in double from the MJCF
@@ -474,8 +473,6 @@ template <typename T>
 struct WheelCon {
   T J[3][13];     // rows: normal, axle tangent (patch), drive tangent
   T aref[3], D[3];
-  T dist;
-  T ja[3], js[3];   // line-search cache: J a - aref, J s
 };
 
 // global dof index of wheel-contact column i for wheel w
@@ -487,21 +484,6 @@ struct GStore {
   T* base;
   int stride;
   BB_HD T& at(int s, int f) const { return base[(s * NGF + f) * stride]; }
-};
-
-// Per-env working set of one forward/RK step.  On the GPU one EnvWork per
-// lane lives in LDS (bb_kernels.hip), so only the solver vectors and the
-// packed Hessian occupy registers.
-template <typename T>
-struct EnvWork {
-  T g[MAXG * NGF];          // ball-terrain contacts
-  WheelCon<T> wc[3];        // ball-wheel contacts
-  Mass<T> M;                // mass-matrix blocks
-  Kin<T> k;                 // kinematics of the current stage
-  T Iw[3][6];               // wheel inertias (base-local) of the current stage
-  T H[NH];                  // Newton Hessian / its Cholesky factor (packed lower)
-  T q0[NQ], v0[NV], vs[NV], as[NV], vp[NV];  // RK4 stage context
-  T qi[NQ], vi[NV];                          // current stage state
 };
 
 // patched mjraw_SphereCapsule (tools/mujoco_fix.patch:11-16) + mju_makeFrame
@@ -517,7 +499,6 @@ BB_HD void wheel_contact(const ModelT<T>& m, const Kin<T>& k, const T* v, int w,
   T dif[3] = {gp[0] + ax[0] * x - k.c[0], gp[1] + ax[1] * x - k.c[1], gp[2] + ax[2] * x - k.c[2]};
   T cd = sqrt(dot3(dif, dif));
   T dist = cd - m.ball_r - m.wheel_r;
-  C.dist = dist;
   const T act = dist <= 0 ? T(1) : T(0);
   T n[3];
   if (cd > 0) { T ic = T(1) / cd; n[0] = dif[0] * ic; n[1] = dif[1] * ic; n[2] = dif[2] * ic; }
@@ -832,195 +813,6 @@ BB_HD void chol_solve_packed(const T* L, T* x) {
     for (int k = i + 1; k < NV; k++) s -= L[hidx(k, i)] * x[k];
     x[i] = s / L[hidx(i, i)];
   }
-}
-
-// J_r . x over the ball dofs for a stored ground contact
-template <typename T>
-BB_HD T ground_row_mul(const GStore<T>& st, int c, int r, const T* x) {
-  const int b = GF_J + 6 * r;
-  return st.at(c, b) * x[9] + st.at(c, b + 1) * x[10] + st.at(c, b + 2) * x[11] + st.at(c, b + 3) * x[12] +
-         st.at(c, b + 4) * x[13] + st.at(c, b + 5) * x[14];
-}
-
-// Newton on  0.5 a'Ma - a'qfs + sum_c cost_c(J_c a - aref_c)   (mj_solNewton).
-// The minimiser is unique (M > 0); returns iterations used.
-template <typename T>
-BB_HD int solve(const ModelT<T>& m, const Mass<T>& M, const T* qfs, WheelCon<T>* WC, int ng, const GStore<T>& st,
-                T* H, T* a) {
-  const T mu_w = m.fr_wheel[0], f1w = m.fr_wheel[0], f2w = m.fr_wheel[1];
-  int it = 0;
-  for (; it < m.maxiter; it++) {
-    T g[NV], Ma[NV];
-    mass_mul(M, a, Ma);
-#pragma unroll
-    for (int i = 0; i < NV; i++) g[i] = Ma[i] - qfs[i];
-    mass_dense(M, H);
-    // ---- wheel contacts (explicit pairs): gradient and Hessian, unrolled
-#pragma unroll
-    for (int w = 0; w < 3; w++) {
-      const WheelCon<T>& C = WC[w];
-      T jar[3], f[3], Cc[6];
-#pragma unroll
-      for (int r = 0; r < 3; r++) jar[r] = wheel_row_mul(C, w, r, a) - C.aref[r];
-      cone_eval(jar, mu_w, f1w, f2w, C.D, f, Cc);
-      // gradient over the 13 structural columns
-#pragma unroll
-      for (int j = 0; j < 13; j++) g[wheel_col(j, w)] -= C.J[0][j] * f[0] + C.J[1][j] * f[1] + C.J[2][j] * f[2];
-      // H += J' C J, rolled over (i, j) with J and H in the LDS workspace
-      for (int i = 0; i < 13; i++) {
-        const T j0 = C.J[0][i], j1 = C.J[1][i], j2 = C.J[2][i];
-        const T u0 = Cc[0] * j0 + Cc[3] * j1 + Cc[4] * j2;
-        const T u1 = Cc[3] * j0 + Cc[1] * j1 + Cc[5] * j2;
-        const T u2 = Cc[4] * j0 + Cc[5] * j1 + Cc[2] * j2;
-        const int ci = wheel_col(i, w);
-        T* Hrow = H + ci * (ci + 1) / 2;
-        for (int j = 0; j <= i; j++) Hrow[wheel_col(j, w)] += C.J[0][j] * u0 + C.J[1][j] * u1 + C.J[2][j] * u2;
-      }
-    }
-    // ---- ground contacts: ball-only columns (6), rows cached in the store
-    {
-      T Hb[21];
-#pragma unroll
-      for (int i = 0; i < 21; i++) Hb[i] = 0;
-      for (int c = 0; c < ng; c++) {
-        T J[3][6];
-#pragma unroll
-        for (int r = 0; r < 3; r++)
-#pragma unroll
-          for (int i = 0; i < 6; i++) J[r][i] = st.at(c, GF_J + 6 * r + i);
-        T jar[3];
-#pragma unroll
-        for (int r = 0; r < 3; r++) {
-          jar[r] = J[r][0] * a[9] + J[r][1] * a[10] + J[r][2] * a[11] + J[r][3] * a[12] + J[r][4] * a[13] +
-                   J[r][5] * a[14] - st.at(c, GF_AREF + r);
-          st.at(c, GF_JAR + r) = jar[r];
-        }
-        const T D = st.at(c, GF_D);
-        T Dv[3] = {D, D, D}, f[3], Cc[6];
-        cone_eval(jar, T(1), T(1), T(1), Dv, f, Cc);
-        T w[3][6];
-#pragma unroll
-        for (int i = 0; i < 6; i++) {
-          g[9 + i] -= J[0][i] * f[0] + J[1][i] * f[1] + J[2][i] * f[2];
-          w[0][i] = Cc[0] * J[0][i] + Cc[3] * J[1][i] + Cc[4] * J[2][i];
-          w[1][i] = Cc[3] * J[0][i] + Cc[1] * J[1][i] + Cc[5] * J[2][i];
-          w[2][i] = Cc[4] * J[0][i] + Cc[5] * J[1][i] + Cc[2] * J[2][i];
-        }
-#pragma unroll
-        for (int i = 0; i < 6; i++)
-#pragma unroll
-          for (int j = 0; j <= i; j++) Hb[i * (i + 1) / 2 + j] += J[0][i] * w[0][j] + J[1][i] * w[1][j] + J[2][i] * w[2][j];
-      }
-#pragma unroll
-      for (int i = 0; i < 6; i++)
-#pragma unroll
-        for (int j = 0; j <= i; j++) H[hidx(9 + i, 9 + j)] += Hb[i * (i + 1) / 2 + j];
-    }
-    T gn = 0;
-#pragma unroll
-    for (int i = 0; i < NV; i++) gn += g[i] * g[i];
-#ifdef BB_TRACE
-    printf("it %d gn %.4e\n", it, double(m.scale * sqrt(gn)));
-#endif
-    if (m.scale * sqrt(gn) < m.tol) break;
-    // ---- Newton direction
-    T hd[NV];
-#pragma unroll
-    for (int i = 0; i < NV; i++) hd[i] = H[hidx(i, i)];
-    chol_packed(H);
-    T s[NV];
-#pragma unroll
-    for (int i = 0; i < NV; i++) s[i] = -g[i];
-    chol_solve_packed(H, s);
-    {
-      // a roundoff-indefinite Hessian (fp32, stiff drive rows) can give a
-      // non-descent or non-finite direction: fall back to diagonal Newton
-      bool fin = true;
-      T dd = 0;
-#pragma unroll
-      for (int i = 0; i < NV; i++) { fin = fin && isfinite(s[i]); dd += s[i] * g[i]; }
-      if (!fin || !(dd < 0)) {
-#pragma unroll
-        for (int i = 0; i < NV; i++) s[i] = -g[i] / maxT(hd[i], T(1e-30));
-      }
-    }
-    // ---- exact line search on phi(alpha) = f(a + alpha s)
-    T Ms[NV];
-    mass_mul(M, s, Ms);
-    T sMs = 0, gs = 0, d0 = 0;
-#pragma unroll
-    for (int i = 0; i < NV; i++) { sMs += s[i] * Ms[i]; gs += s[i] * (Ma[i] - qfs[i]); d0 += s[i] * g[i]; }
-    if (!(d0 < 0)) break;
-#pragma unroll
-    for (int w = 0; w < 3; w++)
-#pragma unroll
-      for (int r = 0; r < 3; r++) {
-        WC[w].ja[r] = wheel_row_mul(WC[w], w, r, a) - WC[w].aref[r];
-        WC[w].js[r] = wheel_row_mul(WC[w], w, r, s);
-      }
-    for (int c = 0; c < ng; c++)
-#pragma unroll
-      for (int r = 0; r < 3; r++) st.at(c, GF_JS + r) = ground_row_mul(st, c, r, s);
-    // 1-D Newton on phi'(alpha) from the full Newton step alpha = 1,
-    // safeguarded by false position on the bracket [lo, hi] (phi' is
-    // continuous and nondecreasing: the cost is convex and C1).
-    T lo = 0, dlo = d0, hi = -1, dhi = 0, alpha = 1;
-    bool ls_ok = false;
-    for (int ls = 1; ls <= m.ls_maxiter; ls++) {
-      T d1 = gs + alpha * sMs, d2 = sMs;
-      T dmag = fabs(gs) + fabs(alpha * sMs);  // magnitude of the summed terms: roundoff floor of d1
-#pragma unroll
-      for (int w = 0; w < 3; w++) {
-        const T x[3] = {WC[w].js[0], WC[w].js[1], WC[w].js[2]};
-        T jr[3] = {WC[w].ja[0] + alpha * x[0], WC[w].ja[1] + alpha * x[1], WC[w].ja[2] + alpha * x[2]};
-        T Dw[3] = {WC[w].D[0], WC[w].D[1], WC[w].D[2]};
-        T f[3], Cc[6];
-        cone_eval(jr, mu_w, f1w, f2w, Dw, f, Cc);
-        d1 -= f[0] * x[0] + f[1] * x[1] + f[2] * x[2];
-        dmag += fabs(f[0] * x[0]) + fabs(f[1] * x[1]) + fabs(f[2] * x[2]);
-        d2 += Cc[0] * x[0] * x[0] + Cc[1] * x[1] * x[1] + Cc[2] * x[2] * x[2] +
-              2 * (Cc[3] * x[0] * x[1] + Cc[4] * x[0] * x[2] + Cc[5] * x[1] * x[2]);
-      }
-      for (int c = 0; c < ng; c++) {
-        T x[3] = {st.at(c, GF_JS), st.at(c, GF_JS + 1), st.at(c, GF_JS + 2)};
-        T jr[3] = {st.at(c, GF_JAR) + alpha * x[0], st.at(c, GF_JAR + 1) + alpha * x[1],
-                   st.at(c, GF_JAR + 2) + alpha * x[2]};
-        const T D = st.at(c, GF_D);
-        T Dv[3] = {D, D, D}, f[3], Cc[6];
-        cone_eval(jr, T(1), T(1), T(1), Dv, f, Cc);
-        d1 -= f[0] * x[0] + f[1] * x[1] + f[2] * x[2];
-        dmag += fabs(f[0] * x[0]) + fabs(f[1] * x[1]) + fabs(f[2] * x[2]);
-        d2 += Cc[0] * x[0] * x[0] + Cc[1] * x[1] * x[1] + Cc[2] * x[2] * x[2] +
-              2 * (Cc[3] * x[0] * x[1] + Cc[4] * x[0] * x[2] + Cc[5] * x[1] * x[2]);
-      }
-      if (ls > 0) {
-        // converged: relative to phi'(0), or at the arithmetic's roundoff floor
-        if (fabs(d1) <= m.ls_tol * fabs(d0) || fabs(d1) <= T(32) * eps_of<T>() * dmag) { ls_ok = true; break; }
-        if (!(d1 == d1)) break;
-        if (d1 < 0) { lo = alpha; dlo = d1; } else { hi = alpha; dhi = d1; }
-      }
-      T an = alpha - d1 / maxT(d2, T(1e-30));
-      if (hi < 0) {
-        if (!(an > lo)) an = lo > 0 ? 2 * lo : T(1);
-      } else if (!(an > lo && an < hi)) {
-        T fp = lo - dlo * (hi - lo) / (dhi - dlo);
-        an = (fp > lo && fp < hi) ? fp : T(0.5) * (lo + hi);
-      }
-      alpha = an;
-    }
-    // unconverged search: fall back to the last point with phi' < 0, which
-    // (phi convex) is guaranteed to lower the cost
-    if (!ls_ok) alpha = lo > 0 ? lo : (hi > 0 ? hi * dlo / (dlo - dhi) : T(0));
-    if (!(alpha > 0)) break;
-#ifdef BB_TRACE
-    printf("   alpha %.4e lo %.3e hi %.3e d0 %.3e sMs %.3e |s| %.3e\n", double(alpha), double(lo), double(hi), double(d0), double(sMs), double(sqrt(s[0]*s[0]+s[9]*s[9]+s[12]*s[12])));
-#endif
-    T sn = 0, an2 = 0;
-#pragma unroll
-    for (int i = 0; i < NV; i++) { a[i] += alpha * s[i]; sn += s[i] * s[i]; an2 += a[i] * a[i]; }
-    if (alpha * alpha * sn <= T(1e-30) + m.step_rel2 * (1 + an2)) { it++; break; }
-  }
-  return it;
 }
 
 }  // namespace bb

@@ -1,0 +1,370 @@
+// bb_solve.h -- team-parallel constrained Newton solve (mj_solNewton, elliptic
+// cones) for one env, executed by a team of L lanes of one wavefront.
+//
+// Minimises  f(a) = 0.5 a'Ma - a'qfs + sum_c s_c(J_c a - aref_c)   over qacc a
+// (the primal of MuJoCo's constraint problem; M > 0 so the minimiser is unique
+// and any convergent method reproduces it).  Work split inside the team:
+//   contact pass    contacts c = tl, tl+L, ...: jar, zone, force, cone Hessian
+//   ground terms    6x6 ball-block partials reduced across the team (shuffles)
+//   Hessian         entries e = tl, tl+L, ... of the packed 15x15 (LDS)
+//   Cholesky        right-looking, column scaling and trailing update in LDS
+//   line search     contact-parallel phi'/phi'' partials + team reduction
+// Small vectors (a, g, s, Ma) are replicated in every lane's registers; the
+// triangular solves and the mass products are computed redundantly per lane.
+// With L = 1 (host tests) every loop covers everything and syncs vanish.
+#pragma once
+
+#include "bb_physics.h"
+
+namespace bb {
+
+struct Team {
+  int L;   // lanes per env (power of two, <= 64)
+  int tl;  // this lane's index inside the team
+};
+
+template <typename T>
+BB_HD T team_sum(const Team& tm, T v) {
+#ifdef __HIP_DEVICE_COMPILE__
+  for (int off = tm.L >> 1; off > 0; off >>= 1) v += __shfl_xor(v, off, tm.L);
+#else
+  (void)tm;
+#endif
+  return v;
+}
+
+BB_HD void team_sync() {
+#ifdef __HIP_DEVICE_COMPILE__
+  __syncthreads();  // one 64-lane wave per workgroup: orders LDS traffic inside the wave
+#endif
+}
+
+// packed lower-triangle index e -> (i, j), j <= i
+BB_HD void tri_unpack(int e, int& i, int& j) {
+  int r = (int)((sqrtf(8.f * float(e) + 1.f) - 1.f) * 0.5f);
+  while ((r + 1) * (r + 2) / 2 <= e) r++;
+  while (r * (r + 1) / 2 > e) r--;
+  i = r;
+  j = e - r * (r + 1) / 2;
+}
+
+// Per-env working set of one RK step (LDS on the GPU, one per team).
+// Phase-local buffers share storage in a union to fit 16 envs per CU.
+template <typename T>
+struct EnvWork {
+  T q0[NQ], v0[NV], vs[NV], as[NV], vp[NV];  // RK4 stage context
+  Mass<T> M;                                 // mass-matrix blocks
+  WheelCon<T> wc[3];                         // ball-wheel contacts
+  T g[MAXG * NGF];                           // ball-terrain contacts
+  T H[NH];                                   // Hessian / Cholesky factor (packed lower)
+  T hd[NV];                                  // Hessian diagonal before factorisation
+  union U {
+    struct {                                 // forward pre-phase
+      Kin<T> k;
+      T Iw[3][6];
+    } pre;
+    struct {                                 // Hessian assembly
+      T cj[3][3][13];                        // C J for each wheel contact
+      T wf[3][3];                            // wheel contact forces
+      T hg[21];                              // ground contribution to the ball block
+    } hes;
+    T ls[3 + MAXG][6];                       // line search: jar(0), J s per contact
+  } u;
+};
+
+// Mass-matrix entry (i >= j) from the block representation.
+template <typename T>
+BB_HD T mass_entry(const Mass<T>& M, int i, int j) {
+  if (i < 3) return i == j ? M.mt : T(0);
+  if (i < 6) {
+    if (j < 3) return M.Mtr[3 * j + (i - 3)];
+    const int a = i - 3, b = j - 3;
+    return a == b ? M.Mrr[a] : M.Mrr[a + b + 2];  // (1,0)->3, (2,0)->4, (2,1)->5
+  }
+  if (i < 9) {
+    const int w = i - 6;
+    if (j < 3) return M.Mth[w][j];
+    if (j < 6) return M.Mrh[w][j - 3];
+    return j == i ? M.Mhh[w] : T(0);
+  }
+  if (j < 9) return T(0);
+  if (i < 12) return i == j ? M.mB : T(0);
+  if (j < 12) return M.MBtr[3 * (j - 9) + (i - 12)];
+  return i == j ? M.MBrr[i - 12] : T(0);
+}
+
+// position of dof i among wheel w's 13 contact columns, or -1
+BB_HD int wheel_pos(int i, int w) { return i < 6 ? i : (i == 6 + w ? 6 : (i >= 9 ? i - 2 : -1)); }
+
+// J_r x for wheel contact w (w may be lane-dependent: the hinge entry is selected)
+template <typename T>
+BB_HD T wheel_dot(const WheelCon<T>& C, int w, int r, const T* x) {
+  const T xh = w == 0 ? x[6] : (w == 1 ? x[7] : x[8]);
+  T acc = C.J[r][6] * xh;
+#pragma unroll
+  for (int i = 0; i < 6; i++) acc += C.J[r][i] * x[i];
+#pragma unroll
+  for (int i = 7; i < 13; i++) acc += C.J[r][i] * x[i + 2];
+  return acc;
+}
+
+// J_r x for a stored ground contact (ball dofs only)
+template <typename T>
+BB_HD T ground_dot(const T* gc, int r, const T* x) {
+  const T* J = gc + GF_J + 6 * r;
+  return J[0] * x[9] + J[1] * x[10] + J[2] * x[11] + J[3] * x[12] + J[4] * x[13] + J[5] * x[14];
+}
+
+// Team-parallel right-looking Cholesky in place.  A pivot that roundoff drives
+// below eps * (original diagonal) is floored so the direction stays finite;
+// descent is enforced by the line search.
+template <typename T>
+BB_HD void chol_team(T* H, const T* hd, const Team& tm) {
+  for (int j = 0; j < NV; j++) {
+    team_sync();
+    const int rj = j * (j + 1) / 2;
+    T s = H[rj + j];
+    const T floor_j = pivot_eps<T>() * maxT(hd[j], T(1e-30));
+    s = s > floor_j ? s : floor_j;
+    const T d = sqrt(s), id = T(1) / d;
+    for (int i = j + 1 + tm.tl; i < NV; i += tm.L) H[i * (i + 1) / 2 + j] *= id;
+    team_sync();
+    if (tm.tl == 0) H[rj + j] = d;
+    const int md = NV - 1 - j, cnt = md * (md + 1) / 2;
+    for (int t = tm.tl; t < cnt; t += tm.L) {
+      int ii, kk;
+      tri_unpack(t, ii, kk);
+      const int i = j + 1 + ii, k = j + 1 + kk;
+      H[i * (i + 1) / 2 + k] -= H[i * (i + 1) / 2 + j] * H[k * (k + 1) / 2 + j];
+    }
+  }
+  team_sync();
+}
+
+// accumulate phi'(alpha), phi''(alpha) and the term magnitude for one contact
+template <typename T>
+BB_HD void ls_contact(const T* c6, T alpha, T mu, T f1, T f2, const T* D, T& d1, T& d2, T& dm) {
+  const T x[3] = {c6[3], c6[4], c6[5]};
+  T jr[3] = {c6[0] + alpha * x[0], c6[1] + alpha * x[1], c6[2] + alpha * x[2]};
+  T f[3], Cc[6];
+  cone_eval(jr, mu, f1, f2, D, f, Cc);
+  const T fx = f[0] * x[0] + f[1] * x[1] + f[2] * x[2];
+  d1 -= fx;
+  dm += fabs(f[0] * x[0]) + fabs(f[1] * x[1]) + fabs(f[2] * x[2]);
+  d2 += Cc[0] * x[0] * x[0] + Cc[1] * x[1] * x[1] + Cc[2] * x[2] * x[2] +
+        2 * (Cc[3] * x[0] * x[1] + Cc[4] * x[0] * x[2] + Cc[5] * x[1] * x[2]);
+}
+
+// Newton on f(a) (mj_solNewton).  a: warm start in, qacc out (replicated in
+// every lane of the team).  Returns the iteration count (team-uniform).
+template <typename T>
+BB_HD int solve_team(const ModelT<T>& m, EnvWork<T>& W, const T* qfs, int ng, T* a, const Team& tm) {
+  const Mass<T>& M = W.M;
+  const T mu_w = m.fr_wheel[0], f1w = m.fr_wheel[0], f2w = m.fr_wheel[1];
+  const int nc = 3 + ng;
+  int it = 0;
+  for (; it < m.maxiter; it++) {
+    team_sync();
+    // ---- (1) contact pass: forces and cone Hessians, contact-parallel
+    T Hg[21], gg[6];
+#pragma unroll
+    for (int i = 0; i < 21; i++) Hg[i] = 0;
+#pragma unroll
+    for (int i = 0; i < 6; i++) gg[i] = 0;
+    for (int c = tm.tl; c < nc; c += tm.L) {
+      if (c < 3) {
+        const WheelCon<T>& C = W.wc[c];
+        T jar[3], f[3], Cc[6];
+#pragma unroll
+        for (int r = 0; r < 3; r++) jar[r] = wheel_dot(C, c, r, a) - C.aref[r];
+        T Dw[3] = {C.D[0], C.D[1], C.D[2]};
+        cone_eval(jar, mu_w, f1w, f2w, Dw, f, Cc);
+#pragma unroll
+        for (int r = 0; r < 3; r++) W.u.hes.wf[c][r] = f[r];
+        for (int i = 0; i < 13; i++) {
+          const T j0 = C.J[0][i], j1 = C.J[1][i], j2 = C.J[2][i];
+          W.u.hes.cj[c][0][i] = Cc[0] * j0 + Cc[3] * j1 + Cc[4] * j2;
+          W.u.hes.cj[c][1][i] = Cc[3] * j0 + Cc[1] * j1 + Cc[5] * j2;
+          W.u.hes.cj[c][2][i] = Cc[4] * j0 + Cc[5] * j1 + Cc[2] * j2;
+        }
+      } else {
+        const T* gc = W.g + (c - 3) * NGF;
+        T J[3][6];
+#pragma unroll
+        for (int r = 0; r < 3; r++)
+#pragma unroll
+          for (int i = 0; i < 6; i++) J[r][i] = gc[GF_J + 6 * r + i];
+        T jar[3];
+#pragma unroll
+        for (int r = 0; r < 3; r++)
+          jar[r] = J[r][0] * a[9] + J[r][1] * a[10] + J[r][2] * a[11] + J[r][3] * a[12] + J[r][4] * a[13] +
+                   J[r][5] * a[14] - gc[GF_AREF + r];
+        const T D = gc[GF_D];
+        T Dv[3] = {D, D, D}, f[3], Cc[6];
+        cone_eval(jar, T(1), T(1), T(1), Dv, f, Cc);
+        T w[3][6];
+#pragma unroll
+        for (int i = 0; i < 6; i++) {
+          gg[i] -= J[0][i] * f[0] + J[1][i] * f[1] + J[2][i] * f[2];
+          w[0][i] = Cc[0] * J[0][i] + Cc[3] * J[1][i] + Cc[4] * J[2][i];
+          w[1][i] = Cc[3] * J[0][i] + Cc[1] * J[1][i] + Cc[5] * J[2][i];
+          w[2][i] = Cc[4] * J[0][i] + Cc[5] * J[1][i] + Cc[2] * J[2][i];
+        }
+#pragma unroll
+        for (int i = 0; i < 6; i++)
+#pragma unroll
+          for (int j = 0; j <= i; j++) Hg[i * (i + 1) / 2 + j] += J[0][i] * w[0][j] + J[1][i] * w[1][j] + J[2][i] * w[2][j];
+      }
+    }
+    // ---- (2) reduce the ground partials across the team
+#pragma unroll
+    for (int i = 0; i < 21; i++) Hg[i] = team_sum(tm, Hg[i]);
+#pragma unroll
+    for (int i = 0; i < 6; i++) gg[i] = team_sum(tm, gg[i]);
+    if (tm.tl == 0) {
+#pragma unroll
+      for (int i = 0; i < 21; i++) W.u.hes.hg[i] = Hg[i];
+    }
+    team_sync();
+    // ---- (3) gradient, replicated: g = M a - qfs - sum_c J_c' f_c
+    T g[NV], Ma[NV];
+    mass_mul(M, a, Ma);
+#pragma unroll
+    for (int i = 0; i < NV; i++) g[i] = Ma[i] - qfs[i];
+#pragma unroll
+    for (int i = 0; i < 6; i++) g[9 + i] += gg[i];
+#pragma unroll
+    for (int w = 0; w < 3; w++) {
+      const T f0 = W.u.hes.wf[w][0], f1 = W.u.hes.wf[w][1], f2 = W.u.hes.wf[w][2];
+      const WheelCon<T>& C = W.wc[w];
+#pragma unroll
+      for (int i = 0; i < 13; i++) g[wheel_col(i, w)] -= C.J[0][i] * f0 + C.J[1][i] * f1 + C.J[2][i] * f2;
+    }
+    T gn = 0;
+#pragma unroll
+    for (int i = 0; i < NV; i++) gn += g[i] * g[i];
+#ifdef BB_SOLVE_TRACE
+    printf("it %d |g| %.3e\n", it, double(m.scale * sqrt(gn)));
+#endif
+    if (m.scale * sqrt(gn) < m.tol) break;
+    // ---- (4) Hessian entries, entry-parallel
+    for (int e = tm.tl; e < NH; e += tm.L) {
+      int i, j;
+      tri_unpack(e, i, j);
+      T h = mass_entry(M, i, j);
+#pragma unroll
+      for (int w = 0; w < 3; w++) {
+        const int pi = wheel_pos(i, w), pj = wheel_pos(j, w);
+        if (pi >= 0 && pj >= 0) {
+          const WheelCon<T>& C = W.wc[w];
+          h += C.J[0][pi] * W.u.hes.cj[w][0][pj] + C.J[1][pi] * W.u.hes.cj[w][1][pj] +
+               C.J[2][pi] * W.u.hes.cj[w][2][pj];
+        }
+      }
+      if (j >= 9) {
+        const int a9 = i - 9, b9 = j - 9;
+        h += W.u.hes.hg[a9 * (a9 + 1) / 2 + b9];
+      }
+      W.H[e] = h;
+      if (i == j) W.hd[i] = h;
+    }
+    // ---- (5) factorise, Newton direction (replicated triangular solves)
+    chol_team(W.H, W.hd, tm);
+    T s[NV];
+#pragma unroll
+    for (int i = 0; i < NV; i++) s[i] = -g[i];
+    chol_solve_packed(W.H, s);
+    T d0 = 0;
+    bool fin = true;
+#pragma unroll
+    for (int i = 0; i < NV; i++) { fin = fin && isfinite(s[i]); d0 += s[i] * g[i]; }
+    if (!fin || !(d0 < 0)) {
+      // roundoff-indefinite Hessian (fp32): diagonal Newton fallback
+      d0 = 0;
+#pragma unroll
+      for (int i = 0; i < NV; i++) {
+        const T hii = mass_entry(M, i, i);
+        s[i] = -g[i] / maxT(hii, T(1e-30));
+        d0 += s[i] * g[i];
+      }
+      if (!(d0 < 0)) break;
+    }
+    // ---- (6) exact line search on phi(alpha) = f(a + alpha s)
+    T Ms[NV];
+    mass_mul(M, s, Ms);
+    T sMs = 0, gs = 0;
+#pragma unroll
+    for (int i = 0; i < NV; i++) { sMs += s[i] * Ms[i]; gs += s[i] * (Ma[i] - qfs[i]); }
+    team_sync();  // hes buffers are dead; the line-search cache reuses them
+    for (int c = tm.tl; c < nc; c += tm.L) {
+      T* c6 = W.u.ls[c];
+      if (c < 3) {
+        const WheelCon<T>& C = W.wc[c];
+#pragma unroll
+        for (int r = 0; r < 3; r++) { c6[r] = wheel_dot(C, c, r, a) - C.aref[r]; c6[3 + r] = wheel_dot(C, c, r, s); }
+      } else {
+        const T* gc = W.g + (c - 3) * NGF;
+#pragma unroll
+        for (int r = 0; r < 3; r++) { c6[r] = ground_dot(gc, r, a) - gc[GF_AREF + r]; c6[3 + r] = ground_dot(gc, r, s); }
+      }
+    }
+    // 1-D Newton on phi'(alpha) from the full step, safeguarded by an
+    // Illinois false-position step on the bracket [lo, hi] (phi' is
+    // continuous and nondecreasing, but its slope jumps by ~1e6 when a stiff
+    // drive-direction row changes cone zone, where plain Newton creeps).
+    T lo = 0, dlo = d0, hi = -1, dhi = 0, alpha = 1;
+    T flo = d0, fhi = 0;  // Illinois-weighted end values
+    int side = 0, same = 0;
+    bool ls_ok = false;
+    for (int ls = 1; ls <= m.ls_maxiter; ls++) {
+      T d1p = 0, d2p = 0, dmp = 0;
+      for (int c = tm.tl; c < nc; c += tm.L) {
+        if (c < 3) {
+          const T Dw[3] = {W.wc[c].D[0], W.wc[c].D[1], W.wc[c].D[2]};
+          ls_contact(W.u.ls[c], alpha, mu_w, f1w, f2w, Dw, d1p, d2p, dmp);
+        } else {
+          const T D = W.g[(c - 3) * NGF + GF_D];
+          const T Dv[3] = {D, D, D};
+          ls_contact(W.u.ls[c], alpha, T(1), T(1), T(1), Dv, d1p, d2p, dmp);
+        }
+      }
+      const T d1 = gs + alpha * sMs + team_sum(tm, d1p);
+      const T d2 = sMs + team_sum(tm, d2p);
+      const T dmag = fabs(gs) + fabs(alpha * sMs) + team_sum(tm, dmp);
+      if (fabs(d1) <= m.ls_tol * fabs(d0) || fabs(d1) <= T(32) * eps_of<T>() * dmag) { ls_ok = true; break; }
+      if (!(d1 == d1)) break;
+      const int sd = d1 < 0 ? -1 : 1;
+      same = sd == side ? same + 1 : 0;
+      side = sd;
+      if (sd < 0) {
+        lo = alpha; dlo = d1; flo = d1;
+        if (same > 0 && hi >= 0) fhi *= T(0.5);
+      } else {
+        hi = alpha; dhi = d1; fhi = d1;
+        if (same > 0) flo *= T(0.5);
+      }
+      T an = alpha - d1 / maxT(d2, T(1e-30));
+      if (hi < 0) {
+        if (!(an > lo)) an = lo > 0 ? 2 * lo : T(1);
+      } else if (!(an > lo && an < hi) || same > 0) {
+        const T fp = lo - flo * (hi - lo) / (fhi - flo);
+        an = (fp > lo && fp < hi) ? fp : T(0.5) * (lo + hi);
+      }
+      alpha = an;
+    }
+    // an unconverged search falls back to the last point with phi' < 0 (a
+    // guaranteed decrease for convex phi)
+    if (!ls_ok) alpha = lo > 0 ? lo : (hi > 0 ? hi * dlo / (dlo - dhi) : T(0));
+#ifdef BB_SOLVE_TRACE
+    printf("   d0 %.3e alpha %.3e ls_ok %d lo %.3e hi %.3e dlo %.3e dhi %.3e\n", double(d0), double(alpha), int(ls_ok), double(lo), double(hi), double(dlo), double(dhi));
+#endif
+    if (!(alpha > 0)) break;
+    T sn = 0, an2 = 0;
+#pragma unroll
+    for (int i = 0; i < NV; i++) { a[i] += alpha * s[i]; sn += s[i] * s[i]; an2 += a[i] * a[i]; }
+    if (alpha * alpha * sn <= T(1e-30) + m.step_rel2 * (1 + an2)) { it++; break; }
+  }
+  return it;
+}
+
+}  // namespace bb

@@ -1,10 +1,10 @@
 // bb_step.h -- one env step = one BBotSimulation.step (ballbot_env.py:854-1036):
 //   action -> ctrl (:903-907), mj_step with RK4 (:912), _get_obs (:771-811),
 //   DirectionalReward + action penalty + survival bonus (:929-937, :1019),
-//   termination (:982-1017).  Per lane, templated on T (see bb_physics.h).
+//   termination (:982-1017).  Per env team of lanes, templated on T (see bb_physics.h).
 #pragma once
 
-#include "bb_physics.h"
+#include "bb_solve.h"
 
 namespace bb {
 
@@ -31,34 +31,29 @@ struct StageOut {
   int ng, iters, overflow;
 };
 
-// mj_forward for this model: returns qacc in acc (acc holds the warm start on entry).
+// mj_forward for this model: returns qacc in acc (acc holds the warm start on
+// entry).  Executed by a team of tm.L lanes; the pre-phase (kinematics, mass,
+// bias, collision) is computed redundantly by every lane of the team, the
+// constraint solve is team-parallel (bb_solve.h).
 template <typename T>
 BB_HD int forward(const ModelT<T>& m, const T* q, const T* v, const T* ctrl, T* acc, const float* hf, T size_z,
-                  EnvWork<T>& W, StageOut<T>* so) {
-  Kin<T>& k = W.k;
+                  EnvWork<T>& W, StageOut<T>* so, const Team& tm) {
+  team_sync();  // previous users of the workspace are done
+  Kin<T>& k = W.u.pre.k;
   kinematics(m, q, k);
   Mass<T>& M = W.M;
-  build_mass(m, k, M, W.Iw);
+  build_mass(m, k, M, W.u.pre.Iw);
   T qfs[NV];
-  bias_forces(m, k, W.Iw, v, qfs);
+  bias_forces(m, k, W.u.pre.Iw, v, qfs);
 #pragma unroll
   for (int i = 0; i < NV; i++) qfs[i] = -qfs[i];
 #pragma unroll
   for (int w = 0; w < 3; w++) qfs[6 + w] += -m.damping * v[6 + w] + ctrl[w];
-  WheelCon<T>* WC = W.wc;
 #pragma unroll
-  for (int w = 0; w < 3; w++) wheel_contact(m, k, v, w, WC[w]);
+  for (int w = 0; w < 3; w++) wheel_contact(m, k, v, w, W.wc[w]);
   const GStore<T> st{W.g, 1};
   int overflow = 0;
   int ng = hf ? collide_ground(m, k, v, hf, size_z, st, &overflow) : 0;
-  bool ok = true;
-#pragma unroll
-  for (int i = 0; i < NV; i++) ok = ok && isfinite(acc[i]);
-  if (!ok) {
-#pragma unroll
-    for (int i = 0; i < NV; i++) acc[i] = 0;
-  }
-  int it = solve(m, M, qfs, WC, ng, st, W.H, acc);
   if (so) {
     T qb[4] = {q[3], q[4], q[5], q[6]};
     qnormalize(qb);
@@ -70,8 +65,17 @@ BB_HD int forward(const ModelT<T>& m, const T* q, const T* v, const T* ctrl, T* 
     cross3(t, so->w_world, cw);
     so->v_com[0] = v[0] + t[0]; so->v_com[1] = v[1] + t[1]; so->v_com[2] = v[2] + t[2];
     so->pb[0] = q[0]; so->pb[1] = q[1]; so->pb[2] = q[2];
-    so->ng = ng; so->iters = it; so->overflow = overflow;
+    so->ng = ng; so->overflow = overflow;
   }
+  bool ok = true;
+#pragma unroll
+  for (int i = 0; i < NV; i++) ok = ok && isfinite(acc[i]);
+  if (!ok) {
+#pragma unroll
+    for (int i = 0; i < NV; i++) acc[i] = 0;
+  }
+  const int it = solve_team(m, W, qfs, ng, acc, tm);
+  if (so) so->iters = it;
   return it;
 }
 
@@ -79,44 +83,39 @@ BB_HD int forward(const ModelT<T>& m, const T* q, const T* v, const T* ctrl, T* 
 // warm: qacc_warmstart (each stage's constraint solve saves its qacc).
 template <typename T>
 BB_HD int rk4_step(const ModelT<T>& m, T* q, T* v, T* warm, const T* ctrl, const float* hf, T size_z,
-                   EnvWork<T>& W, StageOut<T>& so) {
+                   EnvWork<T>& W, StageOut<T>& so, const Team& tm) {
   const T h = m.h;
+  // the RK context lives in the workspace (written identically by every
+  // lane of the team); only the stage state and the warm start are in registers
   T* q0 = W.q0;
   T* v0 = W.v0;
   T* vs = W.vs;
   T* as = W.as;
   T* vp = W.vp;
+  team_sync();
 #pragma unroll
   for (int i = 0; i < NQ; i++) q0[i] = q[i];
 #pragma unroll
   for (int i = 0; i < NV; i++) v0[i] = v[i];
-  (void)vp;
-  // one call site for forward (keeps a single inlined copy of the solver);
-  // the stage state lives in the workspace so nothing but the warm start is
-  // register-resident across the solve
-  T* qi = W.qi;
-  T* vi = W.vi;
   int iters = 0;
 #pragma unroll 1
   for (int stage = 0; stage < 4; stage++) {
-    const T a = stage == 3 ? T(1) : T(0.5);                            // RK4 Butcher A (sub-diagonal)
-    if (stage == 0) {
+    const T a = stage == 3 ? T(1) : T(0.5);  // RK4 Butcher A (sub-diagonal)
+    T qi[NQ], vi[NV];
 #pragma unroll
-      for (int i = 0; i < NQ; i++) qi[i] = q0[i];
+    for (int i = 0; i < NQ; i++) qi[i] = q0[i];
+    if (stage == 0) {
 #pragma unroll
       for (int i = 0; i < NV; i++) vi[i] = v0[i];
     } else {
-      T qq[NQ], dv[NV];
-#pragma unroll
-      for (int i = 0; i < NQ; i++) qq[i] = q0[i];
+      T dv[NV];
 #pragma unroll
       for (int i = 0; i < NV; i++) { dv[i] = a * vp[i]; vi[i] = v0[i] + h * a * warm[i]; }
-      integrate_pos(qq, dv, h);
-#pragma unroll
-      for (int i = 0; i < NQ; i++) qi[i] = qq[i];
+      integrate_pos(qi, dv, h);
     }
-    iters += forward(m, qi, vi, ctrl, warm, hf, size_z, W, stage == 3 ? &so : (StageOut<T>*)nullptr);
+    iters += forward(m, qi, vi, ctrl, warm, hf, size_z, W, stage == 3 ? &so : (StageOut<T>*)nullptr, tm);
     const T b = (stage == 0 || stage == 3) ? T(1.0 / 6) : T(1.0 / 3);  // RK4 weights B
+    team_sync();
     if (stage == 0) {
 #pragma unroll
       for (int i = 0; i < NV; i++) { vs[i] = b * vi[i]; as[i] = b * warm[i]; vp[i] = vi[i]; }
@@ -125,12 +124,16 @@ BB_HD int rk4_step(const ModelT<T>& m, T* q, T* v, T* warm, const T* ctrl, const
       for (int i = 0; i < NV; i++) { vs[i] += b * vi[i]; as[i] += b * warm[i]; vp[i] = vi[i]; }
     }
   }
+  team_sync();
   // mj_advance: qvel = v0 + h*qacc_rk ; qpos = q0 (+) h*v_rk
 #pragma unroll
   for (int i = 0; i < NV; i++) v[i] = v0[i] + h * as[i];
 #pragma unroll
   for (int i = 0; i < NQ; i++) q[i] = q0[i];
-  integrate_pos(q, vs, h);
+  T vv[NV];
+#pragma unroll
+  for (int i = 0; i < NV; i++) vv[i] = vs[i];
+  integrate_pos(q, vv, h);
   return iters;
 }
 
@@ -168,13 +171,13 @@ constexpr int F_TERMINATED = 1, F_FAILURE = 2, F_DIVERGED = 4, F_OVERFLOW = 8;
 template <typename T>
 BB_HD int env_step(const ModelT<T>& m, const EnvCfg& cfg, T* q, T* v, T* warm, int& step, const float* action,
                    const float* hf, T size_z, EnvWork<T>& W, float* obs15, float& reward, float* pos2d,
-                   int* iters) {
+                   int* iters, const Team& tm) {
   const float mwv = cfg.max_wheel_velocity;
   T ctrl[3];
 #pragma unroll
   for (int i = 0; i < 3; i++) ctrl[i] = -T(clipf(action[i] * mwv, -mwv, mwv));  // data.ctrl[:] = -ctrl
   StageOut<T> so;
-  int it = rk4_step(m, q, v, warm, ctrl, hf, size_z, W, so);
+  int it = rk4_step(m, q, v, warm, ctrl, hf, size_z, W, so, tm);
   if (iters) *iters = it;
   int flags = state_bad(q, v) ? F_DIVERGED : 0;
   if (so.overflow) flags |= F_OVERFLOW;

@@ -29,7 +29,7 @@ static int fwd(const double* q, const double* v, const double* ctrl, double* acc
   for (int i = 0; i < 3; i++) cc[i] = T(ctrl[i]);
   static EnvWork<T> W;
   StageOut<T> so;
-  int it = forward(m, qq, vv, cc, aa, hf, T(size_z), W, &so);
+  int it = forward(m, qq, vv, cc, aa, hf, T(size_z), W, &so, Team{1, 0});
   for (int i = 0; i < NV; i++) acc[i] = double(aa[i]);
   if (extra) {
     extra[0] = so.ng; extra[1] = so.iters; extra[2] = so.overflow;
@@ -47,7 +47,7 @@ static int envstep(const EnvCfg* cfg, double* q, double* v, double* w, int* step
   for (int i = 0; i < NV; i++) { vv[i] = T(v[i]); ww[i] = T(w[i]); }
   static EnvWork<T> W;
   int it = 0;
-  int fl = env_step(m, *cfg, qq, vv, ww, *step, a, hf, T(size_z), W, obs, *rew, pos2d, &it);
+  int fl = env_step(m, *cfg, qq, vv, ww, *step, a, hf, T(size_z), W, obs, *rew, pos2d, &it, Team{1, 0});
   for (int i = 0; i < NQ; i++) q[i] = double(qq[i]);
   for (int i = 0; i < NV; i++) { v[i] = double(vv[i]); w[i] = double(ww[i]); }
   return fl | (it << 8);

@@ -38,7 +38,7 @@ void run(const char* path, int fp64) {
     int ov = 0;
     int ng = collide_ground(m, k, v, hf.data(), T(2.0), st, &ov);
     auto t3 = clk::now();
-    int it = solve(m, M, qfs, WC, ng, st, EW.H, a);
+    int it = solve_team(m, EW, qfs, ng, a, Team{1, 0});
     auto t4 = clk::now();
     tk += std::chrono::duration<double>(t1 - t0).count(); tw += std::chrono::duration<double>(t2 - t1).count();
     tc += std::chrono::duration<double>(t3 - t2).count(); ts += std::chrono::duration<double>(t4 - t3).count();

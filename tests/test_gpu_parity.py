@@ -7,7 +7,7 @@ fp64 kernel (the default): every env-step within qpos 1e-9, qvel 1e-6, obs 1e-6,
 reward 1e-7 (the solver stops at MuJoCo's own tolerance, 1e-8 scaled gradient).
 
 fp32 kernel: qpos 1e-5, qvel 1e-3, obs 1e-4, reward 1e-6 for
-at least 99.5% of env-steps; the rest must stay below qvel 0.2.  The residual
+at least 99.9% of env-steps; the rest must stay below qvel 1e-2.  Residual
 fp32 outliers are states where a wheel contact's drive-direction row (R scaled
 by (0.001/1.0)^2, ballbot.xml:90-92) makes the Newton Hessian ~1e10
 ill-conditioned for float arithmetic; DESIGN.md §fp32 documents them.
@@ -18,7 +18,7 @@ import pytest
 torch = pytest.importorskip("torch")
 pytestmark = pytest.mark.gpu
 
-TOL = {"fp32": dict(q=1e-5, v=1e-3, obs=1e-4, r=1e-6, frac=0.995, vmax=0.2),
+TOL = {"fp32": dict(q=1e-5, v=1e-3, obs=1e-4, r=1e-6, frac=0.999, vmax=1e-2),
        "fp64": dict(q=1e-9, v=1e-6, obs=1e-6, r=1e-7, frac=1.0, vmax=1e-6)}
 
 
@@ -78,7 +78,7 @@ def test_native_library_loads():
     from ballbot_gym import _native
 
     L = _native.lib()
-    assert L.bb_abi_version() == 1
+    assert L.bb_abi_version() == _native.ABI_VERSION
 
 
 @pytest.mark.parametrize("precision", ["fp32", "fp64"])
