@@ -74,8 +74,8 @@ def cpu_baseline(seconds: float = 12.0) -> dict:
 def main() -> None:
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=300)
-    ap.add_argument("--warmup", type=int, default=30)
+    ap.add_argument("--steps", type=int, default=500)
+    ap.add_argument("--warmup", type=int, default=300)
     ap.add_argument("--envs", type=int, default=4096, help="envs per GPU")
     ap.add_argument("--precision", default="fp64", choices=["fp32", "fp64"])
     ap.add_argument("--terrain", default="flat")
@@ -138,8 +138,8 @@ def main() -> None:
         tj = Path(args.traffic_json)
         if tj.exists():
             try:
-                tr = json.loads(tj.read_text())
-                if tr.get("precision") == args.precision and tr.get("envs") == n:
+                tr = json.loads(tj.read_text()).get(args.precision) or {}
+                if tr.get("envs") == n and tr.get("terrain", "flat") == args.terrain:
                     traffic = tr.get("bytes_per_launch")
             except Exception:
                 traffic = None

@@ -73,16 +73,27 @@ def build(force: bool = False, verbose: bool = False) -> Path:
 
 
 def lib():
+    """The product library (csrc/bb_kernels.hip built for gfx950); raises if absent."""
     global _lib
-    if _lib is not None:
-        return _lib
-    if not LIB_PATH.exists():
+    if _lib is None:
+        _lib = _load(LIB_PATH)
+    return _lib
+
+
+def use_diagnostic_library(path) -> None:
+    """Load an instrumented build of the same sources (tools/ only, e.g. -DBB_PHASE_CLOCKS)."""
+    global _lib
+    _lib = _load(Path(path))
+
+
+def _load(path: Path):
+    if not path.exists():
         raise NativeLibraryError(
-            f"HIP library {LIB_PATH} not found; run __graft_entry__.build() (hipcc --offload-arch=gfx950)")
+            f"HIP library {path} not found; run __graft_entry__.build() (hipcc --offload-arch=gfx950)")
     try:
-        L = C.CDLL(str(LIB_PATH))
+        L = C.CDLL(str(path))
     except OSError as e:  # pragma: no cover - depends on the box
-        raise NativeLibraryError(f"cannot load {LIB_PATH}: {e}") from e
+        raise NativeLibraryError(f"cannot load {path}: {e}") from e
     vp, fp, dp = C.c_void_p, C.POINTER(C.c_float), C.POINTER(C.c_double)
     L.bb_abi_version.restype = C.c_int
     L.bb_last_error.argtypes = [C.c_char_p, C.c_int]
@@ -104,7 +115,6 @@ def lib():
         getattr(L, name).restype = C.c_int
     if L.bb_abi_version() != ABI_VERSION:
         raise NativeLibraryError("ABI version mismatch")
-    _lib = L
     return L
 
 

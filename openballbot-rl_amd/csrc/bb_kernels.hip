@@ -24,6 +24,10 @@
 
 using namespace bb;
 
+#ifdef BB_PHASE_CLOCKS
+namespace bb { __device__ unsigned long long bb_phase_cycles[16]; }
+#endif
+
 namespace {
 
 constexpr int WAVE = 64;
@@ -507,6 +511,17 @@ int bb_get_config(bb_handle* h, int32_t* out5) {
   out5[4] = h->team;
   return 0;
 }
+
+#ifdef BB_PHASE_CLOCKS
+// diagnostic build only: read and clear the per-phase cycle counters
+int bb_debug_phase_cycles(unsigned long long* out16) {
+  HIPCHK(hipDeviceSynchronize());
+  HIPCHK(hipMemcpyFromSymbol(out16, HIP_SYMBOL(bb::bb_phase_cycles), sizeof(unsigned long long) * 16));
+  unsigned long long z[16] = {0};
+  HIPCHK(hipMemcpyToSymbol(HIP_SYMBOL(bb::bb_phase_cycles), z, sizeof z));
+  return 0;
+}
+#endif
 
 int bb_get_offsets(bb_handle* h, float* out) {
   if (!h || !out) return fail("bb_get_offsets: NULL argument");

@@ -18,6 +18,23 @@
 
 namespace bb {
 
+#ifdef BB_SOLVE_STATS
+static long g_ls_evals = 0;
+#endif
+
+// Diagnostic build only (-DBB_PHASE_CLOCKS): per-phase s_memtime cycles,
+// summed over teams into bb_phase_cycles[] (read back by tools/phase_clocks).
+#if defined(BB_PHASE_CLOCKS) && defined(__HIP_DEVICE_COMPILE__)
+extern __device__ unsigned long long bb_phase_cycles[16];
+#define PH_DECL unsigned long long ph_t = clock64(), ph_acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+#define PH(k) { unsigned long long n_ = clock64(); ph_acc[k] += n_ - ph_t; ph_t = n_; }
+#define PH_FLUSH(tm) if ((tm).tl == 0) { for (int k_ = 0; k_ < 8; k_++) atomicAdd(&bb_phase_cycles[k_], ph_acc[k_]); }
+#else
+#define PH_DECL
+#define PH(k)
+#define PH_FLUSH(tm)
+#endif
+
 struct Team {
   int L;   // lanes per env (power of two, <= 64)
   int tl;  // this lane's index inside the team
@@ -160,6 +177,7 @@ BB_HD void ls_contact(const T* c6, T alpha, T mu, T f1, T f2, const T* D, T& d1,
 template <typename T>
 BB_HD int solve_team(const ModelT<T>& m, EnvWork<T>& W, const T* qfs, int ng, T* a, const Team& tm) {
   const Mass<T>& M = W.M;
+  PH_DECL
   const T mu_w = m.fr_wheel[0], f1w = m.fr_wheel[0], f2w = m.fr_wheel[1];
   const int nc = 3 + ng;
   int it = 0;
@@ -216,6 +234,7 @@ BB_HD int solve_team(const ModelT<T>& m, EnvWork<T>& W, const T* qfs, int ng, T*
           for (int j = 0; j <= i; j++) Hg[i * (i + 1) / 2 + j] += J[0][i] * w[0][j] + J[1][i] * w[1][j] + J[2][i] * w[2][j];
       }
     }
+    PH(0)
     // ---- (2) reduce the ground partials across the team
 #pragma unroll
     for (int i = 0; i < 21; i++) Hg[i] = team_sum(tm, Hg[i]);
@@ -226,6 +245,7 @@ BB_HD int solve_team(const ModelT<T>& m, EnvWork<T>& W, const T* qfs, int ng, T*
       for (int i = 0; i < 21; i++) W.u.hes.hg[i] = Hg[i];
     }
     team_sync();
+    PH(1)
     // ---- (3) gradient, replicated: g = M a - qfs - sum_c J_c' f_c
     T g[NV], Ma[NV];
     mass_mul(M, a, Ma);
@@ -247,6 +267,7 @@ BB_HD int solve_team(const ModelT<T>& m, EnvWork<T>& W, const T* qfs, int ng, T*
     printf("it %d |g| %.3e\n", it, double(m.scale * sqrt(gn)));
 #endif
     if (m.scale * sqrt(gn) < m.tol) break;
+    PH(2)
     // ---- (4) Hessian entries, entry-parallel
     for (int e = tm.tl; e < NH; e += tm.L) {
       int i, j;
@@ -268,8 +289,10 @@ BB_HD int solve_team(const ModelT<T>& m, EnvWork<T>& W, const T* qfs, int ng, T*
       W.H[e] = h;
       if (i == j) W.hd[i] = h;
     }
+    PH(3)
     // ---- (5) factorise, Newton direction (replicated triangular solves)
     chol_team(W.H, W.hd, tm);
+    PH(4)
     T s[NV];
 #pragma unroll
     for (int i = 0; i < NV; i++) s[i] = -g[i];
@@ -289,6 +312,7 @@ BB_HD int solve_team(const ModelT<T>& m, EnvWork<T>& W, const T* qfs, int ng, T*
       }
       if (!(d0 < 0)) break;
     }
+    PH(5)
     // ---- (6) exact line search on phi(alpha) = f(a + alpha s)
     T Ms[NV];
     mass_mul(M, s, Ms);
@@ -317,6 +341,9 @@ BB_HD int solve_team(const ModelT<T>& m, EnvWork<T>& W, const T* qfs, int ng, T*
     int side = 0, same = 0;
     bool ls_ok = false;
     for (int ls = 1; ls <= m.ls_maxiter; ls++) {
+#ifdef BB_SOLVE_STATS
+      g_ls_evals++;
+#endif
       T d1p = 0, d2p = 0, dmp = 0;
       for (int c = tm.tl; c < nc; c += tm.L) {
         if (c < 3) {
@@ -362,8 +389,11 @@ BB_HD int solve_team(const ModelT<T>& m, EnvWork<T>& W, const T* qfs, int ng, T*
     T sn = 0, an2 = 0;
 #pragma unroll
     for (int i = 0; i < NV; i++) { a[i] += alpha * s[i]; sn += s[i] * s[i]; an2 += a[i] * a[i]; }
+    PH(6)
     if (alpha * alpha * sn <= T(1e-30) + m.step_rel2 * (1 + an2)) { it++; break; }
   }
+  PH(7)
+  PH_FLUSH(tm)
   return it;
 }
 

@@ -39,6 +39,9 @@ template <typename T>
 BB_HD int forward(const ModelT<T>& m, const T* q, const T* v, const T* ctrl, T* acc, const float* hf, T size_z,
                   EnvWork<T>& W, StageOut<T>* so, const Team& tm) {
   team_sync();  // previous users of the workspace are done
+#if defined(BB_PHASE_CLOCKS) && defined(__HIP_DEVICE_COMPILE__)
+  const unsigned long long f_t0 = clock64();
+#endif
   Kin<T>& k = W.u.pre.k;
   kinematics(m, q, k);
   Mass<T>& M = W.M;
@@ -53,7 +56,18 @@ BB_HD int forward(const ModelT<T>& m, const T* q, const T* v, const T* ctrl, T* 
   for (int w = 0; w < 3; w++) wheel_contact(m, k, v, w, W.wc[w]);
   const GStore<T> st{W.g, 1};
   int overflow = 0;
+#if defined(BB_PHASE_CLOCKS) && defined(__HIP_DEVICE_COMPILE__)
+  const unsigned long long f_t1 = clock64();
+#endif
   int ng = hf ? collide_ground(m, k, v, hf, size_z, st, &overflow) : 0;
+#if defined(BB_PHASE_CLOCKS) && defined(__HIP_DEVICE_COMPILE__)
+  if (tm.tl == 0) {
+    const unsigned long long f_t2 = clock64();
+    atomicAdd(&bb_phase_cycles[8], f_t1 - f_t0);
+    atomicAdd(&bb_phase_cycles[9], f_t2 - f_t1);
+    atomicAdd(&bb_phase_cycles[10], 1ull);
+  }
+#endif
   if (so) {
     T qb[4] = {q[3], q[4], q[5], q[6]};
     qnormalize(qb);

@@ -45,6 +45,9 @@ void run(const char* path, int fp64) {
     iters += it; ngs += ng;
   }
   n *= 3;
+#ifdef BB_SOLVE_STATS
+  printf("ls evals per newton iter %.2f\n", double(g_ls_evals) / iters); g_ls_evals = 0;
+#endif
   printf("fp64=%d per forward: kin+mass+bias %.2f us, wheel %.2f us, collide %.2f us, solve %.2f us (iters %.2f, ng %.2f)\n",
          fp64, tk / n * 1e6, tw / n * 1e6, tc / n * 1e6, ts / n * 1e6, double(iters) / n, double(ngs) / n);
 }

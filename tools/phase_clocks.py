@@ -1,0 +1,61 @@
+"""Per-phase GPU cycle breakdown of the step kernel (diagnostic, GPU box).
+
+Builds csrc/bb_kernels.hip with -DBB_PHASE_CLOCKS into tools/_build, runs the
+bench workload (4096 envs, flat, random actions) and prints s_memtime cycles
+per phase summed over teams, normalised per forward and per Newton iteration.
+"""
+import argparse
+import ctypes as C
+import json
+import subprocess
+import sys
+from pathlib import Path
+
+ROOT = Path(__file__).resolve().parents[1]
+sys.path.insert(0, str(ROOT / "openballbot-rl_amd"))
+LIB = ROOT / "tools" / "_build" / "libbb_phase.so"
+NAMES = ["contact_pass", "reduce", "gradient", "hessian", "cholesky", "direction", "line_search", "exit",
+         "kin_mass_bias_wheel", "collide", "forwards"]
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--precision", default="fp64")
+    ap.add_argument("--steps", type=int, default=100)
+    ap.add_argument("--warmup", type=int, default=300)
+    ap.add_argument("--build", action="store_true")
+    a = ap.parse_args()
+    if a.build or not LIB.exists():
+        LIB.parent.mkdir(parents=True, exist_ok=True)
+        subprocess.run(["hipcc", "--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC", "-shared", "-DBB_PHASE_CLOCKS",
+                        "-o", str(LIB), str(ROOT / "openballbot-rl_amd" / "csrc" / "bb_kernels.hip")], check=True)
+    import torch
+    from ballbot_gym import _native
+    _native.use_diagnostic_library(LIB)
+    L = _native.lib()
+    L.bb_debug_phase_cycles.argtypes = [C.POINTER(C.c_ulonglong)]
+    from ballbot_gym.envs import BallbotVecEnv
+    env = BallbotVecEnv(4096, device="cuda:0", precision=a.precision)
+    pool = torch.rand(64, 4096, 3, device="cuda:0") * 2 - 1
+    out = (C.c_ulonglong * 16)()
+    for i in range(a.warmup):
+        env.step_async_raw(pool[i % 64])
+    torch.cuda.synchronize()
+    L.bb_debug_phase_cycles(out)
+    s0 = env.stats()
+    for i in range(a.steps):
+        env.step_async_raw(pool[i % 64])
+    torch.cuda.synchronize()
+    L.bb_debug_phase_cycles(out)
+    s1 = env.stats()
+    iters = s1["solver_iters"] - s0["solver_iters"]
+    fw = out[10]
+    res = {"precision": a.precision, "forwards": fw, "newton_iters": iters,
+           "cycles_per_forward": {NAMES[k]: out[k] / fw for k in range(10)},
+           "cycles_per_newton_iter": {NAMES[k]: out[k] / max(iters, 1) for k in range(8)}}
+    res["total_cycles_per_forward"] = sum(out[k] for k in range(10)) / fw
+    print(json.dumps(res, indent=1))
+
+
+if __name__ == "__main__":
+    main()

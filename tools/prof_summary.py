@@ -1,0 +1,85 @@
+"""Summarise tools/profile.sh output into profiles/ (tracked).
+
+  python tools/prof_summary.py gpurun_out/prof_r01_fp64 profiles/r01_fp64 --timed 300
+
+Writes <dst>_kernel_stats.csv (rocprofv3 --stats, verbatim), <dst>_summary.json
+(average step_kernel duration over the timed dispatches, PMC per launch) and,
+with --traffic, updates profiles/traffic.json (read by bench.py for
+roofline.traffic).  FETCH_SIZE is doubled per MI355X_MICROARCH.md (gfx950
+reports half the bytes of wide coalesced reads); WRITE_SIZE is taken as is.
+"""
+import argparse
+import csv
+import json
+import shutil
+from pathlib import Path
+
+KERNEL = "step_kernel"
+
+
+def rows(p):
+    with open(p) as f:
+        return list(csv.DictReader(f))
+
+
+def counters(p, names, last):
+    per = {}
+    for r in rows(p):
+        if KERNEL not in r["Kernel_Name"]:
+            continue
+        d = per.setdefault(int(r["Dispatch_Id"]), {})
+        d[r["Counter_Name"]] = d.get(r["Counter_Name"], 0.0) + float(r["Counter_Value"])
+    ids = sorted(per)[-last:]
+    return {n: sum(per[i].get(n, 0.0) for i in ids) / len(ids) for n in names}, len(ids)
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("src")
+    ap.add_argument("dst")
+    ap.add_argument("--timed", type=int, default=300, help="timed step_kernel dispatches at the end of the trace run")
+    ap.add_argument("--pmc-last", type=int, default=20)
+    ap.add_argument("--traffic", action="store_true")
+    a = ap.parse_args()
+    src, dst = Path(a.src), Path(a.dst)
+    dst.parent.mkdir(parents=True, exist_ok=True)
+    shutil.copy(src / "trace" / "run_kernel_stats.csv", str(dst) + "_kernel_stats.csv")
+    tr = [r for r in rows(src / "trace" / "run_kernel_trace.csv") if KERNEL in r["Kernel_Name"]]
+    tr.sort(key=lambda r: int(r["Start_Timestamp"]))
+    timed = tr[-a.timed:]
+    durs = [(int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) * 1e-6 for r in timed]
+    bench = json.loads((src / "bench_trace.json").read_text())
+    out = {
+        "kernel": timed[0]["Kernel_Name"],
+        "timed_dispatches": len(timed),
+        "avg_ms_rocprof": sum(durs) / len(durs),
+        "min_ms": min(durs), "max_ms": max(durs),
+        "bench_kernel_ms_hip_events": bench["roofline"]["kernel_ms"],
+        "bench_value": bench["value"],
+        "bench_config": bench["config"],
+        "vgpr": timed[0].get("VGPR_Count"), "agpr": timed[0].get("Accum_VGPR_Count"),
+        "sgpr": timed[0].get("SGPR_Count"), "lds": timed[0].get("LDS_Block_Size"),
+        "scratch": timed[0].get("Scratch_Size"),
+    }
+    f, nf = counters(src / "fetch" / "run_counter_collection.csv", ["FETCH_SIZE"], a.pmc_last)
+    w, nw = counters(src / "write" / "run_counter_collection.csv", ["WRITE_SIZE"], a.pmc_last)
+    sqn = ["SQ_WAVES", "SQ_INSTS_VALU", "SQ_INSTS_SALU", "SQ_INSTS_LDS", "SQ_WAIT_ANY", "SQ_WAIT_INST_ANY",
+           "SQ_ACTIVE_INST_ANY", "SQ_WAVE_CYCLES"]
+    sq, ns = counters(src / "sq" / "run_counter_collection.csv", sqn, a.pmc_last)
+    fetch_b = f["FETCH_SIZE"] * 1024 * 2  # KiB -> B, x2 gfx950 correction
+    write_b = w["WRITE_SIZE"] * 1024
+    out["pmc"] = {"dispatches_averaged": min(nf, nw, ns), "FETCH_SIZE_kib_raw": f["FETCH_SIZE"],
+                  "WRITE_SIZE_kib": w["WRITE_SIZE"], "hbm_bytes_per_launch": fetch_b + write_b, **sq}
+    (Path(str(dst) + "_summary.json")).write_text(json.dumps(out, indent=1))
+    print(json.dumps(out, indent=1))
+    if a.traffic:
+        tj = dst.parent / "traffic.json"
+        cur = json.loads(tj.read_text()) if tj.exists() else {}
+        prec = bench["config"]["precision"]
+        cur[prec] = {"precision": prec, "envs": bench["config"]["envs_per_gpu"],
+                     "bytes_per_launch": fetch_b + write_b, "source": str(dst) + "_summary.json"}
+        tj.write_text(json.dumps(cur, indent=1))
+
+
+if __name__ == "__main__":
+    main()
