@@ -97,10 +97,12 @@ def main() -> None:
     dev = torch.device("cuda", local)
     torch.cuda.set_device(dev)
 
+    from ballbot_gym.distributed import env_shard, max_over_ranks, rank_seed
     from ballbot_gym.envs import BallbotVecEnv
 
-    n = args.envs
-    env = BallbotVecEnv(n, device=dev, precision=args.precision, seed=1000 + rank,
+    # weak scaling: every rank owns a contiguous block of `--envs` global env ids
+    first_env, n = env_shard(args.envs * world, rank, world)
+    env = BallbotVecEnv(n, device=dev, precision=args.precision, seed=rank_seed(1000, first_env),
                         terrain_config={"type": args.terrain, "config": {}})
     g = torch.Generator(device=dev).manual_seed(1234 + rank)
     pool = torch.rand(64, n, 3, generator=g, device=dev) * 2 - 1  # random actions resident in HBM
@@ -122,10 +124,7 @@ def main() -> None:
     torch.cuda.synchronize()
     elapsed = time.perf_counter() - t0
     kern_ms = ev0.elapsed_time(ev1) / args.steps  # one step kernel per step, on the env's stream
-    t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
-    if world > 1:
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-    elapsed = float(t.item())
+    elapsed = max_over_ranks(elapsed, device=dev)
     stats = env.stats()
     launch = env.launch_config()
 

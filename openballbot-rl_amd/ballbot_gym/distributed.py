@@ -1,0 +1,50 @@
+"""Multi-GPU layout of the batched env.
+
+Envs are independent: N_total envs are split into contiguous blocks, one per
+rank (one process per GPU), with no collective on the step path.  The global
+env id fixes the seed stream, so a rollout is the same whatever the world
+size.  Collectives exist only at boundaries: the max-over-ranks timing of the
+benchmark and the gather of rollout buffers at a PPO update.
+"""
+from __future__ import annotations
+
+from typing import Tuple
+
+import torch
+import torch.distributed as dist
+
+
+def env_shard(num_envs_total: int, rank: int, world: int) -> Tuple[int, int]:
+    """(first global env id, count) of `rank`'s block; blocks differ by at most 1."""
+    if world < 1 or not 0 <= rank < world:
+        raise ValueError(f"bad rank/world {rank}/{world}")
+    if num_envs_total < world:
+        raise ValueError(f"{num_envs_total} envs cannot be split over {world} ranks")
+    base, extra = divmod(num_envs_total, world)
+    start = rank * base + min(rank, extra)
+    return start, base + (1 if rank < extra else 0)
+
+
+def rank_seed(seed: int, first_env: int) -> int:
+    """Seed of a rank's env block: offset by its first global env id."""
+    return int(seed) + int(first_env)
+
+
+def max_over_ranks(value: float, device=None) -> float:
+    """All-reduce MAX of a scalar (elapsed time); identity without a process group."""
+    if not (dist.is_available() and dist.is_initialized()) or dist.get_world_size() == 1:
+        return float(value)
+    t = torch.tensor([float(value)], dtype=torch.float64, device=device)
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    return float(t.item())
+
+
+def gather_rollouts(buf: torch.Tensor, dst: int = 0):
+    """Gather equally-shaped per-rank rollout buffers [T, n_local, ...] onto `dst`
+    (concatenated along the env axis); other ranks get None."""
+    if not (dist.is_available() and dist.is_initialized()) or dist.get_world_size() == 1:
+        return buf
+    world = dist.get_world_size()
+    parts = [torch.empty_like(buf) for _ in range(world)] if dist.get_rank() == dst else None
+    dist.gather(buf.contiguous(), parts, dst=dst)
+    return torch.cat(parts, dim=1) if parts is not None else None

@@ -46,9 +46,7 @@ class BallbotVecEnv:
         n_terrains: Optional[int] = None,
         auto_reset: bool = True,
     ):
-        from ..core.factories import create_reward
-        from ..rewards.directional import DirectionalReward
-        from ..rewards.distance import DistanceReward
+        from .config import params_from_configs, terrain_bank
 
         if not torch.cuda.is_available():
             raise RuntimeError("BallbotVecEnv needs a ROCm GPU (torch.cuda.is_available() is False)")
@@ -59,36 +57,12 @@ class BallbotVecEnv:
         self.auto_reset = bool(auto_reset)
         self.terrain_config = terrain_config or {"type": "flat", "config": {}}
         self.reward_config = reward_config or {"type": "directional", "config": {"target_direction": [0.0, 1.0]}}
-        env_settings = (env_config or {}).get("env", {})
-        self.max_ep_steps = int(env_settings.get("max_ep_steps", max_ep_steps if max_ep_steps is not None else 4000))
-        rcfg = self.reward_config.get("config", {})
-
-        p = N.default_params()
-        p.max_ep_steps = self.max_ep_steps
-        p.max_allowed_tilt = float(env_settings.get("max_allowed_tilt", 20.0))
-        p.max_wheel_velocity = float(env_settings.get("max_wheel_velocity", 10.0))
-        p.reward_scale = float(rcfg.get("scale", 0.01))
-        p.action_reg_coef = float(rcfg.get("action_reg_coef", -0.0001))
-        p.survival_bonus = float(rcfg.get("survival_bonus", 0.02))
-        # reward plugin -> fused kernel id, or host-side evaluation for custom plugins
-        self.reward_obj = create_reward(self.reward_config)
-        self._host_reward = None
-        if type(self.reward_obj) is DirectionalReward:
-            td = np.asarray(self.reward_obj.target_direction, dtype=np.float32)
-            p.reward_kind = N.REWARD_DIRECTIONAL
-            p.target_dir[0], p.target_dir[1] = float(td[0]), float(td[1])
-        elif type(self.reward_obj) is DistanceReward:
-            p.reward_kind = N.REWARD_DISTANCE
-            p.goal[0], p.goal[1] = float(self.reward_obj.goal_position[0]), float(self.reward_obj.goal_position[1])
-            p.goal_scale = float(self.reward_obj.scale)
-        else:
-            p.reward_kind = N.REWARD_NONE
-            self._host_reward = self.reward_obj
-
-        bank = self._build_terrain_bank(n_terrains, seed)
+        p, self.reward_obj, self._host_reward = params_from_configs(self.reward_config, env_config, max_ep_steps,
+                                                                    precision, seed)
+        self.max_ep_steps = int(p.max_ep_steps)
+        hfields, self.terrain_seeds, size_z = terrain_bank(self.terrain_config, n_terrains, seed)
+        bank = [(h, size_z) for h in hfields]
         p.n_terrains = len(bank)
-        p.seed = int(seed) & 0xFFFFFFFFFFFFFFFF
-        p.fp64 = 1 if precision == "fp64" else 0
         self.precision = "fp64" if p.fp64 else "fp32"
         self._params = p
         L = N.lib()
@@ -110,29 +84,6 @@ class BallbotVecEnv:
             ids = torch.randint(0, self.n_terrains, (n,), generator=g, dtype=torch.int32).to(dev)
             N.check(L.bb_assign_terrain(h, _ptr(ids), self._stream()), "bb_assign_terrain")
         self.reset()
-
-    # ------------------------------------------------------------------ terrain
-    def _build_terrain_bank(self, n_terrains, seed):
-        """Generate heightfields host-side with the registered terrain plugin
-        (ballbot_env.py:501-513) and the ramp/gradient z-rescale (:486-495)."""
-        from ..core.factories import create_terrain
-
-        ttype = self.terrain_config.get("type", "flat")
-        tcfg = self.terrain_config.get("config", {})
-        size_z = 2.0
-        if ttype == "ramp":
-            size_z = float(2 * 5.0 * np.tan(np.radians(tcfg.get("ramp_angle", 15.0))))
-        elif ttype == "gradient":
-            size_z = float(2 * 5.0 * np.tan(np.radians(tcfg.get("max_slope", 20.0))))
-        gen = create_terrain(self.terrain_config)
-        if ttype == "flat":
-            return [(np.asarray(gen(N.HF_N), dtype=np.float32), size_z)]
-        if tcfg.get("seed") is not None:
-            return [(np.asarray(gen(N.HF_N), dtype=np.float32), size_z)]
-        k = int(n_terrains or 16)
-        rng = np.random.default_rng(seed)
-        seeds = rng.integers(0, 10000, size=k)  # reference draws seeds from [0, 10000)
-        return [(np.asarray(gen(N.HF_N, seed=int(s)), dtype=np.float32), size_z) for s in seeds]
 
     # --------------------------------------------------------------------- api
     def _stream(self):

@@ -1,0 +1,70 @@
+"""The C-ABI boundary (include/ballbot_mi355x.h) without a GPU: the built
+gfx950 library loads, exports every declared entry point, reports its ABI
+version and fills default params; no compute call is made here."""
+import ctypes as C
+import re
+from pathlib import Path
+
+import pytest
+
+ROOT = Path(__file__).resolve().parent.parent
+HEADER = ROOT / "include" / "ballbot_mi355x.h"
+
+
+def _declared():
+    text = HEADER.read_text()
+    text = re.sub(r"/\*.*?\*/", "", text, flags=re.S)
+    return sorted(set(re.findall(r"^\s*(?:int|void|const char\*)\s+(bb_\w+)\s*\(", text, flags=re.M)))
+
+
+@pytest.fixture(scope="module")
+def native():
+    from ballbot_gym import _native
+
+    _native.build()  # no-op when up to date; hipcc cross-compiles for gfx950 without a GPU
+    return _native
+
+
+def test_header_declares_boundary():
+    names = _declared()
+    for must in ("bb_create", "bb_destroy", "bb_step", "bb_reset", "bb_set_hfield", "bb_assign_terrain",
+                 "bb_get_state", "bb_set_state", "bb_forward", "bb_last_error", "bb_abi_version"):
+        assert must in names
+
+
+def test_library_exports_every_declared_symbol(native):
+    lib = C.CDLL(str(native.LIB_PATH))
+    missing = [n for n in _declared() if not hasattr(lib, n)]
+    assert not missing, missing
+    assert set(_declared()) == set(native.EXPORTS)
+
+
+def test_abi_version_and_defaults(native):
+    L = native.lib()
+    assert L.bb_abi_version() == native.ABI_VERSION
+    hdr = HEADER.read_text()
+    assert f"#define BB_ABI_VERSION {native.ABI_VERSION}" in hdr
+    p = native.default_params()
+    assert (p.max_ep_steps, p.max_allowed_tilt, p.max_wheel_velocity) == (4000, 20.0, 10.0)
+    assert abs(p.reward_scale - 0.01) < 1e-9 and abs(p.survival_bonus - 0.02) < 1e-9
+    assert p.action_reg_coef == pytest.approx(-1e-4, rel=1e-6)
+    assert (p.target_dir[0], p.target_dir[1]) == (0.0, 1.0)
+    assert C.sizeof(native.BBParams) == C.sizeof(p)
+
+
+def test_errors_are_reported_not_raised(native):
+    """Invalid arguments return < 0 and set bb_last_error (no GPU touched)."""
+    L = native.lib()
+    assert L.bb_step(None, None, None, None, None, None, None, 0, None) < 0
+    assert "NULL handle" in native.last_error()
+    h = C.c_void_p()
+    assert L.bb_create(0, 0, None, C.byref(h)) < 0
+    assert "n_envs" in native.last_error()
+
+
+def test_product_path_has_no_cpu_fallback(native, monkeypatch, tmp_path):
+    """A missing HIP library is an error, never a silent CPU path."""
+    monkeypatch.setattr(native, "_lib", None)
+    monkeypatch.setattr(native, "LIB_PATH", tmp_path / "missing.so")
+    with pytest.raises(native.NativeLibraryError):
+        native.lib()

@@ -1,0 +1,84 @@
+"""Host-side glue of BallbotVecEnv (no GPU): config -> bb_params, reward
+plugin routing (fused kernel id vs host plugin), terrain bank, obs layout."""
+import numpy as np
+import pytest
+
+
+def test_directional_reward_maps_to_fused_kernel(reward_config):
+    from ballbot_gym import _native as N
+    from ballbot_gym.envs.config import params_from_configs
+
+    env_cfg = {"env": {"max_ep_steps": 1000, "max_allowed_tilt": 15.0, "max_wheel_velocity": 8.0}}
+    cfg = {"type": "directional", "config": {"target_direction": [1.0, 0.0], "scale": 0.05,
+                                             "action_reg_coef": -0.001, "survival_bonus": 0.1}}
+    p, plugin, host = params_from_configs(cfg, env_cfg, precision="fp32", seed=7)
+    assert host is None and p.reward_kind == N.REWARD_DIRECTIONAL
+    assert (p.target_dir[0], p.target_dir[1]) == (1.0, 0.0)
+    assert (p.max_ep_steps, p.max_allowed_tilt, p.max_wheel_velocity) == (1000, 15.0, 8.0)
+    assert p.reward_scale == pytest.approx(0.05) and p.survival_bonus == pytest.approx(0.1)
+    assert p.action_reg_coef == pytest.approx(-0.001)
+    assert p.fp64 == 0 and p.seed == 7
+    p, _, _ = params_from_configs(reward_config)
+    assert p.fp64 == 1 and p.max_ep_steps == 4000
+
+
+def test_distance_and_custom_rewards():
+    from ballbot_gym import ComponentRegistry
+    from ballbot_gym import _native as N
+    from ballbot_gym.envs.config import params_from_configs
+    from ballbot_gym.rewards import BaseReward
+
+    p, _, host = params_from_configs({"type": "distance", "config": {"goal_position": [1.0, -2.0], "scale": 3.0}})
+    assert host is None and p.reward_kind == N.REWARD_DISTANCE
+    assert (p.goal[0], p.goal[1], p.goal_scale) == (1.0, -2.0, 3.0)
+
+    class Upright(BaseReward):
+        def __init__(self, weight=1.0):
+            self.weight = weight
+
+        def __call__(self, state):
+            return -self.weight * float(np.linalg.norm(state["orientation"]))
+
+    if "upright_test" not in ComponentRegistry.list_rewards():
+        ComponentRegistry.register_reward("upright_test", Upright)
+    p, plugin, host = params_from_configs({"type": "upright_test", "config": {"weight": 2.0}})
+    assert p.reward_kind == N.REWARD_NONE and host is plugin and plugin.weight == 2.0
+
+
+def test_config_errors():
+    from ballbot_gym.envs.config import params_from_configs
+
+    with pytest.raises(ValueError, match="precision"):
+        params_from_configs(None, precision="bf16")
+    with pytest.raises(ValueError, match="target_direction"):
+        params_from_configs({"type": "directional", "config": {}})
+    with pytest.raises(ValueError, match="Unknown reward"):
+        params_from_configs({"type": "nope", "config": {}})
+
+
+def test_terrain_bank_seeds_and_size_z():
+    from ballbot_gym.envs.config import np_random, terrain_bank
+
+    hf, seeds, sz = terrain_bank({"type": "flat", "config": {}}, None, 0, n=33)
+    assert len(hf) == 1 and sz == 2.0 and hf[0].dtype == np.float32 and not hf[0].any()
+    hf, seeds, sz = terrain_bank({"type": "hills", "config": {}}, 4, 10, n=33)
+    assert seeds == [7765, 9560, 2640, 2076]  # gymnasium np_random(10).integers(0, 10000)
+    from ballbot_gym.terrain import generate_hills_terrain
+
+    np.testing.assert_array_equal(hf[2], generate_hills_terrain(33, seed=2640).astype(np.float32))
+    _, _, sz = terrain_bank({"type": "ramp", "config": {"ramp_angle": 10.0}}, 1, 0, n=33)
+    assert sz == pytest.approx(10 * np.tan(np.radians(10.0)))
+    _, _, sz = terrain_bank({"type": "gradient", "config": {}}, 1, 0, n=33)
+    assert sz == pytest.approx(10 * np.tan(np.radians(20.0)))
+    hf, seeds, _ = terrain_bank({"type": "hills", "config": {"seed": 3}}, 8, 0, n=33)
+    assert len(hf) == 1 and seeds == [3]
+    assert np_random(1).integers(0, 10000) == np_random(1).integers(0, 10000)
+
+
+def test_obs_layout_is_sorted_keys():
+    from ballbot_gym.envs import OBS_KEYS, split_obs
+
+    assert list(OBS_KEYS) == sorted(OBS_KEYS)
+    d = split_obs(np.arange(15.0))
+    assert list(d) == list(OBS_KEYS)
+    np.testing.assert_array_equal(d["orientation"], [9, 10, 11])

@@ -1,0 +1,185 @@
+"""The fp64 CPU oracle (oracle/bb_oracle.c): invariants of the restated
+mj_step and env glue (physics parity vs MuJoCo is UNPINNED,
+so the oracle is validated by physics invariants and by the golden-pinned
+pieces of the env glue).  CPU only, seconds."""
+import numpy as np
+import pytest
+
+G = 9.81
+
+
+@pytest.fixture(autouse=True)
+def _reset_flags(oracle):
+    oracle.set_flags(0)
+    yield
+    oracle.set_flags(0)
+
+
+def test_model_constants(oracle):
+    """Masses from ballbot.xml densities (cone meshes absent -> stand-in 0)."""
+    mi = oracle.model_info()
+    m = mi["mass"]
+    np.testing.assert_allclose(m[1], 0.11 ** 2 * np.pi * 0.28 * 23.6 + 0.2 ** 3 * 400, rtol=1e-6)  # tower + ballast
+    np.testing.assert_allclose(m[2:4], np.pi * 0.01 ** 2 * (0.2 + 4 / 3 * 0.01) * 1000, rtol=1e-6)  # sticks
+    np.testing.assert_allclose(m[4:7], np.pi * 0.025 ** 2 * (0.04 + 4 / 3 * 0.025) * 620, rtol=1e-6)  # wheels
+    np.testing.assert_allclose(m[7], 4 / 3 * np.pi * 0.09 ** 3 * 55, rtol=1e-6)  # ball
+    np.testing.assert_array_equal(mi["qpos0"][[2, 12]], [0.24, 0.26])
+
+
+def test_mass_matrix_spd_and_block_structure(oracle):
+    rng = np.random.default_rng(0)
+    for _ in range(5):
+        q, v, _ = oracle.reset_state(0.01)
+        rv = rng.normal(0, 0.3, 3)
+        th = np.linalg.norm(rv)
+        q[3:7] = [np.cos(th / 2), *(np.sin(th / 2) * rv / th)]
+        q[7:10] = rng.uniform(-3, 3, 3)
+        fo = oracle.forward(q, v, np.zeros(3), None, oracle.flat_hfield())
+        M = np.array(fo.M).reshape(15, 15)
+        np.testing.assert_allclose(M, M.T, atol=1e-14)
+        assert np.linalg.eigvalsh(M).min() > 0
+        assert np.abs(M[:9, 9:]).max() == 0  # base tree and ball are separate trees
+        np.testing.assert_allclose(np.diag(M)[:3], oracle.model_info()["mass"][1:7].sum(), rtol=1e-12)
+        np.testing.assert_allclose(np.diag(M)[9:12], oracle.model_info()["mass"][7], rtol=1e-12)
+
+
+def test_free_fall_is_exact(oracle):
+    """Contacts off: both trees fall with a = -g; RK4 is exact for constant acceleration."""
+    oracle.set_flags(oracle.DISABLE_CONTACT)
+    q, v, w = oracle.reset_state(0.01)
+    z0b, z0B = q[2], q[12]
+    for _ in range(200):
+        oracle.mj_step(q, v, w, np.zeros(3))
+    t = 200 * 0.002
+    np.testing.assert_allclose([q[2], q[12]], [z0b - 0.5 * G * t * t, z0B - 0.5 * G * t * t], atol=1e-10)
+    np.testing.assert_allclose([v[2], v[11]], [-G * t, -G * t], atol=1e-10)
+    np.testing.assert_allclose(v[[0, 1, 3, 4, 5, 9, 10, 12, 13, 14]], 0, atol=1e-10)
+
+
+def _energy(oracle, q, v):
+    fo = oracle.forward(q, v, np.zeros(3), None, None)
+    return fo.energy_kin + fo.energy_pot
+
+
+def test_energy_conserved_without_contact_and_damping(oracle):
+    oracle.set_flags(oracle.DISABLE_CONTACT | oracle.DISABLE_DAMPING)
+    rng = np.random.default_rng(1)
+    q, v, w = oracle.reset_state(0.01)
+    v[:] = rng.normal(0, 1.0, 15)
+    e0 = _energy(oracle, q, v)
+    for _ in range(500):
+        oracle.mj_step(q, v, w, np.zeros(3))
+    assert abs(_energy(oracle, q, v) - e0) < 1e-6 * max(1.0, abs(e0))
+
+
+def test_linear_momentum_conserved_without_gravity(oracle):
+    oracle.set_flags(oracle.DISABLE_CONTACT | oracle.DISABLE_DAMPING | oracle.DISABLE_GRAVITY)
+    rng = np.random.default_rng(2)
+    q, v, w = oracle.reset_state(0.01)
+    v[:] = rng.normal(0, 1.0, 15)
+
+    def momentum():
+        M = np.array(oracle.forward(q, v, np.zeros(3), None, None).M).reshape(15, 15)
+        return M[0:3] @ v, M[9:12] @ v
+
+    p0, P0 = momentum()
+    for _ in range(300):
+        oracle.mj_step(q, v, w, np.zeros(3))
+    p1, P1 = momentum()
+    np.testing.assert_allclose(p1, p0, atol=1e-9)
+    np.testing.assert_allclose(P1, P0, atol=1e-9)
+
+
+def test_patched_contact_frame(oracle):
+    """tools/mujoco_fix.patch: the first tangent of each ball-wheel contact is
+    the capsule axis orthogonalised against the normal; the frame is orthonormal
+    and right-handed (mju_makeFrame)."""
+    q, v, _ = oracle.reset_state(0.01)
+    fo = oracle.forward(q, v, np.zeros(3), None, oracle.flat_hfield())
+    a0 = np.array([-0.1532, -0.6903, -0.7071])
+    a0 /= np.linalg.norm(a0)
+    for k in range(3):
+        F = np.array(fo.con_frame[9 * k:9 * k + 9]).reshape(3, 3)
+        np.testing.assert_allclose(F @ F.T, np.eye(3), atol=1e-12)
+        np.testing.assert_allclose(np.linalg.det(F), 1.0, atol=1e-12)
+        body = fo.con_body2[k]
+        ang = np.radians(120 * (body - 4))
+        Rz = np.array([[np.cos(ang), -np.sin(ang), 0], [np.sin(ang), np.cos(ang), 0], [0, 0, 1]])
+        ax = Rz @ a0  # base upright at reset: base frame == world frame
+        n = F[0]
+        t = ax - ax.dot(n) * n
+        assert abs(abs(F[1].dot(t / np.linalg.norm(t))) - 1) < 1e-3
+
+
+def test_rotvec_formula(oracle):
+    """numpy-quaternion as_rotation_vector: 2 atan2(|v|, w) v/|v|, no w >= 0 flip."""
+    rng = np.random.default_rng(3)
+    for _ in range(50):
+        qq = rng.normal(size=4)
+        qq /= np.linalg.norm(qq)
+        b = np.linalg.norm(qq[1:])
+        np.testing.assert_allclose(oracle.quat_to_rotvec(qq), 2 * np.arctan2(b, qq[0]) * qq[1:] / b, atol=1e-12)
+    np.testing.assert_array_equal(oracle.quat_to_rotvec(np.array([1.0, 0, 0, 0])), 0)
+
+
+def test_reward_chain_matches_reward_plugin(oracle):
+    """env glue: reward = 0.01 * DirectionalReward(vel) + (-1e-4)|a|^2 + 0.02 in float32."""
+    from ballbot_gym.rewards import DirectionalReward
+
+    cfg = oracle.default_cfg()
+    hf = oracle.flat_hfield()
+    q, v, w = oracle.reset_state(oracle.init_offset(hf))
+    s = np.zeros(1, np.int32)
+    rng = np.random.default_rng(4)
+    plugin = DirectionalReward(np.array([0.0, 1.0], np.float32))
+    for _ in range(60):
+        a = rng.uniform(-1, 1, 3).astype(np.float32)
+        obs, r, fl, _, _ = oracle.env_step(cfg, q, v, w, s, a, hf)
+        vel = obs[12:15]
+        exp = np.float32(plugin({"vel": vel})) * np.float32(0.01) + np.float32(-1e-4) * np.float32(
+            np.linalg.norm(a) ** 2)
+        if not fl & 2:
+            exp = exp + np.float32(0.02)
+        assert abs(r - float(exp)) <= 2e-7
+        np.testing.assert_array_equal(obs[0:3], a)
+        assert np.all(np.abs(obs[3:15]) <= 2.0)
+
+
+def test_init_offset_matches_host_restatement(oracle):
+    from ballbot_gym.envs.config import init_offset
+    from ballbot_gym.terrain import generate_hills_terrain
+
+    hf = generate_hills_terrain(293, seed=7).astype(np.float32)
+    assert abs(oracle.init_offset(hf, 2.0) - init_offset(hf, 2.0)) < 1e-6
+    assert oracle.init_offset(oracle.flat_hfield(), 2.0) == pytest.approx(0.01)
+
+
+def test_pid_balances_on_flat(oracle):
+    """scripts/test_pid.py:22-63 behaviour: gains (20, 15, 2) keep the robot up."""
+    from pid_ref import PID, rotvec_to_R
+
+    cfg = oracle.default_cfg()
+    hf = oracle.flat_hfield()
+    q, v, w = oracle.reset_state(oracle.init_offset(hf))
+    s = np.zeros(1, np.int32)
+    pid = PID(0.002, 20, 15, 2)
+    obs = np.zeros(15, np.float32)
+    for _ in range(1500):
+        a = pid.act(rotvec_to_R(obs[9:12])).astype(np.float32)
+        obs, r, fl, _, tilt = oracle.env_step(cfg, q, v, w, s, a, hf)
+        assert fl == 0
+    assert np.linalg.norm(obs[9:12]) < np.radians(5)
+    assert np.abs(v).max() < 1.0
+
+
+def test_ball_rests_on_plane(oracle):
+    """Ball alone settles on the plane: contact depth ~ m g / k-ish, no drift."""
+    cfg = oracle.default_cfg()
+    hf = oracle.flat_hfield()
+    q, v, w = oracle.reset_state(oracle.init_offset(hf))
+    for _ in range(400):
+        oracle.mj_step(q, v, w, np.zeros(3), hf)
+    fo = oracle.forward(q, v, np.zeros(3), w, hf)
+    assert fo.nground >= 1
+    ball_bottom = q[12] - 0.14 - 0.09
+    assert -5e-3 < ball_bottom < 1e-3
