@@ -70,7 +70,7 @@ typedef struct {
   float goal_scale;            /* distance reward scale */
   int n_terrains;              /* terrain bank size (>= 1) */
   uint64_t seed;               /* per-env terrain draws at auto-reset */
-  int fp64;                    /* 0: fp32 arithmetic, 1: fp64 arithmetic */
+  int fp64;                    /* 1 (default): fp64 arithmetic, 0: fp32 */
   int solver_maxiter;          /* 0 = default */
   double solver_tol;           /* 0 = default */
 } bb_params;

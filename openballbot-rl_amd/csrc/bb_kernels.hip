@@ -284,7 +284,7 @@ void bb_default_params(bb_params* p) {
   p->goal_scale = 1.f;
   p->n_terrains = 1;
   p->seed = 0;
-  p->fp64 = 0;
+  p->fp64 = 1;  // fp64 arithmetic by default (parity 1e-9); fp32 opt-in
 }
 
 int bb_create(int n_envs, int device, const bb_params* p, bb_handle** out) {

@@ -11,9 +11,13 @@
  *     (git 99490163 + tools/mujoco_fix.patch) is not vendored in the reference
  *     and cannot be built or imported here.  This file restates MuJoCo's
  *     published algorithms for this one model; it is validated by physical
- *     invariants (tests/test_oracle_invariants.py).
- *   - glue (A10..A15): pinned by golden vectors generated from the reference's
- *     importable Python modules (tests/golden/, tools/gen_goldens.py).
+ *     invariants (tests/test_oracle.py: free fall, energy and momentum
+ *     conservation, mass-matrix structure, patched contact frame, PID balance).
+ *   - glue (A10..A15): the reward chain is checked against the reward plugin
+ *     pinned by golden vectors from the reference's importable Python modules
+ *     (tests/golden/, tools/gen_goldens.py); obs packing (numpy-quaternion
+ *     rotvec) and termination are restated from ballbot_env.py:771-1036 and
+ *     formula-pinned (no MuJoCo run can produce reference outputs here).
  *
  * All state is MuJoCo layout: qpos[17] = base(x,y,z,qw,qx,qy,qz), wheel0..2,
  * ball(x,y,z,qw,qx,qy,qz); qvel[15] = base(v_world[3], w_local[3]),
