@@ -31,6 +31,7 @@ namespace bb { __device__ unsigned long long bb_phase_cycles[16]; }
 namespace {
 
 constexpr int WAVE = 64;
+constexpr int TEAM = 16;  // lanes per env == one DPP row
 char g_err[512] = "";
 
 int fail(const char* fmt, ...) {
@@ -315,10 +316,7 @@ int bb_create(int n_envs, int device, const bb_params* p, bb_handle** out) {
     hipDeviceProp_t prop;
     HIPCHK(hipGetDeviceProperties(&prop, device));
     const int simds = prop.multiProcessorCount * 4;
-    int L = 16;
-    const char* tv = getenv("BB_TEAM");
-    if (tv && atoi(tv) > 0) L = atoi(tv);
-    if (L > WAVE || (L & (L - 1))) { delete h; return fail("bb_create: BB_TEAM must be a power of two <= 64 (got %d)", L); }
+    const int L = TEAM;  // one DPP row per env (bb_team16.h)
     // LDS caps envs per wave: one EnvWork per team + the staged model
     const size_t lds_max = 160 * 1024 - 2048;
     const int cap = (int)(lds_max / (h->fp64 ? work_stride<double>() : work_stride<float>()));

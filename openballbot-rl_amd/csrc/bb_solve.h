@@ -65,15 +65,29 @@ BB_HD void tri_unpack(int e, int& i, int& j) {
   j = e - r * (r + 1) / 2;
 }
 
+// What mjData holds after the last forward of mj_step (RK stage 4).
+template <typename T>
+struct StageOut {
+  T quat_b[4];   // xquat[base] (normalised)
+  T w_world[3];  // cvel[base][0:3]
+  T v_com[3];    // cvel[base][3:6] (linear velocity at subtree_com[base])
+  T pb[3];       // xpos[base]
+  int ng, iters, overflow;
+};
+
 // Per-env working set of one RK step (LDS on the GPU, one per team).
 // Phase-local buffers share storage in a union to fit 16 envs per CU.
 template <typename T>
 struct EnvWork {
   T q0[NQ], v0[NV], vs[NV], as[NV], vp[NV];  // RK4 stage context
+  T qfs[NV];                                 // smooth force of the current forward
+  T qi[NQ], vi[NV];                          // RK stage state (read by the pre-phase)
+  T gv[NV], mq[NV];                          // solver: gradient, M a - qfs (team-replicated)
+  StageOut<T> so;                            // stage-4 outputs for obs/reward
   Mass<T> M;                                 // mass-matrix blocks
   WheelCon<T> wc[3];                         // ball-wheel contacts
   T g[MAXG * NGF];                           // ball-terrain contacts
-  T H[NH];                                   // Hessian / Cholesky factor (packed lower)
+  T H[NH];                                   // Hessian / Cholesky factor (packed lower); dense M on the GPU
   T hd[NV];                                  // Hessian diagonal before factorisation
   union U {
     struct {                                 // forward pre-phase

@@ -4,7 +4,7 @@
 //   termination (:982-1017).  Per env team of lanes, templated on T (see bb_physics.h).
 #pragma once
 
-#include "bb_solve.h"
+#include "bb_team16.h"
 
 namespace bb {
 
@@ -19,16 +19,6 @@ struct EnvCfg {
   float target[2];         // DirectionalReward target_direction
   int reward_kind;         // 0 directional, 1 distance (needs pos2d; raises in ref), 2 none (host plugin)
   float goal[2], goal_scale;
-};
-
-// What mjData holds after the last forward of mj_step (RK stage 4).
-template <typename T>
-struct StageOut {
-  T quat_b[4];   // xquat[base] (normalised)
-  T w_world[3];  // cvel[base][0:3]
-  T v_com[3];    // cvel[base][3:6] (linear velocity at subtree_com[base])
-  T pb[3];       // xpos[base]
-  int ng, iters, overflow;
 };
 
 // mj_forward for this model: returns qacc in acc (acc holds the warm start on
@@ -46,12 +36,17 @@ BB_HD int forward(const ModelT<T>& m, const T* q, const T* v, const T* ctrl, T* 
   kinematics(m, q, k);
   Mass<T>& M = W.M;
   build_mass(m, k, M, W.u.pre.Iw);
-  T qfs[NV];
-  bias_forces(m, k, W.u.pre.Iw, v, qfs);
+  {
+    // qfrc_smooth = -bias + passive + actuation, straight to the workspace
+    T qfs[NV];
+    bias_forces(m, k, W.u.pre.Iw, v, qfs);
 #pragma unroll
-  for (int i = 0; i < NV; i++) qfs[i] = -qfs[i];
+    for (int i = 0; i < NV; i++) qfs[i] = -qfs[i];
 #pragma unroll
-  for (int w = 0; w < 3; w++) qfs[6 + w] += -m.damping * v[6 + w] + ctrl[w];
+    for (int w = 0; w < 3; w++) qfs[6 + w] += -m.damping * v[6 + w] + ctrl[w];
+#pragma unroll
+    for (int i = 0; i < NV; i++) W.qfs[i] = qfs[i];
+  }
 #pragma unroll
   for (int w = 0; w < 3; w++) wheel_contact(m, k, v, w, W.wc[w]);
   const GStore<T> st{W.g, 1};
@@ -88,7 +83,14 @@ BB_HD int forward(const ModelT<T>& m, const T* q, const T* v, const T* ctrl, T* 
 #pragma unroll
     for (int i = 0; i < NV; i++) acc[i] = 0;
   }
-  const int it = solve_team(m, W, qfs, ng, acc, tm);
+#ifdef __HIP_DEVICE_COMPILE__
+  // 16-lane DPP-row solve: smooth force and dense M staged in the team's LDS
+  t16::mass_dense_team(W, tm.tl);
+  team_sync();
+  const int it = t16::solve16(m, W, ng, acc, tm.tl);
+#else
+  const int it = solve_team(m, W, W.qfs, ng, acc, tm);
+#endif
   if (so) so->iters = it;
   return it;
 }
@@ -115,27 +117,36 @@ BB_HD int rk4_step(const ModelT<T>& m, T* q, T* v, T* warm, const T* ctrl, const
 #pragma unroll 1
   for (int stage = 0; stage < 4; stage++) {
     const T a = stage == 3 ? T(1) : T(0.5);  // RK4 Butcher A (sub-diagonal)
-    T qi[NQ], vi[NV];
+    {
+      // stage state X0 (+) h a (v_prev, a_prev), kept in the workspace so that
+      // nothing but the warm start stays in registers across the solve
+      T qi[NQ], vi[NV];
 #pragma unroll
-    for (int i = 0; i < NQ; i++) qi[i] = q0[i];
-    if (stage == 0) {
+      for (int i = 0; i < NQ; i++) qi[i] = q0[i];
+      if (stage == 0) {
 #pragma unroll
-      for (int i = 0; i < NV; i++) vi[i] = v0[i];
-    } else {
-      T dv[NV];
+        for (int i = 0; i < NV; i++) vi[i] = v0[i];
+      } else {
+        T dv[NV];
 #pragma unroll
-      for (int i = 0; i < NV; i++) { dv[i] = a * vp[i]; vi[i] = v0[i] + h * a * warm[i]; }
-      integrate_pos(qi, dv, h);
+        for (int i = 0; i < NV; i++) { dv[i] = a * vp[i]; vi[i] = v0[i] + h * a * warm[i]; }
+        integrate_pos(qi, dv, h);
+      }
+      team_sync();
+#pragma unroll
+      for (int i = 0; i < NQ; i++) W.qi[i] = qi[i];
+#pragma unroll
+      for (int i = 0; i < NV; i++) W.vi[i] = vi[i];
     }
-    iters += forward(m, qi, vi, ctrl, warm, hf, size_z, W, stage == 3 ? &so : (StageOut<T>*)nullptr, tm);
+    iters += forward(m, W.qi, W.vi, ctrl, warm, hf, size_z, W, stage == 3 ? &so : (StageOut<T>*)nullptr, tm);
     const T b = (stage == 0 || stage == 3) ? T(1.0 / 6) : T(1.0 / 3);  // RK4 weights B
     team_sync();
     if (stage == 0) {
 #pragma unroll
-      for (int i = 0; i < NV; i++) { vs[i] = b * vi[i]; as[i] = b * warm[i]; vp[i] = vi[i]; }
+      for (int i = 0; i < NV; i++) { vs[i] = b * W.vi[i]; as[i] = b * warm[i]; vp[i] = W.vi[i]; }
     } else {
 #pragma unroll
-      for (int i = 0; i < NV; i++) { vs[i] += b * vi[i]; as[i] += b * warm[i]; vp[i] = vi[i]; }
+      for (int i = 0; i < NV; i++) { vs[i] += b * W.vi[i]; as[i] += b * warm[i]; vp[i] = W.vi[i]; }
     }
   }
   team_sync();
@@ -190,7 +201,7 @@ BB_HD int env_step(const ModelT<T>& m, const EnvCfg& cfg, T* q, T* v, T* warm, i
   T ctrl[3];
 #pragma unroll
   for (int i = 0; i < 3; i++) ctrl[i] = -T(clipf(action[i] * mwv, -mwv, mwv));  // data.ctrl[:] = -ctrl
-  StageOut<T> so;
+  StageOut<T>& so = W.so;  // team-shared (LDS): not register-resident across the solves
   int it = rk4_step(m, q, v, warm, ctrl, hf, size_z, W, so, tm);
   if (iters) *iters = it;
   int flags = state_bad(q, v) ? F_DIVERGED : 0;

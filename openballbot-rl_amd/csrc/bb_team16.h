@@ -1,0 +1,342 @@
+// bb_team16.h -- the constraint solve of bb_solve.h mapped onto one 16-lane
+// DPP row of a gfx950 wavefront (device only).
+//
+// A team of 16 lanes == one DPP row, so every cross-lane step is a DPP move
+// (1 VALU op, no LDS round trip):
+//   team sum      row_mirror, row_half_mirror, quad_perm [2,3,0,1], [1,0,3,2]
+//                 (every lane ends with the bit-identical total)
+//   broadcast     row_newbcast:j (lane j of the row to all 16)
+// Work split per Newton iteration:
+//   contact pass  lane c owns contact c (c, c+16): cone force / Hessian; its
+//                 -J'f and ground-block C-weighted J'J partials are team-summed
+//   Hessian       lane i owns ROW i of H in registers: dense M row (LDS, built
+//                 once per forward) + wheel blocks J_w' (C J)_w + ground block
+//   Cholesky      right-looking on the register rows; column j scaled by the
+//                 broadcast pivot, trailing update with broadcast L_kj
+//   solves        forward: column sweep with broadcasts; backward: one team
+//                 sum per unknown (lane k holds L_ki)
+//   line search   contact-parallel phi'/phi'' partials + 3 team sums
+// The arithmetic per quantity is the same as bb_solve.h:solve_team (which the
+// host tests run); only the distribution over lanes differs.
+#pragma once
+
+#include <type_traits>
+
+#include "bb_solve.h"
+
+namespace bb {
+#ifdef __HIP_DEVICE_COMPILE__
+namespace t16 {
+
+constexpr int L = 16;
+
+template <int CTRL>
+__device__ __forceinline__ float dpp(float v) {
+  return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), CTRL, 0xF, 0xF, false));
+}
+template <int CTRL>
+__device__ __forceinline__ double dpp(double v) {
+  const unsigned long long u = (unsigned long long)__double_as_longlong(v);
+  const int lo = __builtin_amdgcn_update_dpp(0, (int)(unsigned)u, CTRL, 0xF, 0xF, false);
+  const int hi = __builtin_amdgcn_update_dpp(0, (int)(unsigned)(u >> 32), CTRL, 0xF, 0xF, false);
+  return __longlong_as_double((long long)(((unsigned long long)(unsigned)hi << 32) | (unsigned)lo));
+}
+
+// sum over the 16 lanes of the row; identical bits in every lane
+template <typename T>
+__device__ __forceinline__ T tsum(T v) {
+  v += dpp<0x140>(v);  // row_mirror       i <-> 15-i
+  v += dpp<0x141>(v);  // row_half_mirror  i <-> 7-i within each half
+  v += dpp<0x4E>(v);   // quad_perm [2,3,0,1]
+  v += dpp<0xB1>(v);   // quad_perm [1,0,3,2]
+  return v;
+}
+
+// lane J's value to the whole row
+template <int J, typename T>
+__device__ __forceinline__ T bcast(T v) {
+  return dpp<0x150 + J>(v);
+}
+
+template <int N, typename F>
+__device__ __forceinline__ void static_for(F&& f) {
+  if constexpr (N > 0) {
+    static_for<N - 1>(f);
+    f(std::integral_constant<int, N - 1>{});
+  }
+}
+
+// Cholesky of the register-distributed H (lane i holds row h[0..14]); on exit
+// lane i holds L_ik (k < i) in h[k] and every lane holds diag[] = L_jj.
+template <typename T>
+__device__ __forceinline__ void chol_rows(T (&h)[NV], T hdi, T (&diag)[NV], int tl) {
+  static_for<NV>([&](auto jc) {
+    constexpr int j = decltype(jc)::value;
+    T piv = bcast<j>(h[j]);
+    const T hdj = bcast<j>(hdi);
+    const T fl = pivot_eps<T>() * maxT(hdj, T(1e-30));
+    piv = piv > fl ? piv : fl;
+    const T d = sqrt(piv), id = T(1) / d;
+    diag[j] = d;
+    const T lij = h[j] * id;
+    h[j] = tl > j ? lij : h[j];
+    static_for<NV - 1 - j>([&](auto kc) {
+      constexpr int k = j + 1 + decltype(kc)::value;
+      const T lkj = bcast<k>(h[j]);
+      const T upd = h[k] - h[j] * lkj;
+      h[k] = tl >= k ? upd : h[k];
+    });
+  });
+}
+
+// s = -(L L')^-1 g with L distributed by rows (lane i: L_i,0..i-1 in h[]), g replicated
+template <typename T>
+__device__ __forceinline__ void chol_solve_rows(const T (&h)[NV], const T (&diag)[NV], const T* g, T (&s)[NV],
+                                                int tl) {
+  // forward: L y = -g, column sweep; b = this lane's running right-hand side
+  T b = 0;
+  static_for<NV>([&](auto kc) {
+    constexpr int k = decltype(kc)::value;
+    b = tl == k ? -g[k] : b;
+  });
+  T y[NV];
+  static_for<NV>([&](auto jc) {
+    constexpr int j = decltype(jc)::value;
+    const T yj = bcast<j>(b) / diag[j];
+    y[j] = yj;
+    b -= tl > j ? h[j] * yj : T(0);
+  });
+  // backward: L' s = y; s_i = (y_i - sum_{k>i} L_ki s_k) / L_ii, lane k holds L_ki
+  T own = 0;  // s of this lane's row
+  static_for<NV>([&](auto ic) {
+    constexpr int i = NV - 1 - decltype(ic)::value;
+    const T part = (tl > i && tl < NV) ? h[i] * own : T(0);
+    const T si = (y[i] - tsum(part)) / diag[i];
+    s[i] = si;
+    own = tl == i ? si : own;
+  });
+}
+
+// Newton on f(a); a replicated in every lane of the row.  W.H holds the dense
+// mass matrix (packed lower) for this forward, W.qfs the smooth force.
+template <typename T>
+__device__ int solve16(const ModelT<T>& m, EnvWork<T>& W, int ng, T* a, int tl) {
+  const Mass<T>& M = W.M;
+  const T mu_w = m.fr_wheel[0], f1w = m.fr_wheel[0], f2w = m.fr_wheel[1];
+  const int nc = 3 + ng;
+  const int row = tl < NV ? tl : NV - 1;
+  PH_DECL
+  int it = 0;
+  for (; it < m.maxiter; it++) {
+    team_sync();
+    // ---- (1) contact pass: -J'f and the ground-block C-weighted J'J, per lane
+    T gc[NV], Hg[21];
+#pragma unroll
+    for (int i = 0; i < NV; i++) gc[i] = 0;
+#pragma unroll
+    for (int i = 0; i < 21; i++) Hg[i] = 0;
+    for (int c = tl; c < nc; c += L) {
+      if (c < 3) {
+        const WheelCon<T>& C = W.wc[c];
+        T jar[3], f[3], Cc[6];
+#pragma unroll
+        for (int r = 0; r < 3; r++) jar[r] = wheel_dot(C, c, r, a) - C.aref[r];
+        const T Dw[3] = {C.D[0], C.D[1], C.D[2]};
+        cone_eval(jar, mu_w, f1w, f2w, Dw, f, Cc);
+#pragma unroll
+        for (int q = 0; q < 13; q++) {
+          const T j0 = C.J[0][q], j1 = C.J[1][q], j2 = C.J[2][q];
+          W.u.hes.cj[c][0][q] = Cc[0] * j0 + Cc[3] * j1 + Cc[4] * j2;
+          W.u.hes.cj[c][1][q] = Cc[3] * j0 + Cc[1] * j1 + Cc[5] * j2;
+          W.u.hes.cj[c][2][q] = Cc[4] * j0 + Cc[5] * j1 + Cc[2] * j2;
+          const T jf = j0 * f[0] + j1 * f[1] + j2 * f[2];
+          if (q < 6) gc[q] -= jf;
+          else if (q == 6) { gc[6] -= c == 0 ? jf : T(0); gc[7] -= c == 1 ? jf : T(0); gc[8] -= c == 2 ? jf : T(0); }
+          else gc[q + 2] -= jf;
+        }
+      } else {
+        const T* gcn = W.g + (c - 3) * NGF;
+        T J[3][6];
+#pragma unroll
+        for (int r = 0; r < 3; r++)
+#pragma unroll
+          for (int i = 0; i < 6; i++) J[r][i] = gcn[GF_J + 6 * r + i];
+        T jar[3];
+#pragma unroll
+        for (int r = 0; r < 3; r++)
+          jar[r] = J[r][0] * a[9] + J[r][1] * a[10] + J[r][2] * a[11] + J[r][3] * a[12] + J[r][4] * a[13] +
+                   J[r][5] * a[14] - gcn[GF_AREF + r];
+        const T D = gcn[GF_D];
+        const T Dv[3] = {D, D, D};
+        T f[3], Cc[6];
+        cone_eval(jar, T(1), T(1), T(1), Dv, f, Cc);
+        T w[3][6];
+#pragma unroll
+        for (int i = 0; i < 6; i++) {
+          gc[9 + i] -= J[0][i] * f[0] + J[1][i] * f[1] + J[2][i] * f[2];
+          w[0][i] = Cc[0] * J[0][i] + Cc[3] * J[1][i] + Cc[4] * J[2][i];
+          w[1][i] = Cc[3] * J[0][i] + Cc[1] * J[1][i] + Cc[5] * J[2][i];
+          w[2][i] = Cc[4] * J[0][i] + Cc[5] * J[1][i] + Cc[2] * J[2][i];
+        }
+#pragma unroll
+        for (int i = 0; i < 6; i++)
+#pragma unroll
+          for (int j = 0; j <= i; j++) Hg[i * (i + 1) / 2 + j] += J[0][i] * w[0][j] + J[1][i] * w[1][j] + J[2][i] * w[2][j];
+      }
+    }
+    PH(0)
+    // ---- (2) team sums (DPP)
+#pragma unroll
+    for (int i = 0; i < NV; i++) gc[i] = tsum(gc[i]);
+#pragma unroll
+    for (int i = 0; i < 21; i++) Hg[i] = tsum(Hg[i]);
+    team_sync();  // cj visible to every row owner
+    PH(1)
+    // ---- (3) gradient, replicated
+    T gn = 0;
+    {
+      T Ma[NV];
+      mass_mul(M, a, Ma);
+#pragma unroll
+      for (int i = 0; i < NV; i++) {
+        const T mq = Ma[i] - W.qfs[i];
+        const T gi = mq + gc[i];
+        W.mq[i] = mq;  // every lane stores the same value
+        W.gv[i] = gi;
+        gn += gi * gi;
+      }
+    }
+    if (m.scale * sqrt(gn) < m.tol) break;
+    PH(2)
+    // ---- (4) Hessian row `row` in registers
+    T h[NV];
+#pragma unroll
+    for (int k = 0; k < NV; k++) h[k] = W.H[hidx(row, k)];
+    static_for<3>([&](auto wc_) {
+      constexpr int w = decltype(wc_)::value;
+      const int p = wheel_pos(row, w);
+      if (p >= 0) {
+        const WheelCon<T>& C = W.wc[w];
+        const T j0 = C.J[0][p], j1 = C.J[1][p], j2 = C.J[2][p];
+#pragma unroll
+        for (int q = 0; q < 13; q++) {
+          const int k = wheel_col(q, w);
+          h[k] += j0 * W.u.hes.cj[w][0][q] + j1 * W.u.hes.cj[w][1][q] + j2 * W.u.hes.cj[w][2][q];
+        }
+      }
+    });
+#pragma unroll
+    for (int ai = 0; ai < 6; ai++)
+#pragma unroll
+      for (int b = 0; b < 6; b++) {
+        const T v = Hg[ai >= b ? ai * (ai + 1) / 2 + b : b * (b + 1) / 2 + ai];
+        h[9 + b] += row == 9 + ai ? v : T(0);
+      }
+    T hdi = 0;
+#pragma unroll
+    for (int k = 0; k < NV; k++) hdi = row == k ? h[k] : hdi;
+    PH(3)
+    // ---- (5) factorise and solve
+    T diag[NV], s[NV];
+    chol_rows(h, hdi, diag, tl);
+    PH(4)
+    chol_solve_rows(h, diag, W.gv, s, tl);
+    T d0 = 0;
+    bool fin = true;
+#pragma unroll
+    for (int i = 0; i < NV; i++) { fin = fin && isfinite(s[i]); d0 += s[i] * W.gv[i]; }
+    if (!fin || !(d0 < 0)) {
+      d0 = 0;
+#pragma unroll
+      for (int i = 0; i < NV; i++) {
+        s[i] = -W.gv[i] / maxT(mass_entry(M, i, i), T(1e-30));
+        d0 += s[i] * W.gv[i];
+      }
+      if (!(d0 < 0)) break;
+    }
+    PH(5)
+    // ---- (6) exact line search
+    T Ms[NV];
+    mass_mul(M, s, Ms);
+    T sMs = 0, gs = 0;
+#pragma unroll
+    for (int i = 0; i < NV; i++) { sMs += s[i] * Ms[i]; gs += s[i] * W.mq[i]; }
+    team_sync();  // the cj buffer is dead; the line-search cache reuses it
+    for (int c = tl; c < nc; c += L) {
+      T* c6 = W.u.ls[c];
+      if (c < 3) {
+        const WheelCon<T>& C = W.wc[c];
+#pragma unroll
+        for (int r = 0; r < 3; r++) { c6[r] = wheel_dot(C, c, r, a) - C.aref[r]; c6[3 + r] = wheel_dot(C, c, r, s); }
+      } else {
+        const T* gcn = W.g + (c - 3) * NGF;
+#pragma unroll
+        for (int r = 0; r < 3; r++) { c6[r] = ground_dot(gcn, r, a) - gcn[GF_AREF + r]; c6[3 + r] = ground_dot(gcn, r, s); }
+      }
+    }
+    T lo = 0, dlo = d0, hi = -1, dhi = 0, alpha = 1;
+    T flo = d0, fhi = 0;
+    int side = 0, same = 0;
+    bool ls_ok = false;
+    for (int ls = 1; ls <= m.ls_maxiter; ls++) {
+      T d1p = 0, d2p = 0, dmp = 0;
+      for (int c = tl; c < nc; c += L) {
+        if (c < 3) {
+          const T Dw[3] = {W.wc[c].D[0], W.wc[c].D[1], W.wc[c].D[2]};
+          ls_contact(W.u.ls[c], alpha, mu_w, f1w, f2w, Dw, d1p, d2p, dmp);
+        } else {
+          const T D = W.g[(c - 3) * NGF + GF_D];
+          const T Dv[3] = {D, D, D};
+          ls_contact(W.u.ls[c], alpha, T(1), T(1), T(1), Dv, d1p, d2p, dmp);
+        }
+      }
+      const T d1 = gs + alpha * sMs + tsum(d1p);
+      const T d2 = sMs + tsum(d2p);
+      const T dmag = fabs(gs) + fabs(alpha * sMs) + tsum(dmp);
+      if (fabs(d1) <= m.ls_tol * fabs(d0) || fabs(d1) <= T(32) * eps_of<T>() * dmag) { ls_ok = true; break; }
+      if (!(d1 == d1)) break;
+      const int sd = d1 < 0 ? -1 : 1;
+      same = sd == side ? same + 1 : 0;
+      side = sd;
+      if (sd < 0) {
+        lo = alpha; dlo = d1; flo = d1;
+        if (same > 0 && hi >= 0) fhi *= T(0.5);
+      } else {
+        hi = alpha; dhi = d1; fhi = d1;
+        if (same > 0) flo *= T(0.5);
+      }
+      T an = alpha - d1 / maxT(d2, T(1e-30));
+      if (hi < 0) {
+        if (!(an > lo)) an = lo > 0 ? 2 * lo : T(1);
+      } else if (!(an > lo && an < hi) || same > 0) {
+        const T fp = lo - flo * (hi - lo) / (fhi - flo);
+        an = (fp > lo && fp < hi) ? fp : T(0.5) * (lo + hi);
+      }
+      alpha = an;
+    }
+    if (!ls_ok) alpha = lo > 0 ? lo : (hi > 0 ? hi * dlo / (dlo - dhi) : T(0));
+    if (!(alpha > 0)) break;
+    T sn = 0, an2 = 0;
+#pragma unroll
+    for (int i = 0; i < NV; i++) { a[i] += alpha * s[i]; sn += s[i] * s[i]; an2 += a[i] * a[i]; }
+    PH(6)
+    if (alpha * alpha * sn <= T(1e-30) + m.step_rel2 * (1 + an2)) { it++; break; }
+  }
+  PH(7)
+  PH_FLUSH((Team{L, tl}))
+  return it;
+}
+
+// dense mass matrix (packed lower) into W.H, entry-parallel; once per forward
+template <typename T>
+__device__ __forceinline__ void mass_dense_team(EnvWork<T>& W, int tl) {
+  for (int e = tl; e < NH; e += L) {
+    int i, j;
+    tri_unpack(e, i, j);
+    W.H[e] = mass_entry(W.M, i, j);
+  }
+}
+
+}  // namespace t16
+#endif
+}  // namespace bb
