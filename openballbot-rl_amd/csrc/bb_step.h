@@ -54,7 +54,11 @@ BB_HD int forward(const ModelT<T>& m, const T* q, const T* v, const T* ctrl, T* 
 #if defined(BB_PHASE_CLOCKS) && defined(__HIP_DEVICE_COMPILE__)
   const unsigned long long f_t1 = clock64();
 #endif
+#ifdef __HIP_DEVICE_COMPILE__
+  int ng = hf ? t16::collide_team(m, k, v, hf, size_z, W.g, &overflow, tm.tl) : 0;
+#else
   int ng = hf ? collide_ground(m, k, v, hf, size_z, st, &overflow) : 0;
+#endif
 #if defined(BB_PHASE_CLOCKS) && defined(__HIP_DEVICE_COMPILE__)
   if (tm.tl == 0) {
     const unsigned long long f_t2 = clock64();

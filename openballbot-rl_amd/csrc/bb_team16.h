@@ -66,6 +66,44 @@ __device__ __forceinline__ void static_for(F&& f) {
   }
 }
 
+// cone_eval (bb_physics.h) without branches: the three zones are computed and
+// selected, so lanes of a team in different zones do not serialise.
+template <typename T>
+__device__ __forceinline__ void cone_sel(const T* jar, T mu, T f1, T f2, const T* D, T* force, T* C) {
+  const T U0 = jar[0] * mu, U1 = jar[1] * f1, U2 = jar[2] * f2;
+  const T N = U0, Tn = sqrt(U1 * U1 + U2 * U2);
+  const bool top = N >= mu * Tn || (Tn <= 0 && N >= 0);
+  const bool bot = !top && (mu * N + Tn <= 0 || (Tn <= 0 && N < 0));
+  const T Dm = D[0] / (mu * mu * (1 + mu * mu));
+  const T g = N - mu * Tn;
+  const T iT = T(1) / (Tn > 0 ? Tn : T(1));
+  const T gr1 = -mu * f1 * U1 * iT, gr2 = -mu * f2 * U2 * iT;
+  const T sc = -Dm * g;
+  const T k = Dm * g * (-mu) * iT, iT2 = iT * iT;
+  T fm[3] = {sc * mu, sc * gr1, sc * gr2};
+  T cm[6] = {Dm * mu * mu, Dm * gr1 * gr1 + k * f1 * f1 * (T(1) - U1 * U1 * iT2),
+             Dm * gr2 * gr2 + k * f2 * f2 * (T(1) - U2 * U2 * iT2), Dm * mu * gr1, Dm * mu * gr2,
+             Dm * gr1 * gr2 - k * f1 * f2 * U1 * U2 * iT2};
+#pragma unroll
+  for (int r = 0; r < 3; r++) force[r] = top ? T(0) : (bot ? -D[r] * jar[r] : fm[r]);
+#pragma unroll
+  for (int r = 0; r < 6; r++) C[r] = top ? T(0) : (bot ? (r < 3 ? D[r] : T(0)) : cm[r]);
+}
+
+// per-contact cone parameters: wheels (c < 3) use the pair friction and
+// anisotropic D, ground contacts mu = 1 and one D for all rows
+template <typename T>
+__device__ __forceinline__ void cone_params(const ModelT<T>& m, const EnvWork<T>& W, int c, T& mu, T& f1, T& f2,
+                                            T (&D)[3]) {
+  const bool wheel = c < 3;
+  const T* Dp = wheel ? &W.wc[c].D[0] : &W.g[(c - 3) * NGF + GF_D];
+  const int st = wheel ? 1 : 0;
+  D[0] = Dp[0]; D[1] = Dp[st]; D[2] = Dp[2 * st];
+  mu = wheel ? m.fr_wheel[0] : T(1);
+  f1 = wheel ? m.fr_wheel[0] : T(1);
+  f2 = wheel ? m.fr_wheel[1] : T(1);
+}
+
 // Cholesky of the register-distributed H (lane i holds row h[0..14]); on exit
 // lane i holds L_ik (k < i) in h[k] and every lane holds diag[] = L_jj.
 template <typename T>
@@ -122,7 +160,6 @@ __device__ __forceinline__ void chol_solve_rows(const T (&h)[NV], const T (&diag
 template <typename T>
 __device__ int solve16(const ModelT<T>& m, EnvWork<T>& W, int ng, T* a, int tl) {
   const Mass<T>& M = W.M;
-  const T mu_w = m.fr_wheel[0], f1w = m.fr_wheel[0], f2w = m.fr_wheel[1];
   const int nc = 3 + ng;
   const int row = tl < NV ? tl : NV - 1;
   PH_DECL
@@ -136,13 +173,21 @@ __device__ int solve16(const ModelT<T>& m, EnvWork<T>& W, int ng, T* a, int tl) 
 #pragma unroll
     for (int i = 0; i < 21; i++) Hg[i] = 0;
     for (int c = tl; c < nc; c += L) {
-      if (c < 3) {
-        const WheelCon<T>& C = W.wc[c];
-        T jar[3], f[3], Cc[6];
+      const bool wheel = c < 3;
+      const T* gcn = W.g + (wheel ? 0 : c - 3) * NGF;
+      T jar[3];
+      if (wheel) {
 #pragma unroll
-        for (int r = 0; r < 3; r++) jar[r] = wheel_dot(C, c, r, a) - C.aref[r];
-        const T Dw[3] = {C.D[0], C.D[1], C.D[2]};
-        cone_eval(jar, mu_w, f1w, f2w, Dw, f, Cc);
+        for (int r = 0; r < 3; r++) jar[r] = wheel_dot(W.wc[c], c, r, a) - W.wc[c].aref[r];
+      } else {
+#pragma unroll
+        for (int r = 0; r < 3; r++) jar[r] = ground_dot(gcn, r, a) - gcn[GF_AREF + r];
+      }
+      T mu, f1, f2, D[3], f[3], Cc[6];
+      cone_params(m, W, c, mu, f1, f2, D);
+      cone_sel(jar, mu, f1, f2, D, f, Cc);
+      if (wheel) {
+        const WheelCon<T>& C = W.wc[c];
 #pragma unroll
         for (int q = 0; q < 13; q++) {
           const T j0 = C.J[0][q], j1 = C.J[1][q], j2 = C.J[2][q];
@@ -155,22 +200,11 @@ __device__ int solve16(const ModelT<T>& m, EnvWork<T>& W, int ng, T* a, int tl) 
           else gc[q + 2] -= jf;
         }
       } else {
-        const T* gcn = W.g + (c - 3) * NGF;
-        T J[3][6];
+        T J[3][6], w[3][6];
 #pragma unroll
         for (int r = 0; r < 3; r++)
 #pragma unroll
           for (int i = 0; i < 6; i++) J[r][i] = gcn[GF_J + 6 * r + i];
-        T jar[3];
-#pragma unroll
-        for (int r = 0; r < 3; r++)
-          jar[r] = J[r][0] * a[9] + J[r][1] * a[10] + J[r][2] * a[11] + J[r][3] * a[12] + J[r][4] * a[13] +
-                   J[r][5] * a[14] - gcn[GF_AREF + r];
-        const T D = gcn[GF_D];
-        const T Dv[3] = {D, D, D};
-        T f[3], Cc[6];
-        cone_eval(jar, T(1), T(1), T(1), Dv, f, Cc);
-        T w[3][6];
 #pragma unroll
         for (int i = 0; i < 6; i++) {
           gc[9 + i] -= J[0][i] * f[0] + J[1][i] * f[1] + J[2][i] * f[2];
@@ -281,14 +315,17 @@ __device__ int solve16(const ModelT<T>& m, EnvWork<T>& W, int ng, T* a, int tl) 
     for (int ls = 1; ls <= m.ls_maxiter; ls++) {
       T d1p = 0, d2p = 0, dmp = 0;
       for (int c = tl; c < nc; c += L) {
-        if (c < 3) {
-          const T Dw[3] = {W.wc[c].D[0], W.wc[c].D[1], W.wc[c].D[2]};
-          ls_contact(W.u.ls[c], alpha, mu_w, f1w, f2w, Dw, d1p, d2p, dmp);
-        } else {
-          const T D = W.g[(c - 3) * NGF + GF_D];
-          const T Dv[3] = {D, D, D};
-          ls_contact(W.u.ls[c], alpha, T(1), T(1), T(1), Dv, d1p, d2p, dmp);
-        }
+        T mu, f1, f2, D[3];
+        cone_params(m, W, c, mu, f1, f2, D);
+        const T* c6 = W.u.ls[c];
+        const T x[3] = {c6[3], c6[4], c6[5]};
+        const T jr[3] = {c6[0] + alpha * x[0], c6[1] + alpha * x[1], c6[2] + alpha * x[2]};
+        T f[3], Cc[6];
+        cone_sel(jr, mu, f1, f2, D, f, Cc);
+        d1p -= f[0] * x[0] + f[1] * x[1] + f[2] * x[2];
+        dmp += fabs(f[0] * x[0]) + fabs(f[1] * x[1]) + fabs(f[2] * x[2]);
+        d2p += Cc[0] * x[0] * x[0] + Cc[1] * x[1] * x[1] + Cc[2] * x[2] * x[2] +
+               2 * (Cc[3] * x[0] * x[1] + Cc[4] * x[0] * x[2] + Cc[5] * x[1] * x[2]);
       }
       const T d1 = gs + alpha * sMs + tsum(d1p);
       const T d2 = sMs + tsum(d2p);
@@ -325,6 +362,97 @@ __device__ int solve16(const ModelT<T>& m, EnvWork<T>& W, int ng, T* a, int tl) 
   PH(7)
   PH_FLUSH((Team{L, tl}))
   return it;
+}
+
+// collide_ground (bb_physics.h) spread over the team: the prisms under the
+// ball's AABB are enumerated in MuJoCo's order (row-major over the sub-grid,
+// two triangles per cell in sliding-window order), 16 per round, one per
+// lane; hits are compacted in that order with a ballot, so the contact list
+// (and the MAXG cap) is exactly the serial one.
+template <typename T>
+__device__ __forceinline__ int collide_team(const ModelT<T>& m, const Kin<T>& k, const T* v, const float* hf,
+                                            T size_z, T* g, int* overflow, int tl) {
+  const T r = m.ball_r;
+  const T* c = k.c;
+  const T sx = m.hf_sx, sy = m.hf_sy, zb = m.hf_bottom;
+  const T xmin = c[0] - r, xmax = c[0] + r, ymin = c[1] - r, ymax = c[1] + r, zmin = c[2] - r, zmax = c[2] + r;
+  if (xmin > sx || xmax < -sx || ymin > sy || ymax < -sy || zmin > size_z || zmax < -zb) return 0;
+  const int N1 = HF_N - 1;
+  int cmin = (int)floor((xmin + sx) / (2 * sx) * N1);
+  int cmax = (int)ceil((xmax + sx) / (2 * sx) * N1);
+  int rmin = (int)floor((ymin + sy) / (2 * sy) * N1);
+  int rmax = (int)ceil((ymax + sy) / (2 * sy) * N1);
+  cmin = cmin < 0 ? 0 : cmin;
+  cmax = cmax > N1 ? N1 : cmax;
+  rmin = rmin < 0 ? 0 : rmin;
+  rmax = rmax > N1 ? N1 : rmax;
+  const int ncol = cmax - cmin + 1;
+  const int np = 2 * ncol - 2;            // prisms per grid row
+  const int total = (rmax - rmin) * (np > 0 ? np : 0);
+  const T dx = 2 * sx / N1, dy = 2 * sy / N1;
+  T wB[3];
+  mv3(wB, k.RB, v + 12);
+  const T iw = m.iw_ball;
+  const int team_shift = threadIdx.x & ~(L - 1);
+  int ng = 0;
+  for (int base = 0; base < total; base += L) {
+    const int P = base + tl;
+    bool hit = false;
+    T nn[3] = {0, 0, 1}, dist = 0;
+    if (P < total) {
+      const int rr = rmin + P / np, p = P % np;
+      T V[3][3];
+#pragma unroll
+      for (int t = 0; t < 3; t++) {
+        const int vt = p + t, cc = cmin + (vt >> 1), ri = rr + (vt & 1);
+        V[t][0] = dx * cc - sx;
+        V[t][1] = dy * ri - sy;
+        V[t][2] = T(hf[ri * HF_N + cc]) * size_z;
+      }
+      if (!(V[0][2] < zmin && V[1][2] < zmin && V[2][2] < zmin)) {
+        const T bx0 = minT(V[0][0], minT(V[1][0], V[2][0])), bx1 = maxT(V[0][0], maxT(V[1][0], V[2][0]));
+        const T by0 = minT(V[0][1], minT(V[1][1], V[2][1])), by1 = maxT(V[0][1], maxT(V[1][1], V[2][1]));
+        const T ztop = maxT(V[0][2], maxT(V[1][2], V[2][2]));
+        const T ex = maxT(T(0), maxT(bx0 - c[0], c[0] - bx1));
+        const T ey = maxT(T(0), maxT(by0 - c[1], c[1] - by1));
+        const T ez = maxT(T(0), c[2] - ztop);
+        if (ex * ex + ey * ey + ez * ez <= r * r) hit = sphere_prism(c, r, V, -zb, nn, &dist);
+      }
+    }
+    const unsigned long long bal = __ballot(hit);
+    const unsigned bits = unsigned(bal >> team_shift) & 0xFFFFu;
+    const int slot = ng + __popc(bits & ((1u << tl) - 1u));
+    if (hit) {
+      if (slot < MAXG) {
+        const T sp = r + dist * T(0.5);
+        T lv[3] = {c[0] - nn[0] * sp - k.pB[0], c[1] - nn[1] * sp - k.pB[1], c[2] - nn[2] * sp - k.pB[2]};
+        T t1[3], t2[3];
+        frame_from_normal(nn, t1, t2);
+        const T imp = clampT(impedance(m, dist), T(0.0001), T(0.9999));
+        const T R0 = maxT(T(1e-15), (1 - imp) * iw / imp);
+        T pv[3], tt[3];
+        cross3(tt, wB, lv);
+        pv[0] = v[9] + tt[0]; pv[1] = v[10] + tt[1]; pv[2] = v[11] + tt[2];
+        const T* F[3] = {nn, t1, t2};
+        T* gs = g + slot * NGF;
+#pragma unroll
+        for (int rw = 0; rw < 3; rw++) {
+          T x1[3], x2[3];
+          cross3(x1, lv, F[rw]);
+          mtv3(x2, k.RB, x1);
+#pragma unroll
+          for (int i = 0; i < 3; i++) { gs[GF_J + 6 * rw + i] = F[rw][i]; gs[GF_J + 6 * rw + 3 + i] = x2[i]; }
+        }
+        gs[GF_AREF + 0] = -m.Bd * dot3(nn, pv) - m.K * imp * dist;
+        gs[GF_AREF + 1] = -m.Bd * dot3(t1, pv);
+        gs[GF_AREF + 2] = -m.Bd * dot3(t2, pv);
+        gs[GF_D] = T(1) / R0;
+      }
+    }
+    ng += __popc(bits);
+  }
+  if (ng > MAXG) { ng = MAXG; *overflow = 1; }  // ng counts every hit: team-uniform
+  return ng;
 }
 
 // dense mass matrix (packed lower) into W.H, entry-parallel; once per forward
