@@ -31,12 +31,13 @@ namespace bb {
 
 constexpr int NQ = 17, NV = 15, NU = 3;
 constexpr int HF_N = 293;        // ballbot.xml:23 nrow = ncol
-constexpr int MAXG = 24;         // ball-hfield contact cap (== oracle BBO_MAXGROUND)
+constexpr int MAXG = 50;         // ball-hfield contact cap: MuJoCo's mjMAXCONPAIR (== oracle BBO_MAXGROUND)
 constexpr int NH = NV * (NV + 1) / 2;
-constexpr int NGF = 22;          // fields per stored ground contact (see GF_* below)
-// ground-contact store fields: three Jacobian rows over the ball dofs
-// (world-linear[3], local-angular[3]), aref[3], D
-constexpr int GF_J = 0, GF_AREF = 18, GF_D = 21;
+constexpr int NGF = 10;          // fields per stored ground contact (see GF_* below)
+// ground-contact store fields (compact; the 3x6 Jacobian is rebuilt from the
+// normal and the lever by ground_rows): normal[3], lever from the ball frame
+// origin (world)[3], aref[3], D
+constexpr int GF_N = 0, GF_LV = 3, GF_AREF = 6, GF_D = 9;
 
 // ------------------------------------------------------------------ model
 // Compiled constants (bb_model.cpp computes them in double from the MJCF
@@ -683,6 +684,25 @@ BB_HD bool sphere_prism(const T* c, T r, const T V[3][3], T zb, T* n, T* dist) {
   return true;
 }
 
+// Jacobian rows (normal, t1, t2) of a stored ground contact over the ball dofs:
+// world-linear F_r and local-angular RB' (lever x F_r)
+template <typename T>
+BB_HD void ground_rows(const T* gc, const T* RB, T (&J)[3][6]) {
+  const T n[3] = {gc[GF_N], gc[GF_N + 1], gc[GF_N + 2]};
+  const T lv[3] = {gc[GF_LV], gc[GF_LV + 1], gc[GF_LV + 2]};
+  T t1[3], t2[3];
+  frame_from_normal(n, t1, t2);
+  const T* F[3] = {n, t1, t2};
+#pragma unroll
+  for (int r = 0; r < 3; r++) {
+    T x1[3], x2[3];
+    cross3(x1, lv, F[r]);
+    mtv3(x2, RB, x1);
+#pragma unroll
+    for (int i = 0; i < 3; i++) { J[r][i] = F[r][i]; J[r][3 + i] = x2[i]; }
+  }
+}
+
 // mjc_ConvexHField for the ball: sub-grid from the ball AABB, triangular
 // prisms in MuJoCo's sliding-window order, one contact per penetrated prism.
 // Writes normal/lever/aref/D into the store; returns the contact count.
@@ -746,15 +766,8 @@ BB_HD int collide_ground(const ModelT<T>& m, const Kin<T>& k, const T* v, const 
         T pv[3], tt[3];
         cross3(tt, wB, lv);
         pv[0] = v[9] + tt[0]; pv[1] = v[10] + tt[1]; pv[2] = v[11] + tt[2];
-        const T* F[3] = {nn, t1, t2};
 #pragma unroll
-        for (int r = 0; r < 3; r++) {
-          T x1[3], x2[3];
-          cross3(x1, lv, F[r]);
-          mtv3(x2, k.RB, x1);
-#pragma unroll
-          for (int i = 0; i < 3; i++) { st.at(ng, GF_J + 6 * r + i) = F[r][i]; st.at(ng, GF_J + 6 * r + 3 + i) = x2[i]; }
-        }
+        for (int i = 0; i < 3; i++) { st.at(ng, GF_N + i) = nn[i]; st.at(ng, GF_LV + i) = lv[i]; }
         st.at(ng, GF_AREF + 0) = -m.Bd * dot3(nn, pv) - m.K * imp * dist;
         st.at(ng, GF_AREF + 1) = -m.Bd * dot3(t1, pv);
         st.at(ng, GF_AREF + 2) = -m.Bd * dot3(t2, pv);

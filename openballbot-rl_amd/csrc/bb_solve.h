@@ -86,7 +86,8 @@ struct EnvWork {
   StageOut<T> so;                            // stage-4 outputs for obs/reward
   Mass<T> M;                                 // mass-matrix blocks
   WheelCon<T> wc[3];                         // ball-wheel contacts
-  T g[MAXG * NGF];                           // ball-terrain contacts
+  T g[MAXG * NGF];                           // ball-terrain contacts (compact, GF_*)
+  T RB[9];                                   // ball orientation: rebuilds ground Jacobians
   T H[NH];                                   // Hessian / Cholesky factor (packed lower); dense M on the GPU
   T hd[NV];                                  // Hessian diagonal before factorisation
   union U {
@@ -99,7 +100,6 @@ struct EnvWork {
       T wf[3][3];                            // wheel contact forces
       T hg[21];                              // ground contribution to the ball block
     } hes;
-    T ls[3 + MAXG][6];                       // line search: jar(0), J s per contact
   } u;
 };
 
@@ -139,11 +139,10 @@ BB_HD T wheel_dot(const WheelCon<T>& C, int w, int r, const T* x) {
   return acc;
 }
 
-// J_r x for a stored ground contact (ball dofs only)
+// J_r x over the ball dofs for ground-contact rows J (ground_rows)
 template <typename T>
-BB_HD T ground_dot(const T* gc, int r, const T* x) {
-  const T* J = gc + GF_J + 6 * r;
-  return J[0] * x[9] + J[1] * x[10] + J[2] * x[11] + J[3] * x[12] + J[4] * x[13] + J[5] * x[14];
+BB_HD T ground_dot(const T (&J)[3][6], int r, const T* x) {
+  return J[r][0] * x[9] + J[r][1] * x[10] + J[r][2] * x[11] + J[r][3] * x[12] + J[r][4] * x[13] + J[r][5] * x[14];
 }
 
 // Team-parallel right-looking Cholesky in place.  A pivot that roundoff drives
@@ -222,10 +221,7 @@ BB_HD int solve_team(const ModelT<T>& m, EnvWork<T>& W, const T* qfs, int ng, T*
       } else {
         const T* gc = W.g + (c - 3) * NGF;
         T J[3][6];
-#pragma unroll
-        for (int r = 0; r < 3; r++)
-#pragma unroll
-          for (int i = 0; i < 6; i++) J[r][i] = gc[GF_J + 6 * r + i];
+        ground_rows(gc, W.RB, J);
         T jar[3];
 #pragma unroll
         for (int r = 0; r < 3; r++)
@@ -333,17 +329,19 @@ BB_HD int solve_team(const ModelT<T>& m, EnvWork<T>& W, const T* qfs, int ng, T*
     T sMs = 0, gs = 0;
 #pragma unroll
     for (int i = 0; i < NV; i++) { sMs += s[i] * Ms[i]; gs += s[i] * (Ma[i] - qfs[i]); }
-    team_sync();  // hes buffers are dead; the line-search cache reuses them
+    T lsc[3 + MAXG][6];  // line-search cache (host / reference path: plenty of stack)
     for (int c = tm.tl; c < nc; c += tm.L) {
-      T* c6 = W.u.ls[c];
+      T* c6 = lsc[c];
       if (c < 3) {
         const WheelCon<T>& C = W.wc[c];
 #pragma unroll
         for (int r = 0; r < 3; r++) { c6[r] = wheel_dot(C, c, r, a) - C.aref[r]; c6[3 + r] = wheel_dot(C, c, r, s); }
       } else {
         const T* gc = W.g + (c - 3) * NGF;
+        T J[3][6];
+        ground_rows(gc, W.RB, J);
 #pragma unroll
-        for (int r = 0; r < 3; r++) { c6[r] = ground_dot(gc, r, a) - gc[GF_AREF + r]; c6[3 + r] = ground_dot(gc, r, s); }
+        for (int r = 0; r < 3; r++) { c6[r] = ground_dot(J, r, a) - gc[GF_AREF + r]; c6[3 + r] = ground_dot(J, r, s); }
       }
     }
     // 1-D Newton on phi'(alpha) from the full step, safeguarded by an
@@ -362,11 +360,11 @@ BB_HD int solve_team(const ModelT<T>& m, EnvWork<T>& W, const T* qfs, int ng, T*
       for (int c = tm.tl; c < nc; c += tm.L) {
         if (c < 3) {
           const T Dw[3] = {W.wc[c].D[0], W.wc[c].D[1], W.wc[c].D[2]};
-          ls_contact(W.u.ls[c], alpha, mu_w, f1w, f2w, Dw, d1p, d2p, dmp);
+          ls_contact(lsc[c], alpha, mu_w, f1w, f2w, Dw, d1p, d2p, dmp);
         } else {
           const T D = W.g[(c - 3) * NGF + GF_D];
           const T Dv[3] = {D, D, D};
-          ls_contact(W.u.ls[c], alpha, T(1), T(1), T(1), Dv, d1p, d2p, dmp);
+          ls_contact(lsc[c], alpha, T(1), T(1), T(1), Dv, d1p, d2p, dmp);
         }
       }
       const T d1 = gs + alpha * sMs + team_sum(tm, d1p);

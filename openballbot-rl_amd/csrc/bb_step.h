@@ -67,6 +67,8 @@ BB_HD int forward(const ModelT<T>& m, const T* q, const T* v, const T* ctrl, T* 
     atomicAdd(&bb_phase_cycles[10], 1ull);
   }
 #endif
+#pragma unroll
+  for (int i = 0; i < 9; i++) W.RB[i] = k.RB[i];  // the solve rebuilds ground Jacobians from it
   if (so) {
     T qb[4] = {q[3], q[4], q[5], q[6]};
     qnormalize(qb);

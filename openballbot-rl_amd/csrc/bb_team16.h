@@ -69,13 +69,12 @@ __device__ __forceinline__ void static_for(F&& f) {
 // cone_eval (bb_physics.h) without branches: the three zones are computed and
 // selected, so lanes of a team in different zones do not serialise.
 template <typename T>
-__device__ __forceinline__ void cone_sel(const T* jar, T mu, T f1, T f2, const T* D, T* force, T* C) {
+__device__ __forceinline__ void cone_sel(const T* jar, T mu, T f1, T f2, const T* D, T Dm, T* force, T* C) {
   const T U0 = jar[0] * mu, U1 = jar[1] * f1, U2 = jar[2] * f2;
   const T N = U0, Tn = sqrt(U1 * U1 + U2 * U2);
   const bool top = N >= mu * Tn || (Tn <= 0 && N >= 0);
   const bool bot = !top && (mu * N + Tn <= 0 || (Tn <= 0 && N < 0));
-  const T Dm = D[0] / (mu * mu * (1 + mu * mu));
-  const T g = N - mu * Tn;
+  const T g = N - mu * Tn;  // Dm = D0 / (mu^2 (1 + mu^2)) from cone_params
   const T iT = T(1) / (Tn > 0 ? Tn : T(1));
   const T gr1 = -mu * f1 * U1 * iT, gr2 = -mu * f2 * U2 * iT;
   const T sc = -Dm * g;
@@ -93,19 +92,20 @@ __device__ __forceinline__ void cone_sel(const T* jar, T mu, T f1, T f2, const T
 // per-contact cone parameters: wheels (c < 3) use the pair friction and
 // anisotropic D, ground contacts mu = 1 and one D for all rows
 template <typename T>
-__device__ __forceinline__ void cone_params(const ModelT<T>& m, const EnvWork<T>& W, int c, T& mu, T& f1, T& f2,
-                                            T (&D)[3]) {
+__device__ __forceinline__ void cone_params(const ModelT<T>& m, const EnvWork<T>& W, int c, T kdw, T& mu, T& f1,
+                                            T& f2, T (&D)[3], T& Dm) {
   const bool wheel = c < 3;
   const T* Dp = wheel ? &W.wc[c].D[0] : &W.g[(c - 3) * NGF + GF_D];
   const int st = wheel ? 1 : 0;
   D[0] = Dp[0]; D[1] = Dp[st]; D[2] = Dp[2 * st];
+  Dm = D[0] * (wheel ? kdw : T(0.5));  // 1 / (mu^2 (1 + mu^2)), mu = 1 on the ground
   mu = wheel ? m.fr_wheel[0] : T(1);
   f1 = wheel ? m.fr_wheel[0] : T(1);
   f2 = wheel ? m.fr_wheel[1] : T(1);
 }
 
 // Cholesky of the register-distributed H (lane i holds row h[0..14]); on exit
-// lane i holds L_ik (k < i) in h[k] and every lane holds diag[] = L_jj.
+// lane i holds L_ik (k < i) in h[k] and every lane holds diag[] = 1 / L_jj.
 template <typename T>
 __device__ __forceinline__ void chol_rows(T (&h)[NV], T hdi, T (&diag)[NV], int tl) {
   static_for<NV>([&](auto jc) {
@@ -115,7 +115,7 @@ __device__ __forceinline__ void chol_rows(T (&h)[NV], T hdi, T (&diag)[NV], int 
     const T fl = pivot_eps<T>() * maxT(hdj, T(1e-30));
     piv = piv > fl ? piv : fl;
     const T d = sqrt(piv), id = T(1) / d;
-    diag[j] = d;
+    diag[j] = id;  // inverse pivot: the solves multiply
     const T lij = h[j] * id;
     h[j] = tl > j ? lij : h[j];
     static_for<NV - 1 - j>([&](auto kc) {
@@ -140,7 +140,7 @@ __device__ __forceinline__ void chol_solve_rows(const T (&h)[NV], const T (&diag
   T y[NV];
   static_for<NV>([&](auto jc) {
     constexpr int j = decltype(jc)::value;
-    const T yj = bcast<j>(b) / diag[j];
+    const T yj = bcast<j>(b) * diag[j];
     y[j] = yj;
     b -= tl > j ? h[j] * yj : T(0);
   });
@@ -149,10 +149,29 @@ __device__ __forceinline__ void chol_solve_rows(const T (&h)[NV], const T (&diag
   static_for<NV>([&](auto ic) {
     constexpr int i = NV - 1 - decltype(ic)::value;
     const T part = (tl > i && tl < NV) ? h[i] * own : T(0);
-    const T si = (y[i] - tsum(part)) / diag[i];
+    const T si = (y[i] - tsum(part)) * diag[i];
     s[i] = si;
     own = tl == i ? si : own;
   });
+}
+
+// jar(0) = J a - aref and J s of contact c (zeros when c >= nc)
+template <typename T>
+__device__ __forceinline__ void ls_terms(const EnvWork<T>& W, int c, int nc, const T* a, const T* s, T (&c6)[6]) {
+#pragma unroll
+  for (int r = 0; r < 6; r++) c6[r] = 0;
+  if (c >= nc) return;
+  if (c < 3) {
+    const WheelCon<T>& C = W.wc[c];
+#pragma unroll
+    for (int r = 0; r < 3; r++) { c6[r] = wheel_dot(C, c, r, a) - C.aref[r]; c6[3 + r] = wheel_dot(C, c, r, s); }
+  } else {
+    const T* gcn = W.g + (c - 3) * NGF;
+    T J[3][6];
+    ground_rows(gcn, W.RB, J);
+#pragma unroll
+    for (int r = 0; r < 3; r++) { c6[r] = ground_dot(J, r, a) - gcn[GF_AREF + r]; c6[3 + r] = ground_dot(J, r, s); }
+  }
 }
 
 // Newton on f(a); a replicated in every lane of the row.  W.H holds the dense
@@ -162,6 +181,8 @@ __device__ int solve16(const ModelT<T>& m, EnvWork<T>& W, int ng, T* a, int tl) 
   const Mass<T>& M = W.M;
   const int nc = 3 + ng;
   const int row = tl < NV ? tl : NV - 1;
+  const T muw = m.fr_wheel[0];
+  const T kdw = T(1) / (muw * muw * (1 + muw * muw));
   PH_DECL
   int it = 0;
   for (; it < m.maxiter; it++) {
@@ -175,17 +196,18 @@ __device__ int solve16(const ModelT<T>& m, EnvWork<T>& W, int ng, T* a, int tl) 
     for (int c = tl; c < nc; c += L) {
       const bool wheel = c < 3;
       const T* gcn = W.g + (wheel ? 0 : c - 3) * NGF;
-      T jar[3];
+      T jar[3], J[3][6];
       if (wheel) {
 #pragma unroll
         for (int r = 0; r < 3; r++) jar[r] = wheel_dot(W.wc[c], c, r, a) - W.wc[c].aref[r];
       } else {
+        ground_rows(gcn, W.RB, J);
 #pragma unroll
-        for (int r = 0; r < 3; r++) jar[r] = ground_dot(gcn, r, a) - gcn[GF_AREF + r];
+        for (int r = 0; r < 3; r++) jar[r] = ground_dot(J, r, a) - gcn[GF_AREF + r];
       }
-      T mu, f1, f2, D[3], f[3], Cc[6];
-      cone_params(m, W, c, mu, f1, f2, D);
-      cone_sel(jar, mu, f1, f2, D, f, Cc);
+      T mu, f1, f2, D[3], Dm, f[3], Cc[6];
+      cone_params(m, W, c, kdw, mu, f1, f2, D, Dm);
+      cone_sel(jar, mu, f1, f2, D, Dm, f, Cc);
       if (wheel) {
         const WheelCon<T>& C = W.wc[c];
 #pragma unroll
@@ -200,11 +222,7 @@ __device__ int solve16(const ModelT<T>& m, EnvWork<T>& W, int ng, T* a, int tl) 
           else gc[q + 2] -= jf;
         }
       } else {
-        T J[3][6], w[3][6];
-#pragma unroll
-        for (int r = 0; r < 3; r++)
-#pragma unroll
-          for (int i = 0; i < 6; i++) J[r][i] = gcn[GF_J + 6 * r + i];
+        T w[3][6];
 #pragma unroll
         for (int i = 0; i < 6; i++) {
           gc[9 + i] -= J[0][i] * f[0] + J[1][i] * f[1] + J[2][i] * f[2];
@@ -295,19 +313,10 @@ __device__ int solve16(const ModelT<T>& m, EnvWork<T>& W, int ng, T* a, int tl) 
     T sMs = 0, gs = 0;
 #pragma unroll
     for (int i = 0; i < NV; i++) { sMs += s[i] * Ms[i]; gs += s[i] * W.mq[i]; }
-    team_sync();  // the cj buffer is dead; the line-search cache reuses it
-    for (int c = tl; c < nc; c += L) {
-      T* c6 = W.u.ls[c];
-      if (c < 3) {
-        const WheelCon<T>& C = W.wc[c];
-#pragma unroll
-        for (int r = 0; r < 3; r++) { c6[r] = wheel_dot(C, c, r, a) - C.aref[r]; c6[3 + r] = wheel_dot(C, c, r, s); }
-      } else {
-        const T* gcn = W.g + (c - 3) * NGF;
-#pragma unroll
-        for (int r = 0; r < 3; r++) { c6[r] = ground_dot(gcn, r, a) - gcn[GF_AREF + r]; c6[3 + r] = ground_dot(gcn, r, s); }
-      }
-    }
+    // line-search cache: jar(0) and J s of this lane's first contact in
+    // registers; later rounds (more than 16 contacts) recompute them
+    T c6r[6];
+    ls_terms(W, tl, nc, a, s, c6r);
     T lo = 0, dlo = d0, hi = -1, dhi = 0, alpha = 1;
     T flo = d0, fhi = 0;
     int side = 0, same = 0;
@@ -315,13 +324,18 @@ __device__ int solve16(const ModelT<T>& m, EnvWork<T>& W, int ng, T* a, int tl) 
     for (int ls = 1; ls <= m.ls_maxiter; ls++) {
       T d1p = 0, d2p = 0, dmp = 0;
       for (int c = tl; c < nc; c += L) {
-        T mu, f1, f2, D[3];
-        cone_params(m, W, c, mu, f1, f2, D);
-        const T* c6 = W.u.ls[c];
+        T mu, f1, f2, D[3], Dm, c6[6];
+        cone_params(m, W, c, kdw, mu, f1, f2, D, Dm);
+        if (c == tl) {
+#pragma unroll
+          for (int r = 0; r < 6; r++) c6[r] = c6r[r];
+        } else {
+          ls_terms(W, c, nc, a, s, c6);
+        }
         const T x[3] = {c6[3], c6[4], c6[5]};
         const T jr[3] = {c6[0] + alpha * x[0], c6[1] + alpha * x[1], c6[2] + alpha * x[2]};
         T f[3], Cc[6];
-        cone_sel(jr, mu, f1, f2, D, f, Cc);
+        cone_sel(jr, mu, f1, f2, D, Dm, f, Cc);
         d1p -= f[0] * x[0] + f[1] * x[1] + f[2] * x[2];
         dmp += fabs(f[0] * x[0]) + fabs(f[1] * x[1]) + fabs(f[2] * x[2]);
         d2p += Cc[0] * x[0] * x[0] + Cc[1] * x[1] * x[1] + Cc[2] * x[2] * x[2] +
@@ -433,16 +447,9 @@ __device__ __forceinline__ int collide_team(const ModelT<T>& m, const Kin<T>& k,
         T pv[3], tt[3];
         cross3(tt, wB, lv);
         pv[0] = v[9] + tt[0]; pv[1] = v[10] + tt[1]; pv[2] = v[11] + tt[2];
-        const T* F[3] = {nn, t1, t2};
         T* gs = g + slot * NGF;
 #pragma unroll
-        for (int rw = 0; rw < 3; rw++) {
-          T x1[3], x2[3];
-          cross3(x1, lv, F[rw]);
-          mtv3(x2, k.RB, x1);
-#pragma unroll
-          for (int i = 0; i < 3; i++) { gs[GF_J + 6 * rw + i] = F[rw][i]; gs[GF_J + 6 * rw + 3 + i] = x2[i]; }
-        }
+        for (int i = 0; i < 3; i++) { gs[GF_N + i] = nn[i]; gs[GF_LV + i] = lv[i]; }
         gs[GF_AREF + 0] = -m.Bd * dot3(nn, pv) - m.K * imp * dist;
         gs[GF_AREF + 1] = -m.Bd * dot3(t1, pv);
         gs[GF_AREF + 2] = -m.Bd * dot3(t2, pv);

@@ -35,7 +35,7 @@ extern "C" {
 #define BBO_NU 3
 #define BBO_NBODY 8
 #define BBO_HF_N 293          /* ballbot.xml:23 nrow = ncol = 293 */
-#define BBO_MAXGROUND 24      /* cap on ball-hfield contacts (MuJoCo: mjMAXCONPAIR=50; max observed 20) */
+#define BBO_MAXGROUND 50      /* cap on ball-hfield contacts = MuJoCo mjMAXCONPAIR */
 #define BBO_MAXCON (3 + BBO_MAXGROUND)
 
 /* option flags for invariant tests (0 = reference behaviour) */

@@ -16,7 +16,7 @@ ROOT = Path(__file__).resolve().parent.parent
 ORACLE_DIR = ROOT / "oracle"
 LIB_PATH = ORACLE_DIR / "_build" / "libbb_oracle.so"
 
-NQ, NV, NB, MAXCON = 17, 15, 8, 27
+NQ, NV, NB, MAXCON = 17, 15, 8, 53
 HF_N = 293
 
 DISABLE_CONTACT, DISABLE_GRAVITY, DISABLE_DAMPING = 1, 2, 4
