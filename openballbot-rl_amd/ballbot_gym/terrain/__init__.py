@@ -3,8 +3,9 @@
 Registered on import like the reference (ballbot_gym/terrain/__init__.py:18-36).
 The batched env evaluates them host-side once per bank slot (reset-time work,
 never on the step path) and uploads the heightfields with bb_set_hfield.
-Every numpy generator is pinned bit-for-bit (or to 1e-12) against the
-reference's outputs in tests/golden/terrains.npz."""
+Every numpy generator is pinned bit-for-bit against the reference's outputs
+in tests/golden/terrains.npz; perlin restates the `noise` library's simplex
+fBm (absent here) and is property-tested only (parity unpinned)."""
 import numpy as np
 
 from ballbot_gym.core.registry import ComponentRegistry
@@ -12,6 +13,7 @@ from ballbot_gym.terrain.bowl import generate_bowl_terrain
 from ballbot_gym.terrain.gradient import generate_gradient_terrain
 from ballbot_gym.terrain.hills import generate_hills_terrain
 from ballbot_gym.terrain.mixed import generate_mixed_terrain
+from ballbot_gym.terrain.perlin import generate_perlin_terrain
 from ballbot_gym.terrain.ramp import generate_ramp_terrain
 from ballbot_gym.terrain.ridge_valley import generate_ridge_valley_terrain
 from ballbot_gym.terrain.sinusoidal import generate_sinusoidal_terrain
@@ -27,6 +29,7 @@ def generate_flat_terrain(n: int, **kwargs) -> np.ndarray:
 
 
 BUILTIN_TERRAINS = {
+    "perlin": generate_perlin_terrain,
     "stepped": generate_stepped_terrain,
     "ramp": generate_ramp_terrain,
     "sinusoidal": generate_sinusoidal_terrain,

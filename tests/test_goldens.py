@@ -147,3 +147,22 @@ def test_registry_and_factory_errors_match_reference(clean_registry):
     lists = ref["_lists"]
     assert R.list_rewards() == lists["rewards"] and R.list_terrains() == lists["terrains"]
     assert R.list_policies() == lists["policies"] and R.list_sensors() == lists["sensors"]
+
+
+def test_perlin_properties():
+    """Perlin parity is UNPINNED (noise.snoise2 is absent); the reference's own
+    checks (test_terrains.py:22-44) plus value range and smoothness."""
+    from ballbot_gym.terrain import BUILTIN_TERRAINS
+    from ballbot_gym.core.factories import create_terrain
+
+    a = BUILTIN_TERRAINS["perlin"](129, seed=42)
+    assert a.shape == (129 * 129,) and a.min() >= 0.0 and a.max() <= 1.0
+    np.testing.assert_array_equal(a, BUILTIN_TERRAINS["perlin"](129, seed=42))
+    assert not np.allclose(a, BUILTIN_TERRAINS["perlin"](129, seed=43))
+    assert 0.3 < a.mean() < 0.7 and a.std() > 0.05
+    g = a.reshape(129, 129)
+    assert np.abs(np.diff(g, axis=0)).max() < 0.2 and np.abs(np.diff(g, axis=1)).max() < 0.2
+    t = create_terrain({"type": "perlin", "config": {"scale": 25.0, "octaves": 4, "seed": 42}})(129)
+    np.testing.assert_array_equal(t, a)
+    grad = BUILTIN_TERRAINS["gradient"](33, gradient_type="perlin", seed=5)
+    assert grad.min() == 0.0 and grad.max() == 1.0
