@@ -525,7 +525,7 @@ static void mul6(double* r, const double* I6, const double* v) {
 /* ------------------------------------------------------------- collision */
 typedef struct {
   double dist, pos[3], frame[9];
-  int body2;   /* 4..6 wheel (geom1 = ball), 7 = ball (geom1 = hfield) */
+  int body1, body2; /* jacdif = J(body2) - J(body1); normal points from geom1 (body1) to geom2 (body2) */
   double mu, fr[2];
 } Contact;
 
@@ -630,8 +630,313 @@ static int sphere_prism(const double* c, double r, double T[3][3], double zb, do
   return 1;
 }
 
+
+/* ---------------------------------------------- dynamic (contype) pairs
+ * Besides the explicit ball-wheel pairs and ball-hfield, MuJoCo's broadphase
+ * collides every other geom pair not filtered out (contype = conaffinity = 1
+ * by default; ballbot.xml has no <exclude>; parent-child pairs are filtered,
+ * the world body excepted):
+ *   hfield x {tower cylinder, cam sticks (capsules), wheel capsules}
+ *   ball   x {tower cylinder, cam sticks}
+ * (ballast has contype 0; cam cone meshes are absent from the reference).
+ * Contact geometry is exact: minimum-translation penetration by the
+ * separating-axis theorem for capsule-prism (exact: prism face normals and
+ * segment x edge axes) and cylinder-prism (face normals, cylinder axis,
+ * axis x edges, vertex radials: exact except rim-edge contacts), closed form
+ * for sphere-cylinder.  MuJoCo runs its convex penetration solver (MPR/EPA)
+ * there, which agrees to its ccd tolerance. */
+typedef struct { double c[3], a[3], hh, r; } Convex; /* capsule or cylinder: centre, unit axis, half-length, radius */
+
+typedef struct { double V[6][3]; double pn[5][3], pd[5]; } Prism;
+
+static void prism_build(Prism* P, double T[3][3], double zb) {
+  for (int i = 0; i < 3; i++) {
+    v3copy(P->V[i], T[i]);
+    P->V[3 + i][0] = T[i][0]; P->V[3 + i][1] = T[i][1]; P->V[3 + i][2] = zb;
+  }
+  double e1[3], e2[3], nt[3];
+  v3sub(e1, T[1], T[0]); v3sub(e2, T[2], T[0]);
+  v3cross(nt, e1, e2);
+  if (nt[2] < 0) v3scl(nt, nt, -1);
+  v3normalize(nt);
+  v3copy(P->pn[0], nt); P->pd[0] = v3dot(nt, T[0]);
+  P->pn[1][0] = 0; P->pn[1][1] = 0; P->pn[1][2] = -1; P->pd[1] = -zb;
+  double area = (T[1][0] - T[0][0]) * (T[2][1] - T[0][1]) - (T[2][0] - T[0][0]) * (T[1][1] - T[0][1]);
+  double sgn = area > 0 ? 1 : -1;
+  for (int i = 0; i < 3; i++) {
+    const double* A = T[i]; const double* B = T[(i + 1) % 3];
+    double ex = B[0] - A[0], ey = B[1] - A[1];
+    double nx = ey * sgn, ny = -ex * sgn, nl = sqrt(nx * nx + ny * ny);
+    P->pn[2 + i][0] = nx / nl; P->pn[2 + i][1] = ny / nl; P->pn[2 + i][2] = 0;
+    P->pd[2 + i] = v3dot(P->pn[2 + i], A);
+  }
+}
+
+static double prism_support(const Prism* P, const double* n) {
+  double m = -1e300;
+  for (int i = 0; i < 6; i++) { double d = v3dot(n, P->V[i]); if (d > m) m = d; }
+  return m;
+}
+
+/* closest points of segments p0p1 and q0q1 (Ericson 5.1.9) */
+static double seg_seg(const double* p0, const double* p1, const double* q0, const double* q1, double* cp, double* cq) {
+  double d1[3], d2[3], r[3];
+  v3sub(d1, p1, p0); v3sub(d2, q1, q0); v3sub(r, p0, q0);
+  double a = v3dot(d1, d1), e = v3dot(d2, d2), f = v3dot(d2, r), s, t;
+  if (a <= 1e-30 && e <= 1e-30) { s = t = 0; }
+  else if (a <= 1e-30) { s = 0; t = f / e; t = t < 0 ? 0 : (t > 1 ? 1 : t); }
+  else {
+    double c = v3dot(d1, r);
+    if (e <= 1e-30) { t = 0; s = -c / a; s = s < 0 ? 0 : (s > 1 ? 1 : s); }
+    else {
+      double b = v3dot(d1, d2), den = a * e - b * b;
+      s = den > 0 ? (b * f - c * e) / den : 0;
+      s = s < 0 ? 0 : (s > 1 ? 1 : s);
+      t = (b * s + f) / e;
+      if (t < 0) { t = 0; s = -c / a; s = s < 0 ? 0 : (s > 1 ? 1 : s); }
+      else if (t > 1) { t = 1; s = (b - c) / a; s = s < 0 ? 0 : (s > 1 ? 1 : s); }
+    }
+  }
+  for (int i = 0; i < 3; i++) { cp[i] = p0[i] + s * d1[i]; cq[i] = q0[i] + t * d2[i]; }
+  double d[3]; v3sub(d, cp, cq);
+  return v3norm(d);
+}
+
+/* distance of segment p0p1 to triangle abc (0 if they intersect) */
+static double seg_tri(const double* p0, const double* p1, const double* a, const double* b, const double* c,
+                      double* cp, double* ct) {
+  double e1[3], e2[3], n[3], d[3];
+  v3sub(e1, b, a); v3sub(e2, c, a); v3cross(n, e1, e2); v3sub(d, p1, p0);
+  double den = v3dot(n, d);
+  if (fabs(den) > 1e-30) {
+    double ap[3]; v3sub(ap, a, p0);
+    double t = v3dot(n, ap) / den;
+    if (t >= 0 && t <= 1) {
+      double x[3]; for (int i = 0; i < 3; i++) x[i] = p0[i] + t * d[i];
+      double q[3]; closest_pt_triangle(q, x, a, b, c);
+      double dd[3]; v3sub(dd, x, q);
+      if (v3dot(dd, dd) < 1e-28) { v3copy(cp, x); v3copy(ct, x); return 0; }
+    }
+  }
+  double best = 1e300, q[3], dd[3], x1[3], x2[3];
+  const double* ends[2] = {p0, p1};
+  for (int k = 0; k < 2; k++) {
+    closest_pt_triangle(q, ends[k], a, b, c);
+    v3sub(dd, ends[k], q);
+    double dist = v3norm(dd);
+    if (dist < best) { best = dist; v3copy(cp, ends[k]); v3copy(ct, q); }
+  }
+  const double* E[3][2] = {{a, b}, {b, c}, {c, a}};
+  for (int k = 0; k < 3; k++) {
+    double dist = seg_seg(p0, p1, E[k][0], E[k][1], x1, x2);
+    if (dist < best) { best = dist; v3copy(cp, x1); v3copy(ct, x2); }
+  }
+  return best;
+}
+
+static void convex_ends(const Convex* g, double* p0, double* p1) {
+  for (int i = 0; i < 3; i++) { p0[i] = g->c[i] - g->hh * g->a[i]; p1[i] = g->c[i] + g->hh * g->a[i]; }
+}
+
+/* separating-axis depth along unit n for the segment of g (capsule core) vs prism:
+ * how far the segment must move along +n to clear the prism */
+static double seg_axis_depth(const Prism* P, const double* p0, const double* p1, const double* n) {
+  double lo = fmin(v3dot(n, p0), v3dot(n, p1));
+  return prism_support(P, n) - lo;
+}
+
+/* capsule vs prism; normal from prism to capsule */
+static int capsule_prism(const Convex* g, const Prism* P, double* dist, double* n, double* pos) {
+  double p0[3], p1[3];
+  convex_ends(g, p0, p1);
+  /* segment inside prism?  clip against the 5 half-spaces n.x <= d */
+  double t0 = 0, t1 = 1, dir[3];
+  v3sub(dir, p1, p0);
+  int inter = 1;
+  for (int f = 0; f < 5 && inter; f++) {
+    double a0 = v3dot(P->pn[f], p0) - P->pd[f], ad = v3dot(P->pn[f], dir);
+    if (fabs(ad) < 1e-30) { if (a0 > 0) inter = 0; continue; }
+    double t = -a0 / ad;
+    if (ad > 0) { if (t < t1) t1 = t; } else { if (t > t0) t0 = t; }
+    if (t0 > t1) inter = 0;
+  }
+  if (!inter) {
+    static const int tri[8][3] = {{0, 1, 2}, {3, 4, 5}, {0, 1, 4}, {0, 4, 3}, {1, 2, 5}, {1, 5, 4}, {2, 0, 3}, {2, 3, 5}};
+    double best = 1e300, cp[3] = {0}, cq[3] = {0}, bp[3] = {0}, bq[3] = {0};
+    for (int f = 0; f < 8; f++) {
+      double d = seg_tri(p0, p1, P->V[tri[f][0]], P->V[tri[f][1]], P->V[tri[f][2]], cp, cq);
+      if (d < best) { best = d; v3copy(bp, cp); v3copy(bq, cq); }
+    }
+    if (best >= g->r) return 0;
+    if (best > 1e-12) { v3sub(n, bp, bq); v3scl(n, n, 1.0 / best); }
+    else { v3copy(n, P->pn[0]); }
+    *dist = best - g->r;
+    for (int i = 0; i < 3; i++) pos[i] = bp[i] - n[i] * (g->r + *dist / 2);
+    return 1;
+  }
+  /* intersecting: minimum over the separating-axis candidates */
+  double axes[5 + 4][3];
+  int na = 0;
+  for (int f = 0; f < 5; f++) v3copy(axes[na++], P->pn[f]);
+  double u[3]; v3copy(u, dir);
+  double edges[4][3] = {{0, 0, 1}};
+  for (int i = 0; i < 3; i++) v3sub(edges[1 + i], P->V[(i + 1) % 3], P->V[i]);
+  for (int k = 0; k < 4; k++) {
+    double x[3]; v3cross(x, u, edges[k]);
+    if (v3norm(x) > 1e-12 * (v3norm(u) * v3norm(edges[k]) + 1e-30)) { v3normalize(x); v3copy(axes[na++], x); }
+  }
+  double bestd = 1e300, bn[3] = {0, 0, 1};
+  for (int k = 0; k < na; k++)
+    for (int sgn = -1; sgn <= 1; sgn += 2) {
+      double ax[3]; v3scl(ax, axes[k], sgn);
+      double d = seg_axis_depth(P, p0, p1, ax);
+      if (d < bestd) { bestd = d; v3copy(bn, ax); }
+    }
+  v3copy(n, bn);
+  *dist = -bestd - g->r;
+  /* deepest segment point along -n; when the segment is (nearly) normal to
+   * -n the deepest set is the clipped part [t0, t1] of the segment: take the
+   * point of it nearest the prism centroid */
+  double e0 = v3dot(n, p0), e1 = v3dot(n, p1), xd[3];
+  if (fabs(e0 - e1) < 1e-12) {
+    double cen[3] = {0, 0, 0}, dd = v3dot(dir, dir);
+    for (int v = 0; v < 6; v++) for (int i = 0; i < 3; i++) cen[i] += P->V[v][i] / 6;
+    double cp0[3]; v3sub(cp0, cen, p0);
+    double t = dd > 0 ? v3dot(cp0, dir) / dd : 0;
+    t = t < t0 ? t0 : (t > t1 ? t1 : t);
+    for (int i = 0; i < 3; i++) xd[i] = p0[i] + t * dir[i];
+  } else {
+    v3copy(xd, e0 < e1 ? p0 : p1);
+  }
+  for (int i = 0; i < 3; i++) pos[i] = xd[i] - n[i] * (g->r + *dist / 2);
+  return 1;
+}
+
+static double cyl_support(const Convex* g, const double* n) {
+  double na = v3dot(n, g->a);
+  double rad = 1 - na * na;
+  return v3dot(n, g->c) + g->hh * fabs(na) + g->r * sqrt(rad > 0 ? rad : 0);
+}
+
+/* cylinder vs prism; normal from prism to cylinder */
+static int cylinder_prism(const Convex* g, const Prism* P, double* dist, double* n, double* pos) {
+  double axes[5 + 1 + 4 + 6][3];
+  int na = 0;
+  for (int f = 0; f < 5; f++) v3copy(axes[na++], P->pn[f]);
+  v3copy(axes[na++], g->a);
+  double edges[4][3] = {{0, 0, 1}};
+  for (int i = 0; i < 3; i++) v3sub(edges[1 + i], P->V[(i + 1) % 3], P->V[i]);
+  for (int k = 0; k < 4; k++) {
+    double x[3]; v3cross(x, g->a, edges[k]);
+    if (v3norm(x) > 1e-12 * (v3norm(edges[k]) + 1e-30)) { v3normalize(x); v3copy(axes[na++], x); }
+  }
+  for (int i = 0; i < 6; i++) {
+    double d[3], x[3]; v3sub(d, P->V[i], g->c);
+    double t = v3dot(d, g->a);
+    for (int k = 0; k < 3; k++) x[k] = d[k] - t * g->a[k];
+    if (v3norm(x) > 1e-12) { v3normalize(x); v3copy(axes[na++], x); }
+  }
+  double bestd = 1e300, bn[3] = {0, 0, 1};
+  for (int k = 0; k < na; k++)
+    for (int sgn = -1; sgn <= 1; sgn += 2) {
+      double ax[3], mx[3]; v3scl(ax, axes[k], sgn);
+      v3scl(mx, ax, -1);
+      double d = prism_support(P, ax) + cyl_support(g, mx); /* = max_P ax.y - min_C ax.x */
+      if (d <= 0) return 0; /* separating axis */
+      if (d < bestd) { bestd = d; v3copy(bn, ax); }
+    }
+  v3copy(n, bn);
+  *dist = -bestd;
+  /* deepest cylinder point along -n; in the degenerate directions (n normal
+   * to the axis: a generator line; n along the axis: a cap disk) the point of
+   * that set nearest the prism centroid */
+  double na2 = v3dot(n, g->a), s[3], rad[3], cen[3] = {0, 0, 0}, dc[3];
+  for (int v = 0; v < 6; v++) for (int k = 0; k < 3; k++) cen[k] += P->V[v][k] / 6;
+  v3sub(dc, cen, g->c);
+  for (int k = 0; k < 3; k++) rad[k] = n[k] - na2 * g->a[k];
+  double rl = v3norm(rad);
+  double along;
+  if (fabs(na2) > 1e-9) along = na2 > 0 ? -g->hh : g->hh;
+  else { along = v3dot(dc, g->a); along = along > g->hh ? g->hh : (along < -g->hh ? -g->hh : along); }
+  for (int k = 0; k < 3; k++) s[k] = g->c[k] + along * g->a[k];
+  if (rl > 1e-9) {
+    for (int k = 0; k < 3; k++) s[k] -= g->r * rad[k] / rl;
+  } else {
+    double pr[3], t = v3dot(dc, g->a);
+    for (int k = 0; k < 3; k++) pr[k] = dc[k] - t * g->a[k];
+    double pl = v3norm(pr);
+    if (pl > g->r) v3scl(pr, pr, g->r / pl);
+    for (int k = 0; k < 3; k++) s[k] += pr[k];
+  }
+  for (int k = 0; k < 3; k++) pos[k] = s[k] - n[k] * (*dist / 2);
+  return 1;
+}
+
+/* sphere (geom1) vs cylinder (geom2): normal from sphere to cylinder */
+static int sphere_cylinder(const double* c, double r, const Convex* g, double* dist, double* n, double* pos) {
+  double d[3]; v3sub(d, c, g->c);
+  double z = v3dot(d, g->a), rv[3];
+  for (int k = 0; k < 3; k++) rv[k] = d[k] - z * g->a[k];
+  double rho = v3norm(rv), u[3] = {0, 0, 0};
+  if (rho > 1e-12) v3scl(u, rv, 1.0 / rho);
+  int inside = fabs(z) <= g->hh && rho <= g->r;
+  double q[3];
+  if (!inside) {
+    double zc = z > g->hh ? g->hh : (z < -g->hh ? -g->hh : z);
+    double rc = rho > g->r ? g->r : rho;
+    for (int k = 0; k < 3; k++) q[k] = g->c[k] + zc * g->a[k] + rc * u[k];
+    double dq[3]; v3sub(dq, q, c);
+    double dd = v3norm(dq);
+    if (dd >= r) return 0;
+    *dist = dd - r;
+    if (dd > 1e-12) v3scl(n, dq, 1.0 / dd); else v3copy(n, g->a);
+  } else {
+    double ds = g->r - rho, dc = g->hh - fabs(z);
+    if (ds < dc) { /* exit through the side: the cylinder surface lies outward along u */
+      for (int k = 0; k < 3; k++) n[k] = -u[k];
+      *dist = -ds - r;
+    } else {
+      double sg = z >= 0 ? 1 : -1;
+      for (int k = 0; k < 3; k++) n[k] = -sg * g->a[k];
+      *dist = -dc - r;
+    }
+  }
+  for (int k = 0; k < 3; k++) pos[k] = c[k] + n[k] * (r + *dist / 2);
+  return 1;
+}
+
+/* world poses of the convex geoms of the base tree: 0 tower, 1-2 cam sticks, 3-5 wheels */
+static void body_geoms(const double xpos[NB][3], const double xmat[NB][9], Convex g[6], int cyl[6], int body[6]) {
+  Model* m = &M_;
+  double t[3];
+  /* tower_collision: cylinder r .11 hh .14 at (0,0,0.2) of base (ballbot.xml:41) */
+  m3v(t, xmat[1], (double[3]){0, 0, 0.2});
+  v3add(g[0].c, xpos[1], t);
+  g[0].a[0] = xmat[1][2]; g[0].a[1] = xmat[1][5]; g[0].a[2] = xmat[1][8];
+  g[0].hh = 0.14; g[0].r = 0.11; cyl[0] = 1; body[0] = 1;
+  /* cam_k_stick: capsule fromto (0,0,0)->(-+0.2,0,0), r .01 (ballbot.xml:46,52) */
+  for (int k = 0; k < 2; k++) {
+    int b = 2 + k;
+    double lc[3] = {k == 0 ? -0.1 : 0.1, 0, 0};
+    m3v(t, xmat[b], lc);
+    v3add(g[1 + k].c, xpos[b], t);
+    g[1 + k].a[0] = xmat[b][0]; g[1 + k].a[1] = xmat[b][3]; g[1 + k].a[2] = xmat[b][6];
+    g[1 + k].hh = 0.1; g[1 + k].r = 0.01; cyl[1 + k] = 0; body[1 + k] = b;
+  }
+  /* wheel_mesh_k: capsule r .025 hh .02 (ballbot.xml:57,62,68) */
+  for (int k = 0; k < 3; k++) {
+    int b = 4 + k;
+    double gm[9];
+    m3v(t, xmat[b], WHEEL_GPOS);
+    v3add(g[3 + k].c, xpos[b], t);
+    m3mul(gm, xmat[b], m->wheel_gmat);
+    g[3 + k].a[0] = gm[2]; g[3 + k].a[1] = gm[5]; g[3 + k].a[2] = gm[8];
+    g[3 + k].hh = WHEEL_HH; g[3 + k].r = WHEEL_R; cyl[3 + k] = 0; body[3 + k] = b;
+  }
+}
+
 static int collide(const double xpos[NB][3], const double xmat[NB][9], const float* hf, double size_z,
-                   Contact* con, int* nground_out, int* overflow) {
+                   Contact* con, int* nground_out, int* nbody_out, int* overflow) {
   Model* m = &M_;
   int n = 0;
   double c[3], t[3];
@@ -666,7 +971,7 @@ static int collide(const double xpos[NB][3], const double xmat[NB][9], const flo
     v3copy(cc->frame + 3, axis); /* mujoco_fix.patch:15 */
     make_frame(cc->frame);
     for (int i = 0; i < 3; i++) cc->pos[i] = c[i] + cc->frame[i] * (BALL_R + dist / 2);
-    cc->body2 = b;
+    cc->body1 = 7; cc->body2 = b;
     cc->fr[0] = 0.001; cc->fr[1] = 1.0;
   }
   int nground = 0;
@@ -709,7 +1014,7 @@ static int collide(const double xpos[NB][3], const double xmat[NB][9], const flo
             v3copy(g->frame, nn);
             make_frame(g->frame);
             v3copy(g->pos, pos);
-            g->body2 = 7;
+            g->body1 = 0; g->body2 = 7;
             g->fr[0] = 1.0; g->fr[1] = 1.0; /* max(geom friction) = (1,1,0.005,..) */
             nground++;
           }
@@ -718,6 +1023,98 @@ static int collide(const double xpos[NB][3], const double xmat[NB][9], const flo
     }
   }
   *nground_out = nground;
+
+  /* dynamic pairs with the base-tree geoms (see body_geoms) */
+  Convex bg[6];
+  int cyl[6], bbody[6];
+  body_geoms(xpos, xmat, bg, cyl, bbody);
+  int nbody = 0;
+  /* ball (geom1, sphere) x tower (cylinder) / cam sticks (capsules, patched frame) */
+  for (int k = 0; k < 3; k++) {
+    double dist, nn[3], pos[3];
+    int hit;
+    if (cyl[k]) {
+      hit = sphere_cylinder(c, BALL_R, &bg[k], &dist, nn, pos);
+    } else {
+      double p0[3], p1[3], cp[3], cq[3];
+      convex_ends(&bg[k], p0, p1);
+      double d = seg_seg(c, c, p0, p1, cp, cq);
+      dist = d - BALL_R - bg[k].r;
+      hit = dist <= 0;
+      if (hit) {
+        if (d > 0) { v3sub(nn, cq, c); v3scl(nn, nn, 1.0 / d); } else { nn[0] = 1; nn[1] = nn[2] = 0; }
+        for (int i = 0; i < 3; i++) pos[i] = c[i] + nn[i] * (BALL_R + dist / 2);
+      }
+    }
+    if (!hit) continue;
+    if (nbody >= BBO_MAXBODY) { *overflow |= 2; continue; }
+    Contact* b = &con[n++];
+    memset(b, 0, sizeof *b);
+    b->dist = dist;
+    v3copy(b->frame, nn);
+    if (!cyl[k]) v3copy(b->frame + 3, bg[k].a); /* mujoco_fix.patch: capsule axis as first tangent */
+    make_frame(b->frame);
+    v3copy(b->pos, pos);
+    b->body1 = 7; b->body2 = bbody[k];
+    b->fr[0] = 1.0; b->fr[1] = 1.0;
+    nbody++;
+  }
+  /* hfield (geom1) x convex geom (mjc_ConvexHField): prisms under the geom's AABB */
+  if (hf) {
+    const double sx = HF_SIZE[0], sy = HF_SIZE[1], zb = HF_SIZE[3];
+    const int nrow = BBO_HF_N, ncol = BBO_HF_N;
+    const double dx = 2 * sx / (ncol - 1), dy = 2 * sy / (nrow - 1);
+    for (int k = 0; k < 6; k++) {
+      const Convex* g = &bg[k];
+      double lo[3], hi[3];
+      for (int i = 0; i < 3; i++) {
+        double ai = fabs(g->a[i]);
+        double ext = cyl[k] ? g->hh * ai + g->r * sqrt(fmax(0.0, 1 - ai * ai)) : g->hh * ai + g->r;
+        lo[i] = g->c[i] - ext; hi[i] = g->c[i] + ext;
+      }
+      if (lo[0] > sx || hi[0] < -sx || lo[1] > sy || hi[1] < -sy || lo[2] > size_z || hi[2] < -zb) continue;
+      int cmin = (int)floor((lo[0] + sx) / (2 * sx) * (ncol - 1));
+      int cmax = (int)ceil((hi[0] + sx) / (2 * sx) * (ncol - 1));
+      int rmin = (int)floor((lo[1] + sy) / (2 * sy) * (nrow - 1));
+      int rmax = (int)ceil((hi[1] + sy) / (2 * sy) * (nrow - 1));
+      if (cmin < 0) cmin = 0;
+      if (cmax > ncol - 1) cmax = ncol - 1;
+      if (rmin < 0) rmin = 0;
+      if (rmax > nrow - 1) rmax = nrow - 1;
+      for (int r = rmin; r < rmax; r++) {
+        double win[3][3] = {{0}};
+        int nvert = 0;
+        for (int cc = cmin; cc <= cmax; cc++) {
+          for (int i = 0; i < 2; i++) {
+            win[0][0] = win[1][0]; win[0][1] = win[1][1]; win[0][2] = win[1][2];
+            win[1][0] = win[2][0]; win[1][1] = win[2][1]; win[1][2] = win[2][2];
+            win[2][0] = dx * cc - sx;
+            win[2][1] = dy * (r + i) - sy;
+            win[2][2] = (double)hf[(r + i) * ncol + cc] * size_z;
+            nvert++;
+            if (nvert <= 2) continue;
+            if (win[0][2] < lo[2] && win[1][2] < lo[2] && win[2][2] < lo[2]) continue;
+            Prism P;
+            prism_build(&P, win, -zb);
+            double dist, nn[3], pos[3];
+            int hit = cyl[k] ? cylinder_prism(g, &P, &dist, nn, pos) : capsule_prism(g, &P, &dist, nn, pos);
+            if (!hit) continue;
+            if (nbody >= BBO_MAXBODY) { *overflow |= 2; continue; }
+            Contact* b = &con[n++];
+            memset(b, 0, sizeof *b);
+            b->dist = dist;
+            v3copy(b->frame, nn);
+            make_frame(b->frame);
+            v3copy(b->pos, pos);
+            b->body1 = 0; b->body2 = bbody[k];
+            b->fr[0] = 1.0; b->fr[1] = 1.0;
+            nbody++;
+          }
+        }
+      }
+    }
+  }
+  *nbody_out = nbody;
   return n;
 }
 
@@ -932,9 +1329,9 @@ static void forward_impl(const double* qpos, const double* qvel, const double* c
 
   /* collision + constraints */
   Contact con[BBO_MAXCON];
-  int nground = 0, overflow = 0;
+  int nground = 0, nbody = 0, overflow = 0;
   int nc = 0;
-  if (!(g_flags & BBO_DISABLE_CONTACT)) nc = collide(w->xpos, w->xmat, hf, size_z, con, &nground, &overflow);
+  if (!(g_flags & BBO_DISABLE_CONTACT)) nc = collide(w->xpos, w->xmat, hf, size_z, con, &nground, &nbody, &overflow);
   static __thread Efc E;
   E.nc = nc;
   const double dmax = 0.95, tc = fmax(0.02, 2 * TIMESTEP), dr = 1.0;
@@ -944,7 +1341,7 @@ static void forward_impl(const double* qpos, const double* qvel, const double* c
     /* jacdif = jac(body2, pos) - jac(body1, pos); body1 = ball for wheel pairs, world for hfield */
     double jd[3][NV];
     memset(jd, 0, sizeof jd);
-    int b2 = cc->body2, b1 = (b2 == 7) ? 0 : 7;
+    int b2 = cc->body2, b1 = cc->body1;
     for (int side = 0; side < 2; side++) {
       int b = side == 0 ? b2 : b1;
       double sg = side == 0 ? 1 : -1;
@@ -996,11 +1393,13 @@ static void forward_impl(const double* qpos, const double* qvel, const double* c
     memcpy(out->cvel_base, w->cvel[1], 6 * sizeof(double));
     v3copy(out->subtree_com_base, w->scom[1]);
     out->ncon = nc; out->nground = nground; out->niter = niter; out->ground_overflow = overflow;
+    out->nbody = nbody;
     for (int c = 0; c < nc && c < BBO_MAXCON; c++) {
       out->con_dist[c] = con[c].dist;
       memcpy(out->con_pos + 3 * c, con[c].pos, 3 * sizeof(double));
       memcpy(out->con_frame + 9 * c, con[c].frame, 9 * sizeof(double));
       out->con_body2[c] = con[c].body2;
+      out->con_body1[c] = con[c].body1;
     }
     double ek = 0;
     for (int i = 0; i < NV; i++) for (int j = 0; j < NV; j++) ek += 0.5 * qvel[i] * w->M[i * NV + j] * qvel[j];

@@ -36,7 +36,8 @@ extern "C" {
 #define BBO_NBODY 8
 #define BBO_HF_N 293          /* ballbot.xml:23 nrow = ncol = 293 */
 #define BBO_MAXGROUND 50      /* cap on ball-hfield contacts = MuJoCo mjMAXCONPAIR */
-#define BBO_MAXCON (3 + BBO_MAXGROUND)
+#define BBO_MAXBODY 16        /* cap on base-tree geom contacts (hfield x tower/sticks/wheels, ball x tower/sticks) */
+#define BBO_MAXCON (3 + BBO_MAXGROUND + BBO_MAXBODY)
 
 /* option flags for invariant tests (0 = reference behaviour) */
 #define BBO_DISABLE_CONTACT 1
@@ -58,7 +59,9 @@ typedef struct {
   double con_frame[BBO_MAXCON * 9];
   int con_body2[BBO_MAXCON];    /* 4..6 = wheel (ball is geom1), 7 = ball vs hfield */
   double energy_kin, energy_pot;
-  int ground_overflow;
+  int ground_overflow;          /* bit 0: ball-hfield cap, bit 1: base-tree contact cap */
+  int nbody;                    /* base-tree geom contacts (after the 3 wheel + nground ball contacts) */
+  int con_body1[BBO_MAXCON];    /* 0 world (hfield), 7 ball */
 } bbo_forward_out;
 
 /* Env configuration mirroring BBotSimulation.__init__ (ballbot_env.py:157-231). */

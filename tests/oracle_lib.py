@@ -16,7 +16,7 @@ ROOT = Path(__file__).resolve().parent.parent
 ORACLE_DIR = ROOT / "oracle"
 LIB_PATH = ORACLE_DIR / "_build" / "libbb_oracle.so"
 
-NQ, NV, NB, MAXCON = 17, 15, 8, 53
+NQ, NV, NB, MAXCON = 17, 15, 8, 69
 HF_N = 293
 
 DISABLE_CONTACT, DISABLE_GRAVITY, DISABLE_DAMPING = 1, 2, 4
@@ -42,6 +42,8 @@ class ForwardOut(C.Structure):
         ("energy_kin", C.c_double),
         ("energy_pot", C.c_double),
         ("ground_overflow", C.c_int),
+        ("nbody", C.c_int),
+        ("con_body1", C.c_int * MAXCON),
     ]
 
 

@@ -183,3 +183,72 @@ def test_ball_rests_on_plane(oracle):
     assert fo.nground >= 1
     ball_bottom = q[12] - 0.14 - 0.09
     assert -5e-3 < ball_bottom < 1e-3
+
+
+def _rotx(deg):
+    t = np.radians(deg)
+    return np.array([np.cos(t / 2), np.sin(t / 2), 0.0, 0.0])
+
+
+def test_no_body_contacts_when_upright(oracle):
+    hf = oracle.flat_hfield()
+    q, v, _ = oracle.reset_state(oracle.init_offset(hf))
+    fo = oracle.forward(q, v, np.zeros(3), None, hf)
+    assert fo.nbody == 0 and fo.ncon == fo.nground + 3
+
+
+def test_tower_on_flat_ground_geometry(oracle):
+    """Dynamic hfield x tower-cylinder pair: base rolled 90 deg and lowered
+    so the tower's side is 1 cm into flat ground; interior prisms report the
+    exact depth with normal +z, every contact is terrain(world) -> base."""
+    hf = oracle.flat_hfield()
+    q, v, _ = oracle.reset_state(0.01)
+    q[3:7] = _rotx(90)
+    q[2] = 0.10           # tower axis along world y at z = 0.10, radius 0.11 -> 1 cm deep
+    q[10:13] = [0, 0.6, 0.5]  # ball out of the way
+    fo = oracle.forward(q, v, np.zeros(3), None, hf)
+    k0 = fo.ncon - fo.nbody
+    ks = range(k0, k0 + fo.nbody)
+    assert fo.nbody > 0
+    assert all(fo.con_body1[k] == 0 and fo.con_body2[k] == 1 for k in ks)
+    up = [k for k in ks if fo.con_frame[9 * k + 2] > 0.999]
+    assert up, "no face contact"
+    for k in up:
+        assert fo.con_dist[k] == pytest.approx(-0.01, abs=1e-9)
+        assert -0.34 <= fo.con_pos[3 * k + 1] <= -0.06  # on the tower's footprint
+
+
+def test_stick_dips_into_ground(oracle):
+    """cam stick (capsule r 1 cm) vs flat ground: penetration = r - lowest core z."""
+    hf = oracle.flat_hfield()
+    q, v, _ = oracle.reset_state(0.01)
+    q[10:13] = [0, 0.8, 0.5]
+    best = None
+    for z in np.linspace(0.20, 0.02, 40):
+        q[2] = z
+        q[3:7] = _rotx(35)
+        fo = oracle.forward(q, v, np.zeros(3), None, hf)
+        k0 = fo.ncon - fo.nbody
+        sticks = [k for k in range(k0, k0 + fo.nbody) if fo.con_body2[k] in (2, 3)]
+        if sticks:
+            best = (z, sticks, fo)
+            break
+    assert best is not None
+    z, sticks, fo = best
+    for k in sticks:
+        assert fo.con_body1[k] == 0
+        assert -0.011 < fo.con_dist[k] <= 0  # just touching at the first height that produced a contact
+
+
+def test_body_contacts_keep_robot_above_ground(oracle):
+    """Let the robot fall over on flat ground: the base-tree geoms stop on the
+    terrain (no tunnelling) and the simulation stays finite."""
+    hf = oracle.flat_hfield()
+    q, v, w = oracle.reset_state(oracle.init_offset(hf))
+    q[3:7] = _rotx(25)
+    for _ in range(1500):
+        oracle.mj_step(q, v, w, np.zeros(3), hf)
+    assert np.all(np.isfinite(q)) and np.all(np.isfinite(v))
+    fo = oracle.forward(q, v, np.zeros(3), w, hf)
+    assert fo.nbody > 0                 # lying on its side, touching the ground
+    assert q[2] > 0.0 and np.abs(v[:6]).max() < 0.05  # the base came to rest (the ball may roll off)
