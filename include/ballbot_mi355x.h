@@ -37,7 +37,7 @@
 extern "C" {
 #endif
 
-#define BB_ABI_VERSION 2
+#define BB_ABI_VERSION 3
 #define BB_NQ 17
 #define BB_NV 15
 #define BB_OBS 15

@@ -49,7 +49,7 @@ EXPORTS = [
     "bb_get_offsets", "bb_get_config",
 ]
 
-ABI_VERSION = 2  # include/ballbot_mi355x.h BB_ABI_VERSION
+ABI_VERSION = 3  # include/ballbot_mi355x.h BB_ABI_VERSION
 
 _lib = None
 

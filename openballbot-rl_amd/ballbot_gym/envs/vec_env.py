@@ -155,11 +155,12 @@ class BallbotVecEnv:
                                      s.ctypes.data_as(C.POINTER(C.c_int32))), "bb_set_state")
 
     def forward(self, ctrl):
-        """mj_forward at the current state (diagnostic): returns qacc [N,15], ground contacts [N]."""
+        """mj_forward at the current state (diagnostic): returns qacc [N,15] and contact
+        counts [N,2] = (ball-hfield, base-tree geoms)."""
         n = self.num_envs
         c = np.ascontiguousarray(np.broadcast_to(ctrl, (n, 3)), dtype=np.float64)
         qacc = np.zeros((n, N.NV))
-        ncon = np.zeros(n, np.int32)
+        ncon = np.zeros((n, 2), np.int32)
         dp = C.POINTER(C.c_double)
         N.check(N.lib().bb_forward(self._h, c.ctypes.data_as(dp), qacc.ctypes.data_as(dp),
                                    ncon.ctypes.data_as(C.POINTER(C.c_int32))), "bb_forward")

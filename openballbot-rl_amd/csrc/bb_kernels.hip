@@ -76,6 +76,7 @@ struct Dev {
   const float* bank;
   const float* size_z;
   const float* offset;
+  const float* hmax;  // per terrain: max(hfield) (the top height is hmax * size_z)
   int n_terrains;
   uint64_t seed;
   unsigned long long* stats;  // resets, diverged, overflow, steps, iters
@@ -140,7 +141,8 @@ __global__ __launch_bounds__(64) void step_kernel(ModelT<T> mg, EnvCfg cfg, Dev 
   const float* hf = d.bank + size_t(tid) * (HF_N * HF_N);
   float o[15], r, p2[2];
   int iters = 0;
-  int fl = env_step(m, cfg, q, v, w, step, a, hf, T(d.size_z[tid]), W, o, r, p2, &iters, tm);
+  const TerrainRef<T> tr{hf, T(d.size_z[tid]), T(d.hmax[tid]) * T(d.size_z[tid])};
+  int fl = env_step(m, cfg, q, v, w, step, a, tr, W, o, r, p2, &iters, tm);
   if (!lead) return;
   if (tobs) {
 #pragma unroll
@@ -204,10 +206,11 @@ __global__ __launch_bounds__(64) void forward_kernel(ModelT<T> mg, Dev d, const 
   for (int i = 0; i < 3; i++) c[i] = T(ctrl[3 * e + i]);
   const int tid = d.terrain[e];
   StageOut<T> so;
-  forward(m, q, v, c, w, d.bank + size_t(tid) * (HF_N * HF_N), T(d.size_z[tid]), W, &so, tm);
+  const TerrainRef<T> tr{d.bank + size_t(tid) * (HF_N * HF_N), T(d.size_z[tid]), T(d.hmax[tid]) * T(d.size_z[tid])};
+  forward(m, q, v, c, w, tr, W, &so, tm);
   if (tm.tl != 0) return;
   for (int i = 0; i < NV; i++) qacc[NV * e + i] = double(w[i]);
-  if (ncon) ncon[e] = so.ng;
+  if (ncon) { ncon[2 * e] = so.ng; ncon[2 * e + 1] = so.nb; }
 }
 
 __global__ void assign_kernel(Dev d, const int32_t* ids) {
@@ -229,6 +232,7 @@ struct bb_handle {
   float* bank;
   float* size_z;
   float* offset;
+  float* hmax;
   std::vector<float> h_offset;
 };
 
@@ -346,6 +350,8 @@ int bb_create(int n_envs, int device, const bb_params* p, bb_handle** out) {
   HIPCHK(hipMalloc((void**)&h->bank, sizeof(float) * nt * HF_N * HF_N));
   HIPCHK(hipMalloc((void**)&h->size_z, sizeof(float) * nt));
   HIPCHK(hipMalloc((void**)&h->offset, sizeof(float) * nt));
+  HIPCHK(hipMalloc((void**)&h->hmax, sizeof(float) * nt));
+  HIPCHK(hipMemset(h->hmax, 0, sizeof(float) * nt));
   HIPCHK(hipMalloc((void**)&d.stats, sizeof(unsigned long long) * 8));
   HIPCHK(hipMemset(d.steps, 0, sizeof(int) * n));
   HIPCHK(hipMemset(d.terrain, 0, sizeof(int) * n));
@@ -358,7 +364,7 @@ int bb_create(int n_envs, int device, const bb_params* p, bb_handle** out) {
   h->h_offset.assign(nt, 0.01f);
   HIPCHK(hipMemcpy(h->size_z, sz.data(), sizeof(float) * nt, hipMemcpyHostToDevice));
   HIPCHK(hipMemcpy(h->offset, h->h_offset.data(), sizeof(float) * nt, hipMemcpyHostToDevice));
-  d.bank = h->bank; d.size_z = h->size_z; d.offset = h->offset;
+  d.bank = h->bank; d.size_z = h->size_z; d.offset = h->offset; d.hmax = h->hmax;
   // LDS for the ground-contact store (f64: 120 KiB, above the 64 KiB default)
   {
     const int lb = (int)(h->fp64 ? lds_bytes<double>(h->epw) : lds_bytes<float>(h->epw));
@@ -379,7 +385,7 @@ int bb_destroy(bb_handle* h) {
   (void)hipSetDevice(h->device);
   (void)hipFree(h->d.qpos); (void)hipFree(h->d.qvel); (void)hipFree(h->d.warm);
   (void)hipFree(h->d.steps); (void)hipFree(h->d.terrain); (void)hipFree(h->d.pending_terrain); (void)hipFree(h->d.episodes);
-  (void)hipFree(h->bank); (void)hipFree(h->size_z); (void)hipFree(h->offset); (void)hipFree(h->d.stats);
+  (void)hipFree(h->bank); (void)hipFree(h->size_z); (void)hipFree(h->offset); (void)hipFree(h->hmax); (void)hipFree(h->d.stats);
   delete h;
   return 0;
 }
@@ -395,6 +401,9 @@ int bb_set_hfield(bb_handle* h, int terrain_id, const float* data, float size_z)
                    hipMemcpyHostToDevice));
   float off = init_offset(data, size_z);
   h->h_offset[terrain_id] = off;
+  float hm = 0.f;
+  for (int i = 0; i < HF_N * HF_N; i++) hm = data[i] > hm ? data[i] : hm;
+  HIPCHK(hipMemcpy(h->hmax + terrain_id, &hm, sizeof(float), hipMemcpyHostToDevice));
   HIPCHK(hipMemcpy(h->size_z + terrain_id, &size_z, sizeof(float), hipMemcpyHostToDevice));
   HIPCHK(hipMemcpy(h->offset + terrain_id, &off, sizeof(float), hipMemcpyHostToDevice));
   return 0;
@@ -474,7 +483,7 @@ int bb_forward(bb_handle* h, const double* ctrl, double* qacc, int32_t* ncon) {
   int* dn = nullptr;
   HIPCHK(hipMalloc(&dc, sizeof(double) * 3 * n));
   HIPCHK(hipMalloc(&dq, sizeof(double) * NV * n));
-  HIPCHK(hipMalloc(&dn, sizeof(int) * n));
+  HIPCHK(hipMalloc(&dn, sizeof(int) * 2 * n));
   HIPCHK(hipMemcpy(dc, ctrl, sizeof(double) * 3 * n, hipMemcpyHostToDevice));
   const int epw = h->epw;
   int blocks = (h->n + epw - 1) / epw;
@@ -487,7 +496,7 @@ int bb_forward(bb_handle* h, const double* ctrl, double* qacc, int32_t* ncon) {
   HIPCHK(hipGetLastError());
   HIPCHK(hipDeviceSynchronize());
   HIPCHK(hipMemcpy(qacc, dq, sizeof(double) * NV * n, hipMemcpyDeviceToHost));
-  if (ncon) HIPCHK(hipMemcpy(ncon, dn, sizeof(int) * n, hipMemcpyDeviceToHost));
+  if (ncon) HIPCHK(hipMemcpy(ncon, dn, sizeof(int) * 2 * n, hipMemcpyDeviceToHost));
   (void)hipFree(dc); (void)hipFree(dq); (void)hipFree(dn);
   return 0;
 }

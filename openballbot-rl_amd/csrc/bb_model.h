@@ -101,6 +101,28 @@ inline ModelT<double> compile_model(const SolverCfg& sc) {
   }
   m.m0 = ms;
   for (int i = 0; i < 3; i++) m.h0[i] = h[i];
+  // collision geometry of the base tree (base frame)
+  m.tower_c[0] = 0; m.tower_c[1] = 0; m.tower_c[2] = 0.2; m.tower_r = 0.11; m.tower_hh = 0.14;
+  m.stick_r = 0.01; m.stick_hh = 0.1;
+  double cam_com[2][3];
+  for (int cam = 0; cam < 2; cam++) {
+    double bq[4], R[9], lp[3] = {cam == 0 ? -0.1 : 0.1, 0, 0}, p[3], ex[3] = {1, 0, 0};
+    euler_quat(bq, 180, cam == 0 ? -30 : 30, 0);
+    q2mat(R, bq);
+    mv3(p, R, lp);
+    m.stick_c[cam][0] = p[0] + (cam == 0 ? 0.17 : -0.17);
+    m.stick_c[cam][1] = p[1] - 0.01;
+    m.stick_c[cam][2] = p[2] - 0.06;
+    mv3(m.stick_a[cam], R, ex);
+    for (int i = 0; i < 3; i++) cam_com[cam][i] = m.stick_c[cam][i];
+  }
+  // base body's own COM (tower + ballast; the sticks are the cam bodies' mass)
+  double base_com[3];
+  {
+    const double r = 0.11, hh = 0.14, mc = 23.6 * pi * r * r * 2 * hh, mb = 400.0 * 8 * 0.001;
+    for (int i = 0; i < 3; i++) base_com[i] = 0;
+    base_com[2] = (mc * 0.2 + mb * 0.002) / (mc + mb);
+  }
   for (int i = 0; i < 6; i++) m.I0O[i] = IO[i];
   // ---- wheels (ballbot.xml:56-70): capsule r .025 hh .02 density 620,
   // euler (-45, 9, 0) at (-0.018,-0.08,-0.053); hinge at (0,0,0.0293)
@@ -161,6 +183,27 @@ inline ModelT<double> compile_model(const SolverCfg& sc) {
   for (int i = 0; i < NV; i++) tr += H[hidx(i, i)];
   m.scale = 1.0 / (tr / NV * NV);
   chol_packed(H);
+  // translational invweight at a point rigid with the base (base frame offset)
+  auto invweight_base = [&](const double* lp) {
+    double Jp[3][NV];
+    memset(Jp, 0, sizeof Jp);
+    double l[3];
+    mv3(l, k.Rb, lp);
+    for (int i = 0; i < 3; i++) Jp[i][i] = 1;
+    for (int j = 0; j < 3; j++) {
+      double e[3] = {k.Rb[j], k.Rb[3 + j], k.Rb[6 + j]}, x[3];
+      cross3(x, e, l);
+      for (int i = 0; i < 3; i++) Jp[i][3 + j] = x[i];
+    }
+    double s = 0;
+    for (int i = 0; i < 3; i++) {
+      double x[NV];
+      for (int d = 0; d < NV; d++) x[d] = Jp[i][d];
+      chol_solve_packed(H, x);
+      for (int d = 0; d < NV; d++) s += Jp[i][d] * x[d];
+    }
+    return s / 3;
+  };
   // translational invweight at a body COM: trace(Jp M^-1 Jp')/3
   auto invweight = [&](int body) {
     double Jp[3][NV];
@@ -205,6 +248,9 @@ inline ModelT<double> compile_model(const SolverCfg& sc) {
   };
   m.iw_ball = invweight(7);
   for (int w = 0; w < 3; w++) m.iw_wheel[w] = invweight(4 + w);
+  m.iw_base = invweight_base(base_com);
+  m.iw_cam[0] = invweight_base(cam_com[0]);
+  m.iw_cam[1] = invweight_base(cam_com[1]);
   return m;
 }
 
@@ -220,6 +266,9 @@ inline ModelT<T> cast_model(const ModelT<double>& d) {
   BBA(axis, 3); BBA(jpos, 3); BBA(anchor, 3);
   BBC(wheel_r); BBC(wheel_hh); BBC(armature); BBC(damping);
   BBC(mB); BBC(IB); BBC(ball_r); BBC(dz);
+  BBA(tower_c, 3); BBC(tower_r); BBC(tower_hh); BBA(stick_c[0], 3); BBA(stick_c[1], 3);
+  BBA(stick_a[0], 3); BBA(stick_a[1], 3); BBC(stick_r); BBC(stick_hh);
+  BBC(iw_base); BBA(iw_cam, 2);
   BBC(iw_ball); BBA(iw_wheel, 3); BBC(K); BBC(Bd); BBA(solimp, 5); BBA(fr_wheel, 2);
   BBC(h); BBC(grav); BBC(hf_sx); BBC(hf_sy); BBC(hf_bottom); BBC(scale); BBC(tol); BBC(ls_tol); BBC(step_rel2);
   m.maxiter = d.maxiter; m.ls_maxiter = d.ls_maxiter;

@@ -33,11 +33,16 @@ constexpr int NQ = 17, NV = 15, NU = 3;
 constexpr int HF_N = 293;        // ballbot.xml:23 nrow = ncol
 constexpr int MAXG = 50;         // ball-hfield contact cap: MuJoCo's mjMAXCONPAIR (== oracle BBO_MAXGROUND)
 constexpr int NH = NV * (NV + 1) / 2;
-constexpr int NGF = 10;          // fields per stored ground contact (see GF_* below)
-// ground-contact store fields (compact; the 3x6 Jacobian is rebuilt from the
-// normal and the lever by ground_rows): normal[3], lever from the ball frame
-// origin (world)[3], aref[3], D
-constexpr int GF_N = 0, GF_LV = 3, GF_AREF = 6, GF_D = 9;
+constexpr int NGF = 4;           // fields per stored ground contact (see GF_* below)
+constexpr int MAXB = 16;         // base-tree geom contact cap (== oracle BBO_MAXBODY)
+constexpr int NBF = 8;           // fields per stored base-tree contact (see BF_* below)
+// ground-contact store fields (compact: Jacobian, aref and D are rebuilt on
+// use by ground_contact): normal (hfield -> ball)[3], dist
+constexpr int GF_N = 0, GF_DIST = 3;
+// base-tree contact store: normal (geom1 -> geom2)[3], position (world)[3],
+// dist, body code 8*body1 + body2 (body1: 0 world / 7 ball; body2: 1 base,
+// 2-3 cam bodies, 4-6 wheels)
+constexpr int BF_N = 0, BF_P = 3, BF_DIST = 6, BF_CODE = 7;
 
 // ------------------------------------------------------------------ model
 // Compiled constants (bb_model.cpp computes them in double from the MJCF
@@ -57,8 +62,12 @@ struct ModelT {
   T wheel_r, wheel_hh, armature, damping;
   // ball
   T mB, IB, ball_r, dz;  // geom offset (0,0,dz) in ball frame (ballbot.xml:78)
+  // base-tree collision geoms (dynamic pairs), base frame
+  T tower_c[3], tower_r, tower_hh;         // cylinder (ballbot.xml:41), axis = base z
+  T stick_c[2][3], stick_a[2][3], stick_r, stick_hh;  // cam sticks (capsules, ballbot.xml:46,52)
   // constraint parameters
   T iw_ball, iw_wheel[3];  // body_invweight0 (translational)
+  T iw_base, iw_cam[2];
   T K, Bd;                 // solref (0.02,1) -> stiffness, damping
   T solimp[5];             // (0.9, 0.95, 0.001, 0.5, 2)
   T fr_wheel[2];           // pair friction (0.001, 1.0) (ballbot.xml:90-92)
@@ -684,12 +693,17 @@ BB_HD bool sphere_prism(const T* c, T r, const T V[3][3], T zb, T* n, T* dist) {
   return true;
 }
 
-// Jacobian rows (normal, t1, t2) of a stored ground contact over the ball dofs:
-// world-linear F_r and local-angular RB' (lever x F_r)
+// Stored ground contact -> Jacobian rows (normal, t1, t2) over the ball dofs
+// (world-linear F_r, local-angular RB'(lever x F_r)), aref and D.  RB: ball
+// orientation, v: the stage velocity (qvel) the constraint is built at.
 template <typename T>
-BB_HD void ground_rows(const T* gc, const T* RB, T (&J)[3][6]) {
+BB_HD void ground_contact(const ModelT<T>& m, const T* gc, const T* RB, const T* v, T (&J)[3][6], T (&aref)[3],
+                          T& D) {
   const T n[3] = {gc[GF_N], gc[GF_N + 1], gc[GF_N + 2]};
-  const T lv[3] = {gc[GF_LV], gc[GF_LV + 1], gc[GF_LV + 2]};
+  const T dist = gc[GF_DIST];
+  // lever = (ball geom centre - ball frame origin) - n (r + dist/2)
+  const T sp = m.ball_r + dist * T(0.5);
+  const T lv[3] = {m.dz * RB[2] - n[0] * sp, m.dz * RB[5] - n[1] * sp, m.dz * RB[8] - n[2] * sp};
   T t1[3], t2[3];
   frame_from_normal(n, t1, t2);
   const T* F[3] = {n, t1, t2};
@@ -701,6 +715,134 @@ BB_HD void ground_rows(const T* gc, const T* RB, T (&J)[3][6]) {
 #pragma unroll
     for (int i = 0; i < 3; i++) { J[r][i] = F[r][i]; J[r][3 + i] = x2[i]; }
   }
+  const T imp = clampT(impedance(m, dist), T(0.0001), T(0.9999));
+  const T R0 = maxT(T(1e-15), (1 - imp) * m.iw_ball / imp);
+  D = T(1) / R0;
+#pragma unroll
+  for (int r = 0; r < 3; r++) {
+    const T vel = J[r][0] * v[9] + J[r][1] * v[10] + J[r][2] * v[11] + J[r][3] * v[12] + J[r][4] * v[13] +
+                  J[r][5] * v[14];
+    aref[r] = -m.Bd * vel - (r == 0 ? m.K * imp * dist : T(0));
+  }
+}
+
+// Persistent body poses the solve needs after the kinematics scratch is reused.
+template <typename T>
+struct Poses {
+  T Rb[9], pb[3], RB[9], pB[3];
+};
+
+// Stored base-tree contact -> 13-column Jacobian rows in the wheel-contact
+// layout (base lin 3, base ang 3, hinge 1, ball lin 3, ball ang 3), the hinge
+// slot's wheel (-1: none), aref and D (isotropic friction: mu = 1).
+template <typename T>
+BB_HD void body_contact(const ModelT<T>& m, const T* bc, const Poses<T>& P, const T* v, T (&J)[3][13], int& hinge,
+                        T (&aref)[3], T& D) {
+  const int code = int(bc[BF_CODE]);
+  const int b1 = code >> 3, b2 = code & 7;
+  const T n[3] = {bc[BF_N], bc[BF_N + 1], bc[BF_N + 2]};
+  const T p[3] = {bc[BF_P], bc[BF_P + 1], bc[BF_P + 2]};
+  const T dist = bc[BF_DIST];
+  T t1[3], t2[3];
+  frame_from_normal(n, t1, t2);
+  const T* F[3] = {n, t1, t2};
+  const T db[3] = {p[0] - P.pb[0], p[1] - P.pb[1], p[2] - P.pb[2]};
+  const T dB[3] = {p[0] - P.pB[0], p[1] - P.pB[1], p[2] - P.pB[2]};
+  hinge = (b2 >= 4 && b2 <= 6) ? b2 - 4 : -1;
+  T uw[3] = {0, 0, 0}, da[3] = {0, 0, 0};
+  if (hinge >= 0) {
+    T t[3];
+    mv3(uw, P.Rb, m.u[hinge]);
+    mv3(t, P.Rb, m.anchor);
+    da[0] = db[0] - t[0]; da[1] = db[1] - t[1]; da[2] = db[2] - t[2];
+  }
+  const T ball = b1 == 7 ? T(1) : T(0);
+#pragma unroll
+  for (int r = 0; r < 3; r++) {
+    T x1[3], x2[3];
+    J[r][0] = F[r][0]; J[r][1] = F[r][1]; J[r][2] = F[r][2];
+    cross3(x1, db, F[r]);
+    mtv3(x2, P.Rb, x1);
+    J[r][3] = x2[0]; J[r][4] = x2[1]; J[r][5] = x2[2];
+    cross3(x1, da, F[r]);
+    J[r][6] = hinge >= 0 ? dot3(uw, x1) : T(0);
+    J[r][7] = -ball * F[r][0]; J[r][8] = -ball * F[r][1]; J[r][9] = -ball * F[r][2];
+    cross3(x1, dB, F[r]);
+    mtv3(x2, P.RB, x1);
+    J[r][10] = -ball * x2[0]; J[r][11] = -ball * x2[1]; J[r][12] = -ball * x2[2];
+  }
+  const T iw2 = b2 == 1 ? m.iw_base : (b2 <= 3 ? m.iw_cam[b2 - 2] : m.iw_wheel[b2 - 4]);
+  const T tran = iw2 + (b1 == 7 ? m.iw_ball : T(0));
+  const T imp = clampT(impedance(m, dist), T(0.0001), T(0.9999));
+  D = T(1) / maxT(T(1e-15), (1 - imp) * tran / imp);
+#pragma unroll
+  for (int r = 0; r < 3; r++) {
+    T vel = 0;
+#pragma unroll
+    for (int q = 0; q < 6; q++) vel += J[r][q] * v[q];
+    vel += hinge >= 0 ? J[r][6] * v[6 + hinge] : T(0);
+#pragma unroll
+    for (int q = 7; q < 13; q++) vel += J[r][q] * v[q + 2];
+    aref[r] = -m.Bd * vel - (r == 0 ? m.K * imp * dist : T(0));
+  }
+}
+
+// line-search terms of a body contact without materialising J: per row r,
+// jar0_r = J_r a - aref_r and J_r s; D returned
+template <typename T>
+BB_HD void body_ls_terms(const ModelT<T>& m, const T* bc, const Poses<T>& P, const T* v, const T* a, const T* s,
+                         T (&c6)[6], T& D) {
+  const int code = int(bc[BF_CODE]);
+  const int b1 = code >> 3, b2 = code & 7;
+  const T n[3] = {bc[BF_N], bc[BF_N + 1], bc[BF_N + 2]};
+  const T dist = bc[BF_DIST];
+  T t1[3], t2[3];
+  frame_from_normal(n, t1, t2);
+  const T db[3] = {bc[BF_P] - P.pb[0], bc[BF_P + 1] - P.pb[1], bc[BF_P + 2] - P.pb[2]};
+  const T dB[3] = {bc[BF_P] - P.pB[0], bc[BF_P + 1] - P.pB[1], bc[BF_P + 2] - P.pB[2]};
+  const int hinge = (b2 >= 4 && b2 <= 6) ? b2 - 4 : -1;
+  T uw[3] = {0, 0, 0}, da[3] = {0, 0, 0};
+  if (hinge >= 0) {
+    T t[3];
+    mv3(uw, P.Rb, m.u[hinge]);
+    mv3(t, P.Rb, m.anchor);
+    da[0] = db[0] - t[0]; da[1] = db[1] - t[1]; da[2] = db[2] - t[2];
+  }
+  const T ball = b1 == 7 ? T(1) : T(0);
+  const T iw2 = b2 == 1 ? m.iw_base : (b2 <= 3 ? m.iw_cam[b2 - 2] : m.iw_wheel[b2 - 4]);
+  const T imp = clampT(impedance(m, dist), T(0.0001), T(0.9999));
+  D = T(1) / maxT(T(1e-15), (1 - imp) * (iw2 + (b1 == 7 ? m.iw_ball : T(0))) / imp);
+#pragma unroll
+  for (int r = 0; r < 3; r++) {
+    const T* F = r == 0 ? n : (r == 1 ? t1 : t2);
+    T x1[3], wa[3], wB[3];
+    cross3(x1, db, F);
+    mtv3(wa, P.Rb, x1);
+    cross3(x1, da, F);
+    const T jh = hinge >= 0 ? dot3(uw, x1) : T(0);
+    cross3(x1, dB, F);
+    mtv3(wB, P.RB, x1);
+    auto dotJ = [&](const T* x) {
+      T acc = F[0] * x[0] + F[1] * x[1] + F[2] * x[2] + wa[0] * x[3] + wa[1] * x[4] + wa[2] * x[5];
+      acc += hinge >= 0 ? jh * (hinge == 0 ? x[6] : (hinge == 1 ? x[7] : x[8])) : T(0);
+      acc -= ball * (F[0] * x[9] + F[1] * x[10] + F[2] * x[11] + wB[0] * x[12] + wB[1] * x[13] + wB[2] * x[14]);
+      return acc;
+    };
+    const T aref = -m.Bd * dotJ(v) - (r == 0 ? m.K * imp * dist : T(0));
+    c6[r] = dotJ(a) - aref;
+    c6[3 + r] = dotJ(s);
+  }
+}
+
+// J_r x for a body contact in the 13-column layout
+template <typename T>
+BB_HD T body_dot(const T (&J)[3][13], int hinge, int r, const T* x) {
+  T acc = hinge >= 0 ? J[r][6] * (hinge == 0 ? x[6] : (hinge == 1 ? x[7] : x[8])) : T(0);
+#pragma unroll
+  for (int q = 0; q < 6; q++) acc += J[r][q] * x[q];
+#pragma unroll
+  for (int q = 7; q < 13; q++) acc += J[r][q] * x[q + 2];
+  return acc;
 }
 
 // mjc_ConvexHField for the ball: sub-grid from the ball AABB, triangular
@@ -724,10 +866,7 @@ BB_HD int collide_ground(const ModelT<T>& m, const Kin<T>& k, const T* v, const 
   rmin = rmin < 0 ? 0 : rmin;
   rmax = rmax > N1 ? N1 : rmax;
   const T dx = 2 * sx / N1, dy = 2 * sy / N1;
-  // ball rotation velocity for aref: omega_world = RB w_local
-  T wB[3];
-  mv3(wB, k.RB, v + 12);
-  const T iw = m.iw_ball;
+  (void)v;
   int ng = 0;
   for (int rr = rmin; rr < rmax; rr++) {
     T W[3][3] = {{0, 0, 0}, {0, 0, 0}, {0, 0, 0}};
@@ -756,22 +895,9 @@ BB_HD int collide_ground(const ModelT<T>& m, const Kin<T>& k, const T* v, const 
         T nn[3], dist;
         if (!sphere_prism(c, r, W, -zb, nn, &dist)) continue;
         if (ng >= MAXG) { *overflow = 1; continue; }
-        // contact: pos = c - n (r + dist/2); lever from the ball frame origin
-        T sp = r + dist * T(0.5);
-        T lv[3] = {c[0] - nn[0] * sp - k.pB[0], c[1] - nn[1] * sp - k.pB[1], c[2] - nn[2] * sp - k.pB[2]};
-        T t1[3], t2[3];
-        frame_from_normal(nn, t1, t2);
-        T imp = clampT(impedance(m, dist), T(0.0001), T(0.9999));
-        T R0 = maxT(T(1e-15), (1 - imp) * iw / imp);
-        T pv[3], tt[3];
-        cross3(tt, wB, lv);
-        pv[0] = v[9] + tt[0]; pv[1] = v[10] + tt[1]; pv[2] = v[11] + tt[2];
 #pragma unroll
-        for (int i = 0; i < 3; i++) { st.at(ng, GF_N + i) = nn[i]; st.at(ng, GF_LV + i) = lv[i]; }
-        st.at(ng, GF_AREF + 0) = -m.Bd * dot3(nn, pv) - m.K * imp * dist;
-        st.at(ng, GF_AREF + 1) = -m.Bd * dot3(t1, pv);
-        st.at(ng, GF_AREF + 2) = -m.Bd * dot3(t2, pv);
-        st.at(ng, GF_D) = T(1) / R0;
+        for (int i = 0; i < 3; i++) st.at(ng, GF_N + i) = nn[i];
+        st.at(ng, GF_DIST) = dist;
         ng++;
       }
     }

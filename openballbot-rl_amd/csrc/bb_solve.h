@@ -72,28 +72,39 @@ struct StageOut {
   T w_world[3];  // cvel[base][0:3]
   T v_com[3];    // cvel[base][3:6] (linear velocity at subtree_com[base])
   T pb[3];       // xpos[base]
-  int ng, iters, overflow;
+  int ng, nb, iters, overflow;
+};
+
+// The terrain an env steps on: heightfield (NULL: none), vertical scale and
+// its top height max(hfield) * size_z (base-tree geoms above it skip the
+// prism search).
+template <typename T>
+struct TerrainRef {
+  const float* hf;
+  T size_z, hz;
 };
 
 // Per-env working set of one RK step (LDS on the GPU, one per team).
 // Phase-local buffers share storage in a union to fit 16 envs per CU.
 template <typename T>
 struct EnvWork {
-  T q0[NQ], v0[NV], vs[NV], as[NV], vp[NV];  // RK4 stage context
+  T q0[NQ], v0[NV], vs[NV], as[NV];          // RK4 stage context
   T qfs[NV];                                 // smooth force of the current forward
-  T qi[NQ], vi[NV];                          // RK stage state (read by the pre-phase)
+  T vi[NV];                                  // stage velocity (pre-phase; constraint aref rebuilds)
   T gv[NV], mq[NV];                          // solver: gradient, M a - qfs (team-replicated)
   StageOut<T> so;                            // stage-4 outputs for obs/reward
   Mass<T> M;                                 // mass-matrix blocks
   WheelCon<T> wc[3];                         // ball-wheel contacts
   T g[MAXG * NGF];                           // ball-terrain contacts (compact, GF_*)
-  T RB[9];                                   // ball orientation: rebuilds ground Jacobians
+  T bc[MAXB * NBF];                          // base-tree geom contacts (compact, BF_*)
+  T bj[3][13];                               // the base-tree contact being processed (team-shared)
+  Poses<T> P;                                // body poses for the Jacobian rebuilds
   T H[NH];                                   // Hessian / Cholesky factor (packed lower); dense M on the GPU
-  T hd[NV];                                  // Hessian diagonal before factorisation
   union U {
     struct {                                 // forward pre-phase
       Kin<T> k;
       T Iw[3][6];
+      T qi[NQ];                              // stage position
     } pre;
     struct {                                 // Hessian assembly
       T cj[3][3][13];                        // C J for each wheel contact
@@ -187,12 +198,15 @@ BB_HD void ls_contact(const T* c6, T alpha, T mu, T f1, T f2, const T* D, T& d1,
 
 // Newton on f(a) (mj_solNewton).  a: warm start in, qacc out (replicated in
 // every lane of the team).  Returns the iteration count (team-uniform).
+// Host / reference path (tests/hostcheck): wheel and ball-hfield contacts
+// only; the GPU solve (bb_team16.h) also handles the base-tree contacts.
 template <typename T>
 BB_HD int solve_team(const ModelT<T>& m, EnvWork<T>& W, const T* qfs, int ng, T* a, const Team& tm) {
   const Mass<T>& M = W.M;
   PH_DECL
   const T mu_w = m.fr_wheel[0], f1w = m.fr_wheel[0], f2w = m.fr_wheel[1];
   const int nc = 3 + ng;
+  T hd[NV];  // Hessian diagonal before factorisation (pivot floor)
   int it = 0;
   for (; it < m.maxiter; it++) {
     team_sync();
@@ -220,14 +234,11 @@ BB_HD int solve_team(const ModelT<T>& m, EnvWork<T>& W, const T* qfs, int ng, T*
         }
       } else {
         const T* gc = W.g + (c - 3) * NGF;
-        T J[3][6];
-        ground_rows(gc, W.RB, J);
+        T J[3][6], ar[3], D;
+        ground_contact(m, gc, W.P.RB, W.vi, J, ar, D);
         T jar[3];
 #pragma unroll
-        for (int r = 0; r < 3; r++)
-          jar[r] = J[r][0] * a[9] + J[r][1] * a[10] + J[r][2] * a[11] + J[r][3] * a[12] + J[r][4] * a[13] +
-                   J[r][5] * a[14] - gc[GF_AREF + r];
-        const T D = gc[GF_D];
+        for (int r = 0; r < 3; r++) jar[r] = ground_dot(J, r, a) - ar[r];
         T Dv[3] = {D, D, D}, f[3], Cc[6];
         cone_eval(jar, T(1), T(1), T(1), Dv, f, Cc);
         T w[3][6];
@@ -297,11 +308,11 @@ BB_HD int solve_team(const ModelT<T>& m, EnvWork<T>& W, const T* qfs, int ng, T*
         h += W.u.hes.hg[a9 * (a9 + 1) / 2 + b9];
       }
       W.H[e] = h;
-      if (i == j) W.hd[i] = h;
+      if (i == j) hd[i] = h;
     }
     PH(3)
     // ---- (5) factorise, Newton direction (replicated triangular solves)
-    chol_team(W.H, W.hd, tm);
+    chol_team(W.H, hd, tm);
     PH(4)
     T s[NV];
 #pragma unroll
@@ -329,7 +340,7 @@ BB_HD int solve_team(const ModelT<T>& m, EnvWork<T>& W, const T* qfs, int ng, T*
     T sMs = 0, gs = 0;
 #pragma unroll
     for (int i = 0; i < NV; i++) { sMs += s[i] * Ms[i]; gs += s[i] * (Ma[i] - qfs[i]); }
-    T lsc[3 + MAXG][6];  // line-search cache (host / reference path: plenty of stack)
+    T lsc[3 + MAXG][6], lsD[3 + MAXG];  // line-search cache (host / reference path: plenty of stack)
     for (int c = tm.tl; c < nc; c += tm.L) {
       T* c6 = lsc[c];
       if (c < 3) {
@@ -338,10 +349,11 @@ BB_HD int solve_team(const ModelT<T>& m, EnvWork<T>& W, const T* qfs, int ng, T*
         for (int r = 0; r < 3; r++) { c6[r] = wheel_dot(C, c, r, a) - C.aref[r]; c6[3 + r] = wheel_dot(C, c, r, s); }
       } else {
         const T* gc = W.g + (c - 3) * NGF;
-        T J[3][6];
-        ground_rows(gc, W.RB, J);
+        T J[3][6], ar[3], D;
+        ground_contact(m, gc, W.P.RB, W.vi, J, ar, D);
 #pragma unroll
-        for (int r = 0; r < 3; r++) { c6[r] = ground_dot(J, r, a) - gc[GF_AREF + r]; c6[3 + r] = ground_dot(J, r, s); }
+        for (int r = 0; r < 3; r++) { c6[r] = ground_dot(J, r, a) - ar[r]; c6[3 + r] = ground_dot(J, r, s); }
+        lsD[c] = D;
       }
     }
     // 1-D Newton on phi'(alpha) from the full step, safeguarded by an
@@ -362,7 +374,7 @@ BB_HD int solve_team(const ModelT<T>& m, EnvWork<T>& W, const T* qfs, int ng, T*
           const T Dw[3] = {W.wc[c].D[0], W.wc[c].D[1], W.wc[c].D[2]};
           ls_contact(lsc[c], alpha, mu_w, f1w, f2w, Dw, d1p, d2p, dmp);
         } else {
-          const T D = W.g[(c - 3) * NGF + GF_D];
+          const T D = lsD[c];
           const T Dv[3] = {D, D, D};
           ls_contact(lsc[c], alpha, T(1), T(1), T(1), Dv, d1p, d2p, dmp);
         }

@@ -26,9 +26,14 @@ struct EnvCfg {
 // bias, collision) is computed redundantly by every lane of the team, the
 // constraint solve is team-parallel (bb_solve.h).
 template <typename T>
-BB_HD int forward(const ModelT<T>& m, const T* q, const T* v, const T* ctrl, T* acc, const float* hf, T size_z,
+BB_HD int forward(const ModelT<T>& m, const T* q, const T* v, const T* ctrl, T* acc, const TerrainRef<T>& tr,
                   EnvWork<T>& W, StageOut<T>* so, const Team& tm) {
   team_sync();  // previous users of the workspace are done
+  if (v != W.vi) {  // the constraint rebuilds in the solve read the velocity from the workspace
+#pragma unroll
+    for (int i = 0; i < NV; i++) W.vi[i] = v[i];
+    team_sync();
+  }
 #if defined(BB_PHASE_CLOCKS) && defined(__HIP_DEVICE_COMPILE__)
   const unsigned long long f_t0 = clock64();
 #endif
@@ -55,9 +60,10 @@ BB_HD int forward(const ModelT<T>& m, const T* q, const T* v, const T* ctrl, T* 
   const unsigned long long f_t1 = clock64();
 #endif
 #ifdef __HIP_DEVICE_COMPILE__
-  int ng = hf ? t16::collide_team(m, k, v, hf, size_z, W.g, &overflow, tm.tl) : 0;
+  const int ng = tr.hf ? t16::collide_team(m, k, v, tr.hf, tr.size_z, W.g, &overflow, tm.tl) : 0;
+  const int nb = t16::collide_body_team(m, k, tr.hf, tr.size_z, tr.hz, W.bc, &overflow, tm.tl);
 #else
-  int ng = hf ? collide_ground(m, k, v, hf, size_z, st, &overflow) : 0;
+  const int ng = tr.hf ? collide_ground(m, k, v, tr.hf, tr.size_z, st, &overflow) : 0;
 #endif
 #if defined(BB_PHASE_CLOCKS) && defined(__HIP_DEVICE_COMPILE__)
   if (tm.tl == 0) {
@@ -68,7 +74,9 @@ BB_HD int forward(const ModelT<T>& m, const T* q, const T* v, const T* ctrl, T* 
   }
 #endif
 #pragma unroll
-  for (int i = 0; i < 9; i++) W.RB[i] = k.RB[i];  // the solve rebuilds ground Jacobians from it
+  for (int i = 0; i < 9; i++) { W.P.Rb[i] = k.Rb[i]; W.P.RB[i] = k.RB[i]; }  // Jacobian rebuilds in the solve
+#pragma unroll
+  for (int i = 0; i < 3; i++) { W.P.pb[i] = k.pb[i]; W.P.pB[i] = k.pB[i]; }
   if (so) {
     T qb[4] = {q[3], q[4], q[5], q[6]};
     qnormalize(qb);
@@ -81,6 +89,11 @@ BB_HD int forward(const ModelT<T>& m, const T* q, const T* v, const T* ctrl, T* 
     so->v_com[0] = v[0] + t[0]; so->v_com[1] = v[1] + t[1]; so->v_com[2] = v[2] + t[2];
     so->pb[0] = q[0]; so->pb[1] = q[1]; so->pb[2] = q[2];
     so->ng = ng; so->overflow = overflow;
+#ifdef __HIP_DEVICE_COMPILE__
+    so->nb = nb;
+#else
+    so->nb = 0;
+#endif
   }
   bool ok = true;
 #pragma unroll
@@ -93,7 +106,7 @@ BB_HD int forward(const ModelT<T>& m, const T* q, const T* v, const T* ctrl, T* 
   // 16-lane DPP-row solve: smooth force and dense M staged in the team's LDS
   t16::mass_dense_team(W, tm.tl);
   team_sync();
-  const int it = t16::solve16(m, W, ng, acc, tm.tl);
+  const int it = t16::solve16(m, W, ng, nb, acc, tm.tl);
 #else
   const int it = solve_team(m, W, W.qfs, ng, acc, tm);
 #endif
@@ -104,7 +117,7 @@ BB_HD int forward(const ModelT<T>& m, const T* q, const T* v, const T* ctrl, T* 
 // mj_step with integrator RK4 = mj_forward + mj_RungeKutta(N=4) + mj_advance.
 // warm: qacc_warmstart (each stage's constraint solve saves its qacc).
 template <typename T>
-BB_HD int rk4_step(const ModelT<T>& m, T* q, T* v, T* warm, const T* ctrl, const float* hf, T size_z,
+BB_HD int rk4_step(const ModelT<T>& m, T* q, T* v, T* warm, const T* ctrl, const TerrainRef<T>& tr,
                    EnvWork<T>& W, StageOut<T>& so, const Team& tm) {
   const T h = m.h;
   // the RK context lives in the workspace (written identically by every
@@ -113,7 +126,6 @@ BB_HD int rk4_step(const ModelT<T>& m, T* q, T* v, T* warm, const T* ctrl, const
   T* v0 = W.v0;
   T* vs = W.vs;
   T* as = W.as;
-  T* vp = W.vp;
   team_sync();
 #pragma unroll
   for (int i = 0; i < NQ; i++) q0[i] = q[i];
@@ -135,24 +147,24 @@ BB_HD int rk4_step(const ModelT<T>& m, T* q, T* v, T* warm, const T* ctrl, const
       } else {
         T dv[NV];
 #pragma unroll
-        for (int i = 0; i < NV; i++) { dv[i] = a * vp[i]; vi[i] = v0[i] + h * a * warm[i]; }
+        for (int i = 0; i < NV; i++) { dv[i] = a * W.vi[i]; vi[i] = v0[i] + h * a * warm[i]; }  // W.vi: previous stage
         integrate_pos(qi, dv, h);
       }
       team_sync();
 #pragma unroll
-      for (int i = 0; i < NQ; i++) W.qi[i] = qi[i];
+      for (int i = 0; i < NQ; i++) W.u.pre.qi[i] = qi[i];
 #pragma unroll
       for (int i = 0; i < NV; i++) W.vi[i] = vi[i];
     }
-    iters += forward(m, W.qi, W.vi, ctrl, warm, hf, size_z, W, stage == 3 ? &so : (StageOut<T>*)nullptr, tm);
+    iters += forward(m, W.u.pre.qi, W.vi, ctrl, warm, tr, W, stage == 3 ? &so : (StageOut<T>*)nullptr, tm);
     const T b = (stage == 0 || stage == 3) ? T(1.0 / 6) : T(1.0 / 3);  // RK4 weights B
     team_sync();
     if (stage == 0) {
 #pragma unroll
-      for (int i = 0; i < NV; i++) { vs[i] = b * W.vi[i]; as[i] = b * warm[i]; vp[i] = W.vi[i]; }
+      for (int i = 0; i < NV; i++) { vs[i] = b * W.vi[i]; as[i] = b * warm[i]; }
     } else {
 #pragma unroll
-      for (int i = 0; i < NV; i++) { vs[i] += b * W.vi[i]; as[i] += b * warm[i]; vp[i] = W.vi[i]; }
+      for (int i = 0; i < NV; i++) { vs[i] += b * W.vi[i]; as[i] += b * warm[i]; }
     }
   }
   team_sync();
@@ -201,14 +213,14 @@ constexpr int F_TERMINATED = 1, F_FAILURE = 2, F_DIVERGED = 4, F_OVERFLOW = 8;
 // motor_state, orientation, vel), the order the policy's Extractor consumes.
 template <typename T>
 BB_HD int env_step(const ModelT<T>& m, const EnvCfg& cfg, T* q, T* v, T* warm, int& step, const float* action,
-                   const float* hf, T size_z, EnvWork<T>& W, float* obs15, float& reward, float* pos2d,
+                   const TerrainRef<T>& tr, EnvWork<T>& W, float* obs15, float& reward, float* pos2d,
                    int* iters, const Team& tm) {
   const float mwv = cfg.max_wheel_velocity;
   T ctrl[3];
 #pragma unroll
   for (int i = 0; i < 3; i++) ctrl[i] = -T(clipf(action[i] * mwv, -mwv, mwv));  // data.ctrl[:] = -ctrl
   StageOut<T>& so = W.so;  // team-shared (LDS): not register-resident across the solves
-  int it = rk4_step(m, q, v, warm, ctrl, hf, size_z, W, so, tm);
+  int it = rk4_step(m, q, v, warm, ctrl, tr, W, so, tm);
   if (iters) *iters = it;
   int flags = state_bad(q, v) ? F_DIVERGED : 0;
   if (so.overflow) flags |= F_OVERFLOW;

@@ -22,6 +22,7 @@
 
 #include <type_traits>
 
+#include "bb_bodycon.h"
 #include "bb_solve.h"
 
 namespace bb {
@@ -89,20 +90,8 @@ __device__ __forceinline__ void cone_sel(const T* jar, T mu, T f1, T f2, const T
   for (int r = 0; r < 6; r++) C[r] = top ? T(0) : (bot ? (r < 3 ? D[r] : T(0)) : cm[r]);
 }
 
-// per-contact cone parameters: wheels (c < 3) use the pair friction and
-// anisotropic D, ground contacts mu = 1 and one D for all rows
-template <typename T>
-__device__ __forceinline__ void cone_params(const ModelT<T>& m, const EnvWork<T>& W, int c, T kdw, T& mu, T& f1,
-                                            T& f2, T (&D)[3], T& Dm) {
-  const bool wheel = c < 3;
-  const T* Dp = wheel ? &W.wc[c].D[0] : &W.g[(c - 3) * NGF + GF_D];
-  const int st = wheel ? 1 : 0;
-  D[0] = Dp[0]; D[1] = Dp[st]; D[2] = Dp[2 * st];
-  Dm = D[0] * (wheel ? kdw : T(0.5));  // 1 / (mu^2 (1 + mu^2)), mu = 1 on the ground
-  mu = wheel ? m.fr_wheel[0] : T(1);
-  f1 = wheel ? m.fr_wheel[0] : T(1);
-  f2 = wheel ? m.fr_wheel[1] : T(1);
-}
+// which wheel dof a 13-column contact Jacobian's column q maps to (-1: none)
+__device__ __forceinline__ int col_dof(int q, int hinge) { return q < 6 ? q : (q == 6 ? (hinge >= 0 ? 6 + hinge : -1) : q + 2); }
 
 // Cholesky of the register-distributed H (lane i holds row h[0..14]); on exit
 // lane i holds L_ik (k < i) in h[k] and every lane holds diag[] = 1 / L_jj.
@@ -155,31 +144,52 @@ __device__ __forceinline__ void chol_solve_rows(const T (&h)[NV], const T (&diag
   });
 }
 
-// jar(0) = J a - aref and J s of contact c (zeros when c >= nc)
+// line-search terms of contact c: jar(0) = J a - aref, J s and the contact's
+// D (isotropic contacts) -- zeros when c >= nc
 template <typename T>
-__device__ __forceinline__ void ls_terms(const EnvWork<T>& W, int c, int nc, const T* a, const T* s, T (&c6)[6]) {
+__device__ __forceinline__ void ls_terms(const ModelT<T>& m, const EnvWork<T>& W, int c, int ng, int nc, const T* a,
+                                         const T* s, T (&c6)[6], T& D) {
 #pragma unroll
   for (int r = 0; r < 6; r++) c6[r] = 0;
+  D = 0;
   if (c >= nc) return;
   if (c < 3) {
     const WheelCon<T>& C = W.wc[c];
 #pragma unroll
     for (int r = 0; r < 3; r++) { c6[r] = wheel_dot(C, c, r, a) - C.aref[r]; c6[3 + r] = wheel_dot(C, c, r, s); }
-  } else {
-    const T* gcn = W.g + (c - 3) * NGF;
-    T J[3][6];
-    ground_rows(gcn, W.RB, J);
+  } else if (c < 3 + ng) {
+    T J[3][6], ar[3];
+    ground_contact(m, W.g + (c - 3) * NGF, W.P.RB, W.vi, J, ar, D);
 #pragma unroll
-    for (int r = 0; r < 3; r++) { c6[r] = ground_dot(J, r, a) - gcn[GF_AREF + r]; c6[3 + r] = ground_dot(J, r, s); }
+    for (int r = 0; r < 3; r++) { c6[r] = ground_dot(J, r, a) - ar[r]; c6[3 + r] = ground_dot(J, r, s); }
+  } else {
+    body_ls_terms(m, W.bc + (c - 3 - ng) * NBF, W.P, W.vi, a, s, c6, D);
   }
+}
+
+// Rebuild base-tree contact b into the team-shared W.bj (every lane writes
+// the same values), evaluate its cone at a: returns the hinge slot's wheel.
+template <typename T>
+__device__ __forceinline__ int body_eval(const ModelT<T>& m, EnvWork<T>& W, int b, const T* a, T (&ar)[3], T& Dc,
+                                         T (&f)[3], T (&Cc)[6]) {
+  team_sync();  // previous users of bj are done
+  int hinge;
+  body_contact(m, W.bc + b * NBF, W.P, W.vi, W.bj, hinge, ar, Dc);
+  team_sync();
+  T jar[3];
+#pragma unroll
+  for (int r = 0; r < 3; r++) jar[r] = body_dot(W.bj, hinge, r, a) - ar[r];
+  const T D[3] = {Dc, Dc, Dc};
+  cone_sel(jar, T(1), T(1), T(1), D, Dc * T(0.5), f, Cc);
+  return hinge;
 }
 
 // Newton on f(a); a replicated in every lane of the row.  W.H holds the dense
 // mass matrix (packed lower) for this forward, W.qfs the smooth force.
 template <typename T>
-__device__ int solve16(const ModelT<T>& m, EnvWork<T>& W, int ng, T* a, int tl) {
+__device__ int solve16(const ModelT<T>& m, EnvWork<T>& W, int ng, int nb, T* a, int tl) {
   const Mass<T>& M = W.M;
-  const int nc = 3 + ng;
+  const int nc = 3 + ng + nb;
   const int row = tl < NV ? tl : NV - 1;
   const T muw = m.fr_wheel[0];
   const T kdw = T(1) / (muw * muw * (1 + muw * muw));
@@ -193,20 +203,22 @@ __device__ int solve16(const ModelT<T>& m, EnvWork<T>& W, int ng, T* a, int tl) 
     for (int i = 0; i < NV; i++) gc[i] = 0;
 #pragma unroll
     for (int i = 0; i < 21; i++) Hg[i] = 0;
-    for (int c = tl; c < nc; c += L) {
-      const bool wheel = c < 3;
-      const T* gcn = W.g + (wheel ? 0 : c - 3) * NGF;
-      T jar[3], J[3][6];
+    for (int c = tl; c < 3 + ng; c += L) {
+      const bool wheel = c < 3;  // else ball-hfield
+      T jar[3], Dc = 0, Jg[3][6];
       if (wheel) {
 #pragma unroll
         for (int r = 0; r < 3; r++) jar[r] = wheel_dot(W.wc[c], c, r, a) - W.wc[c].aref[r];
       } else {
-        ground_rows(gcn, W.RB, J);
+        T ar[3];
+        ground_contact(m, W.g + (c - 3) * NGF, W.P.RB, W.vi, Jg, ar, Dc);
 #pragma unroll
-        for (int r = 0; r < 3; r++) jar[r] = ground_dot(J, r, a) - gcn[GF_AREF + r];
+        for (int r = 0; r < 3; r++) jar[r] = ground_dot(Jg, r, a) - ar[r];
       }
-      T mu, f1, f2, D[3], Dm, f[3], Cc[6];
-      cone_params(m, W, c, kdw, mu, f1, f2, D, Dm);
+      const T D[3] = {wheel ? W.wc[c].D[0] : Dc, wheel ? W.wc[c].D[1] : Dc, wheel ? W.wc[c].D[2] : Dc};
+      const T mu = wheel ? m.fr_wheel[0] : T(1), f1 = wheel ? m.fr_wheel[0] : T(1), f2 = wheel ? m.fr_wheel[1] : T(1);
+      const T Dm = D[0] * (wheel ? kdw : T(0.5));  // 1 / (mu^2 (1 + mu^2))
+      T f[3], Cc[6];
       cone_sel(jar, mu, f1, f2, D, Dm, f, Cc);
       if (wheel) {
         const WheelCon<T>& C = W.wc[c];
@@ -225,15 +237,15 @@ __device__ int solve16(const ModelT<T>& m, EnvWork<T>& W, int ng, T* a, int tl) 
         T w[3][6];
 #pragma unroll
         for (int i = 0; i < 6; i++) {
-          gc[9 + i] -= J[0][i] * f[0] + J[1][i] * f[1] + J[2][i] * f[2];
-          w[0][i] = Cc[0] * J[0][i] + Cc[3] * J[1][i] + Cc[4] * J[2][i];
-          w[1][i] = Cc[3] * J[0][i] + Cc[1] * J[1][i] + Cc[5] * J[2][i];
-          w[2][i] = Cc[4] * J[0][i] + Cc[5] * J[1][i] + Cc[2] * J[2][i];
+          gc[9 + i] -= Jg[0][i] * f[0] + Jg[1][i] * f[1] + Jg[2][i] * f[2];
+          w[0][i] = Cc[0] * Jg[0][i] + Cc[3] * Jg[1][i] + Cc[4] * Jg[2][i];
+          w[1][i] = Cc[3] * Jg[0][i] + Cc[1] * Jg[1][i] + Cc[5] * Jg[2][i];
+          w[2][i] = Cc[4] * Jg[0][i] + Cc[5] * Jg[1][i] + Cc[2] * Jg[2][i];
         }
 #pragma unroll
         for (int i = 0; i < 6; i++)
 #pragma unroll
-          for (int j = 0; j <= i; j++) Hg[i * (i + 1) / 2 + j] += J[0][i] * w[0][j] + J[1][i] * w[1][j] + J[2][i] * w[2][j];
+          for (int j = 0; j <= i; j++) Hg[i * (i + 1) / 2 + j] += Jg[0][i] * w[0][j] + Jg[1][i] * w[1][j] + Jg[2][i] * w[2][j];
       }
     }
     PH(0)
@@ -243,6 +255,19 @@ __device__ int solve16(const ModelT<T>& m, EnvWork<T>& W, int ng, T* a, int tl) 
 #pragma unroll
     for (int i = 0; i < 21; i++) Hg[i] = tsum(Hg[i]);
     team_sync();  // cj visible to every row owner
+    // base-tree contacts (rare): sequential over the contacts, every lane
+    // computing the same -J'f (added after the team sums)
+    for (int b = 0; b < nb; b++) {
+      T ar[3], Dc, f[3], Cc[6];
+      const int hinge = body_eval(m, W, b, a, ar, Dc, f, Cc);
+#pragma unroll
+      for (int q = 0; q < 13; q++) {
+        const T jf = W.bj[0][q] * f[0] + W.bj[1][q] * f[1] + W.bj[2][q] * f[2];
+        if (q < 6) gc[q] -= jf;
+        else if (q == 6) { gc[6] -= hinge == 0 ? jf : T(0); gc[7] -= hinge == 1 ? jf : T(0); gc[8] -= hinge == 2 ? jf : T(0); }
+        else gc[q + 2] -= jf;
+      }
+    }
     PH(1)
     // ---- (3) gradient, replicated
     T gn = 0;
@@ -284,6 +309,27 @@ __device__ int solve16(const ModelT<T>& m, EnvWork<T>& W, int ng, T* a, int tl) 
         const T v = Hg[ai >= b ? ai * (ai + 1) / 2 + b : b * (b + 1) / 2 + ai];
         h[9 + b] += row == 9 + ai ? v : T(0);
       }
+    // base-tree contacts (rare): each lane rebuilds contact b and adds
+    // J_b' C_b J_b to its row
+    for (int b = 0; b < nb; b++) {
+      T ar[3], Dc, f[3], Cc[6];
+      const int hinge = body_eval(m, W, b, a, ar, Dc, f, Cc);
+      // this row's column of J (dof row -> column position, or none)
+      const int prow = row < 6 ? row : (row < 9 ? (row == 6 + hinge ? 6 : -1) : row - 2);
+      const T jc[3] = {prow >= 0 ? W.bj[0][prow] : T(0), prow >= 0 ? W.bj[1][prow] : T(0),
+                       prow >= 0 ? W.bj[2][prow] : T(0)};
+      // w = C jc ; h[dof(q)] += w . J[:, q]
+      const T w0 = Cc[0] * jc[0] + Cc[3] * jc[1] + Cc[4] * jc[2];
+      const T w1 = Cc[3] * jc[0] + Cc[1] * jc[1] + Cc[5] * jc[2];
+      const T w2 = Cc[4] * jc[0] + Cc[5] * jc[1] + Cc[2] * jc[2];
+#pragma unroll
+      for (int q = 0; q < 13; q++) {
+        const T add = w0 * W.bj[0][q] + w1 * W.bj[1][q] + w2 * W.bj[2][q];
+        if (q < 6) h[q] += add;
+        else if (q == 6) { h[6] += hinge == 0 ? add : T(0); h[7] += hinge == 1 ? add : T(0); h[8] += hinge == 2 ? add : T(0); }
+        else h[q + 2] += add;
+      }
+    }
     T hdi = 0;
 #pragma unroll
     for (int k = 0; k < NV; k++) hdi = row == k ? h[k] : hdi;
@@ -315,8 +361,8 @@ __device__ int solve16(const ModelT<T>& m, EnvWork<T>& W, int ng, T* a, int tl) 
     for (int i = 0; i < NV; i++) { sMs += s[i] * Ms[i]; gs += s[i] * W.mq[i]; }
     // line-search cache: jar(0) and J s of this lane's first contact in
     // registers; later rounds (more than 16 contacts) recompute them
-    T c6r[6];
-    ls_terms(W, tl, nc, a, s, c6r);
+    T c6r[6], Dr;
+    ls_terms(m, W, tl, ng, nc, a, s, c6r, Dr);
     T lo = 0, dlo = d0, hi = -1, dhi = 0, alpha = 1;
     T flo = d0, fhi = 0;
     int side = 0, same = 0;
@@ -324,14 +370,18 @@ __device__ int solve16(const ModelT<T>& m, EnvWork<T>& W, int ng, T* a, int tl) 
     for (int ls = 1; ls <= m.ls_maxiter; ls++) {
       T d1p = 0, d2p = 0, dmp = 0;
       for (int c = tl; c < nc; c += L) {
-        T mu, f1, f2, D[3], Dm, c6[6];
-        cone_params(m, W, c, kdw, mu, f1, f2, D, Dm);
+        T c6[6], Dc;
         if (c == tl) {
 #pragma unroll
           for (int r = 0; r < 6; r++) c6[r] = c6r[r];
+          Dc = Dr;
         } else {
-          ls_terms(W, c, nc, a, s, c6);
+          ls_terms(m, W, c, ng, nc, a, s, c6, Dc);
         }
+        const bool wheel = c < 3;
+        const T D[3] = {wheel ? W.wc[c].D[0] : Dc, wheel ? W.wc[c].D[1] : Dc, wheel ? W.wc[c].D[2] : Dc};
+        const T mu = wheel ? m.fr_wheel[0] : T(1), f1 = wheel ? m.fr_wheel[0] : T(1), f2 = wheel ? m.fr_wheel[1] : T(1);
+        const T Dm = D[0] * (wheel ? kdw : T(0.5));
         const T x[3] = {c6[3], c6[4], c6[5]};
         const T jr[3] = {c6[0] + alpha * x[0], c6[1] + alpha * x[1], c6[2] + alpha * x[2]};
         T f[3], Cc[6];
@@ -404,9 +454,7 @@ __device__ __forceinline__ int collide_team(const ModelT<T>& m, const Kin<T>& k,
   const int np = 2 * ncol - 2;            // prisms per grid row
   const int total = (rmax - rmin) * (np > 0 ? np : 0);
   const T dx = 2 * sx / N1, dy = 2 * sy / N1;
-  T wB[3];
-  mv3(wB, k.RB, v + 12);
-  const T iw = m.iw_ball;
+  (void)v;
   const int team_shift = threadIdx.x & ~(L - 1);
   int ng = 0;
   for (int base = 0; base < total; base += L) {
@@ -438,28 +486,111 @@ __device__ __forceinline__ int collide_team(const ModelT<T>& m, const Kin<T>& k,
     const int slot = ng + __popc(bits & ((1u << tl) - 1u));
     if (hit) {
       if (slot < MAXG) {
-        const T sp = r + dist * T(0.5);
-        T lv[3] = {c[0] - nn[0] * sp - k.pB[0], c[1] - nn[1] * sp - k.pB[1], c[2] - nn[2] * sp - k.pB[2]};
-        T t1[3], t2[3];
-        frame_from_normal(nn, t1, t2);
-        const T imp = clampT(impedance(m, dist), T(0.0001), T(0.9999));
-        const T R0 = maxT(T(1e-15), (1 - imp) * iw / imp);
-        T pv[3], tt[3];
-        cross3(tt, wB, lv);
-        pv[0] = v[9] + tt[0]; pv[1] = v[10] + tt[1]; pv[2] = v[11] + tt[2];
         T* gs = g + slot * NGF;
 #pragma unroll
-        for (int i = 0; i < 3; i++) { gs[GF_N + i] = nn[i]; gs[GF_LV + i] = lv[i]; }
-        gs[GF_AREF + 0] = -m.Bd * dot3(nn, pv) - m.K * imp * dist;
-        gs[GF_AREF + 1] = -m.Bd * dot3(t1, pv);
-        gs[GF_AREF + 2] = -m.Bd * dot3(t2, pv);
-        gs[GF_D] = T(1) / R0;
+        for (int i = 0; i < 3; i++) gs[GF_N + i] = nn[i];
+        gs[GF_DIST] = dist;
       }
     }
     ng += __popc(bits);
   }
   if (ng > MAXG) { ng = MAXG; *overflow = 1; }  // ng counts every hit: team-uniform
   return ng;
+}
+
+// store one base-tree contact (slot already compacted)
+template <typename T>
+__device__ __forceinline__ void put_body(T* bc, int slot, const T* n, const T* pos, T dist, int b1, int b2) {
+  T* s = bc + slot * NBF;
+#pragma unroll
+  for (int i = 0; i < 3; i++) { s[BF_N + i] = n[i]; s[BF_P + i] = pos[i]; }
+  s[BF_DIST] = dist;
+  s[BF_CODE] = T(8 * b1 + b2);
+}
+
+// Dynamic pairs of the base-tree geoms (bb_bodycon.h), team-parallel, in the
+// oracle's order: ball x {tower, stick0, stick1}, then hfield x {tower,
+// stick0, stick1, wheel0..2} prism by prism.  hz: the terrain's top height
+// (max(hfield) * size_z): geoms above it skip the prism loop.  Returns the
+// contact count (team-uniform); *overflow |= 2 past MAXB.
+template <typename T>
+__device__ int collide_body_team(const ModelT<T>& m, const Kin<T>& k, const float* hf, T size_z, T hz, T* bc,
+                                 int* overflow, int tl) {
+  const int team_shift = threadIdx.x & ~(L - 1);
+  int nb = 0, total_hits = 0;
+  auto compact = [&](bool hit) -> int {  // -> this lane's slot (valid if hit)
+    const unsigned long long bal = __ballot(hit);
+    const unsigned bits = unsigned(bal >> team_shift) & 0xFFFFu;
+    const int slot = nb + __popc(bits & ((1u << tl) - 1u));
+    total_hits += int(__popc(bits));
+    nb = minT(nb + int(__popc(bits)), MAXB);
+    return slot;
+  };
+  // ball (geom1, sphere) x tower (cylinder) / sticks (capsules): lanes 0..2
+  {
+    bool hit = false;
+    T dist = 0, n[3] = {0, 0, 1}, pos[3] = {0, 0, 0};
+    if (tl < 3) {
+      Seg<T> g;
+      body_geom(m, k, tl, g);
+      hit = tl == 0 ? sphere_cylinder(k.c, m.ball_r, g, dist, n, pos) : sphere_capsule(k.c, m.ball_r, g, dist, n, pos);
+    }
+    const int slot = compact(hit);
+    if (hit && slot < MAXB) put_body(bc, slot, n, pos, dist, 7, tl + 1);
+  }
+  // hfield (geom1) x convex geom: prisms under the geom's AABB
+  if (hf) {
+    const T sx = m.hf_sx, sy = m.hf_sy, zb = m.hf_bottom;
+    const int N1 = HF_N - 1;
+    const T dx = 2 * sx / N1, dy = 2 * sy / N1;
+    for (int gi = 0; gi < 6; gi++) {
+      Seg<T> g;
+      body_geom(m, k, gi, g);
+      const bool cyl = gi == 0;
+      T lo[3], hi[3];
+#pragma unroll
+      for (int i = 0; i < 3; i++) {
+        const T ai = fabs(g.a[i]);
+        const T rad = T(1) - ai * ai;
+        const T ext = cyl ? g.hh * ai + g.r * sqrt(rad > 0 ? rad : T(0)) : g.hh * ai + g.r;
+        lo[i] = g.c[i] - ext; hi[i] = g.c[i] + ext;
+      }
+      if (lo[2] > hz) continue;  // above every vertex of the terrain
+      if (lo[0] > sx || hi[0] < -sx || lo[1] > sy || hi[1] < -sy || lo[2] > size_z || hi[2] < -zb) continue;
+      int cmin = (int)floor((lo[0] + sx) / (2 * sx) * N1), cmax = (int)ceil((hi[0] + sx) / (2 * sx) * N1);
+      int rmin = (int)floor((lo[1] + sy) / (2 * sy) * N1), rmax = (int)ceil((hi[1] + sy) / (2 * sy) * N1);
+      cmin = cmin < 0 ? 0 : cmin; cmax = cmax > N1 ? N1 : cmax;
+      rmin = rmin < 0 ? 0 : rmin; rmax = rmax > N1 ? N1 : rmax;
+      const int np = 2 * (cmax - cmin + 1) - 2;
+      const int total = (rmax - rmin) * (np > 0 ? np : 0);
+      const int b2 = gi + 1;  // body ids: tower 1, sticks 2-3, wheels 4-6
+      for (int base = 0; base < total; base += L) {
+        const int P = base + tl;
+        bool hit = false;
+        T dist = 0, n[3] = {0, 0, 1}, pos[3] = {0, 0, 0};
+        if (P < total) {
+          const int rr = rmin + P / np, p = P % np;
+          T V[3][3];
+#pragma unroll
+          for (int t = 0; t < 3; t++) {
+            const int vt = p + t, cc = cmin + (vt >> 1), ri = rr + (vt & 1);
+            V[t][0] = dx * cc - sx;
+            V[t][1] = dy * ri - sy;
+            V[t][2] = T(hf[ri * HF_N + cc]) * size_z;
+          }
+          if (!(V[0][2] < lo[2] && V[1][2] < lo[2] && V[2][2] < lo[2])) {
+            PrismG<T> Pr;
+            prism_build(Pr, V, -zb);
+            hit = cyl ? cylinder_prism(g, Pr, dist, n, pos) : capsule_prism(g, Pr, dist, n, pos);
+          }
+        }
+        const int slot = compact(hit);
+        if (hit && slot < MAXB) put_body(bc, slot, n, pos, dist, 0, b2);
+      }
+    }
+  }
+  if (total_hits > MAXB) *overflow |= 2;
+  return nb;
 }
 
 // dense mass matrix (packed lower) into W.H, entry-parallel; once per forward

@@ -29,7 +29,7 @@ static int fwd(const double* q, const double* v, const double* ctrl, double* acc
   for (int i = 0; i < 3; i++) cc[i] = T(ctrl[i]);
   static EnvWork<T> W;
   StageOut<T> so;
-  int it = forward(m, qq, vv, cc, aa, hf, T(size_z), W, &so, Team{1, 0});
+  int it = forward(m, qq, vv, cc, aa, TerrainRef<T>{hf, T(size_z), T(1e30)}, W, &so, Team{1, 0});
   for (int i = 0; i < NV; i++) acc[i] = double(aa[i]);
   if (extra) {
     extra[0] = so.ng; extra[1] = so.iters; extra[2] = so.overflow;
@@ -47,7 +47,7 @@ static int envstep(const EnvCfg* cfg, double* q, double* v, double* w, int* step
   for (int i = 0; i < NV; i++) { vv[i] = T(v[i]); ww[i] = T(w[i]); }
   static EnvWork<T> W;
   int it = 0;
-  int fl = env_step(m, *cfg, qq, vv, ww, *step, a, hf, T(size_z), W, obs, *rew, pos2d, &it, Team{1, 0});
+  int fl = env_step(m, *cfg, qq, vv, ww, *step, a, TerrainRef<T>{hf, T(size_z), T(1e30)}, W, obs, *rew, pos2d, &it, Team{1, 0});
   for (int i = 0; i < NQ; i++) q[i] = double(qq[i]);
   for (int i = 0; i < NV; i++) { v[i] = double(vv[i]); w[i] = double(ww[i]); }
   return fl | (it << 8);
@@ -67,5 +67,7 @@ void hc_model(double* out) {
   ModelT<double> m = compile_model(default_solver(true));
   out[0] = m.m0; out[1] = m.mw; out[2] = m.mB; out[3] = m.iw_ball;
   out[4] = m.iw_wheel[0]; out[5] = m.iw_wheel[1]; out[6] = m.iw_wheel[2]; out[7] = 1.0 / (m.scale * 15);
+  out[8] = m.iw_base; out[9] = m.iw_cam[0]; out[10] = m.iw_cam[1];
+  for (int i = 0; i < 3; i++) { out[11 + i] = m.stick_c[0][i]; out[14 + i] = m.stick_a[0][i]; out[17 + i] = m.stick_c[1][i]; out[20 + i] = m.stick_a[1][i]; }
 }
 }

@@ -94,7 +94,7 @@ def test_forward_parity(oracle, flat_traj, precision):
         for e in range(env.num_envs):
             fo = oracle.forward(rec["qpos"][t][e], rec["qvel"][t][e], ctrl[e], rec["warm"][t][e], hf)
             ref = np.array(fo.qacc)
-            assert ncon[e] == fo.nground
+            assert ncon[e, 0] == fo.nground and ncon[e, 1] == fo.nbody
             err = np.abs(qacc[e] - ref).max() / max(1.0, np.abs(ref).max())
             assert err < (2e-4 if precision == "fp32" else 1e-7), (t, e, err)
     env.close()
@@ -112,4 +112,63 @@ def test_step_parity_hills(hills_traj, precision):
     hf, rec = hills_traj
     env = _make_env(rec["qpos"].shape[1], precision, terrain={"type": "hills", "config": {"seed": 7}})
     _teacher_forced(env, rec, TOL[precision])
+    env.close()
+
+
+def _body_contact_states(oracle, n, seed):
+    """States where base-tree geoms touch the terrain or the ball: rolled and
+    lowered bases (tower/stick/wheel vs hfield), displaced balls (ball vs
+    tower/sticks), random velocities."""
+    rng = np.random.default_rng(seed)
+    qs, vs = [], []
+    for i in range(n):
+        q, v, _ = oracle.reset_state(0.01)
+        ang = rng.uniform(30, 100)
+        ax = rng.normal(size=3)
+        ax[2] = 0
+        ax /= np.linalg.norm(ax)
+        t = np.radians(ang)
+        q[3:7] = [np.cos(t / 2), *(np.sin(t / 2) * ax)]
+        q[2] = rng.uniform(0.06, 0.16)
+        if i % 3 == 0:
+            q[10:13] = q[0:3] + rng.normal(0, 0.12, 3)  # ball near the base geoms
+        else:
+            q[10:13] = [rng.uniform(-1, 1), rng.uniform(-1, 1), 0.5]
+        q[13:17] = [1, 0, 0, 0]
+        q[7:10] = rng.uniform(-3, 3, 3)
+        v[:] = rng.normal(0, 0.3, 15)
+        qs.append(q)
+        vs.append(v)
+    return np.array(qs), np.array(vs)
+
+
+@pytest.mark.parametrize("precision", ["fp64"])
+@pytest.mark.parametrize("terrain", ["flat", "hills"])
+def test_forward_parity_base_tree_contacts(oracle, precision, terrain):
+    """Dynamic pairs hfield x {tower, sticks, wheels} and ball x {tower, sticks}:
+    the HIP forward (qacc, contact counts) vs the oracle."""
+    from ballbot_gym.terrain import generate_hills_terrain
+
+    n = 64
+    if terrain == "flat":
+        hf = oracle.flat_hfield()
+        tcfg = {"type": "flat", "config": {}}
+    else:
+        hf = generate_hills_terrain(293, seed=7).astype(np.float32)
+        tcfg = {"type": "hills", "config": {"seed": 7}}
+    env = _make_env(n, precision, tcfg)
+    qs, vs = _body_contact_states(oracle, n, seed=11)
+    rng = np.random.default_rng(1)
+    ctrl = rng.uniform(-10, 10, (n, 3))
+    env.set_state(qs, vs, np.zeros((n, 15)))
+    qacc, ncon = env.forward(ctrl)
+    touched = 0
+    for e in range(n):
+        fo = oracle.forward(qs[e], vs[e], ctrl[e], np.zeros(15), hf)
+        assert (ncon[e, 0], ncon[e, 1]) == (fo.nground, fo.nbody), e
+        touched += fo.nbody > 0
+        ref = np.array(fo.qacc)
+        err = np.abs(qacc[e] - ref).max() / max(1.0, np.abs(ref).max())
+        assert err < 1e-7, (e, err, fo.nbody)
+    assert touched >= n // 4
     env.close()
