@@ -169,7 +169,7 @@ class BallbotVecEnv:
     def stats(self) -> Dict[str, int]:
         out = (C.c_int64 * 6)()
         N.check(N.lib().bb_get_stats(self._h, out), "bb_get_stats")
-        return {"resets": out[0], "diverged": out[1], "overflow": out[2],
+        return {"resets": out[0], "diverged": out[1], "overflow": out[2], "slow_path": out[3],
                 "solver_iters": out[4] + (out[5] << 32)}
 
     def launch_config(self) -> Dict[str, int]:

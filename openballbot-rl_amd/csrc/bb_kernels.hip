@@ -79,7 +79,9 @@ struct Dev {
   const float* hmax;  // per terrain: max(hfield) (the top height is hmax * size_z)
   int n_terrains;
   uint64_t seed;
-  unsigned long long* stats;  // resets, diverged, overflow, steps, iters
+  unsigned long long* stats;  // resets, diverged, overflow, slow-path env-steps, iters
+  int* slow_list;             // envs the fast kernel handed to the full kernel this step
+  int* slow_count;
 };
 
 template <typename T>
@@ -113,7 +115,10 @@ __device__ __forceinline__ void reset_lane(const ModelT<T>& m, const Dev& d, int
   step = 0;
 }
 
-template <typename T>
+// BODY = false: the fast kernel (no base-tree contact support compiled in;
+// envs that may touch a base-tree geom are appended to d.slow_list and left
+// untouched).  BODY = true: the full kernel over d.slow_list.
+template <typename T, bool BODY>
 __global__ __launch_bounds__(64) void step_kernel(ModelT<T> mg, EnvCfg cfg, Dev d, const float* __restrict__ act,
                                                   float* __restrict__ obs, float* __restrict__ rew,
                                                   uint8_t* __restrict__ done, float* __restrict__ tobs,
@@ -129,7 +134,11 @@ __global__ __launch_bounds__(64) void step_kernel(ModelT<T> mg, EnvCfg cfg, Dev 
   const Team tm{L, int(threadIdx.x) & (L - 1)};
   const int team = threadIdx.x / L;
   if (team >= epw) return;
-  const int e = blockIdx.x * epw + team;
+  int e = blockIdx.x * epw + team;
+  if constexpr (BODY) {
+    if (e >= *d.slow_count) return;
+    e = d.slow_list[e];
+  }
   if (e >= d.n) return;
   const bool lead = tm.tl == 0;
   EnvWork<T>& W = team_work<T>(smem, team);
@@ -142,7 +151,14 @@ __global__ __launch_bounds__(64) void step_kernel(ModelT<T> mg, EnvCfg cfg, Dev 
   float o[15], r, p2[2];
   int iters = 0;
   const TerrainRef<T> tr{hf, T(d.size_z[tid]), T(d.hmax[tid]) * T(d.size_z[tid])};
-  int fl = env_step(m, cfg, q, v, w, step, a, tr, W, o, r, p2, &iters, tm);
+  int fl = env_step<T, BODY>(m, cfg, q, v, w, step, a, tr, W, o, r, p2, &iters, tm);
+  if (!BODY && (fl & F_SLOWPATH)) {
+    if (lead) {
+      d.slow_list[atomicAdd(d.slow_count, 1)] = e;
+      atomicAdd(&d.stats[3], 1ull);
+    }
+    return;
+  }
   if (!lead) return;
   if (tobs) {
 #pragma unroll
@@ -207,7 +223,7 @@ __global__ __launch_bounds__(64) void forward_kernel(ModelT<T> mg, Dev d, const 
   const int tid = d.terrain[e];
   StageOut<T> so;
   const TerrainRef<T> tr{d.bank + size_t(tid) * (HF_N * HF_N), T(d.size_z[tid]), T(d.hmax[tid]) * T(d.size_z[tid])};
-  forward(m, q, v, c, w, tr, W, &so, tm);
+  forward<T, true>(m, q, v, c, w, tr, W, &so, tm);
   if (tm.tl != 0) return;
   for (int i = 0; i < NV; i++) qacc[NV * e + i] = double(w[i]);
   if (ncon) { ncon[2 * e] = so.ng; ncon[2 * e + 1] = so.nb; }
@@ -260,8 +276,13 @@ int launch_step(bb_handle* h, const float* a, float* o, float* r, uint8_t* dn, f
   const ModelT<T>& m = model_of<T>(h);
   const int epw = h->epw;
   int blocks = (h->n + epw - 1) / epw;
-  hipLaunchKernelGGL(step_kernel<T>, dim3(blocks), dim3(WAVE), lds_bytes<T>(epw), s, m, h->cfg, h->d, a, o, r, dn,
-                     t, p2, ar, h->team, epw);
+  // fast kernel for every env, then the full kernel over the envs it handed over
+  HIPCHK(hipMemsetAsync(h->d.slow_count, 0, sizeof(int), s));
+  hipLaunchKernelGGL((step_kernel<T, false>), dim3(blocks), dim3(WAVE), lds_bytes<T>(epw), s, m, h->cfg, h->d, a, o, r,
+                     dn, t, p2, ar, h->team, epw);
+  HIPCHK(hipGetLastError());
+  hipLaunchKernelGGL((step_kernel<T, true>), dim3(blocks), dim3(WAVE), lds_bytes<T>(epw), s, m, h->cfg, h->d, a, o, r,
+                     dn, t, p2, ar, h->team, epw);
   HIPCHK(hipGetLastError());
   return 0;
 }
@@ -353,6 +374,9 @@ int bb_create(int n_envs, int device, const bb_params* p, bb_handle** out) {
   HIPCHK(hipMalloc((void**)&h->hmax, sizeof(float) * nt));
   HIPCHK(hipMemset(h->hmax, 0, sizeof(float) * nt));
   HIPCHK(hipMalloc((void**)&d.stats, sizeof(unsigned long long) * 8));
+  HIPCHK(hipMalloc((void**)&d.slow_list, sizeof(int) * n));
+  HIPCHK(hipMalloc((void**)&d.slow_count, sizeof(int)));
+  HIPCHK(hipMemset(d.slow_count, 0, sizeof(int)));
   HIPCHK(hipMemset(d.steps, 0, sizeof(int) * n));
   HIPCHK(hipMemset(d.terrain, 0, sizeof(int) * n));
   HIPCHK(hipMemset(d.pending_terrain, 0, sizeof(int) * n));
@@ -368,7 +392,9 @@ int bb_create(int n_envs, int device, const bb_params* p, bb_handle** out) {
   // LDS for the ground-contact store (f64: 120 KiB, above the 64 KiB default)
   {
     const int lb = (int)(h->fp64 ? lds_bytes<double>(h->epw) : lds_bytes<float>(h->epw));
-    const void* sk = h->fp64 ? (const void*)step_kernel<double> : (const void*)step_kernel<float>;
+    const void* sk = h->fp64 ? (const void*)step_kernel<double, false> : (const void*)step_kernel<float, false>;
+    const void* sk2 = h->fp64 ? (const void*)step_kernel<double, true> : (const void*)step_kernel<float, true>;
+    HIPCHK(hipFuncSetAttribute(sk2, hipFuncAttributeMaxDynamicSharedMemorySize, lb));
     const void* fk = h->fp64 ? (const void*)forward_kernel<double> : (const void*)forward_kernel<float>;
     HIPCHK(hipFuncSetAttribute(sk, hipFuncAttributeMaxDynamicSharedMemorySize, lb));
     HIPCHK(hipFuncSetAttribute(fk, hipFuncAttributeMaxDynamicSharedMemorySize, lb));
@@ -386,6 +412,7 @@ int bb_destroy(bb_handle* h) {
   (void)hipFree(h->d.qpos); (void)hipFree(h->d.qvel); (void)hipFree(h->d.warm);
   (void)hipFree(h->d.steps); (void)hipFree(h->d.terrain); (void)hipFree(h->d.pending_terrain); (void)hipFree(h->d.episodes);
   (void)hipFree(h->bank); (void)hipFree(h->size_z); (void)hipFree(h->offset); (void)hipFree(h->hmax); (void)hipFree(h->d.stats);
+  (void)hipFree(h->d.slow_list); (void)hipFree(h->d.slow_count);
   delete h;
   return 0;
 }

@@ -25,7 +25,7 @@ struct EnvCfg {
 // entry).  Executed by a team of tm.L lanes; the pre-phase (kinematics, mass,
 // bias, collision) is computed redundantly by every lane of the team, the
 // constraint solve is team-parallel (bb_solve.h).
-template <typename T>
+template <typename T, bool BODY = true>
 BB_HD int forward(const ModelT<T>& m, const T* q, const T* v, const T* ctrl, T* acc, const TerrainRef<T>& tr,
                   EnvWork<T>& W, StageOut<T>* so, const Team& tm) {
   team_sync();  // previous users of the workspace are done
@@ -61,7 +61,14 @@ BB_HD int forward(const ModelT<T>& m, const T* q, const T* v, const T* ctrl, T* 
 #endif
 #ifdef __HIP_DEVICE_COMPILE__
   const int ng = tr.hf ? t16::collide_team(m, k, v, tr.hf, tr.size_z, W.g, &overflow, tm.tl) : 0;
-  const int nb = t16::collide_body_team(m, k, tr.hf, tr.size_z, tr.hz, W.bc, &overflow, tm.tl);
+  int nb = 0;
+  if constexpr (BODY) {
+    nb = t16::collide_body_team(m, k, tr.hf, tr.size_z, tr.hz, W.bc, &overflow, tm.tl);
+  } else {
+    // fast path: no base-tree contact support compiled in; configurations that
+    // could have one abort here and are re-run by the full kernel
+    if (t16::body_candidates(m, k, tr.hf, tr.size_z, tr.hz, tm.tl)) return -1;
+  }
 #else
   const int ng = tr.hf ? collide_ground(m, k, v, tr.hf, tr.size_z, st, &overflow) : 0;
 #endif
@@ -106,7 +113,7 @@ BB_HD int forward(const ModelT<T>& m, const T* q, const T* v, const T* ctrl, T* 
   // 16-lane DPP-row solve: smooth force and dense M staged in the team's LDS
   t16::mass_dense_team(W, tm.tl);
   team_sync();
-  const int it = t16::solve16(m, W, ng, nb, acc, tm.tl);
+  const int it = t16::solve16<BODY>(m, W, ng, nb, acc, tm.tl);
 #else
   const int it = solve_team(m, W, W.qfs, ng, acc, tm);
 #endif
@@ -116,7 +123,7 @@ BB_HD int forward(const ModelT<T>& m, const T* q, const T* v, const T* ctrl, T* 
 
 // mj_step with integrator RK4 = mj_forward + mj_RungeKutta(N=4) + mj_advance.
 // warm: qacc_warmstart (each stage's constraint solve saves its qacc).
-template <typename T>
+template <typename T, bool BODY = true>
 BB_HD int rk4_step(const ModelT<T>& m, T* q, T* v, T* warm, const T* ctrl, const TerrainRef<T>& tr,
                    EnvWork<T>& W, StageOut<T>& so, const Team& tm) {
   const T h = m.h;
@@ -156,7 +163,9 @@ BB_HD int rk4_step(const ModelT<T>& m, T* q, T* v, T* warm, const T* ctrl, const
 #pragma unroll
       for (int i = 0; i < NV; i++) W.vi[i] = vi[i];
     }
-    iters += forward(m, W.u.pre.qi, W.vi, ctrl, warm, tr, W, stage == 3 ? &so : (StageOut<T>*)nullptr, tm);
+    const int fit = forward<T, BODY>(m, W.u.pre.qi, W.vi, ctrl, warm, tr, W, stage == 3 ? &so : (StageOut<T>*)nullptr, tm);
+    if (fit < 0) return -1;  // fast path aborted (team-uniform)
+    iters += fit;
     const T b = (stage == 0 || stage == 3) ? T(1.0 / 6) : T(1.0 / 3);  // RK4 weights B
     team_sync();
     if (stage == 0) {
@@ -206,12 +215,13 @@ BB_HD bool state_bad(const T* q, const T* v) {
   return bad;
 }
 
-// flags returned by env_step
-constexpr int F_TERMINATED = 1, F_FAILURE = 2, F_DIVERGED = 4, F_OVERFLOW = 8;
+// flags returned by env_step; F_SLOWPATH: the fast kernel left this env to
+// the full kernel (nothing was stepped)
+constexpr int F_TERMINATED = 1, F_FAILURE = 2, F_DIVERGED = 4, F_OVERFLOW = 8, F_SLOWPATH = 1 << 16;
 
 // One BBotSimulation.step.  obs15 = sorted keys (actions, angular_vel,
 // motor_state, orientation, vel), the order the policy's Extractor consumes.
-template <typename T>
+template <typename T, bool BODY = true>
 BB_HD int env_step(const ModelT<T>& m, const EnvCfg& cfg, T* q, T* v, T* warm, int& step, const float* action,
                    const TerrainRef<T>& tr, EnvWork<T>& W, float* obs15, float& reward, float* pos2d,
                    int* iters, const Team& tm) {
@@ -220,7 +230,8 @@ BB_HD int env_step(const ModelT<T>& m, const EnvCfg& cfg, T* q, T* v, T* warm, i
 #pragma unroll
   for (int i = 0; i < 3; i++) ctrl[i] = -T(clipf(action[i] * mwv, -mwv, mwv));  // data.ctrl[:] = -ctrl
   StageOut<T>& so = W.so;  // team-shared (LDS): not register-resident across the solves
-  int it = rk4_step(m, q, v, warm, ctrl, tr, W, so, tm);
+  int it = rk4_step<T, BODY>(m, q, v, warm, ctrl, tr, W, so, tm);
+  if (it < 0) return F_SLOWPATH;
   if (iters) *iters = it;
   int flags = state_bad(q, v) ? F_DIVERGED : 0;
   if (so.overflow) flags |= F_OVERFLOW;

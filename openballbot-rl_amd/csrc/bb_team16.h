@@ -146,7 +146,7 @@ __device__ __forceinline__ void chol_solve_rows(const T (&h)[NV], const T (&diag
 
 // line-search terms of contact c: jar(0) = J a - aref, J s and the contact's
 // D (isotropic contacts) -- zeros when c >= nc
-template <typename T>
+template <bool BODY, typename T>
 __device__ __forceinline__ void ls_terms(const ModelT<T>& m, const EnvWork<T>& W, int c, int ng, int nc, const T* a,
                                          const T* s, T (&c6)[6], T& D) {
 #pragma unroll
@@ -162,7 +162,7 @@ __device__ __forceinline__ void ls_terms(const ModelT<T>& m, const EnvWork<T>& W
     ground_contact(m, W.g + (c - 3) * NGF, W.P.RB, W.vi, J, ar, D);
 #pragma unroll
     for (int r = 0; r < 3; r++) { c6[r] = ground_dot(J, r, a) - ar[r]; c6[3 + r] = ground_dot(J, r, s); }
-  } else {
+  } else if constexpr (BODY) {
     body_ls_terms(m, W.bc + (c - 3 - ng) * NBF, W.P, W.vi, a, s, c6, D);
   }
 }
@@ -186,8 +186,9 @@ __device__ __forceinline__ int body_eval(const ModelT<T>& m, EnvWork<T>& W, int 
 
 // Newton on f(a); a replicated in every lane of the row.  W.H holds the dense
 // mass matrix (packed lower) for this forward, W.qfs the smooth force.
-template <typename T>
+template <bool BODY, typename T>
 __device__ int solve16(const ModelT<T>& m, EnvWork<T>& W, int ng, int nb, T* a, int tl) {
+  if constexpr (!BODY) nb = 0;
   const Mass<T>& M = W.M;
   const int nc = 3 + ng + nb;
   const int row = tl < NV ? tl : NV - 1;
@@ -257,7 +258,7 @@ __device__ int solve16(const ModelT<T>& m, EnvWork<T>& W, int ng, int nb, T* a, 
     team_sync();  // cj visible to every row owner
     // base-tree contacts (rare): sequential over the contacts, every lane
     // computing the same -J'f (added after the team sums)
-    for (int b = 0; b < nb; b++) {
+    for (int b = 0; BODY && b < nb; b++) {
       T ar[3], Dc, f[3], Cc[6];
       const int hinge = body_eval(m, W, b, a, ar, Dc, f, Cc);
 #pragma unroll
@@ -311,7 +312,7 @@ __device__ int solve16(const ModelT<T>& m, EnvWork<T>& W, int ng, int nb, T* a, 
       }
     // base-tree contacts (rare): each lane rebuilds contact b and adds
     // J_b' C_b J_b to its row
-    for (int b = 0; b < nb; b++) {
+    for (int b = 0; BODY && b < nb; b++) {
       T ar[3], Dc, f[3], Cc[6];
       const int hinge = body_eval(m, W, b, a, ar, Dc, f, Cc);
       // this row's column of J (dof row -> column position, or none)
@@ -362,7 +363,7 @@ __device__ int solve16(const ModelT<T>& m, EnvWork<T>& W, int ng, int nb, T* a, 
     // line-search cache: jar(0) and J s of this lane's first contact in
     // registers; later rounds (more than 16 contacts) recompute them
     T c6r[6], Dr;
-    ls_terms(m, W, tl, ng, nc, a, s, c6r, Dr);
+    ls_terms<BODY>(m, W, tl, ng, nc, a, s, c6r, Dr);
     T lo = 0, dlo = d0, hi = -1, dhi = 0, alpha = 1;
     T flo = d0, fhi = 0;
     int side = 0, same = 0;
@@ -376,7 +377,7 @@ __device__ int solve16(const ModelT<T>& m, EnvWork<T>& W, int ng, int nb, T* a, 
           for (int r = 0; r < 6; r++) c6[r] = c6r[r];
           Dc = Dr;
         } else {
-          ls_terms(m, W, c, ng, nc, a, s, c6, Dc);
+          ls_terms<BODY>(m, W, c, ng, nc, a, s, c6, Dc);
         }
         const bool wheel = c < 3;
         const T D[3] = {wheel ? W.wc[c].D[0] : Dc, wheel ? W.wc[c].D[1] : Dc, wheel ? W.wc[c].D[2] : Dc};
@@ -506,6 +507,53 @@ __device__ __forceinline__ void put_body(T* bc, int slot, const T* n, const T* p
   for (int i = 0; i < 3; i++) { s[BF_N + i] = n[i]; s[BF_P + i] = pos[i]; }
   s[BF_DIST] = dist;
   s[BF_CODE] = T(8 * b1 + b2);
+}
+
+// Fast-path test: can any base-tree contact exist at this configuration?
+// Exact for ball x {tower, sticks}; for hfield x geom it asks whether any
+// heightfield vertex under the geom's AABB reaches the geom's lowest point --
+// MuJoCo's own prism pre-filter (a prism whose three top vertices are below
+// the geom's AABB is skipped), so "no" is exact and "yes" sends the env to the
+// full kernel.  Team-uniform result.
+template <typename T>
+__device__ bool body_candidates(const ModelT<T>& m, const Kin<T>& k, const float* hf, T size_z, T hz, int tl) {
+  bool cand = false;
+  if (tl < 3) {
+    Seg<T> g;
+    body_geom(m, k, tl, g);
+    T dist, n[3], pos[3];
+    cand = tl == 0 ? sphere_cylinder(k.c, m.ball_r, g, dist, n, pos) : sphere_capsule(k.c, m.ball_r, g, dist, n, pos);
+  }
+  if (hf) {
+    const T sx = m.hf_sx, sy = m.hf_sy, zb = m.hf_bottom;
+    const int N1 = HF_N - 1;
+    for (int gi = 0; gi < 6; gi++) {
+      Seg<T> g;
+      body_geom(m, k, gi, g);
+      T lo[3], hi[3];
+#pragma unroll
+      for (int i = 0; i < 3; i++) {
+        const T ai = fabs(g.a[i]);
+        const T rad = T(1) - ai * ai;
+        const T ext = gi == 0 ? g.hh * ai + g.r * sqrt(rad > 0 ? rad : T(0)) : g.hh * ai + g.r;
+        lo[i] = g.c[i] - ext; hi[i] = g.c[i] + ext;
+      }
+      if (lo[2] > hz) continue;
+      if (lo[0] > sx || hi[0] < -sx || lo[1] > sy || hi[1] < -sy || lo[2] > size_z || hi[2] < -zb) continue;
+      int cmin = (int)floor((lo[0] + sx) / (2 * sx) * N1), cmax = (int)ceil((hi[0] + sx) / (2 * sx) * N1);
+      int rmin = (int)floor((lo[1] + sy) / (2 * sy) * N1), rmax = (int)ceil((hi[1] + sy) / (2 * sy) * N1);
+      cmin = cmin < 0 ? 0 : cmin; cmax = cmax > N1 ? N1 : cmax;
+      rmin = rmin < 0 ? 0 : rmin; rmax = rmax > N1 ? N1 : rmax;
+      if (rmax <= rmin || cmax <= cmin) continue;  // no prism
+      const int nc = cmax - cmin + 1, total = (rmax - rmin + 1) * nc;
+      for (int i = tl; i < total; i += L) {
+        const int ri = rmin + i / nc, ci = cmin + i % nc;
+        cand = cand || T(hf[ri * HF_N + ci]) * size_z >= lo[2];
+      }
+    }
+  }
+  const unsigned bits = unsigned(__ballot(cand) >> (threadIdx.x & ~(L - 1))) & 0xFFFFu;
+  return bits != 0;
 }
 
 // Dynamic pairs of the base-tree geoms (bb_bodycon.h), team-parallel, in the

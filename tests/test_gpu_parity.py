@@ -172,3 +172,35 @@ def test_forward_parity_base_tree_contacts(oracle, precision, terrain):
         assert err < 1e-7, (e, err, fo.nbody)
     assert touched >= n // 4
     env.close()
+
+
+@pytest.mark.parametrize("terrain", ["flat", "hills"])
+def test_step_parity_base_tree_contacts(oracle, terrain):
+    """env.step from states with base-tree contacts: the fast kernel hands
+    these envs to the full kernel (stats.slow_path), results vs the oracle."""
+    from ballbot_gym.terrain import generate_hills_terrain
+
+    n = 64
+    if terrain == "flat":
+        hf = oracle.flat_hfield()
+        tcfg = {"type": "flat", "config": {}}
+    else:
+        hf = generate_hills_terrain(293, seed=7).astype(np.float32)
+        tcfg = {"type": "hills", "config": {"seed": 7}}
+    env = _make_env(n, "fp64", tcfg)
+    qs, vs = _body_contact_states(oracle, n, seed=12)
+    rng = np.random.default_rng(2)
+    acts = rng.uniform(-1, 1, (n, 3)).astype(np.float32)
+    env.set_state(qs, vs, np.zeros((n, 15)), np.zeros(n, np.int32))
+    s0 = env.stats()["slow_path"]
+    obs, rew, term, trunc, info = env.step(torch.tensor(acts, device=env.device))
+    assert env.stats()["slow_path"] - s0 >= n // 4
+    q, v, w, st = env.get_state()
+    cfg = oracle.default_cfg()
+    for e in range(n):
+        qe, ve, we, se = qs[e].copy(), vs[e].copy(), np.zeros(15), np.zeros(1, np.int32)
+        o, r, fl, _, _ = oracle.env_step(cfg, qe, ve, we, se, acts[e], hf)
+        assert np.abs(q[e] - qe).max() < 1e-9, e
+        assert np.abs(v[e] - ve).max() < 1e-6 * max(1.0, np.abs(ve).max()), e
+        assert np.abs(obs.cpu().numpy()[e] - o).max() < 1e-6, e
+    env.close()

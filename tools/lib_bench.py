@@ -1,0 +1,72 @@
+"""A/B timing of variant builds of csrc/bb_kernels.hip (diagnostic, GPU box).
+
+  python tools/lib_bench.py --variant NAME:-DFLAG[,-DFLAG2] ... [--precision fp64]
+
+Each variant is compiled into tools/_build/libbb_<NAME>.so (hipcc gfx950),
+loaded in a fresh process and timed on the bench workload (4096 envs, flat,
+random actions); prints one JSON line per variant.
+"""
+import argparse
+import json
+import subprocess
+import sys
+import time
+from pathlib import Path
+
+ROOT = Path(__file__).resolve().parents[1]
+sys.path.insert(0, str(ROOT / "openballbot-rl_amd"))
+
+
+def build(name, flags):
+    out = ROOT / "tools" / "_build" / f"libbb_{name}.so"
+    out.parent.mkdir(parents=True, exist_ok=True)
+    cmd = ["hipcc", "--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC", "-shared", *flags, "-o", str(out),
+           str(ROOT / "openballbot-rl_amd" / "csrc" / "bb_kernels.hip")]
+    subprocess.run(cmd, check=True)
+    return out
+
+
+def run_one(lib, precision, terrain, steps, warmup):
+    import torch
+    from ballbot_gym import _native
+    from ballbot_gym.envs import BallbotVecEnv
+
+    _native.use_diagnostic_library(lib)
+    env = BallbotVecEnv(4096, device="cuda:0", precision=precision, terrain_config={"type": terrain, "config": {}})
+    pool = torch.rand(64, 4096, 3, device="cuda:0") * 2 - 1
+    for i in range(warmup):
+        env.step_async_raw(pool[i % 64])
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for i in range(steps):
+        env.step_async_raw(pool[i % 64])
+    torch.cuda.synchronize()
+    dt = (time.perf_counter() - t0) / steps
+    return {"ms": dt * 1e3, "env_steps_per_s": 4096 / dt, "stats": env.stats()}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--variant", action="append", default=[], help="NAME:-DFLAG,-DFLAG2 (empty flags allowed)")
+    ap.add_argument("--precision", default="fp64")
+    ap.add_argument("--terrain", default="flat")
+    ap.add_argument("--steps", type=int, default=300)
+    ap.add_argument("--warmup", type=int, default=300)
+    ap.add_argument("--child", default=None)
+    a = ap.parse_args()
+    if a.child:
+        print(json.dumps(run_one(a.child, a.precision, a.terrain, a.steps, a.warmup)))
+        return
+    for v in a.variant:
+        name, _, fl = v.partition(":")
+        lib = build(name, [f for f in fl.split(",") if f])
+        r = subprocess.run([sys.executable, __file__, "--child", str(lib), "--precision", a.precision,
+                            "--terrain", a.terrain, "--steps", str(a.steps), "--warmup", str(a.warmup)],
+                           capture_output=True, text=True, timeout=600)
+        line = r.stdout.strip().splitlines()[-1] if r.returncode == 0 else r.stderr[-2000:]
+        print(json.dumps({"variant": name, "flags": fl, "precision": a.precision, "terrain": a.terrain,
+                          "result": json.loads(line) if r.returncode == 0 else line}), flush=True)
+
+
+if __name__ == "__main__":
+    main()
