@@ -155,6 +155,12 @@ BB_HD bool capsule_prism(const Seg<T>& g, const PrismG<T>& P, T& dist, T* n, T* 
   T p0[3], p1[3];
   seg_ends(g, p0, p1);
   T dir[3] = {p1[0] - p0[0], p1[1] - p0[1], p1[2] - p0[2]};
+  // separated by more than r along a face normal: no contact (cheap early out)
+#pragma unroll
+  for (int f = 0; f < 5; f++) {
+    const T d0 = dot3(P.pn[f], p0) - P.pd[f], d1 = dot3(P.pn[f], p1) - P.pd[f];
+    if (d0 >= g.r && d1 >= g.r) return false;
+  }
   T t0 = 0, t1 = 1;
   bool inter = true;
 #pragma unroll

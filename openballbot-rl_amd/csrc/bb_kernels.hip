@@ -81,7 +81,10 @@ struct Dev {
   uint64_t seed;
   unsigned long long* stats;  // resets, diverged, overflow, slow-path env-steps, iters
   int* slow_list;             // envs the fast kernel handed to the full kernel this step
-  int* slow_count;
+  int* slow_count;            // [0] fast list size, [1] predicted-slow list size, [2] hand-overs
+  int* fast_envs;             // this step's fast-kernel env list (ascending)
+  int* pred_envs;             // envs predicted to need base-tree contacts (full kernel, concurrent)
+  uint8_t* pred_mark;
 };
 
 template <typename T>
@@ -122,7 +125,8 @@ template <typename T, bool BODY>
 __global__ __launch_bounds__(64) void step_kernel(ModelT<T> mg, EnvCfg cfg, Dev d, const float* __restrict__ act,
                                                   float* __restrict__ obs, float* __restrict__ rew,
                                                   uint8_t* __restrict__ done, float* __restrict__ tobs,
-                                                  float* __restrict__ pos2d, int auto_reset, int L, int epw) {
+                                                  float* __restrict__ pos2d, int auto_reset, int L, int epw,
+                                                  const int* __restrict__ elist, const int* __restrict__ ecount) {
   // epw teams of L lanes per 64-lane wave (teams >= epw idle)
   extern __shared__ __align__(16) unsigned char smem[];
   // model constants staged in LDS once per workgroup: uniform-address LDS
@@ -135,9 +139,9 @@ __global__ __launch_bounds__(64) void step_kernel(ModelT<T> mg, EnvCfg cfg, Dev 
   const int team = threadIdx.x / L;
   if (team >= epw) return;
   int e = blockIdx.x * epw + team;
-  if constexpr (BODY) {
-    if (e >= *d.slow_count) return;
-    e = d.slow_list[e];
+  if (elist) {  // env list of this launch (ascending env ids)
+    if (e >= *ecount) return;
+    e = elist[e];
   }
   if (e >= d.n) return;
   const bool lead = tm.tl == 0;
@@ -154,12 +158,12 @@ __global__ __launch_bounds__(64) void step_kernel(ModelT<T> mg, EnvCfg cfg, Dev 
   int fl = env_step<T, BODY>(m, cfg, q, v, w, step, a, tr, W, o, r, p2, &iters, tm);
   if (!BODY && (fl & F_SLOWPATH)) {
     if (lead) {
-      d.slow_list[atomicAdd(d.slow_count, 1)] = e;
-      atomicAdd(&d.stats[3], 1ull);
+      d.slow_list[atomicAdd(d.slow_count + 2, 1)] = e;
     }
     return;
   }
   if (!lead) return;
+  if (BODY) atomicAdd(&d.stats[3], 1ull);  // env-steps through the full kernel
   if (tobs) {
 #pragma unroll
     for (int i = 0; i < 15; i++) tobs[15 * e + i] = o[i];
@@ -229,6 +233,123 @@ __global__ __launch_bounds__(64) void forward_kernel(ModelT<T> mg, Dev d, const 
   if (ncon) { ncon[2 * e] = so.ng; ncon[2 * e + 1] = so.nb; }
 }
 
+// Which envs should take the full kernel this step: a base-tree geom within a
+// margin of the ball or of a heightfield vertex under it (the fast kernel's
+// exact per-stage test stays the arbiter; this only routes work).  One lane
+// per env.
+template <typename T>
+__global__ __launch_bounds__(64) void predict_kernel(ModelT<T> mg, Dev d) {
+  __shared__ ModelT<T> ms;
+  if (threadIdx.x == 0) ms = mg;
+  __syncthreads();
+  const ModelT<T>& m = ms;
+  const int e = blockIdx.x * 64 + threadIdx.x;
+  if (e >= d.n) return;
+  const T* Q = (const T*)d.qpos;
+  const T* V = (const T*)d.qvel;
+  T pb[3], qb[4], pB[3], qB[4];
+#pragma unroll
+  for (int i = 0; i < 3; i++) { pb[i] = Q[i * d.n + e]; pB[i] = Q[(10 + i) * d.n + e]; }
+#pragma unroll
+  for (int i = 0; i < 4; i++) { qb[i] = Q[(3 + i) * d.n + e]; qB[i] = Q[(13 + i) * d.n + e]; }
+  qnormalize(qb);
+  qnormalize(qB);
+  T Rb[9], RB[9];
+  q2mat(Rb, qb);
+  q2mat(RB, qB);
+  T vb = 0, wb = 0;
+#pragma unroll
+  for (int i = 0; i < 3; i++) {
+    const T a = V[i * d.n + e], b = V[(3 + i) * d.n + e];
+    vb += a * a; wb += b * b;
+  }
+  // one step's reach of any geom point (|v| + 0.5 m |w|) h, x3, + 1 cm
+  const T margin = T(3) * m.h * (sqrt(vb) + T(0.5) * sqrt(wb)) + T(0.01);
+  const T cB[3] = {pB[0] + RB[2] * m.dz, pB[1] + RB[5] * m.dz, pB[2] + RB[8] * m.dz};  // ball centre
+  const int tid = d.terrain[e];
+  const float* hf = d.bank + size_t(tid) * (HF_N * HF_N);
+  const T size_z = T(d.size_z[tid]), hz = T(d.hmax[tid]) * size_z;
+  bool slow = false;
+  for (int gi = 0; gi < 6 && !slow; gi++) {
+    // geom gi as a segment (base frame): tower axis, stick, wheel capsule
+    // (axis = hinge axis; centre at zero hinge angle, +1 mm for its 0.3 mm offset)
+    T cl[3], al[3], hh, gr;
+    if (gi == 0) {
+      cl[0] = m.tower_c[0]; cl[1] = m.tower_c[1]; cl[2] = m.tower_c[2];
+      al[0] = 0; al[1] = 0; al[2] = 1;
+      hh = m.tower_hh; gr = m.tower_r;
+    } else if (gi <= 2) {
+#pragma unroll
+      for (int i = 0; i < 3; i++) { cl[i] = m.stick_c[gi - 1][i]; al[i] = m.stick_a[gi - 1][i]; }
+      hh = m.stick_hh; gr = m.stick_r;
+    } else {
+      const int w = gi - 3;
+      T R[9], t[3];
+      q2mat(R, m.wq[w]);
+      const T dd[3] = {m.cw[0] - m.jpos[0], m.cw[1] - m.jpos[1], m.cw[2] - m.jpos[2]};
+      mv3(t, R, dd);
+      cl[0] = m.anchor[0] + t[0]; cl[1] = m.anchor[1] + t[1]; cl[2] = m.anchor[2] + t[2];
+      al[0] = m.u[w][0]; al[1] = m.u[w][1]; al[2] = m.u[w][2];
+      hh = m.wheel_hh; gr = m.wheel_r + T(0.001);
+    }
+    T cw[3], aw[3];
+    mv3(cw, Rb, cl);
+    cw[0] += pb[0]; cw[1] += pb[1]; cw[2] += pb[2];
+    mv3(aw, Rb, al);
+    T p0[3], p1[3];
+#pragma unroll
+    for (int i = 0; i < 3; i++) { p0[i] = cw[i] - hh * aw[i]; p1[i] = cw[i] + hh * aw[i]; }
+    if (gi == 0) {  // ball x tower: distance to the cylinder
+      const T dd[3] = {cB[0] - cw[0], cB[1] - cw[1], cB[2] - cw[2]};
+      const T z = dot3(dd, aw);
+      const T rv[3] = {dd[0] - z * aw[0], dd[1] - z * aw[1], dd[2] - z * aw[2]};
+      const T ez = maxT(fabs(z) - hh, T(0)), er = maxT(sqrt(dot3(rv, rv)) - gr, T(0));
+      slow = sqrt(ez * ez + er * er) < m.ball_r + margin;
+    } else if (gi < 3) {  // ball x sticks
+      T cp[3], cq[3];
+      slow = seg_seg(cB, cB, p0, p1, cp, cq) < m.ball_r + gr + margin;
+    }
+    // capsule-hull AABB of the geom, grown by the margin
+    const T ext = gr + margin;
+    const T lo = minT(p0[2], p1[2]) - ext;
+    if (slow || lo > hz) continue;
+    const T x0 = minT(p0[0], p1[0]) - ext, x1 = maxT(p0[0], p1[0]) + ext;
+    const T y0 = minT(p0[1], p1[1]) - ext, y1 = maxT(p0[1], p1[1]) + ext;
+    const T sx = m.hf_sx, sy = m.hf_sy;
+    const int N1 = HF_N - 1;
+    if (x0 > sx || x1 < -sx || y0 > sy || y1 < -sy) continue;
+    int cmin = (int)floor((x0 + sx) / (2 * sx) * N1), cmax = (int)ceil((x1 + sx) / (2 * sx) * N1);
+    int rmin = (int)floor((y0 + sy) / (2 * sy) * N1), rmax = (int)ceil((y1 + sy) / (2 * sy) * N1);
+    cmin = cmin < 0 ? 0 : cmin; cmax = cmax > N1 ? N1 : cmax;
+    rmin = rmin < 0 ? 0 : rmin; rmax = rmax > N1 ? N1 : rmax;
+    for (int r = rmin; r <= rmax && !slow; r++)
+      for (int c = cmin; c <= cmax; c++)
+        if (T(hf[r * HF_N + c]) * size_z >= lo) { slow = true; break; }
+  }
+  d.pred_mark[e] = slow ? 1 : 0;
+}
+
+// Stable split of 0..n-1 by pred_mark into fast_envs / pred_envs (one block).
+__global__ __launch_bounds__(1024) void split_kernel(Dev d) {
+  __shared__ int sf[1024], ss[1024];
+  const int t = threadIdx.x, per = (d.n + 1023) / 1024, b = t * per, e_ = min(d.n, b + per);
+  int nf = 0, ns = 0;
+  for (int e = b; e < e_; e++) { if (d.pred_mark[e]) ns++; else nf++; }
+  sf[t] = nf; ss[t] = ns;
+  __syncthreads();
+  for (int off = 1; off < 1024; off <<= 1) {  // inclusive scan
+    const int af = t >= off ? sf[t - off] : 0, as = t >= off ? ss[t - off] : 0;
+    __syncthreads();
+    sf[t] += af; ss[t] += as;
+    __syncthreads();
+  }
+  int of = sf[t] - nf, os = ss[t] - ns;
+  for (int e = b; e < e_; e++) {
+    if (d.pred_mark[e]) d.pred_envs[os++] = e; else d.fast_envs[of++] = e;
+  }
+  if (t == 1023) { d.slow_count[0] = sf[t]; d.slow_count[1] = ss[t]; d.slow_count[2] = 0; }
+}
+
 __global__ void assign_kernel(Dev d, const int32_t* ids) {
   const int e = blockIdx.x * blockDim.x + threadIdx.x;
   if (e >= d.n) return;
@@ -240,6 +361,8 @@ __global__ void assign_kernel(Dev d, const int32_t* ids) {
 
 struct bb_handle {
   int n, device, fp64, team, epw;
+  hipStream_t side;                 // the concurrent full-kernel launch
+  hipEvent_t fork, join;
   bb_params p;
   EnvCfg cfg;
   ModelT<float> mf;
@@ -275,14 +398,23 @@ int launch_step(bb_handle* h, const float* a, float* o, float* r, uint8_t* dn, f
                 hipStream_t s) {
   const ModelT<T>& m = model_of<T>(h);
   const int epw = h->epw;
-  int blocks = (h->n + epw - 1) / epw;
-  // fast kernel for every env, then the full kernel over the envs it handed over
-  HIPCHK(hipMemsetAsync(h->d.slow_count, 0, sizeof(int), s));
-  hipLaunchKernelGGL((step_kernel<T, false>), dim3(blocks), dim3(WAVE), lds_bytes<T>(epw), s, m, h->cfg, h->d, a, o, r,
-                     dn, t, p2, ar, h->team, epw);
-  HIPCHK(hipGetLastError());
-  hipLaunchKernelGGL((step_kernel<T, true>), dim3(blocks), dim3(WAVE), lds_bytes<T>(epw), s, m, h->cfg, h->d, a, o, r,
-                     dn, t, p2, ar, h->team, epw);
+  const int blocks = (h->n + epw - 1) / epw;
+  const size_t lds = lds_bytes<T>(epw);
+  int* cnt = h->d.slow_count;
+  // route: envs near a base-tree contact -> full kernel (side stream,
+  // concurrent); the rest -> fast kernel; its hand-overs -> full kernel after
+  hipLaunchKernelGGL(predict_kernel<T>, dim3((h->n + 63) / 64), dim3(64), 0, s, m, h->d);
+  hipLaunchKernelGGL(split_kernel, dim3(1), dim3(1024), 0, s, h->d);
+  HIPCHK(hipEventRecord(h->fork, s));
+  HIPCHK(hipStreamWaitEvent(h->side, h->fork, 0));
+  hipLaunchKernelGGL((step_kernel<T, true>), dim3(blocks), dim3(WAVE), lds, h->side, m, h->cfg, h->d, a, o, r, dn, t,
+                     p2, ar, h->team, epw, (const int*)h->d.pred_envs, (const int*)(cnt + 1));
+  hipLaunchKernelGGL((step_kernel<T, false>), dim3(blocks), dim3(WAVE), lds, s, m, h->cfg, h->d, a, o, r, dn, t, p2,
+                     ar, h->team, epw, (const int*)h->d.fast_envs, (const int*)(cnt + 0));
+  HIPCHK(hipEventRecord(h->join, h->side));
+  HIPCHK(hipStreamWaitEvent(s, h->join, 0));
+  hipLaunchKernelGGL((step_kernel<T, true>), dim3(blocks), dim3(WAVE), lds, s, m, h->cfg, h->d, a, o, r, dn, t, p2,
+                     ar, h->team, epw, (const int*)h->d.slow_list, (const int*)(cnt + 2));
   HIPCHK(hipGetLastError());
   return 0;
 }
@@ -375,8 +507,14 @@ int bb_create(int n_envs, int device, const bb_params* p, bb_handle** out) {
   HIPCHK(hipMemset(h->hmax, 0, sizeof(float) * nt));
   HIPCHK(hipMalloc((void**)&d.stats, sizeof(unsigned long long) * 8));
   HIPCHK(hipMalloc((void**)&d.slow_list, sizeof(int) * n));
-  HIPCHK(hipMalloc((void**)&d.slow_count, sizeof(int)));
-  HIPCHK(hipMemset(d.slow_count, 0, sizeof(int)));
+  HIPCHK(hipMalloc((void**)&d.slow_count, sizeof(int) * 4));
+  HIPCHK(hipMemset(d.slow_count, 0, sizeof(int) * 4));
+  HIPCHK(hipMalloc((void**)&d.fast_envs, sizeof(int) * n));
+  HIPCHK(hipMalloc((void**)&d.pred_envs, sizeof(int) * n));
+  HIPCHK(hipMalloc((void**)&d.pred_mark, n));
+  HIPCHK(hipStreamCreateWithFlags(&h->side, hipStreamNonBlocking));
+  HIPCHK(hipEventCreateWithFlags(&h->fork, hipEventDisableTiming));
+  HIPCHK(hipEventCreateWithFlags(&h->join, hipEventDisableTiming));
   HIPCHK(hipMemset(d.steps, 0, sizeof(int) * n));
   HIPCHK(hipMemset(d.terrain, 0, sizeof(int) * n));
   HIPCHK(hipMemset(d.pending_terrain, 0, sizeof(int) * n));
@@ -413,6 +551,8 @@ int bb_destroy(bb_handle* h) {
   (void)hipFree(h->d.steps); (void)hipFree(h->d.terrain); (void)hipFree(h->d.pending_terrain); (void)hipFree(h->d.episodes);
   (void)hipFree(h->bank); (void)hipFree(h->size_z); (void)hipFree(h->offset); (void)hipFree(h->hmax); (void)hipFree(h->d.stats);
   (void)hipFree(h->d.slow_list); (void)hipFree(h->d.slow_count);
+  (void)hipFree(h->d.fast_envs); (void)hipFree(h->d.pred_envs); (void)hipFree(h->d.pred_mark);
+  (void)hipStreamDestroy(h->side); (void)hipEventDestroy(h->fork); (void)hipEventDestroy(h->join);
   delete h;
   return 0;
 }

@@ -749,6 +749,9 @@ static double seg_axis_depth(const Prism* P, const double* p0, const double* p1,
 static int capsule_prism(const Convex* g, const Prism* P, double* dist, double* n, double* pos) {
   double p0[3], p1[3];
   convex_ends(g, p0, p1);
+  /* separated by more than r along a face normal: no contact */
+  for (int f = 0; f < 5; f++)
+    if (v3dot(P->pn[f], p0) - P->pd[f] >= g->r && v3dot(P->pn[f], p1) - P->pd[f] >= g->r) return 0;
   /* segment inside prism?  clip against the 5 half-spaces n.x <= d */
   double t0 = 0, t1 = 1, dir[3];
   v3sub(dir, p1, p0);

@@ -176,8 +176,8 @@ def test_forward_parity_base_tree_contacts(oracle, precision, terrain):
 
 @pytest.mark.parametrize("terrain", ["flat", "hills"])
 def test_step_parity_base_tree_contacts(oracle, terrain):
-    """env.step from states with base-tree contacts: the fast kernel hands
-    these envs to the full kernel (stats.slow_path), results vs the oracle."""
+    """env.step from states with base-tree contacts: they are routed to the full
+    kernel (stats.slow_path counts full-kernel env-steps), results vs the oracle."""
     from ballbot_gym.terrain import generate_hills_terrain
 
     n = 64
