@@ -113,6 +113,7 @@ def main() -> None:
         dist.barrier()
     torch.cuda.synchronize()
     ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    env.time_kernel(args.steps)  # HIP events around the dominant (fast step) kernel on the env's stream
     t0 = time.perf_counter()
     ev0.record()
     for i in range(args.steps):
@@ -123,7 +124,8 @@ def main() -> None:
         dist.barrier()
     torch.cuda.synchronize()
     elapsed = time.perf_counter() - t0
-    kern_ms = ev0.elapsed_time(ev1) / args.steps  # one step kernel per step, on the env's stream
+    step_ms = ev0.elapsed_time(ev1) / args.steps  # whole bb_step sequence per step, torch's stream
+    kern_ms, kern_n = env.kernel_ms()  # dominant kernel alone
     elapsed = max_over_ranks(elapsed, device=dev)
     stats = env.stats()
     launch = env.launch_config()
@@ -163,7 +165,8 @@ def main() -> None:
                          "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
                          "note": "latency/VALU-bound per-lane physics; HBM bytes = algorithmic state I/O "
                                  f"({algorithmic_bytes(args.precision)} B/env-step)",
-                         "kernel_ms": kern_ms},
+                         "kernel": "step_kernel<T,false> (fast path)", "kernel_ms": kern_ms,
+                         "kernel_launches_timed": kern_n, "step_ms_hip_events": step_ms},
             "stats": stats,
         }
         if world == 1 and not args.no_cpu_baseline:

@@ -110,6 +110,12 @@ int bb_get_stats(bb_handle* h, int64_t* out6);
 int bb_get_config(bb_handle* h, int32_t* out5);
 /* init height offset per terrain (ballbot_env.py:546-563) */
 int bb_get_offsets(bb_handle* h, float* out);
+/* measurement: time the next max_launches fast step kernels (the dominant
+ * kernel of bb_step) with HIP events on the caller's stream; bb_kernel_ms
+ * waits for them and returns their average duration.  No reference
+ * counterpart (bench.py's roofline.achieved). */
+int bb_time_kernel(bb_handle* h, int max_launches);
+int bb_kernel_ms(bb_handle* h, double* avg_ms, int32_t* launches);
 
 #ifdef __cplusplus
 }

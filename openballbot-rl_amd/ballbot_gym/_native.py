@@ -46,7 +46,7 @@ class BBParams(C.Structure):
 EXPORTS = [
     "bb_abi_version", "bb_last_error", "bb_default_params", "bb_create", "bb_destroy", "bb_set_hfield",
     "bb_assign_terrain", "bb_reset", "bb_step", "bb_get_state", "bb_set_state", "bb_forward", "bb_get_stats",
-    "bb_get_offsets", "bb_get_config",
+    "bb_get_offsets", "bb_get_config", "bb_time_kernel", "bb_kernel_ms",
 ]
 
 ABI_VERSION = 3  # include/ballbot_mi355x.h BB_ABI_VERSION
@@ -111,6 +111,8 @@ def _load(path: Path):
     L.bb_get_stats.argtypes = [vp, C.POINTER(C.c_int64)]
     L.bb_get_offsets.argtypes = [vp, fp]
     L.bb_get_config.argtypes = [vp, C.POINTER(C.c_int32)]
+    L.bb_time_kernel.argtypes = [vp, C.c_int]
+    L.bb_kernel_ms.argtypes = [vp, C.POINTER(C.c_double), C.POINTER(C.c_int32)]
     for name in [n for n in EXPORTS if n not in ("bb_default_params", "bb_abi_version")]:
         getattr(L, name).restype = C.c_int
     if L.bb_abi_version() != ABI_VERSION:

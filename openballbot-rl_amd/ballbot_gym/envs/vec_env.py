@@ -172,6 +172,16 @@ class BallbotVecEnv:
         return {"resets": out[0], "diverged": out[1], "overflow": out[2], "slow_path": out[3],
                 "solver_iters": out[4] + (out[5] << 32)}
 
+    def time_kernel(self, max_launches: int) -> None:
+        """Time the next `max_launches` fast step kernels with HIP events (bench.py)."""
+        N.check(N.lib().bb_time_kernel(self._h, int(max_launches)), "bb_time_kernel")
+
+    def kernel_ms(self):
+        """(average fast-step-kernel duration in ms, launches timed) since time_kernel()."""
+        ms, k = C.c_double(), C.c_int32()
+        N.check(N.lib().bb_kernel_ms(self._h, C.byref(ms), C.byref(k)), "bb_kernel_ms")
+        return ms.value, k.value
+
     def launch_config(self) -> Dict[str, int]:
         out = (C.c_int32 * 5)()
         N.check(N.lib().bb_get_config(self._h, out), "bb_get_config")

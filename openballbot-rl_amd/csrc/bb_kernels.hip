@@ -373,6 +373,9 @@ struct bb_handle {
   float* offset;
   float* hmax;
   std::vector<float> h_offset;
+  // optional HIP-event timing of the fast step kernel (bb_time_kernel)
+  std::vector<hipEvent_t> tev;
+  int tcap = 0, tn = 0;
 };
 
 template <typename T> const ModelT<T>& model_of(const bb_handle* h);
@@ -409,8 +412,11 @@ int launch_step(bb_handle* h, const float* a, float* o, float* r, uint8_t* dn, f
   HIPCHK(hipStreamWaitEvent(h->side, h->fork, 0));
   hipLaunchKernelGGL((step_kernel<T, true>), dim3(blocks), dim3(WAVE), lds, h->side, m, h->cfg, h->d, a, o, r, dn, t,
                      p2, ar, h->team, epw, (const int*)h->d.pred_envs, (const int*)(cnt + 1));
+  const bool timed = h->tn < h->tcap;
+  if (timed) HIPCHK(hipEventRecord(h->tev[2 * h->tn], s));
   hipLaunchKernelGGL((step_kernel<T, false>), dim3(blocks), dim3(WAVE), lds, s, m, h->cfg, h->d, a, o, r, dn, t, p2,
                      ar, h->team, epw, (const int*)h->d.fast_envs, (const int*)(cnt + 0));
+  if (timed) { HIPCHK(hipEventRecord(h->tev[2 * h->tn + 1], s)); h->tn++; }
   HIPCHK(hipEventRecord(h->join, h->side));
   HIPCHK(hipStreamWaitEvent(s, h->join, 0));
   hipLaunchKernelGGL((step_kernel<T, true>), dim3(blocks), dim3(WAVE), lds, s, m, h->cfg, h->d, a, o, r, dn, t, p2,
@@ -553,6 +559,7 @@ int bb_destroy(bb_handle* h) {
   (void)hipFree(h->d.slow_list); (void)hipFree(h->d.slow_count);
   (void)hipFree(h->d.fast_envs); (void)hipFree(h->d.pred_envs); (void)hipFree(h->d.pred_mark);
   (void)hipStreamDestroy(h->side); (void)hipEventDestroy(h->fork); (void)hipEventDestroy(h->join);
+  for (hipEvent_t e : h->tev) (void)hipEventDestroy(e);
   delete h;
   return 0;
 }
@@ -696,6 +703,34 @@ int bb_debug_phase_cycles(unsigned long long* out16) {
   return 0;
 }
 #endif
+
+int bb_time_kernel(bb_handle* h, int max_launches) {
+  if (!h) return fail("bb_time_kernel: NULL handle");
+  if (max_launches < 0) return fail("bb_time_kernel: max_launches must be >= 0");
+  HIPCHK(hipSetDevice(h->device));
+  HIPCHK(hipDeviceSynchronize());
+  for (hipEvent_t e : h->tev) (void)hipEventDestroy(e);
+  h->tev.assign(2 * (size_t)max_launches, nullptr);
+  for (hipEvent_t& e : h->tev) HIPCHK(hipEventCreate(&e));
+  h->tcap = max_launches;
+  h->tn = 0;
+  return 0;
+}
+
+int bb_kernel_ms(bb_handle* h, double* avg_ms, int32_t* launches) {
+  if (!h || !avg_ms) return fail("bb_kernel_ms: NULL argument");
+  HIPCHK(hipSetDevice(h->device));
+  double sum = 0.0;
+  for (int i = 0; i < h->tn; i++) {
+    HIPCHK(hipEventSynchronize(h->tev[2 * i + 1]));
+    float ms = 0.f;
+    HIPCHK(hipEventElapsedTime(&ms, h->tev[2 * i], h->tev[2 * i + 1]));
+    sum += ms;
+  }
+  *avg_ms = h->tn ? sum / h->tn : 0.0;
+  if (launches) *launches = h->tn;
+  return 0;
+}
 
 int bb_get_offsets(bb_handle* h, float* out) {
   if (!h || !out) return fail("bb_get_offsets: NULL argument");

@@ -17,6 +17,11 @@ from pathlib import Path
 KERNEL = "step_kernel"
 
 
+def is_fast(name):
+    """The dominant kernel: the fast step kernel step_kernel<T, false>."""
+    return KERNEL in name and ", false>" in name
+
+
 def rows(p):
     with open(p) as f:
         return list(csv.DictReader(f))
@@ -25,7 +30,7 @@ def rows(p):
 def counters(p, names, last):
     per = {}
     for r in rows(p):
-        if KERNEL not in r["Kernel_Name"]:
+        if not is_fast(r["Kernel_Name"]):
             continue
         d = per.setdefault(int(r["Dispatch_Id"]), {})
         d[r["Counter_Name"]] = d.get(r["Counter_Name"], 0.0) + float(r["Counter_Value"])
@@ -44,7 +49,7 @@ def main():
     src, dst = Path(a.src), Path(a.dst)
     dst.parent.mkdir(parents=True, exist_ok=True)
     shutil.copy(src / "trace" / "run_kernel_stats.csv", str(dst) + "_kernel_stats.csv")
-    tr = [r for r in rows(src / "trace" / "run_kernel_trace.csv") if KERNEL in r["Kernel_Name"]]
+    tr = [r for r in rows(src / "trace" / "run_kernel_trace.csv") if is_fast(r["Kernel_Name"])]
     tr.sort(key=lambda r: int(r["Start_Timestamp"]))
     timed = tr[-a.timed:]
     durs = [(int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) * 1e-6 for r in timed]
