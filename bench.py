@@ -79,6 +79,8 @@ def main() -> None:
     ap.add_argument("--envs", type=int, default=4096, help="envs per GPU")
     ap.add_argument("--precision", default="fp64", choices=["fp32", "fp64"])
     ap.add_argument("--terrain", default="flat")
+    ap.add_argument("--n-terrains", type=int, default=None,
+                    help="terrain bank size (default: 16 host-generated seeds; perlin: the whole 10^4 seed space on the GPU)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
     ap.add_argument("--traffic-json", default=str(ROOT / "profiles" / "traffic.json"))
@@ -103,7 +105,7 @@ def main() -> None:
     # weak scaling: every rank owns a contiguous block of `--envs` global env ids
     first_env, n = env_shard(args.envs * world, rank, world)
     env = BallbotVecEnv(n, device=dev, precision=args.precision, seed=rank_seed(1000, first_env),
-                        terrain_config={"type": args.terrain, "config": {}})
+                        terrain_config={"type": args.terrain, "config": {}}, n_terrains=args.n_terrains)
     g = torch.Generator(device=dev).manual_seed(1234 + rank)
     pool = torch.rand(64, n, 3, generator=g, device=dev) * 2 - 1  # random actions resident in HBM
     for i in range(args.warmup):
@@ -145,7 +147,7 @@ def main() -> None:
             except Exception:
                 traffic = None
         line = {
-            "metric": "env-steps/sec at 4096 envs per GPU (flat terrain, random actions)",
+            "metric": f"env-steps/sec at {n} envs per GPU ({args.terrain} terrain, random actions)",
             "value": value,
             "unit": "env-steps/s",
             "n_gpus": world,
@@ -157,7 +159,9 @@ def main() -> None:
             "vs_baseline": None,
             "dtype": "f64" if args.precision == "fp64" else "f32",
             "data": "synthetic (uniform random actions in [-1,1], resident in HBM)",
-            "config": {"workload": f"{n} envs/GPU, {args.terrain} terrain, random actions (BASELINE configs[1])",
+            "config": {"workload": f"{n} envs/GPU, {args.terrain} terrain, random actions "
+                                   f"(BASELINE configs[{1 if args.terrain == 'flat' else 2}])",
+                       "n_terrains": env.n_terrains,
                        "envs_per_gpu": n, "total_envs": n * world, "precision": args.precision,
                        "parallelism": f"env-sharded x{world} (no collective on the step path)",
                        "launch": launch},

@@ -7,6 +7,7 @@
  *   bb_set_hfield    model.hfield_data = terrain_gen(n, seed)   ballbot_env.py:513
  *                    (+ hfield_size[2] rescale                  ballbot_env.py:486-495)
  *                    (+ init height offset                      ballbot_env.py:527-565)
+ *   bb_generate_perlin  generate_perlin_terrain per seed       terrain/perlin.py:8-74
  *   bb_assign_terrain   choice of terrain per env at reset      ballbot_env.py:501-513
  *   bb_reset         mj_resetData + height offset + mj_forward  ballbot_env.py:612-620
  *   bb_step          ctrl = -clip(10a); mj_step; _get_obs;      ballbot_env.py:903-1036
@@ -37,7 +38,7 @@
 extern "C" {
 #endif
 
-#define BB_ABI_VERSION 3
+#define BB_ABI_VERSION 4
 #define BB_NQ 17
 #define BB_NV 15
 #define BB_OBS 15
@@ -84,6 +85,23 @@ int bb_destroy(bb_handle* h);
 
 /* upload one terrain (host float32[293*293], row-major, values in [0,1]) */
 int bb_set_hfield(bb_handle* h, int terrain_id, const float* data_host, float size_z);
+/* perlin terrain generator arguments (terrain/perlin.py:8-16) */
+typedef struct {
+  double scale;       /* 25.0 */
+  int octaves;        /* 4 */
+  float persistence;  /* 0.2 */
+  float lacunarity;   /* 2.0 */
+  double amplitude;   /* 1.0 */
+} bb_perlin_cfg;
+
+/* generate perlin terrains for seeds_host[0..count) into bank slots
+ * [first_terrain_id, first_terrain_id + count) on the GPU, with their init
+ * offsets (synchronous).  Replaces generate_perlin_terrain(293, seed=s) +
+ * the hfield_data write at reset (terrain/perlin.py:8-74, ballbot_env.py:501-513). */
+int bb_generate_perlin(bb_handle* h, int first_terrain_id, int count, const int32_t* seeds_host,
+                       const bb_perlin_cfg* cfg, float size_z);
+/* copy terrain bank slot terrain_id (float32[293*293]) to host memory */
+int bb_get_hfield(bb_handle* h, int terrain_id, float* data_host);
 /* per-env terrain ids (device int32[n]) applied at the next reset */
 int bb_assign_terrain(bb_handle* h, const int32_t* ids_dev, void* stream);
 

@@ -62,6 +62,39 @@ def terrain_bank(terrain_config: Dict[str, Any], n_terrains: Optional[int], seed
     return [np.asarray(gen(n, seed=s), dtype=np.float32) for s in seeds], seeds, size_z
 
 
+PERLIN_DEFAULTS = {"scale": 25.0, "octaves": 4, "persistence": 0.2, "lacunarity": 2.0, "amplitude": 1.0}
+
+
+def gpu_perlin_plan(terrain_config: Dict[str, Any], n_terrains: Optional[int],
+                    seed: Optional[int]) -> Optional[Tuple[List[int], N.PerlinCfg, float]]:
+    """Seeds + generator args when the bank is generated on the GPU (bb_generate_perlin), else None.
+
+    Perlin without a fixed config seed: the reference draws a fresh seed from
+    integers(0, 10000) at every reset and regenerates (ballbot_env.py:501-513).
+    With n_terrains None the bank holds that whole seed space (slot == seed,
+    3.4 GB of HBM), so every reset draw the reference can make is resident; an
+    explicit n_terrains keeps the first n_terrains draws of np_random(seed)."""
+    if terrain_config.get("type", "flat") != "perlin":
+        return None
+    tcfg = dict(terrain_config.get("config", {}) or {})
+    if tcfg.get("seed") is not None:
+        return None
+    tcfg.pop("seed", None)
+    unknown = set(tcfg) - set(PERLIN_DEFAULTS)
+    if unknown:  # generate_perlin_terrain() would raise TypeError on these too
+        raise ValueError(f"perlin terrain: unknown config keys {sorted(unknown)}")
+    args = {**PERLIN_DEFAULTS, **tcfg}
+    if n_terrains is None:
+        seeds = list(range(TERRAIN_SEED_HIGH))
+    else:
+        if int(n_terrains) < 1:
+            raise ValueError(f"n_terrains must be >= 1, got {n_terrains}")
+        seeds = [int(s) for s in np_random(seed).integers(0, TERRAIN_SEED_HIGH, size=int(n_terrains))]
+    pc = N.PerlinCfg(float(args["scale"]), int(args["octaves"]), float(args["persistence"]),
+                     float(args["lacunarity"]), float(args["amplitude"]))
+    return seeds, pc, terrain_size_z(terrain_config)
+
+
 def init_offset(hfield: np.ndarray, size_z: float, n: int = N.HF_N) -> float:
     """Initial height offset: max terrain height under the ball footprint + 1 cm."""
     sz = HFIELD_HALF_SIZE

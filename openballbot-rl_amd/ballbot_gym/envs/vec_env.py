@@ -46,7 +46,7 @@ class BallbotVecEnv:
         n_terrains: Optional[int] = None,
         auto_reset: bool = True,
     ):
-        from .config import params_from_configs, terrain_bank
+        from .config import TERRAIN_SEED_HIGH, gpu_perlin_plan, np_random, params_from_configs, terrain_bank
 
         if not torch.cuda.is_available():
             raise RuntimeError("BallbotVecEnv needs a ROCm GPU (torch.cuda.is_available() is False)")
@@ -60,9 +60,14 @@ class BallbotVecEnv:
         p, self.reward_obj, self._host_reward = params_from_configs(self.reward_config, env_config, max_ep_steps,
                                                                     precision, seed)
         self.max_ep_steps = int(p.max_ep_steps)
-        hfields, self.terrain_seeds, size_z = terrain_bank(self.terrain_config, n_terrains, seed)
-        bank = [(h, size_z) for h in hfields]
-        p.n_terrains = len(bank)
+        plan = gpu_perlin_plan(self.terrain_config, n_terrains, seed)
+        if plan is None:
+            hfields, self.terrain_seeds, size_z = terrain_bank(self.terrain_config, n_terrains, seed)
+            bank = [(h, size_z) for h in hfields]
+        else:  # perlin: generated on the GPU below
+            self.terrain_seeds, pcfg, size_z = plan
+            bank = []
+        p.n_terrains = len(bank) or len(self.terrain_seeds)
         self.precision = "fp64" if p.fp64 else "fp32"
         self._params = p
         L = N.lib()
@@ -72,14 +77,23 @@ class BallbotVecEnv:
         for i, (data, size_z) in enumerate(bank):
             arr = np.ascontiguousarray(data, dtype=np.float32)
             N.check(L.bb_set_hfield(h, i, arr.ctypes.data_as(C.POINTER(C.c_float)), float(size_z)), "bb_set_hfield")
-        self.n_terrains = len(bank)
+        if plan is not None:
+            sd = np.ascontiguousarray(self.terrain_seeds, dtype=np.int32)
+            N.check(L.bb_generate_perlin(h, 0, len(sd), sd.ctypes.data_as(C.POINTER(C.c_int32)), C.byref(pcfg),
+                                         float(size_z)), "bb_generate_perlin")
+        self.n_terrains = p.n_terrains
         n, dev = self.num_envs, self.device
         self.obs = torch.zeros(n, N.NOBS, dtype=torch.float32, device=dev)
         self.terminal_obs = torch.zeros(n, N.NOBS, dtype=torch.float32, device=dev)
         self.reward = torch.zeros(n, dtype=torch.float32, device=dev)
         self.done = torch.zeros(n, dtype=torch.uint8, device=dev)
         self.pos2d = torch.zeros(n, 2, dtype=torch.float32, device=dev)
-        if self.n_terrains > 1:
+        if plan is not None and self.n_terrains == TERRAIN_SEED_HIGH:
+            # whole seed space resident (slot == seed): the first reset draws the
+            # reference's seed stream, integers(0, 10000) (ballbot_env.py:505-510)
+            ids = torch.from_numpy(np_random(seed).integers(0, TERRAIN_SEED_HIGH, size=n).astype(np.int32)).to(dev)
+            N.check(L.bb_assign_terrain(h, _ptr(ids), self._stream()), "bb_assign_terrain")
+        elif self.n_terrains > 1:
             g = torch.Generator(device="cpu").manual_seed(int(seed))
             ids = torch.randint(0, self.n_terrains, (n,), generator=g, dtype=torch.int32).to(dev)
             N.check(L.bb_assign_terrain(h, _ptr(ids), self._stream()), "bb_assign_terrain")
@@ -171,6 +185,13 @@ class BallbotVecEnv:
         N.check(N.lib().bb_get_stats(self._h, out), "bb_get_stats")
         return {"resets": out[0], "diverged": out[1], "overflow": out[2], "slow_path": out[3],
                 "solver_iters": out[4] + (out[5] << 32)}
+
+    def hfield(self, terrain_id: int) -> np.ndarray:
+        """Terrain bank slot `terrain_id` as float32[293*293] (host copy)."""
+        out = np.empty(N.HF_N * N.HF_N, np.float32)
+        N.check(N.lib().bb_get_hfield(self._h, int(terrain_id), out.ctypes.data_as(C.POINTER(C.c_float))),
+                "bb_get_hfield")
+        return out
 
     def time_kernel(self, max_launches: int) -> None:
         """Time the next `max_launches` fast step kernels with HIP events (bench.py)."""

@@ -8,7 +8,12 @@ reference, so this module restates its published algorithm:
 
 * tiled 2-D noise is 4-D simplex noise on a torus: each tiled axis u with
   period R maps to (sin(2 pi u/R), cos(2 pi u/R)) * R / (2 pi), the cosine
-  part added to the 'base' coordinate (z for x, w for y);
+  part added to the 'base' coordinate (z for x, w for y).  The library takes
+  sine and cosine from its polynomial fast_sin/fast_cos (_noise.h: input
+  u2 = u*2/R in [0, 2] <-> [0, 2 pi]; wrap by the 1.5*2^24 round trick;
+  y = u2 - u2|u2|; y*(3.1 + 3.6|y|); cos(u2) = sin(u2 + 0.5)), so this
+  restatement does too -- the approximation error (~1e-3) moves points by
+  O(0.1) noise units, well above float rounding;
 * fBm: total = sum_o noise(p * lacunarity^o) * persistence^o / sum_o persistence^o;
 * simplex corners by coordinate ranking (Gustavson), Perlin's permutation,
   the 32 4-D gradients, radius 0.6, scale 27 (4-D) / 32 (3-D);
@@ -130,6 +135,15 @@ def noise4(x, y, z, w):
     return total * f32(27.0)
 
 
+def fast_sin(u2):
+    """noise/_noise.h fast_sin on float32: sin(pi * u2) by a wrapped parabola."""
+    x = np.asarray(u2, np.float32)
+    z = x + f32(25165824.0)
+    x = x - (z - f32(25165824.0))
+    y = x - x * np.abs(x)
+    return y * (f32(3.1) + f32(3.6) * np.abs(y))
+
+
 def snoise2_grid(xs, ys, octaves=1, persistence=0.5, lacunarity=2.0, base=0.0, repeat=1024.0):
     """snoise2 over the grid xs[i] x ys[j] ('ij'), float32; repeat=None -> untiled (3-D, z = base)."""
     X, Y = np.meshgrid(np.asarray(xs, np.float32), np.asarray(ys, np.float32), indexing="ij")
@@ -143,12 +157,12 @@ def snoise2_grid(xs, ys, octaves=1, persistence=0.5, lacunarity=2.0, base=0.0, r
             freq = freq * lac
             amp = amp * pers
         return (total / mx).astype(np.float32)
-    R = float(repeat)
-    r = f32(R / (2.0 * np.pi))
-    ang_x = (X.astype(np.float64) * 2.0 * np.pi / R).astype(np.float32)
-    ang_y = (Y.astype(np.float64) * 2.0 * np.pi / R).astype(np.float32)
-    x4, z4 = np.sin(ang_x) * r, f32(base) + np.cos(ang_x) * r
-    y4, w4 = np.sin(ang_y) * r, f32(base) + np.cos(ang_y) * r
+    R = float(np.float32(repeat))
+    r = f32(R * (1.0 / np.pi) * 0.5)                      # repeat * M_1_PI * 0.5
+    u_x = (X.astype(np.float64) * 2.0 / R).astype(np.float32)  # x * 2.0 / repeatx
+    u_y = (Y.astype(np.float64) * 2.0 / R).astype(np.float32)
+    x4, z4 = fast_sin(u_x) * r, f32(base) + fast_sin(u_x + f32(0.5)) * r
+    y4, w4 = fast_sin(u_y) * r, f32(base) + fast_sin(u_y + f32(0.5)) * r
     total = noise4(x4, y4, z4, w4)
     amp, freq, mx = f32(1.0), f32(1.0), f32(1.0)
     for _ in range(1, int(octaves)):

@@ -21,6 +21,7 @@
 #include "../../include/ballbot_mi355x.h"
 #include "bb_model.h"
 #include "bb_step.h"
+#include "bb_terrain.h"
 
 using namespace bb;
 
@@ -580,6 +581,42 @@ int bb_set_hfield(bb_handle* h, int terrain_id, const float* data, float size_z)
   HIPCHK(hipMemcpy(h->hmax + terrain_id, &hm, sizeof(float), hipMemcpyHostToDevice));
   HIPCHK(hipMemcpy(h->size_z + terrain_id, &size_z, sizeof(float), hipMemcpyHostToDevice));
   HIPCHK(hipMemcpy(h->offset + terrain_id, &off, sizeof(float), hipMemcpyHostToDevice));
+  return 0;
+}
+
+int bb_generate_perlin(bb_handle* h, int first, int count, const int32_t* seeds, const bb_perlin_cfg* cfg,
+                       float size_z) {
+  static_assert(HF_N == HF_N_, "terrain generator and physics disagree on the hfield size");
+  if (!h || !seeds || !cfg) return fail("bb_generate_perlin: NULL argument");
+  if (count < 0 || first < 0 || first + count > h->p.n_terrains)
+    return fail("bb_generate_perlin: slots [%d,%d) out of range [0,%d)", first, first + count, h->p.n_terrains);
+  if (!(cfg->scale > 0) || cfg->octaves < 1) return fail("bb_generate_perlin: need scale > 0 and octaves >= 1");
+  if (!(size_z > 0)) return fail("bb_generate_perlin: size_z must be > 0");
+  if (count == 0) return 0;
+  HIPCHK(hipSetDevice(h->device));
+  int32_t* ds = nullptr;
+  HIPCHK(hipMalloc(&ds, sizeof(int32_t) * count));
+  HIPCHK(hipMemcpy(ds, seeds, sizeof(int32_t) * count, hipMemcpyHostToDevice));
+  PerlinCfg pc{cfg->scale, cfg->octaves, cfg->persistence, cfg->lacunarity, cfg->amplitude};
+  std::vector<float> sz(count, size_z);
+  HIPCHK(hipMemcpy(h->size_z + first, sz.data(), sizeof(float) * count, hipMemcpyHostToDevice));
+  int rc = launch_perlin_bank(h->bank + size_t(first) * HF_N * HF_N, ds, count, pc, size_z, h->offset + first,
+                              h->hmax + first, 0);
+  HIPCHK(hipDeviceSynchronize());
+  (void)hipFree(ds);
+  if (rc) return fail("bb_generate_perlin: launch failed");
+  HIPCHK(hipMemcpy(h->h_offset.data() + first, h->offset + first, sizeof(float) * count, hipMemcpyDeviceToHost));
+  return 0;
+}
+
+int bb_get_hfield(bb_handle* h, int terrain_id, float* out) {
+  if (!h || !out) return fail("bb_get_hfield: NULL argument");
+  if (terrain_id < 0 || terrain_id >= h->p.n_terrains)
+    return fail("bb_get_hfield: terrain_id %d out of range [0,%d)", terrain_id, h->p.n_terrains);
+  HIPCHK(hipSetDevice(h->device));
+  HIPCHK(hipDeviceSynchronize());
+  HIPCHK(hipMemcpy(out, h->bank + size_t(terrain_id) * HF_N * HF_N, sizeof(float) * HF_N * HF_N,
+                   hipMemcpyDeviceToHost));
   return 0;
 }
 

@@ -82,3 +82,31 @@ def test_obs_layout_is_sorted_keys():
     d = split_obs(np.arange(15.0))
     assert list(d) == list(OBS_KEYS)
     np.testing.assert_array_equal(d["orientation"], [9, 10, 11])
+
+
+def test_fast_sin_restated():
+    """noise/_noise.h fast_sin: sin(pi u) to ~1e-3, exact at the quarter points, periodic."""
+    from ballbot_gym.terrain.perlin import fast_sin
+
+    u = np.linspace(-2, 2, 4001, dtype=np.float32)
+    err = np.abs(fast_sin(u) - np.sin(np.pi * u.astype(np.float64)))
+    assert err.max() < 1.2e-3
+    assert fast_sin(np.float32(0.5)) == 1.0 and fast_sin(np.float32(0.0)) == 0.0
+    assert np.array_equal(fast_sin(u[:1000] + np.float32(2.0)), fast_sin(u[:1000]))
+
+
+def test_gpu_perlin_plan():
+    from ballbot_gym.envs.config import gpu_perlin_plan
+
+    assert gpu_perlin_plan({"type": "hills", "config": {}}, None, 0) is None
+    assert gpu_perlin_plan({"type": "perlin", "config": {"seed": 5}}, None, 0) is None  # fixed seed: host path
+    seeds, pc, sz = gpu_perlin_plan({"type": "perlin", "config": {"seed": None}}, None, 0)
+    assert seeds == list(range(10000)) and sz == 2.0
+    assert (pc.scale, pc.octaves, pc.lacunarity, pc.amplitude) == (25.0, 4, 2.0, 1.0)
+    assert abs(pc.persistence - 0.2) < 1e-7
+    seeds, pc, _ = gpu_perlin_plan({"type": "perlin", "config": {"octaves": 5}}, 4, 10)
+    assert seeds == [7765, 9560, 2640, 2076] and pc.octaves == 5
+    with pytest.raises(ValueError, match="unknown config keys"):
+        gpu_perlin_plan({"type": "perlin", "config": {"octave": 3}}, 4, 0)
+    with pytest.raises(ValueError):
+        gpu_perlin_plan({"type": "perlin", "config": {}}, 0, 0)
