@@ -12,6 +12,7 @@
  *   bb_reset         mj_resetData + height offset + mj_forward  ballbot_env.py:612-620
  *   bb_step          ctrl = -clip(10a); mj_step; _get_obs;      ballbot_env.py:903-1036
  *                    reward plugin; termination
+ *   bb_gae           SB3 RolloutBuffer.compute_returns_and_advantage (PPO)
  *   bb_forward       mujoco.mj_forward (diagnostic)             ballbot_env.py:525,620
  *   bb_get_state/    read/write qpos/qvel/qacc_warmstart        ballbot_env.py:616-617
  *   bb_set_state     (MjData.qpos / qvel)
@@ -38,7 +39,7 @@
 extern "C" {
 #endif
 
-#define BB_ABI_VERSION 4
+#define BB_ABI_VERSION 5
 #define BB_NQ 17
 #define BB_NV 15
 #define BB_OBS 15
@@ -100,6 +101,15 @@ typedef struct {
  * the hfield_data write at reset (terrain/perlin.py:8-74, ballbot_env.py:501-513). */
 int bb_generate_perlin(bb_handle* h, int first_terrain_id, int count, const int32_t* seeds_host,
                        const bb_perlin_cfg* cfg, float size_z);
+/* PPO update boundary: GAE(gamma, lambda) advantages and returns of a device
+ * rollout laid out [T][n_envs] (float32 rewards/values, uint8 episode starts;
+ * last_values/last_dones [n_envs] for the bootstrap).  Replaces stable-
+ * baselines3 RolloutBuffer.compute_returns_and_advantage as called by PPO
+ * (ballbot_rl/training/train.py:125-142, model.learn at :284).  Enqueued on
+ * stream; needs no handle. */
+int bb_gae(const float* rewards_dev, const float* values_dev, const uint8_t* episode_starts_dev,
+           const float* last_values_dev, const uint8_t* last_dones_dev, int T, int n_envs, double gamma,
+           double gae_lambda, float* advantages_dev, float* returns_dev, void* stream);
 /* copy terrain bank slot terrain_id (float32[293*293]) to host memory */
 int bb_get_hfield(bb_handle* h, int terrain_id, float* data_host);
 /* per-env terrain ids (device int32[n]) applied at the next reset */

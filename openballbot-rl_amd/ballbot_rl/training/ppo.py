@@ -1,0 +1,324 @@
+"""Batched PPO on the GPU env.
+
+Restates stable-baselines3 2.6.0 PPO as the reference configures it
+(ballbot_rl/training/train.py:38-142, 284; configs/train/ppo_directional.yaml):
+
+collect_rollouts (SB3 OnPolicyAlgorithm.collect_rollouts)
+  n_steps env.steps of every env; actions are sampled from the Gaussian policy,
+  CLIPPED to the action space [-1, 1] for env.step and stored UNCLIPPED;
+  episode_starts[t] = done of the previous step; the reference env never
+  truncates (ballbot_env.py:1030), so no time-limit bootstrap.
+compute_returns_and_advantage -> bb_gae (HIP kernel, csrc/bb_rollout.hip).
+train (SB3 PPO.train)
+  n_epochs passes over random minibatches of batch_size; ratio = exp(logp -
+  old_logp); clipped surrogate; value loss = MSE(returns, values) (no value
+  clipping); entropy loss = -mean(entropy); loss = pg + ent_coef*ent +
+  vf_coef*vf; approx_kl = mean(exp(r) - 1 - r) with r the log ratio, and the
+  update STOPS (before the step) once approx_kl > 1.5 * target_kl; gradients
+  clipped to max_grad_norm (0.5) by global norm; AdamW(weight_decay) with the
+  learning rate from the schedule at progress_remaining = 1 - t/T.
+Logs: SB3's keys and order (training/logger.py), rollout stats over the last 100
+episodes (Monitor + ep_info_buffer).
+
+Everything stays on the GPU: rollout buffers [T][N] in HBM, one host sync per
+rollout for episode statistics and one per minibatch for the KL early stop
+(SB3's semantics need it).  Multi-GPU: each rank
+steps its own env shard; at the update boundary the rollout buffers are
+gathered to rank 0 over RCCL (gather_rollouts), rank 0 runs the update and
+broadcasts the new parameters.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import time
+from collections import deque
+from typing import Any, Callable, Dict, Optional, Union
+
+import numpy as np
+import torch
+import torch.distributed as dist
+from torch import nn
+
+from ballbot_rl.policies.mlp_policy import ActorCriticPolicy, obs_spaces
+from ballbot_rl.training.logger import CSVLogger
+
+Schedule = Union[float, Callable[[float], float]]
+
+
+def _ptr(t: torch.Tensor):
+    return C.c_void_p(t.data_ptr())
+
+
+def gae_hip(rewards, values, episode_starts, last_values, last_dones, gamma: float, gae_lambda: float):
+    """GAE on device tensors [T][N] through the C-ABI (bb_gae); raises off-GPU."""
+    from ballbot_gym import _native as N
+
+    if not rewards.is_cuda:
+        raise RuntimeError("bb_gae runs on the GPU; rollout tensors must live on a ROCm device")
+    T, n = rewards.shape
+    ts = [rewards, values, episode_starts, last_values, last_dones]
+    want = [(torch.float32, (T, n)), (torch.float32, (T, n)), (torch.uint8, (T, n)), (torch.float32, (n,)),
+            (torch.uint8, (n,))]
+    for t, (dt, sh) in zip(ts, want):
+        if t.dtype != dt or tuple(t.shape) != sh or not t.is_contiguous():
+            raise ValueError(f"bb_gae: expected contiguous {dt} {sh}, got {t.dtype} {tuple(t.shape)}")
+    adv = torch.empty_like(rewards)
+    ret = torch.empty_like(rewards)
+    stream = C.c_void_p(torch.cuda.current_stream(rewards.device).cuda_stream)
+    N.check(N.lib().bb_gae(*[_ptr(t) for t in ts], int(T), int(n), float(gamma), float(gae_lambda), _ptr(adv),
+                           _ptr(ret), stream), "bb_gae")
+    return adv, ret
+
+
+def explained_variance(y_pred: torch.Tensor, y_true: torch.Tensor) -> float:
+    """SB3 common.utils.explained_variance: 1 - Var[y - y_pred] / Var[y] (nan if Var[y] == 0)."""
+    var_y = torch.var(y_true, unbiased=False)
+    if float(var_y) == 0:
+        return float("nan")
+    return float(1.0 - torch.var(y_true - y_pred, unbiased=False) / var_y)
+
+
+class RolloutBuffer:
+    """[T][N] device buffers of one rollout (SB3 RolloutBuffer, device-resident)."""
+
+    def __init__(self, T: int, n: int, obs_dim: int, act_dim: int, device):
+        f32 = dict(dtype=torch.float32, device=device)
+        self.T, self.n = T, n
+        self.obs = torch.zeros(T, n, obs_dim, **f32)
+        self.actions = torch.zeros(T, n, act_dim, **f32)
+        self.rewards = torch.zeros(T, n, **f32)
+        self.values = torch.zeros(T, n, **f32)
+        self.log_probs = torch.zeros(T, n, **f32)
+        self.starts = torch.zeros(T, n, dtype=torch.uint8, device=device)
+        self.advantages = None
+        self.returns = None
+
+    def flat(self) -> Dict[str, torch.Tensor]:
+        """Flattened [T*N] views (the sample order does not matter: minibatches are random)."""
+        T, n = self.T, self.n
+        return {"obs": self.obs.reshape(T * n, -1), "actions": self.actions.reshape(T * n, -1),
+                "values": self.values.reshape(-1), "log_probs": self.log_probs.reshape(-1),
+                "advantages": self.advantages.reshape(-1), "returns": self.returns.reshape(-1)}
+
+
+class BatchedPPO:
+    """PPO with SB3's arguments and defaults, over a batched GPU env.
+
+    env: BallbotVecEnv-like object with num_envs, device, reset() -> (obs, info)
+    and step(actions) -> (obs, reward, terminated, truncated, info), obs a
+    packed [N, 15] tensor.  Rollout length per env is n_steps, so one rollout
+    holds num_envs * n_steps samples."""
+
+    def __init__(self, env, learning_rate: Schedule = 3e-4, n_steps: int = 2048, batch_size: int = 64,
+                 n_epochs: int = 10, gamma: float = 0.99, gae_lambda: float = 0.95, clip_range: Schedule = 0.2,
+                 normalize_advantage: bool = True, ent_coef: float = 0.0, vf_coef: float = 0.5,
+                 max_grad_norm: float = 0.5, target_kl: Optional[float] = None, weight_decay: float = 0.01,
+                 net_arch: Optional[Dict[str, Any]] = None, activation_fn=nn.LeakyReLU, seed: int = 0,
+                 logger: Optional[CSVLogger] = None, stats_window_size: int = 100,
+                 gae_fn: Callable = gae_hip, policy: Optional[ActorCriticPolicy] = None):
+        self.env = env
+        self.device = torch.device(env.device)
+        self.n_envs = int(env.num_envs)
+        self.n_steps, self.batch_size, self.n_epochs = int(n_steps), int(batch_size), int(n_epochs)
+        self.gamma, self.gae_lambda = float(gamma), float(gae_lambda)
+        self.lr_schedule = learning_rate if callable(learning_rate) else (lambda _p, v=float(learning_rate): v)
+        self.clip_schedule = clip_range if callable(clip_range) else (lambda _p, v=float(clip_range): v)
+        self.normalize_advantage = bool(normalize_advantage)
+        self.ent_coef, self.vf_coef, self.max_grad_norm = float(ent_coef), float(vf_coef), float(max_grad_norm)
+        self.target_kl = None if target_kl is None else float(target_kl)
+        self.gae_fn = gae_fn
+        self.rank = dist.get_rank() if dist.is_available() and dist.is_initialized() else 0
+        self.world = dist.get_world_size() if dist.is_available() and dist.is_initialized() else 1
+        torch.manual_seed(int(seed))
+        self.policy = (policy or ActorCriticPolicy(obs_spaces(), 3, net_arch, activation_fn)).to(self.device)
+        self._sync_params()
+        self.optimizer = torch.optim.AdamW(self.policy.parameters(), lr=self.lr_schedule(1.0),
+                                           weight_decay=float(weight_decay))
+        self.gen = torch.Generator(device=self.device)
+        self.gen.manual_seed(int(seed) * 1000003 + self.rank)
+        self.shuffle_gen = torch.Generator(device=self.device)
+        self.shuffle_gen.manual_seed(int(seed) + 7)
+        self.logger = logger or CSVLogger(None, stdout=False)
+        self.buf = RolloutBuffer(self.n_steps, self.n_envs, 15, 3, self.device)
+        self.num_timesteps = 0
+        self._n_updates = 0
+        self.ep_info_buffer: deque = deque(maxlen=int(stats_window_size))
+        self._last_obs = None
+        self._last_starts = torch.ones(self.n_envs, dtype=torch.uint8, device=self.device)
+        self._ep_ret = torch.zeros(self.n_envs, dtype=torch.float64, device=self.device)
+        self._ep_len = torch.zeros(self.n_envs, dtype=torch.int64, device=self.device)
+        self.progress_remaining = 1.0
+
+    # ------------------------------------------------------------ distributed
+    def _sync_params(self) -> None:
+        if self.world == 1:
+            return
+        vec = nn.utils.parameters_to_vector(self.policy.parameters()).detach().contiguous()
+        dist.broadcast(vec, src=0)
+        nn.utils.vector_to_parameters(vec, self.policy.parameters())
+
+    # ---------------------------------------------------------------- rollout
+    @torch.no_grad()
+    def collect_rollouts(self) -> None:
+        env, b = self.env, self.buf
+        if self._last_obs is None:
+            self._last_obs, _ = env.reset()
+        ep_r, ep_l = [], []
+        for t in range(self.n_steps):
+            b.obs[t].copy_(self._last_obs)        # env.obs is reused by the next step
+            b.starts[t].copy_(self._last_starts)
+            actions, values, logp = self.policy(b.obs[t], generator=self.gen)
+            b.actions[t].copy_(actions)
+            b.values[t].copy_(values)
+            b.log_probs[t].copy_(logp)
+            obs, reward, term, trunc, info = env.step(actions.clamp(-1.0, 1.0))
+            flags = info.get("done_flags") if isinstance(info, dict) else None
+            done = (term | trunc) if flags is None else ((flags & 5) != 0) | trunc
+            b.rewards[t].copy_(reward)
+            self._ep_ret += reward.double()
+            self._ep_len += 1
+            ep_r.append(torch.where(done, self._ep_ret, torch.full_like(self._ep_ret, float("nan"))))
+            ep_l.append(torch.where(done, self._ep_len, torch.zeros_like(self._ep_len)))
+            self._ep_ret.masked_fill_(done, 0.0)
+            self._ep_len.masked_fill_(done, 0)
+            self._last_obs = obs
+            self._last_starts = done.to(torch.uint8)
+        self.num_timesteps += self.n_envs * self.n_steps * self.world
+        last_v = self.policy.predict_values(self._last_obs)
+        b.advantages, b.returns = self.gae_fn(b.rewards, b.values, b.starts, last_v.contiguous(),
+                                              self._last_starts.contiguous(), self.gamma, self.gae_lambda)
+        # finished episodes in time order (one host sync per rollout)
+        r = torch.stack(ep_r).cpu().numpy()
+        ln = torch.stack(ep_l).cpu().numpy()
+        mask = ~np.isnan(r)
+        finished = list(zip(r[mask].tolist(), ln[mask].tolist()))
+        if self.world > 1:
+            parts = [None] * self.world
+            dist.all_gather_object(parts, finished)
+            finished = [x for p in parts for x in p]
+        for rr, ll in finished:
+            self.ep_info_buffer.append({"r": rr, "l": ll})
+
+    # ----------------------------------------------------------------- update
+    def _gathered(self) -> Optional[Dict[str, torch.Tensor]]:
+        d = self.buf.flat()
+        if self.world == 1:
+            return d
+        from ballbot_gym.distributed import gather_rollouts
+
+        out = {}
+        for k, v in d.items():  # [T*n, ...] per rank -> concatenated on rank 0
+            g = gather_rollouts(v.unsqueeze(0))
+            out[k] = None if g is None else g.reshape(-1, *v.shape[1:])
+        return out if self.rank == 0 else None
+
+    def train(self) -> None:
+        data = self._gathered()
+        if data is not None:
+            self._update(data)
+        self._sync_params()
+
+    def _update(self, d: Dict[str, torch.Tensor]) -> None:
+        self.policy.train()
+        lr = self.lr_schedule(self.progress_remaining)
+        for g in self.optimizer.param_groups:
+            g["lr"] = lr
+        clip = self.clip_schedule(self.progress_remaining)
+        n = d["obs"].shape[0]
+        ent_l, pg_l, vf_l, clip_f = [], [], [], []
+        cont = True
+        loss = torch.zeros((), device=self.device)
+        approx_kl = 0.0
+        for _epoch in range(self.n_epochs):
+            kls = []
+            perm = torch.randperm(n, generator=self.shuffle_gen, device=self.device)
+            for s in range(0, n, self.batch_size):
+                idx = perm[s:s + self.batch_size]
+                obs, act = d["obs"][idx], d["actions"][idx]
+                values, logp, entropy = self.policy.evaluate_actions(obs, act)
+                adv = d["advantages"][idx]
+                if self.normalize_advantage and len(adv) > 1:
+                    adv = (adv - adv.mean()) / (adv.std() + 1e-8)
+                log_ratio = logp - d["log_probs"][idx]
+                ratio = torch.exp(log_ratio)
+                pg = -torch.min(adv * ratio, adv * torch.clamp(ratio, 1 - clip, 1 + clip)).mean()
+                vf = nn.functional.mse_loss(d["returns"][idx], values)
+                ent = -torch.mean(entropy)
+                loss = pg + self.ent_coef * ent + self.vf_coef * vf
+                with torch.no_grad():
+                    kl = torch.mean((ratio - 1) - log_ratio)
+                    pg_l.append(pg.detach()); vf_l.append(vf.detach()); ent_l.append(ent.detach())
+                    clip_f.append(torch.mean((torch.abs(ratio - 1) > clip).float()))
+                approx_kl = float(kl)  # the early stop needs it before the step (host sync)
+                kls.append(approx_kl)
+                if self.target_kl is not None and approx_kl > 1.5 * self.target_kl:
+                    cont = False
+                    break
+                self.optimizer.zero_grad(set_to_none=True)
+                loss.backward()
+                nn.utils.clip_grad_norm_(self.policy.parameters(), self.max_grad_norm)
+                self.optimizer.step()
+            self._n_updates += 1
+            if not cont:
+                break
+        L = self.logger
+        mean = lambda xs: float(torch.stack(xs).mean()) if xs else float("nan")  # noqa: E731
+        L.record("train/entropy_loss", mean(ent_l))
+        L.record("train/policy_gradient_loss", mean(pg_l))
+        L.record("train/value_loss", mean(vf_l))
+        L.record("train/approx_kl", float(np.mean(kls)) if kls else float("nan"))
+        L.record("train/clip_fraction", mean(clip_f))
+        L.record("train/loss", float(loss))
+        L.record("train/explained_variance", explained_variance(d["values"], d["returns"]))
+        L.record("train/std", float(torch.exp(self.policy.log_std).mean()))
+        L.record("train/n_updates", self._n_updates)
+        L.record("train/clip_range", clip)
+        L.record("train/learning_rate", lr)
+
+    # ------------------------------------------------------------------ learn
+    def learn(self, total_timesteps: int, callback: Optional[Callable[["BatchedPPO"], bool]] = None,
+              log_interval: int = 1) -> "BatchedPPO":
+        """SB3 OnPolicyAlgorithm.learn: rollout -> (logs) -> update until total_timesteps."""
+        total = int(total_timesteps)
+        t0 = time.perf_counter()
+        start_steps = self.num_timesteps
+        iteration = 0
+        while self.num_timesteps < total:
+            self.collect_rollouts()
+            iteration += 1
+            self.progress_remaining = 1.0 - float(self.num_timesteps) / float(total)
+            if log_interval and iteration % log_interval == 0 and self.rank == 0:
+                el = max(time.perf_counter() - t0, 1e-9)
+                L = self.logger
+                L.record("time/iterations", iteration)
+                if self.ep_info_buffer:
+                    L.record("rollout/ep_rew_mean", float(np.mean([e["r"] for e in self.ep_info_buffer])))
+                    L.record("rollout/ep_len_mean", float(np.mean([e["l"] for e in self.ep_info_buffer])))
+                L.record("time/fps", int((self.num_timesteps - start_steps) / el))
+                L.record("time/time_elapsed", int(el))
+                L.record("time/total_timesteps", self.num_timesteps)
+                L.dump(step=self.num_timesteps)
+            self.train()
+            if callback is not None and callback(self) is False:
+                break
+        return self
+
+    # ------------------------------------------------------------- save/load
+    def save(self, path: str) -> None:
+        """Policy weights as safetensors (no pickle) + hyperparameters as JSON."""
+        import json
+
+        from safetensors.torch import save_file
+
+        save_file({k: v.detach().contiguous().cpu() for k, v in self.policy.state_dict().items()}, path)
+        meta = {"num_timesteps": self.num_timesteps, "n_updates": self._n_updates, "gamma": self.gamma,
+                "gae_lambda": self.gae_lambda, "n_steps": self.n_steps, "batch_size": self.batch_size,
+                "n_epochs": self.n_epochs}
+        with open(str(path) + ".json", "w") as f:
+            json.dump(meta, f)
+
+    def load_policy(self, path: str) -> None:
+        from safetensors.torch import load_file
+
+        self.policy.load_state_dict(load_file(path, device=str(self.device)))
+        self._sync_params()

@@ -1,0 +1,157 @@
+"""Train a policy from the reference's YAML configs (ballbot_rl/training/train.py:38-284).
+
+    python -m ballbot_rl.training.train --config configs/train/ppo_directional.yaml
+    torchrun --nproc-per-node 8 ... -m ballbot_rl.training.train --config ...   (one rank per GPU)
+
+Same config keys as the reference (algo.*, hidden_sz, num_envs, total_timesteps,
+seed, evaluation.*, env.*, problem.terrain/reward).  Differences, by design:
+* `num_envs` envs run in ONE BallbotVecEnv per GPU (split over ranks) instead of
+  a SubprocVecEnv of CPU MuJoCo processes; GPU-sized runs raise num_envs into the
+  thousands and lower n_steps (configs in tools/ppo_gpu.yaml);
+* the interactive overwrite/updates-per-rollout confirmations (train.py:194-266)
+  become printed warnings -- a batch job cannot answer them;
+* checkpoints are safetensors (no pickled SB3 zip); cameras/frozen encoders
+   are not part of this trainer yet.
+Output directory layout as the reference: outputs/experiments/runs/
+{timestamp}_{algo}_{terrain}_{reward}_seed{seed}/ with config.yaml, info.txt,
+progress.csv (SB3 columns), best_model.safetensors and final_model.safetensors.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import random
+from datetime import datetime
+from pathlib import Path
+from typing import Any, Dict, Optional
+
+import numpy as np
+import torch
+import torch.distributed as dist
+import yaml
+
+from ballbot_gym.core.config import get_component_config, load_training_config
+from ballbot_rl.training.logger import CSVLogger
+from ballbot_rl.training.ppo import BatchedPPO
+from ballbot_rl.training.schedules import lr_schedule
+
+
+def ppo_kwargs(config: Dict[str, Any]) -> Dict[str, Any]:
+    """The PPO(...) arguments the reference passes (train.py:125-142, 39-56)."""
+    a = config["algo"]
+    lr = float(a["learning_rate"])
+    h = int(config.get("hidden_sz", 128))
+    return dict(ent_coef=float(a["ent_coef"]), clip_range=float(a["clip_range"]),
+                target_kl=float(a["target_kl"]) if a.get("target_kl") is not None else None,
+                vf_coef=float(a["vf_coef"]), learning_rate=lr if lr != -1 else lr_schedule,
+                n_steps=int(a["n_steps"]), batch_size=int(a["batch_sz"]), n_epochs=int(a["n_epochs"]),
+                normalize_advantage=bool(a["normalize_advantage"]), weight_decay=float(a["weight_decay"]),
+                net_arch={"pi": [h] * 4, "vf": [h] * 4})
+
+
+def experiment_dir(config: Dict[str, Any], out: Optional[str] = None) -> Path:
+    ts = datetime.now().strftime("%Y%m%d_%H%M%S")
+    terrain = config.get("problem", {}).get("terrain", {}).get("type", "unknown")
+    reward = config.get("problem", {}).get("reward", {}).get("type", "unknown")
+    name = f"{ts}_{config['algo']['name']}_{terrain}_{reward}_seed{config.get('seed', 'unknown')}"
+    if out and out.strip():
+        p = Path(out).resolve()
+        return p / name if (p.is_dir() or not p.suffix) else p
+    return Path("outputs/experiments/runs") / name
+
+
+def make_env(config: Dict[str, Any], num_envs: int, device, seed: int, precision: str = "fp64"):
+    from ballbot_gym.envs import BallbotVecEnv
+
+    env_cfg = {"camera": config.get("camera", {}), "env": config.get("env", {}), "logging": config.get("logging", {})}
+    return BallbotVecEnv(num_envs, device=device, reward_config=get_component_config(config, "reward"),
+                         terrain_config=get_component_config(config, "terrain"), env_config=env_cfg, seed=seed,
+                         precision=precision, n_terrains=config.get("n_terrains"))
+
+
+def main(config: Dict[str, Any], seed: int, out: Optional[str] = None, total_timesteps: Optional[int] = None,
+         precision: str = "fp64") -> BatchedPPO:
+    from ballbot_gym.distributed import env_shard, rank_seed
+    from ballbot_rl.evaluation import evaluate_policy
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1 and not dist.is_initialized():
+        os.environ.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    dev = torch.device("cuda", local)
+    n_total = int(config["num_envs"])
+    first, n_local = env_shard(n_total, rank, world)
+    env = make_env(config, n_local, dev, rank_seed(seed, first), precision)
+    eval_cfg = config.get("evaluation", {}) or {}
+    n_eval = int(eval_cfg.get("n_episodes", 8))
+    eval_env = make_env(config, max(n_eval, 1), dev, seed + n_total, precision) if rank == 0 else None
+
+    out_path = experiment_dir(config, out if out is not None else config.get("out"))
+    logger = None
+    if rank == 0:
+        if out_path.exists() and any(out_path.iterdir()):
+            print(f"warning: output directory {out_path} exists and is not empty; files will be overwritten")
+        out_path.mkdir(parents=True, exist_ok=True)
+        with (out_path / "config.yaml").open("w") as f:
+            yaml.safe_dump(config, f)
+        with (out_path / "info.txt").open("w") as f:
+            json.dump({"algo": config["algo"]["name"], "num_envs": n_total, "out": str(out_path),
+                       "resume": config.get("resume", ""), "seed": seed, "world_size": world}, f)
+        logger = CSVLogger(str(out_path) + "/", stdout=True)
+        upd = config["algo"]["n_epochs"] * n_total * config["algo"]["n_steps"] / config["algo"]["batch_sz"]
+        print(f"{upd:.1f} gradient updates per rollout (n_epochs x num_envs x n_steps / batch_sz)")
+
+    model = BatchedPPO(env, seed=seed, logger=logger, **ppo_kwargs(config))
+    if config.get("resume"):
+        model.load_policy(config["resume"])
+    eval_freq = int(eval_cfg.get("freq", 5000))
+    state = {"best": -np.inf, "next_eval": eval_freq}
+
+    def on_rollout(m: BatchedPPO) -> bool:
+        vec_steps = m.num_timesteps // n_total  # SB3 EvalCallback counts vec-env steps
+        if rank == 0 and eval_env is not None and vec_steps >= state["next_eval"]:
+            state["next_eval"] = (vec_steps // eval_freq + 1) * eval_freq
+            r = evaluate_policy(m.policy, eval_env, n_eval_episodes=n_eval, deterministic=True)
+            m.logger.record("eval/mean_reward", r["mean_reward"])
+            m.logger.record("eval/mean_ep_length", r["mean_ep_length"])
+            if r["mean_reward"] > state["best"]:
+                state["best"] = r["mean_reward"]
+                m.save(str(out_path / "best_model.safetensors"))
+        return True
+
+    total = int(float(total_timesteps if total_timesteps is not None else config["total_timesteps"]))
+    model.learn(total_timesteps=total, callback=on_rollout)
+    if rank == 0:
+        model.save(str(out_path / "final_model.safetensors"))
+    env.close()
+    if eval_env is not None:
+        eval_env.close()
+    model.out_path = out_path
+    return model
+
+
+def cli_main() -> None:
+    ap = argparse.ArgumentParser(description="Train a policy on the MI355X batched ballbot env.")
+    ap.add_argument("--config", required=True, help="training YAML (reference format)")
+    ap.add_argument("--total-timesteps", type=float, default=None)
+    ap.add_argument("--out", default=None)
+    ap.add_argument("--precision", default="fp64", choices=["fp32", "fp64"])
+    args = ap.parse_args()
+    cfg = load_training_config(str(Path(args.config).resolve()))
+    seed = int(cfg.get("seed", 0))
+    if seed != -1:
+        random.seed(seed)
+        np.random.seed(seed)
+        torch.manual_seed(seed)
+    main(cfg, seed, out=args.out, total_timesteps=None if args.total_timesteps is None else int(args.total_timesteps),
+         precision=args.precision)
+    if dist.is_initialized():
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    cli_main()

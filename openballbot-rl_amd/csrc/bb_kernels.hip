@@ -22,6 +22,7 @@
 #include "bb_model.h"
 #include "bb_step.h"
 #include "bb_terrain.h"
+#include "bb_rollout.h"
 
 using namespace bb;
 
@@ -606,6 +607,15 @@ int bb_generate_perlin(bb_handle* h, int first, int count, const int32_t* seeds,
   (void)hipFree(ds);
   if (rc) return fail("bb_generate_perlin: launch failed");
   HIPCHK(hipMemcpy(h->h_offset.data() + first, h->offset + first, sizeof(float) * count, hipMemcpyDeviceToHost));
+  return 0;
+}
+
+int bb_gae(const float* rew, const float* val, const uint8_t* start, const float* last_val, const uint8_t* last_done,
+           int T, int n, double gamma, double lam, float* adv, float* ret, void* stream) {
+  if (!rew || !val || !start || !last_val || !last_done || !adv || !ret) return fail("bb_gae: NULL argument");
+  if (T < 1 || n < 1) return fail("bb_gae: need T >= 1 and n_envs >= 1 (got %d, %d)", T, n);
+  if (launch_gae(rew, val, start, last_val, last_done, T, n, gamma, lam, adv, ret, (hipStream_t)stream))
+    return fail("bb_gae: launch failed: %s", hipGetErrorString(hipGetLastError()));
   return 0;
 }
 

@@ -56,3 +56,38 @@ def test_gloo_world2_gather_and_max():
     assert t == 2.0
     assert ids == [float(i) for i in range(10)]
     assert seed0 == 5
+
+
+def _ppo_worker(rank, world, port, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    from fake_env import FakeEnv
+    from test_ppo import _ppo
+
+    torch.manual_seed(100 + rank)  # different local init: the broadcast must align them
+    env = FakeEnv(8, seed=rank, ep_len=4)
+    m = _ppo(env, n_steps=4, batch_size=16, n_epochs=1)
+    m.learn(total_timesteps=2 * 8 * 4 * world)
+    vec = torch.nn.utils.parameters_to_vector(m.policy.parameters()).detach()
+    q.put((rank, m.num_timesteps, m._n_updates, vec.numpy(), len(m.ep_info_buffer)))
+    dist.destroy_process_group()
+
+
+def test_gloo_world2_ppo_update_boundary():
+    """Rollouts gathered to rank 0 (64 samples per update), one update there,
+    parameters broadcast: both ranks end with identical policies."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_ppo_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = sorted([q.get(timeout=180) for _ in range(2)], key=lambda x: x[0])
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    (_, t0, u0, v0, e0), (_, t1, u1, v1, e1) = res
+    assert t0 == t1 == 2 * 8 * 4 * 2        # timesteps count every rank's envs
+    assert u0 == 2 and u1 == 0             # SB3 counts epochs: 1 epoch x 2 iterations, on rank 0 only
+    assert (v0 == v1).all()
+    assert e0 == e1 > 0                    # episode stats gathered from both ranks
