@@ -268,7 +268,7 @@ class BatchedPPO:
         L.record("train/value_loss", mean(vf_l))
         L.record("train/approx_kl", float(np.mean(kls)) if kls else float("nan"))
         L.record("train/clip_fraction", mean(clip_f))
-        L.record("train/loss", float(loss))
+        L.record("train/loss", float(loss.detach()))
         L.record("train/explained_variance", explained_variance(d["values"], d["returns"]))
         L.record("train/std", float(torch.exp(self.policy.log_std).mean()))
         L.record("train/n_updates", self._n_updates)

@@ -40,7 +40,7 @@ def test_batched_ppo_on_gpu_env(tmp_path):
     from ballbot_rl.training.logger import CSVLogger, read_progress
     from ballbot_rl.training.ppo import BatchedPPO
 
-    env = BallbotVecEnv(1024, device="cuda:0", max_ep_steps=200, seed=3)
+    env = BallbotVecEnv(1024, device="cuda:0", max_ep_steps=10, seed=3)  # episodes end inside the run
     m = BatchedPPO(env, n_steps=16, batch_size=4096, n_epochs=2, ent_coef=0.001, clip_range=0.015, vf_coef=2.0,
                    target_kl=0.3, learning_rate=1e-4, normalize_advantage=False, seed=10,
                    logger=CSVLogger(str(tmp_path), stdout=False))

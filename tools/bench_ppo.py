@@ -1,0 +1,99 @@
+"""PPO training throughput and learning curve on the GPU env.
+
+    python tools/bench_ppo.py --envs 4096 --n-steps 64 --timesteps 10e6 --out gpurun_out/ppo_flat
+
+One JSON line: env-steps/s of whole PPO iterations (rollout + GAE + update),
+the rollout/update time split, and the final rollout statistics; the SB3-format
+progress.csv lands in --out (compare with the reference's archived
+outputs/experiments/archived_models/2025-12-04_ppo-flat-directional-seed10/progress.csv:
+ep_rew_mean ~8, ep_len_mean ~300 over 10M steps at ~200 env-steps/s).
+Hyperparameters are the reference's (configs/train/ppo_directional.yaml) except
+the rollout shape: num_envs x n_steps and batch_sz scaled for one GPU.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import sys
+import time
+from pathlib import Path
+
+ROOT = Path(__file__).resolve().parent.parent
+sys.path.insert(0, str(ROOT / "openballbot-rl_amd"))
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--envs", type=int, default=4096)
+    ap.add_argument("--n-steps", type=int, default=64)
+    ap.add_argument("--batch", type=int, default=8192)
+    ap.add_argument("--epochs", type=int, default=5)
+    ap.add_argument("--timesteps", type=float, default=4096 * 64 * 4)
+    ap.add_argument("--terrain", default="flat")
+    ap.add_argument("--precision", default="fp64")
+    ap.add_argument("--lr", type=float, default=-1, help="-1: the reference's lr_schedule")
+    ap.add_argument("--out", default=None)
+    ap.add_argument("--seed", type=int, default=10)
+    a = ap.parse_args()
+
+    import torch
+
+    from ballbot_gym.envs import BallbotVecEnv
+    from ballbot_rl.training.logger import CSVLogger
+    from ballbot_rl.training.ppo import BatchedPPO
+    from ballbot_rl.training.schedules import lr_schedule
+
+    env = BallbotVecEnv(a.envs, device="cuda:0", precision=a.precision, seed=a.seed,
+                        terrain_config={"type": a.terrain, "config": {}})
+    m = BatchedPPO(env, n_steps=a.n_steps, batch_size=a.batch, n_epochs=a.epochs, ent_coef=0.001, clip_range=0.015,
+                   vf_coef=2.0, target_kl=0.3, learning_rate=lr_schedule if a.lr == -1 else a.lr,
+                   normalize_advantage=False, weight_decay=0.01, seed=a.seed,
+                   logger=CSVLogger(a.out, stdout=False))
+    t_roll = t_upd = 0.0
+    orig_collect, orig_train = m.collect_rollouts, m.train
+
+    def collect():
+        nonlocal t_roll
+        torch.cuda.synchronize(); t = time.perf_counter()
+        orig_collect(); torch.cuda.synchronize(); t_roll += time.perf_counter() - t
+
+    def train():
+        nonlocal t_upd
+        torch.cuda.synchronize(); t = time.perf_counter()
+        orig_train(); torch.cuda.synchronize(); t_upd += time.perf_counter() - t
+
+    m.collect_rollouts, m.train = collect, train
+    iters = [0]
+
+    def cb(_m):
+        iters[0] += 1
+        if iters[0] % 10 == 0:
+            print(f"iter {iters[0]} t={_m.num_timesteps} ep_rew={_eprew(_m):.3f}", file=sys.stderr, flush=True)
+        return True
+
+    t0 = time.perf_counter()
+    m.learn(total_timesteps=int(a.timesteps), callback=cb)
+    torch.cuda.synchronize()
+    el = time.perf_counter() - t0
+    out = {"metric": "PPO env-steps/sec (rollout + GAE + update)", "value": m.num_timesteps / el,
+           "unit": "env-steps/s", "timesteps": m.num_timesteps, "iterations": iters[0], "wall_s": el,
+           "rollout_s": t_roll, "update_s": t_upd, "rollout_env_steps_per_s": m.num_timesteps / max(t_roll, 1e-9),
+           "config": {"envs": a.envs, "n_steps": a.n_steps, "batch_size": a.batch, "n_epochs": a.epochs,
+                      "terrain": a.terrain, "precision": a.precision},
+           "ep_rew_mean": _eprew(m), "ep_len_mean": _eplen(m), "env_stats": env.stats()}
+    print(json.dumps(out), flush=True)
+    env.close()
+
+
+def _eprew(m):
+    import numpy as np
+    return float(np.mean([e["r"] for e in m.ep_info_buffer])) if m.ep_info_buffer else float("nan")
+
+
+def _eplen(m):
+    import numpy as np
+    return float(np.mean([e["l"] for e in m.ep_info_buffer])) if m.ep_info_buffer else float("nan")
+
+
+if __name__ == "__main__":
+    main()
