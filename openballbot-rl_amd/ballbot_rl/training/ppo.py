@@ -101,6 +101,74 @@ class RolloutBuffer:
                 "advantages": self.advantages.reshape(-1), "returns": self.returns.reshape(-1)}
 
 
+class _UpdateGraphs:
+    """Two captured graphs for one full minibatch of PPO.train over static data buffers.
+
+    fwd_bwd: gather rows idx of the data, loss terms, zero + backward the grads;
+    opt_step: clip_grad_norm_ + AdamW.step (capturable).  Split so the KL early
+    stop is decided on the host between them, exactly as SB3 does."""
+
+    def __init__(self, ppo: "BatchedPPO", n: int):
+        dev, B = ppo.device, ppo.batch_size
+        self.n = n
+        self.data = {"obs": torch.zeros(n, 15, device=dev), "actions": torch.zeros(n, 3, device=dev),
+                     "log_probs": torch.zeros(n, device=dev), "advantages": torch.zeros(n, device=dev),
+                     "returns": torch.zeros(n, device=dev)}
+        self.idx = torch.zeros(B, dtype=torch.int64, device=dev)
+        self.clip = torch.zeros((), device=dev)
+        pol, opt = ppo.policy, ppo.optimizer
+        params = [p for p in pol.parameters() if p.requires_grad]
+        # snapshot: the warm-up step below must not change the policy or AdamW state
+        p_snap = [p.detach().clone() for p in params]
+        st_snap = {id(p): {k: v.clone() for k, v in opt.state[p].items()} for p in params if p in opt.state}
+
+        def fwd_bwd():
+            d = self.data
+            out = ppo._loss(d["obs"][self.idx], d["actions"][self.idx], d["log_probs"][self.idx],
+                            d["advantages"][self.idx], d["returns"][self.idx], self.clip)
+            for p in params:
+                if p.grad is not None:
+                    p.grad.zero_()
+            out[0].backward()
+            return out
+
+        def opt_step():
+            nn.utils.clip_grad_norm_(params, ppo.max_grad_norm)
+            opt.step()
+
+        self.idx.copy_(torch.arange(B, device=dev) % max(n, 1))
+        side = torch.cuda.Stream(device=dev)
+        side.wait_stream(torch.cuda.current_stream(dev))
+        with torch.cuda.stream(side):
+            for _ in range(2):
+                fwd_bwd()
+                opt_step()
+        torch.cuda.current_stream(dev).wait_stream(side)
+        for p in params:  # backward allocates the grads inside the graph pool (static addresses)
+            p.grad = None
+        self.fwd_bwd = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(self.fwd_bwd):
+            self.out = fwd_bwd()
+        self.opt_step = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(self.opt_step, pool=self.fwd_bwd.pool()):
+            opt_step()
+        torch.cuda.synchronize(dev)
+        with torch.no_grad():
+            for p, s in zip(params, p_snap):
+                p.copy_(s)
+            for p in params:
+                prev = st_snap.get(id(p))
+                for k, v in opt.state[p].items():
+                    if prev is not None and k in prev:
+                        v.copy_(prev[k])
+                    else:
+                        v.zero_()
+
+    def load(self, d: Dict[str, torch.Tensor]) -> None:
+        for k, v in self.data.items():
+            v.copy_(d[k])
+
+
 class BatchedPPO:
     """PPO with SB3's arguments and defaults, over a batched GPU env.
 
@@ -115,7 +183,8 @@ class BatchedPPO:
                  max_grad_norm: float = 0.5, target_kl: Optional[float] = None, weight_decay: float = 0.01,
                  net_arch: Optional[Dict[str, Any]] = None, activation_fn=nn.LeakyReLU, seed: int = 0,
                  logger: Optional[CSVLogger] = None, stats_window_size: int = 100,
-                 gae_fn: Callable = gae_hip, policy: Optional[ActorCriticPolicy] = None):
+                 gae_fn: Callable = gae_hip, policy: Optional[ActorCriticPolicy] = None,
+                 use_graphs: Optional[bool] = None):
         self.env = env
         self.device = torch.device(env.device)
         self.n_envs = int(env.num_envs)
@@ -132,8 +201,16 @@ class BatchedPPO:
         torch.manual_seed(int(seed))
         self.policy = (policy or ActorCriticPolicy(obs_spaces(), 3, net_arch, activation_fn)).to(self.device)
         self._sync_params()
-        self.optimizer = torch.optim.AdamW(self.policy.parameters(), lr=self.lr_schedule(1.0),
-                                           weight_decay=float(weight_decay))
+        # full-size minibatches replay two HIP graphs (forward+backward, clip+AdamW);
+        # AdamW is then 'capturable' with its learning rate in a device tensor
+        self.use_graphs = (self.device.type == "cuda") if use_graphs is None else bool(use_graphs)
+        lr0 = self.lr_schedule(1.0)
+        if self.use_graphs:
+            self.optimizer = torch.optim.AdamW(self.policy.parameters(), lr=torch.tensor(lr0, device=self.device),
+                                               weight_decay=float(weight_decay), capturable=True)
+        else:
+            self.optimizer = torch.optim.AdamW(self.policy.parameters(), lr=lr0, weight_decay=float(weight_decay))
+        self._graphs = None
         self.gen = torch.Generator(device=self.device)
         self.gen.manual_seed(int(seed) * 1000003 + self.rank)
         self.shuffle_gen = torch.Generator(device=self.device)
@@ -212,52 +289,80 @@ class BatchedPPO:
             out[k] = None if g is None else g.reshape(-1, *v.shape[1:])
         return out if self.rank == 0 else None
 
+    def _graphs_for(self, d: Dict[str, torch.Tensor], n: int) -> Optional[_UpdateGraphs]:
+        if n < self.batch_size:
+            return None
+        if self._graphs is None or self._graphs.n != n:
+            self._graphs = _UpdateGraphs(self, n)
+        self._graphs.load(d)
+        return self._graphs
+
     def train(self) -> None:
         data = self._gathered()
         if data is not None:
             self._update(data)
         self._sync_params()
 
+    def _loss(self, obs, act, old_logp, adv, ret, clip):
+        """One minibatch of SB3 PPO.train: -> (loss, pg, vf, ent, approx_kl, clip_fraction)."""
+        values, logp, entropy = self.policy.evaluate_actions(obs, act)
+        if self.normalize_advantage and adv.shape[0] > 1:
+            adv = (adv - adv.mean()) / (adv.std() + 1e-8)
+        log_ratio = logp - old_logp
+        ratio = torch.exp(log_ratio)
+        pg = -torch.min(adv * ratio, adv * torch.clamp(ratio, 1 - clip, 1 + clip)).mean()
+        vf = nn.functional.mse_loss(ret, values)
+        ent = -torch.mean(entropy)
+        loss = pg + self.ent_coef * ent + self.vf_coef * vf
+        with torch.no_grad():
+            kl = torch.mean((ratio - 1) - log_ratio)
+            cf = torch.mean((torch.abs(ratio - 1) > clip).float())
+        return loss, pg.detach(), vf.detach(), ent.detach(), kl, cf
+
     def _update(self, d: Dict[str, torch.Tensor]) -> None:
         self.policy.train()
         lr = self.lr_schedule(self.progress_remaining)
-        for g in self.optimizer.param_groups:
-            g["lr"] = lr
         clip = self.clip_schedule(self.progress_remaining)
         n = d["obs"].shape[0]
+        graphs = self._graphs_for(d, n) if self.use_graphs else None
+        for g in self.optimizer.param_groups:
+            if isinstance(g["lr"], torch.Tensor):
+                g["lr"].fill_(lr)
+            else:
+                g["lr"] = lr
+        if graphs is not None:
+            graphs.clip.fill_(clip)
         ent_l, pg_l, vf_l, clip_f = [], [], [], []
         cont = True
         loss = torch.zeros((), device=self.device)
-        approx_kl = 0.0
+        kls = []
         for _epoch in range(self.n_epochs):
             kls = []
             perm = torch.randperm(n, generator=self.shuffle_gen, device=self.device)
             for s in range(0, n, self.batch_size):
                 idx = perm[s:s + self.batch_size]
-                obs, act = d["obs"][idx], d["actions"][idx]
-                values, logp, entropy = self.policy.evaluate_actions(obs, act)
-                adv = d["advantages"][idx]
-                if self.normalize_advantage and len(adv) > 1:
-                    adv = (adv - adv.mean()) / (adv.std() + 1e-8)
-                log_ratio = logp - d["log_probs"][idx]
-                ratio = torch.exp(log_ratio)
-                pg = -torch.min(adv * ratio, adv * torch.clamp(ratio, 1 - clip, 1 + clip)).mean()
-                vf = nn.functional.mse_loss(d["returns"][idx], values)
-                ent = -torch.mean(entropy)
-                loss = pg + self.ent_coef * ent + self.vf_coef * vf
-                with torch.no_grad():
-                    kl = torch.mean((ratio - 1) - log_ratio)
-                    pg_l.append(pg.detach()); vf_l.append(vf.detach()); ent_l.append(ent.detach())
-                    clip_f.append(torch.mean((torch.abs(ratio - 1) > clip).float()))
+                if graphs is not None and idx.shape[0] == self.batch_size:
+                    graphs.idx.copy_(idx)
+                    graphs.fwd_bwd.replay()          # loss terms + gradients
+                    loss, pg, vf, ent, kl, cf = (t.clone() for t in graphs.out)
+                    step = graphs.opt_step.replay    # clip_grad_norm + AdamW
+                else:
+                    loss, pg, vf, ent, kl, cf = self._loss(d["obs"][idx], d["actions"][idx], d["log_probs"][idx],
+                                                           d["advantages"][idx], d["returns"][idx], clip)
+                    step = None
+                pg_l.append(pg); vf_l.append(vf); ent_l.append(ent); clip_f.append(cf)
                 approx_kl = float(kl)  # the early stop needs it before the step (host sync)
                 kls.append(approx_kl)
                 if self.target_kl is not None and approx_kl > 1.5 * self.target_kl:
                     cont = False
                     break
-                self.optimizer.zero_grad(set_to_none=True)
-                loss.backward()
-                nn.utils.clip_grad_norm_(self.policy.parameters(), self.max_grad_norm)
-                self.optimizer.step()
+                if step is not None:
+                    step()
+                else:
+                    self.optimizer.zero_grad(set_to_none=False)
+                    loss.backward()
+                    nn.utils.clip_grad_norm_(self.policy.parameters(), self.max_grad_norm)
+                    self.optimizer.step()
             self._n_updates += 1
             if not cont:
                 break
@@ -266,7 +371,7 @@ class BatchedPPO:
         L.record("train/entropy_loss", mean(ent_l))
         L.record("train/policy_gradient_loss", mean(pg_l))
         L.record("train/value_loss", mean(vf_l))
-        L.record("train/approx_kl", float(np.mean(kls)) if kls else float("nan"))
+        L.record("train/approx_kl", float(np.mean(kls)) if kls else float("nan"))  # last epoch, as SB3
         L.record("train/clip_fraction", mean(clip_f))
         L.record("train/loss", float(loss.detach()))
         L.record("train/explained_variance", explained_variance(d["values"], d["returns"]))
