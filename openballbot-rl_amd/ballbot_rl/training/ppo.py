@@ -102,60 +102,83 @@ class RolloutBuffer:
 
 
 class _UpdateGraphs:
-    """Two captured graphs for one full minibatch of PPO.train over static data buffers.
+    """PPO.train as ONE captured graph per minibatch, replayed with no host sync.
 
-    fwd_bwd: gather rows idx of the data, loss terms, zero + backward the grads;
-    opt_step: clip_grad_norm_ + AdamW.step (capturable).  Split so the KL early
-    stop is decided on the host between them, exactly as SB3 does."""
+    The graph reads minibatch `k` of a static permutation (device counter),
+    evaluates the SB3 loss terms, back-propagates, and runs clip_grad_norm_ +
+    AdamW (capturable).  SB3's KL early stop -- break BEFORE the step once
+    approx_kl > 1.5 * target_kl, and end the update -- becomes a sticky device
+    flag: from the flagged minibatch on, the step is undone in-graph
+    (parameters and AdamW state restored with torch.where) and the minibatch's
+    log row is marked; after the update one host sync reads the log rows and
+    keeps exactly the minibatches SB3 would have logged.  Requires
+    n % batch_size == 0 (SB3's short last minibatch goes through the eager path)."""
+
+    LOG_COLS = 7  # loss, pg, vf, ent, kl, clip_fraction, logged
 
     def __init__(self, ppo: "BatchedPPO", n: int):
         dev, B = ppo.device, ppo.batch_size
-        self.n = n
+        self.n, self.nb = n, n // B
         self.data = {"obs": torch.zeros(n, 15, device=dev), "actions": torch.zeros(n, 3, device=dev),
                      "log_probs": torch.zeros(n, device=dev), "advantages": torch.zeros(n, device=dev),
                      "returns": torch.zeros(n, device=dev)}
-        self.idx = torch.zeros(B, dtype=torch.int64, device=dev)
+        self.perm = torch.zeros(self.nb, B, dtype=torch.int64, device=dev)
+        self.k = torch.zeros(1, dtype=torch.int64, device=dev)        # minibatch within the epoch
+        self.row = torch.zeros(1, dtype=torch.int64, device=dev)      # log row within the update
         self.clip = torch.zeros((), device=dev)
+        self.kl_stop = torch.full((), float("inf"), device=dev)       # 1.5 * target_kl
+        self.stop = torch.zeros((), dtype=torch.bool, device=dev)
+        self.log = torch.zeros(ppo.n_epochs * self.nb, self.LOG_COLS, device=dev)
         pol, opt = ppo.policy, ppo.optimizer
         params = [p for p in pol.parameters() if p.requires_grad]
-        # snapshot: the warm-up step below must not change the policy or AdamW state
         p_snap = [p.detach().clone() for p in params]
         st_snap = {id(p): {k: v.clone() for k, v in opt.state[p].items()} for p in params if p in opt.state}
 
-        def fwd_bwd():
+        def mb_step():
             d = self.data
-            out = ppo._loss(d["obs"][self.idx], d["actions"][self.idx], d["log_probs"][self.idx],
-                            d["advantages"][self.idx], d["returns"][self.idx], self.clip)
+            idx = self.perm.index_select(0, self.k).view(-1)
+            loss, pg, vf, ent, kl, cf = ppo._loss(d["obs"][idx], d["actions"][idx], d["log_probs"][idx],
+                                                  d["advantages"][idx], d["returns"][idx], self.clip)
+            logged = (~self.stop).float()                        # SB3 logs the minibatch that trips the stop
+            self.stop.logical_or_(kl > self.kl_stop)
+            row = torch.stack([loss.detach(), pg, vf, ent, kl, cf, logged]).view(1, -1)
+            self.log.index_copy_(0, self.row, row)
             for p in params:
                 if p.grad is not None:
                     p.grad.zero_()
-            out[0].backward()
-            return out
-
-        def opt_step():
+            loss.backward()
+            with torch.no_grad():
+                keep_p = [p.detach().clone() for p in params]
+                keep_s = [[v.clone() for v in opt.state[p].values()] for p in params] if len(opt.state) else None
             nn.utils.clip_grad_norm_(params, ppo.max_grad_norm)
             opt.step()
+            with torch.no_grad():
+                for i, p in enumerate(params):
+                    p.copy_(torch.where(self.stop, keep_p[i], p))
+                    if keep_s is not None:
+                        for v, kv in zip(opt.state[p].values(), keep_s[i]):
+                            v.copy_(torch.where(self.stop, kv, v))
+                self.k.add_(1)
+                self.row.add_(1)
 
-        self.idx.copy_(torch.arange(B, device=dev) % max(n, 1))
+        self.perm.copy_(torch.arange(self.nb * B, device=dev).view(self.nb, B) % max(n, 1))
         side = torch.cuda.Stream(device=dev)
         side.wait_stream(torch.cuda.current_stream(dev))
         with torch.cuda.stream(side):
-            for _ in range(2):
-                fwd_bwd()
-                opt_step()
+            for _ in range(2):  # warm-up (also creates the AdamW state the graph updates)
+                self.k.zero_(); self.row.zero_()
+                mb_step()
         torch.cuda.current_stream(dev).wait_stream(side)
         for p in params:  # backward allocates the grads inside the graph pool (static addresses)
             p.grad = None
-        self.fwd_bwd = torch.cuda.CUDAGraph()
-        with torch.cuda.graph(self.fwd_bwd):
-            self.out = fwd_bwd()
-        self.opt_step = torch.cuda.CUDAGraph()
-        with torch.cuda.graph(self.opt_step, pool=self.fwd_bwd.pool()):
-            opt_step()
+        self.k.zero_(); self.row.zero_()
+        self.graph = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(self.graph):
+            mb_step()
         torch.cuda.synchronize(dev)
-        with torch.no_grad():
-            for p, s in zip(params, p_snap):
-                p.copy_(s)
+        with torch.no_grad():  # undo the warm-up: policy and AdamW state as before
+            for p, s_ in zip(params, p_snap):
+                p.copy_(s_)
             for p in params:
                 prev = st_snap.get(id(p))
                 for k, v in opt.state[p].items():
@@ -164,9 +187,20 @@ class _UpdateGraphs:
                     else:
                         v.zero_()
 
-    def load(self, d: Dict[str, torch.Tensor]) -> None:
+    def run(self, ppo: "BatchedPPO", d: Dict[str, torch.Tensor], clip: float):
+        """All epochs of one update; -> per-minibatch log rows [n_epochs * nb, 7] on the host."""
         for k, v in self.data.items():
             v.copy_(d[k])
+        self.clip.fill_(clip)
+        self.kl_stop.fill_(float("inf") if ppo.target_kl is None else 1.5 * ppo.target_kl)
+        self.stop.zero_()
+        self.row.zero_()
+        for _epoch in range(ppo.n_epochs):
+            self.perm.copy_(torch.randperm(self.n, generator=ppo.shuffle_gen, device=ppo.device).view(self.nb, -1))
+            self.k.zero_()
+            for _ in range(self.nb):
+                self.graph.replay()
+        return self.log.cpu().numpy()
 
 
 class BatchedPPO:
@@ -289,12 +323,11 @@ class BatchedPPO:
             out[k] = None if g is None else g.reshape(-1, *v.shape[1:])
         return out if self.rank == 0 else None
 
-    def _graphs_for(self, d: Dict[str, torch.Tensor], n: int) -> Optional[_UpdateGraphs]:
-        if n < self.batch_size:
+    def _graphs_for(self, n: int) -> Optional[_UpdateGraphs]:
+        if n < self.batch_size or n % self.batch_size:
             return None
         if self._graphs is None or self._graphs.n != n:
             self._graphs = _UpdateGraphs(self, n)
-        self._graphs.load(d)
         return self._graphs
 
     def train(self) -> None:
@@ -324,48 +357,50 @@ class BatchedPPO:
         lr = self.lr_schedule(self.progress_remaining)
         clip = self.clip_schedule(self.progress_remaining)
         n = d["obs"].shape[0]
-        graphs = self._graphs_for(d, n) if self.use_graphs else None
         for g in self.optimizer.param_groups:
             if isinstance(g["lr"], torch.Tensor):
                 g["lr"].fill_(lr)
             else:
                 g["lr"] = lr
-        if graphs is not None:
-            graphs.clip.fill_(clip)
-        ent_l, pg_l, vf_l, clip_f = [], [], [], []
-        cont = True
+        graphs = self._graphs_for(n) if self.use_graphs else None
         loss = torch.zeros((), device=self.device)
-        kls = []
-        for _epoch in range(self.n_epochs):
-            kls = []
-            perm = torch.randperm(n, generator=self.shuffle_gen, device=self.device)
-            for s in range(0, n, self.batch_size):
-                idx = perm[s:s + self.batch_size]
-                if graphs is not None and idx.shape[0] == self.batch_size:
-                    graphs.idx.copy_(idx)
-                    graphs.fwd_bwd.replay()          # loss terms + gradients
-                    loss, pg, vf, ent, kl, cf = (t.clone() for t in graphs.out)
-                    step = graphs.opt_step.replay    # clip_grad_norm + AdamW
-                else:
+        ent_l, pg_l, vf_l, clip_f, kls = [], [], [], [], []
+        if graphs is not None:
+            log = graphs.run(self, d, clip)
+            nb = graphs.nb
+            for e in range(self.n_epochs):
+                rows = log[e * nb:(e + 1) * nb]
+                rows = rows[rows[:, 6] > 0]
+                if len(rows) == 0:
+                    break
+                self._n_updates += 1
+                kls = rows[:, 4].tolist()
+                for r in rows:
+                    pg_l.append(torch.tensor(r[1])); vf_l.append(torch.tensor(r[2])); ent_l.append(torch.tensor(r[3]))
+                    clip_f.append(torch.tensor(r[5]))
+                loss = torch.tensor(rows[-1, 0])
+        else:
+            cont = True
+            for _epoch in range(self.n_epochs):
+                kls = []
+                perm = torch.randperm(n, generator=self.shuffle_gen, device=self.device)
+                for s in range(0, n, self.batch_size):
+                    idx = perm[s:s + self.batch_size]
                     loss, pg, vf, ent, kl, cf = self._loss(d["obs"][idx], d["actions"][idx], d["log_probs"][idx],
                                                            d["advantages"][idx], d["returns"][idx], clip)
-                    step = None
-                pg_l.append(pg); vf_l.append(vf); ent_l.append(ent); clip_f.append(cf)
-                approx_kl = float(kl)  # the early stop needs it before the step (host sync)
-                kls.append(approx_kl)
-                if self.target_kl is not None and approx_kl > 1.5 * self.target_kl:
-                    cont = False
-                    break
-                if step is not None:
-                    step()
-                else:
+                    pg_l.append(pg); vf_l.append(vf); ent_l.append(ent); clip_f.append(cf)
+                    approx_kl = float(kl)  # the early stop needs it before the step (host sync)
+                    kls.append(approx_kl)
+                    if self.target_kl is not None and approx_kl > 1.5 * self.target_kl:
+                        cont = False
+                        break
                     self.optimizer.zero_grad(set_to_none=False)
                     loss.backward()
                     nn.utils.clip_grad_norm_(self.policy.parameters(), self.max_grad_norm)
                     self.optimizer.step()
-            self._n_updates += 1
-            if not cont:
-                break
+                self._n_updates += 1
+                if not cont:
+                    break
         L = self.logger
         mean = lambda xs: float(torch.stack(xs).mean()) if xs else float("nan")  # noqa: E731
         L.record("train/entropy_loss", mean(ent_l))
@@ -375,7 +410,7 @@ class BatchedPPO:
         L.record("train/clip_fraction", mean(clip_f))
         L.record("train/loss", float(loss.detach()))
         L.record("train/explained_variance", explained_variance(d["values"], d["returns"]))
-        L.record("train/std", float(torch.exp(self.policy.log_std).mean()))
+        L.record("train/std", float(torch.exp(self.policy.log_std.detach()).mean()))
         L.record("train/n_updates", self._n_updates)
         L.record("train/clip_range", clip)
         L.record("train/learning_rate", lr)

@@ -74,9 +74,11 @@ def test_train_main_end_to_end(tmp_path):
     assert "eval/mean_reward" in cols
 
 
-def test_graph_update_matches_eager():
-    """The two-graph minibatch update == the eager SB3 update on the same rollout data."""
+@pytest.mark.parametrize("target_kl", [None, 2e-4])
+def test_graph_update_matches_eager(target_kl):
+    """The graph-replayed update (device-side KL stop) == the eager SB3 update on the same rollout."""
     from fake_env import FakeEnv
+    from ballbot_rl.training.logger import CSVLogger
     from ballbot_rl.training.ppo import BatchedPPO
 
     dev = torch.device("cuda:0")
@@ -96,14 +98,23 @@ def test_graph_update_matches_eager():
 
     models = []
     for graphs in (False, True):
-        m = BatchedPPO(GpuFake(), n_steps=16, batch_size=512, n_epochs=3, learning_rate=1e-3, target_kl=None,
-                       normalize_advantage=True, seed=4, use_graphs=graphs)
+        m = BatchedPPO(GpuFake(), n_steps=16, batch_size=512, n_epochs=3, learning_rate=1e-3, target_kl=target_kl,
+                       normalize_advantage=True, seed=4, use_graphs=graphs, logger=CSVLogger(None, stdout=False))
+        if not graphs:  # same AdamW kernels as the graph path
+            m.optimizer = torch.optim.AdamW(m.policy.parameters(), lr=torch.tensor(1e-3, device=dev),
+                                            weight_decay=0.01, capturable=True)
         m.collect_rollouts()
         models.append(m)
     d0 = models[0].buf.flat()
     for m in models:  # same rollout data and shuffles for both
         m.shuffle_gen.manual_seed(99)
         m._update({k: v.clone() for k, v in d0.items()})
+    assert models[1]._graphs is not None
+    assert models[0]._n_updates == models[1]._n_updates
+    if target_kl is not None:
+        assert models[0]._n_updates < 3  # the stop fired
     for a, b in zip(models[0].policy.parameters(), models[1].policy.parameters()):
         assert torch.allclose(a, b, rtol=1e-5, atol=1e-6), (a - b).abs().max()
-    assert models[1]._graphs is not None
+    la, lb = models[0].logger.values, models[1].logger.values
+    for k in ("train/policy_gradient_loss", "train/value_loss", "train/approx_kl", "train/clip_fraction"):
+        assert la[k] == pytest.approx(lb[k], rel=1e-4, abs=1e-7), k
