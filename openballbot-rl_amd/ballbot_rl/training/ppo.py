@@ -105,16 +105,18 @@ class _UpdateGraphs:
     """PPO.train as ONE captured graph per minibatch, replayed with no host sync.
 
     The graph reads minibatch `k` of a static permutation (device counter),
-    evaluates the SB3 loss terms, back-propagates, and runs clip_grad_norm_ +
-    AdamW (capturable).  SB3's KL early stop -- break BEFORE the step once
-    approx_kl > 1.5 * target_kl, and end the update -- becomes a sticky device
-    flag: from the flagged minibatch on, the step is undone in-graph
-    (parameters and AdamW state restored with torch.where) and the minibatch's
-    log row is marked; after the update one host sync reads the log rows and
-    keeps exactly the minibatches SB3 would have logged.  Requires
-    n % batch_size == 0 (SB3's short last minibatch goes through the eager path)."""
+    evaluates the SB3 loss terms into a log row, back-propagates, and runs
+    clip_grad_norm_ + AdamW (capturable).  SB3's KL early stop (break BEFORE the
+    step once approx_kl > 1.5 * target_kl, ending the update) is applied
+    optimistically: all epochs replay back to back, one host sync reads the log
+    rows, and if some row r tripped the stop the policy and AdamW state are
+    restored from the snapshot taken at the start and rows 0..r-1 are replayed
+    again with the same permutations -- the exact steps SB3 takes.  The stop is
+    rare (approx_kl ~1e-3 against 0.45 in the reference's runs), so the common
+    update costs no sync at all.  Requires n % batch_size == 0 (SB3's short last
+    minibatch goes through the eager path)."""
 
-    LOG_COLS = 7  # loss, pg, vf, ent, kl, clip_fraction, logged
+    LOG_COLS = 6  # loss, pg, vf, ent, kl, clip_fraction
 
     def __init__(self, ppo: "BatchedPPO", n: int):
         dev, B = ppo.device, ppo.batch_size
@@ -123,14 +125,13 @@ class _UpdateGraphs:
                      "log_probs": torch.zeros(n, device=dev), "advantages": torch.zeros(n, device=dev),
                      "returns": torch.zeros(n, device=dev)}
         self.perm = torch.zeros(self.nb, B, dtype=torch.int64, device=dev)
+        self.perms = torch.zeros(ppo.n_epochs, self.nb, B, dtype=torch.int64, device=dev)
         self.k = torch.zeros(1, dtype=torch.int64, device=dev)        # minibatch within the epoch
         self.row = torch.zeros(1, dtype=torch.int64, device=dev)      # log row within the update
         self.clip = torch.zeros((), device=dev)
-        self.kl_stop = torch.full((), float("inf"), device=dev)       # 1.5 * target_kl
-        self.stop = torch.zeros((), dtype=torch.bool, device=dev)
         self.log = torch.zeros(ppo.n_epochs * self.nb, self.LOG_COLS, device=dev)
-        pol, opt = ppo.policy, ppo.optimizer
-        params = [p for p in pol.parameters() if p.requires_grad]
+        self.params = params = [p for p in ppo.policy.parameters() if p.requires_grad]
+        opt = ppo.optimizer
         p_snap = [p.detach().clone() for p in params]
         st_snap = {id(p): {k: v.clone() for k, v in opt.state[p].items()} for p in params if p in opt.state}
 
@@ -139,25 +140,14 @@ class _UpdateGraphs:
             idx = self.perm.index_select(0, self.k).view(-1)
             loss, pg, vf, ent, kl, cf = ppo._loss(d["obs"][idx], d["actions"][idx], d["log_probs"][idx],
                                                   d["advantages"][idx], d["returns"][idx], self.clip)
-            logged = (~self.stop).float()                        # SB3 logs the minibatch that trips the stop
-            self.stop.logical_or_(kl > self.kl_stop)
-            row = torch.stack([loss.detach(), pg, vf, ent, kl, cf, logged]).view(1, -1)
-            self.log.index_copy_(0, self.row, row)
+            self.log.index_copy_(0, self.row, torch.stack([loss.detach(), pg, vf, ent, kl, cf]).view(1, -1))
             for p in params:
                 if p.grad is not None:
                     p.grad.zero_()
             loss.backward()
-            with torch.no_grad():
-                keep_p = [p.detach().clone() for p in params]
-                keep_s = [[v.clone() for v in opt.state[p].values()] for p in params] if len(opt.state) else None
             nn.utils.clip_grad_norm_(params, ppo.max_grad_norm)
             opt.step()
             with torch.no_grad():
-                for i, p in enumerate(params):
-                    p.copy_(torch.where(self.stop, keep_p[i], p))
-                    if keep_s is not None:
-                        for v, kv in zip(opt.state[p].values(), keep_s[i]):
-                            v.copy_(torch.where(self.stop, kv, v))
                 self.k.add_(1)
                 self.row.add_(1)
 
@@ -176,31 +166,56 @@ class _UpdateGraphs:
         with torch.cuda.graph(self.graph):
             mb_step()
         torch.cuda.synchronize(dev)
-        with torch.no_grad():  # undo the warm-up: policy and AdamW state as before
-            for p, s_ in zip(params, p_snap):
+        self._restore(opt, [p_snap, {i: st_snap.get(id(p)) for i, p in enumerate(params)}])
+
+    def _snapshot(self, opt):
+        return [[p.detach().clone() for p in self.params],
+                {i: {k: v.clone() for k, v in opt.state[p].items()} for i, p in enumerate(self.params)}]
+
+    def _restore(self, opt, snap) -> None:
+        with torch.no_grad():
+            for p, s_ in zip(self.params, snap[0]):
                 p.copy_(s_)
-            for p in params:
-                prev = st_snap.get(id(p))
+            for i, p in enumerate(self.params):
+                prev = snap[1].get(i)
                 for k, v in opt.state[p].items():
                     if prev is not None and k in prev:
                         v.copy_(prev[k])
                     else:
                         v.zero_()
 
+    def _replay(self, rows: int) -> None:
+        self.row.zero_()
+        done = 0
+        for e in range(self.perms.shape[0]):
+            if done >= rows:
+                break
+            self.perm.copy_(self.perms[e])
+            self.k.zero_()
+            for _ in range(min(self.nb, rows - done)):
+                self.graph.replay()
+                done += 1
+
     def run(self, ppo: "BatchedPPO", d: Dict[str, torch.Tensor], clip: float):
-        """All epochs of one update; -> per-minibatch log rows [n_epochs * nb, 7] on the host."""
+        """All epochs of one update; -> the log rows SB3 would have recorded, [rows, 6] on the host."""
         for k, v in self.data.items():
             v.copy_(d[k])
         self.clip.fill_(clip)
-        self.kl_stop.fill_(float("inf") if ppo.target_kl is None else 1.5 * ppo.target_kl)
-        self.stop.zero_()
-        self.row.zero_()
-        for _epoch in range(ppo.n_epochs):
-            self.perm.copy_(torch.randperm(self.n, generator=ppo.shuffle_gen, device=ppo.device).view(self.nb, -1))
-            self.k.zero_()
-            for _ in range(self.nb):
-                self.graph.replay()
-        return self.log.cpu().numpy()
+        for e in range(ppo.n_epochs):
+            self.perms[e].copy_(torch.randperm(self.n, generator=ppo.shuffle_gen, device=ppo.device).view(self.nb, -1))
+        total = ppo.n_epochs * self.nb
+        snap = self._snapshot(ppo.optimizer) if ppo.target_kl is not None else None
+        self._replay(total)
+        log = self.log.cpu().numpy()
+        if ppo.target_kl is not None:
+            trip = np.nonzero(log[:, 4] > 1.5 * ppo.target_kl)[0]
+            if len(trip):
+                r = int(trip[0])
+                self._restore(ppo.optimizer, snap)
+                self._replay(r)            # the steps before the tripping minibatch
+                keep = log[:r + 1].copy()  # ... whose own terms SB3 still logs
+                return keep
+        return log
 
 
 class BatchedPPO:
@@ -370,7 +385,6 @@ class BatchedPPO:
             nb = graphs.nb
             for e in range(self.n_epochs):
                 rows = log[e * nb:(e + 1) * nb]
-                rows = rows[rows[:, 6] > 0]
                 if len(rows) == 0:
                     break
                 self._n_updates += 1
