@@ -12,6 +12,7 @@
  *   bb_reset         mj_resetData + height offset + mj_forward  ballbot_env.py:612-620
  *   bb_step          ctrl = -clip(10a); mj_step; _get_obs;      ballbot_env.py:903-1036
  *                    reward plugin; termination
+ *   bb_render_depth  RGBDInputs depth cams (_get_obs)           sensors/rgbd.py:46-82
  *   bb_gae           SB3 RolloutBuffer.compute_returns_and_advantage (PPO)
  *   bb_forward       mujoco.mj_forward (diagnostic)             ballbot_env.py:525,620
  *   bb_get_state/    read/write qpos/qvel/qacc_warmstart        ballbot_env.py:616-617
@@ -39,7 +40,7 @@
 extern "C" {
 #endif
 
-#define BB_ABI_VERSION 5
+#define BB_ABI_VERSION 6
 #define BB_NQ 17
 #define BB_NV 15
 #define BB_OBS 15
@@ -110,6 +111,16 @@ int bb_generate_perlin(bb_handle* h, int first_terrain_id, int count, const int3
 int bb_gae(const float* rewards_dev, const float* values_dev, const uint8_t* episode_starts_dev,
            const float* last_values_dev, const uint8_t* last_dones_dev, int T, int n_envs, double gamma,
            double gae_lambda, float* advantages_dev, float* returns_dev, void* stream);
+/* depth cameras cam_0/cam_1 (ballbot.xml:44-54, fovy 90): for every env whose
+ * step counter is a multiple of `every` (or all envs when force != 0), render
+ * the linear z-depth clipped to 1 m into depth_dev float[n][2][height][width]
+ * (row 0 = top); rel_ts_dev float[n] (may be NULL) receives
+ * relative_image_timestamp = (steps % every) * 2 ms.  Replaces RGBDInputs with
+ * disable_rgb (sensors/rgbd.py:46-82) as called by _get_obs
+ * (ballbot_env.py:743-767, every = ceil((1/frame_rate)/dt), :389-411).
+ * Enqueued on stream, after bb_step / bb_reset. */
+int bb_render_depth(bb_handle* h, float* depth_dev, float* rel_ts_dev, int height, int width, int every,
+                    int force, void* stream);
 /* copy terrain bank slot terrain_id (float32[293*293]) to host memory */
 int bb_get_hfield(bb_handle* h, int terrain_id, float* data_host);
 /* per-env terrain ids (device int32[n]) applied at the next reset */

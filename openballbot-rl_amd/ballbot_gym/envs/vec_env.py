@@ -45,6 +45,7 @@ class BallbotVecEnv:
         precision: str = "fp64",
         n_terrains: Optional[int] = None,
         auto_reset: bool = True,
+        disable_cameras: bool = True,
     ):
         from .config import TERRAIN_SEED_HIGH, gpu_perlin_plan, np_random, params_from_configs, terrain_bank
 
@@ -55,6 +56,16 @@ class BallbotVecEnv:
             raise ValueError(f"BallbotVecEnv runs on a GPU device, got {self.device}")
         self.num_envs = int(num_envs)
         self.auto_reset = bool(auto_reset)
+        # depth cameras (ballbot_env.py:211-290; camera: height/width/frame_rate/disable_rgb).
+        # The reference defaults to cameras on; the batched env defaults to off (the
+        # proprio hot path) -- pass disable_cameras=False for rgbd_0/rgbd_1 obs.
+        self.cameras = not disable_cameras
+        cam = ((env_config or {}).get("camera", {}) or {})
+        self.cam_h, self.cam_w = int(cam.get("height", 64)), int(cam.get("width", 64))
+        fr = float(cam.get("frame_rate", 90))
+        self.cam_every = int(np.ceil((1.0 / fr) / 0.002))  # effective_camera_frame_rate (ballbot_env.py:389-411)
+        if self.cameras and not cam.get("disable_rgb", True):
+            raise ValueError("only depth cameras are rendered (camera.disable_rgb must be true)")
         self.terrain_config = terrain_config or {"type": "flat", "config": {}}
         self.reward_config = reward_config or {"type": "directional", "config": {"target_direction": [0.0, 1.0]}}
         p, self.reward_obj, self._host_reward = params_from_configs(self.reward_config, env_config, max_ep_steps,
@@ -88,6 +99,9 @@ class BallbotVecEnv:
         self.reward = torch.zeros(n, dtype=torch.float32, device=dev)
         self.done = torch.zeros(n, dtype=torch.uint8, device=dev)
         self.pos2d = torch.zeros(n, 2, dtype=torch.float32, device=dev)
+        if self.cameras:
+            self.depth = torch.ones(n, 2, self.cam_h, self.cam_w, dtype=torch.float32, device=dev)
+            self.rel_ts = torch.zeros(n, dtype=torch.float32, device=dev)
         if plan is not None and self.n_terrains == TERRAIN_SEED_HIGH:
             # whole seed space resident (slot == seed): the first reset draws the
             # reference's seed stream, integers(0, 10000) (ballbot_env.py:505-510)
@@ -106,7 +120,20 @@ class BallbotVecEnv:
     def reset(self, mask: Optional[torch.Tensor] = None):
         m = None if mask is None else mask.to(device=self.device, dtype=torch.uint8).contiguous()
         N.check(N.lib().bb_reset(self._h, _ptr(m), _ptr(self.obs), self._stream()), "bb_reset")
+        if self.cameras:
+            self._render(force=m is None)
         return self.obs, {}
+
+    def _render(self, force: bool) -> None:
+        N.check(N.lib().bb_render_depth(self._h, _ptr(self.depth), _ptr(self.rel_ts), self.cam_h, self.cam_w,
+                                        self.cam_every, int(force), self._stream()), "bb_render_depth")
+
+    def render_depth(self, force: bool = True) -> torch.Tensor:
+        """Depth images [N, 2, H, W] of cam_0/cam_1 at the current state (linear depth, clipped to 1 m)."""
+        if not self.cameras:
+            raise RuntimeError("cameras are disabled (BallbotVecEnv(..., disable_cameras=False))")
+        self._render(force)
+        return self.depth
 
     def step(self, actions: torch.Tensor):
         """One env.step for all envs: returns (obs[N,15], reward[N], terminated[N], truncated[N], info)."""
@@ -117,6 +144,8 @@ class BallbotVecEnv:
         N.check(N.lib().bb_step(self._h, _ptr(actions), _ptr(self.obs), _ptr(self.reward), _ptr(self.done),
                                 _ptr(self.terminal_obs), _ptr(self.pos2d), int(self.auto_reset), self._stream()),
                 "bb_step")
+        if self.cameras:  # envs whose counter hit the frame interval (incl. auto-resets) re-render
+            self._render(force=False)
         terminated = (self.done & N.DONE_TERMINATED) != 0
         info = {"done_flags": self.done, "terminal_observation": self.terminal_obs, "pos2d": self.pos2d,
                 "failure": (self.done & N.DONE_FAILURE) != 0}
@@ -144,7 +173,12 @@ class BallbotVecEnv:
 
     def obs_dict(self, obs: Optional[torch.Tensor] = None) -> Dict[str, torch.Tensor]:
         o = self.obs if obs is None else obs
-        return {k: o[:, 3 * i:3 * i + 3] for i, k in enumerate(OBS_KEYS)}
+        d = {k: o[:, 3 * i:3 * i + 3] for i, k in enumerate(OBS_KEYS)}
+        if self.cameras:  # the reference's camera keys (ballbot_env.py:812-826), channels-first
+            d["rgbd_0"] = self.depth[:, 0:1]
+            d["rgbd_1"] = self.depth[:, 1:2]
+            d["relative_image_timestamp"] = self.rel_ts.unsqueeze(1)
+        return dict(sorted(d.items()))
 
     # ------------------------------------------------------------ parity/state
     def get_state(self):

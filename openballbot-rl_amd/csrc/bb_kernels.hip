@@ -23,6 +23,7 @@
 #include "bb_step.h"
 #include "bb_terrain.h"
 #include "bb_rollout.h"
+#include "bb_render.h"
 
 using namespace bb;
 
@@ -378,6 +379,8 @@ struct bb_handle {
   // optional HIP-event timing of the fast step kernel (bb_time_kernel)
   std::vector<hipEvent_t> tev;
   int tcap = 0, tn = 0;
+  CamRig rig;  // depth cameras in the base body (bb_render_depth)
+  void* scenes = nullptr;
 };
 
 template <typename T> const ModelT<T>& model_of(const bb_handle* h);
@@ -496,6 +499,18 @@ int bb_create(int n_envs, int device, const bb_params* p, bb_handle** out) {
   }
   h->md = compile_model(sc);
   h->mf = cast_model<float>(h->md);
+  // cam_k: body cam_k_body (pos (+-0.17, -0.01, -0.06), euler 180 -+30 0) and
+  // camera euler 180 0 0 in it (ballbot.xml:44-54)
+  for (int cam = 0; cam < 2; cam++) {
+    double qb[4], qc[4], q[4], R[9];
+    bb::detail::euler_quat(qb, 180, cam == 0 ? -30 : 30, 0);
+    bb::detail::euler_quat(qc, 180, 0, 0);
+    qmul(q, qb, qc);
+    q2mat(R, q);
+    const double p[3] = {cam == 0 ? 0.17 : -0.17, -0.01, -0.06};
+    for (int i = 0; i < 3; i++) h->rig.p[cam][i] = float(p[i]);
+    for (int i = 0; i < 9; i++) h->rig.R[cam][i] = float(R[i]);
+  }
   const size_t es = h->fp64 ? sizeof(double) : sizeof(float);
   const size_t n = n_envs, nt = pp.n_terrains;
   Dev& d = h->d;
@@ -562,6 +577,7 @@ int bb_destroy(bb_handle* h) {
   (void)hipFree(h->d.fast_envs); (void)hipFree(h->d.pred_envs); (void)hipFree(h->d.pred_mark);
   (void)hipStreamDestroy(h->side); (void)hipEventDestroy(h->fork); (void)hipEventDestroy(h->join);
   for (hipEvent_t e : h->tev) (void)hipEventDestroy(e);
+  (void)hipFree(h->scenes);
   delete h;
   return 0;
 }
@@ -616,6 +632,21 @@ int bb_gae(const float* rew, const float* val, const uint8_t* start, const float
   if (T < 1 || n < 1) return fail("bb_gae: need T >= 1 and n_envs >= 1 (got %d, %d)", T, n);
   if (launch_gae(rew, val, start, last_val, last_done, T, n, gamma, lam, adv, ret, (hipStream_t)stream))
     return fail("bb_gae: launch failed: %s", hipGetErrorString(hipGetLastError()));
+  return 0;
+}
+
+int bb_render_depth(bb_handle* h, float* depth, float* rel_ts, int height, int width, int every, int force,
+                    void* stream) {
+  if (!h || !depth) return fail("bb_render_depth: NULL argument");
+  if (height < 1 || width < 1 || height > 1024 || width > 1024)
+    return fail("bb_render_depth: image size %dx%d out of range [1,1024]", height, width);
+  if (every < 1) return fail("bb_render_depth: frame interval must be >= 1 step (got %d)", every);
+  HIPCHK(hipSetDevice(h->device));
+  RenderDev rd{h->n, h->d.qpos, h->d.steps, h->d.terrain, h->bank, h->size_z};
+  if (!h->scenes) HIPCHK(hipMalloc(&h->scenes, scene_bytes(h->n)));
+  if (launch_depth(h->fp64 != 0, h->mf, h->rig, rd, height, width, every, force, 0.002f, h->scenes, depth, rel_ts,
+                   (hipStream_t)stream))
+    return fail("bb_render_depth: launch failed: %s", hipGetErrorString(hipGetLastError()));
   return 0;
 }
 

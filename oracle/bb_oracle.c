@@ -1590,3 +1590,172 @@ int bbo_env_step_batch(const bbo_env_cfg* cfg, int n, double* qpos, double* qvel
   }
   return nd;
 }
+
+/* ------------------------------------------------------------ depth cameras
+ * Restates what RGBDInputs (sensors/rgbd.py:46-82) reads from MuJoCo's
+ * renderer for cam_0 / cam_1 (ballbot.xml:44-54): the linear eye-space depth
+ * (z along the camera's -z axis, mujoco.Renderer's near/(1 - z(1 - near/far))
+ * conversion of the depth buffer), one sample per pixel centre, fovy 90,
+ * clipped to <= 1.0 (rgbd.py:74).  Visible geoms (groups 0-2): the hfield,
+ * the ball, the tower cylinder, the cam sticks and the wheel capsules; the
+ * ballast (group 3) is hidden and the cone meshes are missing from the
+ * reference.  Back faces are culled (a ray starting inside a geom does not see
+ * it), surfaces nearer than znear = 1e-4 * extent (extent 10*sqrt(2), the
+ * model's comment at ballbot.xml:9) are clipped.  The hfield surface is
+ * triangulated as the collision prisms (cell (r,c): (r,c)(r+1,c)(r,c+1) and
+ * (r+1,c)(r,c+1)(r+1,c+1)); its side walls are not drawn.  Row 0 = top of the
+ * image (x right, y up in the camera frame).  PARITY UNPINNED against
+ * MuJoCo's OpenGL rasteriser (not available); tests pin it by analytic scenes.
+ */
+#define BBO_ZNEAR (1e-4 * 14.142135623730951)
+
+static double ray_sphere(const double* o, const double* d, const double* c, double r) {
+  double oc[3]; v3sub(oc, o, c);
+  double b = v3dot(oc, d), cc = v3dot(oc, oc) - r * r, h = b * b - cc;
+  if (h < 0) return -1;
+  return -b - sqrt(h);
+}
+
+/* front-face entry of a capsule (segment pa-pb, radius r); -1 if none; |d| = 1 */
+static double ray_capsule(const double* o, const double* d, const double* pa, const double* pb, double r) {
+  double ba[3], oa[3];
+  v3sub(ba, pb, pa); v3sub(oa, o, pa);
+  double baba = v3dot(ba, ba), bard = v3dot(ba, d), baoa = v3dot(ba, oa), rdoa = v3dot(d, oa), oaoa = v3dot(oa, oa);
+  double a = baba - bard * bard, b = baba * rdoa - baoa * bard, c = baba * oaoa - baoa * baoa - r * r * baba;
+  double h = b * b - a * c;
+  if (h < 0) return -1;
+  double t = a > 1e-300 ? (-b - sqrt(h)) / a : -1;
+  double y = baoa + t * bard;
+  if (a > 1e-300 && y > 0 && y < baba) return t;
+  /* caps: the sphere at the end the body hit falls beyond */
+  double oc[3];
+  if (y <= 0) v3copy(oc, oa); else v3sub(oc, o, pb);
+  double bb = v3dot(d, oc), cc = v3dot(oc, oc) - r * r, hh = bb * bb - cc;
+  if (hh > 0) return -bb - sqrt(hh);
+  return -1;
+}
+
+/* front-face entry of a capped cylinder (axis pa-pb, radius r); -1 if none; |d| = 1 */
+static double ray_cylinder(const double* o, const double* d, const double* pa, const double* pb, double r) {
+  double ba[3], oc[3];
+  v3sub(ba, pb, pa); v3sub(oc, o, pa);
+  double baba = v3dot(ba, ba), bard = v3dot(ba, d), baoc = v3dot(ba, oc);
+  double k2 = baba - bard * bard, k1 = baba * v3dot(oc, d) - baoc * bard;
+  double k0 = baba * v3dot(oc, oc) - baoc * baoc - r * r * baba;
+  double h = k1 * k1 - k2 * k0;
+  if (h < 0) return -1;
+  h = sqrt(h);
+  if (k2 > 1e-300) {
+    double t = (-k1 - h) / k2, y = baoc + t * bard;
+    if (y > 0 && y < baba) return t;
+    if (fabs(bard) < 1e-300) return -1;
+    t = (((y < 0) ? 0 : baba) - baoc) / bard;
+    if (fabs(k1 + k2 * t) < h) return t;
+    return -1;
+  }
+  /* ray parallel to the axis: caps only */
+  if (k0 > 0 || fabs(bard) < 1e-300) return -1;
+  double t0 = (0 - baoc) / bard, t1 = (baba - baoc) / bard;
+  return t0 < t1 ? t0 : t1;
+}
+
+/* two-sided Moller-Trumbore; -1 if none */
+static double ray_tri(const double* o, const double* d, const double* a, const double* b, const double* c) {
+  double e1[3], e2[3], p[3], s[3], q[3];
+  v3sub(e1, b, a); v3sub(e2, c, a);
+  v3cross(p, d, e2);
+  double det = v3dot(e1, p);
+  if (fabs(det) < 1e-300) return -1;
+  double inv = 1.0 / det;
+  v3sub(s, o, a);
+  double u = v3dot(s, p) * inv;
+  if (u < 0 || u > 1) return -1;
+  v3cross(q, s, e1);
+  double v = v3dot(d, q) * inv;
+  if (v < 0 || u + v > 1) return -1;
+  return v3dot(e2, q) * inv;
+}
+
+static double hf_z(const float* hf, int r, int c, double size_z) { return (double)hf[r * BBO_HF_N + c] * size_z; }
+
+/* nearest hfield hit along o + t d (|d| = 1) for t in (tmin, tmax); -1 if none.
+ * 2-D DDA over the cells the ray's xy projection crosses. */
+static double ray_hfield(const double* o, const double* d, const float* hf, double size_z, double tmin, double tmax) {
+  const int N1 = BBO_HF_N - 1;
+  const double sx = HF_SIZE[0], sy = HF_SIZE[1], dx = 2 * sx / N1, dy = 2 * sy / N1;
+  /* clip the parameter range to the field's xy box */
+  double t0 = tmin, t1 = tmax;
+  for (int ax = 0; ax < 2; ax++) {
+    double lo = -HF_SIZE[ax], hi = HF_SIZE[ax];
+    if (fabs(d[ax]) < 1e-300) { if (o[ax] < lo || o[ax] > hi) return -1; continue; }
+    double ta = (lo - o[ax]) / d[ax], tb = (hi - o[ax]) / d[ax];
+    if (ta > tb) { double s = ta; ta = tb; tb = s; }
+    if (ta > t0) t0 = ta;
+    if (tb < t1) t1 = tb;
+  }
+  if (t0 > t1) return -1;
+  double px = o[0] + t0 * d[0], py = o[1] + t0 * d[1];
+  int c = (int)floor((px + sx) / dx), r = (int)floor((py + sy) / dy);
+  c = c < 0 ? 0 : (c > N1 - 1 ? N1 - 1 : c);
+  r = r < 0 ? 0 : (r > N1 - 1 ? N1 - 1 : r);
+  int stc = d[0] > 0 ? 1 : -1, str = d[1] > 0 ? 1 : -1;
+  double tdx = fabs(d[0]) > 1e-300 ? dx / fabs(d[0]) : 1e300, tdy = fabs(d[1]) > 1e-300 ? dy / fabs(d[1]) : 1e300;
+  double nx = -sx + (c + (stc > 0 ? 1 : 0)) * dx, ny = -sy + (r + (str > 0 ? 1 : 0)) * dy;
+  double tmx = fabs(d[0]) > 1e-300 ? (nx - o[0]) / d[0] : 1e300, tmy = fabs(d[1]) > 1e-300 ? (ny - o[1]) / d[1] : 1e300;
+  for (int it = 0; it < 4 * BBO_HF_N; it++) {
+    double x0 = -sx + c * dx, x1 = -sx + (c + 1) * dx, y0 = -sy + r * dy, y1 = -sy + (r + 1) * dy;
+    double A[3] = {x0, y0, hf_z(hf, r, c, size_z)}, B[3] = {x0, y1, hf_z(hf, r + 1, c, size_z)};
+    double C[3] = {x1, y0, hf_z(hf, r, c + 1, size_z)}, D[3] = {x1, y1, hf_z(hf, r + 1, c + 1, size_z)};
+    double best = -1;
+    double ta = ray_tri(o, d, A, B, C), tb = ray_tri(o, d, B, C, D);
+    if (ta > tmin && ta < tmax) best = ta;
+    if (tb > tmin && tb < tmax && (best < 0 || tb < best)) best = tb;
+    if (best > 0) return best;
+    double tn = tmx < tmy ? tmx : tmy;
+    if (tn > t1) break;
+    if (tmx < tmy) { c += stc; tmx += tdx; if (c < 0 || c > N1 - 1) break; }
+    else { r += str; tmy += tdy; if (r < 0 || r > N1 - 1) break; }
+  }
+  return -1;
+}
+
+/* camera frames in their bodies (ballbot.xml:47,53: pos 0, euler 180 0 0) */
+void bbo_render_depth(const double* qpos, const float* hf, double size_z, int cam, int H, int W, float* out) {
+  double xpos[NB][3], xquat[NB][4], xmat[NB][9], xipos[NB][3], xI[NB][9], xanchor[3][3], xaxis[3][3];
+  kinematics_all(qpos, xpos, xquat, xmat, xipos, xI, xanchor, xaxis);
+  int b = 2 + cam;
+  double qc[4], cq[4], R[9];
+  euler2quat(qc, 180, 0, 0);
+  qmul(cq, xquat[b], qc);
+  q2mat(R, cq);
+  const double* o = xpos[b];
+  Convex g[6]; int cyl[6], body[6];
+  body_geoms(xpos, xmat, g, cyl, body);
+  double ball[3], t[3];
+  m3v(t, xmat[7], BALL_GPOS);
+  v3add(ball, xpos[7], t);
+  const double tanh_ = 1.0; /* tan(fovy / 2), fovy 90 */
+  for (int i = 0; i < H; i++)
+    for (int j = 0; j < W; j++) {
+      double xc = (2.0 * (j + 0.5) / W - 1.0) * tanh_ * ((double)W / H);
+      double yc = (1.0 - 2.0 * (i + 0.5) / H) * tanh_;
+      double dc[3] = {xc, yc, -1.0}, d[3];
+      m3v(d, R, dc);
+      double len = sqrt(v3dot(d, d));
+      for (int k = 0; k < 3; k++) d[k] /= len;
+      const double tmin = BBO_ZNEAR * len, tmax = 1.0 * len;  /* z-depth in (znear, 1] */
+      double best = tmax;
+      double th = ray_sphere(o, d, ball, BALL_R);
+      if (th > tmin && th < best) best = th;
+      for (int k = 0; k < 6; k++) {
+        double pa[3], pb[3];
+        for (int q = 0; q < 3; q++) { pa[q] = g[k].c[q] - g[k].a[q] * g[k].hh; pb[q] = g[k].c[q] + g[k].a[q] * g[k].hh; }
+        double tk = cyl[k] ? ray_cylinder(o, d, pa, pb, g[k].r) : ray_capsule(o, d, pa, pb, g[k].r);
+        if (tk > tmin && tk < best) best = tk;
+      }
+      double tg = ray_hfield(o, d, hf, size_z, tmin, best);
+      if (tg > tmin && tg < best) best = tg;
+      double z = best / len;
+      out[i * W + j] = (float)(z >= 1.0 ? 1.0 : z);
+    }
+}

@@ -111,6 +111,10 @@ double bbo_init_offset(const float* hfield, double size_z);
 /* numpy-quaternion as_rotation_vector restatement (quaternion_log). */
 void bbo_quat_to_rotvec(const double* q, double* rv);
 
+/* Depth image of cam (0/1) at qpos: float32[H][W], linear z-depth clipped to 1
+ * (sensors/rgbd.py:46-82 over ballbot.xml:44-54; see bb_oracle.c). */
+void bbo_render_depth(const double* qpos, const float* hfield, double size_z, int cam, int H, int W, float* out);
+
 /* Batch helper: n envs stepped sequentially on one thread (CPU baseline). */
 int bbo_env_step_batch(const bbo_env_cfg* cfg, int n, double* qpos, double* qvel,
                        double* warm, int* step_counter, const float* actions,

@@ -100,6 +100,7 @@ def lib():
         L.bbo_env_step_batch.argtypes = [C.POINTER(EnvCfg), C.c_int, dp, dp, dp, ip, fp, fp, C.c_double,
                                          fp, fp, C.POINTER(C.c_ubyte), C.c_double]
         L.bbo_env_step_batch.restype = C.c_int
+        L.bbo_render_depth.argtypes = [dp, fp, C.c_double, C.c_int, C.c_int, C.c_int, fp]
         _lib = L
     return _lib
 
@@ -128,6 +129,15 @@ def model_info() -> dict:
         "wheel0_ipos": out[42:45].copy(),
         "base_inertia": out[45:54].reshape(3, 3).copy(),
     }
+
+
+def render_depth(qpos: np.ndarray, hfield: np.ndarray, cam: int, H: int = 64, W: int = 64,
+                 size_z: float = 2.0) -> np.ndarray:
+    """Depth image float32[H, W] of cam 0/1 (bbo_render_depth)."""
+    out = np.zeros((H, W), np.float32)
+    q = np.ascontiguousarray(qpos, np.float64)
+    lib().bbo_render_depth(_d(q), _f(np.ascontiguousarray(hfield, np.float32)), float(size_z), int(cam), H, W, _f(out))
+    return out
 
 
 def set_flags(flags: int) -> None:

@@ -252,3 +252,54 @@ def test_body_contacts_keep_robot_above_ground(oracle):
     fo = oracle.forward(q, v, np.zeros(3), w, hf)
     assert fo.nbody > 0                 # lying on its side, touching the ground
     assert q[2] > 0.0 and np.abs(v[:6]).max() < 0.05  # the base came to rest (the ball may roll off)
+
+
+def _cam_pose(q, cam):
+    """Camera origin and camera->world rotation from qpos (ballbot.xml:44-54), numpy."""
+    from scipy.spatial.transform import Rotation as Rot
+
+    Rb = Rot.from_quat([q[4], q[5], q[6], q[3]]).as_matrix()
+    Rbody = Rot.from_euler("XYZ", [180, -30 if cam == 0 else 30, 0], degrees=True).as_matrix()
+    Rcam = Rot.from_euler("XYZ", [180, 0, 0], degrees=True).as_matrix()
+    o = q[:3] + Rb @ np.array([0.17 if cam == 0 else -0.17, -0.01, -0.06])
+    return o, Rb @ Rbody @ Rcam
+
+
+@pytest.mark.parametrize("cam", [0, 1])
+def test_depth_camera_flat_ground_analytic(oracle, cam):
+    """Every pixel sees the analytic ground-plane depth or something nearer (a robot
+    geom); most pixels see the ground; far pixels clip to 1 (sensors/rgbd.py:74)."""
+    rng = np.random.default_rng(cam)
+    for trial in range(4):
+        q, _, _ = oracle.reset_state(0.01)
+        q = q.copy()
+        q[2] += rng.uniform(0, 0.6)
+        q[12] += q[2] - 0.25 - 0.01
+        ang = rng.uniform(-0.2, 0.2, 3)
+        from scipy.spatial.transform import Rotation as Rot
+
+        qq = Rot.from_rotvec(ang).as_quat()
+        q[3:7] = [qq[3], qq[0], qq[1], qq[2]]
+        d = oracle.render_depth(q, oracle.flat_hfield(), cam)
+        o, R = _cam_pose(q, cam)
+        H = W = 64
+        j, i = np.meshgrid(np.arange(W), np.arange(H))
+        xc = 2 * (j + 0.5) / W - 1
+        yc = 1 - 2 * (i + 0.5) / H
+        dirs = np.stack([xc, yc, -np.ones_like(xc)], -1) @ R.T
+        s = -o[2] / dirs[..., 2]
+        ground = np.where(s > 0, np.minimum(s, 1.0), 1.0)
+        assert (d <= ground + 1e-5).all()
+        same = np.abs(d - ground) < 1e-5
+        assert same.mean() > 0.3, same.mean()
+        assert d.max() <= 1.0 and d.min() > 0
+
+
+def test_depth_camera_sees_ball_and_culls_inside(oracle):
+    """The ball occludes the ground below the robot; a camera inside its own stick
+    capsule does not see the capsule (back faces culled)."""
+    q, _, _ = oracle.reset_state(0.01)
+    d0 = oracle.render_depth(q, oracle.flat_hfield(), 0)
+    d0_far = oracle.render_depth(np.r_[q[:10], q[10] + 3.0, q[11:]], oracle.flat_hfield(), 0)  # ball moved away
+    assert (d0 <= d0_far + 1e-6).all() and (d0 < d0_far - 1e-3).sum() > 50
+    assert d0.min() > 0.005  # the 1 cm stick capsule around the camera origin is not drawn
