@@ -81,6 +81,7 @@ def main() -> None:
     ap.add_argument("--terrain", default="flat")
     ap.add_argument("--n-terrains", type=int, default=None,
                     help="terrain bank size (default: 16 host-generated seeds; perlin: the whole 10^4 seed space on the GPU)")
+    ap.add_argument("--cameras", action="store_true", help="also render the depth cameras (F2) every 6 steps")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
     ap.add_argument("--traffic-json", default=str(ROOT / "profiles" / "traffic.json"))
@@ -105,11 +106,17 @@ def main() -> None:
     # weak scaling: every rank owns a contiguous block of `--envs` global env ids
     first_env, n = env_shard(args.envs * world, rank, world)
     env = BallbotVecEnv(n, device=dev, precision=args.precision, seed=rank_seed(1000, first_env),
-                        terrain_config={"type": args.terrain, "config": {}}, n_terrains=args.n_terrains)
+                        terrain_config={"type": args.terrain, "config": {}}, n_terrains=args.n_terrains,
+                        disable_cameras=not args.cameras)
+
+    def step(a):
+        env.step_async_raw(a)
+        if args.cameras:
+            env._render(force=False)
     g = torch.Generator(device=dev).manual_seed(1234 + rank)
     pool = torch.rand(64, n, 3, generator=g, device=dev) * 2 - 1  # random actions resident in HBM
     for i in range(args.warmup):
-        env.step_async_raw(pool[i % 64])
+        step(pool[i % 64])
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
@@ -119,7 +126,7 @@ def main() -> None:
     t0 = time.perf_counter()
     ev0.record()
     for i in range(args.steps):
-        env.step_async_raw(pool[i % 64])
+        step(pool[i % 64])
     ev1.record()
     torch.cuda.synchronize()
     if world > 1:
@@ -161,7 +168,7 @@ def main() -> None:
             "data": "synthetic (uniform random actions in [-1,1], resident in HBM)",
             "config": {"workload": f"{n} envs/GPU, {args.terrain} terrain, random actions "
                                    f"(BASELINE configs[{1 if args.terrain == 'flat' else 2}])",
-                       "n_terrains": env.n_terrains,
+                       "n_terrains": env.n_terrains, "depth_cameras": bool(args.cameras),
                        "envs_per_gpu": n, "total_envs": n * world, "precision": args.precision,
                        "parallelism": f"env-sharded x{world} (no collective on the step path)",
                        "launch": launch},

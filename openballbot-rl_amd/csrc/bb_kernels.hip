@@ -132,6 +132,9 @@ __global__ __launch_bounds__(64) void step_kernel(ModelT<T> mg, EnvCfg cfg, Dev 
                                                   const int* __restrict__ elist, const int* __restrict__ ecount) {
   // epw teams of L lanes per 64-lane wave (teams >= epw idle)
   extern __shared__ __align__(16) unsigned char smem[];
+  // list launches are sized for every env; workgroups past the list end leave
+  // before touching LDS (on flat terrain the full-kernel lists are empty)
+  if (elist && int(blockIdx.x) * epw >= *ecount) return;
   // model constants staged in LDS once per workgroup: uniform-address LDS
   // reads broadcast, and ~150 uniform doubles no longer overflow the SGPRs
   __shared__ ModelT<T> ms;
@@ -642,7 +645,7 @@ int bb_render_depth(bb_handle* h, float* depth, float* rel_ts, int height, int w
     return fail("bb_render_depth: image size %dx%d out of range [1,1024]", height, width);
   if (every < 1) return fail("bb_render_depth: frame interval must be >= 1 step (got %d)", every);
   HIPCHK(hipSetDevice(h->device));
-  RenderDev rd{h->n, h->d.qpos, h->d.steps, h->d.terrain, h->bank, h->size_z};
+  RenderDev rd{h->n, h->d.qpos, h->d.steps, h->d.terrain, h->bank, h->size_z, h->hmax};
   if (!h->scenes) HIPCHK(hipMalloc(&h->scenes, scene_bytes(h->n)));
   if (launch_depth(h->fp64 != 0, h->mf, h->rig, rd, height, width, every, force, 0.002f, h->scenes, depth, rel_ts,
                    (hipStream_t)stream))

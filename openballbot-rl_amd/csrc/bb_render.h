@@ -21,6 +21,7 @@ struct RenderDev {
   const int* terrain;     // bank slot per env
   const float* bank;
   const float* size_z;
+  const float* hmax;      // per terrain: max(hfield)
 };
 
 // scratch the launch needs: per (env, camera) scene

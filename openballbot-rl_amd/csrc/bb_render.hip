@@ -35,6 +35,7 @@ struct Scene {
   float pa[6][3], pb[6][3];  // 0 tower (cylinder), 1-2 sticks, 3-5 wheels (capsules)
   float rad[6];
   float size_z;
+  float ztop;  // max terrain height (hmax * size_z): rays above it skip the march
   int tid;
 };
 
@@ -102,11 +103,16 @@ __device__ float ray_tri(const float* o, const float* d, const float* a, const f
 }
 
 // nearest hfield hit in (tmin, tmax) by a 2-D DDA over the cells the ray crosses
-__device__ float ray_hfield(const float* o, const float* d, const float* hf, float size_z, float sx, float sy,
-                            float tmin, float tmax) {
+__device__ float ray_hfield(const float* o, const float* d, const float* hf, float size_z, float ztop, float sx,
+                            float sy, float tmin, float tmax) {
   const int N1 = HF_N - 1;
   const float dx = 2.f * sx / N1, dy = 2.f * sy / N1;
   float t0 = tmin, t1 = tmax;
+  // no surface above ztop: start where the ray descends through it (flat: the plane hit)
+  if (o[2] > ztop) {
+    if (d[2] >= 0.f) return -1.f;
+    t0 = fmaxf(t0, (ztop - o[2]) / d[2] * (1.f - 1e-6f));
+  }
   const float half[2] = {sx, sy};
 #pragma unroll
   for (int ax = 0; ax < 2; ax++) {
@@ -195,6 +201,7 @@ __global__ __launch_bounds__(64) void scene_kernel(ModelT<float> m, CamRig rig, 
   }
   S.tid = d.terrain[e];
   S.size_z = d.size_z[S.tid];
+  S.ztop = d.hmax[S.tid] * S.size_z;
   for (int cam = 0; cam < 2; cam++) {
     to_world(k, rig.p[cam], S.o);
     mm3(S.R, k.Rb, rig.R[cam]);
@@ -237,7 +244,7 @@ __global__ __launch_bounds__(256) void depth_kernel(ModelT<float> m, RenderDev d
       const float t = ray_capsule(S.o, dr, S.pa[g], S.pb[g], S.rad[g]);
       if (t > tmin && t < best) best = t;
     }
-    const float tg = ray_hfield(S.o, dr, hf, S.size_z, m.hf_sx, m.hf_sy, tmin, best);
+    const float tg = ray_hfield(S.o, dr, hf, S.size_z, S.ztop, m.hf_sx, m.hf_sy, tmin, best);
     if (tg > tmin && tg < best) best = tg;
     out[px] = fminf(best * il, 1.f);
   }
