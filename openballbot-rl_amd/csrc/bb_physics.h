@@ -85,6 +85,17 @@ template <typename T> BB_HD void cross3(T* r, const T* a, const T* b) {
   T x = a[1] * b[2] - a[2] * b[1], y = a[2] * b[0] - a[0] * b[2], z = a[0] * b[1] - a[1] * b[0];
   r[0] = x; r[1] = y; r[2] = z;
 }
+// x[6 + w] for a runtime w in {0,1,2}, without an indexed load: LLVM folds
+// `w == 0 ? x[6] : ...` into x[6 + w], which turns the whole register array x
+// into a scratch-memory array.  Bit masks keep it a register select.
+template <typename T>
+BB_HD T hinge_sel(int w, const T* x) {
+  using U = typename std::conditional<sizeof(T) == 8, unsigned long long, unsigned int>::type;
+  const U m0 = U(0) - U(w == 0), m1 = U(0) - U(w == 1), m2 = U(0) - U(w == 2);
+  const U b = (__builtin_bit_cast(U, x[6]) & m0) | (__builtin_bit_cast(U, x[7]) & m1) | (__builtin_bit_cast(U, x[8]) & m2);
+  return __builtin_bit_cast(T, b);
+}
+
 template <typename T> BB_HD void mv3(T* r, const T* M, const T* v) {  // r = M v
   T x = M[0] * v[0] + M[1] * v[1] + M[2] * v[2];
   T y = M[3] * v[0] + M[4] * v[1] + M[5] * v[2];
@@ -824,7 +835,7 @@ BB_HD void body_ls_terms(const ModelT<T>& m, const T* bc, const Poses<T>& P, con
     mtv3(wB, P.RB, x1);
     auto dotJ = [&](const T* x) {
       T acc = F[0] * x[0] + F[1] * x[1] + F[2] * x[2] + wa[0] * x[3] + wa[1] * x[4] + wa[2] * x[5];
-      acc += hinge >= 0 ? jh * (hinge == 0 ? x[6] : (hinge == 1 ? x[7] : x[8])) : T(0);
+      acc += hinge >= 0 ? jh * hinge_sel(hinge, x) : T(0);
       acc -= ball * (F[0] * x[9] + F[1] * x[10] + F[2] * x[11] + wB[0] * x[12] + wB[1] * x[13] + wB[2] * x[14]);
       return acc;
     };
@@ -837,7 +848,7 @@ BB_HD void body_ls_terms(const ModelT<T>& m, const T* bc, const Poses<T>& P, con
 // J_r x for a body contact in the 13-column layout
 template <typename T>
 BB_HD T body_dot(const T (&J)[3][13], int hinge, int r, const T* x) {
-  T acc = hinge >= 0 ? J[r][6] * (hinge == 0 ? x[6] : (hinge == 1 ? x[7] : x[8])) : T(0);
+  T acc = hinge >= 0 ? J[r][6] * hinge_sel(hinge, x) : T(0);
 #pragma unroll
   for (int q = 0; q < 6; q++) acc += J[r][q] * x[q];
 #pragma unroll

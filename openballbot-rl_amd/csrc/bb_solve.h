@@ -141,7 +141,7 @@ BB_HD int wheel_pos(int i, int w) { return i < 6 ? i : (i == 6 + w ? 6 : (i >= 9
 // J_r x for wheel contact w (w may be lane-dependent: the hinge entry is selected)
 template <typename T>
 BB_HD T wheel_dot(const WheelCon<T>& C, int w, int r, const T* x) {
-  const T xh = w == 0 ? x[6] : (w == 1 ? x[7] : x[8]);
+  const T xh = hinge_sel(w, x);
   T acc = C.J[r][6] * xh;
 #pragma unroll
   for (int i = 0; i < 6; i++) acc += C.J[r][i] * x[i];

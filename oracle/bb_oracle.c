@@ -1186,9 +1186,14 @@ static int newton(const Efc* e, const double* Mm, const double* a0, double* a, d
   double jar[BBO_MAXCON * 3], force[BBO_MAXCON * 3], Hc[BBO_MAXCON * 9];
   for (it = 0; it < g_maxiter; it++) {
     for (int r = 0; r < nr; r++) { double s = -e->aref[r]; for (int d = 0; d < NV; d++) s += e->J[r][d] * a[d]; jar[r] = s; }
-    total_cost(e, jar, force, Hc);
+    double ccost = total_cost(e, jar, force, Hc);
     double grad[NV], dq[NV];
     for (int d = 0; d < NV; d++) dq[d] = a[d] - a0[d];
+    if (g_flags & 512) {  /* diagnostics: MuJoCo's cost = Gauss + constraint */
+      double gauss = 0;
+      for (int i = 0; i < NV; i++) for (int j = 0; j < NV; j++) gauss += 0.5 * dq[i] * Mm[i * NV + j] * dq[j];
+      fprintf(stderr, "C %d %.17g\n", it, scale * (gauss + ccost));
+    }
     for (int i = 0; i < NV; i++) {
       double s = 0;
       for (int j = 0; j < NV; j++) s += Mm[i * NV + j] * dq[j];
@@ -1198,6 +1203,7 @@ static int newton(const Efc* e, const double* Mm, const double* a0, double* a, d
     double gn = 0;
     for (int i = 0; i < NV; i++) gn += grad[i] * grad[i];
     if (g_flags & 256) fprintf(stderr, "it %d gn %.3e\n", it, scale * sqrt(gn));
+    if (g_flags & 512) fprintf(stderr, "G %d %.17g\n", it, scale * sqrt(gn));
     if (scale * sqrt(gn) < g_tol) break;
     double H[NV * NV];
     memcpy(H, Mm, sizeof H);

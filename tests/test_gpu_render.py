@@ -13,25 +13,31 @@ torch = pytest.importorskip("torch")
 pytestmark = pytest.mark.gpu
 
 
-def _env(n, terrain, seed=0):
+def _env(n, terrain, seed=0, **kw):
     from ballbot_gym.envs import BallbotVecEnv
 
     return BallbotVecEnv(n, device="cuda:0", terrain_config=terrain, disable_cameras=False, auto_reset=False,
-                         seed=seed)
+                         seed=seed, **kw)
 
 
-@pytest.mark.parametrize("terrain", ["flat", "hills"])
+@pytest.mark.parametrize("terrain", ["flat", "hills", "perlin"])
 def test_depth_matches_oracle(oracle, terrain):
     import traj
+    from ballbot_gym.envs.config import np_random
     from ballbot_gym.terrain import generate_hills_terrain
+    from ballbot_gym.terrain.perlin import generate_perlin_terrain
 
+    kw = {}
     if terrain == "flat":
         hf, tcfg = oracle.flat_hfield(), {"type": "flat", "config": {}}
-    else:
+    elif terrain == "hills":
         hf = generate_hills_terrain(293, seed=7).astype(np.float32)
         tcfg = {"type": "hills", "config": {"seed": 7}}
+    else:  # GPU bank slot 0 = the first seed of np_random(0); sloped ground in view
+        hf = generate_perlin_terrain(293, seed=int(np_random(0).integers(0, 10000))).astype(np.float32)
+        tcfg, kw = {"type": "perlin", "config": {}}, {"n_terrains": 1}
     rec = traj.record(n_envs=32, n_steps=40, hfield=hf, seed=21)
-    env = _env(32, tcfg)
+    env = _env(32, tcfg, **kw)
     for t in (0, 13, 39):
         q = rec["qpos"][t]
         env.set_state(q, rec["qvel"][t], rec["warm"][t], np.zeros(32, np.int32))

@@ -28,7 +28,9 @@ def main():
     if a.build or not LIB.exists():
         LIB.parent.mkdir(parents=True, exist_ok=True)
         subprocess.run(["hipcc", "--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC", "-shared", "-DBB_PHASE_CLOCKS",
-                        "-o", str(LIB), str(ROOT / "openballbot-rl_amd" / "csrc" / "bb_kernels.hip")], check=True)
+                        "-o", str(LIB)] + [str(ROOT / "openballbot-rl_amd" / "csrc" / f) for f in
+                                           ("bb_kernels.hip", "bb_terrain.hip", "bb_rollout.hip", "bb_render.hip")],
+                       check=True)
     import torch
     from ballbot_gym import _native
     _native.use_diagnostic_library(LIB)
