@@ -81,10 +81,13 @@ def explained_variance(y_pred: torch.Tensor, y_true: torch.Tensor) -> float:
 class RolloutBuffer:
     """[T][N] device buffers of one rollout (SB3 RolloutBuffer, device-resident)."""
 
-    def __init__(self, T: int, n: int, obs_dim: int, act_dim: int, device):
+    def __init__(self, T: int, n: int, obs_dim: int, act_dim: int, device, image_shape=None):
         f32 = dict(dtype=torch.float32, device=device)
         self.T, self.n = T, n
         self.obs = torch.zeros(T, n, obs_dim, **f32)
+        # depth cameras (F2): [T][N][2][H][W] images + relative_image_timestamp
+        self.depth = torch.zeros(T, n, *image_shape, **f32) if image_shape else None
+        self.rel_ts = torch.zeros(T, n, **f32) if image_shape else None
         self.actions = torch.zeros(T, n, act_dim, **f32)
         self.rewards = torch.zeros(T, n, **f32)
         self.values = torch.zeros(T, n, **f32)
@@ -96,9 +99,27 @@ class RolloutBuffer:
     def flat(self) -> Dict[str, torch.Tensor]:
         """Flattened [T*N] views (the sample order does not matter: minibatches are random)."""
         T, n = self.T, self.n
-        return {"obs": self.obs.reshape(T * n, -1), "actions": self.actions.reshape(T * n, -1),
-                "values": self.values.reshape(-1), "log_probs": self.log_probs.reshape(-1),
-                "advantages": self.advantages.reshape(-1), "returns": self.returns.reshape(-1)}
+        d = {"obs": self.obs.reshape(T * n, -1), "actions": self.actions.reshape(T * n, -1),
+             "values": self.values.reshape(-1), "log_probs": self.log_probs.reshape(-1),
+             "advantages": self.advantages.reshape(-1), "returns": self.returns.reshape(-1)}
+        if self.depth is not None:
+            d["depth"] = self.depth.reshape(T * n, *self.depth.shape[2:])
+            d["rel_ts"] = self.rel_ts.reshape(-1)
+        return d
+
+
+def policy_obs(obs15: torch.Tensor, depth: Optional[torch.Tensor] = None,
+               rel_ts: Optional[torch.Tensor] = None):
+    """The policy's observation: the packed proprio tensor, or with cameras the
+    reference's key dict (ballbot_env.py:812-826) the Extractor concatenates."""
+    if depth is None:
+        return obs15
+    d = {k: obs15[:, 3 * i:3 * i + 3] for i, k in enumerate(("actions", "angular_vel", "motor_state",
+                                                             "orientation", "vel"))}
+    d["rgbd_0"] = depth[:, 0:1]
+    d["rgbd_1"] = depth[:, 1:2]
+    d["relative_image_timestamp"] = rel_ts.reshape(-1, 1)
+    return d
 
 
 class _UpdateGraphs:
@@ -124,6 +145,9 @@ class _UpdateGraphs:
         self.data = {"obs": torch.zeros(n, 15, device=dev), "actions": torch.zeros(n, 3, device=dev),
                      "log_probs": torch.zeros(n, device=dev), "advantages": torch.zeros(n, device=dev),
                      "returns": torch.zeros(n, device=dev)}
+        if ppo.cameras:
+            self.data["depth"] = torch.zeros(n, 2, ppo.env.cam_h, ppo.env.cam_w, device=dev)
+            self.data["rel_ts"] = torch.zeros(n, device=dev)
         self.perm = torch.zeros(self.nb, B, dtype=torch.int64, device=dev)
         self.perms = torch.zeros(ppo.n_epochs, self.nb, B, dtype=torch.int64, device=dev)
         self.k = torch.zeros(1, dtype=torch.int64, device=dev)        # minibatch within the epoch
@@ -138,7 +162,7 @@ class _UpdateGraphs:
         def mb_step():
             d = self.data
             idx = self.perm.index_select(0, self.k).view(-1)
-            loss, pg, vf, ent, kl, cf = ppo._loss(d["obs"][idx], d["actions"][idx], d["log_probs"][idx],
+            loss, pg, vf, ent, kl, cf = ppo._loss(ppo._mb_obs(d, idx), d["actions"][idx], d["log_probs"][idx],
                                                   d["advantages"][idx], d["returns"][idx], self.clip)
             self.log.index_copy_(0, self.row, torch.stack([loss.detach(), pg, vf, ent, kl, cf]).view(1, -1))
             for p in params:
@@ -248,9 +272,12 @@ class BatchedPPO:
         self.rank = dist.get_rank() if dist.is_available() and dist.is_initialized() else 0
         self.world = dist.get_world_size() if dist.is_available() and dist.is_initialized() else 1
         torch.manual_seed(int(seed))
-        self.policy = (policy or ActorCriticPolicy(obs_spaces(), 3, net_arch, activation_fn)).to(self.device)
+        self.cameras = bool(getattr(env, "cameras", False))
+        img = (2, env.cam_h, env.cam_w) if self.cameras else None
+        spaces = obs_spaces(cameras=True, height=env.cam_h, width=env.cam_w) if self.cameras else obs_spaces()
+        self.policy = (policy or ActorCriticPolicy(spaces, 3, net_arch, activation_fn)).to(self.device)
         self._sync_params()
-        # full-size minibatches replay two HIP graphs (forward+backward, clip+AdamW);
+        # full-size minibatches replay one HIP graph (forward+backward, clip+AdamW);
         # AdamW is then 'capturable' with its learning rate in a device tensor
         self.use_graphs = (self.device.type == "cuda") if use_graphs is None else bool(use_graphs)
         lr0 = self.lr_schedule(1.0)
@@ -265,7 +292,7 @@ class BatchedPPO:
         self.shuffle_gen = torch.Generator(device=self.device)
         self.shuffle_gen.manual_seed(int(seed) + 7)
         self.logger = logger or CSVLogger(None, stdout=False)
-        self.buf = RolloutBuffer(self.n_steps, self.n_envs, 15, 3, self.device)
+        self.buf = RolloutBuffer(self.n_steps, self.n_envs, 15, 3, self.device, img)
         self.num_timesteps = 0
         self._n_updates = 0
         self.ep_info_buffer: deque = deque(maxlen=int(stats_window_size))
@@ -287,13 +314,20 @@ class BatchedPPO:
     @torch.no_grad()
     def collect_rollouts(self) -> None:
         env, b = self.env, self.buf
+        self.policy.eval()  # SB3 set_training_mode(False): BatchNorm uses running stats
         if self._last_obs is None:
             self._last_obs, _ = env.reset()
         ep_r, ep_l = [], []
         for t in range(self.n_steps):
             b.obs[t].copy_(self._last_obs)        # env.obs is reused by the next step
             b.starts[t].copy_(self._last_starts)
-            actions, values, logp = self.policy(b.obs[t], generator=self.gen)
+            if self.cameras:
+                b.depth[t].copy_(env.depth)
+                b.rel_ts[t].copy_(env.rel_ts)
+                pobs = policy_obs(b.obs[t], b.depth[t], b.rel_ts[t])
+            else:
+                pobs = b.obs[t]
+            actions, values, logp = self.policy(pobs, generator=self.gen)
             b.actions[t].copy_(actions)
             b.values[t].copy_(values)
             b.log_probs[t].copy_(logp)
@@ -310,7 +344,8 @@ class BatchedPPO:
             self._last_obs = obs
             self._last_starts = done.to(torch.uint8)
         self.num_timesteps += self.n_envs * self.n_steps * self.world
-        last_v = self.policy.predict_values(self._last_obs)
+        last_v = self.policy.predict_values(
+            policy_obs(self._last_obs, env.depth, env.rel_ts) if self.cameras else self._last_obs)
         b.advantages, b.returns = self.gae_fn(b.rewards, b.values, b.starts, last_v.contiguous(),
                                               self._last_starts.contiguous(), self.gamma, self.gae_lambda)
         # finished episodes in time order (one host sync per rollout)
@@ -367,6 +402,11 @@ class BatchedPPO:
             cf = torch.mean((torch.abs(ratio - 1) > clip).float())
         return loss, pg.detach(), vf.detach(), ent.detach(), kl, cf
 
+    def _mb_obs(self, d: Dict[str, torch.Tensor], idx: torch.Tensor):
+        if "depth" in d:
+            return policy_obs(d["obs"][idx], d["depth"][idx], d["rel_ts"][idx])
+        return d["obs"][idx]
+
     def _update(self, d: Dict[str, torch.Tensor]) -> None:
         self.policy.train()
         lr = self.lr_schedule(self.progress_remaining)
@@ -400,8 +440,9 @@ class BatchedPPO:
                 perm = torch.randperm(n, generator=self.shuffle_gen, device=self.device)
                 for s in range(0, n, self.batch_size):
                     idx = perm[s:s + self.batch_size]
-                    loss, pg, vf, ent, kl, cf = self._loss(d["obs"][idx], d["actions"][idx], d["log_probs"][idx],
-                                                           d["advantages"][idx], d["returns"][idx], clip)
+                    loss, pg, vf, ent, kl, cf = self._loss(self._mb_obs(d, idx), d["actions"][idx],
+                                                           d["log_probs"][idx], d["advantages"][idx],
+                                                           d["returns"][idx], clip)
                     pg_l.append(pg); vf_l.append(vf); ent_l.append(ent); clip_f.append(cf)
                     approx_kl = float(kl)  # the early stop needs it before the step (host sync)
                     kls.append(approx_kl)

@@ -118,3 +118,25 @@ def test_graph_update_matches_eager(target_kl):
     la, lb = models[0].logger.values, models[1].logger.values
     for k in ("train/policy_gradient_loss", "train/value_loss", "train/approx_kl", "train/clip_fraction"):
         assert la[k] == pytest.approx(lb[k], rel=1e-4, abs=1e-7), k
+
+
+def test_batched_ppo_with_depth_cameras(tmp_path):
+    """rgbd_0/rgbd_1 + relative_image_timestamp through the Extractor's CNN branches
+    (mlp_policy.py:25-46): rollout images stored, graph update over dict observations."""
+    from ballbot_gym.envs import BallbotVecEnv
+    from ballbot_rl.training.logger import CSVLogger, read_progress
+    from ballbot_rl.training.ppo import BatchedPPO
+
+    env = BallbotVecEnv(256, device="cuda:0", max_ep_steps=10, seed=5, disable_cameras=False)
+    m = BatchedPPO(env, n_steps=8, batch_size=512, n_epochs=2, ent_coef=0.001, clip_range=0.015, vf_coef=2.0,
+                   target_kl=0.3, learning_rate=1e-4, normalize_advantage=False, seed=10,
+                   logger=CSVLogger(str(tmp_path), stdout=False))
+    assert m.policy.features_extractor.features_dim == 15 + 1 + 20 + 20
+    m.learn(total_timesteps=256 * 8 * 3)
+    assert m._graphs is not None and "depth" in m._graphs.data
+    assert float(m.buf.depth.min()) > 0 and float(m.buf.depth.max()) <= 1.0
+    ts = m.buf.rel_ts.cpu().numpy()
+    assert set(np.round(np.unique(ts) / 0.002).astype(int)) <= set(range(6))
+    cols = read_progress(str(tmp_path / "progress.csv"))
+    assert all(np.isfinite(x) for x in cols["train/loss"][1:])
+    env.close()
