@@ -10,8 +10,10 @@ seed, evaluation.*, env.*, problem.terrain/reward).  Differences, by design:
   thousands and lower n_steps (configs in tools/ppo_gpu.yaml);
 * the interactive overwrite/updates-per-rollout confirmations (train.py:194-266)
   become printed warnings -- a batch job cannot answer them;
-* checkpoints are safetensors (no pickled SB3 zip); cameras/frozen encoders
-   are not part of this trainer yet.
+* checkpoints are safetensors (no pickled SB3 zip); with a `camera` section the
+  depth cameras are on, as in the reference, and feed the Extractor's trainable
+  CNN branches -- the reference's pickled frozen encoder (`frozen_cnn`) is not
+  loaded.
 Output directory layout as the reference: outputs/experiments/runs/
 {timestamp}_{algo}_{terrain}_{reward}_seed{seed}/ with config.yaml, info.txt,
 progress.csv (SB3 columns), best_model.safetensors and final_model.safetensors.
@@ -65,9 +67,12 @@ def make_env(config: Dict[str, Any], num_envs: int, device, seed: int, precision
     from ballbot_gym.envs import BallbotVecEnv
 
     env_cfg = {"camera": config.get("camera", {}), "env": config.get("env", {}), "logging": config.get("logging", {})}
+    # the reference trains with its depth cameras on (make_ballbot_env(disable_cams=False),
+    # training/utils.py:11-20) whenever the config has a camera section
+    cams = bool(config.get("camera")) and not config.get("disable_cameras", False)
     return BallbotVecEnv(num_envs, device=device, reward_config=get_component_config(config, "reward"),
                          terrain_config=get_component_config(config, "terrain"), env_config=env_cfg, seed=seed,
-                         precision=precision, n_terrains=config.get("n_terrains"))
+                         precision=precision, n_terrains=config.get("n_terrains"), disable_cameras=not cams)
 
 
 def main(config: Dict[str, Any], seed: int, out: Optional[str] = None, total_timesteps: Optional[int] = None,

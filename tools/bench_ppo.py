@@ -34,6 +34,7 @@ def main():
     ap.add_argument("--lr", type=float, default=-1, help="-1: the reference's lr_schedule")
     ap.add_argument("--out", default=None)
     ap.add_argument("--seed", type=int, default=10)
+    ap.add_argument("--cameras", action="store_true", help="depth cameras on (rgbd policy branch)")
     a = ap.parse_args()
 
     import torch
@@ -44,7 +45,7 @@ def main():
     from ballbot_rl.training.schedules import lr_schedule
 
     env = BallbotVecEnv(a.envs, device="cuda:0", precision=a.precision, seed=a.seed,
-                        terrain_config={"type": a.terrain, "config": {}})
+                        terrain_config={"type": a.terrain, "config": {}}, disable_cameras=not a.cameras)
     m = BatchedPPO(env, n_steps=a.n_steps, batch_size=a.batch, n_epochs=a.epochs, ent_coef=0.001, clip_range=0.015,
                    vf_coef=2.0, target_kl=0.3, learning_rate=lr_schedule if a.lr == -1 else a.lr,
                    normalize_advantage=False, weight_decay=0.01, seed=a.seed,
@@ -79,7 +80,7 @@ def main():
            "unit": "env-steps/s", "timesteps": m.num_timesteps, "iterations": iters[0], "wall_s": el,
            "rollout_s": t_roll, "update_s": t_upd, "rollout_env_steps_per_s": m.num_timesteps / max(t_roll, 1e-9),
            "config": {"envs": a.envs, "n_steps": a.n_steps, "batch_size": a.batch, "n_epochs": a.epochs,
-                      "terrain": a.terrain, "precision": a.precision},
+                      "terrain": a.terrain, "precision": a.precision, "cameras": a.cameras},
            "ep_rew_mean": _eprew(m), "ep_len_mean": _eplen(m), "env_stats": env.stats()}
     print(json.dumps(out), flush=True)
     env.close()
