@@ -34,7 +34,7 @@ constexpr int HF_N = 293;        // ballbot.xml:23 nrow = ncol
 constexpr int MAXG = 50;         // ball-hfield contact cap: MuJoCo's mjMAXCONPAIR (== oracle BBO_MAXGROUND)
 constexpr int NH = NV * (NV + 1) / 2;
 constexpr int NGF = 4;           // fields per stored ground contact (see GF_* below)
-constexpr int MAXB = 16;         // base-tree geom contact cap (== oracle BBO_MAXBODY)
+constexpr int MAXB = 32;         // base-tree geom contact cap (== oracle BBO_MAXBODY)
 constexpr int NBF = 8;           // fields per stored base-tree contact (see BF_* below)
 // ground-contact store fields (compact: Jacobian, aref and D are rebuilt on
 // use by ground_contact): normal (hfield -> ball)[3], dist

@@ -36,7 +36,7 @@ extern "C" {
 #define BBO_NBODY 8
 #define BBO_HF_N 293          /* ballbot.xml:23 nrow = ncol = 293 */
 #define BBO_MAXGROUND 50      /* cap on ball-hfield contacts = MuJoCo mjMAXCONPAIR */
-#define BBO_MAXBODY 16        /* cap on base-tree geom contacts (hfield x tower/sticks/wheels, ball x tower/sticks) */
+#define BBO_MAXBODY 32        /* cap on base-tree geom contacts (hfield x tower/sticks/wheels, ball x tower/sticks) */
 #define BBO_MAXCON (3 + BBO_MAXGROUND + BBO_MAXBODY)
 
 /* option flags for invariant tests (0 = reference behaviour) */

@@ -35,9 +35,13 @@ def main():
     ap.add_argument("--out", default=None)
     ap.add_argument("--seed", type=int, default=10)
     ap.add_argument("--cameras", action="store_true", help="depth cameras on (rgbd policy branch)")
+    ap.add_argument("--conv-benchmark", action="store_true", help="MIOpen kernel search for the CNN")
     a = ap.parse_args()
 
     import torch
+
+    if a.conv_benchmark:
+        torch.backends.cudnn.benchmark = True
 
     from ballbot_gym.envs import BallbotVecEnv
     from ballbot_rl.training.logger import CSVLogger
