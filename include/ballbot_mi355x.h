@@ -13,6 +13,7 @@
  *   bb_step          ctrl = -clip(10a); mj_step; _get_obs;      ballbot_env.py:903-1036
  *                    reward plugin; termination
  *   bb_render_depth  RGBDInputs depth cams (_get_obs)           sensors/rgbd.py:46-82
+ *   bb_ppo_loss      SB3 PPO.train minibatch loss + grads
  *   bb_gae           SB3 RolloutBuffer.compute_returns_and_advantage (PPO)
  *   bb_forward       mujoco.mj_forward (diagnostic)             ballbot_env.py:525,620
  *   bb_get_state/    read/write qpos/qvel/qacc_warmstart        ballbot_env.py:616-617
@@ -40,7 +41,7 @@
 extern "C" {
 #endif
 
-#define BB_ABI_VERSION 6
+#define BB_ABI_VERSION 7
 #define BB_NQ 17
 #define BB_NV 15
 #define BB_OBS 15
@@ -121,6 +122,17 @@ int bb_gae(const float* rewards_dev, const float* values_dev, const uint8_t* epi
  * Enqueued on stream, after bb_step / bb_reset. */
 int bb_render_depth(bb_handle* h, float* depth_dev, float* rel_ts_dev, int height, int width, int every,
                     int force, void* stream);
+/* PPO update: fused minibatch loss of SB3 PPO.train (diagonal Gaussian,
+ * clipped surrogate, MSE value loss, entropy; ppo/ppo.py, called through
+ * model.learn at ballbot_rl/training/train.py:284) and its gradients.  All
+ * pointers are device float32: mean/actions [B][3], values/old_logp/adv/
+ * returns [B], log_std [3], clip (scalar).  Writes terms[9] = loss, pg, vf,
+ * entropy loss, approx_kl, clip_fraction, dloss/dlog_std[3], grad_mean [B][3],
+ * grad_values [B].  One workgroup, enqueued on stream; graph-capturable. */
+int bb_ppo_loss(const float* mean_dev, const float* values_dev, const float* log_std_dev, const float* actions_dev,
+                const float* old_logp_dev, const float* adv_dev, const float* returns_dev, const float* clip_dev,
+                int B, int normalize_advantage, float ent_coef, float vf_coef, float* terms_dev,
+                float* grad_mean_dev, float* grad_values_dev, void* stream);
 /* copy terrain bank slot terrain_id (float32[293*293]) to host memory */
 int bb_get_hfield(bb_handle* h, int terrain_id, float* data_host);
 /* per-env terrain ids (device int32[n]) applied at the next reset */

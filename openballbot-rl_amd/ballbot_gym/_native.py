@@ -58,16 +58,16 @@ EXPORTS = [
     "bb_abi_version", "bb_last_error", "bb_default_params", "bb_create", "bb_destroy", "bb_set_hfield",
     "bb_assign_terrain", "bb_reset", "bb_step", "bb_get_state", "bb_set_state", "bb_forward", "bb_get_stats",
     "bb_get_offsets", "bb_get_config", "bb_time_kernel", "bb_kernel_ms", "bb_generate_perlin", "bb_get_hfield",
-    "bb_gae", "bb_render_depth",
+    "bb_gae", "bb_render_depth", "bb_ppo_loss",
 ]
 
-ABI_VERSION = 6  # include/ballbot_mi355x.h BB_ABI_VERSION
+ABI_VERSION = 7  # include/ballbot_mi355x.h BB_ABI_VERSION
 
 _lib = None
 
 
 def build(force: bool = False, verbose: bool = False) -> Path:
-    """Compile csrc/bb_kernels.hip + bb_terrain.hip + bb_rollout.hip + bb_render.hip for gfx950 into _lib/libbb_mi355x.so."""
+    """Compile csrc/bb_kernels.hip + bb_terrain.hip + bb_rollout.hip + bb_render.hip + bb_ppo.hip for gfx950 into _lib/libbb_mi355x.so."""
     import subprocess
 
     srcs = list(CSRC.glob("*.h")) + list(CSRC.glob("*.hip")) + list(INCLUDE.glob("*.h"))
@@ -77,7 +77,8 @@ def build(force: bool = False, verbose: bool = False) -> Path:
     tmp = LIB_PATH.with_suffix(".so.tmp")
     cmd = ["hipcc", "--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC", "-shared",
            "-o", str(tmp), str(CSRC / "bb_kernels.hip"), str(CSRC / "bb_terrain.hip"),
-           str(CSRC / "bb_rollout.hip"), str(CSRC / "bb_render.hip")]
+           str(CSRC / "bb_rollout.hip"), str(CSRC / "bb_render.hip"),
+           str(CSRC / "bb_ppo.hip")]
     if verbose:
         print(" ".join(cmd))
     subprocess.run(cmd, check=True)
@@ -128,6 +129,7 @@ def _load(path: Path):
     L.bb_generate_perlin.argtypes = [vp, C.c_int, C.c_int, C.POINTER(C.c_int32), C.POINTER(PerlinCfg), C.c_float]
     L.bb_get_hfield.argtypes = [vp, C.c_int, fp]
     L.bb_render_depth.argtypes = [vp, vp, vp, C.c_int, C.c_int, C.c_int, C.c_int, vp]
+    L.bb_ppo_loss.argtypes = [vp] * 8 + [C.c_int, C.c_int, C.c_float, C.c_float, vp, vp, vp, vp]
     L.bb_gae.argtypes = [vp, vp, vp, vp, vp, C.c_int, C.c_int, C.c_double, C.c_double, vp, vp, vp]
     L.bb_kernel_ms.argtypes = [vp, C.POINTER(C.c_double), C.POINTER(C.c_int32)]
     for name in [n for n in EXPORTS if n not in ("bb_default_params", "bb_abi_version")]:

@@ -70,6 +70,35 @@ def gae_hip(rewards, values, episode_starts, last_values, last_dones, gamma: flo
     return adv, ret
 
 
+class _PPOLossHIP(torch.autograd.Function):
+    """bb_ppo_loss: the SB3 minibatch loss and its gradients in one HIP launch.
+
+    forward -> (loss, pg, vf, ent, approx_kl, clip_fraction); backward scales the
+    gradients the kernel already wrote (d loss / d mean, values, log_std)."""
+
+    @staticmethod
+    def forward(ctx, mean, values, log_std, actions, old_logp, adv, ret, clip_t, normalize, ent_coef, vf_coef):
+        from ballbot_gym import _native as N
+
+        B = mean.shape[0]
+        terms = torch.empty(9, device=mean.device, dtype=torch.float32)
+        gmean = torch.empty_like(mean)
+        gval = torch.empty_like(values)
+        ts = [t.contiguous() for t in (mean, values, log_std, actions, old_logp, adv, ret, clip_t)]
+        stream = C.c_void_p(torch.cuda.current_stream(mean.device).cuda_stream)
+        N.check(N.lib().bb_ppo_loss(*[_ptr(t) for t in ts], int(B), int(normalize), float(ent_coef),
+                                    float(vf_coef), _ptr(terms), _ptr(gmean), _ptr(gval), stream), "bb_ppo_loss")
+        ctx.save_for_backward(gmean, gval, terms)
+        aux = terms[1:6].clone()
+        ctx.mark_non_differentiable(aux)
+        return terms[0].clone(), aux
+
+    @staticmethod
+    def backward(ctx, g_loss, _g_terms):
+        gmean, gval, terms = ctx.saved_tensors
+        return (g_loss * gmean, g_loss * gval, g_loss * terms[6:9], None, None, None, None, None, None, None, None)
+
+
 def explained_variance(y_pred: torch.Tensor, y_true: torch.Tensor) -> float:
     """SB3 common.utils.explained_variance: 1 - Var[y - y_pred] / Var[y] (nan if Var[y] == 0)."""
     var_y = torch.var(y_true, unbiased=False)
@@ -387,7 +416,16 @@ class BatchedPPO:
         self._sync_params()
 
     def _loss(self, obs, act, old_logp, adv, ret, clip):
-        """One minibatch of SB3 PPO.train: -> (loss, pg, vf, ent, approx_kl, clip_fraction)."""
+        """One minibatch of SB3 PPO.train: -> (loss, pg, vf, ent, approx_kl, clip_fraction).
+
+        On the GPU the loss and its gradients are one bb_ppo_loss launch; the
+        torch expression below is the CPU stand-in path of the host tests."""
+        if self.device.type == "cuda":
+            mean, values = self.policy._heads(obs)
+            clip_t = clip if isinstance(clip, torch.Tensor) else torch.tensor(float(clip), device=self.device)
+            loss, t = _PPOLossHIP.apply(mean, values, self.policy.log_std, act, old_logp, adv, ret, clip_t,
+                                        self.normalize_advantage, self.ent_coef, self.vf_coef)
+            return loss, t[0], t[1], t[2], t[3], t[4]
         values, logp, entropy = self.policy.evaluate_actions(obs, act)
         if self.normalize_advantage and adv.shape[0] > 1:
             adv = (adv - adv.mean()) / (adv.std() + 1e-8)

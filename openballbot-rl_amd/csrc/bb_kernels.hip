@@ -24,6 +24,7 @@
 #include "bb_terrain.h"
 #include "bb_rollout.h"
 #include "bb_render.h"
+#include "bb_ppo.h"
 
 using namespace bb;
 
@@ -650,6 +651,20 @@ int bb_render_depth(bb_handle* h, float* depth, float* rel_ts, int height, int w
   if (launch_depth(h->fp64 != 0, h->mf, h->rig, rd, height, width, every, force, 0.002f, h->scenes, depth, rel_ts,
                    (hipStream_t)stream))
     return fail("bb_render_depth: launch failed: %s", hipGetErrorString(hipGetLastError()));
+  return 0;
+}
+
+int bb_ppo_loss(const float* mean, const float* values, const float* log_std, const float* actions,
+                const float* old_logp, const float* adv, const float* returns, const float* clip, int B, int normalize,
+                float ent_coef, float vf_coef, float* terms, float* grad_mean, float* grad_values, void* stream) {
+  if (!mean || !values || !log_std || !actions || !old_logp || !adv || !returns || !clip || !terms || !grad_mean ||
+      !grad_values)
+    return fail("bb_ppo_loss: NULL argument");
+  if (B < 1) return fail("bb_ppo_loss: B must be >= 1 (got %d)", B);
+  PPOLossArgs a{mean, values, log_std, actions, old_logp, adv, returns, clip, B, normalize ? 1 : 0, ent_coef, vf_coef,
+                terms, grad_mean, grad_values};
+  if (launch_ppo_loss(a, (hipStream_t)stream))
+    return fail("bb_ppo_loss: launch failed: %s", hipGetErrorString(hipGetLastError()));
   return 0;
 }
 

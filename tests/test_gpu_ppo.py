@@ -140,3 +140,48 @@ def test_batched_ppo_with_depth_cameras(tmp_path):
     cols = read_progress(str(tmp_path / "progress.csv"))
     assert all(np.isfinite(x) for x in cols["train/loss"][1:])
     env.close()
+
+
+@pytest.mark.parametrize("normalize", [False, True])
+def test_fused_ppo_loss_matches_torch(normalize):
+    """bb_ppo_loss (loss terms + gradients) vs the torch expression of SB3 PPO.train."""
+    from ballbot_rl.training.ppo import _PPOLossHIP
+
+    dev = torch.device("cuda:0")
+    g = torch.Generator(device="cpu").manual_seed(3)
+    B = 8192
+    mean = torch.randn(B, 3, generator=g).to(dev).requires_grad_()
+    values = torch.randn(B, generator=g).to(dev).requires_grad_()
+    log_std = (0.3 * torch.randn(3, generator=g)).to(dev).requires_grad_()
+    actions = torch.randn(B, 3, generator=g).to(dev)
+    adv = torch.randn(B, generator=g).to(dev)
+    ret = torch.randn(B, generator=g).to(dev)
+    with torch.no_grad():  # old log-probs: exact ties (rho = 1) on a third, far off on a third
+        lp = torch.distributions.Normal(mean, torch.exp(log_std)).log_prob(actions).sum(-1)
+        old = lp.clone()
+        old[B // 3:2 * B // 3] += 0.5 * torch.randn(B // 3 + (2 * B // 3 - B // 3 - B // 3), generator=g).to(dev)
+        old[2 * B // 3:] += 0.01 * torch.randn(B - 2 * B // 3, generator=g).to(dev)
+    clip, ent_coef, vf_coef = 0.015, 0.001, 2.0
+
+    def ref(mean, values, log_std):
+        lp = torch.distributions.Normal(mean, torch.exp(log_std)).log_prob(actions).sum(-1)
+        ent = torch.distributions.Normal(mean, torch.exp(log_std)).entropy().sum(-1)
+        a = (adv - adv.mean()) / (adv.std() + 1e-8) if normalize else adv
+        lr = lp - old
+        r = torch.exp(lr)
+        pg = -torch.min(a * r, a * torch.clamp(r, 1 - clip, 1 + clip)).mean()
+        vf = torch.nn.functional.mse_loss(ret, values)
+        el = -torch.mean(ent)
+        return pg + ent_coef * el + vf_coef * vf, pg, vf, el, torch.mean((r - 1) - lr), \
+            torch.mean((torch.abs(r - 1) > clip).float())
+
+    lref, *tref = ref(mean, values, log_std)
+    gref = torch.autograd.grad(lref, (mean, values, log_std))
+    loss, t = _PPOLossHIP.apply(mean, values, log_std, actions, old, adv, ret, torch.tensor(clip, device=dev),
+                                normalize, ent_coef, vf_coef)
+    got = torch.autograd.grad(loss, (mean, values, log_std))
+    assert torch.allclose(loss, lref, rtol=1e-5, atol=1e-6)
+    for a, b in zip(t, tref):
+        assert torch.allclose(a, b.float(), rtol=1e-4, atol=1e-6), (a, b)
+    for a, b in zip(got, gref):
+        assert torch.allclose(a, b, rtol=1e-4, atol=1e-7), (a - b).abs().max()

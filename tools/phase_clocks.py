@@ -29,7 +29,7 @@ def main():
         LIB.parent.mkdir(parents=True, exist_ok=True)
         subprocess.run(["hipcc", "--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC", "-shared", "-DBB_PHASE_CLOCKS",
                         "-o", str(LIB)] + [str(ROOT / "openballbot-rl_amd" / "csrc" / f) for f in
-                                           ("bb_kernels.hip", "bb_terrain.hip", "bb_rollout.hip", "bb_render.hip")],
+                                           ("bb_kernels.hip", "bb_terrain.hip", "bb_rollout.hip", "bb_render.hip", "bb_ppo.hip")],
                        check=True)
     import torch
     from ballbot_gym import _native
