@@ -18,6 +18,7 @@ concatenating the dict is the identity on it).
 """
 from __future__ import annotations
 
+import copy
 import math
 from collections import OrderedDict
 from typing import Dict, Optional, Sequence, Tuple, Union
@@ -65,10 +66,11 @@ class Extractor(nn.Module):
                     C, H, W = shape
                     ex[key] = depth_cnn(C, H, W)
                     total += 20
-                else:
-                    ex[key] = frozen_encoder
-                    total += [m for m in frozen_encoder.modules() if isinstance(m, nn.Linear)][-1].out_features
-                    for p in frozen_encoder.parameters():
+                else:  # one copy per camera key, as the reference loads it once per key (mlp_policy.py:51-54)
+                    enc = copy.deepcopy(frozen_encoder)
+                    ex[key] = enc
+                    total += [m for m in enc.modules() if isinstance(m, nn.Linear)][-1].out_features
+                    for p in enc.parameters():
                         p.requires_grad = False
             else:
                 ex[key] = nn.Flatten()

@@ -286,7 +286,7 @@ class BatchedPPO:
                  net_arch: Optional[Dict[str, Any]] = None, activation_fn=nn.LeakyReLU, seed: int = 0,
                  logger: Optional[CSVLogger] = None, stats_window_size: int = 100,
                  gae_fn: Callable = gae_hip, policy: Optional[ActorCriticPolicy] = None,
-                 use_graphs: Optional[bool] = None):
+                 use_graphs: Optional[bool] = None, frozen_encoder: Optional[nn.Module] = None):
         self.env = env
         self.device = torch.device(env.device)
         self.n_envs = int(env.num_envs)
@@ -304,7 +304,8 @@ class BatchedPPO:
         self.cameras = bool(getattr(env, "cameras", False))
         img = (2, env.cam_h, env.cam_w) if self.cameras else None
         spaces = obs_spaces(cameras=True, height=env.cam_h, width=env.cam_w) if self.cameras else obs_spaces()
-        self.policy = (policy or ActorCriticPolicy(spaces, 3, net_arch, activation_fn)).to(self.device)
+        self.policy = (policy or ActorCriticPolicy(spaces, 3, net_arch, activation_fn,
+                                                   frozen_encoder=frozen_encoder)).to(self.device)
         self._sync_params()
         # full-size minibatches replay one HIP graph (forward+backward, clip+AdamW);
         # AdamW is then 'capturable' with its learning rate in a device tensor

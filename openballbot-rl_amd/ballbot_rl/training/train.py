@@ -11,9 +11,10 @@ seed, evaluation.*, env.*, problem.terrain/reward).  Differences, by design:
 * the interactive overwrite/updates-per-rollout confirmations (train.py:194-266)
   become printed warnings -- a batch job cannot answer them;
 * checkpoints are safetensors (no pickled SB3 zip); with a `camera` section the
-  depth cameras are on, as in the reference, and feed the Extractor's trainable
-  CNN branches -- the reference's pickled frozen encoder (`frozen_cnn`) is not
-  loaded.
+  depth cameras are on, as in the reference; `frozen_cnn` names an encoder
+  pretrained by ballbot_rl.encoders.pretrain (safetensors) -- the reference's
+  pickled encoder files are never loaded -- else the rgbd
+  branches are the Extractor's trainable CNNs.
 Output directory layout as the reference: outputs/experiments/runs/
 {timestamp}_{algo}_{terrain}_{reward}_seed{seed}/ with config.yaml, info.txt,
 progress.csv (SB3 columns), best_model.safetensors and final_model.safetensors.
@@ -110,7 +111,16 @@ def main(config: Dict[str, Any], seed: int, out: Optional[str] = None, total_tim
         upd = config["algo"]["n_epochs"] * n_total * config["algo"]["n_steps"] / config["algo"]["batch_sz"]
         print(f"{upd:.1f} gradient updates per rollout (n_epochs x num_envs x n_steps / batch_sz)")
 
-    model = BatchedPPO(env, seed=seed, logger=logger, **ppo_kwargs(config))
+    frozen = None
+    fc = str(config.get("frozen_cnn") or "")
+    if env.cameras and fc.endswith(".safetensors") and Path(fc).exists():
+        from ballbot_rl.encoders import load_frozen_encoder
+
+        frozen = load_frozen_encoder(fc, device=dev)  # the reference's frozen_cnn (train.py:45-47)
+    elif env.cameras and fc and rank == 0:
+        print(f"warning: frozen_cnn {fc!r} is not a safetensors encoder (pickled modules are not loaded); "
+              "the rgbd branches train from scratch")
+    model = BatchedPPO(env, seed=seed, logger=logger, frozen_encoder=frozen, **ppo_kwargs(config))
     if config.get("resume"):
         model.load_policy(config["resume"])
     eval_freq = int(eval_cfg.get("freq", 5000))

@@ -185,3 +185,25 @@ def test_fused_ppo_loss_matches_torch(normalize):
         assert torch.allclose(a, b.float(), rtol=1e-4, atol=1e-6), (a, b)
     for a, b in zip(got, gref):
         assert torch.allclose(a, b, rtol=1e-4, atol=1e-7), (a - b).abs().max()
+
+
+def test_encoder_pretrain_on_gpu_frames(tmp_path):
+    """Depth frames straight from the GPU cameras -> TinyAutoencoder -> frozen encoder in PPO."""
+    from ballbot_gym.envs import BallbotVecEnv
+    from ballbot_rl.encoders import TinyAutoencoder, collect_depth_images, load_frozen_encoder, train_autoencoder
+    from ballbot_rl.training.ppo import BatchedPPO
+
+    env = BallbotVecEnv(256, device="cuda:0", terrain_config={"type": "perlin", "config": {}}, n_terrains=4,
+                        disable_cameras=False, seed=1)
+    imgs = collect_depth_images(env, 4000, seed=1)
+    assert imgs.shape == (4000, 1, 64, 64) and float(imgs.max()) <= 1.0 and float(imgs.min()) > 0
+    path = str(tmp_path / "enc.safetensors")
+    h = train_autoencoder(TinyAutoencoder(64, 64), imgs, epochs=3, batch_size=256, save_path=path,
+                          log=lambda *_: None)
+    assert h["best_val_loss"] < 0.05
+    enc = load_frozen_encoder(path, device="cuda:0")
+    m = BatchedPPO(env, n_steps=8, batch_size=512, n_epochs=1, learning_rate=1e-4, seed=2, frozen_encoder=enc)
+    w0 = m.policy.features_extractor.extractors["rgbd_0"][0].weight.clone()
+    m.learn(total_timesteps=256 * 8 * 2)
+    assert torch.equal(w0, m.policy.features_extractor.extractors["rgbd_0"][0].weight)  # frozen
+    env.close()

@@ -160,3 +160,31 @@ def test_training_config_loader(tmp_path):
         load_training_config(str(tmp_path / "train" / "bad.yaml"))
     with pytest.raises(ValueError, match="must have 'type'"):
         get_component_config({"reward": {"config": {}}}, "reward")
+
+
+def test_encoder_roundtrip_and_frozen_extractor(tmp_path):
+    """TinyAutoencoder (reference encoders/models.py) shapes, safetensors save/load with
+    the p_sum check, and the frozen copies inside the Extractor."""
+    from ballbot_rl.encoders import TinyAutoencoder, load_frozen_encoder, save_encoder
+    from ballbot_rl.encoders.pretrain import train_autoencoder
+    from ballbot_rl.policies import ActorCriticPolicy, obs_spaces
+
+    torch.manual_seed(0)
+    imgs = torch.rand(96, 1, 64, 64)
+    ae = TinyAutoencoder(64, 64)
+    assert ae(imgs[:4]).shape == (4, 1, 64, 64)
+    path = str(tmp_path / "enc.safetensors")
+    hist = train_autoencoder(ae, imgs, epochs=2, batch_size=32, save_path=path, log=lambda *_: None)
+    assert np.isfinite(hist["best_val_loss"])
+    enc = load_frozen_encoder(path)
+    assert not any(p.requires_grad for p in enc.parameters())
+    pol = ActorCriticPolicy(obs_spaces(cameras=True), frozen_encoder=enc)
+    e0, e1 = pol.features_extractor.extractors["rgbd_0"], pol.features_extractor.extractors["rgbd_1"]
+    assert e0 is not e1 and torch.equal(e0[0].weight, enc[0].weight)  # untouched by the orthogonal init
+    assert pol.features_extractor.features_dim == 56
+    import json
+    meta = json.loads(open(path + ".json").read())
+    meta["p_sum"] += 1.0
+    open(path + ".json", "w").write(json.dumps(meta))
+    with pytest.raises(ValueError, match="corrupted"):
+        load_frozen_encoder(path)
