@@ -154,6 +154,28 @@ class BallbotVecEnv:
             reward = reward + self._host_reward_batch()
         return self.obs, reward, terminated, torch.zeros_like(terminated), info
 
+    def capture_step(self, actions: torch.Tensor) -> "torch.cuda.CUDAGraph":
+        """Capture one env.step (routing, fast/full step kernels on the env's two
+        streams, depth cameras) reading `actions` as ONE HIP graph; replay() then
+        steps every env with whatever `actions` holds (one launch per rollout step)."""
+        if actions.shape != (self.num_envs, 3) or actions.dtype != torch.float32 or not actions.is_contiguous():
+            raise ValueError("capture_step needs a contiguous float32 [num_envs, 3] action buffer")
+        graph = torch.cuda.CUDAGraph()
+        side = torch.cuda.Stream(device=self.device)
+        side.wait_stream(torch.cuda.current_stream(self.device))
+        torch.cuda.synchronize(self.device)
+        with torch.cuda.graph(graph, stream=side):
+            self._step_launch(actions)
+        torch.cuda.synchronize(self.device)
+        return graph
+
+    def _step_launch(self, actions: torch.Tensor) -> None:
+        N.check(N.lib().bb_step(self._h, _ptr(actions), _ptr(self.obs), _ptr(self.reward), _ptr(self.done),
+                                _ptr(self.terminal_obs), _ptr(self.pos2d), int(self.auto_reset), self._stream()),
+                "bb_step")
+        if self.cameras:
+            self._render(force=False)
+
     def step_async_raw(self, actions: torch.Tensor) -> None:
         """Launch-only step (graph capture / benchmarking): no derived tensors."""
         N.lib().bb_step(self._h, _ptr(actions), _ptr(self.obs), _ptr(self.reward), _ptr(self.done),

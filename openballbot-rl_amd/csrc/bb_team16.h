@@ -369,6 +369,9 @@ __device__ int solve16(const ModelT<T>& m, EnvWork<T>& W, int ng, int nb, T* a, 
     int side = 0, same = 0;
     bool ls_ok = false;
     for (int ls = 1; ls <= m.ls_maxiter; ls++) {
+#if defined(BB_PHASE_CLOCKS) && defined(__HIP_DEVICE_COMPILE__)
+      if (tl == 0) atomicAdd(&bb_phase_cycles[11], 1ull);  // line-search evaluations
+#endif
       T d1p = 0, d2p = 0, dmp = 0;
       for (int c = tl; c < nc; c += L) {
         T c6[6], Dc;

@@ -204,3 +204,32 @@ def test_step_parity_base_tree_contacts(oracle, terrain):
         assert np.abs(v[e] - ve).max() < 1e-6 * max(1.0, np.abs(ve).max()), e
         assert np.abs(obs.cpu().numpy()[e] - o).max() < 1e-6, e
     env.close()
+
+
+@pytest.mark.parametrize("cameras", [False, True])
+def test_step_as_hip_graph(cameras):
+    """One rollout step (route + fast/full step kernels on two streams + depth cameras)
+    captured as a single HIP graph and replayed == eager stepping, bit for bit."""
+    from ballbot_gym.envs import BallbotVecEnv
+
+    n = 512
+    envs = [BallbotVecEnv(n, device="cuda:0", seed=4, disable_cameras=not cameras,
+                          terrain_config={"type": "perlin", "config": {}}, n_terrains=8) for _ in range(2)]
+    g = torch.Generator(device="cuda:0").manual_seed(0)
+    acts = torch.rand(20, n, 3, generator=g, device="cuda:0") * 2 - 1
+    static_a = torch.zeros(n, 3, device="cuda:0")
+    e_eager, e_graph = envs
+    graph = e_graph.capture_step(static_a)
+    for t in range(20):
+        e_eager.step(acts[t])
+        static_a.copy_(acts[t])
+        graph.replay()
+    torch.cuda.synchronize()
+    qa, va, wa, sa = e_eager.get_state()
+    qb, vb, wb, sb = e_graph.get_state()
+    assert np.array_equal(qa, qb) and np.array_equal(va, vb) and np.array_equal(sa, sb)
+    assert torch.equal(e_eager.obs, e_graph.obs) and torch.equal(e_eager.reward, e_graph.reward)
+    if cameras:
+        assert torch.equal(e_eager.depth, e_graph.depth)
+    for e in envs:
+        e.close()

@@ -56,6 +56,7 @@ def main():
            "cycles_per_forward": {NAMES[k]: out[k] / fw for k in range(10)},
            "cycles_per_newton_iter": {NAMES[k]: out[k] / max(iters, 1) for k in range(8)}}
     res["total_cycles_per_forward"] = sum(out[k] for k in range(10)) / fw
+    res["line_search_evals_per_newton_iter"] = out[11] / max(iters, 1)
     print(json.dumps(res, indent=1))
 
 
