@@ -82,6 +82,8 @@ def main() -> None:
     ap.add_argument("--n-terrains", type=int, default=None,
                     help="terrain bank size (default: 16 host-generated seeds; perlin: the whole 10^4 seed space on the GPU)")
     ap.add_argument("--cameras", action="store_true", help="also render the depth cameras (F2) every 6 steps")
+    ap.add_argument("--graph", action="store_true",
+                    help="replay the step as one HIP graph (kernel_ms is then timed on eager steps after the run)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
     ap.add_argument("--traffic-json", default=str(ROOT / "profiles" / "traffic.json"))
@@ -109,7 +111,14 @@ def main() -> None:
                         terrain_config={"type": args.terrain, "config": {}}, n_terrains=args.n_terrains,
                         disable_cameras=not args.cameras)
 
+    static_a = torch.zeros(n, 3, device=dev)
+    graph = env.capture_step(static_a) if args.graph else None  # one rollout step = one HIP graph
+
     def step(a):
+        if graph is not None:
+            static_a.copy_(a)
+            graph.replay()
+            return
         env.step_async_raw(a)
         if args.cameras:
             env._render(force=False)
@@ -134,6 +143,11 @@ def main() -> None:
     torch.cuda.synchronize()
     elapsed = time.perf_counter() - t0
     step_ms = ev0.elapsed_time(ev1) / args.steps  # whole bb_step sequence per step, torch's stream
+    if graph is not None:  # graph replays carry no per-kernel events: time eager steps of the same kernels
+        env.time_kernel(min(args.steps, 100))
+        for i in range(min(args.steps, 100)):
+            env.step_async_raw(pool[i % 64])
+        torch.cuda.synchronize()
     kern_ms, kern_n = env.kernel_ms()  # dominant kernel alone
     elapsed = max_over_ranks(elapsed, device=dev)
     stats = env.stats()
@@ -169,6 +183,7 @@ def main() -> None:
             "config": {"workload": f"{n} envs/GPU, {args.terrain} terrain, random actions "
                                    f"(BASELINE configs[{1 if args.terrain == 'flat' else 2}])",
                        "n_terrains": env.n_terrains, "depth_cameras": bool(args.cameras),
+                       "hip_graph": graph is not None,
                        "envs_per_gpu": n, "total_envs": n * world, "precision": args.precision,
                        "parallelism": f"env-sharded x{world} (no collective on the step path)",
                        "launch": launch},
