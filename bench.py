@@ -34,15 +34,15 @@ def algorithmic_bytes(precision: str) -> int:
     return 2 * state + 12 + 60 + 4 + 1 + 8 + 4  # r/w state, action, obs, reward, done, step r/w, terrain id
 
 
-def cpu_baseline(seconds: float = 12.0) -> dict:
+def cpu_baseline(seconds: float = 12.0, threads: int = 1) -> dict:
     """The fp64 oracle (a port of the reference step semantics, not MuJoCo) on
-    one host core, 32 envs with random actions, flat terrain."""
+    `threads` host cores (one env per OpenMP thread), random actions, flat terrain."""
     import numpy as np
 
     import oracle_lib as O
 
     O.build()
-    n = 32
+    n = 32 * threads
     cfg = O.default_cfg()
     hf = O.flat_hfield()
     off = O.init_offset(hf)
@@ -55,7 +55,7 @@ def cpu_baseline(seconds: float = 12.0) -> dict:
     t0 = time.perf_counter()
     while time.perf_counter() - t0 < seconds:
         a = rng.uniform(-1, 1, (n, 3)).astype(np.float32)
-        O.env_step_batch(cfg, q, v, w, steps, a, hf, 2.0, off)
+        O.env_step_batch(cfg, q, v, w, steps, a, hf, 2.0, off, threads=threads)
         done_steps += n
     dt = time.perf_counter() - t0
     cpu = platform.processor() or platform.machine()
@@ -66,8 +66,8 @@ def cpu_baseline(seconds: float = 12.0) -> dict:
                 break
     except OSError:
         pass
-    return {"value": done_steps / dt, "unit": "env-steps/s", "cores": 1, "kind": "port",
-            "sample": f"{n} envs x {done_steps // n} steps, flat, random actions, 1 thread on '{cpu}' "
+    return {"value": done_steps / dt, "unit": "env-steps/s", "cores": threads, "kind": "port",
+            "sample": f"{n} envs x {done_steps // n} steps, flat, random actions, {threads} thread(s) on '{cpu}' "
                       f"(fp64 oracle restating the reference step; MuJoCo itself is not available)"}
 
 
@@ -197,6 +197,10 @@ def main() -> None:
         }
         if world == 1 and not args.no_cpu_baseline:
             line["cpu_baseline"] = cpu_baseline(args.cpu_seconds)
+            # all host cores granted to this job (OMP_NUM_THREADS; 16 on the GPU box)
+            thr = int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or min(16, os.cpu_count() or 1)
+            if thr > 1:
+                line["cpu_baseline_multicore"] = cpu_baseline(args.cpu_seconds / 2, threads=thr)
         print(json.dumps(line), flush=True)
     env.close()
     if world > 1:

@@ -1597,6 +1597,28 @@ int bbo_env_step_batch(const bbo_env_cfg* cfg, int n, double* qpos, double* qvel
   return nd;
 }
 
+/* the same, one env per OpenMP thread (independent envs; the CPU baseline on
+ * all granted host cores) */
+int bbo_env_step_batch_mt(const bbo_env_cfg* cfg, int n, double* qpos, double* qvel, double* warm,
+                          int* step_counter, const float* actions, const float* hfield, double size_z,
+                          float* obs, float* reward, unsigned char* done, double offset, int threads) {
+  compile_model(); /* once, before the threads share the model */
+  int nd = 0;
+#pragma omp parallel for num_threads(threads) schedule(dynamic, 4) reduction(+ : nd)
+  for (int e = 0; e < n; e++) {
+    double* q = qpos + e * NQ; double* v = qvel + e * NV; double* w = warm + e * NV;
+    int f = bbo_env_step(cfg, q, v, w, step_counter + e, actions + 3 * e, hfield, size_z, obs + 15 * e,
+                         reward + e, NULL, NULL);
+    done[e] = (unsigned char)(f & 7);
+    if (f & 5) {
+      bbo_reset_state(offset, q, v, w);
+      step_counter[e] = 0;
+      nd++;
+    }
+  }
+  return nd;
+}
+
 /* ------------------------------------------------------------ depth cameras
  * Restates what RGBDInputs (sensors/rgbd.py:46-82) reads from MuJoCo's
  * renderer for cam_0 / cam_1 (ballbot.xml:44-54): the linear eye-space depth

@@ -121,6 +121,11 @@ int bbo_env_step_batch(const bbo_env_cfg* cfg, int n, double* qpos, double* qvel
                        const float* hfield, double size_z, float* obs,
                        float* reward, unsigned char* done, double offset);
 
+/* bbo_env_step_batch with one env per OpenMP thread (threads >= 1). */
+int bbo_env_step_batch_mt(const bbo_env_cfg* cfg, int n, double* qpos, double* qvel, double* warm,
+                          int* step_counter, const float* actions, const float* hfield, double size_z,
+                          float* obs, float* reward, unsigned char* done, double offset, int threads);
+
 #ifdef __cplusplus
 }
 #endif

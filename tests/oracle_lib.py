@@ -100,6 +100,8 @@ def lib():
         L.bbo_env_step_batch.argtypes = [C.POINTER(EnvCfg), C.c_int, dp, dp, dp, ip, fp, fp, C.c_double,
                                          fp, fp, C.POINTER(C.c_ubyte), C.c_double]
         L.bbo_env_step_batch.restype = C.c_int
+        L.bbo_env_step_batch_mt.argtypes = L.bbo_env_step_batch.argtypes + [C.c_int]
+        L.bbo_env_step_batch_mt.restype = C.c_int
         L.bbo_render_depth.argtypes = [dp, fp, C.c_double, C.c_int, C.c_int, C.c_int, fp]
         _lib = L
     return _lib
@@ -203,14 +205,18 @@ def quat_to_rotvec(q) -> np.ndarray:
     return rv
 
 
-def env_step_batch(cfg, qpos, qvel, warm, steps, actions, hfield, size_z, offset):
+def env_step_batch(cfg, qpos, qvel, warm, steps, actions, hfield, size_z, offset, threads=1):
+    """Step n envs on the CPU (threads > 1: one env per OpenMP thread)."""
     n = qpos.shape[0]
     obs = np.zeros((n, 15), dtype=np.float32)
     rew = np.zeros(n, dtype=np.float32)
     done = np.zeros(n, dtype=np.uint8)
     hf = np.ascontiguousarray(hfield, dtype=np.float32)
     a = np.ascontiguousarray(actions, dtype=np.float32)
-    lib().bbo_env_step_batch(C.byref(cfg), n, _d(qpos), _d(qvel), _d(warm),
-                             steps.ctypes.data_as(C.POINTER(C.c_int)), _f(a), _f(hf), size_z, _f(obs), _f(rew),
-                             done.ctypes.data_as(C.POINTER(C.c_ubyte)), offset)
+    args = (C.byref(cfg), n, _d(qpos), _d(qvel), _d(warm), steps.ctypes.data_as(C.POINTER(C.c_int)), _f(a), _f(hf),
+            size_z, _f(obs), _f(rew), done.ctypes.data_as(C.POINTER(C.c_ubyte)), offset)
+    if threads > 1:
+        lib().bbo_env_step_batch_mt(*args, int(threads))
+    else:
+        lib().bbo_env_step_batch(*args)
     return obs, rew, done

@@ -303,3 +303,24 @@ def test_depth_camera_sees_ball_and_culls_inside(oracle):
     d0_far = oracle.render_depth(np.r_[q[:10], q[10] + 3.0, q[11:]], oracle.flat_hfield(), 0)  # ball moved away
     assert (d0 <= d0_far + 1e-6).all() and (d0 < d0_far - 1e-3).sum() > 50
     assert d0.min() > 0.005  # the 1 cm stick capsule around the camera origin is not drawn
+
+
+def test_openmp_batch_equals_serial(oracle):
+    """bbo_env_step_batch_mt (the multi-core CPU baseline) == the serial batch, bit for bit."""
+    n = 16
+    cfg = oracle.default_cfg()
+    hf = oracle.flat_hfield()
+    off = oracle.init_offset(hf)
+    rng = np.random.default_rng(2)
+    states = []
+    for threads in (1, 4):
+        q = np.zeros((n, 17)); v = np.zeros((n, 15)); w = np.zeros((n, 15))
+        for e in range(n):
+            q[e], v[e], w[e] = oracle.reset_state(off)
+        st = np.zeros(n, np.int32)
+        rr = np.random.default_rng(2)
+        for _ in range(5):
+            oracle.env_step_batch(cfg, q, v, w, st, rr.uniform(-1, 1, (n, 3)).astype(np.float32), hf, 2.0, off,
+                                  threads=threads)
+        states.append((q.copy(), v.copy()))
+    assert np.array_equal(states[0][0], states[1][0]) and np.array_equal(states[0][1], states[1][1])
