@@ -95,11 +95,18 @@ def main() -> None:
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    # BB_BENCH_BACKEND=gloo + ranks sharing one device rehearse the N>1 path on a
+    # one-GPU box; the driver's multi-GPU runs use RCCL ("nccl"), one GPU per rank
+    backend = os.environ.get("BB_BENCH_BACKEND", "nccl")
+    gpu = local % max(torch.cuda.device_count(), 1) if backend != "nccl" else local
     if world > 1:
         os.environ.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
-        torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
-    dev = torch.device("cuda", local)
+        torch.cuda.set_device(gpu)
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device("cuda", gpu))
+        else:
+            dist.init_process_group(backend)
+    dev = torch.device("cuda", gpu)
     torch.cuda.set_device(dev)
 
     from ballbot_gym.distributed import env_shard, max_over_ranks, rank_seed
