@@ -36,6 +36,8 @@ def main():
     ap.add_argument("--seed", type=int, default=10)
     ap.add_argument("--cameras", action="store_true", help="depth cameras on (rgbd policy branch)")
     ap.add_argument("--conv-benchmark", action="store_true", help="MIOpen kernel search for the CNN")
+    ap.add_argument("--frozen-encoder", action="store_true",
+                    help="with --cameras: pretrain a TinyAutoencoder on GPU frames first and freeze it (reference setup)")
     a = ap.parse_args()
 
     import torch
@@ -50,10 +52,22 @@ def main():
 
     env = BallbotVecEnv(a.envs, device="cuda:0", precision=a.precision, seed=a.seed,
                         terrain_config={"type": a.terrain, "config": {}}, disable_cameras=not a.cameras)
+    frozen, pre_s = None, 0.0
+    if a.cameras and a.frozen_encoder:
+        from ballbot_rl.encoders import TinyAutoencoder, collect_depth_images, train_autoencoder
+
+        t = time.perf_counter()
+        imgs = collect_depth_images(env, 65536, seed=a.seed)
+        ae = TinyAutoencoder(env.cam_h, env.cam_w)
+        train_autoencoder(ae, imgs, epochs=2, batch_size=256, log=lambda *_: None)
+        frozen = ae.encoder.eval()
+        torch.cuda.synchronize()
+        pre_s = time.perf_counter() - t
+        del imgs
     m = BatchedPPO(env, n_steps=a.n_steps, batch_size=a.batch, n_epochs=a.epochs, ent_coef=0.001, clip_range=0.015,
                    vf_coef=2.0, target_kl=0.3, learning_rate=lr_schedule if a.lr == -1 else a.lr,
                    normalize_advantage=False, weight_decay=0.01, seed=a.seed,
-                   logger=CSVLogger(a.out, stdout=False))
+                   logger=CSVLogger(a.out, stdout=False), frozen_encoder=frozen)
     t_roll = t_upd = 0.0
     orig_collect, orig_train = m.collect_rollouts, m.train
 
@@ -84,7 +98,8 @@ def main():
            "unit": "env-steps/s", "timesteps": m.num_timesteps, "iterations": iters[0], "wall_s": el,
            "rollout_s": t_roll, "update_s": t_upd, "rollout_env_steps_per_s": m.num_timesteps / max(t_roll, 1e-9),
            "config": {"envs": a.envs, "n_steps": a.n_steps, "batch_size": a.batch, "n_epochs": a.epochs,
-                      "terrain": a.terrain, "precision": a.precision, "cameras": a.cameras},
+                      "terrain": a.terrain, "precision": a.precision, "cameras": a.cameras,
+                      "frozen_encoder": frozen is not None, "encoder_pretrain_s": pre_s},
            "ep_rew_mean": _eprew(m), "ep_len_mean": _eplen(m), "env_stats": env.stats()}
     print(json.dumps(out), flush=True)
     env.close()
