@@ -68,3 +68,34 @@ def test_product_path_has_no_cpu_fallback(native, monkeypatch, tmp_path):
     monkeypatch.setattr(native, "LIB_PATH", tmp_path / "missing.so")
     with pytest.raises(native.NativeLibraryError):
         native.lib()
+
+
+def _err(native):
+    return native.last_error()
+
+
+def test_argument_errors_without_gpu(native):
+    """Invalid arguments are rejected before any HIP call: status < 0 and a
+    bb_last_error message (the header's error contract), no crash."""
+    L = native.lib()
+    h = C.c_void_p()
+    p = native.default_params()
+    assert L.bb_create(0, 0, C.byref(p), C.byref(h)) < 0
+    assert "n_envs must be > 0" in _err(native)
+    p.n_terrains = 0
+    assert L.bb_create(16, 0, C.byref(p), C.byref(h)) < 0
+    assert "n_terrains" in _err(native)
+    assert L.bb_create(16, 0, None, None) < 0 and "out is NULL" in _err(native)
+    for call, msg in ((lambda: L.bb_step(None, None, None, None, None, None, None, 0, None), "NULL handle"),
+                      (lambda: L.bb_reset(None, None, None, None), "NULL handle"),
+                      (lambda: L.bb_set_hfield(None, 0, None, C.c_float(2.0)), "NULL handle"),
+                      (lambda: L.bb_render_depth(None, None, None, 64, 64, 6, 0, None), "NULL argument"),
+                      (lambda: L.bb_gae(None, None, None, None, None, 4, 4, 0.99, 0.95, None, None, None),
+                       "NULL argument"),
+                      (lambda: L.bb_ppo_loss(*([None] * 8), 8, 0, C.c_float(0.0), C.c_float(1.0), None, None, None,
+                                             None), "NULL argument"),
+                      (lambda: L.bb_generate_perlin(None, 0, 1, None, None, C.c_float(2.0)), "NULL argument"),
+                      (lambda: L.bb_kernel_ms(None, None, None), "NULL argument"),
+                      (lambda: L.bb_get_stats(None, None), "NULL argument")):
+        assert call() < 0
+        assert msg in _err(native), (msg, _err(native))

@@ -233,3 +233,33 @@ def test_step_as_hip_graph(cameras):
         assert torch.equal(e_eager.depth, e_graph.depth)
     for e in envs:
         e.close()
+
+
+def test_c_abi_range_errors_on_gpu():
+    """Out-of-range ids and sizes come back as errors with messages, the handle stays usable."""
+    import ctypes as C
+
+    from ballbot_gym import _native as N
+    from ballbot_gym.envs import BallbotVecEnv
+
+    env = BallbotVecEnv(64, device="cuda:0", n_terrains=2, terrain_config={"type": "hills", "config": {}})
+    L, h = N.lib(), env._h
+    hf = np.zeros(293 * 293, np.float32)
+    fp = hf.ctypes.data_as(C.POINTER(C.c_float))
+    assert L.bb_set_hfield(h, 5, fp, C.c_float(2.0)) < 0 and "out of range" in N.last_error()
+    assert L.bb_set_hfield(h, 0, fp, C.c_float(0.0)) < 0 and "size_z" in N.last_error()
+    assert L.bb_get_hfield(h, -1, fp) < 0 and "out of range" in N.last_error()
+    seeds = np.array([1, 2, 3], np.int32)
+    pc = N.PerlinCfg(25.0, 4, 0.2, 2.0, 1.0)
+    assert L.bb_generate_perlin(h, 0, 3, seeds.ctypes.data_as(C.POINTER(C.c_int32)), C.byref(pc),
+                                C.c_float(2.0)) < 0
+    assert "out of range" in N.last_error()
+    d = torch.zeros(64, 2, 8, 8, device="cuda:0")
+    assert L.bb_render_depth(h, C.c_void_p(d.data_ptr()), None, 0, 8, 6, 1, None) < 0
+    assert "image size" in N.last_error()
+    assert L.bb_render_depth(h, C.c_void_p(d.data_ptr()), None, 8, 8, 0, 1, None) < 0
+    assert "frame interval" in N.last_error()
+    assert L.bb_time_kernel(h, -1) < 0
+    env.step(torch.zeros(64, 3, device="cuda:0"))  # still fine
+    assert env.stats()["diverged"] == 0
+    env.close()
