@@ -207,3 +207,21 @@ def test_encoder_pretrain_on_gpu_frames(tmp_path):
     m.learn(total_timesteps=256 * 8 * 2)
     assert torch.equal(w0, m.policy.features_extractor.extractors["rgbd_0"][0].weight)  # frozen
     env.close()
+
+
+def test_split_k_linear_matches_linear():
+    from ballbot_rl.policies.mlp_policy import SplitKLinear
+
+    dev = torch.device("cuda:0")
+    torch.manual_seed(0)
+    lin = SplitKLinear(128, 128).to(dev)
+    ref = torch.nn.Linear(128, 128).to(dev)
+    ref.load_state_dict(lin.state_dict())
+    x = torch.randn(8192, 128, device=dev, requires_grad=True)
+    x2 = x.detach().clone().requires_grad_()
+    gy = torch.randn(8192, 128, device=dev)
+    lin(x).backward(gy)
+    ref(x2).backward(gy)
+    assert torch.allclose(x.grad, x2.grad, rtol=1e-5, atol=1e-5)
+    assert torch.allclose(lin.weight.grad, ref.weight.grad, rtol=1e-4, atol=1e-3)
+    assert torch.allclose(lin.bias.grad, ref.bias.grad, rtol=1e-4, atol=1e-3)
