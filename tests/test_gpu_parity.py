@@ -263,3 +263,47 @@ def test_c_abi_range_errors_on_gpu():
     env.step(torch.zeros(64, 3, device="cuda:0"))  # still fine
     assert env.stats()["diverged"] == 0
     env.close()
+
+
+def test_full_size_step_properties():
+    """BASELINE configs[1] size (4096 envs), 150 steps of random actions: properties that
+    hold for every env-step whatever the trajectory (size-independent checks):
+    - the reward is the reference's float32 chain of the returned obs and action
+      (DirectionalReward + action penalty + survival bonus, ballbot_env.py:929-937, 1019);
+    - failure <=> tilt(obs orientation) > 20 deg (:982-1017), done => reset obs;
+    - obs echoes the action, clips hold (|vel|, |angular_vel| <= 2, |motor| <= 2);
+    - free-joint quaternions stay unit, nothing diverges."""
+    from ballbot_gym.envs import BallbotVecEnv
+    from scipy.spatial.transform import Rotation as Rot
+
+    n = 4096
+    env = BallbotVecEnv(n, device="cuda:0", seed=11)
+    g = torch.Generator(device="cuda:0").manual_seed(5)
+    f32 = np.float32
+    for t in range(150):
+        a = (torch.rand(n, 3, generator=g, device="cuda:0") * 2.4 - 1.2)
+        obs, rew, term, trunc, info = env.step(a)
+        a_h = a.cpu().numpy()
+        o = info["terminal_observation"].cpu().numpy()
+        r = rew.cpu().numpy()
+        fl = info["done_flags"].cpu().numpy()
+        assert np.array_equal(o[:, 0:3], a_h)
+        assert np.abs(o[:, 3:9]).max() <= 2 and np.abs(o[:, 12:15]).max() <= 2
+        failed = (fl & 2) != 0
+        vel = o[:, 12:15]
+        base = (vel[:, 0] * f32(0.0) + vel[:, 1] * f32(1.0)) * f32(0.01)
+        nrm = np.sqrt((a_h * a_h).sum(1, dtype=f32), dtype=f32)
+        exp = base + f32(-0.0001) * (nrm * nrm)
+        exp = np.where(failed, exp, exp + f32(0.02)).astype(f32)
+        assert np.allclose(r, exp, rtol=0, atol=2e-8), np.abs(r - exp).max()
+        tilt = np.degrees(np.arccos(np.clip(Rot.from_rotvec(o[:, 9:12].astype(np.float64)).as_matrix()[:, 2, 2],
+                                            -1, 1)))
+        edge = np.abs(tilt - 20.0) < 1e-4
+        assert np.array_equal(failed[~edge], tilt[~edge] > 20.0)
+        done = (fl & 5) != 0
+        assert np.all(obs.cpu().numpy()[done] == 0)  # auto-reset observation
+    q, v, _, _ = env.get_state()
+    assert np.allclose(np.linalg.norm(q[:, 3:7], axis=1), 1, atol=1e-9)
+    assert np.allclose(np.linalg.norm(q[:, 13:17], axis=1), 1, atol=1e-9)
+    assert env.stats()["diverged"] == 0
+    env.close()
