@@ -72,11 +72,13 @@ __device__ __forceinline__ void static_for(F&& f) {
 template <typename T>
 __device__ __forceinline__ void cone_sel(const T* jar, T mu, T f1, T f2, const T* D, T Dm, T* force, T* C) {
   const T U0 = jar[0] * mu, U1 = jar[1] * f1, U2 = jar[2] * f2;
-  const T N = U0, Tn = sqrt(U1 * U1 + U2 * U2);
+  const T t2 = U1 * U1 + U2 * U2;
+  const T rt = t2 > 0 ? rsqrt(t2) : T(0);
+  const T N = U0, Tn = t2 * rt;  // sqrt(t2) via the reciprocal root the Hessian needs anyway
   const bool top = N >= mu * Tn || (Tn <= 0 && N >= 0);
   const bool bot = !top && (mu * N + Tn <= 0 || (Tn <= 0 && N < 0));
   const T g = N - mu * Tn;  // Dm = D0 / (mu^2 (1 + mu^2)) from cone_params
-  const T iT = T(1) / (Tn > 0 ? Tn : T(1));
+  const T iT = Tn > 0 ? rt : T(1);
   const T gr1 = -mu * f1 * U1 * iT, gr2 = -mu * f2 * U2 * iT;
   const T sc = -Dm * g;
   const T k = Dm * g * (-mu) * iT, iT2 = iT * iT;
@@ -103,7 +105,7 @@ __device__ __forceinline__ void chol_rows(T (&h)[NV], T hdi, T (&diag)[NV], int 
     const T hdj = bcast<j>(hdi);
     const T fl = pivot_eps<T>() * maxT(hdj, T(1e-30));
     piv = piv > fl ? piv : fl;
-    const T d = sqrt(piv), id = T(1) / d;
+    const T id = rsqrt(piv);  // 1 / L_jj in one reciprocal square root (no sqrt + divide chain)
     diag[j] = id;  // inverse pivot: the solves multiply
     const T lij = h[j] * id;
     h[j] = tl > j ? lij : h[j];
@@ -284,7 +286,7 @@ __device__ int solve16(const ModelT<T>& m, EnvWork<T>& W, int ng, int nb, T* a, 
         gn += gi * gi;
       }
     }
-    if (m.scale * sqrt(gn) < m.tol) break;
+    if (m.scale * m.scale * gn < m.tol * m.tol) break;  // scale * ||g|| < tol without the sqrt
     PH(2)
     // ---- (4) Hessian row `row` in registers
     T h[NV];
