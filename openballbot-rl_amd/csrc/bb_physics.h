@@ -450,7 +450,7 @@ BB_HD void frame_from_normal(const T* n, T* t1, T* t2) {
   if (fabs(n[1]) < T(0.5)) y[1] = 1; else y[2] = 1;
   T d = dot3(n, y);
   t1[0] = y[0] - d * n[0]; t1[1] = y[1] - d * n[1]; t1[2] = y[2] - d * n[2];
-  T inv = T(1) / sqrt(dot3(t1, t1));
+  T inv = rsqrt(dot3(t1, t1));
   t1[0] *= inv; t1[1] *= inv; t1[2] *= inv;
   cross3(t2, n, t1);
 }
@@ -727,8 +727,7 @@ BB_HD void ground_contact(const ModelT<T>& m, const T* gc, const T* RB, const T*
     for (int i = 0; i < 3; i++) { J[r][i] = F[r][i]; J[r][3 + i] = x2[i]; }
   }
   const T imp = clampT(impedance(m, dist), T(0.0001), T(0.9999));
-  const T R0 = maxT(T(1e-15), (1 - imp) * m.iw_ball / imp);
-  D = T(1) / R0;
+  D = minT(T(1e15), imp / ((1 - imp) * m.iw_ball));  // 1 / max(1e-15, (1 - imp) iw / imp), one divide
 #pragma unroll
   for (int r = 0; r < 3; r++) {
     const T vel = J[r][0] * v[9] + J[r][1] * v[10] + J[r][2] * v[11] + J[r][3] * v[12] + J[r][4] * v[13] +
