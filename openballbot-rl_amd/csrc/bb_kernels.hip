@@ -329,9 +329,28 @@ __global__ __launch_bounds__(64) void predict_kernel(ModelT<T> mg, Dev d) {
     int rmin = (int)floor((y0 + sy) / (2 * sy) * N1), rmax = (int)ceil((y1 + sy) / (2 * sy) * N1);
     cmin = cmin < 0 ? 0 : cmin; cmax = cmax > N1 ? N1 : cmax;
     rmin = rmin < 0 ? 0 : rmin; rmax = rmax > N1 ? N1 : rmax;
-    for (int r = rmin; r <= rmax && !slow; r++)
-      for (int c = cmin; c <= cmax; c++)
-        if (T(hf[r * HF_N + c]) * size_z >= lo) { slow = true; break; }
+    // the kernels' prisms (cells [rmin, rmax) x [cmin, cmax)) that the grown
+    // geom could reach this step (the same conservative test the kernels prune with)
+    Seg<T> sg;
+#pragma unroll
+    for (int i = 0; i < 3; i++) { sg.c[i] = cw[i]; sg.a[i] = aw[i]; }
+    sg.hh = hh;
+    sg.r = ext;
+    const T dx = 2 * sx / N1, dy = 2 * sy / N1;
+    for (int r = rmin; r < rmax && !slow; r++)
+      for (int c = cmin; c < cmax; c++) {
+        const T x0 = dx * c - sx, x1 = dx * (c + 1) - sx, y0 = dy * r - sy, y1 = dy * (r + 1) - sy;
+        const T z00 = T(hf[r * HF_N + c]) * size_z, z10 = T(hf[(r + 1) * HF_N + c]) * size_z;
+        const T z01 = T(hf[r * HF_N + c + 1]) * size_z, z11 = T(hf[(r + 1) * HF_N + c + 1]) * size_z;
+        if (maxT(maxT(z00, z10), maxT(z01, z11)) < lo) continue;
+        const T A[3][3] = {{x0, y0, z00}, {x0, y1, z10}, {x1, y0, z01}};
+        const T B[3][3] = {{x0, y1, z10}, {x1, y0, z01}, {x1, y1, z11}};
+#ifdef __HIP_DEVICE_COMPILE__
+        if (t16::prism_may_hit(sg, A) || t16::prism_may_hit(sg, B)) { slow = true; break; }
+#else
+        (void)A; (void)B; slow = true;  // host pass of the kernel: never run
+#endif
+      }
   }
   d.pred_mark[e] = slow ? 1 : 0;
 }

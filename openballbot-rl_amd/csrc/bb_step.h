@@ -63,7 +63,17 @@ BB_HD int forward(const ModelT<T>& m, const T* q, const T* v, const T* ctrl, T* 
   const int ng = tr.hf ? t16::collide_team(m, k, v, tr.hf, tr.size_z, W.g, &overflow, tm.tl) : 0;
   int nb = 0;
   if constexpr (BODY) {
+#if defined(BB_PHASE_CLOCKS)
+    const unsigned long long b_t0 = clock64();
+#endif
     nb = t16::collide_body_team(m, k, tr.hf, tr.size_z, tr.hz, W.bc, &overflow, tm.tl);
+#if defined(BB_PHASE_CLOCKS)
+    if (tm.tl == 0) {  // full kernel: forwards, body contacts, body-collision cycles
+      atomicAdd(&bb_phase_cycles[12], 1ull);
+      atomicAdd(&bb_phase_cycles[13], (unsigned long long)nb);
+      atomicAdd(&bb_phase_cycles[14], clock64() - b_t0);
+    }
+#endif
   } else {
     // fast path: no base-tree contact support compiled in; configurations that
     // could have one abort here and are re-run by the full kernel
@@ -113,7 +123,13 @@ BB_HD int forward(const ModelT<T>& m, const T* q, const T* v, const T* ctrl, T* 
   // 16-lane DPP-row solve: smooth force and dense M staged in the team's LDS
   t16::mass_dense_team(W, tm.tl);
   team_sync();
+#if defined(BB_PHASE_CLOCKS)
+  const unsigned long long s_t0 = clock64();
+#endif
   const int it = t16::solve16<BODY>(m, W, ng, nb, acc, tm.tl);
+#if defined(BB_PHASE_CLOCKS)
+  if (BODY && tm.tl == 0) atomicAdd(&bb_phase_cycles[15], clock64() - s_t0);  // full-kernel solve cycles
+#endif
 #else
   const int it = solve_team(m, W, W.qfs, ng, acc, tm);
 #endif

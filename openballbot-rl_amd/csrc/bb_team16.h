@@ -520,6 +520,34 @@ __device__ __forceinline__ void put_body(T* bc, int slot, const T* n, const T* p
 // MuJoCo's own prism pre-filter (a prism whose three top vertices are below
 // the geom's AABB is skipped), so "no" is exact and "yes" sends the env to the
 // full kernel.  Team-uniform result.
+// Conservative prune before the exact prism test: every point of a capsule or
+// cylinder g lies within g.r, coordinate-wise, of its axis segment c + t a,
+// |t| <= hh.  It can only reach the prism (xy in its top triangle, z below the
+// highest top vertex) if some segment point has x, y within g.r of the
+// triangle's bounding box and z - g.r below that top.  False only when no
+// contact is possible, so the exact SAT keeps deciding every contact.
+template <typename T>
+__device__ __forceinline__ bool prism_may_hit(const Seg<T>& g, const T (&V)[3][3]) {
+  T t0 = -g.hh, t1 = g.hh;
+#pragma unroll
+  for (int ax = 0; ax < 2; ax++) {
+    const T lo = minT(V[0][ax], minT(V[1][ax], V[2][ax])) - g.r;
+    const T hi = maxT(V[0][ax], maxT(V[1][ax], V[2][ax])) + g.r;
+    if (fabs(g.a[ax]) < T(1e-12)) {
+      if (g.c[ax] < lo || g.c[ax] > hi) return false;
+    } else {
+      const T ia = T(1) / g.a[ax];
+      const T ta = (lo - g.c[ax]) * ia, tb = (hi - g.c[ax]) * ia;
+      t0 = maxT(t0, minT(ta, tb));
+      t1 = minT(t1, maxT(ta, tb));
+    }
+  }
+  if (t0 > t1) return false;
+  const T ztop = maxT(V[0][2], maxT(V[1][2], V[2][2]));
+  const T zmin = g.c[2] + minT(t0 * g.a[2], t1 * g.a[2]) - g.r;
+  return zmin <= ztop;
+}
+
 template <typename T>
 __device__ bool body_candidates(const ModelT<T>& m, const Kin<T>& k, const float* hf, T size_z, T hz, int tl) {
   bool cand = false;
@@ -550,10 +578,21 @@ __device__ bool body_candidates(const ModelT<T>& m, const Kin<T>& k, const float
       cmin = cmin < 0 ? 0 : cmin; cmax = cmax > N1 ? N1 : cmax;
       rmin = rmin < 0 ? 0 : rmin; rmax = rmax > N1 ? N1 : rmax;
       if (rmax <= rmin || cmax <= cmin) continue;  // no prism
-      const int nc = cmax - cmin + 1, total = (rmax - rmin + 1) * nc;
-      for (int i = tl; i < total; i += L) {
+      // the full kernel's prisms (cells [rmin, rmax) x [cmin, cmax), two
+      // triangles each) under its own two prunes: a candidate iff the exact
+      // prism test would run on at least one of them
+      const T dx = 2 * sx / N1, dy = 2 * sy / N1;
+      const int nc = cmax - cmin, total = (rmax - rmin) * nc;
+      for (int i = tl; i < total && !cand; i += L) {
         const int ri = rmin + i / nc, ci = cmin + i % nc;
-        cand = cand || T(hf[ri * HF_N + ci]) * size_z >= lo[2];
+        const T x0 = dx * ci - sx, x1 = dx * (ci + 1) - sx, y0 = dy * ri - sy, y1 = dy * (ri + 1) - sy;
+        const T z00 = T(hf[ri * HF_N + ci]) * size_z, z10 = T(hf[(ri + 1) * HF_N + ci]) * size_z;
+        const T z01 = T(hf[ri * HF_N + ci + 1]) * size_z, z11 = T(hf[(ri + 1) * HF_N + ci + 1]) * size_z;
+        const T A[3][3] = {{x0, y0, z00}, {x0, y1, z10}, {x1, y0, z01}};
+        const T B[3][3] = {{x0, y1, z10}, {x1, y0, z01}, {x1, y1, z11}};
+        const bool ta = !(z00 < lo[2] && z10 < lo[2] && z01 < lo[2]) && prism_may_hit(g, A);
+        const bool tb = !(z10 < lo[2] && z01 < lo[2] && z11 < lo[2]) && prism_may_hit(g, B);
+        cand = ta || tb;
       }
     }
   }
@@ -631,7 +670,7 @@ __device__ int collide_body_team(const ModelT<T>& m, const Kin<T>& k, const floa
             V[t][1] = dy * ri - sy;
             V[t][2] = T(hf[ri * HF_N + cc]) * size_z;
           }
-          if (!(V[0][2] < lo[2] && V[1][2] < lo[2] && V[2][2] < lo[2])) {
+          if (!(V[0][2] < lo[2] && V[1][2] < lo[2] && V[2][2] < lo[2]) && prism_may_hit(g, V)) {
             PrismG<T> Pr;
             prism_build(Pr, V, -zb);
             hit = cyl ? cylinder_prism(g, Pr, dist, n, pos) : capsule_prism(g, Pr, dist, n, pos);

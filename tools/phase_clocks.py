@@ -24,6 +24,7 @@ def main():
     ap.add_argument("--steps", type=int, default=100)
     ap.add_argument("--warmup", type=int, default=300)
     ap.add_argument("--build", action="store_true")
+    ap.add_argument("--terrain", default="flat")
     a = ap.parse_args()
     if a.build or not LIB.exists():
         LIB.parent.mkdir(parents=True, exist_ok=True)
@@ -37,7 +38,7 @@ def main():
     L = _native.lib()
     L.bb_debug_phase_cycles.argtypes = [C.POINTER(C.c_ulonglong)]
     from ballbot_gym.envs import BallbotVecEnv
-    env = BallbotVecEnv(4096, device="cuda:0", precision=a.precision)
+    env = BallbotVecEnv(4096, device="cuda:0", precision=a.precision, terrain_config={"type": a.terrain, "config": {}})
     pool = torch.rand(64, 4096, 3, device="cuda:0") * 2 - 1
     out = (C.c_ulonglong * 16)()
     for i in range(a.warmup):
@@ -57,6 +58,10 @@ def main():
            "cycles_per_newton_iter": {NAMES[k]: out[k] / max(iters, 1) for k in range(8)}}
     res["total_cycles_per_forward"] = sum(out[k] for k in range(10)) / fw
     res["line_search_evals_per_newton_iter"] = out[11] / max(iters, 1)
+    if out[12]:
+        res["full_kernel"] = {"forwards": out[12], "body_contacts_per_forward": out[13] / out[12],
+                              "body_collide_cycles_per_forward": out[14] / out[12],
+                              "solve_cycles_per_forward": out[15] / out[12]}
     print(json.dumps(res, indent=1))
 
 
