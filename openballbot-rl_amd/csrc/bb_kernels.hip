@@ -402,6 +402,7 @@ struct bb_handle {
   // optional HIP-event timing of the fast step kernel (bb_time_kernel)
   std::vector<hipEvent_t> tev;
   int tcap = 0, tn = 0;
+  int route = 0;  // 0: predict + concurrent full kernel; 1: serial fast-then-full (BB_ROUTE=1)
   CamRig rig;  // depth cameras in the base body (bb_render_depth)
   void* scenes = nullptr;
 };
@@ -432,6 +433,20 @@ int launch_step(bb_handle* h, const float* a, float* o, float* r, uint8_t* dn, f
   const int blocks = (h->n + epw - 1) / epw;
   const size_t lds = lds_bytes<T>(epw);
   int* cnt = h->d.slow_count;
+  if (h->route == 1) {
+    // serial route: the fast kernel over every env, then the full kernel over
+    // the envs it handed over (no prediction, no second stream)
+    HIPCHK(hipMemsetAsync(cnt + 2, 0, sizeof(int), s));
+    const bool timed = h->tn < h->tcap;
+    if (timed) HIPCHK(hipEventRecord(h->tev[2 * h->tn], s));
+    hipLaunchKernelGGL((step_kernel<T, false>), dim3(blocks), dim3(WAVE), lds, s, m, h->cfg, h->d, a, o, r, dn, t,
+                       p2, ar, h->team, epw, (const int*)nullptr, (const int*)nullptr);
+    if (timed) { HIPCHK(hipEventRecord(h->tev[2 * h->tn + 1], s)); h->tn++; }
+    hipLaunchKernelGGL((step_kernel<T, true>), dim3(blocks), dim3(WAVE), lds, s, m, h->cfg, h->d, a, o, r, dn, t,
+                       p2, ar, h->team, epw, (const int*)h->d.slow_list, (const int*)(cnt + 2));
+    HIPCHK(hipGetLastError());
+    return 0;
+  }
   // route: envs near a base-tree contact -> full kernel (side stream,
   // concurrent); the rest -> fast kernel; its hand-overs -> full kernel after
   hipLaunchKernelGGL(predict_kernel<T>, dim3((h->n + 63) / 64), dim3(64), 0, s, m, h->d);
@@ -519,6 +534,8 @@ int bb_create(int n_envs, int device, const bb_params* p, bb_handle** out) {
     if (epw > cap) epw = cap;
     h->team = L;
     h->epw = epw;
+    const char* rt = getenv("BB_ROUTE");
+    if (rt) h->route = atoi(rt);
   }
   h->md = compile_model(sc);
   h->mf = cast_model<float>(h->md);
