@@ -97,7 +97,6 @@ struct EnvWork {
   WheelCon<T> wc[3];                         // ball-wheel contacts
   T g[MAXG * NGF];                           // ball-terrain contacts (compact, GF_*)
   T bc[MAXB * NBF];                          // base-tree geom contacts (compact, BF_*)
-  T bj[3][13];                               // the base-tree contact being processed (team-shared)
   Poses<T> P;                                // body poses for the Jacobian rebuilds
   T H[NH];                                   // Hessian / Cholesky factor (packed lower); dense M on the GPU
   union U {

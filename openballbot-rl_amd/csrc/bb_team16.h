@@ -169,23 +169,6 @@ __device__ __forceinline__ void ls_terms(const ModelT<T>& m, const EnvWork<T>& W
   }
 }
 
-// Rebuild base-tree contact b into the team-shared W.bj (every lane writes
-// the same values), evaluate its cone at a: returns the hinge slot's wheel.
-template <typename T>
-__device__ __forceinline__ int body_eval(const ModelT<T>& m, EnvWork<T>& W, int b, const T* a, T (&ar)[3], T& Dc,
-                                         T (&f)[3], T (&Cc)[6]) {
-  team_sync();  // previous users of bj are done
-  int hinge;
-  body_contact(m, W.bc + b * NBF, W.P, W.vi, W.bj, hinge, ar, Dc);
-  team_sync();
-  T jar[3];
-#pragma unroll
-  for (int r = 0; r < 3; r++) jar[r] = body_dot(W.bj, hinge, r, a) - ar[r];
-  const T D[3] = {Dc, Dc, Dc};
-  cone_sel(jar, T(1), T(1), T(1), D, Dc * T(0.5), f, Cc);
-  return hinge;
-}
-
 // Newton on f(a); a replicated in every lane of the row.  W.H holds the dense
 // mass matrix (packed lower) for this forward, W.qfs the smooth force.
 template <bool BODY, typename T>
@@ -252,25 +235,77 @@ __device__ int solve16(const ModelT<T>& m, EnvWork<T>& W, int ng, int nb, T* a, 
       }
     }
     PH(0)
+    // ---- (1b) base-tree contacts, contact-parallel: lane tl rebuilds contact
+    // b0 + tl (Jacobian, cone force and Hessian), adds its -J'f to its gradient
+    // partial (summed below with the rest), then the 16 contacts of the round
+    // are broadcast over the row (DPP) so that every lane accumulates its own
+    // Hessian row sum_b J_b[:, row]' C_b J_b into hb.
+    T hb[NV];
+#pragma unroll
+    for (int i = 0; i < NV; i++) hb[i] = 0;
+    if constexpr (BODY) {
+      for (int b0 = 0; b0 < nb; b0 += L) {  // team-uniform
+        T J[3][13], f[3] = {0, 0, 0}, Cc[6] = {0, 0, 0, 0, 0, 0};
+#pragma unroll
+        for (int r = 0; r < 3; r++)
+#pragma unroll
+          for (int q = 0; q < 13; q++) J[r][q] = 0;
+        int hinge = -1;
+        if (b0 + tl < nb) {
+          T ar[3], Dc;
+          body_contact(m, W.bc + (b0 + tl) * NBF, W.P, W.vi, J, hinge, ar, Dc);
+          T jar[3];
+#pragma unroll
+          for (int r = 0; r < 3; r++) jar[r] = body_dot(J, hinge, r, a) - ar[r];
+          const T D[3] = {Dc, Dc, Dc};
+          cone_sel(jar, T(1), T(1), T(1), D, Dc * T(0.5), f, Cc);
+#pragma unroll
+          for (int q = 0; q < 13; q++) {
+            const T jf = J[0][q] * f[0] + J[1][q] * f[1] + J[2][q] * f[2];
+            if (q < 6) gc[q] -= jf;
+            else if (q == 6) { gc[6] -= hinge == 0 ? jf : T(0); gc[7] -= hinge == 1 ? jf : T(0); gc[8] -= hinge == 2 ? jf : T(0); }
+            else gc[q + 2] -= jf;
+          }
+        }
+        const int cnt = nb - b0;
+        static_for<L>([&](auto jc_) {
+          constexpr int j = decltype(jc_)::value;
+          if (j < cnt) {  // team-uniform
+            const int hj = __builtin_amdgcn_update_dpp(0, hinge, 0x150 + j, 0xF, 0xF, false);
+            T Jb[3][13], Cb[6];
+#pragma unroll
+            for (int r = 0; r < 3; r++)
+#pragma unroll
+              for (int q = 0; q < 13; q++) Jb[r][q] = bcast<j>(J[r][q]);
+#pragma unroll
+            for (int r = 0; r < 6; r++) Cb[r] = bcast<j>(Cc[r]);
+            // this row's column of J_b (dof row -> column position, or none)
+            const int prow = row < 6 ? row : (row < 9 ? (row == 6 + hj ? 6 : -1) : row - 2);
+            T jc[3] = {0, 0, 0};
+#pragma unroll
+            for (int q = 0; q < 13; q++)
+#pragma unroll
+              for (int r = 0; r < 3; r++) jc[r] = prow == q ? Jb[r][q] : jc[r];
+            const T w0 = Cb[0] * jc[0] + Cb[3] * jc[1] + Cb[4] * jc[2];
+            const T w1 = Cb[3] * jc[0] + Cb[1] * jc[1] + Cb[5] * jc[2];
+            const T w2 = Cb[4] * jc[0] + Cb[5] * jc[1] + Cb[2] * jc[2];
+#pragma unroll
+            for (int q = 0; q < 13; q++) {
+              const T add = w0 * Jb[0][q] + w1 * Jb[1][q] + w2 * Jb[2][q];
+              if (q < 6) hb[q] += add;
+              else if (q == 6) { hb[6] += hj == 0 ? add : T(0); hb[7] += hj == 1 ? add : T(0); hb[8] += hj == 2 ? add : T(0); }
+              else hb[q + 2] += add;
+            }
+          }
+        });
+      }
+    }
     // ---- (2) team sums (DPP)
 #pragma unroll
     for (int i = 0; i < NV; i++) gc[i] = tsum(gc[i]);
 #pragma unroll
     for (int i = 0; i < 21; i++) Hg[i] = tsum(Hg[i]);
     team_sync();  // cj visible to every row owner
-    // base-tree contacts (rare): sequential over the contacts, every lane
-    // computing the same -J'f (added after the team sums)
-    for (int b = 0; BODY && b < nb; b++) {
-      T ar[3], Dc, f[3], Cc[6];
-      const int hinge = body_eval(m, W, b, a, ar, Dc, f, Cc);
-#pragma unroll
-      for (int q = 0; q < 13; q++) {
-        const T jf = W.bj[0][q] * f[0] + W.bj[1][q] * f[1] + W.bj[2][q] * f[2];
-        if (q < 6) gc[q] -= jf;
-        else if (q == 6) { gc[6] -= hinge == 0 ? jf : T(0); gc[7] -= hinge == 1 ? jf : T(0); gc[8] -= hinge == 2 ? jf : T(0); }
-        else gc[q + 2] -= jf;
-      }
-    }
     PH(1)
     // ---- (3) gradient, replicated
     T gn = 0;
@@ -312,27 +347,9 @@ __device__ int solve16(const ModelT<T>& m, EnvWork<T>& W, int ng, int nb, T* a, 
         const T v = Hg[ai >= b ? ai * (ai + 1) / 2 + b : b * (b + 1) / 2 + ai];
         h[9 + b] += row == 9 + ai ? v : T(0);
       }
-    // base-tree contacts (rare): each lane rebuilds contact b and adds
-    // J_b' C_b J_b to its row
-    for (int b = 0; BODY && b < nb; b++) {
-      T ar[3], Dc, f[3], Cc[6];
-      const int hinge = body_eval(m, W, b, a, ar, Dc, f, Cc);
-      // this row's column of J (dof row -> column position, or none)
-      const int prow = row < 6 ? row : (row < 9 ? (row == 6 + hinge ? 6 : -1) : row - 2);
-      const T jc[3] = {prow >= 0 ? W.bj[0][prow] : T(0), prow >= 0 ? W.bj[1][prow] : T(0),
-                       prow >= 0 ? W.bj[2][prow] : T(0)};
-      // w = C jc ; h[dof(q)] += w . J[:, q]
-      const T w0 = Cc[0] * jc[0] + Cc[3] * jc[1] + Cc[4] * jc[2];
-      const T w1 = Cc[3] * jc[0] + Cc[1] * jc[1] + Cc[5] * jc[2];
-      const T w2 = Cc[4] * jc[0] + Cc[5] * jc[1] + Cc[2] * jc[2];
+    // base-tree contacts: this lane's row, accumulated in the contact pass
 #pragma unroll
-      for (int q = 0; q < 13; q++) {
-        const T add = w0 * W.bj[0][q] + w1 * W.bj[1][q] + w2 * W.bj[2][q];
-        if (q < 6) h[q] += add;
-        else if (q == 6) { h[6] += hinge == 0 ? add : T(0); h[7] += hinge == 1 ? add : T(0); h[8] += hinge == 2 ? add : T(0); }
-        else h[q + 2] += add;
-      }
-    }
+    for (int k = 0; k < NV; k++) h[k] += hb[k];
     T hdi = 0;
 #pragma unroll
     for (int k = 0; k < NV; k++) hdi = row == k ? h[k] : hdi;
