@@ -29,7 +29,7 @@
 using namespace bb;
 
 #ifdef BB_PHASE_CLOCKS
-namespace bb { __device__ unsigned long long bb_phase_cycles[16]; }
+namespace bb { __device__ unsigned long long bb_phase_cycles[32]; }
 #endif
 
 namespace {
@@ -337,6 +337,10 @@ __global__ __launch_bounds__(64) void predict_kernel(ModelT<T> mg, Dev d) {
     sg.hh = hh;
     sg.r = ext;
     const T dx = 2 * sx / N1, dy = 2 * sy / N1;
+#ifdef __HIP_DEVICE_COMPILE__
+    t16::Reach<T> sr;
+    t16::make_reach(sg, sr);
+#endif
     for (int r = rmin; r < rmax && !slow; r++)
       for (int c = cmin; c < cmax; c++) {
         const T x0 = dx * c - sx, x1 = dx * (c + 1) - sx, y0 = dy * r - sy, y1 = dy * (r + 1) - sy;
@@ -346,7 +350,7 @@ __global__ __launch_bounds__(64) void predict_kernel(ModelT<T> mg, Dev d) {
         const T A[3][3] = {{x0, y0, z00}, {x0, y1, z10}, {x1, y0, z01}};
         const T B[3][3] = {{x0, y1, z10}, {x1, y0, z01}, {x1, y1, z11}};
 #ifdef __HIP_DEVICE_COMPILE__
-        if (t16::prism_may_hit(sg, A) || t16::prism_may_hit(sg, B)) { slow = true; break; }
+        if (t16::prism_may_hit(sr, A) || t16::prism_may_hit(sr, B)) { slow = true; break; }
 #else
         (void)A; (void)B; slow = true;  // host pass of the kernel: never run
 #endif
@@ -387,6 +391,7 @@ __global__ void assign_kernel(Dev d, const int32_t* ids) {
 
 struct bb_handle {
   int n, device, fp64, team, epw;
+  int epw_full;  // envs per wave of the full kernel (its lists are a minority of the envs)
   hipStream_t side;                 // the concurrent full-kernel launch
   hipEvent_t fork, join;
   bb_params p;
@@ -432,6 +437,9 @@ int launch_step(bb_handle* h, const float* a, float* o, float* r, uint8_t* dn, f
   const int epw = h->epw;
   const int blocks = (h->n + epw - 1) / epw;
   const size_t lds = lds_bytes<T>(epw);
+  const int epf = h->epw_full;
+  const int fblocks = (h->n + epf - 1) / epf;
+  const size_t flds = lds_bytes<T>(epf);
   int* cnt = h->d.slow_count;
   if (h->route == 1) {
     // serial route: the fast kernel over every env, then the full kernel over
@@ -442,8 +450,8 @@ int launch_step(bb_handle* h, const float* a, float* o, float* r, uint8_t* dn, f
     hipLaunchKernelGGL((step_kernel<T, false>), dim3(blocks), dim3(WAVE), lds, s, m, h->cfg, h->d, a, o, r, dn, t,
                        p2, ar, h->team, epw, (const int*)nullptr, (const int*)nullptr);
     if (timed) { HIPCHK(hipEventRecord(h->tev[2 * h->tn + 1], s)); h->tn++; }
-    hipLaunchKernelGGL((step_kernel<T, true>), dim3(blocks), dim3(WAVE), lds, s, m, h->cfg, h->d, a, o, r, dn, t,
-                       p2, ar, h->team, epw, (const int*)h->d.slow_list, (const int*)(cnt + 2));
+    hipLaunchKernelGGL((step_kernel<T, true>), dim3(fblocks), dim3(WAVE), flds, s, m, h->cfg, h->d, a, o, r, dn, t,
+                       p2, ar, h->team, epf, (const int*)h->d.slow_list, (const int*)(cnt + 2));
     HIPCHK(hipGetLastError());
     return 0;
   }
@@ -453,8 +461,8 @@ int launch_step(bb_handle* h, const float* a, float* o, float* r, uint8_t* dn, f
   hipLaunchKernelGGL(split_kernel, dim3(1), dim3(1024), 0, s, h->d);
   HIPCHK(hipEventRecord(h->fork, s));
   HIPCHK(hipStreamWaitEvent(h->side, h->fork, 0));
-  hipLaunchKernelGGL((step_kernel<T, true>), dim3(blocks), dim3(WAVE), lds, h->side, m, h->cfg, h->d, a, o, r, dn, t,
-                     p2, ar, h->team, epw, (const int*)h->d.pred_envs, (const int*)(cnt + 1));
+  hipLaunchKernelGGL((step_kernel<T, true>), dim3(fblocks), dim3(WAVE), flds, h->side, m, h->cfg, h->d, a, o, r, dn,
+                     t, p2, ar, h->team, epf, (const int*)h->d.pred_envs, (const int*)(cnt + 1));
   const bool timed = h->tn < h->tcap;
   if (timed) HIPCHK(hipEventRecord(h->tev[2 * h->tn], s));
   hipLaunchKernelGGL((step_kernel<T, false>), dim3(blocks), dim3(WAVE), lds, s, m, h->cfg, h->d, a, o, r, dn, t, p2,
@@ -462,8 +470,8 @@ int launch_step(bb_handle* h, const float* a, float* o, float* r, uint8_t* dn, f
   if (timed) { HIPCHK(hipEventRecord(h->tev[2 * h->tn + 1], s)); h->tn++; }
   HIPCHK(hipEventRecord(h->join, h->side));
   HIPCHK(hipStreamWaitEvent(s, h->join, 0));
-  hipLaunchKernelGGL((step_kernel<T, true>), dim3(blocks), dim3(WAVE), lds, s, m, h->cfg, h->d, a, o, r, dn, t, p2,
-                     ar, h->team, epw, (const int*)h->d.slow_list, (const int*)(cnt + 2));
+  hipLaunchKernelGGL((step_kernel<T, true>), dim3(fblocks), dim3(WAVE), flds, s, m, h->cfg, h->d, a, o, r, dn, t, p2,
+                     ar, h->team, epf, (const int*)h->d.slow_list, (const int*)(cnt + 2));
   HIPCHK(hipGetLastError());
   return 0;
 }
@@ -534,6 +542,15 @@ int bb_create(int n_envs, int device, const bb_params* p, bb_handle** out) {
     if (epw > cap) epw = cap;
     h->team = L;
     h->epw = epw;
+    // envs per wave of the full kernel: the same as the fast kernel's by
+    // default.  Fewer (BB_EPW_FULL=1, 2) spread the full lists over more SIMDs
+    // but cost more issue slots in total: perlin 1.51 M (1), 1.67 M (2),
+    // 1.78 M (4) env-steps/s -- the step kernels are issue-bound, not latency-bound
+    int epf = epw;
+    const char* of = getenv("BB_EPW_FULL");
+    if (of && atoi(of) > 0) epf = atoi(of);
+    if (epf > epw) epf = epw;
+    h->epw_full = epf;
     const char* rt = getenv("BB_ROUTE");
     if (rt) h->route = atoi(rt);
   }
@@ -829,8 +846,8 @@ int bb_get_config(bb_handle* h, int32_t* out5) {
 // diagnostic build only: read and clear the per-phase cycle counters
 int bb_debug_phase_cycles(unsigned long long* out16) {
   HIPCHK(hipDeviceSynchronize());
-  HIPCHK(hipMemcpyFromSymbol(out16, HIP_SYMBOL(bb::bb_phase_cycles), sizeof(unsigned long long) * 16));
-  unsigned long long z[16] = {0};
+  HIPCHK(hipMemcpyFromSymbol(out16, HIP_SYMBOL(bb::bb_phase_cycles), sizeof(unsigned long long) * 32));
+  unsigned long long z[32] = {0};
   HIPCHK(hipMemcpyToSymbol(HIP_SYMBOL(bb::bb_phase_cycles), z, sizeof z));
   return 0;
 }

@@ -25,7 +25,7 @@ static long g_ls_evals = 0;
 // Diagnostic build only (-DBB_PHASE_CLOCKS): per-phase s_memtime cycles,
 // summed over teams into bb_phase_cycles[] (read back by tools/phase_clocks).
 #if defined(BB_PHASE_CLOCKS) && defined(__HIP_DEVICE_COMPILE__)
-extern __device__ unsigned long long bb_phase_cycles[16];
+extern __device__ unsigned long long bb_phase_cycles[32];
 #define PH_DECL unsigned long long ph_t = clock64(), ph_acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
 #define PH(k) { unsigned long long n_ = clock64(); ph_acc[k] += n_ - ph_t; ph_t = n_; }
 #define PH_FLUSH(tm) if ((tm).tl == 0) { for (int k_ = 0; k_ < 8; k_++) atomicAdd(&bb_phase_cycles[k_], ph_acc[k_]); }

@@ -66,7 +66,9 @@ BB_HD int forward(const ModelT<T>& m, const T* q, const T* v, const T* ctrl, T* 
 #if defined(BB_PHASE_CLOCKS)
     const unsigned long long b_t0 = clock64();
 #endif
-    nb = t16::collide_body_team(m, k, tr.hf, tr.size_z, tr.hz, W.bc, &overflow, tm.tl);
+    // W.H is free until mass_dense_team below: it holds the SAT candidate list
+    static_assert(sizeof(W.H) >= t16::CAND_CAP * sizeof(int), "candidate list does not fit W.H");
+    nb = t16::collide_body_team(m, k, tr.hf, tr.size_z, tr.hz, W.bc, &overflow, tm.tl, reinterpret_cast<int*>(W.H));
 #if defined(BB_PHASE_CLOCKS)
     if (tm.tl == 0) {  // full kernel: forwards, body contacts, body-collision cycles
       atomicAdd(&bb_phase_cycles[12], 1ull);
@@ -128,7 +130,10 @@ BB_HD int forward(const ModelT<T>& m, const T* q, const T* v, const T* ctrl, T* 
 #endif
   const int it = t16::solve16<BODY>(m, W, ng, nb, acc, tm.tl);
 #if defined(BB_PHASE_CLOCKS)
-  if (BODY && tm.tl == 0) atomicAdd(&bb_phase_cycles[15], clock64() - s_t0);  // full-kernel solve cycles
+  if (BODY && tm.tl == 0) {  // full-kernel solve cycles and Newton iterations
+    atomicAdd(&bb_phase_cycles[15], clock64() - s_t0);
+    atomicAdd(&bb_phase_cycles[20], (unsigned long long)it);
+  }
 #endif
 #else
   const int it = solve_team(m, W, W.qfs, ng, acc, tm);

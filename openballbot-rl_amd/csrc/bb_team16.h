@@ -531,40 +531,59 @@ __device__ __forceinline__ void put_body(T* bc, int slot, const T* n, const T* p
   s[BF_CODE] = T(8 * b1 + b2);
 }
 
+// Conservative prune before the exact prism test: every point of a capsule or
+// cylinder g lies within g.r, coordinate-wise, of its axis segment c + t a,
+// |t| <= hh.  It can only reach the prism (xy in its top triangle, z below the
+// highest top vertex) if some segment point has x, y within g.r of the
+// triangle's bounding box and z - g.r below that top.  False only when no
+// contact is possible, so the exact SAT keeps deciding every contact.  The
+// slab reciprocals are per geom (Reach), not per prism.
+template <typename T>
+struct Reach {
+  T c[3], a[3], hh, r, ia[2];
+  bool par[2];  // axis parallel to the slab's planes
+};
+
+template <typename T>
+__device__ __forceinline__ void make_reach(const Seg<T>& g, Reach<T>& R) {
+#pragma unroll
+  for (int i = 0; i < 3; i++) { R.c[i] = g.c[i]; R.a[i] = g.a[i]; }
+  R.hh = g.hh; R.r = g.r;
+#pragma unroll
+  for (int ax = 0; ax < 2; ax++) {
+    R.par[ax] = fabs(g.a[ax]) < T(1e-12);
+    R.ia[ax] = R.par[ax] ? T(0) : T(1) / g.a[ax];
+  }
+}
+
+template <typename T>
+__device__ __forceinline__ bool prism_may_hit(const Reach<T>& g, const T (&V)[3][3]) {
+  T t0 = -g.hh, t1 = g.hh;
+  bool out = false;
+#pragma unroll
+  for (int ax = 0; ax < 2; ax++) {
+    const T lo = minT(V[0][ax], minT(V[1][ax], V[2][ax])) - g.r;
+    const T hi = maxT(V[0][ax], maxT(V[1][ax], V[2][ax])) + g.r;
+    if (g.par[ax]) {
+      out = out || g.c[ax] < lo || g.c[ax] > hi;
+    } else {
+      const T ta = (lo - g.c[ax]) * g.ia[ax], tb = (hi - g.c[ax]) * g.ia[ax];
+      t0 = maxT(t0, minT(ta, tb));
+      t1 = minT(t1, maxT(ta, tb));
+    }
+  }
+  if (out || t0 > t1) return false;
+  const T ztop = maxT(V[0][2], maxT(V[1][2], V[2][2]));
+  const T zmin = g.c[2] + minT(t0 * g.a[2], t1 * g.a[2]) - g.r;
+  return zmin <= ztop;
+}
+
 // Fast-path test: can any base-tree contact exist at this configuration?
 // Exact for ball x {tower, sticks}; for hfield x geom it asks whether any
 // heightfield vertex under the geom's AABB reaches the geom's lowest point --
 // MuJoCo's own prism pre-filter (a prism whose three top vertices are below
 // the geom's AABB is skipped), so "no" is exact and "yes" sends the env to the
 // full kernel.  Team-uniform result.
-// Conservative prune before the exact prism test: every point of a capsule or
-// cylinder g lies within g.r, coordinate-wise, of its axis segment c + t a,
-// |t| <= hh.  It can only reach the prism (xy in its top triangle, z below the
-// highest top vertex) if some segment point has x, y within g.r of the
-// triangle's bounding box and z - g.r below that top.  False only when no
-// contact is possible, so the exact SAT keeps deciding every contact.
-template <typename T>
-__device__ __forceinline__ bool prism_may_hit(const Seg<T>& g, const T (&V)[3][3]) {
-  T t0 = -g.hh, t1 = g.hh;
-#pragma unroll
-  for (int ax = 0; ax < 2; ax++) {
-    const T lo = minT(V[0][ax], minT(V[1][ax], V[2][ax])) - g.r;
-    const T hi = maxT(V[0][ax], maxT(V[1][ax], V[2][ax])) + g.r;
-    if (fabs(g.a[ax]) < T(1e-12)) {
-      if (g.c[ax] < lo || g.c[ax] > hi) return false;
-    } else {
-      const T ia = T(1) / g.a[ax];
-      const T ta = (lo - g.c[ax]) * ia, tb = (hi - g.c[ax]) * ia;
-      t0 = maxT(t0, minT(ta, tb));
-      t1 = minT(t1, maxT(ta, tb));
-    }
-  }
-  if (t0 > t1) return false;
-  const T ztop = maxT(V[0][2], maxT(V[1][2], V[2][2]));
-  const T zmin = g.c[2] + minT(t0 * g.a[2], t1 * g.a[2]) - g.r;
-  return zmin <= ztop;
-}
-
 template <typename T>
 __device__ bool body_candidates(const ModelT<T>& m, const Kin<T>& k, const float* hf, T size_z, T hz, int tl) {
   bool cand = false;
@@ -580,6 +599,8 @@ __device__ bool body_candidates(const ModelT<T>& m, const Kin<T>& k, const float
     for (int gi = 0; gi < 6; gi++) {
       Seg<T> g;
       body_geom(m, k, gi, g);
+      Reach<T> gr;
+      make_reach(g, gr);
       T lo[3], hi[3];
 #pragma unroll
       for (int i = 0; i < 3; i++) {
@@ -607,8 +628,8 @@ __device__ bool body_candidates(const ModelT<T>& m, const Kin<T>& k, const float
         const T z01 = T(hf[ri * HF_N + ci + 1]) * size_z, z11 = T(hf[(ri + 1) * HF_N + ci + 1]) * size_z;
         const T A[3][3] = {{x0, y0, z00}, {x0, y1, z10}, {x1, y0, z01}};
         const T B[3][3] = {{x0, y1, z10}, {x1, y0, z01}, {x1, y1, z11}};
-        const bool ta = !(z00 < lo[2] && z10 < lo[2] && z01 < lo[2]) && prism_may_hit(g, A);
-        const bool tb = !(z10 < lo[2] && z01 < lo[2] && z11 < lo[2]) && prism_may_hit(g, B);
+        const bool ta = !(z00 < lo[2] && z10 < lo[2] && z01 < lo[2]) && prism_may_hit(gr, A);
+        const bool tb = !(z10 < lo[2] && z01 < lo[2] && z11 < lo[2]) && prism_may_hit(gr, B);
         cand = ta || tb;
       }
     }
@@ -617,14 +638,20 @@ __device__ bool body_candidates(const ModelT<T>& m, const Kin<T>& k, const float
   return bits != 0;
 }
 
+// per-team SAT candidate list capacity (ints, in the team's W.H: free until
+// mass_dense_team; 91 floats at fp32)
+constexpr int CAND_CAP = 80;
+
 // Dynamic pairs of the base-tree geoms (bb_bodycon.h), team-parallel, in the
 // oracle's order: ball x {tower, stick0, stick1}, then hfield x {tower,
 // stick0, stick1, wheel0..2} prism by prism.  hz: the terrain's top height
 // (max(hfield) * size_z): geoms above it skip the prism loop.  Returns the
-// contact count (team-uniform); *overflow |= 2 past MAXB.
+// contact count (team-uniform); *overflow |= 2 past MAXB.  cand: the team's
+// candidate list (CAND_CAP ints of LDS).
+
 template <typename T>
 __device__ int collide_body_team(const ModelT<T>& m, const Kin<T>& k, const float* hf, T size_z, T hz, T* bc,
-                                 int* overflow, int tl) {
+                                 int* overflow, int tl, int* cand) {
   const int team_shift = threadIdx.x & ~(L - 1);
   int nb = 0, total_hits = 0;
   auto compact = [&](bool hit) -> int {  // -> this lane's slot (valid if hit)
@@ -647,14 +674,56 @@ __device__ int collide_body_team(const ModelT<T>& m, const Kin<T>& k, const floa
     const int slot = compact(hit);
     if (hit && slot < MAXB) put_body(bc, slot, n, pos, dist, 7, tl + 1);
   }
-  // hfield (geom1) x convex geom: prisms under the geom's AABB
+  // hfield (geom1) x convex geom, in two passes so the exact test runs on full
+  // rounds.  Pass 1 walks the prisms under each geom's AABB 16 at a time with
+  // the cheap conservative prunes and appends survivors, in (geom, row-major
+  // prism) order, to a per-team candidate list in LDS; pass 2 runs the exact
+  // body-prism SAT 16 candidates per round.  Perlin: ~230 prisms over 6 geoms
+  // leave ~8 candidates per forward -- one SAT round instead of up to 8.
+  // Contact order is unchanged (both passes keep list order).
   if (hf) {
     const T sx = m.hf_sx, sy = m.hf_sy, zb = m.hf_bottom;
     const int N1 = HF_N - 1;
     const T dx = 2 * sx / N1, dy = 2 * sy / N1;
+    int nc = 0;  // candidates pending in cand[]
+    auto vertices = [&](int rr, int p, T (&V)[3][3]) {
+#pragma unroll
+      for (int t = 0; t < 3; t++) {
+        const int vt = p + t, cc = (vt >> 1), ri = rr + (vt & 1);
+        V[t][0] = dx * cc - sx;
+        V[t][1] = dy * ri - sy;
+        V[t][2] = T(hf[ri * HF_N + cc]) * size_z;
+      }
+    };
+    auto flush = [&]() {
+      team_sync();  // cand[] writes visible to the team
+      for (int base = 0; base < nc; base += L) {
+        bool hit = false;
+        T dist = 0, n[3] = {0, 0, 1}, pos[3] = {0, 0, 0};
+        int b2 = 0;
+        if (base + tl < nc) {
+          const int code = cand[base + tl];
+          const int gi = code >> 26, rr = (code >> 13) & 0x1FFF, p = code & 0x1FFF;
+          Seg<T> g;
+          body_geom(m, k, gi, g);
+          T V[3][3];
+          vertices(rr, p, V);
+          PrismG<T> Pr;
+          prism_build(Pr, V, -zb);
+          hit = gi == 0 ? cylinder_prism(g, Pr, dist, n, pos) : capsule_prism(g, Pr, dist, n, pos);
+          b2 = gi + 1;  // body ids: tower 1, sticks 2-3, wheels 4-6
+        }
+        const int slot = compact(hit);
+        if (hit && slot < MAXB) put_body(bc, slot, n, pos, dist, 0, b2);
+      }
+      team_sync();  // cand[] reads done before it is refilled
+      nc = 0;
+    };
     for (int gi = 0; gi < 6; gi++) {
       Seg<T> g;
       body_geom(m, k, gi, g);
+      Reach<T> gr;
+      make_reach(g, gr);
       const bool cyl = gi == 0;
       T lo[3], hi[3];
 #pragma unroll
@@ -672,31 +741,35 @@ __device__ int collide_body_team(const ModelT<T>& m, const Kin<T>& k, const floa
       rmin = rmin < 0 ? 0 : rmin; rmax = rmax > N1 ? N1 : rmax;
       const int np = 2 * (cmax - cmin + 1) - 2;
       const int total = (rmax - rmin) * (np > 0 ? np : 0);
-      const int b2 = gi + 1;  // body ids: tower 1, sticks 2-3, wheels 4-6
       for (int base = 0; base < total; base += L) {
         const int P = base + tl;
-        bool hit = false;
-        T dist = 0, n[3] = {0, 0, 1}, pos[3] = {0, 0, 0};
+        bool cand_hit = false;
+        int code = 0;
         if (P < total) {
-          const int rr = rmin + P / np, p = P % np;
+          const int rr = rmin + P / np, p = 2 * cmin + P % np;
           T V[3][3];
-#pragma unroll
-          for (int t = 0; t < 3; t++) {
-            const int vt = p + t, cc = cmin + (vt >> 1), ri = rr + (vt & 1);
-            V[t][0] = dx * cc - sx;
-            V[t][1] = dy * ri - sy;
-            V[t][2] = T(hf[ri * HF_N + cc]) * size_z;
-          }
-          if (!(V[0][2] < lo[2] && V[1][2] < lo[2] && V[2][2] < lo[2]) && prism_may_hit(g, V)) {
-            PrismG<T> Pr;
-            prism_build(Pr, V, -zb);
-            hit = cyl ? cylinder_prism(g, Pr, dist, n, pos) : capsule_prism(g, Pr, dist, n, pos);
-          }
+          vertices(rr, p, V);
+          cand_hit = !(V[0][2] < lo[2] && V[1][2] < lo[2] && V[2][2] < lo[2]) && prism_may_hit(gr, V);
+          code = (gi << 26) | (rr << 13) | p;
         }
-        const int slot = compact(hit);
-        if (hit && slot < MAXB) put_body(bc, slot, n, pos, dist, 0, b2);
+        const unsigned long long bal = __ballot(cand_hit);
+        const unsigned bits = unsigned(bal >> team_shift) & 0xFFFFu;
+        if (cand_hit) cand[nc + __popc(bits & ((1u << tl) - 1u))] = code;
+        nc += int(__popc(bits));
+#if defined(BB_PHASE_CLOCKS) && defined(__HIP_DEVICE_COMPILE__)
+        if (tl == 0) atomicAdd(&bb_phase_cycles[19], (unsigned long long)__popc(bits));  // SAT runs
+#endif
+        if (nc > CAND_CAP - L) flush();
       }
+#if defined(BB_PHASE_CLOCKS) && defined(__HIP_DEVICE_COMPILE__)
+      if (tl == 0) {  // geoms reaching the prism loop, prisms, rounds
+        atomicAdd(&bb_phase_cycles[16], 1ull);
+        atomicAdd(&bb_phase_cycles[17], (unsigned long long)total);
+        atomicAdd(&bb_phase_cycles[18], (unsigned long long)((total + L - 1) / L));
+      }
+#endif
     }
+    if (nc > 0) flush();
   }
   if (total_hits > MAXB) *overflow |= 2;
   return nb;

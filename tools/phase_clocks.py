@@ -40,7 +40,7 @@ def main():
     from ballbot_gym.envs import BallbotVecEnv
     env = BallbotVecEnv(4096, device="cuda:0", precision=a.precision, terrain_config={"type": a.terrain, "config": {}})
     pool = torch.rand(64, 4096, 3, device="cuda:0") * 2 - 1
-    out = (C.c_ulonglong * 16)()
+    out = (C.c_ulonglong * 32)()
     for i in range(a.warmup):
         env.step_async_raw(pool[i % 64])
     torch.cuda.synchronize()
@@ -61,7 +61,12 @@ def main():
     if out[12]:
         res["full_kernel"] = {"forwards": out[12], "body_contacts_per_forward": out[13] / out[12],
                               "body_collide_cycles_per_forward": out[14] / out[12],
-                              "solve_cycles_per_forward": out[15] / out[12]}
+                              "solve_cycles_per_forward": out[15] / out[12],
+                              "newton_iters_per_forward": out[20] / out[12],
+                              "geoms_in_prism_loop_per_forward": out[16] / out[12],
+                              "prisms_per_forward": out[17] / out[12],
+                              "prism_rounds_per_forward": out[18] / out[12],
+                              "sat_runs_per_forward": out[19] / out[12]}
     print(json.dumps(res, indent=1))
 
 
