@@ -152,7 +152,8 @@ int bb_step(bb_handle* h, const float* actions_dev, float* obs_dev, float* rewar
 int bb_get_state(bb_handle* h, double* qpos, double* qvel, double* warm, int32_t* steps);
 int bb_set_state(bb_handle* h, const double* qpos, const double* qvel, const double* warm, const int32_t* steps);
 int bb_forward(bb_handle* h, const double* ctrl, double* qacc, int32_t* ncontact);
-/* counters since create: [resets, diverged, overflow, slow-path env-steps (envs the fast
+/* counters since create: [resets, diverged, overflow (env-steps where a geom pair hit MuJoCo's
+ * mjMAXCONPAIR = 50 contacts and was truncated, as MuJoCo does), slow-path env-steps (envs the fast
  * kernel handed to the full kernel: base-tree geom contacts possible), solver_iters_lo,
  * solver_iters_hi] */
 int bb_get_stats(bb_handle* h, int64_t* out6);

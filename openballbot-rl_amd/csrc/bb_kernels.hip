@@ -89,7 +89,14 @@ struct Dev {
   int* fast_envs;             // this step's fast-kernel env list (ascending)
   int* pred_envs;             // envs predicted to need base-tree contacts (full kernel, concurrent)
   uint8_t* pred_mark;
+  void* body_spill;           // T[n][MAXB - MAXB_LDS][NBF]: base-tree contacts past the LDS slots
 };
+
+// env e's spill block for base-tree contacts MAXB_LDS..MAXB-1
+template <typename T>
+__device__ __forceinline__ T* body_spill_of(const Dev& d, int e) {
+  return reinterpret_cast<T*>(d.body_spill) + size_t(e) * ((MAXB - MAXB_LDS) * NBF);
+}
 
 template <typename T>
 __device__ __forceinline__ void load_state(const Dev& d, int e, T* q, T* v, T* w, int& step) {
@@ -153,6 +160,7 @@ __global__ __launch_bounds__(64) void step_kernel(ModelT<T> mg, EnvCfg cfg, Dev 
   if (e >= d.n) return;
   const bool lead = tm.tl == 0;
   EnvWork<T>& W = team_work<T>(smem, team);
+  if (BODY && lead) W.bspill = body_spill_of<T>(d, e);  // read after the forward's first team_sync
   T q[NQ], v[NV], w[NV];
   int step;
   load_state(d, e, q, v, w, step);
@@ -227,6 +235,7 @@ __global__ __launch_bounds__(64) void forward_kernel(ModelT<T> mg, Dev d, const 
   const int e = blockIdx.x * epw + team;
   if (e >= d.n) return;
   EnvWork<T>& W = team_work<T>(smem, team);
+  if (tm.tl == 0) W.bspill = body_spill_of<T>(d, e);
   T q[NQ], v[NV], w[NV], c[3];
   int step;
   load_state(d, e, q, v, w, step);
@@ -592,6 +601,7 @@ int bb_create(int n_envs, int device, const bb_params* p, bb_handle** out) {
   HIPCHK(hipMalloc((void**)&d.fast_envs, sizeof(int) * n));
   HIPCHK(hipMalloc((void**)&d.pred_envs, sizeof(int) * n));
   HIPCHK(hipMalloc((void**)&d.pred_mark, n));
+  HIPCHK(hipMalloc(&d.body_spill, es * (MAXB - MAXB_LDS) * NBF * size_t(n)));
   HIPCHK(hipStreamCreateWithFlags(&h->side, hipStreamNonBlocking));
   HIPCHK(hipEventCreateWithFlags(&h->fork, hipEventDisableTiming));
   HIPCHK(hipEventCreateWithFlags(&h->join, hipEventDisableTiming));
@@ -632,6 +642,7 @@ int bb_destroy(bb_handle* h) {
   (void)hipFree(h->bank); (void)hipFree(h->size_z); (void)hipFree(h->offset); (void)hipFree(h->hmax); (void)hipFree(h->d.stats);
   (void)hipFree(h->d.slow_list); (void)hipFree(h->d.slow_count);
   (void)hipFree(h->d.fast_envs); (void)hipFree(h->d.pred_envs); (void)hipFree(h->d.pred_mark);
+  (void)hipFree(h->d.body_spill);
   (void)hipStreamDestroy(h->side); (void)hipEventDestroy(h->fork); (void)hipEventDestroy(h->join);
   for (hipEvent_t e : h->tev) (void)hipEventDestroy(e);
   (void)hipFree(h->scenes);

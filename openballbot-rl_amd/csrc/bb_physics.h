@@ -34,7 +34,9 @@ constexpr int HF_N = 293;        // ballbot.xml:23 nrow = ncol
 constexpr int MAXG = 50;         // ball-hfield contact cap: MuJoCo's mjMAXCONPAIR (== oracle BBO_MAXGROUND)
 constexpr int NH = NV * (NV + 1) / 2;
 constexpr int NGF = 4;           // fields per stored ground contact (see GF_* below)
-constexpr int MAXB = 32;         // base-tree geom contact cap (== oracle BBO_MAXBODY)
+constexpr int MAXPAIR = 50;      // contacts per hfield x geom pair: MuJoCo's mjMAXCONPAIR (== oracle BBO_MAXPAIR)
+constexpr int MAXB = 3 + 6 * MAXPAIR;  // base-tree geom contacts (== oracle BBO_MAXBODY)
+constexpr int MAXB_LDS = 32;     // of which in the team's LDS; the rest spill to a per-env HBM block
 constexpr int NBF = 8;           // fields per stored base-tree contact (see BF_* below)
 // ground-contact store fields (compact: Jacobian, aref and D are rebuilt on
 // use by ground_contact): normal (hfield -> ball)[3], dist

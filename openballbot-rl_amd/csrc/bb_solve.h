@@ -96,7 +96,8 @@ struct EnvWork {
   Mass<T> M;                                 // mass-matrix blocks
   WheelCon<T> wc[3];                         // ball-wheel contacts
   T g[MAXG * NGF];                           // ball-terrain contacts (compact, GF_*)
-  T bc[MAXB * NBF];                          // base-tree geom contacts (compact, BF_*)
+  T bc[MAXB_LDS * NBF];                      // base-tree geom contacts 0..MAXB_LDS-1 (compact, BF_*)
+  T* bspill;                                 // contacts MAXB_LDS..MAXB-1: this env's HBM block (full kernel)
   Poses<T> P;                                // body poses for the Jacobian rebuilds
   T H[NH];                                   // Hessian / Cholesky factor (packed lower); dense M on the GPU
   union U {
@@ -112,6 +113,12 @@ struct EnvWork {
     } hes;
   } u;
 };
+
+// base-tree contact b: the first MAXB_LDS in LDS, the rest in the env's spill block
+template <typename T>
+BB_HD T* body_slot(T* bc, T* spill, int b) {
+  return b < MAXB_LDS ? bc + b * NBF : spill + (b - MAXB_LDS) * NBF;
+}
 
 // Mass-matrix entry (i >= j) from the block representation.
 template <typename T>

@@ -68,7 +68,8 @@ BB_HD int forward(const ModelT<T>& m, const T* q, const T* v, const T* ctrl, T* 
 #endif
     // W.H is free until mass_dense_team below: it holds the SAT candidate list
     static_assert(sizeof(W.H) >= t16::CAND_CAP * sizeof(int), "candidate list does not fit W.H");
-    nb = t16::collide_body_team(m, k, tr.hf, tr.size_z, tr.hz, W.bc, &overflow, tm.tl, reinterpret_cast<int*>(W.H));
+    nb = t16::collide_body_team(m, k, tr.hf, tr.size_z, tr.hz, W.bc, W.bspill, &overflow, tm.tl,
+                                reinterpret_cast<int*>(W.H));
 #if defined(BB_PHASE_CLOCKS)
     if (tm.tl == 0) {  // full kernel: forwards, body contacts, body-collision cycles
       atomicAdd(&bb_phase_cycles[12], 1ull);

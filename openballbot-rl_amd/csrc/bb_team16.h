@@ -165,7 +165,7 @@ __device__ __forceinline__ void ls_terms(const ModelT<T>& m, const EnvWork<T>& W
 #pragma unroll
     for (int r = 0; r < 3; r++) { c6[r] = ground_dot(J, r, a) - ar[r]; c6[3 + r] = ground_dot(J, r, s); }
   } else if constexpr (BODY) {
-    body_ls_terms(m, W.bc + (c - 3 - ng) * NBF, W.P, W.vi, a, s, c6, D);
+    body_ls_terms(m, body_slot(const_cast<T*>(W.bc), W.bspill, c - 3 - ng), W.P, W.vi, a, s, c6, D);
   }
 }
 
@@ -253,7 +253,7 @@ __device__ int solve16(const ModelT<T>& m, EnvWork<T>& W, int ng, int nb, T* a, 
         int hinge = -1;
         if (b0 + tl < nb) {
           T ar[3], Dc;
-          body_contact(m, W.bc + (b0 + tl) * NBF, W.P, W.vi, J, hinge, ar, Dc);
+          body_contact(m, body_slot(W.bc, W.bspill, b0 + tl), W.P, W.vi, J, hinge, ar, Dc);
           T jar[3];
 #pragma unroll
           for (int r = 0; r < 3; r++) jar[r] = body_dot(J, hinge, r, a) - ar[r];
@@ -523,8 +523,8 @@ __device__ __forceinline__ int collide_team(const ModelT<T>& m, const Kin<T>& k,
 
 // store one base-tree contact (slot already compacted)
 template <typename T>
-__device__ __forceinline__ void put_body(T* bc, int slot, const T* n, const T* pos, T dist, int b1, int b2) {
-  T* s = bc + slot * NBF;
+__device__ __forceinline__ void put_body(T* bc, T* spill, int slot, const T* n, const T* pos, T dist, int b1, int b2) {
+  T* s = body_slot(bc, spill, slot);
 #pragma unroll
   for (int i = 0; i < 3; i++) { s[BF_N + i] = n[i]; s[BF_P + i] = pos[i]; }
   s[BF_DIST] = dist;
@@ -645,21 +645,22 @@ constexpr int CAND_CAP = 80;
 // Dynamic pairs of the base-tree geoms (bb_bodycon.h), team-parallel, in the
 // oracle's order: ball x {tower, stick0, stick1}, then hfield x {tower,
 // stick0, stick1, wheel0..2} prism by prism.  hz: the terrain's top height
-// (max(hfield) * size_z): geoms above it skip the prism loop.  Returns the
-// contact count (team-uniform); *overflow |= 2 past MAXB.  cand: the team's
-// candidate list (CAND_CAP ints of LDS).
+// (max(hfield) * size_z): geoms above it skip the prism loop.  Each hfield
+// pair keeps its first MAXPAIR contacts in prism order (MuJoCo's
+// mjMAXCONPAIR; *overflow |= 2 when a pair had more).  Contacts go to bc (the
+// first MAXB_LDS, LDS) and spill (the rest, HBM).  Returns the contact count
+// (team-uniform).  cand: the team's candidate list (CAND_CAP ints of LDS).
 
 template <typename T>
 __device__ int collide_body_team(const ModelT<T>& m, const Kin<T>& k, const float* hf, T size_z, T hz, T* bc,
-                                 int* overflow, int tl, int* cand) {
+                                 T* spill, int* overflow, int tl, int* cand) {
   const int team_shift = threadIdx.x & ~(L - 1);
-  int nb = 0, total_hits = 0;
+  const unsigned below = (1u << tl) - 1u;
+  int nb = 0;
   auto compact = [&](bool hit) -> int {  // -> this lane's slot (valid if hit)
-    const unsigned long long bal = __ballot(hit);
-    const unsigned bits = unsigned(bal >> team_shift) & 0xFFFFu;
-    const int slot = nb + __popc(bits & ((1u << tl) - 1u));
-    total_hits += int(__popc(bits));
-    nb = minT(nb + int(__popc(bits)), MAXB);
+    const unsigned bits = unsigned(__ballot(hit) >> team_shift) & 0xFFFFu;
+    const int slot = nb + __popc(bits & below);
+    nb += int(__popc(bits));
     return slot;
   };
   // ball (geom1, sphere) x tower (cylinder) / sticks (capsules): lanes 0..2
@@ -672,7 +673,7 @@ __device__ int collide_body_team(const ModelT<T>& m, const Kin<T>& k, const floa
       hit = tl == 0 ? sphere_cylinder(k.c, m.ball_r, g, dist, n, pos) : sphere_capsule(k.c, m.ball_r, g, dist, n, pos);
     }
     const int slot = compact(hit);
-    if (hit && slot < MAXB) put_body(bc, slot, n, pos, dist, 7, tl + 1);
+    if (hit) put_body(bc, spill, slot, n, pos, dist, 7, tl + 1);
   }
   // hfield (geom1) x convex geom, in two passes so the exact test runs on full
   // rounds.  Pass 1 walks the prisms under each geom's AABB 16 at a time with
@@ -686,6 +687,7 @@ __device__ int collide_body_team(const ModelT<T>& m, const Kin<T>& k, const floa
     const int N1 = HF_N - 1;
     const T dx = 2 * sx / N1, dy = 2 * sy / N1;
     int nc = 0;  // candidates pending in cand[]
+    int pair_n[6] = {0, 0, 0, 0, 0, 0};  // contacts so far per hfield pair (team-uniform)
     auto vertices = [&](int rr, int p, T (&V)[3][3]) {
 #pragma unroll
       for (int t = 0; t < 3; t++) {
@@ -713,8 +715,18 @@ __device__ int collide_body_team(const ModelT<T>& m, const Kin<T>& k, const floa
           hit = gi == 0 ? cylinder_prism(g, Pr, dist, n, pos) : capsule_prism(g, Pr, dist, n, pos);
           b2 = gi + 1;  // body ids: tower 1, sticks 2-3, wheels 4-6
         }
-        const int slot = compact(hit);
-        if (hit && slot < MAXB) put_body(bc, slot, n, pos, dist, 0, b2);
+        // per-pair cap: a hit is kept while its pair has fewer than MAXPAIR
+        // (candidates of one pair sit in consecutive lanes, in prism order)
+        bool keep = hit;
+#pragma unroll
+        for (int g = 0; g < 6; g++) {
+          const unsigned gb = unsigned(__ballot(hit && b2 == g + 1) >> team_shift) & 0xFFFFu;
+          if (hit && b2 == g + 1) keep = pair_n[g] + __popc(gb & below) < MAXPAIR;
+          if (pair_n[g] + __popc(gb) > MAXPAIR) *overflow |= 2;
+          pair_n[g] = minT(pair_n[g] + int(__popc(gb)), MAXPAIR);
+        }
+        const int slot = compact(keep);
+        if (keep) put_body(bc, spill, slot, n, pos, dist, 0, b2);
       }
       team_sync();  // cand[] reads done before it is refilled
       nc = 0;
@@ -771,7 +783,6 @@ __device__ int collide_body_team(const ModelT<T>& m, const Kin<T>& k, const floa
     }
     if (nc > 0) flush();
   }
-  if (total_hits > MAXB) *overflow |= 2;
   return nb;
 }
 

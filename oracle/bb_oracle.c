@@ -1050,7 +1050,6 @@ static int collide(const double xpos[NB][3], const double xmat[NB][9], const flo
       }
     }
     if (!hit) continue;
-    if (nbody >= BBO_MAXBODY) { *overflow |= 2; continue; }
     Contact* b = &con[n++];
     memset(b, 0, sizeof *b);
     b->dist = dist;
@@ -1069,6 +1068,7 @@ static int collide(const double xpos[NB][3], const double xmat[NB][9], const flo
     const double dx = 2 * sx / (ncol - 1), dy = 2 * sy / (nrow - 1);
     for (int k = 0; k < 6; k++) {
       const Convex* g = &bg[k];
+      int npair = 0; /* mjc_ConvexHField keeps the pair's first mjMAXCONPAIR contacts */
       double lo[3], hi[3];
       for (int i = 0; i < 3; i++) {
         double ai = fabs(g->a[i]);
@@ -1102,7 +1102,8 @@ static int collide(const double xpos[NB][3], const double xmat[NB][9], const flo
             double dist, nn[3], pos[3];
             int hit = cyl[k] ? cylinder_prism(g, &P, &dist, nn, pos) : capsule_prism(g, &P, &dist, nn, pos);
             if (!hit) continue;
-            if (nbody >= BBO_MAXBODY) { *overflow |= 2; continue; }
+            if (npair >= BBO_MAXPAIR) { *overflow |= 2; continue; } /* MuJoCo drops these too */
+            npair++;
             Contact* b = &con[n++];
             memset(b, 0, sizeof *b);
             b->dist = dist;

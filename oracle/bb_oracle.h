@@ -36,7 +36,9 @@ extern "C" {
 #define BBO_NBODY 8
 #define BBO_HF_N 293          /* ballbot.xml:23 nrow = ncol = 293 */
 #define BBO_MAXGROUND 50      /* cap on ball-hfield contacts = MuJoCo mjMAXCONPAIR */
-#define BBO_MAXBODY 32        /* cap on base-tree geom contacts (hfield x tower/sticks/wheels, ball x tower/sticks) */
+#define BBO_MAXPAIR 50        /* contacts per hfield x geom pair = MuJoCo mjMAXCONPAIR (first 50 in prism order) */
+/* base-tree geom contacts: ball x {tower, sticks} (one each) + hfield x {tower, sticks, wheels} */
+#define BBO_MAXBODY (3 + 6 * BBO_MAXPAIR)
 #define BBO_MAXCON (3 + BBO_MAXGROUND + BBO_MAXBODY)
 
 /* option flags for invariant tests (0 = reference behaviour) */

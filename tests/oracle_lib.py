@@ -16,7 +16,7 @@ ROOT = Path(__file__).resolve().parent.parent
 ORACLE_DIR = ROOT / "oracle"
 LIB_PATH = ORACLE_DIR / "_build" / "libbb_oracle.so"
 
-NQ, NV, NB, MAXCON = 17, 15, 8, 85  # MAXCON = 3 + BBO_MAXGROUND 50 + BBO_MAXBODY 32
+NQ, NV, NB, MAXCON = 17, 15, 8, 356  # MAXCON = 3 + BBO_MAXGROUND 50 + BBO_MAXBODY (3 + 6 x 50)
 HF_N = 293
 
 DISABLE_CONTACT, DISABLE_GRAVITY, DISABLE_DAMPING = 1, 2, 4

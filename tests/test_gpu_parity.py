@@ -175,6 +175,52 @@ def test_forward_parity_base_tree_contacts(oracle, precision, terrain):
 
 
 @pytest.mark.parametrize("terrain", ["flat", "hills"])
+def test_forward_parity_contacts_past_lds(oracle, terrain):
+    """Toppled robots lying on the terrain: more base-tree contacts than the
+    team's 32 LDS slots (the rest spill to the env's HBM block), and towers
+    across more prisms than MuJoCo's mjMAXCONPAIR (that pair keeps its first
+    50 in prism order).  Contact counts, overflow-free qacc vs the oracle."""
+    from ballbot_gym.terrain import generate_hills_terrain
+
+    n = 32
+    if terrain == "flat":
+        hf = oracle.flat_hfield()
+        tcfg = {"type": "flat", "config": {}}
+    else:
+        hf = generate_hills_terrain(293, seed=7).astype(np.float32)
+        tcfg = {"type": "hills", "config": {"seed": 7}}
+    rng = np.random.default_rng(21)
+    qs, vs = [], []
+    for i in range(n):
+        q, v, _ = oracle.reset_state(0.01)
+        t, yaw = np.radians(rng.uniform(80, 100)), rng.uniform(0, 2 * np.pi)
+        ax = np.array([np.cos(yaw), np.sin(yaw), 0.0])
+        q[3:7] = [np.cos(t / 2), *(np.sin(t / 2) * ax)]
+        q[0:2] = rng.uniform(-0.5, 0.5, 2)
+        q[2] = rng.uniform(0.09, 0.12) + (0.0 if terrain == "flat" else 0.02)
+        q[10:13] = [q[0] + 0.6 * np.cos(yaw), q[1] + 0.6 * np.sin(yaw), 0.5]
+        q[13:17] = [1, 0, 0, 0]
+        v[:] = rng.normal(0, 0.1, 15)
+        qs.append(q)
+        vs.append(v)
+    qs, vs = np.array(qs), np.array(vs)
+    env = _make_env(n, "fp64", tcfg)
+    ctrl = rng.uniform(-10, 10, (n, 3))
+    env.set_state(qs, vs, np.zeros((n, 15)))
+    qacc, ncon = env.forward(ctrl)
+    past = 0
+    for e in range(n):
+        fo = oracle.forward(qs[e], vs[e], ctrl[e], np.zeros(15), hf)
+        assert (ncon[e, 0], ncon[e, 1]) == (fo.nground, fo.nbody), e
+        past += fo.nbody > 32
+        ref = np.array(fo.qacc)
+        err = np.abs(qacc[e] - ref).max() / max(1.0, np.abs(ref).max())
+        assert err < 1e-7, (e, err, fo.nbody)
+    assert past >= n // 8, past
+    env.close()
+
+
+@pytest.mark.parametrize("terrain", ["flat", "hills"])
 def test_step_parity_base_tree_contacts(oracle, terrain):
     """env.step from states with base-tree contacts: they are routed to the full
     kernel (stats.slow_path counts full-kernel env-steps), results vs the oracle."""

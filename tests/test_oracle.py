@@ -200,7 +200,9 @@ def test_no_body_contacts_when_upright(oracle):
 def test_tower_on_flat_ground_geometry(oracle):
     """Dynamic hfield x tower-cylinder pair: base rolled 90 deg and lowered
     so the tower's side is 1 cm into flat ground; interior prisms report the
-    exact depth with normal +z, every contact is terrain(world) -> base."""
+    exact depth with normal +z, every contact is terrain(world) -> base tree.
+    The tower lies across more prisms than MuJoCo's mjMAXCONPAIR: its pair
+    keeps the first 50 and flags the cap (bit 1)."""
     hf = oracle.flat_hfield()
     q, v, _ = oracle.reset_state(0.01)
     q[3:7] = _rotx(90)
@@ -210,8 +212,11 @@ def test_tower_on_flat_ground_geometry(oracle):
     k0 = fo.ncon - fo.nbody
     ks = range(k0, k0 + fo.nbody)
     assert fo.nbody > 0
-    assert all(fo.con_body1[k] == 0 and fo.con_body2[k] == 1 for k in ks)
-    up = [k for k in ks if fo.con_frame[9 * k + 2] > 0.999]
+    assert all(fo.con_body1[k] == 0 for k in ks)
+    tower = [k for k in ks if fo.con_body2[k] == 1]
+    assert len(tower) == 50 and fo.ground_overflow & 2
+    assert tower == list(range(k0, k0 + 50))  # the tower pair comes first
+    up = [k for k in tower if fo.con_frame[9 * k + 2] > 0.999]
     assert up, "no face contact"
     for k in up:
         assert fo.con_dist[k] == pytest.approx(-0.01, abs=1e-9)
