@@ -165,15 +165,16 @@ def main() -> None:
         value = total_steps / elapsed
         abytes = algorithmic_bytes(args.precision) * n
         achieved = abytes / (kern_ms * 1e-3) / 1e9
-        traffic = None
+        traffic = issue_frac = None
         tj = Path(args.traffic_json)
         if tj.exists():
             try:
                 tr = json.loads(tj.read_text()).get(args.precision) or {}
                 if tr.get("envs") == n and tr.get("terrain", "flat") == args.terrain:
                     traffic = tr.get("bytes_per_launch")
+                    issue_frac = tr.get("issue_frac")
             except Exception:
-                traffic = None
+                traffic = issue_frac = None
         line = {
             "metric": f"env-steps/sec at {n} envs per GPU ({args.terrain} terrain, random actions)",
             "value": value,
@@ -199,7 +200,10 @@ def main() -> None:
                          "note": "latency/VALU-bound per-lane physics; HBM bytes = algorithmic state I/O "
                                  f"({algorithmic_bytes(args.precision)} B/env-step)",
                          "kernel": "step_kernel<T,false> (fast path)", "kernel_ms": kern_ms,
-                         "kernel_launches_timed": kern_n, "step_ms_hip_events": step_ms},
+                         "kernel_launches_timed": kern_n, "step_ms_hip_events": step_ms,
+                         # share of the kernel's wave cycles spent issuing (rocprofv3 SQ
+                         # counters, profiles/): the bound that binds is instruction issue
+                         "issue_frac": issue_frac},
             "stats": stats,
         }
         if world == 1 and not args.no_cpu_baseline:

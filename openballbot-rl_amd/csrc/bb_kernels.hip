@@ -111,6 +111,9 @@ __device__ __forceinline__ void load_state(const Dev& d, int e, T* q, T* v, T* w
 }
 template <typename T>
 __device__ __forceinline__ void store_state(const Dev& d, int e, const T* q, const T* v, const T* w, int step) {
+  // e opaque here: otherwise the 47 per-element addresses of load_state are
+  // kept live (94 VGPRs) across the whole step and spill to scratch
+  asm volatile("" : "+v"(e));
   T* Q = (T*)d.qpos;
   T* V = (T*)d.qvel;
   T* W = (T*)d.warm;
@@ -161,7 +164,11 @@ __global__ __launch_bounds__(64) void step_kernel(ModelT<T> mg, EnvCfg cfg, Dev 
   const bool lead = tm.tl == 0;
   EnvWork<T>& W = team_work<T>(smem, team);
   if (BODY && lead) W.bspill = body_spill_of<T>(d, e);  // read after the forward's first team_sync
-  T q[NQ], v[NV], w[NV];
+  // the env state lives in the team's workspace (every lane writes the same
+  // values): 47 values held in registers across four solves would spill
+  T* q = W.qn;
+  T* v = W.vn;
+  T* w = W.wn;
   int step;
   load_state(d, e, q, v, w, step);
   float a[3] = {act[3 * e], act[3 * e + 1], act[3 * e + 2]};

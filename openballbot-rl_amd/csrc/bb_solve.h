@@ -89,6 +89,8 @@ struct TerrainRef {
 template <typename T>
 struct EnvWork {
   T q0[NQ], v0[NV], vs[NV], as[NV];          // RK4 stage context
+  T qn[NQ], vn[NV], wn[NV];                  // env state and warm start (step kernel: not held in
+                                             // registers across the solves)
   T qfs[NV];                                 // smooth force of the current forward
   T vi[NV];                                  // stage velocity (pre-phase; constraint aref rebuilds)
   T gv[NV], mq[NV];                          // solver: gradient, M a - qfs (team-replicated)

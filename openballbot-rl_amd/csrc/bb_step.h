@@ -185,8 +185,15 @@ BB_HD int rk4_step(const ModelT<T>& m, T* q, T* v, T* warm, const T* ctrl, const
 #pragma unroll
       for (int i = 0; i < NV; i++) W.vi[i] = vi[i];
     }
-    const int fit = forward<T, BODY>(m, W.u.pre.qi, W.vi, ctrl, warm, tr, W, stage == 3 ? &so : (StageOut<T>*)nullptr, tm);
+    // the solve's warm start / result in registers for this forward only
+    // (warm may live in the workspace, see step_kernel)
+    T acc[NV];
+#pragma unroll
+    for (int i = 0; i < NV; i++) acc[i] = warm[i];
+    const int fit = forward<T, BODY>(m, W.u.pre.qi, W.vi, ctrl, acc, tr, W, stage == 3 ? &so : (StageOut<T>*)nullptr, tm);
     if (fit < 0) return -1;  // fast path aborted (team-uniform)
+#pragma unroll
+    for (int i = 0; i < NV; i++) warm[i] = acc[i];
     iters += fit;
     const T b = (stage == 0 || stage == 3) ? T(1.0 / 6) : T(1.0 / 3);  // RK4 weights B
     team_sync();

@@ -66,7 +66,7 @@ def main():
         "sgpr": timed[0].get("SGPR_Count"), "lds": timed[0].get("LDS_Block_Size"),
         "scratch": timed[0].get("Scratch_Size"),
     }
-    f, nf = counters(src / "fetch" / "run_counter_collection.csv", ["FETCH_SIZE"], a.pmc_last)
+    f, nf = counters(src / "fetch" / "run_counter_collection.csv", ["FETCH_SIZE", "GRBM_GUI_ACTIVE"], a.pmc_last)
     w, nw = counters(src / "write" / "run_counter_collection.csv", ["WRITE_SIZE"], a.pmc_last)
     sqn = ["SQ_WAVES", "SQ_INSTS_VALU", "SQ_INSTS_SALU", "SQ_INSTS_LDS", "SQ_WAIT_ANY", "SQ_WAIT_INST_ANY",
            "SQ_ACTIVE_INST_ANY", "SQ_WAVE_CYCLES"]
@@ -74,7 +74,18 @@ def main():
     fetch_b = f["FETCH_SIZE"] * 1024 * 2  # KiB -> B, x2 gfx950 correction
     write_b = w["WRITE_SIZE"] * 1024
     out["pmc"] = {"dispatches_averaged": min(nf, nw, ns), "FETCH_SIZE_kib_raw": f["FETCH_SIZE"],
-                  "WRITE_SIZE_kib": w["WRITE_SIZE"], "hbm_bytes_per_launch": fetch_b + write_b, **sq}
+                  "WRITE_SIZE_kib": w["WRITE_SIZE"], "hbm_bytes_per_launch": fetch_b + write_b,
+                  "GRBM_GUI_ACTIVE": f["GRBM_GUI_ACTIVE"], **sq}
+    # issue-bound evidence: the share of wave cycles in which the wave issued an
+    # instruction (SQ_* cycle counters are quad-cycles, both sides alike), VALU
+    # instructions per wave, and the effective clock (GRBM_GUI_ACTIVE sums the 8 XCDs)
+    waves = max(sq["SQ_WAVES"], 1.0)
+    out["derived"] = {
+        "issue_frac": sq["SQ_ACTIVE_INST_ANY"] / max(sq["SQ_WAVE_CYCLES"], 1.0),
+        "valu_insts_per_wave": sq["SQ_INSTS_VALU"] / waves,
+        "wave_cycles_per_wave": 4 * sq["SQ_WAVE_CYCLES"] / waves,
+        "effective_clock_ghz": f["GRBM_GUI_ACTIVE"] / 8 / (out["avg_ms_rocprof"] * 1e-3) / 1e9,
+    }
     (Path(str(dst) + "_summary.json")).write_text(json.dumps(out, indent=1))
     print(json.dumps(out, indent=1))
     if a.traffic:
@@ -82,7 +93,8 @@ def main():
         cur = json.loads(tj.read_text()) if tj.exists() else {}
         prec = bench["config"]["precision"]
         cur[prec] = {"precision": prec, "envs": bench["config"]["envs_per_gpu"],
-                     "bytes_per_launch": fetch_b + write_b, "source": str(dst) + "_summary.json"}
+                     "bytes_per_launch": fetch_b + write_b, "issue_frac": out["derived"]["issue_frac"],
+                     "source": str(dst) + "_summary.json"}
         tj.write_text(json.dumps(cur, indent=1))
 
 

@@ -1,7 +1,8 @@
 #!/bin/bash
 # rocprofv3 evidence for bench.py (run on the GPU box from the repo root):
 #   trace  : --kernel-trace --stats  (per-kernel average duration)
-#   fetch  : --pmc FETCH_SIZE        (HBM read bytes; x2 on gfx950 per MI355X_MICROARCH.md)
+#   fetch  : --pmc FETCH_SIZE GRBM_GUI_ACTIVE (HBM read bytes, x2 on gfx950 per MI355X_MICROARCH.md;
+#            busy cycles summed over the 8 XCDs -> effective clock)
 #   write  : --pmc WRITE_SIZE
 #   sq     : SQ instruction / wait counters
 # Each pass is its own process (counters never combined with traces).
@@ -14,7 +15,7 @@ export TMPDIR=/tmp
 B="bench.py --precision $PREC --no-cpu-baseline"
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/trace -o run -- \
   python3 $B --steps 300 --warmup 300 > $OUT/bench_trace.json || exit $?
-timeout -k 10 300 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $OUT/fetch -o run -- \
+timeout -k 10 300 rocprofv3 --pmc FETCH_SIZE GRBM_GUI_ACTIVE --output-format csv -d $OUT/fetch -o run -- \
   python3 $B --steps 20 --warmup 300 > $OUT/bench_fetch.json || exit $?
 timeout -k 10 300 rocprofv3 --pmc WRITE_SIZE --output-format csv -d $OUT/write -o run -- \
   python3 $B --steps 20 --warmup 300 > $OUT/bench_write.json || exit $?
