@@ -14,6 +14,7 @@
  *                    reward plugin; termination
  *   bb_render_depth  RGBDInputs depth cams (_get_obs)           sensors/rgbd.py:46-82
  *   bb_ppo_loss      SB3 PPO.train minibatch loss + grads
+ *   bb_adamw_clip    SB3 PPO.train clip_grad_norm_ + AdamW step
  *   bb_gae           SB3 RolloutBuffer.compute_returns_and_advantage (PPO)
  *   bb_forward       mujoco.mj_forward (diagnostic)             ballbot_env.py:525,620
  *   bb_get_state/    read/write qpos/qvel/qacc_warmstart        ballbot_env.py:616-617
@@ -41,7 +42,7 @@
 extern "C" {
 #endif
 
-#define BB_ABI_VERSION 7
+#define BB_ABI_VERSION 8
 #define BB_NQ 17
 #define BB_NV 15
 #define BB_OBS 15
@@ -133,6 +134,16 @@ int bb_ppo_loss(const float* mean_dev, const float* values_dev, const float* log
                 const float* old_logp_dev, const float* adv_dev, const float* returns_dev, const float* clip_dev,
                 int B, int normalize_advantage, float ent_coef, float vf_coef, float* terms_dev,
                 float* grad_mean_dev, float* grad_values_dev, void* stream);
+/* SB3 PPO.train's optimiser step on flat fp32 device buffers of n elements:
+ * clip_grad_norm_(max_norm) then torch.optim.AdamW (betas, eps, weight_decay;
+ * learning rate read from lr_dev, step counter step_dev incremented on device;
+ * coef_dev: 4 floats of scratch).  grad is read, not modified, and must be
+ * 16-byte aligned.  Two launches on stream; graph-capturable.
+ * Replaces SB3 2.6.0 PPO.train's clip_grad_norm_ + optimizer.step (the PPO the
+ * reference builds in ballbot_rl/training/train.py:125-142). */
+int bb_adamw_clip(float* param_dev, const float* grad_dev, float* exp_avg_dev, float* exp_avg_sq_dev, int64_t n,
+                  const float* lr_dev, float* step_dev, float* coef_dev, double beta1, double beta2, double eps,
+                  double weight_decay, double max_norm, void* stream);
 /* copy terrain bank slot terrain_id (float32[293*293]) to host memory */
 int bb_get_hfield(bb_handle* h, int terrain_id, float* data_host);
 /* per-env terrain ids (device int32[n]) applied at the next reset */

@@ -58,10 +58,10 @@ EXPORTS = [
     "bb_abi_version", "bb_last_error", "bb_default_params", "bb_create", "bb_destroy", "bb_set_hfield",
     "bb_assign_terrain", "bb_reset", "bb_step", "bb_get_state", "bb_set_state", "bb_forward", "bb_get_stats",
     "bb_get_offsets", "bb_get_config", "bb_time_kernel", "bb_kernel_ms", "bb_generate_perlin", "bb_get_hfield",
-    "bb_gae", "bb_render_depth", "bb_ppo_loss",
+    "bb_gae", "bb_render_depth", "bb_ppo_loss", "bb_adamw_clip",
 ]
 
-ABI_VERSION = 7  # include/ballbot_mi355x.h BB_ABI_VERSION
+ABI_VERSION = 8  # include/ballbot_mi355x.h BB_ABI_VERSION
 
 _lib = None
 
@@ -130,6 +130,7 @@ def _load(path: Path):
     L.bb_get_hfield.argtypes = [vp, C.c_int, fp]
     L.bb_render_depth.argtypes = [vp, vp, vp, C.c_int, C.c_int, C.c_int, C.c_int, vp]
     L.bb_ppo_loss.argtypes = [vp] * 8 + [C.c_int, C.c_int, C.c_float, C.c_float, vp, vp, vp, vp]
+    L.bb_adamw_clip.argtypes = [vp, vp, vp, vp, C.c_int64, vp, vp, vp] + [C.c_double] * 5 + [vp]
     L.bb_gae.argtypes = [vp, vp, vp, vp, vp, C.c_int, C.c_int, C.c_double, C.c_double, vp, vp, vp]
     L.bb_kernel_ms.argtypes = [vp, C.POINTER(C.c_double), C.POINTER(C.c_int32)]
     for name in [n for n in EXPORTS if n not in ("bb_default_params", "bb_abi_version")]:

@@ -20,6 +20,7 @@ from __future__ import annotations
 
 import copy
 import math
+import os
 from collections import OrderedDict
 from typing import Dict, Optional, Sequence, Tuple, Union
 
@@ -115,14 +116,16 @@ class _SplitKLinearFn(torch.autograd.Function):
 
 class SplitKLinear(nn.Linear):
     """nn.Linear (same parameters and state dict) whose large-batch GPU backward
-    uses the split-K weight gradient."""
+    uses the split-K weight gradient: K slices of ROWS rows each, so a 128x128
+    dW tile grid has B / ROWS workgroups (128 at B = 8192) instead of 16."""
 
-    SPLITS = 16
+    ROWS = int(os.environ.get("BB_SPLITK_ROWS", "64"))
 
     def forward(self, x: torch.Tensor) -> torch.Tensor:
         B = x.shape[0] if x.dim() == 2 else 0
-        if x.is_cuda and B >= 2048 and B % self.SPLITS == 0 and torch.is_grad_enabled():
-            return _SplitKLinearFn.apply(x, self.weight, self.bias, self.SPLITS)
+        S = B // self.ROWS if self.ROWS > 0 else 0
+        if x.is_cuda and B >= 2048 and S >= 2 and B % S == 0 and torch.is_grad_enabled():
+            return _SplitKLinearFn.apply(x, self.weight, self.bias, S)
         return super().forward(x)
 
 

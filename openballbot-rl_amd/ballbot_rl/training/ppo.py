@@ -198,7 +198,8 @@ class _UpdateGraphs:
                 if p.grad is not None:
                     p.grad.zero_()
             loss.backward()
-            nn.utils.clip_grad_norm_(params, ppo.max_grad_norm)
+            if not getattr(opt, "clips_grad", False):
+                nn.utils.clip_grad_norm_(params, ppo.max_grad_norm)
             opt.step()
             with torch.no_grad():
                 self.k.add_(1)
@@ -307,13 +308,16 @@ class BatchedPPO:
         self.policy = (policy or ActorCriticPolicy(spaces, 3, net_arch, activation_fn,
                                                    frozen_encoder=frozen_encoder)).to(self.device)
         self._sync_params()
-        # full-size minibatches replay one HIP graph (forward+backward, clip+AdamW);
-        # AdamW is then 'capturable' with its learning rate in a device tensor
+        # full-size minibatches replay one HIP graph (forward+backward, clip+AdamW).
+        # On the GPU clip_grad_norm_ + AdamW are bb_adamw_clip over flat buffers
+        # (FlatAdamW, learning rate in a device tensor); on the CPU torch's AdamW
         self.use_graphs = (self.device.type == "cuda") if use_graphs is None else bool(use_graphs)
         lr0 = self.lr_schedule(1.0)
-        if self.use_graphs:
-            self.optimizer = torch.optim.AdamW(self.policy.parameters(), lr=torch.tensor(lr0, device=self.device),
-                                               weight_decay=float(weight_decay), capturable=True)
+        if self.device.type == "cuda":
+            from ballbot_rl.training.optim import FlatAdamW
+
+            self.optimizer = FlatAdamW(self.policy.parameters(), lr=lr0, weight_decay=float(weight_decay),
+                                       max_grad_norm=self.max_grad_norm)
         else:
             self.optimizer = torch.optim.AdamW(self.policy.parameters(), lr=lr0, weight_decay=float(weight_decay))
         self._graphs = None
@@ -338,7 +342,12 @@ class BatchedPPO:
             return
         vec = nn.utils.parameters_to_vector(self.policy.parameters()).detach().contiguous()
         dist.broadcast(vec, src=0)
-        nn.utils.vector_to_parameters(vec, self.policy.parameters())
+        with torch.no_grad():  # in place: FlatAdamW's parameters are views of its flat buffer
+            off = 0
+            for p in self.policy.parameters():
+                k = p.numel()
+                p.copy_(vec[off:off + k].view_as(p))
+                off += k
 
     # ---------------------------------------------------------------- rollout
     @torch.no_grad()
@@ -490,7 +499,8 @@ class BatchedPPO:
                         break
                     self.optimizer.zero_grad(set_to_none=False)
                     loss.backward()
-                    nn.utils.clip_grad_norm_(self.policy.parameters(), self.max_grad_norm)
+                    if not getattr(self.optimizer, "clips_grad", False):
+                        nn.utils.clip_grad_norm_(self.policy.parameters(), self.max_grad_norm)
                     self.optimizer.step()
                 self._n_updates += 1
                 if not cont:

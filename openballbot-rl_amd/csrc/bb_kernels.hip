@@ -739,6 +739,22 @@ int bb_ppo_loss(const float* mean, const float* values, const float* log_std, co
   return 0;
 }
 
+int bb_adamw_clip(float* param, const float* grad, float* exp_avg, float* exp_avg_sq, int64_t n, const float* lr,
+                  float* step, float* coef, double beta1, double beta2, double eps, double weight_decay,
+                  double max_norm, void* stream) {
+  if (!param || !grad || !exp_avg || !exp_avg_sq || !lr || !step || !coef) return fail("bb_adamw_clip: NULL argument");
+  if (n < 1) return fail("bb_adamw_clip: n must be >= 1 (got %lld)", (long long)n);
+  if (!(beta1 >= 0.0 && beta1 < 1.0) || !(beta2 >= 0.0 && beta2 < 1.0))
+    return fail("bb_adamw_clip: betas must be in [0, 1) (got %g, %g)", beta1, beta2);
+  if (!(eps >= 0.0) || !(max_norm > 0.0)) return fail("bb_adamw_clip: eps must be >= 0 and max_norm > 0");
+  if ((reinterpret_cast<uintptr_t>(grad) & 15) != 0) return fail("bb_adamw_clip: grad must be 16-byte aligned");
+  AdamWArgs a{param, grad, exp_avg, exp_avg_sq, (long long)n, lr, step, coef, beta1, beta2, weight_decay,
+              float(beta2), float(1.0 - beta1), float(1.0 - beta2), float(eps), float(max_norm)};
+  if (launch_adamw_clip(a, (hipStream_t)stream))
+    return fail("bb_adamw_clip: launch failed: %s", hipGetErrorString(hipGetLastError()));
+  return 0;
+}
+
 int bb_get_hfield(bb_handle* h, int terrain_id, float* out) {
   if (!h || !out) return fail("bb_get_hfield: NULL argument");
   if (terrain_id < 0 || terrain_id >= h->p.n_terrains)

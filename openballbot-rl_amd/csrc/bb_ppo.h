@@ -23,4 +23,24 @@ struct PPOLossArgs {
 
 int launch_ppo_loss(const PPOLossArgs& a, hipStream_t s);
 
+// clip_grad_norm_ + AdamW on flat fp32 buffers (bb_adamw_clip)
+struct AdamWArgs {
+  float* param;            // [n]
+  const float* grad;       // [n] (not modified; the clip factor is applied on the fly)
+  float* exp_avg;          // [n]
+  float* exp_avg_sq;       // [n]
+  long long n;
+  const float* lr;         // device scalar (graph-replayable schedule)
+  float* step;             // device scalar, incremented once per call (torch's float32 step)
+  float* coef;             // device scratch [4]: clip factor, step size, sqrt(1 - b2^t), 1 - lr wd
+  // torch takes the hyper-parameters as Python doubles: 1 - beta etc. are
+  // formed in double and rounded once, as its kernels receive them
+  double beta1, beta2;     // bias corrections beta^t (double, as torch's eager AdamW)
+  double weight_decay;
+  float b2, omb1, omb2;    // float(beta2), float(1 - beta1), float(1 - beta2)
+  float eps, max_norm;
+};
+
+int launch_adamw_clip(const AdamWArgs& a, hipStream_t s);
+
 }  // namespace bb

@@ -1,4 +1,5 @@
-// bb_ppo.hip -- fused PPO minibatch loss + gradients.
+// bb_ppo.hip -- fused PPO minibatch loss + gradients, and the fused
+// clip_grad_norm_ + AdamW step.
 //
 // SB3 2.6.0 PPO.train evaluates, per minibatch of B samples (the reference's
 // PPO, ballbot_rl/training/train.py:125-142), with a diagonal Gaussian policy:
@@ -118,7 +119,67 @@ __global__ __launch_bounds__(PPO_THREADS) void ppo_loss_kernel(PPOLossArgs p) {
   }
 }
 
+// ---- optimiser step (SB3 2.6.0 PPO.train after loss.backward; the reference's PPO,
+// ballbot_rl/training/train.py:125-142):
+//   th.nn.utils.clip_grad_norm_(params, max_grad_norm): g *= min(1, max_norm / (||g||_2 + 1e-6))
+//   AdamW.step (torch.optim.AdamW, amsgrad=False, maximize=False):
+//     p *= 1 - lr wd;  m += (1 - b1)(g - m);  v = b2 v + (1 - b2) g^2
+//     p -= lr / (1 - b1^t) * m / (sqrt(v) / sqrt(1 - b2^t) + eps)
+// One single-workgroup launch reduces ||g||^2 and prepares the per-step
+// scalars (bias corrections in double, as torch's eager AdamW does on the
+// host); a grid-wide elementwise launch then updates p, m, v in one pass.
+// Replaces ~60 small PyTorch launches per minibatch (per-tensor norms, foreach
+// clip, capturable AdamW's per-tensor weight decay and bias corrections).
+constexpr int OPT_THREADS = 1024;
+
+__global__ __launch_bounds__(OPT_THREADS) void adamw_prep_kernel(AdamWArgs p) {
+  __shared__ float red[OPT_THREADS / 64][NACC];
+  float v[NACC] = {0, 0, 0, 0, 0, 0, 0, 0};
+  const long long n4 = p.n / 4;
+  const float4* g4 = reinterpret_cast<const float4*>(p.grad);
+  for (long long i = threadIdx.x; i < n4; i += OPT_THREADS) {
+    const float4 g = g4[i];
+    v[0] += g.x * g.x + g.y * g.y + g.z * g.z + g.w * g.w;
+  }
+  for (long long i = n4 * 4 + threadIdx.x; i < p.n; i += OPT_THREADS) v[0] += p.grad[i] * p.grad[i];
+  block_sums(v, red);
+  if (threadIdx.x == 0) {
+    const float norm = sqrtf(v[0]);
+    const float clip = fminf(p.max_norm / (norm + 1e-6f), 1.f);
+    const float t = *p.step + 1.f;
+    *p.step = t;
+    const double lr = double(*p.lr);
+    const double bc1 = 1.0 - pow(p.beta1, double(t)), bc2 = 1.0 - pow(p.beta2, double(t));
+    p.coef[0] = clip;
+    p.coef[1] = float(lr / bc1);
+    p.coef[2] = float(sqrt(bc2));
+    p.coef[3] = float(1.0 - lr * p.weight_decay);
+  }
+}
+
+__global__ __launch_bounds__(256) void adamw_update_kernel(AdamWArgs p) {
+  const long long i = (long long)blockIdx.x * 256 + threadIdx.x;
+  if (i >= p.n) return;
+  const float clip = p.coef[0], step_size = p.coef[1], bc2s = p.coef[2], decay = p.coef[3];
+  const float g = p.grad[i] * clip;
+  const float w = p.param[i] * decay;
+  float m = p.exp_avg[i];
+  m = m + p.omb1 * (g - m);  // torch.lerp_ (weight < 0.5 branch)
+  const float v = p.b2 * p.exp_avg_sq[i] + p.omb2 * g * g;  // mul_(beta2).addcmul_(g, g, 1 - beta2)
+  const float denom = sqrtf(v) / bc2s + p.eps;
+  p.exp_avg[i] = m;
+  p.exp_avg_sq[i] = v;
+  p.param[i] = w - step_size * (m / denom);
+}
+
 }  // namespace
+
+int launch_adamw_clip(const AdamWArgs& a, hipStream_t s) {
+  if (a.n <= 0) return 0;
+  hipLaunchKernelGGL(adamw_prep_kernel, dim3(1), dim3(OPT_THREADS), 0, s, a);
+  hipLaunchKernelGGL(adamw_update_kernel, dim3((unsigned)((a.n + 255) / 256)), dim3(256), 0, s, a);
+  return hipGetLastError() == hipSuccess ? 0 : -1;
+}
 
 int launch_ppo_loss(const PPOLossArgs& a, hipStream_t s) {
   if (a.B <= 0) return 0;

@@ -95,6 +95,10 @@ def test_argument_errors_without_gpu(native):
                       (lambda: L.bb_ppo_loss(*([None] * 8), 8, 0, C.c_float(0.0), C.c_float(1.0), None, None, None,
                                              None), "NULL argument"),
                       (lambda: L.bb_generate_perlin(None, 0, 1, None, None, C.c_float(2.0)), "NULL argument"),
+                      (lambda: L.bb_adamw_clip(None, None, None, None, 16, None, None, None, 0.9, 0.999, 1e-8, 0.01,
+                                               0.5, None), "NULL argument"),
+                      (lambda: L.bb_adamw_clip(16, 16, 16, 16, 0, 16, 16, 16, 0.9, 0.999, 1e-8, 0.01, 0.5, None),
+                       "n must be >= 1"),
                       (lambda: L.bb_kernel_ms(None, None, None), "NULL argument"),
                       (lambda: L.bb_get_stats(None, None), "NULL argument")):
         assert call() < 0

@@ -100,9 +100,6 @@ def test_graph_update_matches_eager(target_kl):
     for graphs in (False, True):
         m = BatchedPPO(GpuFake(), n_steps=16, batch_size=512, n_epochs=3, learning_rate=1e-3, target_kl=target_kl,
                        normalize_advantage=True, seed=4, use_graphs=graphs, logger=CSVLogger(None, stdout=False))
-        if not graphs:  # same AdamW kernels as the graph path
-            m.optimizer = torch.optim.AdamW(m.policy.parameters(), lr=torch.tensor(1e-3, device=dev),
-                                            weight_decay=0.01, capturable=True)
         m.collect_rollouts()
         models.append(m)
     d0 = models[0].buf.flat()
@@ -225,3 +222,54 @@ def test_split_k_linear_matches_linear():
     assert torch.allclose(x.grad, x2.grad, rtol=1e-5, atol=1e-5)
     assert torch.allclose(lin.weight.grad, ref.weight.grad, rtol=1e-4, atol=1e-3)
     assert torch.allclose(lin.bias.grad, ref.bias.grad, rtol=1e-4, atol=1e-3)
+
+
+@pytest.mark.parametrize("max_norm", [0.5, 1e3])
+def test_flat_adamw_matches_torch(max_norm):
+    """bb_adamw_clip (FlatAdamW) vs clip_grad_norm_ + torch.optim.AdamW over several steps
+    with a changing learning rate; max_norm 0.5 clips every step, 1e3 never."""
+    from ballbot_rl.training.optim import FlatAdamW
+
+    dev = torch.device("cuda:0")
+    torch.manual_seed(3)
+    shapes = [(128, 15), (128,), (128, 128), (128,), (3, 128), (3,), (3,)]
+    ref = [torch.nn.Parameter(torch.randn(s, device=dev) * 0.1) for s in shapes]
+    mine = [torch.nn.Parameter(p.detach().clone()) for p in ref]
+    opt_ref = torch.optim.AdamW(ref, lr=3e-4, weight_decay=0.01)
+    opt = FlatAdamW(mine, lr=3e-4, weight_decay=0.01, max_grad_norm=max_norm)
+    assert all(p.data_ptr() >= opt.flat.data_ptr() for p in mine)  # views of the flat buffer
+    for step in range(6):
+        lr = 3e-4 * (1 - step / 10)
+        opt_ref.param_groups[0]["lr"] = lr
+        opt.param_groups[0]["lr"].fill_(lr)
+        grads = [torch.randn(s, device=dev) for s in shapes]
+        for p, q, g in zip(ref, mine, grads):
+            p.grad = g.clone()
+            q.grad = g.clone()
+        torch.nn.utils.clip_grad_norm_(ref, max_norm)
+        opt_ref.step()
+        opt.step()
+    torch.cuda.synchronize()
+    assert float(opt.step_t) == 6.0
+    for p, q in zip(ref, mine):
+        assert torch.allclose(p, q, rtol=1e-5, atol=1e-7), (p - q).abs().max()
+    for p, q in zip(ref, mine):
+        st = opt_ref.state[p]
+        # m = 0.9 m + 0.1 g cancels for small m: an fma contraction moves it by ~ulp(0.1 |g|)
+        assert torch.allclose(st["exp_avg"], opt.state[q]["exp_avg"], rtol=1e-5, atol=1e-7), \
+            (st["exp_avg"] - opt.state[q]["exp_avg"]).abs().max()
+        assert torch.allclose(st["exp_avg_sq"], opt.state[q]["exp_avg_sq"], rtol=1e-5, atol=1e-9), \
+            (st["exp_avg_sq"] - opt.state[q]["exp_avg_sq"]).abs().max()
+
+
+def test_adamw_clip_rejects_bad_arguments():
+    from ballbot_gym import _native as N
+
+    L = N.lib()
+    x = torch.zeros(16, device="cuda:0")
+    s = torch.zeros(4, device="cuda:0")
+    p = x.data_ptr()
+    assert L.bb_adamw_clip(p, p, p, p, 0, p, s.data_ptr(), s.data_ptr(), 0.9, 0.999, 1e-8, 0.01, 0.5, None) < 0
+    assert "n must be" in N.last_error()
+    assert L.bb_adamw_clip(p, p, p, p, 16, p, s.data_ptr(), s.data_ptr(), 1.0, 0.999, 1e-8, 0.01, 0.5, None) < 0
+    assert L.bb_adamw_clip(None, p, p, p, 16, p, s.data_ptr(), s.data_ptr(), 0.9, 0.999, 1e-8, 0.01, 0.5, None) < 0
