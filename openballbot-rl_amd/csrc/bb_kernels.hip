@@ -423,7 +423,13 @@ struct bb_handle {
   // optional HIP-event timing of the fast step kernel (bb_time_kernel)
   std::vector<hipEvent_t> tev;
   int tcap = 0, tn = 0;
-  int route = 0;  // 0: predict + concurrent full kernel; 1: serial fast-then-full (BB_ROUTE=1)
+  // step routing: 0 predict + concurrent full kernel; 1 serial fast-then-full;
+  // -1 (default) serial while every terrain in the bank is flat, else 0.  On
+  // flat banks hand-overs are rare and the serial route saves the predict and
+  // split launches (3.66 M vs 3.57 M env-steps/s at 4096 flat envs)
+  int route = -1;
+  std::vector<uint8_t> relief;  // per terrain: max height > 0
+  int n_relief = 0;
   CamRig rig;  // depth cameras in the base body (bb_render_depth)
   void* scenes = nullptr;
 };
@@ -457,7 +463,8 @@ int launch_step(bb_handle* h, const float* a, float* o, float* r, uint8_t* dn, f
   const int fblocks = (h->n + epf - 1) / epf;
   const size_t flds = lds_bytes<T>(epf);
   int* cnt = h->d.slow_count;
-  if (h->route == 1) {
+  const int route = h->route >= 0 ? h->route : (h->n_relief == 0 ? 1 : 0);
+  if (route == 1) {
     // serial route: the fast kernel over every env, then the full kernel over
     // the envs it handed over (no prediction, no second stream)
     HIPCHK(hipMemsetAsync(cnt + 2, 0, sizeof(int), s));
@@ -621,6 +628,8 @@ int bb_create(int n_envs, int device, const bb_params* p, bb_handle** out) {
   // default: every terrain flat (terrain/__init__.py:32-34), size_z 2.0 (ballbot.xml:23)
   std::vector<float> sz(nt, 2.0f);
   h->h_offset.assign(nt, 0.01f);
+  h->relief.assign(nt, 0);
+  h->n_relief = 0;
   HIPCHK(hipMemcpy(h->size_z, sz.data(), sizeof(float) * nt, hipMemcpyHostToDevice));
   HIPCHK(hipMemcpy(h->offset, h->h_offset.data(), sizeof(float) * nt, hipMemcpyHostToDevice));
   d.bank = h->bank; d.size_z = h->size_z; d.offset = h->offset; d.hmax = h->hmax;
@@ -657,6 +666,11 @@ int bb_destroy(bb_handle* h) {
   return 0;
 }
 
+static void set_relief(bb_handle* h, int t, bool r) {
+  h->n_relief += int(r) - int(h->relief[t]);
+  h->relief[t] = r ? 1 : 0;
+}
+
 int bb_set_hfield(bb_handle* h, int terrain_id, const float* data, float size_z) {
   if (!h) return fail("bb_set_hfield: NULL handle");
   if (terrain_id < 0 || terrain_id >= h->p.n_terrains)
@@ -671,6 +685,7 @@ int bb_set_hfield(bb_handle* h, int terrain_id, const float* data, float size_z)
   float hm = 0.f;
   for (int i = 0; i < HF_N * HF_N; i++) hm = data[i] > hm ? data[i] : hm;
   HIPCHK(hipMemcpy(h->hmax + terrain_id, &hm, sizeof(float), hipMemcpyHostToDevice));
+  set_relief(h, terrain_id, hm > 0.f);
   HIPCHK(hipMemcpy(h->size_z + terrain_id, &size_z, sizeof(float), hipMemcpyHostToDevice));
   HIPCHK(hipMemcpy(h->offset + terrain_id, &off, sizeof(float), hipMemcpyHostToDevice));
   return 0;
@@ -698,6 +713,9 @@ int bb_generate_perlin(bb_handle* h, int first, int count, const int32_t* seeds,
   (void)hipFree(ds);
   if (rc) return fail("bb_generate_perlin: launch failed");
   HIPCHK(hipMemcpy(h->h_offset.data() + first, h->offset + first, sizeof(float) * count, hipMemcpyDeviceToHost));
+  std::vector<float> hm(count);
+  HIPCHK(hipMemcpy(hm.data(), h->hmax + first, sizeof(float) * count, hipMemcpyDeviceToHost));
+  for (int i = 0; i < count; i++) set_relief(h, first + i, hm[i] > 0.f);
   return 0;
 }
 
