@@ -176,14 +176,16 @@ class ActorCriticPolicy(nn.Module):
     def entropy(self, n: int) -> torch.Tensor:
         return (0.5 + 0.5 * self.LOG_2PI + self.log_std).sum().expand(n)
 
-    def forward(self, obs: Obs, deterministic: bool = False,
-                generator: Optional[torch.Generator] = None) -> Tuple[torch.Tensor, torch.Tensor, torch.Tensor]:
-        """-> (actions, values, log_prob), actions unclipped (SB3 clips before env.step)."""
+    def forward(self, obs: Obs, deterministic: bool = False, generator: Optional[torch.Generator] = None,
+                noise: Optional[torch.Tensor] = None) -> Tuple[torch.Tensor, torch.Tensor, torch.Tensor]:
+        """-> (actions, values, log_prob), actions unclipped (SB3 clips before env.step).
+        `noise`: standard-normal draws to use instead of sampling (graph replays)."""
         mean, values = self._heads(obs)
         if deterministic:
             actions = mean
         else:
-            eps = torch.randn(mean.shape, generator=generator, device=mean.device, dtype=mean.dtype)
+            eps = noise if noise is not None else torch.randn(mean.shape, generator=generator, device=mean.device,
+                                                              dtype=mean.dtype)
             actions = mean + eps * torch.exp(self.log_std)
         return actions, values, self.log_prob(mean, actions)
 

@@ -357,6 +357,8 @@ class BatchedPPO:
         if self._last_obs is None:
             self._last_obs, _ = env.reset()
         ep_r, ep_l = [], []
+        # the rollout's Gaussian draws in one launch (SB3 samples per step; same distribution)
+        noise = torch.randn(self.n_steps, self.n_envs, 3, generator=self.gen, device=self.device)
         for t in range(self.n_steps):
             b.obs[t].copy_(self._last_obs)        # env.obs is reused by the next step
             b.starts[t].copy_(self._last_starts)
@@ -366,7 +368,7 @@ class BatchedPPO:
                 pobs = policy_obs(b.obs[t], b.depth[t], b.rel_ts[t])
             else:
                 pobs = b.obs[t]
-            actions, values, logp = self.policy(pobs, generator=self.gen)
+            actions, values, logp = self.policy(pobs, noise=noise[t])
             b.actions[t].copy_(actions)
             b.values[t].copy_(values)
             b.log_probs[t].copy_(logp)

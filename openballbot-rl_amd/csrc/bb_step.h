@@ -135,6 +135,10 @@ BB_HD int forward(const ModelT<T>& m, const T* q, const T* v, const T* ctrl, T* 
     atomicAdd(&bb_phase_cycles[15], clock64() - s_t0);
     atomicAdd(&bb_phase_cycles[20], (unsigned long long)it);
   }
+  if (tm.tl == 0) {  // Newton iterations per forward: max, histogram in buckets of 2
+    atomicMax(&bb_phase_cycles[21], (unsigned long long)it);
+    atomicAdd(&bb_phase_cycles[22 + (it / 2 < 9 ? it / 2 : 9)], 1ull);
+  }
 #endif
 #else
   const int it = solve_team(m, W, W.qfs, ng, acc, tm);

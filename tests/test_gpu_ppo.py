@@ -273,3 +273,4 @@ def test_adamw_clip_rejects_bad_arguments():
     assert "n must be" in N.last_error()
     assert L.bb_adamw_clip(p, p, p, p, 16, p, s.data_ptr(), s.data_ptr(), 1.0, 0.999, 1e-8, 0.01, 0.5, None) < 0
     assert L.bb_adamw_clip(None, p, p, p, 16, p, s.data_ptr(), s.data_ptr(), 0.9, 0.999, 1e-8, 0.01, 0.5, None) < 0
+

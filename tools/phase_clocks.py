@@ -58,6 +58,8 @@ def main():
            "cycles_per_newton_iter": {NAMES[k]: out[k] / max(iters, 1) for k in range(8)}}
     res["total_cycles_per_forward"] = sum(out[k] for k in range(10)) / fw
     res["line_search_evals_per_newton_iter"] = out[11] / max(iters, 1)
+    res["newton_iters_per_forward_max"] = out[21]
+    res["newton_iters_per_forward_hist"] = {f"{2 * b}-{2 * b + 1}" if b < 9 else ">=18": out[22 + b] for b in range(10)}
     if out[12]:
         res["full_kernel"] = {"forwards": out[12], "body_contacts_per_forward": out[13] / out[12],
                               "body_collide_cycles_per_forward": out[14] / out[12],
