@@ -221,6 +221,44 @@ def test_forward_parity_contacts_past_lds(oracle, terrain):
 
 
 @pytest.mark.parametrize("terrain", ["flat", "hills"])
+def test_step_routes_agree(oracle, terrain, monkeypatch):
+    """The two step routes (predict + concurrent full kernel, BB_ROUTE=0; serial
+    fast-then-full, BB_ROUTE=1; the default picks serial on flat banks) and the
+    full kernel's envs per wave (BB_EPW_FULL) only move work between kernels:
+    the same states and outputs over several steps from base-tree-contact states.  An env
+    the predictor sends to the full kernel without a base-tree contact runs the full
+    kernel's instantiation of the same physics, so agreement is to rounding, not bitwise."""
+    from ballbot_gym.terrain import generate_hills_terrain  # noqa: F401  (hills bank via the env config)
+
+    n = 64
+    tcfg = {"type": "flat", "config": {}} if terrain == "flat" else {"type": "hills", "config": {"seed": 7}}
+    qs, vs = _body_contact_states(oracle, n, seed=13)
+    acts = torch.tensor(np.random.default_rng(3).uniform(-1, 1, (5, n, 3)), dtype=torch.float32, device="cuda:0")
+    res = []
+    for route, epf in (("0", "4"), ("1", "4"), ("0", "1")):
+        monkeypatch.setenv("BB_ROUTE", route)
+        monkeypatch.setenv("BB_EPW_FULL", epf)
+        env = _make_env(n, "fp64", tcfg)
+        env.set_state(qs, vs, np.zeros((n, 15)), np.zeros(n, np.int32))
+        outs = []
+        for k in range(5):
+            obs, rew, term, trunc, info = env.step(acts[k])
+            outs += [obs.clone(), rew.clone(), info["done_flags"].clone()]
+        q, v, w, st = env.get_state()
+        res.append((outs, q, v, w, env.stats()["slow_path"]))
+        env.close()
+    for outs, q, v, w, slow in res:
+        assert slow > 0  # some env-steps took the full kernel on every route
+        assert np.allclose(q, res[0][1], rtol=0, atol=1e-11)
+        assert np.allclose(v, res[0][2], rtol=1e-9, atol=1e-9)
+        for i, (a, b) in enumerate(zip(outs, res[0][0])):
+            if i % 3 == 2:
+                assert torch.equal(a, b)  # done flags
+            else:
+                assert torch.allclose(a, b, rtol=1e-6, atol=1e-6)
+
+
+@pytest.mark.parametrize("terrain", ["flat", "hills"])
 def test_step_parity_base_tree_contacts(oracle, terrain):
     """env.step from states with base-tree contacts: they are routed to the full
     kernel (stats.slow_path counts full-kernel env-steps), results vs the oracle."""
