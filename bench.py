@@ -71,6 +71,35 @@ def cpu_baseline(seconds: float = 12.0, threads: int = 1) -> dict:
                       f"(fp64 oracle restating the reference step; MuJoCo itself is not available)"}
 
 
+def parity_probe(env, n_probe: int = 64) -> dict:
+    """BASELINE.json's 'per-step qpos L2' next to the throughput: the first
+    n_probe envs' current (post-benchmark) states take one teacher-forced step
+    on the GPU and in the fp64 oracle (the checker, as in tests/); reported are
+    the L2 norms of the qpos / qvel differences.  Envs that terminate in the
+    probe step (the GPU auto-resets them) are skipped.  Flat terrain only."""
+    import numpy as np
+    import torch
+
+    import oracle_lib as O
+
+    O.build()
+    q, v, w, st = env.get_state()
+    a = np.random.default_rng(7).uniform(-1, 1, (env.num_envs, 3)).astype(np.float32)
+    env.step(torch.tensor(a, device=env.device))
+    q1, v1, _, _ = env.get_state()
+    cfg, hf = O.default_cfg(), O.flat_hfield()
+    eq, ev = [], []
+    for e in range(min(n_probe, env.num_envs)):
+        qe, ve, we, se = q[e].copy(), v[e].copy(), w[e].copy(), np.array([st[e]], np.int32)
+        _, _, fl, _, _ = O.env_step(cfg, qe, ve, we, se, a[e], hf)
+        if fl & 5:  # terminated / diverged: reset on the GPU
+            continue
+        eq.append(float(np.linalg.norm(q1[e] - qe)))
+        ev.append(float(np.linalg.norm(v1[e] - ve)))
+    return {"envs": len(eq), "qpos_l2_max": max(eq, default=None), "qpos_l2_median": float(np.median(eq)) if eq else None,
+            "qvel_l2_max": max(ev, default=None), "reference": "fp64 oracle (tests/oracle_lib), teacher-forced one step"}
+
+
 def main() -> None:
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -207,6 +236,8 @@ def main() -> None:
             "stats": stats,
         }
         if world == 1 and not args.no_cpu_baseline:
+            if args.terrain == "flat":
+                line["parity"] = parity_probe(env)
             line["cpu_baseline"] = cpu_baseline(args.cpu_seconds)
             # all host cores granted to this job (OMP_NUM_THREADS; 16 on the GPU box)
             thr = int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or min(16, os.cpu_count() or 1)
