@@ -196,7 +196,7 @@ struct Kin {
 };
 
 template <typename T>
-BB_HD void kinematics(const ModelT<T>& m, const T* q, Kin<T>& k) {
+BB_HD void kinematics_base(const ModelT<T>& m, const T* q, Kin<T>& k) {
   T qb[4] = {q[3], q[4], q[5], q[6]};
   qnormalize(qb);
   q2mat(k.Rb, qb);
@@ -208,24 +208,33 @@ BB_HD void kinematics(const ModelT<T>& m, const T* q, Kin<T>& k) {
   k.c[0] = k.pB[0] + k.RB[2] * m.dz;
   k.c[1] = k.pB[1] + k.RB[5] * m.dz;
   k.c[2] = k.pB[2] + k.RB[8] * m.dz;
+}
+
+// wheel w's local frame and COM (the device forward runs one wheel per lane)
+template <typename T>
+BB_HD void kinematics_wheel(const ModelT<T>& m, const T* q, int w, Kin<T>& k) {
+  // xquat_wheel = xquat_base * body_quat * axisangle(axis, theta - theta0)
+  T th = q[7 + w] - m.qpos0[7 + w];
+  T s = sin(th * T(0.5)), cth = cos(th * T(0.5));
+  T ql[4] = {cth, m.axis[0] * s, m.axis[1] * s, m.axis[2] * s};
+  T qw[4];
+  qmul(qw, m.wq[w], ql);
+  qnormalize(qw);
+  q2mat(k.Rw[w], qw);
+  // origin = anchor - Rw jpos ; COM = origin + Rw cw
+  T d[3] = {m.cw[0] - m.jpos[0], m.cw[1] - m.jpos[1], m.cw[2] - m.jpos[2]};
+  T t[3];
+  mv3(t, k.Rw[w], d);
+  k.wc[w][0] = m.anchor[0] + t[0];
+  k.wc[w][1] = m.anchor[1] + t[1];
+  k.wc[w][2] = m.anchor[2] + t[2];
+}
+
+template <typename T>
+BB_HD void kinematics(const ModelT<T>& m, const T* q, Kin<T>& k) {
+  kinematics_base(m, q, k);
 #pragma unroll
-  for (int w = 0; w < 3; w++) {
-    // xquat_wheel = xquat_base * body_quat * axisangle(axis, theta - theta0)
-    T th = q[7 + w] - m.qpos0[7 + w];
-    T s = sin(th * T(0.5)), cth = cos(th * T(0.5));
-    T ql[4] = {cth, m.axis[0] * s, m.axis[1] * s, m.axis[2] * s};
-    T qw[4];
-    qmul(qw, m.wq[w], ql);
-    qnormalize(qw);
-    q2mat(k.Rw[w], qw);
-    // origin = anchor - Rw jpos ; COM = origin + Rw cw
-    T d[3] = {m.cw[0] - m.jpos[0], m.cw[1] - m.jpos[1], m.cw[2] - m.jpos[2]};
-    T t[3];
-    mv3(t, k.Rw[w], d);
-    k.wc[w][0] = m.anchor[0] + t[0];
-    k.wc[w][1] = m.anchor[1] + t[1];
-    k.wc[w][2] = m.anchor[2] + t[2];
-  }
+  for (int w = 0; w < 3; w++) kinematics_wheel(m, q, w, k);
 }
 
 // ------------------------------------------------------------ mass matrix

@@ -38,7 +38,14 @@ BB_HD int forward(const ModelT<T>& m, const T* q, const T* v, const T* ctrl, T* 
   const unsigned long long f_t0 = clock64();
 #endif
   Kin<T>& k = W.u.pre.k;
+#ifdef __HIP_DEVICE_COMPILE__
+  // base/ball frames on every lane, wheel w's frame on lane w
+  kinematics_base(m, q, k);
+  if (tm.tl < 3) kinematics_wheel(m, q, tm.tl, k);
+  team_sync();
+#else
   kinematics(m, q, k);
+#endif
   Mass<T>& M = W.M;
   build_mass(m, k, M, W.u.pre.Iw);
   {
@@ -52,8 +59,12 @@ BB_HD int forward(const ModelT<T>& m, const T* q, const T* v, const T* ctrl, T* 
 #pragma unroll
     for (int i = 0; i < NV; i++) W.qfs[i] = qfs[i];
   }
+#ifdef __HIP_DEVICE_COMPILE__
+  if (tm.tl < 3) wheel_contact(m, k, v, tm.tl, W.wc[tm.tl]);  // lane w: wheel w (read after the solve's team_sync)
+#else
 #pragma unroll
   for (int w = 0; w < 3; w++) wheel_contact(m, k, v, w, W.wc[w]);
+#endif
   const GStore<T> st{W.g, 1};
   int overflow = 0;
 #if defined(BB_PHASE_CLOCKS) && defined(__HIP_DEVICE_COMPILE__)
