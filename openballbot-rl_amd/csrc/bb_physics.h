@@ -254,36 +254,48 @@ struct Mass {
   T MBrr[3];       // ball rot diagonal (constant)
 };
 
+// wheel w's share of the tree-1 mass matrix: its rotated inertia Iw, the hinge
+// columns Mth/Mrh/Mhh[w] and its terms of the tree-1 first moment (mrw) and
+// inertia about the base origin (IOw); build_mass adds the terms in wheel order
 template <typename T>
-BB_HD void build_mass(const ModelT<T>& m, const Kin<T>& k, Mass<T>& M, T (&Iw)[3][6]) {
+BB_HD void mass_wheel(const ModelT<T>& m, const Kin<T>& k, int w, Mass<T>& M, T* Iw, T* mrw, T* IOw) {
+  const T* c = k.wc[w];
+  sym_rot(Iw, k.Rw[w], m.Iw);
+  mrw[0] = m.mw * c[0]; mrw[1] = m.mw * c[1]; mrw[2] = m.mw * c[2];
+  T cc = dot3(c, c);
+  IOw[0] = Iw[0] + m.mw * (cc - c[0] * c[0]);
+  IOw[1] = Iw[1] + m.mw * (cc - c[1] * c[1]);
+  IOw[2] = Iw[2] + m.mw * (cc - c[2] * c[2]);
+  IOw[3] = Iw[3] - m.mw * c[0] * c[1];
+  IOw[4] = Iw[4] - m.mw * c[0] * c[2];
+  IOw[5] = Iw[5] - m.mw * c[1] * c[2];
+  // hinge motion subspace S = (u; anchor x u) about the base origin
+  const T* u = m.u[w];
+  T ca[3] = {c[0] - m.anchor[0], c[1] - m.anchor[1], c[2] - m.anchor[2]};
+  T vc[3];
+  cross3(vc, u, ca);                       // wheel COM velocity per unit rate
+  T p[3] = {m.mw * vc[0], m.mw * vc[1], m.mw * vc[2]};
+  T L[3], t[3];
+  symv(L, Iw, u);
+  T uIu = dot3(u, L);
+  cross3(t, c, p);
+  L[0] += t[0]; L[1] += t[1]; L[2] += t[2];  // angular momentum about base origin
+  mv3(M.Mth[w], k.Rb, p);
+  M.Mrh[w][0] = L[0]; M.Mrh[w][1] = L[1]; M.Mrh[w][2] = L[2];
+  M.Mhh[w] = uIu + m.mw * dot3(vc, vc) + m.armature;
+}
+
+// the rest of the mass matrix from the wheel terms (mrw[w][3], IOw[w][6])
+template <typename T>
+BB_HD void mass_finish(const ModelT<T>& m, const Kin<T>& k, Mass<T>& M, const T (*mrw)[3], const T (*IOw)[6]) {
   T mr[3] = {m.h0[0], m.h0[1], m.h0[2]};
   T IO[6] = {m.I0O[0], m.I0O[1], m.I0O[2], m.I0O[3], m.I0O[4], m.I0O[5]};
 #pragma unroll
   for (int w = 0; w < 3; w++) {
-    const T* c = k.wc[w];
-    sym_rot(Iw[w], k.Rw[w], m.Iw);
-    mr[0] += m.mw * c[0]; mr[1] += m.mw * c[1]; mr[2] += m.mw * c[2];
-    T cc = dot3(c, c);
-    IO[0] += Iw[w][0] + m.mw * (cc - c[0] * c[0]);
-    IO[1] += Iw[w][1] + m.mw * (cc - c[1] * c[1]);
-    IO[2] += Iw[w][2] + m.mw * (cc - c[2] * c[2]);
-    IO[3] += Iw[w][3] - m.mw * c[0] * c[1];
-    IO[4] += Iw[w][4] - m.mw * c[0] * c[2];
-    IO[5] += Iw[w][5] - m.mw * c[1] * c[2];
-    // hinge motion subspace S = (u; anchor x u) about the base origin
-    const T* u = m.u[w];
-    T ca[3] = {c[0] - m.anchor[0], c[1] - m.anchor[1], c[2] - m.anchor[2]};
-    T vc[3];
-    cross3(vc, u, ca);                       // wheel COM velocity per unit rate
-    T p[3] = {m.mw * vc[0], m.mw * vc[1], m.mw * vc[2]};
-    T L[3], t[3];
-    symv(L, Iw[w], u);
-    T uIu = dot3(u, L);
-    cross3(t, c, p);
-    L[0] += t[0]; L[1] += t[1]; L[2] += t[2];  // angular momentum about base origin
-    mv3(M.Mth[w], k.Rb, p);
-    M.Mrh[w][0] = L[0]; M.Mrh[w][1] = L[1]; M.Mrh[w][2] = L[2];
-    M.Mhh[w] = uIu + m.mw * dot3(vc, vc) + m.armature;
+#pragma unroll
+    for (int i = 0; i < 3; i++) mr[i] += mrw[w][i];
+#pragma unroll
+    for (int i = 0; i < 6; i++) IO[i] += IOw[w][i];
   }
   M.mt = m.m0 + 3 * m.mw;
   M.mr[0] = mr[0]; M.mr[1] = mr[1]; M.mr[2] = mr[2];
@@ -298,6 +310,14 @@ BB_HD void build_mass(const ModelT<T>& m, const Kin<T>& k, Mass<T>& M, T (&Iw)[3
   M.MBrr[0] = m.IB + m.mB * dz * dz;
   M.MBrr[1] = m.IB + m.mB * dz * dz;
   M.MBrr[2] = m.IB;
+}
+
+template <typename T>
+BB_HD void build_mass(const ModelT<T>& m, const Kin<T>& k, Mass<T>& M, T (&Iw)[3][6]) {
+  T mrw[3][3], IOw[3][6];
+#pragma unroll
+  for (int w = 0; w < 3; w++) mass_wheel(m, k, w, M, Iw[w], mrw[w], IOw[w]);
+  mass_finish(m, k, M, mrw, IOw);
 }
 
 template <typename T>
@@ -379,18 +399,46 @@ BB_HD void body_force(T m, const T* c, const T* Ic, const T* Aw, const T* Av, co
   cross3(t, Vw, pv); fl[0] = pa[0] + t[0]; fl[1] = pa[1] + t[1]; fl[2] = pa[2] + t[2];
 }
 
-// qfrc_bias = C(q,v) v + gravity  (mj_rne with flg_acc = 0)
+// tree-1 motion at the base origin (base-local): angular w0, linear vl and the
+// spatial acceleration a0 = Rb' (0,0,g) + vl x w0
 template <typename T>
-BB_HD void bias_forces(const ModelT<T>& m, const Kin<T>& k, const T (&Iw)[3][6], const T* v, T* bias) {
-  // ---- tree 1, base-local coordinates about the base origin
-  T w0[3] = {v[3], v[4], v[5]};
-  T vl[3];
+BB_HD void bias_base_motion(const ModelT<T>& m, const Kin<T>& k, const T* v, T* w0, T* vl, T* a0) {
+  w0[0] = v[3]; w0[1] = v[4]; w0[2] = v[5];
   mtv3(vl, k.Rb, v);
-  T a0[3], t[3];
+  T t[3];
   cross3(t, vl, w0);
-  a0[0] = m.grav * k.Rb[6] + t[0];  // Rb' (0,0,g) + v x w   (spatial accel at origin)
+  a0[0] = m.grav * k.Rb[6] + t[0];
   a0[1] = m.grav * k.Rb[7] + t[1];
   a0[2] = m.grav * k.Rb[8] + t[2];
+}
+
+// wheel w's RNE force (fa; fl) about the base origin; returns qfrc_bias[6+w]
+template <typename T>
+BB_HD T bias_wheel(const ModelT<T>& m, const Kin<T>& k, const T* Iw, const T* v, int w, const T* w0, const T* vl,
+                   const T* a0, T* fa, T* fl) {
+  const T* u = m.u[w];
+  T au[3];
+  cross3(au, m.anchor, u);           // S = (u; anchor x u)
+  T qd = v[6 + w];
+  T Vw[3] = {w0[0] + qd * u[0], w0[1] + qd * u[1], w0[2] + qd * u[2]};
+  T Vv[3] = {vl[0] + qd * au[0], vl[1] + qd * au[1], vl[2] + qd * au[2]};
+  // A = A0 + qd (V0 xm S) ; V0 xm S = (w x u; w x au + v x u)
+  T x1[3], x2[3], x3[3];
+  cross3(x1, w0, u);
+  cross3(x2, w0, au);
+  cross3(x3, vl, u);
+  T Aw[3] = {qd * x1[0], qd * x1[1], qd * x1[2]};
+  T Av[3] = {a0[0] + qd * (x2[0] + x3[0]), a0[1] + qd * (x2[1] + x3[1]), a0[2] + qd * (x2[2] + x3[2])};
+  body_force(m.mw, k.wc[w], Iw, Aw, Av, Vw, Vv, fa, fl);
+  return dot3(u, fa) + dot3(au, fl);
+}
+
+// qfrc_bias from the wheel forces fw[w] = (fa; fl): base composite, the
+// wheel sums in wheel order, and the ball (bias[6..8] are set by the caller)
+template <typename T>
+BB_HD void bias_finish(const ModelT<T>& m, const Kin<T>& k, const T* v, const T (*fw)[6], T* bias) {
+  T w0[3], vl[3], a0[3], t[3];
+  bias_base_motion(m, k, v, w0, vl, a0);
   const T zero[3] = {0, 0, 0};
   // base composite: mass m0, COM h0/m0, inertia about COM derived from I0O
   T Fa[3], Fl[3];
@@ -404,24 +452,8 @@ BB_HD void bias_forces(const ModelT<T>& m, const Kin<T>& k, const T (&Iw)[3][6],
   }
 #pragma unroll
   for (int w = 0; w < 3; w++) {
-    const T* u = m.u[w];
-    T au[3];
-    cross3(au, m.anchor, u);           // S = (u; anchor x u)
-    T qd = v[6 + w];
-    T Vw[3] = {w0[0] + qd * u[0], w0[1] + qd * u[1], w0[2] + qd * u[2]};
-    T Vv[3] = {vl[0] + qd * au[0], vl[1] + qd * au[1], vl[2] + qd * au[2]};
-    // A = A0 + qd (V0 xm S) ; V0 xm S = (w x u; w x au + v x u)
-    T x1[3], x2[3], x3[3];
-    cross3(x1, w0, u);
-    cross3(x2, w0, au);
-    cross3(x3, vl, u);
-    T Aw[3] = {qd * x1[0], qd * x1[1], qd * x1[2]};
-    T Av[3] = {a0[0] + qd * (x2[0] + x3[0]), a0[1] + qd * (x2[1] + x3[1]), a0[2] + qd * (x2[2] + x3[2])};
-    T fa[3], fl[3];
-    body_force(m.mw, k.wc[w], Iw[w], Aw, Av, Vw, Vv, fa, fl);
-    bias[6 + w] = dot3(u, fa) + dot3(au, fl);
-    Fa[0] += fa[0]; Fa[1] += fa[1]; Fa[2] += fa[2];
-    Fl[0] += fl[0]; Fl[1] += fl[1]; Fl[2] += fl[2];
+    Fa[0] += fw[w][0]; Fa[1] += fw[w][1]; Fa[2] += fw[w][2];
+    Fl[0] += fw[w][3]; Fl[1] += fw[w][4]; Fl[2] += fw[w][5];
   }
   mv3(bias, k.Rb, Fl);
   bias[3] = Fa[0]; bias[4] = Fa[1]; bias[5] = Fa[2];
@@ -437,6 +469,16 @@ BB_HD void bias_forces(const ModelT<T>& m, const Kin<T>& k, const T (&Iw)[3][6],
   body_force(m.mB, cB, IcB, zero, aB, wB, vB, fa, fl);
   mv3(bias + 9, k.RB, fl);
   bias[12] = fa[0]; bias[13] = fa[1]; bias[14] = fa[2];
+}
+
+// qfrc_bias = C(q,v) v + gravity  (mj_rne with flg_acc = 0)
+template <typename T>
+BB_HD void bias_forces(const ModelT<T>& m, const Kin<T>& k, const T (&Iw)[3][6], const T* v, T* bias) {
+  T w0[3], vl[3], a0[3], fw[3][6];
+  bias_base_motion(m, k, v, w0, vl, a0);
+#pragma unroll
+  for (int w = 0; w < 3; w++) bias[6 + w] = bias_wheel(m, k, Iw[w], v, w, w0, vl, a0, fw[w], fw[w] + 3);
+  bias_finish(m, k, v, fw, bias);
 }
 
 // ------------------------------------------------------------- contacts

@@ -22,7 +22,8 @@ struct EnvCfg {
 };
 
 // mj_forward for this model: returns qacc in acc (acc holds the warm start on
-// entry).  Executed by a team of tm.L lanes; the pre-phase (kinematics, mass,
+// entry).  Executed by a team of tm.L lanes; the per-wheel pre-phase work (frames,
+// mass terms, RNE forces, contacts) runs one wheel per lane, the rest of the pre-phase (kinematics, mass,
 // bias, collision) is computed redundantly by every lane of the team, the
 // constraint solve is team-parallel (bb_solve.h).
 template <typename T, bool BODY = true>
@@ -47,6 +48,36 @@ BB_HD int forward(const ModelT<T>& m, const T* q, const T* v, const T* ctrl, T* 
   kinematics(m, q, k);
 #endif
   Mass<T>& M = W.M;
+#ifdef __HIP_DEVICE_COMPILE__
+  {
+    // lane w: wheel w's mass terms, RNE force and contact; W.H (free until
+    // mass_dense_team) holds the per-wheel terms that every lane then sums
+    // in wheel order
+    T (*mrw)[3] = reinterpret_cast<T (*)[3]>(W.H);
+    T (*IOw)[6] = reinterpret_cast<T (*)[6]>(W.H + 9);
+    T (*fw)[6] = reinterpret_cast<T (*)[6]>(W.H + 27);
+    static_assert(NH >= 45, "per-wheel terms do not fit W.H");
+    if (tm.tl < 3) {
+      const int w = tm.tl;
+      mass_wheel(m, k, w, M, W.u.pre.Iw[w], mrw[w], IOw[w]);
+      T w0[3], vl[3], a0[3];
+      bias_base_motion(m, k, v, w0, vl, a0);
+      const T qb = -bias_wheel(m, k, W.u.pre.Iw[w], v, w, w0, vl, a0, fw[w], fw[w] + 3);
+      const T cw = w == 0 ? ctrl[0] : (w == 1 ? ctrl[1] : ctrl[2]);  // no dynamic index into registers
+      W.qfs[6 + w] = qb + (-m.damping * v[6 + w] + cw);
+      wheel_contact(m, k, v, w, W.wc[w]);  // read after the solve's team_sync
+    }
+    team_sync();
+    mass_finish(m, k, M, mrw, IOw);
+    // qfrc_smooth = -bias + passive + actuation, straight to the workspace
+    T qfs[NV];
+    bias_finish(m, k, v, fw, qfs);
+#pragma unroll
+    for (int i = 0; i < NV; i++)
+      if (i < 6 || i > 8) W.qfs[i] = -qfs[i];
+    team_sync();  // W.H free again (candidate list of the body collision)
+  }
+#else
   build_mass(m, k, M, W.u.pre.Iw);
   {
     // qfrc_smooth = -bias + passive + actuation, straight to the workspace
@@ -59,9 +90,6 @@ BB_HD int forward(const ModelT<T>& m, const T* q, const T* v, const T* ctrl, T* 
 #pragma unroll
     for (int i = 0; i < NV; i++) W.qfs[i] = qfs[i];
   }
-#ifdef __HIP_DEVICE_COMPILE__
-  if (tm.tl < 3) wheel_contact(m, k, v, tm.tl, W.wc[tm.tl]);  // lane w: wheel w (read after the solve's team_sync)
-#else
 #pragma unroll
   for (int w = 0; w < 3; w++) wheel_contact(m, k, v, w, W.wc[w]);
 #endif
