@@ -145,7 +145,14 @@ __global__ __launch_bounds__(64) void step_kernel(ModelT<T> mg, EnvCfg cfg, Dev 
   extern __shared__ __align__(16) unsigned char smem[];
   // list launches are sized for every env; workgroups past the list end leave
   // before touching LDS (on flat terrain the full-kernel lists are empty)
-  if (elist && int(blockIdx.x) * epw >= *ecount) return;
+  // XCD-aware workgroup order: the dispatcher deals workgroups round-robin over
+  // the 8 XCDs (workgroup b runs on XCD b % 8), so give each XCD a contiguous
+  // range of env groups.  A 128-B line of SoA state holds 16 fp64 envs, i.e.
+  // four 4-env workgroups: in launch order those sat on four XCDs and the line
+  // was fetched into four L2s.  Any permutation is exact (envs are independent).
+  const int nwg = int(gridDim.x), b = int(blockIdx.x);
+  const int g = (nwg & 7) ? b : (b & 7) * (nwg >> 3) + (b >> 3);
+  if (elist && g * epw >= *ecount) return;
   // model constants staged in LDS once per workgroup: uniform-address LDS
   // reads broadcast, and ~150 uniform doubles no longer overflow the SGPRs
   __shared__ ModelT<T> ms;
@@ -155,7 +162,7 @@ __global__ __launch_bounds__(64) void step_kernel(ModelT<T> mg, EnvCfg cfg, Dev 
   const Team tm{L, int(threadIdx.x) & (L - 1)};
   const int team = threadIdx.x / L;
   if (team >= epw) return;
-  int e = blockIdx.x * epw + team;
+  int e = g * epw + team;
   if (elist) {  // env list of this launch (ascending env ids)
     if (e >= *ecount) return;
     e = elist[e];
