@@ -105,6 +105,10 @@ def main() -> None:
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=500)
     ap.add_argument("--warmup", type=int, default=300)
+    ap.add_argument("--burn-in", type=int, default=400,
+                    help="untimed steps before the warmup that bring the envs from the common reset state into the "
+                         "steady-state mix of episode ages (drop/settle, balancing, falls and auto-resets), so that a "
+                         "short --warmup does not time the 4 cm free fall every env starts in")
     ap.add_argument("--envs", type=int, default=4096, help="envs per GPU")
     ap.add_argument("--precision", default="fp64", choices=["fp32", "fp64"])
     ap.add_argument("--terrain", default="flat")
@@ -160,7 +164,7 @@ def main() -> None:
             env._render(force=False)
     g = torch.Generator(device=dev).manual_seed(1234 + rank)
     pool = torch.rand(64, n, 3, generator=g, device=dev) * 2 - 1  # random actions resident in HBM
-    for i in range(args.warmup):
+    for i in range(args.burn_in + args.warmup):
         step(pool[i % 64])
     torch.cuda.synchronize()
     if world > 1:
@@ -216,11 +220,12 @@ def main() -> None:
             "scaling": "weak",
             "vs_baseline": None,
             "dtype": "f64" if args.precision == "fp64" else "f32",
-            "data": "synthetic (uniform random actions in [-1,1], resident in HBM)",
+            "data": "synthetic (uniform random actions in [-1,1], resident in HBM; "
+                    f"{args.burn_in} untimed burn-in steps into the steady-state episode mix before the warmup)",
             "config": {"workload": f"{n} envs/GPU, {args.terrain} terrain, random actions "
                                    f"(BASELINE configs[{1 if args.terrain == 'flat' else 2}])",
                        "n_terrains": env.n_terrains, "depth_cameras": bool(args.cameras),
-                       "hip_graph": graph is not None,
+                       "hip_graph": graph is not None, "burn_in_steps": args.burn_in,
                        "envs_per_gpu": n, "total_envs": n * world, "precision": args.precision,
                        "parallelism": f"env-sharded x{world} (no collective on the step path)",
                        "launch": launch},

@@ -150,9 +150,24 @@ __global__ __launch_bounds__(64) void step_kernel(ModelT<T> mg, EnvCfg cfg, Dev 
   // range of env groups.  A 128-B line of SoA state holds 16 fp64 envs, i.e.
   // four 4-env workgroups: in launch order those sat on four XCDs and the line
   // was fetched into four L2s.  Any permutation is exact (envs are independent).
+  // List launches are sized for every env but only the first na = ceil(count /
+  // epw) workgroups have work: the permutation is taken over those (rounded up
+  // to a multiple of 8), so the active groups spread over all eight XCDs
+  // instead of piling onto the first few.
   const int nwg = int(gridDim.x), b = int(blockIdx.x);
-  const int g = (nwg & 7) ? b : (b & 7) * (nwg >> 3) + (b >> 3);
-  if (elist && g * epw >= *ecount) return;
+  int g;
+  if (elist) {
+    const int na = (*ecount + epw - 1) / epw, nb = (na + 7) & ~7;
+    if (nb > nwg) {
+      g = b;  // too few workgroups in the grid for the rounded-up permutation
+    } else {
+      if (b >= nb) return;
+      g = (b & 7) * (nb >> 3) + (b >> 3);
+    }
+    if (g >= na) return;
+  } else {
+    g = (nwg & 7) ? b : (b & 7) * (nwg >> 3) + (b >> 3);
+  }
   // model constants staged in LDS once per workgroup: uniform-address LDS
   // reads broadcast, and ~150 uniform doubles no longer overflow the SGPRs
   __shared__ ModelT<T> ms;

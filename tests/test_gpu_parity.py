@@ -227,10 +227,12 @@ def test_step_routes_agree(oracle, terrain, monkeypatch):
     full kernel's envs per wave (BB_EPW_FULL) only move work between kernels:
     the same states and outputs over several steps from base-tree-contact states.  An env
     the predictor sends to the full kernel without a base-tree contact runs the full
-    kernel's instantiation of the same physics, so agreement is to rounding, not bitwise."""
+    kernel's instantiation of the same physics, so agreement is to rounding, not bitwise.
+    128 envs = 32 workgroups, so the list launches' XCD-aware permutation over the
+    active workgroups is exercised."""
     from ballbot_gym.terrain import generate_hills_terrain  # noqa: F401  (hills bank via the env config)
 
-    n = 64
+    n = 128
     tcfg = {"type": "flat", "config": {}} if terrain == "flat" else {"type": "hills", "config": {"seed": 7}}
     qs, vs = _body_contact_states(oracle, n, seed=13)
     acts = torch.tensor(np.random.default_rng(3).uniform(-1, 1, (5, n, 3)), dtype=torch.float32, device="cuda:0")

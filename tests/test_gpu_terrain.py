@@ -62,15 +62,19 @@ def test_perlin_full_seed_space():
 
 
 def test_step_parity_on_perlin(oracle):
-    """Teacher-forced fp64 steps on a GPU-generated perlin terrain vs the oracle on the restated field."""
+    """Teacher-forced fp64 steps on a GPU-generated perlin terrain vs the oracle on the restated field.
+
+    128 envs at 4 per workgroup = 32 workgroups: the relief bank takes the
+    predict/split route, whose list launches use the XCD-aware workgroup
+    permutation over the active list (non-trivial from 9 active workgroups)."""
     import traj
     from ballbot_gym.terrain.perlin import generate_perlin_terrain
     from test_gpu_parity import TOL, _teacher_forced
 
-    env = _env({}, n_terrains=1, n_envs=32, seed=10)
+    env = _env({}, n_terrains=1, n_envs=128, seed=10)
     s = int(env.terrain_seeds[0])
     hf = generate_perlin_terrain(293, seed=s).astype(np.float32)
     assert np.array_equal(env.hfield(0), hf)
-    rec = traj.record(n_envs=32, n_steps=60, hfield=hf, seed=9)
+    rec = traj.record(n_envs=128, n_steps=60, hfield=hf, seed=9)
     _teacher_forced(env, rec, TOL["fp64"])
     env.close()

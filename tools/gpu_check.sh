@@ -10,3 +10,6 @@ timeout -k 10 300 python -u bench.py > gpurun_out/bench_fp64.json 2> gpurun_out/
 cat gpurun_out/bench_fp64.json
 timeout -k 10 300 python -u bench.py --precision fp32 --no-cpu-baseline > gpurun_out/bench_fp32.json 2> gpurun_out/bench_fp32.err || exit 1
 cat gpurun_out/bench_fp32.json
+# the driver's own short form (steady state comes from the burn-in, not the warmup)
+timeout -k 10 300 python -u bench.py --steps 20 --warmup 5 --no-cpu-baseline > gpurun_out/bench_short.json 2> gpurun_out/bench_short.err || exit 1
+cat gpurun_out/bench_short.json
