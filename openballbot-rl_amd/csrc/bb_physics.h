@@ -138,7 +138,44 @@ template <typename T> BB_HD void sym_rot(T* out, const T* R, const T* S) {  // R
 }
 template <typename T> BB_HD T clampT(T x, T lo, T hi) { return x < lo ? lo : (x > hi ? hi : x); }
 template <typename T> BB_HD T maxT(T a, T b) { return a > b ? a : b; }
+// 1/sqrt(x): the device's reciprocal square root; the host test builds divide
+template <typename T> BB_HD T rsqrtT(T x) {
+#ifdef __HIP_DEVICE_COMPILE__
+  return rsqrt(x);
+#else
+  return T(1) / sqrt(x);
+#endif
+}
 template <typename T> BB_HD T minT(T a, T b) { return a < b ? a : b; }
+// Line-search arithmetic (the trial points only steer the search; the solver's
+// stopping test and the returned qacc do not depend on these roundings):
+// 1/sqrt(x) and a / b from the hardware estimates plus one Newton step
+// (relative error ~1e-13 in double) instead of the correctly rounded sequences.
+template <typename T> BB_HD T rsqrt_ls(T x) {
+#ifdef __HIP_DEVICE_COMPILE__
+  if constexpr (sizeof(T) == 8) {
+    const double r = __builtin_amdgcn_rsq(x);
+    return r * fma(-0.5 * x * r, r, 1.5);
+  } else {
+    return __builtin_amdgcn_rsqf(x);
+  }
+#else
+  return T(1) / sqrt(x);
+#endif
+}
+template <typename T> BB_HD T div_ls(T a, T b) {
+#ifdef __HIP_DEVICE_COMPILE__
+  if constexpr (sizeof(T) == 8) {
+    double r = __builtin_amdgcn_rcp(b);
+    r = fma(r, fma(-b, r, 1.0), r);
+    return a * r;
+  } else {
+    return a * __builtin_amdgcn_rcpf(b);
+  }
+#else
+  return a / b;
+#endif
+}
 
 // quaternion (w,x,y,z)
 template <typename T> BB_HD void qmul(T* r, const T* a, const T* b) {
@@ -503,7 +540,7 @@ BB_HD void frame_from_normal(const T* n, T* t1, T* t2) {
   if (fabs(n[1]) < T(0.5)) y[1] = 1; else y[2] = 1;
   T d = dot3(n, y);
   t1[0] = y[0] - d * n[0]; t1[1] = y[1] - d * n[1]; t1[2] = y[2] - d * n[2];
-  T inv = rsqrt(dot3(t1, t1));
+  T inv = rsqrtT(dot3(t1, t1));
   t1[0] *= inv; t1[1] *= inv; t1[2] *= inv;
   cross3(t2, n, t1);
 }

@@ -20,6 +20,8 @@ namespace bb {
 
 #ifdef BB_SOLVE_STATS
 static long g_ls_evals = 0;
+static long g_ls_hist[16] = {0};  // line-search evaluations per Newton iteration
+static long g_alpha1 = 0;         // Newton iterations whose first evaluation (alpha = 1) was accepted
 #endif
 
 // Diagnostic build only (-DBB_PHASE_CLOCKS): per-phase s_memtime cycles,
@@ -190,19 +192,123 @@ BB_HD void chol_team(T* H, const T* hd, const Team& tm) {
   team_sync();
 }
 
-// accumulate phi'(alpha), phi''(alpha) and the term magnitude for one contact
+// One contact along the Newton direction s, in the cone variables of
+// mj_constraintUpdate's elliptic zones: U(alpha) = u0 + alpha du with
+// U = (mu jar0, f1 jar1, f2 jar2) and jar = J (a + alpha s) - aref.  Prepared
+// once per Newton iteration; each line-search evaluation then costs the zone
+// tests and the closed-form derivatives of the contact's cost:
+//   top     (N >= mu T)            0
+//   bottom  (mu N + T <= 0)        1/2 sum_r D_r jar_r^2   -> b0 + alpha b1, b1
+//   middle                         1/2 Dm g^2, g = N - mu T -> Dm g g', Dm (g'^2 + g g'')
+// with T(alpha) = |U_t(alpha)|, T' = U_t.dU_t / T, T'' = (|dU_t|^2 - T'^2) / T.
+// kink: the alpha where T is smallest, if the contact is in the middle zone
+// there.  Near it phi' turns by ~Dm g mu |dU_t| within a width of
+// T_min / |dU_t| (for a wheel, the axle friction 0.001 of ballbot.xml:90-92
+// sets T_min): a near-kink that the line search evaluates before stepping
+// across (LineSearch::update); -1 when there is none.
 template <typename T>
-BB_HD void ls_contact(const T* c6, T alpha, T mu, T f1, T f2, const T* D, T& d1, T& d2, T& dm) {
-  const T x[3] = {c6[3], c6[4], c6[5]};
-  T jr[3] = {c6[0] + alpha * x[0], c6[1] + alpha * x[1], c6[2] + alpha * x[2]};
-  T f[3], Cc[6];
-  cone_eval(jr, mu, f1, f2, D, f, Cc);
-  const T fx = f[0] * x[0] + f[1] * x[1] + f[2] * x[2];
-  d1 -= fx;
-  dm += fabs(f[0] * x[0]) + fabs(f[1] * x[1]) + fabs(f[2] * x[2]);
-  d2 += Cc[0] * x[0] * x[0] + Cc[1] * x[1] * x[1] + Cc[2] * x[2] * x[2] +
-        2 * (Cc[3] * x[0] * x[1] + Cc[4] * x[0] * x[2] + Cc[5] * x[1] * x[2]);
-}
+struct LsTerm {
+  T u0[3], du[3], mu, Dm, b0, b1, vv, kink;
+  BB_HD void prep(const T* j0, const T* x, T mu_, T f1, T f2, const T* D, T Dm_) {
+    mu = mu_;
+    Dm = Dm_;
+    u0[0] = mu * j0[0]; u0[1] = f1 * j0[1]; u0[2] = f2 * j0[2];
+    du[0] = mu * x[0]; du[1] = f1 * x[1]; du[2] = f2 * x[2];
+    b0 = D[0] * j0[0] * x[0] + D[1] * j0[1] * x[1] + D[2] * j0[2] * x[2];
+    b1 = D[0] * x[0] * x[0] + D[1] * x[1] * x[1] + D[2] * x[2] * x[2];
+    vv = du[1] * du[1] + du[2] * du[2];
+    kink = T(-1);
+    if (vv > 0) {
+      const T ak = -(u0[1] * du[1] + u0[2] * du[2]) / vv;
+      const T N = u0[0] + ak * du[0], U1 = u0[1] + ak * du[1], U2 = u0[2] + ak * du[2];
+      const T Tn = sqrt(U1 * U1 + U2 * U2);
+      if (ak > 0 && N < mu * Tn && mu * N + Tn > 0) kink = ak;
+    }
+  }
+  BB_HD void none() {
+    u0[0] = u0[1] = u0[2] = du[0] = du[1] = du[2] = T(0);
+    u0[0] = T(1);  // separated: top zone at every alpha
+    mu = Dm = b0 = b1 = vv = T(0);
+    kink = T(-1);
+  }
+  // adds phi_c'(alpha), phi_c''(alpha) and a magnitude bound of the terms of phi_c'
+  BB_HD void eval(T alpha, T& d1, T& d2, T& dm) const {
+    const T N = u0[0] + alpha * du[0], U1 = u0[1] + alpha * du[1], U2 = u0[2] + alpha * du[2];
+    const T t2 = U1 * U1 + U2 * U2;
+    const T rt = t2 > 0 ? rsqrt_ls(t2) : T(0);
+    const T Tn = t2 * rt;
+    const bool top = N >= mu * Tn || (Tn <= 0 && N >= 0);
+    const bool bot = !top && (mu * N + Tn <= 0 || (Tn <= 0 && N < 0));
+    const T g = N - mu * Tn;
+    const T tp = (U1 * du[1] + U2 * du[2]) * rt;
+    const T gp = du[0] - mu * tp;
+    const T tpp = (vv - tp * tp) * rt;
+    const T Dg = Dm * g;
+    const T m1 = Dg * gp, m2 = Dm * gp * gp - mu * Dg * tpp;
+    const T q1 = b0 + alpha * b1;
+    d1 += top ? T(0) : (bot ? q1 : m1);
+    d2 += top ? T(0) : (bot ? b1 : m2);
+    dm += top ? T(0) : (bot ? fabs(b0) + fabs(alpha * b1) : fabs(Dg) * (fabs(du[0]) + mu * fabs(tp)));
+  }
+};
+
+// One update of the exact line search on phi'(alpha) (phi convex, phi'
+// continuous and nondecreasing): the evaluation (alpha, d1 = phi', d2 = phi'')
+// tightens the bracket [lo, hi] and picks the next alpha.  1-D Newton from the
+// latest point while it lands inside the bracket; Illinois false position when
+// two evaluations in a row fall on the same side, or when the latest
+// evaluation did not halve the bracket.  The second case is a Newton 2-cycle:
+// a stiff drive-direction row (R scaled by (0.001/1)^2, ballbot.xml:90-92)
+// changes cone zone between lo and hi, so phi'' jumps by ~1e6 there and the
+// Newton steps from either side overshoot onto the other side, keeping the
+// bracket width for up to ls_maxiter evaluations.
+//
+// Kinks (LsTerm::kink): a step that would cross a contact's near-kink stops
+// at it instead (snap); the bracket then closes on the kink from either side
+// in a few evaluations, where Newton and false position from the far smooth
+// parts otherwise creep.
+template <typename T>
+struct LineSearch {
+  T lo, dlo, hi, dhi, alpha, flo, fhi, prev;
+  int side, same;
+  BB_HD void init(T d0) {
+    lo = 0; dlo = d0; hi = -1; dhi = 0; alpha = 1; flo = d0; fhi = 0; prev = 0;
+    side = 0; same = 0;
+  }
+  // is the kink k strictly between the last evaluated point and the proposed
+  // one, and inside the bracket?
+  BB_HD bool crosses(T k) const {
+    const bool between = alpha > prev ? (k > prev && k < alpha) : (k < prev && k > alpha);
+    return between && k > lo && (hi < 0 || k < hi);
+  }
+  // of two crossed kinks, the one nearer the last evaluated point
+  BB_HD T nearer(T a, T b) const { return fabs(a - prev) <= fabs(b - prev) ? a : b; }
+  BB_HD void update(T d1, T d2) {
+    prev = alpha;
+    const T w0 = hi >= 0 ? hi - lo : T(-1);  // bracket width before this evaluation (-1: none yet)
+    const int sd = d1 < 0 ? -1 : 1;
+    same = sd == side ? same + 1 : 0;
+    side = sd;
+    if (sd < 0) {
+      lo = alpha; dlo = d1; flo = d1;
+      if (same > 0 && hi >= 0) fhi *= T(0.5);
+    } else {
+      hi = alpha; dhi = d1; fhi = d1;
+      if (same > 0) flo *= T(0.5);
+    }
+    T an = alpha - div_ls(d1, maxT(d2, T(1e-30)));
+    if (hi < 0) {
+      if (!(an > lo)) an = lo > 0 ? 2 * lo : T(1);
+    } else if (!(an > lo && an < hi) || (w0 >= 0 && hi - lo > T(0.5) * w0)) {
+      const T fp = lo - div_ls(flo * (hi - lo), fhi - flo);
+      an = (fp > lo && fp < hi) ? fp : T(0.5) * (lo + hi);
+    }
+    alpha = an;
+  }
+  // an unconverged search falls back to the last point with phi' < 0 (a
+  // guaranteed decrease for convex phi)
+  BB_HD T fallback() const { return lo > 0 ? lo : (hi > 0 ? hi * dlo / (dlo - dhi) : T(0)); }
+};
 
 // Newton on f(a) (mj_solNewton).  a: warm start in, qacc out (replicated in
 // every lane of the team).  Returns the iteration count (team-uniform).
@@ -348,74 +454,65 @@ BB_HD int solve_team(const ModelT<T>& m, EnvWork<T>& W, const T* qfs, int ng, T*
     T sMs = 0, gs = 0;
 #pragma unroll
     for (int i = 0; i < NV; i++) { sMs += s[i] * Ms[i]; gs += s[i] * (Ma[i] - qfs[i]); }
-    T lsc[3 + MAXG][6], lsD[3 + MAXG];  // line-search cache (host / reference path: plenty of stack)
+    LsTerm<T> lst[3 + MAXG];  // line-search terms (host / reference path: plenty of stack)
+    const T kdw = T(1) / (mu_w * mu_w * (1 + mu_w * mu_w));
     for (int c = tm.tl; c < nc; c += tm.L) {
-      T* c6 = lsc[c];
+      T j0[3], x[3];
       if (c < 3) {
         const WheelCon<T>& C = W.wc[c];
 #pragma unroll
-        for (int r = 0; r < 3; r++) { c6[r] = wheel_dot(C, c, r, a) - C.aref[r]; c6[3 + r] = wheel_dot(C, c, r, s); }
+        for (int r = 0; r < 3; r++) { j0[r] = wheel_dot(C, c, r, a) - C.aref[r]; x[r] = wheel_dot(C, c, r, s); }
+        lst[c].prep(j0, x, mu_w, f1w, f2w, C.D, C.D[0] * kdw);
       } else {
         const T* gc = W.g + (c - 3) * NGF;
         T J[3][6], ar[3], D;
         ground_contact(m, gc, W.P.RB, W.vi, J, ar, D);
 #pragma unroll
-        for (int r = 0; r < 3; r++) { c6[r] = ground_dot(J, r, a) - ar[r]; c6[3 + r] = ground_dot(J, r, s); }
-        lsD[c] = D;
+        for (int r = 0; r < 3; r++) { j0[r] = ground_dot(J, r, a) - ar[r]; x[r] = ground_dot(J, r, s); }
+        const T Dv[3] = {D, D, D};
+        lst[c].prep(j0, x, T(1), T(1), T(1), Dv, D * T(0.5));
       }
     }
-    // 1-D Newton on phi'(alpha) from the full step, safeguarded by an
-    // Illinois false-position step on the bracket [lo, hi] (phi' is
-    // continuous and nondecreasing, but its slope jumps by ~1e6 when a stiff
-    // drive-direction row changes cone zone, where plain Newton creeps).
-    T lo = 0, dlo = d0, hi = -1, dhi = 0, alpha = 1;
-    T flo = d0, fhi = 0;  // Illinois-weighted end values
-    int side = 0, same = 0;
+    // exact line search from the full step (LineSearch)
+    LineSearch<T> lsr;
+    lsr.init(d0);
+    const T& alpha = lsr.alpha;
     bool ls_ok = false;
     for (int ls = 1; ls <= m.ls_maxiter; ls++) {
 #ifdef BB_SOLVE_STATS
       g_ls_evals++;
 #endif
       T d1p = 0, d2p = 0, dmp = 0;
-      for (int c = tm.tl; c < nc; c += tm.L) {
-        if (c < 3) {
-          const T Dw[3] = {W.wc[c].D[0], W.wc[c].D[1], W.wc[c].D[2]};
-          ls_contact(lsc[c], alpha, mu_w, f1w, f2w, Dw, d1p, d2p, dmp);
-        } else {
-          const T D = lsD[c];
-          const T Dv[3] = {D, D, D};
-          ls_contact(lsc[c], alpha, T(1), T(1), T(1), Dv, d1p, d2p, dmp);
-        }
-      }
+      for (int c = tm.tl; c < nc; c += tm.L) lst[c].eval(alpha, d1p, d2p, dmp);
       const T d1 = gs + alpha * sMs + team_sum(tm, d1p);
       const T d2 = sMs + team_sum(tm, d2p);
       const T dmag = fabs(gs) + fabs(alpha * sMs) + team_sum(tm, dmp);
-      if (fabs(d1) <= m.ls_tol * fabs(d0) || fabs(d1) <= T(32) * eps_of<T>() * dmag) { ls_ok = true; break; }
+#ifdef BB_LS_TRACE
+      printf("    ls %d alpha %.17g d1 %.6e d2 %.6e d0 %.6e\n", ls, double(alpha), double(d1), double(d2), double(d0));
+#endif
+      if (fabs(d1) <= m.ls_tol * fabs(d0) || fabs(d1) <= T(32) * eps_of<T>() * dmag) {
+        ls_ok = true;
+#ifdef BB_SOLVE_STATS
+        g_ls_hist[ls < 15 ? ls : 15]++;
+        if (ls == 1) g_alpha1++;
+#endif
+        break;
+      }
       if (!(d1 == d1)) break;
-      const int sd = d1 < 0 ? -1 : 1;
-      same = sd == side ? same + 1 : 0;
-      side = sd;
-      if (sd < 0) {
-        lo = alpha; dlo = d1; flo = d1;
-        if (same > 0 && hi >= 0) fhi *= T(0.5);
-      } else {
-        hi = alpha; dhi = d1; fhi = d1;
-        if (same > 0) flo *= T(0.5);
+      lsr.update(d1, d2);
+#ifndef BB_NO_KINK
+      {
+        T kn = T(-1);
+        for (int c = 0; c < nc; c++)
+          if (lsr.crosses(lst[c].kink)) kn = kn < 0 ? lst[c].kink : lsr.nearer(kn, lst[c].kink);
+        if (kn > 0) lsr.alpha = kn;
       }
-      T an = alpha - d1 / maxT(d2, T(1e-30));
-      if (hi < 0) {
-        if (!(an > lo)) an = lo > 0 ? 2 * lo : T(1);
-      } else if (!(an > lo && an < hi) || same > 0) {
-        const T fp = lo - flo * (hi - lo) / (fhi - flo);
-        an = (fp > lo && fp < hi) ? fp : T(0.5) * (lo + hi);
-      }
-      alpha = an;
+#endif
     }
-    // an unconverged search falls back to the last point with phi' < 0 (a
-    // guaranteed decrease for convex phi)
-    if (!ls_ok) alpha = lo > 0 ? lo : (hi > 0 ? hi * dlo / (dlo - dhi) : T(0));
+    if (!ls_ok) lsr.alpha = lsr.fallback();
 #ifdef BB_SOLVE_TRACE
-    printf("   d0 %.3e alpha %.3e ls_ok %d lo %.3e hi %.3e dlo %.3e dhi %.3e\n", double(d0), double(alpha), int(ls_ok), double(lo), double(hi), double(dlo), double(dhi));
+    printf("   d0 %.3e alpha %.3e ls_ok %d lo %.3e hi %.3e dlo %.3e dhi %.3e\n", double(d0), double(alpha), int(ls_ok),
+           double(lsr.lo), double(lsr.hi), double(lsr.dlo), double(lsr.dhi));
 #endif
     if (!(alpha > 0)) break;
     T sn = 0, an2 = 0;

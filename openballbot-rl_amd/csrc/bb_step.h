@@ -190,7 +190,7 @@ BB_HD int forward(const ModelT<T>& m, const T* q, const T* v, const T* ctrl, T* 
 // warm: qacc_warmstart (each stage's constraint solve saves its qacc).
 template <typename T, bool BODY = true>
 BB_HD int rk4_step(const ModelT<T>& m, T* q, T* v, T* warm, const T* ctrl, const TerrainRef<T>& tr,
-                   EnvWork<T>& W, StageOut<T>& so, const Team& tm) {
+                   EnvWork<T>& W, StageOut<T>& so, const Team& tm, T* stage_warm = nullptr) {
   const T h = m.h;
   // the RK context lives in the workspace (written identically by every
   // lane of the team); only the stage state and the warm start are in registers
@@ -233,10 +233,18 @@ BB_HD int rk4_step(const ModelT<T>& m, T* q, T* v, T* warm, const T* ctrl, const
     T acc[NV];
 #pragma unroll
     for (int i = 0; i < NV; i++) acc[i] = warm[i];
+    if (stage_warm) {
+#pragma unroll
+      for (int i = 0; i < NV; i++) acc[i] = stage_warm[stage * NV + i];
+    }
     const int fit = forward<T, BODY>(m, W.u.pre.qi, W.vi, ctrl, acc, tr, W, stage == 3 ? &so : (StageOut<T>*)nullptr, tm);
     if (fit < 0) return -1;  // fast path aborted (team-uniform)
 #pragma unroll
     for (int i = 0; i < NV; i++) warm[i] = acc[i];
+    if (stage_warm) {
+#pragma unroll
+      for (int i = 0; i < NV; i++) stage_warm[stage * NV + i] = acc[i];
+    }
     iters += fit;
     const T b = (stage == 0 || stage == 3) ? T(1.0 / 6) : T(1.0 / 3);  // RK4 weights B
     team_sync();
@@ -296,13 +304,13 @@ constexpr int F_TERMINATED = 1, F_FAILURE = 2, F_DIVERGED = 4, F_OVERFLOW = 8, F
 template <typename T, bool BODY = true>
 BB_HD int env_step(const ModelT<T>& m, const EnvCfg& cfg, T* q, T* v, T* warm, int& step, const float* action,
                    const TerrainRef<T>& tr, EnvWork<T>& W, float* obs15, float& reward, float* pos2d,
-                   int* iters, const Team& tm) {
+                   int* iters, const Team& tm, T* stage_warm = nullptr) {
   const float mwv = cfg.max_wheel_velocity;
   T ctrl[3];
 #pragma unroll
   for (int i = 0; i < 3; i++) ctrl[i] = -T(clipf(action[i] * mwv, -mwv, mwv));  // data.ctrl[:] = -ctrl
   StageOut<T>& so = W.so;  // team-shared (LDS): not register-resident across the solves
-  int it = rk4_step<T, BODY>(m, q, v, warm, ctrl, tr, W, so, tm);
+  int it = rk4_step<T, BODY>(m, q, v, warm, ctrl, tr, W, so, tm, stage_warm);
   if (it < 0) return F_SLOWPATH;
   if (iters) *iters = it;
   int flags = state_bad(q, v) ? F_DIVERGED : 0;

@@ -53,6 +53,16 @@ __device__ __forceinline__ T tsum(T v) {
   return v;
 }
 
+// minimum over the 16 lanes of the row (exact: identical in every lane)
+template <typename T>
+__device__ __forceinline__ T tmin(T v) {
+  v = minT(v, dpp<0x140>(v));
+  v = minT(v, dpp<0x141>(v));
+  v = minT(v, dpp<0x4E>(v));
+  v = minT(v, dpp<0xB1>(v));
+  return v;
+}
+
 // lane J's value to the whole row
 template <int J, typename T>
 __device__ __forceinline__ T bcast(T v) {
@@ -167,6 +177,23 @@ __device__ __forceinline__ void ls_terms(const ModelT<T>& m, const EnvWork<T>& W
   } else if constexpr (BODY) {
     body_ls_terms(m, body_slot(const_cast<T*>(W.bc), W.bspill, c - 3 - ng), W.P, W.vi, a, s, c6, D);
   }
+}
+
+// LsTerm (bb_solve.h) of contact c for the line search along s; an inert
+// term when c >= nc
+template <bool BODY, typename T>
+__device__ __forceinline__ void ls_term(const ModelT<T>& m, const EnvWork<T>& W, int c, int ng, int nc, const T* a,
+                                        const T* s, T kdw, LsTerm<T>& lt) {
+  T c6[6], Dc;
+  ls_terms<BODY>(m, W, c, ng, nc, a, s, c6, Dc);
+  if (c >= nc) {
+    lt.none();
+    return;
+  }
+  const bool wheel = c < 3;
+  const T D[3] = {wheel ? W.wc[c].D[0] : Dc, wheel ? W.wc[c].D[1] : Dc, wheel ? W.wc[c].D[2] : Dc};
+  const T mu = wheel ? m.fr_wheel[0] : T(1), f1 = wheel ? m.fr_wheel[0] : T(1), f2 = wheel ? m.fr_wheel[1] : T(1);
+  lt.prep(c6, c6 + 3, mu, f1, f2, D, D[0] * (wheel ? kdw : T(0.5)));  // Dm = D0 / (mu^2 (1 + mu^2))
 }
 
 // Newton on f(a); a replicated in every lane of the row.  W.H holds the dense
@@ -379,66 +406,40 @@ __device__ int solve16(const ModelT<T>& m, EnvWork<T>& W, int ng, int nb, T* a, 
     T sMs = 0, gs = 0;
 #pragma unroll
     for (int i = 0; i < NV; i++) { sMs += s[i] * Ms[i]; gs += s[i] * W.mq[i]; }
-    // line-search cache: jar(0) and J s of this lane's first contact in
-    // registers; later rounds (more than 16 contacts) recompute them
-    T c6r[6], Dr;
-    ls_terms<BODY>(m, W, tl, ng, nc, a, s, c6r, Dr);
-    T lo = 0, dlo = d0, hi = -1, dhi = 0, alpha = 1;
-    T flo = d0, fhi = 0;
-    int side = 0, same = 0;
+    // line-search terms of this lane's first contact in registers; later
+    // rounds (more than 16 contacts) rebuild theirs per evaluation
+    LsTerm<T> lt;
+    ls_term<BODY>(m, W, tl, ng, nc, a, s, kdw, lt);
+    LineSearch<T> lsr;
+    lsr.init(d0);
     bool ls_ok = false;
     for (int ls = 1; ls <= m.ls_maxiter; ls++) {
 #if defined(BB_PHASE_CLOCKS) && defined(__HIP_DEVICE_COMPILE__)
       if (tl == 0) atomicAdd(&bb_phase_cycles[11], 1ull);  // line-search evaluations
 #endif
+      const T alpha = lsr.alpha;
       T d1p = 0, d2p = 0, dmp = 0;
-      for (int c = tl; c < nc; c += L) {
-        T c6[6], Dc;
-        if (c == tl) {
-#pragma unroll
-          for (int r = 0; r < 6; r++) c6[r] = c6r[r];
-          Dc = Dr;
-        } else {
-          ls_terms<BODY>(m, W, c, ng, nc, a, s, c6, Dc);
-        }
-        const bool wheel = c < 3;
-        const T D[3] = {wheel ? W.wc[c].D[0] : Dc, wheel ? W.wc[c].D[1] : Dc, wheel ? W.wc[c].D[2] : Dc};
-        const T mu = wheel ? m.fr_wheel[0] : T(1), f1 = wheel ? m.fr_wheel[0] : T(1), f2 = wheel ? m.fr_wheel[1] : T(1);
-        const T Dm = D[0] * (wheel ? kdw : T(0.5));
-        const T x[3] = {c6[3], c6[4], c6[5]};
-        const T jr[3] = {c6[0] + alpha * x[0], c6[1] + alpha * x[1], c6[2] + alpha * x[2]};
-        T f[3], Cc[6];
-        cone_sel(jr, mu, f1, f2, D, Dm, f, Cc);
-        d1p -= f[0] * x[0] + f[1] * x[1] + f[2] * x[2];
-        dmp += fabs(f[0] * x[0]) + fabs(f[1] * x[1]) + fabs(f[2] * x[2]);
-        d2p += Cc[0] * x[0] * x[0] + Cc[1] * x[1] * x[1] + Cc[2] * x[2] * x[2] +
-               2 * (Cc[3] * x[0] * x[1] + Cc[4] * x[0] * x[2] + Cc[5] * x[1] * x[2]);
+      lt.eval(alpha, d1p, d2p, dmp);
+      for (int c = tl + L; c < nc; c += L) {
+        LsTerm<T> lc;
+        ls_term<BODY>(m, W, c, ng, nc, a, s, kdw, lc);
+        lc.eval(alpha, d1p, d2p, dmp);
       }
       const T d1 = gs + alpha * sMs + tsum(d1p);
       const T d2 = sMs + tsum(d2p);
       const T dmag = fabs(gs) + fabs(alpha * sMs) + tsum(dmp);
       if (fabs(d1) <= m.ls_tol * fabs(d0) || fabs(d1) <= T(32) * eps_of<T>() * dmag) { ls_ok = true; break; }
       if (!(d1 == d1)) break;
-      const int sd = d1 < 0 ? -1 : 1;
-      same = sd == side ? same + 1 : 0;
-      side = sd;
-      if (sd < 0) {
-        lo = alpha; dlo = d1; flo = d1;
-        if (same > 0 && hi >= 0) fhi *= T(0.5);
-      } else {
-        hi = alpha; dhi = d1; fhi = d1;
-        if (same > 0) flo *= T(0.5);
-      }
-      T an = alpha - d1 / maxT(d2, T(1e-30));
-      if (hi < 0) {
-        if (!(an > lo)) an = lo > 0 ? 2 * lo : T(1);
-      } else if (!(an > lo && an < hi) || same > 0) {
-        const T fp = lo - flo * (hi - lo) / (fhi - flo);
-        an = (fp > lo && fp < hi) ? fp : T(0.5) * (lo + hi);
-      }
-      alpha = an;
+      lsr.update(d1, d2);
+      // stop at the nearest near-kink the step would cross (first-round
+      // contacts; exact team minimum, so every lane takes the same alpha)
+      const bool up = lsr.alpha > lsr.prev;
+      const T big = T(1e30);
+      const T kv = tmin(lsr.crosses(lt.kink) ? (up ? lt.kink : -lt.kink) : big);
+      if (kv < big) lsr.alpha = up ? kv : -kv;
     }
-    if (!ls_ok) alpha = lo > 0 ? lo : (hi > 0 ? hi * dlo / (dlo - dhi) : T(0));
+    if (!ls_ok) lsr.alpha = lsr.fallback();
+    const T alpha = lsr.alpha;
     if (!(alpha > 0)) break;
     T sn = 0, an2 = 0;
 #pragma unroll
