@@ -255,24 +255,25 @@ struct LsTerm {
 // One update of the exact line search on phi'(alpha) (phi convex, phi'
 // continuous and nondecreasing): the evaluation (alpha, d1 = phi', d2 = phi'')
 // tightens the bracket [lo, hi] and picks the next alpha.  1-D Newton from the
-// latest point while it lands inside the bracket; Illinois false position when
-// two evaluations in a row fall on the same side, or when the latest
-// evaluation did not halve the bracket.  The second case is a Newton 2-cycle:
-// a stiff drive-direction row (R scaled by (0.001/1)^2, ballbot.xml:90-92)
-// changes cone zone between lo and hi, so phi'' jumps by ~1e6 there and the
-// Newton steps from either side overshoot onto the other side, keeping the
-// bracket width for up to ls_maxiter evaluations.
+// latest point while it lands inside the bracket and its step is less than
+// half the step before the last one (the progress test of a safeguarded
+// Newton, as in rtsafe); otherwise Illinois false position on the bracket.
+// The failures this catches: a stiff drive-direction row (R scaled by
+// (0.001/1)^2, ballbot.xml:90-92) changes cone zone between lo and hi, so
+// phi'' jumps by ~1e6 there, and Newton steps from the smooth parts either
+// overshoot back and forth across it (a 2-cycle that keeps the bracket for
+// up to ls_maxiter evaluations) or creep towards it.
 //
 // Kinks (LsTerm::kink): a step that would cross a contact's near-kink stops
-// at it instead (snap); the bracket then closes on the kink from either side
-// in a few evaluations, where Newton and false position from the far smooth
-// parts otherwise creep.
+// at it instead; the bracket then closes on the kink from either side in a
+// few evaluations.
 template <typename T>
 struct LineSearch {
-  T lo, dlo, hi, dhi, alpha, flo, fhi, prev;
+  T lo, dlo, hi, dhi, alpha, flo, fhi, prev, dx, dxold;
   int side, same;
   BB_HD void init(T d0) {
     lo = 0; dlo = d0; hi = -1; dhi = 0; alpha = 1; flo = d0; fhi = 0; prev = 0;
+    dx = dxold = T(1e30);
     side = 0; same = 0;
   }
   // is the kink k strictly between the last evaluated point and the proposed
@@ -281,11 +282,8 @@ struct LineSearch {
     const bool between = alpha > prev ? (k > prev && k < alpha) : (k < prev && k > alpha);
     return between && k > lo && (hi < 0 || k < hi);
   }
-  // of two crossed kinks, the one nearer the last evaluated point
-  BB_HD T nearer(T a, T b) const { return fabs(a - prev) <= fabs(b - prev) ? a : b; }
   BB_HD void update(T d1, T d2) {
     prev = alpha;
-    const T w0 = hi >= 0 ? hi - lo : T(-1);  // bracket width before this evaluation (-1: none yet)
     const int sd = d1 < 0 ? -1 : 1;
     same = sd == side ? same + 1 : 0;
     side = sd;
@@ -299,11 +297,18 @@ struct LineSearch {
     T an = alpha - div_ls(d1, maxT(d2, T(1e-30)));
     if (hi < 0) {
       if (!(an > lo)) an = lo > 0 ? 2 * lo : T(1);
-    } else if (!(an > lo && an < hi) || (w0 >= 0 && hi - lo > T(0.5) * w0)) {
+    } else if (!(an > lo && an < hi) || fabs(an - alpha) > T(0.5) * dxold) {
       const T fp = lo - div_ls(flo * (hi - lo), fhi - flo);
       an = (fp > lo && fp < hi) ? fp : T(0.5) * (lo + hi);
     }
+    dxold = dx;
+    dx = fabs(an - alpha);
     alpha = an;
+  }
+  // the step was shortened to a kink
+  BB_HD void snap(T k) {
+    alpha = k;
+    dx = fabs(k - prev);
   }
   // an unconverged search falls back to the last point with phi' < 0 (a
   // guaranteed decrease for convex phi)
@@ -502,10 +507,12 @@ BB_HD int solve_team(const ModelT<T>& m, EnvWork<T>& W, const T* qfs, int ng, T*
       lsr.update(d1, d2);
 #ifndef BB_NO_KINK
       {
+        // the crossed kink nearest the last evaluated point
+        const bool up = lsr.alpha > lsr.prev;
         T kn = T(-1);
         for (int c = 0; c < nc; c++)
-          if (lsr.crosses(lst[c].kink)) kn = kn < 0 ? lst[c].kink : lsr.nearer(kn, lst[c].kink);
-        if (kn > 0) lsr.alpha = kn;
+          if (lsr.crosses(lst[c].kink) && (kn < 0 || (up ? lst[c].kink < kn : lst[c].kink > kn))) kn = lst[c].kink;
+        if (kn > 0) lsr.snap(kn);
       }
 #endif
     }

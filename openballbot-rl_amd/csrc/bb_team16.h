@@ -436,7 +436,7 @@ __device__ int solve16(const ModelT<T>& m, EnvWork<T>& W, int ng, int nb, T* a, 
       const bool up = lsr.alpha > lsr.prev;
       const T big = T(1e30);
       const T kv = tmin(lsr.crosses(lt.kink) ? (up ? lt.kink : -lt.kink) : big);
-      if (kv < big) lsr.alpha = up ? kv : -kv;
+      if (kv < big) lsr.snap(up ? kv : -kv);
     }
     if (!ls_ok) lsr.alpha = lsr.fallback();
     const T alpha = lsr.alpha;
