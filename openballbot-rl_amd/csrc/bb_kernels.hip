@@ -29,7 +29,7 @@
 using namespace bb;
 
 #ifdef BB_PHASE_CLOCKS
-namespace bb { __device__ unsigned long long bb_phase_cycles[32]; }
+namespace bb { __device__ unsigned long long bb_phase_cycles[40]; }
 #endif
 
 namespace {
@@ -920,8 +920,8 @@ int bb_get_config(bb_handle* h, int32_t* out5) {
 // diagnostic build only: read and clear the per-phase cycle counters
 int bb_debug_phase_cycles(unsigned long long* out16) {
   HIPCHK(hipDeviceSynchronize());
-  HIPCHK(hipMemcpyFromSymbol(out16, HIP_SYMBOL(bb::bb_phase_cycles), sizeof(unsigned long long) * 32));
-  unsigned long long z[32] = {0};
+  HIPCHK(hipMemcpyFromSymbol(out16, HIP_SYMBOL(bb::bb_phase_cycles), sizeof(unsigned long long) * 40));
+  unsigned long long z[40] = {0};
   HIPCHK(hipMemcpyToSymbol(HIP_SYMBOL(bb::bb_phase_cycles), z, sizeof z));
   return 0;
 }

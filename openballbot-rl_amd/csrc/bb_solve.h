@@ -27,10 +27,12 @@ static long g_alpha1 = 0;         // Newton iterations whose first evaluation (a
 // Diagnostic build only (-DBB_PHASE_CLOCKS): per-phase s_memtime cycles,
 // summed over teams into bb_phase_cycles[] (read back by tools/phase_clocks).
 #if defined(BB_PHASE_CLOCKS) && defined(__HIP_DEVICE_COMPILE__)
-extern __device__ unsigned long long bb_phase_cycles[32];
-#define PH_DECL unsigned long long ph_t = clock64(), ph_acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+extern __device__ unsigned long long bb_phase_cycles[40];
+#define PH_DECL unsigned long long ph_t = clock64(), ph_acc[10] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
 #define PH(k) { unsigned long long n_ = clock64(); ph_acc[k] += n_ - ph_t; ph_t = n_; }
-#define PH_FLUSH(tm) if ((tm).tl == 0) { for (int k_ = 0; k_ < 8; k_++) atomicAdd(&bb_phase_cycles[k_], ph_acc[k_]); }
+// phases 0-7 -> slots 0-7; 8 (line-search setup) -> 32, 9 (line-search loop) -> 33
+#define PH_FLUSH(tm) if ((tm).tl == 0) { for (int k_ = 0; k_ < 8; k_++) atomicAdd(&bb_phase_cycles[k_], ph_acc[k_]); \
+                                          atomicAdd(&bb_phase_cycles[32], ph_acc[8]); atomicAdd(&bb_phase_cycles[33], ph_acc[9]); }
 #else
 #define PH_DECL
 #define PH(k)
@@ -237,8 +239,8 @@ struct LsTerm {
     const T t2 = U1 * U1 + U2 * U2;
     const T rt = t2 > 0 ? rsqrt_ls(t2) : T(0);
     const T Tn = t2 * rt;
-    const bool top = N >= mu * Tn || (Tn <= 0 && N >= 0);
-    const bool bot = !top && (mu * N + Tn <= 0 || (Tn <= 0 && N < 0));
+    const bool top = (N >= mu * Tn) | ((Tn <= 0) & (N >= 0));   // bitwise: selects, not branches
+    const bool bot = !top & ((mu * N + Tn <= 0) | ((Tn <= 0) & (N < 0)));
     const T g = N - mu * Tn;
     const T tp = (U1 * du[1] + U2 * du[2]) * rt;
     const T gp = du[0] - mu * tp;
@@ -282,25 +284,29 @@ struct LineSearch {
     const bool between = alpha > prev ? (k > prev && k < alpha) : (k < prev && k > alpha);
     return between && k > lo && (hi < 0 || k < hi);
   }
+  // select-only (no branches): the lanes of a team agree, the teams of a wave
+  // do not, and divergent branches would run every path with exec masks
   BB_HD void update(T d1, T d2) {
     prev = alpha;
-    const int sd = d1 < 0 ? -1 : 1;
+    const bool neg = d1 < 0;
+    const int sd = neg ? -1 : 1;
     same = sd == side ? same + 1 : 0;
     side = sd;
-    if (sd < 0) {
-      lo = alpha; dlo = d1; flo = d1;
-      if (same > 0 && hi >= 0) fhi *= T(0.5);
-    } else {
-      hi = alpha; dhi = d1; fhi = d1;
-      if (same > 0) flo *= T(0.5);
-    }
-    T an = alpha - div_ls(d1, maxT(d2, T(1e-30)));
-    if (hi < 0) {
-      if (!(an > lo)) an = lo > 0 ? 2 * lo : T(1);
-    } else if (!(an > lo && an < hi) || fabs(an - alpha) > T(0.5) * dxold) {
-      const T fp = lo - div_ls(flo * (hi - lo), fhi - flo);
-      an = (fp > lo && fp < hi) ? fp : T(0.5) * (lo + hi);
-    }
+    const bool rep = same > 0;
+    const T hlo = (!neg & rep) ? T(0.5) : T(1);             // Illinois: halve the stale end's weight
+    const T hhi = (neg & rep & (hi >= 0)) ? T(0.5) : T(1);
+    lo = neg ? alpha : lo;
+    dlo = neg ? d1 : dlo;
+    flo = neg ? d1 : flo * hlo;
+    hi = neg ? hi : alpha;
+    dhi = neg ? dhi : d1;
+    fhi = neg ? fhi * hhi : d1;
+    const T an_n = alpha - div_ls(d1, maxT(d2, T(1e-30)));  // Newton from the latest point
+    const T fp = lo - div_ls(flo * (hi - lo), fhi - flo);   // false position (bracket only)
+    const T an_f = ((fp > lo) & (fp < hi)) ? fp : T(0.5) * (lo + hi);
+    const T an_o = an_n > lo ? an_n : (lo > 0 ? 2 * lo : T(1));  // no upper end yet
+    const bool newton = (an_n > lo) & (an_n < hi) & (fabs(an_n - alpha) <= T(0.5) * dxold);
+    const T an = hi < 0 ? an_o : (newton ? an_n : an_f);
     dxold = dx;
     dx = fabs(an - alpha);
     alpha = an;

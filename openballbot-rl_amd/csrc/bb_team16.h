@@ -31,15 +31,17 @@ namespace t16 {
 
 constexpr int L = 16;
 
+// every pattern used here reads a valid lane of the same row, so no "old"
+// value is needed (mov_dpp: no register initialisation before each move)
 template <int CTRL>
 __device__ __forceinline__ float dpp(float v) {
-  return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), CTRL, 0xF, 0xF, false));
+  return __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), CTRL, 0xF, 0xF, true));
 }
 template <int CTRL>
 __device__ __forceinline__ double dpp(double v) {
   const unsigned long long u = (unsigned long long)__double_as_longlong(v);
-  const int lo = __builtin_amdgcn_update_dpp(0, (int)(unsigned)u, CTRL, 0xF, 0xF, false);
-  const int hi = __builtin_amdgcn_update_dpp(0, (int)(unsigned)(u >> 32), CTRL, 0xF, 0xF, false);
+  const int lo = __builtin_amdgcn_mov_dpp((int)(unsigned)u, CTRL, 0xF, 0xF, true);
+  const int hi = __builtin_amdgcn_mov_dpp((int)(unsigned)(u >> 32), CTRL, 0xF, 0xF, true);
   return __longlong_as_double((long long)(((unsigned long long)(unsigned)hi << 32) | (unsigned)lo));
 }
 
@@ -56,10 +58,10 @@ __device__ __forceinline__ T tsum(T v) {
 // minimum over the 16 lanes of the row (exact: identical in every lane)
 template <typename T>
 __device__ __forceinline__ T tmin(T v) {
-  v = minT(v, dpp<0x140>(v));
-  v = minT(v, dpp<0x141>(v));
-  v = minT(v, dpp<0x4E>(v));
-  v = minT(v, dpp<0xB1>(v));
+  v = fmin(v, dpp<0x140>(v));  // v_min (no NaNs here: kinks or the 1e30 sentinel)
+  v = fmin(v, dpp<0x141>(v));
+  v = fmin(v, dpp<0x4E>(v));
+  v = fmin(v, dpp<0xB1>(v));
   return v;
 }
 
@@ -413,6 +415,7 @@ __device__ int solve16(const ModelT<T>& m, EnvWork<T>& W, int ng, int nb, T* a, 
     LineSearch<T> lsr;
     lsr.init(d0);
     bool ls_ok = false;
+    PH(8)
     for (int ls = 1; ls <= m.ls_maxiter; ls++) {
 #if defined(BB_PHASE_CLOCKS) && defined(__HIP_DEVICE_COMPILE__)
       if (tl == 0) atomicAdd(&bb_phase_cycles[11], 1ull);  // line-search evaluations
@@ -436,9 +439,12 @@ __device__ int solve16(const ModelT<T>& m, EnvWork<T>& W, int ng, int nb, T* a, 
       const bool up = lsr.alpha > lsr.prev;
       const T big = T(1e30);
       const T kv = tmin(lsr.crosses(lt.kink) ? (up ? lt.kink : -lt.kink) : big);
-      if (kv < big) lsr.snap(up ? kv : -kv);
+      const T ks = up ? kv : -kv;
+      lsr.dx = kv < big ? fabs(ks - lsr.prev) : lsr.dx;
+      lsr.alpha = kv < big ? ks : lsr.alpha;
     }
     if (!ls_ok) lsr.alpha = lsr.fallback();
+    PH(9)
     const T alpha = lsr.alpha;
     if (!(alpha > 0)) break;
     T sn = 0, an2 = 0;

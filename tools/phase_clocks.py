@@ -40,7 +40,7 @@ def main():
     from ballbot_gym.envs import BallbotVecEnv
     env = BallbotVecEnv(4096, device="cuda:0", precision=a.precision, terrain_config={"type": a.terrain, "config": {}})
     pool = torch.rand(64, 4096, 3, device="cuda:0") * 2 - 1
-    out = (C.c_ulonglong * 32)()
+    out = (C.c_ulonglong * 40)()
     for i in range(a.warmup):
         env.step_async_raw(pool[i % 64])
     torch.cuda.synchronize()
@@ -56,7 +56,10 @@ def main():
     res = {"precision": a.precision, "forwards": fw, "newton_iters": iters,
            "cycles_per_forward": {NAMES[k]: out[k] / fw for k in range(10)},
            "cycles_per_newton_iter": {NAMES[k]: out[k] / max(iters, 1) for k in range(8)}}
-    res["total_cycles_per_forward"] = sum(out[k] for k in range(10)) / fw
+    res["total_cycles_per_forward"] = (sum(out[k] for k in range(10)) + out[32] + out[33]) / fw
+    # the line-search phase split: setup (M s, s'Ms, per-contact terms) and the evaluation loop
+    res["cycles_per_forward"]["line_search_setup"] = out[32] / fw
+    res["cycles_per_forward"]["line_search_loop"] = out[33] / fw
     res["line_search_evals_per_newton_iter"] = out[11] / max(iters, 1)
     res["newton_iters_per_forward_max"] = out[21]
     res["newton_iters_per_forward_hist"] = {f"{2 * b}-{2 * b + 1}" if b < 9 else ">=18": out[22 + b] for b in range(10)}
