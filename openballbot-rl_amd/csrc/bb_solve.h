@@ -93,6 +93,7 @@ struct TerrainRef {
 template <typename T>
 struct EnvWork {
   T q0[NQ], v0[NV], vs[NV], as[NV];          // RK4 stage context
+  T k1[NV];                                  // stage-1 qacc (stage 4's warm start 2 k3 - k1)
   T qn[NQ], vn[NV], wn[NV];                  // env state and warm start (step kernel: not held in
                                              // registers across the solves)
   T qfs[NV];                                 // smooth force of the current forward

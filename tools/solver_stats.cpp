@@ -32,8 +32,6 @@ int main(int argc, char** argv) {
   static EnvWork<double> W;
   std::vector<double> q(n * NQ), v(n * NV), w(n * NV);
   std::vector<int> st(n, 0);
-  const bool sw = getenv("BB_STAGEWARM") != nullptr;  // per-stage warm starts from the previous step
-  std::vector<double> w4(size_t(n) * 4 * NV, 0.0);
   for (int e = 0; e < n; e++) reset_state(m, 0.01, &q[e * NQ], &v[e * NV], &w[e * NV]);
   std::mt19937_64 rng(12345);
   std::uniform_real_distribution<float> U(-1.f, 1.f);
@@ -45,7 +43,7 @@ int main(int argc, char** argv) {
       int it = 0;
       const long lsb = g_ls_evals;
       int fl = env_step<double, false>(m, cfg, &q[e * NQ], &v[e * NV], &w[e * NV], st[e], a, tr, W, obs, r, p2, &it,
-                                       Team{1, 0}, sw ? &w4[size_t(e) * 4 * NV] : nullptr);
+                                       Team{1, 0});
       if (t >= skip) {
         fwd += 4; newton += it; ls0 += g_ls_evals - lsb;
         hist[it / 4 < 31 ? it / 4 : 31]++;
@@ -53,7 +51,6 @@ int main(int argc, char** argv) {
       if (fl & 5) {
         reset_state(m, 0.01, &q[e * NQ], &v[e * NV], &w[e * NV]);
         st[e] = 0; resets++;
-        for (int i = 0; i < 4 * NV; i++) w4[size_t(e) * 4 * NV + i] = 0.0;
       }
     }
   }
