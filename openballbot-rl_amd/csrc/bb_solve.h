@@ -33,6 +33,11 @@ extern __device__ unsigned long long bb_phase_cycles[40];
 // phases 0-7 -> slots 0-7; 8 (line-search setup) -> 32, 9 (line-search loop) -> 33
 #define PH_FLUSH(tm) if ((tm).tl == 0) { for (int k_ = 0; k_ < 8; k_++) atomicAdd(&bb_phase_cycles[k_], ph_acc[k_]); \
                                           atomicAdd(&bb_phase_cycles[32], ph_acc[8]); atomicAdd(&bb_phase_cycles[33], ph_acc[9]); }
+#elif defined(BB_ISA_MARKS) && defined(__HIP_DEVICE_COMPILE__)
+// ISA analysis build: phase boundaries as assembler comments
+#define PH_DECL
+#define PH(k) asm volatile("; PHASE_MARK " #k);
+#define PH_FLUSH(tm)
 #else
 #define PH_DECL
 #define PH(k)

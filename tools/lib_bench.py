@@ -18,10 +18,12 @@ sys.path.insert(0, str(ROOT / "openballbot-rl_amd"))
 
 
 def build(name, flags):
+    """tools/_build/libbb_<name>.so from csrc/bb_kernels.hip with extra flags (python tools/lib_bench.py --build-only)."""
     out = ROOT / "tools" / "_build" / f"libbb_{name}.so"
     out.parent.mkdir(parents=True, exist_ok=True)
-    cmd = ["hipcc", "--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC", "-shared", *flags, "-o", str(out),
-           str(ROOT / "openballbot-rl_amd" / "csrc" / "bb_kernels.hip")]
+    cmd = ["hipcc", "--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC", "-shared", *flags, "-o", str(out)] + [
+        str(ROOT / "openballbot-rl_amd" / "csrc" / f)
+        for f in ("bb_kernels.hip", "bb_terrain.hip", "bb_rollout.hip", "bb_render.hip", "bb_ppo.hip")]
     subprocess.run(cmd, check=True)
     return out
 
@@ -53,13 +55,20 @@ def main():
     ap.add_argument("--steps", type=int, default=300)
     ap.add_argument("--warmup", type=int, default=300)
     ap.add_argument("--child", default=None)
+    ap.add_argument("--no-build", action="store_true", help="use the prebuilt tools/_build/libbb_<NAME>.so")
+    ap.add_argument("--build-only", action="store_true", help="compile the variants (here, on the CPU) and exit")
     a = ap.parse_args()
+    if a.build_only:
+        import concurrent.futures as cf
+        with cf.ThreadPoolExecutor(8) as ex:
+            list(ex.map(lambda v: build(v.partition(":")[0], [f for f in v.partition(":")[2].split(",") if f]), a.variant))
+        return
     if a.child:
         print(json.dumps(run_one(a.child, a.precision, a.terrain, a.steps, a.warmup)))
         return
     for v in a.variant:
         name, _, fl = v.partition(":")
-        lib = build(name, [f for f in fl.split(",") if f])
+        lib = (ROOT / "tools" / "_build" / f"libbb_{name}.so") if a.no_build else build(name, [f for f in fl.split(",") if f])
         r = subprocess.run([sys.executable, __file__, "--child", str(lib), "--precision", a.precision,
                             "--terrain", a.terrain, "--steps", str(a.steps), "--warmup", str(a.warmup)],
                            capture_output=True, text=True, timeout=600)
