@@ -412,32 +412,6 @@ __device__ int solve16(const ModelT<T>& m, EnvWork<T>& W, int ng, int nb, T* a, 
     // rounds (more than 16 contacts) rebuild theirs per evaluation
     LsTerm<T> lt;
     ls_term<BODY>(m, W, tl, ng, nc, a, s, kdw, lt);
-      const T alpha = lsx.alpha;
-      T d1p = 0, d2p = 0, dmp = 0;
-      lt.eval(alpha, d1p, d2p, dmp);
-      for (int c = tl + L; c < nc; c += L) {
-        LsTerm<T> lc;
-        ls_term<BODY>(m, W, c, ng, nc, a, s, kdw, lc);
-        lc.eval(alpha, d1p, d2p, dmp);
-      }
-      const T d1 = gs + alpha * sMs + tsum(d1p);
-      const T d2 = sMs + tsum(d2p);
-      const T dmag = fabs(gs) + fabs(alpha * sMs) + tsum(dmp);
-      if (fabs(d1) <= m.ls_tol * fabs(d0) || fabs(d1) <= T(32) * eps_of<T>() * dmag) { lsx_ok = true; break; }
-      if (!(d1 == d1)) break;
-      lsx.update(d1, d2);
-      // stop at the nearest near-kink the step would cross (first-round
-      // contacts; exact team minimum, so every lane takes the same alpha)
-      const bool up = lsx.alpha > lsx.prev;
-      const T big = T(1e30);
-      const T kv = tmin(lsx.crosses(lt.kink) ? (up ? lt.kink : -lt.kink) : big);
-      const T ks = up ? kv : -kv;
-      lsx.dx = kv < big ? fabs(ks - lsx.prev) : lsx.dx;
-      lsx.alpha = kv < big ? ks : lsx.alpha;
-    }
-    asm volatile("" :: "v"(lsx.alpha) : "memory");
-  }
-#endif
     LineSearch<T> lsr;
     lsr.init(d0);
     bool ls_ok = false;
