@@ -165,10 +165,14 @@ BB_HD int forward(const ModelT<T>& m, const T* q, const T* v, const T* ctrl, T* 
   // 16-lane DPP-row solve: smooth force and dense M staged in the team's LDS
   t16::mass_dense_team(W, tm.tl);
   team_sync();
+  if constexpr (!BODY) t16::ground_setup(m, W, ng, tm.tl);  // into the mass blocks: after mass_dense_team
+
 #if defined(BB_PHASE_CLOCKS)
   const unsigned long long s_t0 = clock64();
 #endif
-  const int it = t16::solve16<BODY>(m, W, ng, nb, acc, tm.tl);
+  int it;
+  if constexpr (BODY) it = t16::solve16<BODY>(m, W, ng, nb, acc, tm.tl);
+  else it = t16::solve16_fast(m, W, ng, acc, tm.tl);
 #if defined(BB_PHASE_CLOCKS)
   if (BODY && tm.tl == 0) {  // full-kernel solve cycles and Newton iterations
     atomicAdd(&bb_phase_cycles[15], clock64() - s_t0);

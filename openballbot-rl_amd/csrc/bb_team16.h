@@ -130,16 +130,14 @@ __device__ __forceinline__ void chol_rows(T (&h)[NV], T hdi, T (&diag)[NV], int 
   });
 }
 
-// s = -(L L')^-1 g with L distributed by rows (lane i: L_i,0..i-1 in h[]), g replicated
+// s = -(L L')^-1 g with L distributed by rows (lane i: L_i,0..i-1 in h[]);
+// lane i supplies g_i (gown) and gets the whole s (replicated) plus its own
+// component s_i (sown); lanes >= NV get sown = 0
 template <typename T>
-__device__ __forceinline__ void chol_solve_rows(const T (&h)[NV], const T (&diag)[NV], const T* g, T (&s)[NV],
+__device__ __forceinline__ void chol_solve_rows(const T (&h)[NV], const T (&diag)[NV], T gown, T (&s)[NV], T& sown,
                                                 int tl) {
   // forward: L y = -g, column sweep; b = this lane's running right-hand side
-  T b = 0;
-  static_for<NV>([&](auto kc) {
-    constexpr int k = decltype(kc)::value;
-    b = tl == k ? -g[k] : b;
-  });
+  T b = tl < NV ? -gown : T(0);
   T y[NV];
   static_for<NV>([&](auto jc) {
     constexpr int j = decltype(jc)::value;
@@ -156,6 +154,7 @@ __device__ __forceinline__ void chol_solve_rows(const T (&h)[NV], const T (&diag
     s[i] = si;
     own = tl == i ? si : own;
   });
+  sown = own;
 }
 
 // line-search terms of contact c: jar(0) = J a - aref, J s and the contact's
@@ -384,10 +383,10 @@ __device__ int solve16(const ModelT<T>& m, EnvWork<T>& W, int ng, int nb, T* a, 
     for (int k = 0; k < NV; k++) hdi = row == k ? h[k] : hdi;
     PH(3)
     // ---- (5) factorise and solve
-    T diag[NV], s[NV];
+    T diag[NV], s[NV], sown;
     chol_rows(h, hdi, diag, tl);
     PH(4)
-    chol_solve_rows(h, diag, W.gv, s, tl);
+    chol_solve_rows(h, diag, W.gv[row], s, sown, tl);
     T d0 = 0;
     bool fin = true;
 #pragma unroll
@@ -436,6 +435,278 @@ __device__ int solve16(const ModelT<T>& m, EnvWork<T>& W, int ng, int nb, T* a, 
       lsr.update(d1, d2);
       // stop at the nearest near-kink the step would cross (first-round
       // contacts; exact team minimum, so every lane takes the same alpha)
+      const bool up = lsr.alpha > lsr.prev;
+      const T big = T(1e30);
+      const T kv = tmin(lsr.crosses(lt.kink) ? (up ? lt.kink : -lt.kink) : big);
+      const T ks = up ? kv : -kv;
+      lsr.dx = kv < big ? fabs(ks - lsr.prev) : lsr.dx;
+      lsr.alpha = kv < big ? ks : lsr.alpha;
+    }
+    if (!ls_ok) lsr.alpha = lsr.fallback();
+    PH(9)
+    const T alpha = lsr.alpha;
+    if (!(alpha > 0)) break;
+    T sn = 0, an2 = 0;
+#pragma unroll
+    for (int i = 0; i < NV; i++) { a[i] += alpha * s[i]; sn += s[i] * s[i]; an2 += a[i] * a[i]; }
+    PH(6)
+    if (alpha * alpha * sn <= T(1e-30) + m.step_rel2 * (1 + an2)) { it++; break; }
+  }
+  PH(7)
+  PH_FLUSH((Team{L, tl}))
+  return it;
+}
+
+// ---------------------------------------------------------------------------
+// Fast-kernel solve (no base-tree contacts).  Same Newton / line search as
+// solve16; what differs is where the work sits:
+//   per forward    lane 3+c builds ball-terrain contact c's Jacobian, aref and D
+//                  once (ground_setup) into LDS for c < GC_LDS (the BODY-only
+//                  W.bc region and the mass blocks, dead during the solve);
+//                  later contacts (rare: more than 13) are rebuilt per use
+//   contact pass   wheel lanes publish C J and f (LDS); ground lanes add their
+//                  ball-block gradient and C-weighted J'J partials
+//   gradient       lane i: g_i = (M a)_i - qfs_i - sum_w J_w[:,i]' f_w from its
+//                  dense M row and the wheel data, plus the team-summed
+//                  ball-block ground part: 6 + 21 team sums (solve16: 15 + 21)
+//   line search    s'M s and s'(M a - qfs) from the rows (team sums, no
+//                  replicated mass products); each contact term from the
+//                  contact pass's jar and the stored Jacobian
+constexpr int GC_LDS = 13;  // ball-terrain contacts with an LDS Jacobian (one contact per lane: 3 + 13 = 16)
+static_assert(GC_LDS * 18 <= MAXB_LDS * NBF, "ground Jacobians do not fit W.bc");
+
+// aref[3], D of ground contact c (c < GC_LDS), in the mass-block storage
+template <typename T>
+__device__ __forceinline__ T* ground_ad(EnvWork<T>& W, int c) {
+  static_assert(sizeof(Mass<T>) >= GC_LDS * 4 * sizeof(T), "ground aref/D do not fit the mass blocks");
+  return reinterpret_cast<T*>(&W.M) + 4 * c;
+}
+
+// lane 3 + c: ground contact c's Jacobian rows, aref and D, once per forward
+// (they depend on the stage state only).  W.P and W.vi must be set, and the
+// mass blocks must be consumed (mass_dense_team) before.
+template <typename T>
+__device__ __forceinline__ void ground_setup(const ModelT<T>& m, EnvWork<T>& W, int ng, int tl) {
+  const int c = tl - 3;
+  if (c >= 0 && c < ng && c < GC_LDS) {
+    T J[3][6], ar[3], D;
+    ground_contact(m, W.g + c * NGF, W.P.RB, W.vi, J, ar, D);
+    T* o = W.bc + c * 18;
+#pragma unroll
+    for (int r = 0; r < 3; r++)
+#pragma unroll
+      for (int i = 0; i < 6; i++) o[6 * r + i] = J[r][i];
+    T* ad = ground_ad(W, c);
+#pragma unroll
+    for (int r = 0; r < 3; r++) ad[r] = ar[r];
+    ad[3] = D;
+  }
+}
+
+// ground contact c's Jacobian, aref and D: stored, or rebuilt past GC_LDS
+template <typename T>
+__device__ __forceinline__ void ground_get(const ModelT<T>& m, EnvWork<T>& W, int c, T (&J)[3][6], T (&ar)[3], T& D) {
+  if (c < GC_LDS) {
+    const T* o = W.bc + c * 18;
+#pragma unroll
+    for (int r = 0; r < 3; r++)
+#pragma unroll
+      for (int i = 0; i < 6; i++) J[r][i] = o[6 * r + i];
+    const T* ad = ground_ad(W, c);
+#pragma unroll
+    for (int r = 0; r < 3; r++) ar[r] = ad[r];
+    D = ad[3];
+  } else {
+    ground_contact(m, W.g + c * NGF, W.P.RB, W.vi, J, ar, D);
+  }
+}
+
+template <typename T>
+__device__ int solve16_fast(const ModelT<T>& m, EnvWork<T>& W, int ng, T* a, int tl) {
+  const int nc = 3 + ng;
+  const bool rowl = tl < NV;
+  const int row = rowl ? tl : NV - 1;
+  const T muw = m.fr_wheel[0];
+  const T kdw = T(1) / (muw * muw * (1 + muw * muw));
+  const T qfs_i = W.qfs[row];
+  PH_DECL
+  int it = 0;
+  for (; it < m.maxiter; it++) {
+    team_sync();
+    // ---- (1) contact pass, contact-parallel (c = tl, tl + 16, ...)
+    T gg[6], Hg[21];
+#pragma unroll
+    for (int i = 0; i < 6; i++) gg[i] = 0;
+#pragma unroll
+    for (int i = 0; i < 21; i++) Hg[i] = 0;
+    T jar0[3] = {0, 0, 0};  // this lane's first contact, kept for the line search
+    for (int c = tl; c < nc; c += L) {
+      const bool wheel = c < 3;
+      T jar[3], Dc = 0, Jg[3][6];
+      if (wheel) {
+#pragma unroll
+        for (int r = 0; r < 3; r++) jar[r] = wheel_dot(W.wc[c], c, r, a) - W.wc[c].aref[r];
+      } else {
+        T ar[3];
+        ground_get(m, W, c - 3, Jg, ar, Dc);
+#pragma unroll
+        for (int r = 0; r < 3; r++) jar[r] = ground_dot(Jg, r, a) - ar[r];
+      }
+      if (c == tl) {
+#pragma unroll
+        for (int r = 0; r < 3; r++) jar0[r] = jar[r];
+      }
+      const T D[3] = {wheel ? W.wc[c].D[0] : Dc, wheel ? W.wc[c].D[1] : Dc, wheel ? W.wc[c].D[2] : Dc};
+      const T mu = wheel ? muw : T(1), f1 = wheel ? muw : T(1), f2 = wheel ? m.fr_wheel[1] : T(1);
+      const T Dm = D[0] * (wheel ? kdw : T(0.5));  // 1 / (mu^2 (1 + mu^2))
+      T f[3], Cc[6];
+      cone_sel(jar, mu, f1, f2, D, Dm, f, Cc);
+      if (wheel) {
+        const WheelCon<T>& C = W.wc[c];
+#pragma unroll
+        for (int q = 0; q < 13; q++) {
+          const T j0 = C.J[0][q], j1 = C.J[1][q], j2 = C.J[2][q];
+          W.u.hes.cj[c][0][q] = Cc[0] * j0 + Cc[3] * j1 + Cc[4] * j2;
+          W.u.hes.cj[c][1][q] = Cc[3] * j0 + Cc[1] * j1 + Cc[5] * j2;
+          W.u.hes.cj[c][2][q] = Cc[4] * j0 + Cc[5] * j1 + Cc[2] * j2;
+        }
+#pragma unroll
+        for (int r = 0; r < 3; r++) W.u.hes.wf[c][r] = f[r];
+      } else {
+        T w[3][6];
+#pragma unroll
+        for (int i = 0; i < 6; i++) {
+          gg[i] -= Jg[0][i] * f[0] + Jg[1][i] * f[1] + Jg[2][i] * f[2];
+          w[0][i] = Cc[0] * Jg[0][i] + Cc[3] * Jg[1][i] + Cc[4] * Jg[2][i];
+          w[1][i] = Cc[3] * Jg[0][i] + Cc[1] * Jg[1][i] + Cc[5] * Jg[2][i];
+          w[2][i] = Cc[4] * Jg[0][i] + Cc[5] * Jg[1][i] + Cc[2] * Jg[2][i];
+        }
+#pragma unroll
+        for (int i = 0; i < 6; i++)
+#pragma unroll
+          for (int j = 0; j <= i; j++) Hg[i * (i + 1) / 2 + j] += Jg[0][i] * w[0][j] + Jg[1][i] * w[1][j] + Jg[2][i] * w[2][j];
+      }
+    }
+    PH(0)
+    // ---- (2) ball-block ground sums (DPP)
+#pragma unroll
+    for (int i = 0; i < 6; i++) gg[i] = tsum(gg[i]);
+#pragma unroll
+    for (int i = 0; i < 21; i++) Hg[i] = tsum(Hg[i]);
+    team_sync();  // cj, wf visible to every row owner
+    PH(1)
+    // ---- (3) gradient, row i: (M a)_i - qfs_i - sum_w J_w[:,i]' f_w (+ ground)
+    T h[NV];
+#pragma unroll
+    for (int k = 0; k < NV; k++) h[k] = W.H[hidx(row, k)];  // dense M row
+    T Ma = 0;
+#pragma unroll
+    for (int k = 0; k < NV; k++) Ma += h[k] * a[k];
+    const T mq = rowl ? Ma - qfs_i : T(0);
+    T gi = mq;
+    static_for<3>([&](auto wc_) {
+      constexpr int w = decltype(wc_)::value;
+      const int p = wheel_pos(row, w);
+      if (p >= 0) {
+        const WheelCon<T>& C = W.wc[w];
+        gi -= C.J[0][p] * W.u.hes.wf[w][0] + C.J[1][p] * W.u.hes.wf[w][1] + C.J[2][p] * W.u.hes.wf[w][2];
+      }
+    });
+#pragma unroll
+    for (int i = 0; i < 6; i++) gi += row == 9 + i ? gg[i] : T(0);
+    gi = rowl ? gi : T(0);
+    const T gn = tsum(gi * gi);
+    if (m.scale * m.scale * gn < m.tol * m.tol) break;  // scale * ||g|| < tol without the sqrt
+    PH(2)
+    // ---- (4) Hessian row: M row + wheel blocks + ground block
+    static_for<3>([&](auto wc_) {
+      constexpr int w = decltype(wc_)::value;
+      const int p = wheel_pos(row, w);
+      if (p >= 0) {
+        const WheelCon<T>& C = W.wc[w];
+        const T j0 = C.J[0][p], j1 = C.J[1][p], j2 = C.J[2][p];
+#pragma unroll
+        for (int q = 0; q < 13; q++) {
+          const int k = wheel_col(q, w);
+          h[k] += j0 * W.u.hes.cj[w][0][q] + j1 * W.u.hes.cj[w][1][q] + j2 * W.u.hes.cj[w][2][q];
+        }
+      }
+    });
+#pragma unroll
+    for (int ai = 0; ai < 6; ai++)
+#pragma unroll
+      for (int b = 0; b < 6; b++) {
+        const T v = Hg[ai >= b ? ai * (ai + 1) / 2 + b : b * (b + 1) / 2 + ai];
+        h[9 + b] += row == 9 + ai ? v : T(0);
+      }
+    T hdi = 0;
+#pragma unroll
+    for (int k = 0; k < NV; k++) hdi = row == k ? h[k] : hdi;
+    PH(3)
+    // ---- (5) factorise and solve
+    T diag[NV], s[NV], sown;
+    chol_rows(h, hdi, diag, tl);
+    PH(4)
+    chol_solve_rows(h, diag, gi, s, sown, tl);
+    T d0 = tsum(sown * gi);
+    bool fin = true;
+#pragma unroll
+    for (int i = 0; i < NV; i++) fin = fin && isfinite(s[i]);
+    if (!fin || !(d0 < 0)) {
+      // roundoff-indefinite Hessian: diagonal Newton from this row, then replicated
+      sown = rowl ? -gi / maxT(W.H[hidx(row, row)], T(1e-30)) : T(0);
+      static_for<NV>([&](auto kc) {
+        constexpr int k = decltype(kc)::value;
+        s[k] = bcast<k>(sown);
+      });
+      d0 = tsum(sown * gi);
+      if (!(d0 < 0)) break;
+    }
+    PH(5)
+    // ---- (6) exact line search
+    T Ms = 0;
+#pragma unroll
+    for (int k = 0; k < NV; k++) Ms += W.H[hidx(row, k)] * s[k];
+    const T sMs = tsum(sown * Ms), gs = tsum(sown * mq);
+    // this lane's first contact's term from its jar; later rounds rebuild theirs
+    LsTerm<T> lt;
+    if (tl < nc) {
+      const bool wheel = tl < 3;
+      T x[3], Dc[3];
+      if (wheel) {
+        const WheelCon<T>& C = W.wc[tl];
+#pragma unroll
+        for (int r = 0; r < 3; r++) { x[r] = wheel_dot(C, tl, r, s); Dc[r] = C.D[r]; }
+      } else {
+        T Jg[3][6], ar[3], D;
+        ground_get(m, W, tl - 3, Jg, ar, D);
+#pragma unroll
+        for (int r = 0; r < 3; r++) { x[r] = ground_dot(Jg, r, s); Dc[r] = D; }
+      }
+      const T mu = wheel ? muw : T(1), f1 = wheel ? muw : T(1), f2 = wheel ? m.fr_wheel[1] : T(1);
+      lt.prep(jar0, x, mu, f1, f2, Dc, Dc[0] * (wheel ? kdw : T(0.5)));
+    } else {
+      lt.none();
+    }
+    LineSearch<T> lsr;
+    lsr.init(d0);
+    bool ls_ok = false;
+    PH(8)
+    for (int ls = 1; ls <= m.ls_maxiter; ls++) {
+      const T alpha = lsr.alpha;
+      T d1p = 0, d2p = 0, dmp = 0;
+      lt.eval(alpha, d1p, d2p, dmp);
+      for (int c = tl + L; c < nc; c += L) {
+        LsTerm<T> lc;
+        ls_term<false>(m, W, c, ng, nc, a, s, kdw, lc);
+        lc.eval(alpha, d1p, d2p, dmp);
+      }
+      const T d1 = gs + alpha * sMs + tsum(d1p);
+      const T d2 = sMs + tsum(d2p);
+      const T dmag = fabs(gs) + fabs(alpha * sMs) + tsum(dmp);
+      if (fabs(d1) <= m.ls_tol * fabs(d0) || fabs(d1) <= T(32) * eps_of<T>() * dmag) { ls_ok = true; break; }
+      if (!(d1 == d1)) break;
+      lsr.update(d1, d2);
       const bool up = lsr.alpha > lsr.prev;
       const T big = T(1e30);
       const T kv = tmin(lsr.crosses(lt.kink) ? (up ? lt.kink : -lt.kink) : big);

@@ -37,6 +37,7 @@ int main(int argc, char** argv) {
   std::uniform_real_distribution<float> U(-1.f, 1.f);
   long fwd = 0, newton = 0, ls0 = 0, resets = 0;
   long hist[32] = {0};
+  long nghist[32] = {0};  // ball-terrain contacts at the last RK stage
   for (int t = 0; t < steps; t++) {
     for (int e = 0; e < n; e++) {
       float a[3] = {U(rng), U(rng), U(rng)}, obs[15], r, p2[2];
@@ -45,6 +46,7 @@ int main(int argc, char** argv) {
       int fl = env_step<double, false>(m, cfg, &q[e * NQ], &v[e * NV], &w[e * NV], st[e], a, tr, W, obs, r, p2, &it,
                                        Team{1, 0});
       if (t >= skip) {
+        nghist[W.so.ng < 31 ? W.so.ng : 31]++;
         fwd += 4; newton += it; ls0 += g_ls_evals - lsb;
         hist[it / 4 < 31 ? it / 4 : 31]++;
       }
@@ -58,6 +60,8 @@ int main(int argc, char** argv) {
          "\"ls_evals_per_newton\": %.4f, \"ls_evals_per_forward\": %.4f, \"resets\": %ld, \"iters_per_step_hist4\": [",
          n, steps - skip, fwd, double(newton) / fwd, double(ls0) / newton, double(ls0) / fwd, resets);
   for (int i = 0; i < 12; i++) printf("%s%ld", i ? ", " : "", hist[i]);
+  printf("], \"ground_contacts_hist\": [");
+  for (int i = 0; i < 20; i++) printf("%s%ld", i ? ", " : "", nghist[i]);
   printf("], \"ls_evals_hist\": [");
   for (int i = 1; i < 16; i++) printf("%s%ld", i > 1 ? ", " : "", g_ls_hist[i]);
   printf("]}\n");
