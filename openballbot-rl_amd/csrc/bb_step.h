@@ -170,9 +170,7 @@ BB_HD int forward(const ModelT<T>& m, const T* q, const T* v, const T* ctrl, T* 
 #if defined(BB_PHASE_CLOCKS)
   const unsigned long long s_t0 = clock64();
 #endif
-  int it;
-  if constexpr (BODY) it = t16::solve16<BODY>(m, W, ng, nb, acc, tm.tl);
-  else it = t16::solve16_fast(m, W, ng, acc, tm.tl);
+  const int it = t16::solve16<BODY>(m, W, ng, nb, acc, tm.tl);
 #if defined(BB_PHASE_CLOCKS)
   if (BODY && tm.tl == 0) {  // full-kernel solve cycles and Newton iterations
     atomicAdd(&bb_phase_cycles[15], clock64() - s_t0);

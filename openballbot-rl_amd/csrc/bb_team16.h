@@ -197,278 +197,25 @@ __device__ __forceinline__ void ls_term(const ModelT<T>& m, const EnvWork<T>& W,
   lt.prep(c6, c6 + 3, mu, f1, f2, D, D[0] * (wheel ? kdw : T(0.5)));  // Dm = D0 / (mu^2 (1 + mu^2))
 }
 
-// Newton on f(a); a replicated in every lane of the row.  W.H holds the dense
-// mass matrix (packed lower) for this forward, W.qfs the smooth force.
-template <bool BODY, typename T>
-__device__ int solve16(const ModelT<T>& m, EnvWork<T>& W, int ng, int nb, T* a, int tl) {
-  if constexpr (!BODY) nb = 0;
-  const Mass<T>& M = W.M;
-  const int nc = 3 + ng + nb;
-  const int row = tl < NV ? tl : NV - 1;
-  const T muw = m.fr_wheel[0];
-  const T kdw = T(1) / (muw * muw * (1 + muw * muw));
-  PH_DECL
-  int it = 0;
-  for (; it < m.maxiter; it++) {
-    team_sync();
-    // ---- (1) contact pass: -J'f and the ground-block C-weighted J'J, per lane
-    T gc[NV], Hg[21];
-#pragma unroll
-    for (int i = 0; i < NV; i++) gc[i] = 0;
-#pragma unroll
-    for (int i = 0; i < 21; i++) Hg[i] = 0;
-    for (int c = tl; c < 3 + ng; c += L) {
-      const bool wheel = c < 3;  // else ball-hfield
-      T jar[3], Dc = 0, Jg[3][6];
-      if (wheel) {
-#pragma unroll
-        for (int r = 0; r < 3; r++) jar[r] = wheel_dot(W.wc[c], c, r, a) - W.wc[c].aref[r];
-      } else {
-        T ar[3];
-        ground_contact(m, W.g + (c - 3) * NGF, W.P.RB, W.vi, Jg, ar, Dc);
-#pragma unroll
-        for (int r = 0; r < 3; r++) jar[r] = ground_dot(Jg, r, a) - ar[r];
-      }
-      const T D[3] = {wheel ? W.wc[c].D[0] : Dc, wheel ? W.wc[c].D[1] : Dc, wheel ? W.wc[c].D[2] : Dc};
-      const T mu = wheel ? m.fr_wheel[0] : T(1), f1 = wheel ? m.fr_wheel[0] : T(1), f2 = wheel ? m.fr_wheel[1] : T(1);
-      const T Dm = D[0] * (wheel ? kdw : T(0.5));  // 1 / (mu^2 (1 + mu^2))
-      T f[3], Cc[6];
-      cone_sel(jar, mu, f1, f2, D, Dm, f, Cc);
-      if (wheel) {
-        const WheelCon<T>& C = W.wc[c];
-#pragma unroll
-        for (int q = 0; q < 13; q++) {
-          const T j0 = C.J[0][q], j1 = C.J[1][q], j2 = C.J[2][q];
-          W.u.hes.cj[c][0][q] = Cc[0] * j0 + Cc[3] * j1 + Cc[4] * j2;
-          W.u.hes.cj[c][1][q] = Cc[3] * j0 + Cc[1] * j1 + Cc[5] * j2;
-          W.u.hes.cj[c][2][q] = Cc[4] * j0 + Cc[5] * j1 + Cc[2] * j2;
-          const T jf = j0 * f[0] + j1 * f[1] + j2 * f[2];
-          if (q < 6) gc[q] -= jf;
-          else if (q == 6) { gc[6] -= c == 0 ? jf : T(0); gc[7] -= c == 1 ? jf : T(0); gc[8] -= c == 2 ? jf : T(0); }
-          else gc[q + 2] -= jf;
-        }
-      } else {
-        T w[3][6];
-#pragma unroll
-        for (int i = 0; i < 6; i++) {
-          gc[9 + i] -= Jg[0][i] * f[0] + Jg[1][i] * f[1] + Jg[2][i] * f[2];
-          w[0][i] = Cc[0] * Jg[0][i] + Cc[3] * Jg[1][i] + Cc[4] * Jg[2][i];
-          w[1][i] = Cc[3] * Jg[0][i] + Cc[1] * Jg[1][i] + Cc[5] * Jg[2][i];
-          w[2][i] = Cc[4] * Jg[0][i] + Cc[5] * Jg[1][i] + Cc[2] * Jg[2][i];
-        }
-#pragma unroll
-        for (int i = 0; i < 6; i++)
-#pragma unroll
-          for (int j = 0; j <= i; j++) Hg[i * (i + 1) / 2 + j] += Jg[0][i] * w[0][j] + Jg[1][i] * w[1][j] + Jg[2][i] * w[2][j];
-      }
-    }
-    PH(0)
-    // ---- (1b) base-tree contacts, contact-parallel: lane tl rebuilds contact
-    // b0 + tl (Jacobian, cone force and Hessian), adds its -J'f to its gradient
-    // partial (summed below with the rest), then the 16 contacts of the round
-    // are broadcast over the row (DPP) so that every lane accumulates its own
-    // Hessian row sum_b J_b[:, row]' C_b J_b into hb.
-    T hb[NV];
-#pragma unroll
-    for (int i = 0; i < NV; i++) hb[i] = 0;
-    if constexpr (BODY) {
-      for (int b0 = 0; b0 < nb; b0 += L) {  // team-uniform
-        T J[3][13], f[3] = {0, 0, 0}, Cc[6] = {0, 0, 0, 0, 0, 0};
-#pragma unroll
-        for (int r = 0; r < 3; r++)
-#pragma unroll
-          for (int q = 0; q < 13; q++) J[r][q] = 0;
-        int hinge = -1;
-        if (b0 + tl < nb) {
-          T ar[3], Dc;
-          body_contact(m, body_slot(W.bc, W.bspill, b0 + tl), W.P, W.vi, J, hinge, ar, Dc);
-          T jar[3];
-#pragma unroll
-          for (int r = 0; r < 3; r++) jar[r] = body_dot(J, hinge, r, a) - ar[r];
-          const T D[3] = {Dc, Dc, Dc};
-          cone_sel(jar, T(1), T(1), T(1), D, Dc * T(0.5), f, Cc);
-#pragma unroll
-          for (int q = 0; q < 13; q++) {
-            const T jf = J[0][q] * f[0] + J[1][q] * f[1] + J[2][q] * f[2];
-            if (q < 6) gc[q] -= jf;
-            else if (q == 6) { gc[6] -= hinge == 0 ? jf : T(0); gc[7] -= hinge == 1 ? jf : T(0); gc[8] -= hinge == 2 ? jf : T(0); }
-            else gc[q + 2] -= jf;
-          }
-        }
-        const int cnt = nb - b0;
-        static_for<L>([&](auto jc_) {
-          constexpr int j = decltype(jc_)::value;
-          if (j < cnt) {  // team-uniform
-            const int hj = __builtin_amdgcn_update_dpp(0, hinge, 0x150 + j, 0xF, 0xF, false);
-            T Jb[3][13], Cb[6];
-#pragma unroll
-            for (int r = 0; r < 3; r++)
-#pragma unroll
-              for (int q = 0; q < 13; q++) Jb[r][q] = bcast<j>(J[r][q]);
-#pragma unroll
-            for (int r = 0; r < 6; r++) Cb[r] = bcast<j>(Cc[r]);
-            // this row's column of J_b (dof row -> column position, or none)
-            const int prow = row < 6 ? row : (row < 9 ? (row == 6 + hj ? 6 : -1) : row - 2);
-            T jc[3] = {0, 0, 0};
-#pragma unroll
-            for (int q = 0; q < 13; q++)
-#pragma unroll
-              for (int r = 0; r < 3; r++) jc[r] = prow == q ? Jb[r][q] : jc[r];
-            const T w0 = Cb[0] * jc[0] + Cb[3] * jc[1] + Cb[4] * jc[2];
-            const T w1 = Cb[3] * jc[0] + Cb[1] * jc[1] + Cb[5] * jc[2];
-            const T w2 = Cb[4] * jc[0] + Cb[5] * jc[1] + Cb[2] * jc[2];
-#pragma unroll
-            for (int q = 0; q < 13; q++) {
-              const T add = w0 * Jb[0][q] + w1 * Jb[1][q] + w2 * Jb[2][q];
-              if (q < 6) hb[q] += add;
-              else if (q == 6) { hb[6] += hj == 0 ? add : T(0); hb[7] += hj == 1 ? add : T(0); hb[8] += hj == 2 ? add : T(0); }
-              else hb[q + 2] += add;
-            }
-          }
-        });
-      }
-    }
-    // ---- (2) team sums (DPP)
-#pragma unroll
-    for (int i = 0; i < NV; i++) gc[i] = tsum(gc[i]);
-#pragma unroll
-    for (int i = 0; i < 21; i++) Hg[i] = tsum(Hg[i]);
-    team_sync();  // cj visible to every row owner
-    PH(1)
-    // ---- (3) gradient, replicated
-    T gn = 0;
-    {
-      T Ma[NV];
-      mass_mul(M, a, Ma);
-#pragma unroll
-      for (int i = 0; i < NV; i++) {
-        const T mq = Ma[i] - W.qfs[i];
-        const T gi = mq + gc[i];
-        W.mq[i] = mq;  // every lane stores the same value
-        W.gv[i] = gi;
-        gn += gi * gi;
-      }
-    }
-    if (m.scale * m.scale * gn < m.tol * m.tol) break;  // scale * ||g|| < tol without the sqrt
-    PH(2)
-    // ---- (4) Hessian row `row` in registers
-    T h[NV];
-#pragma unroll
-    for (int k = 0; k < NV; k++) h[k] = W.H[hidx(row, k)];
-    static_for<3>([&](auto wc_) {
-      constexpr int w = decltype(wc_)::value;
-      const int p = wheel_pos(row, w);
-      if (p >= 0) {
-        const WheelCon<T>& C = W.wc[w];
-        const T j0 = C.J[0][p], j1 = C.J[1][p], j2 = C.J[2][p];
-#pragma unroll
-        for (int q = 0; q < 13; q++) {
-          const int k = wheel_col(q, w);
-          h[k] += j0 * W.u.hes.cj[w][0][q] + j1 * W.u.hes.cj[w][1][q] + j2 * W.u.hes.cj[w][2][q];
-        }
-      }
-    });
-#pragma unroll
-    for (int ai = 0; ai < 6; ai++)
-#pragma unroll
-      for (int b = 0; b < 6; b++) {
-        const T v = Hg[ai >= b ? ai * (ai + 1) / 2 + b : b * (b + 1) / 2 + ai];
-        h[9 + b] += row == 9 + ai ? v : T(0);
-      }
-    // base-tree contacts: this lane's row, accumulated in the contact pass
-#pragma unroll
-    for (int k = 0; k < NV; k++) h[k] += hb[k];
-    T hdi = 0;
-#pragma unroll
-    for (int k = 0; k < NV; k++) hdi = row == k ? h[k] : hdi;
-    PH(3)
-    // ---- (5) factorise and solve
-    T diag[NV], s[NV], sown;
-    chol_rows(h, hdi, diag, tl);
-    PH(4)
-    chol_solve_rows(h, diag, W.gv[row], s, sown, tl);
-    T d0 = 0;
-    bool fin = true;
-#pragma unroll
-    for (int i = 0; i < NV; i++) { fin = fin && isfinite(s[i]); d0 += s[i] * W.gv[i]; }
-    if (!fin || !(d0 < 0)) {
-      d0 = 0;
-#pragma unroll
-      for (int i = 0; i < NV; i++) {
-        s[i] = -W.gv[i] / maxT(mass_entry(M, i, i), T(1e-30));
-        d0 += s[i] * W.gv[i];
-      }
-      if (!(d0 < 0)) break;
-    }
-    PH(5)
-    // ---- (6) exact line search
-    T Ms[NV];
-    mass_mul(M, s, Ms);
-    T sMs = 0, gs = 0;
-#pragma unroll
-    for (int i = 0; i < NV; i++) { sMs += s[i] * Ms[i]; gs += s[i] * W.mq[i]; }
-    // line-search terms of this lane's first contact in registers; later
-    // rounds (more than 16 contacts) rebuild theirs per evaluation
-    LsTerm<T> lt;
-    ls_term<BODY>(m, W, tl, ng, nc, a, s, kdw, lt);
-    LineSearch<T> lsr;
-    lsr.init(d0);
-    bool ls_ok = false;
-    PH(8)
-    for (int ls = 1; ls <= m.ls_maxiter; ls++) {
-#if defined(BB_PHASE_CLOCKS) && defined(__HIP_DEVICE_COMPILE__)
-      if (tl == 0) atomicAdd(&bb_phase_cycles[11], 1ull);  // line-search evaluations
-#endif
-      const T alpha = lsr.alpha;
-      T d1p = 0, d2p = 0, dmp = 0;
-      lt.eval(alpha, d1p, d2p, dmp);
-      for (int c = tl + L; c < nc; c += L) {
-        LsTerm<T> lc;
-        ls_term<BODY>(m, W, c, ng, nc, a, s, kdw, lc);
-        lc.eval(alpha, d1p, d2p, dmp);
-      }
-      const T d1 = gs + alpha * sMs + tsum(d1p);
-      const T d2 = sMs + tsum(d2p);
-      const T dmag = fabs(gs) + fabs(alpha * sMs) + tsum(dmp);
-      if (fabs(d1) <= m.ls_tol * fabs(d0) || fabs(d1) <= T(32) * eps_of<T>() * dmag) { ls_ok = true; break; }
-      if (!(d1 == d1)) break;
-      lsr.update(d1, d2);
-      // stop at the nearest near-kink the step would cross (first-round
-      // contacts; exact team minimum, so every lane takes the same alpha)
-      const bool up = lsr.alpha > lsr.prev;
-      const T big = T(1e30);
-      const T kv = tmin(lsr.crosses(lt.kink) ? (up ? lt.kink : -lt.kink) : big);
-      const T ks = up ? kv : -kv;
-      lsr.dx = kv < big ? fabs(ks - lsr.prev) : lsr.dx;
-      lsr.alpha = kv < big ? ks : lsr.alpha;
-    }
-    if (!ls_ok) lsr.alpha = lsr.fallback();
-    PH(9)
-    const T alpha = lsr.alpha;
-    if (!(alpha > 0)) break;
-    T sn = 0, an2 = 0;
-#pragma unroll
-    for (int i = 0; i < NV; i++) { a[i] += alpha * s[i]; sn += s[i] * s[i]; an2 += a[i] * a[i]; }
-    PH(6)
-    if (alpha * alpha * sn <= T(1e-30) + m.step_rel2 * (1 + an2)) { it++; break; }
-  }
-  PH(7)
-  PH_FLUSH((Team{L, tl}))
-  return it;
-}
-
 // ---------------------------------------------------------------------------
-// Fast-kernel solve (no base-tree contacts).  Same Newton / line search as
-// solve16; what differs is where the work sits:
-//   per forward    lane 3+c builds ball-terrain contact c's Jacobian, aref and D
-//                  once (ground_setup) into LDS for c < GC_LDS (the BODY-only
-//                  W.bc region and the mass blocks, dead during the solve);
-//                  later contacts (rare: more than 13) are rebuilt per use
+// Newton on f(a) (mj_solNewton), a replicated in every lane of the row; W.H
+// holds the dense mass matrix (packed lower) for this forward, W.qfs the
+// smooth force.  The host reference (bb_solve.h:solve_team) runs the same
+// iteration serially.  Work split over the 16 lanes:
+//   per forward    fast kernel: lane 3+c builds ball-terrain contact c's
+//                  Jacobian, aref and D once (ground_setup) into LDS for
+//                  c < GC_LDS (the BODY-only W.bc region and the mass blocks,
+//                  dead during the solve); later contacts (rare: more than 13)
+//                  and the full kernel's rebuild them per use
 //   contact pass   wheel lanes publish C J and f (LDS); ground lanes add their
-//                  ball-block gradient and C-weighted J'J partials
+//                  ball-block gradient and C-weighted J'J partials; base-tree
+//                  contacts (full kernel) are rebuilt by one lane each and
+//                  broadcast (DPP) so that every lane adds its own Hessian row
+//                  and gradient entry
 //   gradient       lane i: g_i = (M a)_i - qfs_i - sum_w J_w[:,i]' f_w from its
 //                  dense M row and the wheel data, plus the team-summed
-//                  ball-block ground part: 6 + 21 team sums (solve16: 15 + 21)
+//                  ball-block ground part: 6 + 21 team sums (all-replicated
+//                  gradient: 15 + 21)
 //   line search    s'M s and s'(M a - qfs) from the rows (team sums, no
 //                  replicated mass products); each contact term from the
 //                  contact pass's jar and the stored Jacobian
@@ -503,10 +250,11 @@ __device__ __forceinline__ void ground_setup(const ModelT<T>& m, EnvWork<T>& W, 
   }
 }
 
-// ground contact c's Jacobian, aref and D: stored, or rebuilt past GC_LDS
-template <typename T>
+// ground contact c's Jacobian, aref and D: stored (fast kernel), or rebuilt
+// past GC_LDS and in the full kernel (its W.bc holds the base-tree contacts)
+template <bool BODY, typename T>
 __device__ __forceinline__ void ground_get(const ModelT<T>& m, EnvWork<T>& W, int c, T (&J)[3][6], T (&ar)[3], T& D) {
-  if (c < GC_LDS) {
+  if (!BODY && c < GC_LDS) {
     const T* o = W.bc + c * 18;
 #pragma unroll
     for (int r = 0; r < 3; r++)
@@ -521,9 +269,11 @@ __device__ __forceinline__ void ground_get(const ModelT<T>& m, EnvWork<T>& W, in
   }
 }
 
-template <typename T>
-__device__ int solve16_fast(const ModelT<T>& m, EnvWork<T>& W, int ng, T* a, int tl) {
-  const int nc = 3 + ng;
+template <bool BODY, typename T>
+__device__ int solve16(const ModelT<T>& m, EnvWork<T>& W, int ng, int nb, T* a, int tl) {
+  if constexpr (!BODY) nb = 0;
+  const int ngc = 3 + ng;    // wheel and ball-terrain contacts
+  const int nc = ngc + nb;   // + base-tree contacts
   const bool rowl = tl < NV;
   const int row = rowl ? tl : NV - 1;
   const T muw = m.fr_wheel[0];
@@ -540,7 +290,7 @@ __device__ int solve16_fast(const ModelT<T>& m, EnvWork<T>& W, int ng, T* a, int
 #pragma unroll
     for (int i = 0; i < 21; i++) Hg[i] = 0;
     T jar0[3] = {0, 0, 0};  // this lane's first contact, kept for the line search
-    for (int c = tl; c < nc; c += L) {
+    for (int c = tl; c < ngc; c += L) {
       const bool wheel = c < 3;
       T jar[3], Dc = 0, Jg[3][6];
       if (wheel) {
@@ -548,7 +298,7 @@ __device__ int solve16_fast(const ModelT<T>& m, EnvWork<T>& W, int ng, T* a, int
         for (int r = 0; r < 3; r++) jar[r] = wheel_dot(W.wc[c], c, r, a) - W.wc[c].aref[r];
       } else {
         T ar[3];
-        ground_get(m, W, c - 3, Jg, ar, Dc);
+        ground_get<BODY>(m, W, c - 3, Jg, ar, Dc);
 #pragma unroll
         for (int r = 0; r < 3; r++) jar[r] = ground_dot(Jg, r, a) - ar[r];
       }
@@ -587,6 +337,67 @@ __device__ int solve16_fast(const ModelT<T>& m, EnvWork<T>& W, int ng, T* a, int
           for (int j = 0; j <= i; j++) Hg[i * (i + 1) / 2 + j] += Jg[0][i] * w[0][j] + Jg[1][i] * w[1][j] + Jg[2][i] * w[2][j];
       }
     }
+    // base-tree contacts (full kernel), contact-parallel: lane tl rebuilds
+    // contact b0 + tl (Jacobian, cone force and Hessian); the 16 contacts of
+    // the round are then broadcast over the row (DPP) so that every lane adds
+    // its own Hessian row sum_b J_b[:, row]' C_b J_b and gradient entry
+    // -J_b[:, row]' f_b
+    T hb[NV], gb = 0;
+#pragma unroll
+    for (int i = 0; i < NV; i++) hb[i] = 0;
+    if constexpr (BODY) {
+      for (int b0 = 0; b0 < nb; b0 += L) {  // team-uniform
+        T J[3][13], f[3] = {0, 0, 0}, Cc[6] = {0, 0, 0, 0, 0, 0};
+#pragma unroll
+        for (int r = 0; r < 3; r++)
+#pragma unroll
+          for (int q = 0; q < 13; q++) J[r][q] = 0;
+        int hinge = -1;
+        if (b0 + tl < nb) {
+          T ar[3], Dc;
+          body_contact(m, body_slot(W.bc, W.bspill, b0 + tl), W.P, W.vi, J, hinge, ar, Dc);
+          T jar[3];
+#pragma unroll
+          for (int r = 0; r < 3; r++) jar[r] = body_dot(J, hinge, r, a) - ar[r];
+          const T D[3] = {Dc, Dc, Dc};
+          cone_sel(jar, T(1), T(1), T(1), D, Dc * T(0.5), f, Cc);
+        }
+        const int cnt = nb - b0;
+        static_for<L>([&](auto jc_) {
+          constexpr int j = decltype(jc_)::value;
+          if (j < cnt) {  // team-uniform
+            const int hj = __builtin_amdgcn_update_dpp(0, hinge, 0x150 + j, 0xF, 0xF, false);
+            T Jb[3][13], Cb[6], fb[3];
+#pragma unroll
+            for (int r = 0; r < 3; r++)
+#pragma unroll
+              for (int q = 0; q < 13; q++) Jb[r][q] = bcast<j>(J[r][q]);
+#pragma unroll
+            for (int r = 0; r < 6; r++) Cb[r] = bcast<j>(Cc[r]);
+#pragma unroll
+            for (int r = 0; r < 3; r++) fb[r] = bcast<j>(f[r]);
+            // this row's column of J_b (dof row -> column position, or none)
+            const int prow = row < 6 ? row : (row < 9 ? (row == 6 + hj ? 6 : -1) : row - 2);
+            T jc[3] = {0, 0, 0};
+#pragma unroll
+            for (int q = 0; q < 13; q++)
+#pragma unroll
+              for (int r = 0; r < 3; r++) jc[r] = prow == q ? Jb[r][q] : jc[r];
+            gb -= jc[0] * fb[0] + jc[1] * fb[1] + jc[2] * fb[2];
+            const T w0 = Cb[0] * jc[0] + Cb[3] * jc[1] + Cb[4] * jc[2];
+            const T w1 = Cb[3] * jc[0] + Cb[1] * jc[1] + Cb[5] * jc[2];
+            const T w2 = Cb[4] * jc[0] + Cb[5] * jc[1] + Cb[2] * jc[2];
+#pragma unroll
+            for (int q = 0; q < 13; q++) {
+              const T add = w0 * Jb[0][q] + w1 * Jb[1][q] + w2 * Jb[2][q];
+              if (q < 6) hb[q] += add;
+              else if (q == 6) { hb[6] += hj == 0 ? add : T(0); hb[7] += hj == 1 ? add : T(0); hb[8] += hj == 2 ? add : T(0); }
+              else hb[q + 2] += add;
+            }
+          }
+        });
+      }
+    }
     PH(0)
     // ---- (2) ball-block ground sums (DPP)
 #pragma unroll
@@ -614,7 +425,7 @@ __device__ int solve16_fast(const ModelT<T>& m, EnvWork<T>& W, int ng, T* a, int
     });
 #pragma unroll
     for (int i = 0; i < 6; i++) gi += row == 9 + i ? gg[i] : T(0);
-    gi = rowl ? gi : T(0);
+    gi = rowl ? gi + gb : T(0);
     const T gn = tsum(gi * gi);
     if (m.scale * m.scale * gn < m.tol * m.tol) break;  // scale * ||g|| < tol without the sqrt
     PH(2)
@@ -639,6 +450,10 @@ __device__ int solve16_fast(const ModelT<T>& m, EnvWork<T>& W, int ng, T* a, int
         const T v = Hg[ai >= b ? ai * (ai + 1) / 2 + b : b * (b + 1) / 2 + ai];
         h[9 + b] += row == 9 + ai ? v : T(0);
       }
+    if constexpr (BODY) {
+#pragma unroll
+      for (int k = 0; k < NV; k++) h[k] += hb[k];
+    }
     T hdi = 0;
 #pragma unroll
     for (int k = 0; k < NV; k++) hdi = row == k ? h[k] : hdi;
@@ -670,7 +485,7 @@ __device__ int solve16_fast(const ModelT<T>& m, EnvWork<T>& W, int ng, T* a, int
     const T sMs = tsum(sown * Ms), gs = tsum(sown * mq);
     // this lane's first contact's term from its jar; later rounds rebuild theirs
     LsTerm<T> lt;
-    if (tl < nc) {
+    if (tl < ngc) {
       const bool wheel = tl < 3;
       T x[3], Dc[3];
       if (wheel) {
@@ -679,14 +494,14 @@ __device__ int solve16_fast(const ModelT<T>& m, EnvWork<T>& W, int ng, T* a, int
         for (int r = 0; r < 3; r++) { x[r] = wheel_dot(C, tl, r, s); Dc[r] = C.D[r]; }
       } else {
         T Jg[3][6], ar[3], D;
-        ground_get(m, W, tl - 3, Jg, ar, D);
+        ground_get<BODY>(m, W, tl - 3, Jg, ar, D);
 #pragma unroll
         for (int r = 0; r < 3; r++) { x[r] = ground_dot(Jg, r, s); Dc[r] = D; }
       }
       const T mu = wheel ? muw : T(1), f1 = wheel ? muw : T(1), f2 = wheel ? m.fr_wheel[1] : T(1);
       lt.prep(jar0, x, mu, f1, f2, Dc, Dc[0] * (wheel ? kdw : T(0.5)));
     } else {
-      lt.none();
+      ls_term<BODY>(m, W, tl, ng, nc, a, s, kdw, lt);  // a base-tree contact (rebuilt), or none
     }
     LineSearch<T> lsr;
     lsr.init(d0);
@@ -698,7 +513,7 @@ __device__ int solve16_fast(const ModelT<T>& m, EnvWork<T>& W, int ng, T* a, int
       lt.eval(alpha, d1p, d2p, dmp);
       for (int c = tl + L; c < nc; c += L) {
         LsTerm<T> lc;
-        ls_term<false>(m, W, c, ng, nc, a, s, kdw, lc);
+        ls_term<BODY>(m, W, c, ng, nc, a, s, kdw, lc);
         lc.eval(alpha, d1p, d2p, dmp);
       }
       const T d1 = gs + alpha * sMs + tsum(d1p);
