@@ -103,7 +103,6 @@ struct EnvWork {
                                              // registers across the solves)
   T qfs[NV];                                 // smooth force of the current forward
   T vi[NV];                                  // stage velocity (pre-phase; constraint aref rebuilds)
-  T gv[NV], mq[NV];                          // solver: gradient, M a - qfs (team-replicated)
   StageOut<T> so;                            // stage-4 outputs for obs/reward
   Mass<T> M;                                 // mass-matrix blocks
   WheelCon<T> wc[3];                         // ball-wheel contacts

@@ -107,8 +107,26 @@ __device__ __forceinline__ void cone_sel(const T* jar, T mu, T f1, T f2, const T
 // which wheel dof a 13-column contact Jacobian's column q maps to (-1: none)
 __device__ __forceinline__ int col_dof(int q, int hinge) { return q < 6 ? q : (q == 6 ? (hinge >= 0 ? 6 + hinge : -1) : q + 2); }
 
+// 1/sqrt(x) for the Cholesky pivots: the hardware estimate and one
+// second-order correction r (1 + e/2 + 3e^2/8), e = 1 - x r^2 (the device
+// library's sequence without its inf/zero class check: the pivots are
+// floored, so x > 0 and finite); the pivot chain is the factorisation's
+// critical path
+template <typename T>
+__device__ __forceinline__ T rsqrt_piv(T x) {
+  if constexpr (sizeof(T) == 8) {
+    const double r = __builtin_amdgcn_rsq(x);
+    const double e = fma(-x * r, r, 1.0);
+    return fma(r * e, fma(e, 0.375, 0.5), r);
+  } else {
+    return __builtin_amdgcn_rsqf(x);
+  }
+}
+
 // Cholesky of the register-distributed H (lane i holds row h[0..14]); on exit
 // lane i holds L_ik (k < i) in h[k] and every lane holds diag[] = 1 / L_jj.
+// Entries right of a lane's diagonal (the upper triangle) are updated too,
+// without a select: they are never read, by the factorisation or the solves.
 template <typename T>
 __device__ __forceinline__ void chol_rows(T (&h)[NV], T hdi, T (&diag)[NV], int tl) {
   static_for<NV>([&](auto jc) {
@@ -116,42 +134,56 @@ __device__ __forceinline__ void chol_rows(T (&h)[NV], T hdi, T (&diag)[NV], int 
     T piv = bcast<j>(h[j]);
     const T hdj = bcast<j>(hdi);
     const T fl = pivot_eps<T>() * maxT(hdj, T(1e-30));
-    piv = piv > fl ? piv : fl;
-    const T id = rsqrt(piv);  // 1 / L_jj in one reciprocal square root (no sqrt + divide chain)
+    piv = fmax(piv, fl);  // one v_max on the pivot chain (piv is finite or the direction is rejected)
+    const T id = rsqrt_piv(piv);  // 1 / L_jj in one reciprocal square root (no sqrt + divide chain)
     diag[j] = id;  // inverse pivot: the solves multiply
-    const T lij = h[j] * id;
-    h[j] = tl > j ? lij : h[j];
+    h[j] *= id;
     static_for<NV - 1 - j>([&](auto kc) {
       constexpr int k = j + 1 + decltype(kc)::value;
       const T lkj = bcast<k>(h[j]);
-      const T upd = h[k] - h[j] * lkj;
-      h[k] = tl >= k ? upd : h[k];
+      h[k] -= h[j] * lkj;
     });
   });
 }
 
 // s = -(L L')^-1 g with L distributed by rows (lane i: L_i,0..i-1 in h[]);
 // lane i supplies g_i (gown) and gets the whole s (replicated) plus its own
-// component s_i (sown); lanes >= NV get sown = 0
+// component s_i (sown); lanes >= NV get sown = 0.
+//   forward   L y = -g, column sweep: lane j's right-hand side broadcast, every
+//             later row updates its own
+//   backward  L' s = y, column sweep over L' after a transpose through LDS
+//             (scr: >= NV (NV - 1) / 2 elements of team scratch): lane k holds
+//             column k of L, so s_i needs one broadcast instead of a team sum
 template <typename T>
 __device__ __forceinline__ void chol_solve_rows(const T (&h)[NV], const T (&diag)[NV], T gown, T (&s)[NV], T& sown,
-                                                int tl) {
-  // forward: L y = -g, column sweep; b = this lane's running right-hand side
+                                                int tl, T* scr) {
   T b = tl < NV ? -gown : T(0);
-  T y[NV];
+  T z = 0;  // y of this lane's row
   static_for<NV>([&](auto jc) {
     constexpr int j = decltype(jc)::value;
     const T yj = bcast<j>(b) * diag[j];
-    y[j] = yj;
-    b -= tl > j ? h[j] * yj : T(0);
+    z = tl == j ? yj : z;
+    b -= h[j] * yj;  // rows <= j no longer read their right-hand side
   });
-  // backward: L' s = y; s_i = (y_i - sum_{k>i} L_ki s_k) / L_ii, lane k holds L_ki
-  T own = 0;  // s of this lane's row
+  // strictly lower L, packed by rows (row i at i (i - 1) / 2)
+  if (tl < NV) {
+    static_for<NV - 1>([&](auto kc) {
+      constexpr int k = decltype(kc)::value;
+      if (k < tl) scr[tl * (tl - 1) / 2 + k] = h[k];
+    });
+  }
+  team_sync();
+  T Lc[NV];  // Lc[i] = L_i,tl below the diagonal, else 0
+  static_for<NV>([&](auto ic) {
+    constexpr int i = decltype(ic)::value;
+    Lc[i] = (i > tl) ? scr[i * (i - 1) / 2 + tl] : T(0);
+  });
+  T own = 0;
   static_for<NV>([&](auto ic) {
     constexpr int i = NV - 1 - decltype(ic)::value;
-    const T part = (tl > i && tl < NV) ? h[i] * own : T(0);
-    const T si = (y[i] - tsum(part)) * diag[i];
+    const T si = bcast<i>(z) * diag[i];
     s[i] = si;
+    z -= Lc[i] * si;
     own = tl == i ? si : own;
   });
   sown = own;
@@ -279,6 +311,7 @@ __device__ int solve16(const ModelT<T>& m, EnvWork<T>& W, int ng, int nb, T* a, 
   const T muw = m.fr_wheel[0];
   const T kdw = T(1) / (muw * muw * (1 + muw * muw));
   const T qfs_i = W.qfs[row];
+  const int gcol = row - 9;  // this row's ball dof (rows 9..14), else < 0
   PH_DECL
   int it = 0;
   for (; it < m.maxiter; it++) {
@@ -404,7 +437,11 @@ __device__ int solve16(const ModelT<T>& m, EnvWork<T>& W, int ng, int nb, T* a, 
     for (int i = 0; i < 6; i++) gg[i] = tsum(gg[i]);
 #pragma unroll
     for (int i = 0; i < 21; i++) Hg[i] = tsum(Hg[i]);
-    team_sync();  // cj, wf visible to every row owner
+    if (tl == 0) {  // identical in every lane: the ball-row owners read their row from LDS
+#pragma unroll
+      for (int i = 0; i < 21; i++) W.u.hes.hg[i] = Hg[i];
+    }
+    team_sync();  // cj, wf, hg visible to every row owner
     PH(1)
     // ---- (3) gradient, row i: (M a)_i - qfs_i - sum_w J_w[:,i]' f_w (+ ground)
     T h[NV];
@@ -443,13 +480,10 @@ __device__ int solve16(const ModelT<T>& m, EnvWork<T>& W, int ng, int nb, T* a, 
         }
       }
     });
+    if (gcol >= 0) {
 #pragma unroll
-    for (int ai = 0; ai < 6; ai++)
-#pragma unroll
-      for (int b = 0; b < 6; b++) {
-        const T v = Hg[ai >= b ? ai * (ai + 1) / 2 + b : b * (b + 1) / 2 + ai];
-        h[9 + b] += row == 9 + ai ? v : T(0);
-      }
+      for (int b = 0; b < 6; b++) h[9 + b] += W.u.hes.hg[gcol >= b ? gcol * (gcol + 1) / 2 + b : b * (b + 1) / 2 + gcol];
+    }
     if constexpr (BODY) {
 #pragma unroll
       for (int k = 0; k < NV; k++) h[k] += hb[k];
@@ -462,7 +496,7 @@ __device__ int solve16(const ModelT<T>& m, EnvWork<T>& W, int ng, int nb, T* a, 
     T diag[NV], s[NV], sown;
     chol_rows(h, hdi, diag, tl);
     PH(4)
-    chol_solve_rows(h, diag, gi, s, sown, tl);
+    chol_solve_rows(h, diag, gi, s, sown, tl, &W.u.hes.cj[0][0][0]);  // cj is dead after the Hessian
     T d0 = tsum(sown * gi);
     bool fin = true;
 #pragma unroll
