@@ -312,11 +312,23 @@ __device__ int solve16(const ModelT<T>& m, EnvWork<T>& W, int ng, int nb, T* a, 
   const T kdw = T(1) / (muw * muw * (1 + muw * muw));
   const T qfs_i = W.qfs[row];
   const int gcol = row - 9;  // this row's ball dof (rows 9..14), else < 0
+  // the wheels' f and C (packed C[6], f[3] each) go through LDS (the wf + hg
+  // scratch).  Publishing the ball-terrain contacts' the same way for the
+  // ball-row owners was measured and dropped: the per-contact LDS loop on the
+  // row lanes exposes its latency (flat 0.808 ms/step against 0.666 with the
+  // ball-block team sums)
+  static_assert(offsetof(typename EnvWork<T>::U, hes.hg) == offsetof(typename EnvWork<T>::U, hes.wf) + 9 * sizeof(T),
+                "wheel f/C scratch needs wf and hg adjacent");
+  T* const wCf = &W.u.hes.wf[0][0];
+  const bool gsum = ng > 0;  // team-uniform
   PH_DECL
   int it = 0;
   for (; it < m.maxiter; it++) {
     team_sync();
-    // ---- (1) contact pass, contact-parallel (c = tl, tl + 16, ...)
+    // ---- (1) contact pass, contact-parallel (c = tl, tl + 16, ...): the
+    // wheels' cone force f and Hessian C (3x3, packed) into LDS for the row
+    // owners; ball-terrain contacts add ball-block gradient and C-weighted J'J
+    // partials for team sums
     T gg[6], Hg[21];
 #pragma unroll
     for (int i = 0; i < 6; i++) gg[i] = 0;
@@ -345,16 +357,11 @@ __device__ int solve16(const ModelT<T>& m, EnvWork<T>& W, int ng, int nb, T* a, 
       T f[3], Cc[6];
       cone_sel(jar, mu, f1, f2, D, Dm, f, Cc);
       if (wheel) {
-        const WheelCon<T>& C = W.wc[c];
+        T* p = wCf + 9 * c;
 #pragma unroll
-        for (int q = 0; q < 13; q++) {
-          const T j0 = C.J[0][q], j1 = C.J[1][q], j2 = C.J[2][q];
-          W.u.hes.cj[c][0][q] = Cc[0] * j0 + Cc[3] * j1 + Cc[4] * j2;
-          W.u.hes.cj[c][1][q] = Cc[3] * j0 + Cc[1] * j1 + Cc[5] * j2;
-          W.u.hes.cj[c][2][q] = Cc[4] * j0 + Cc[5] * j1 + Cc[2] * j2;
-        }
+        for (int r = 0; r < 6; r++) p[r] = Cc[r];
 #pragma unroll
-        for (int r = 0; r < 3; r++) W.u.hes.wf[c][r] = f[r];
+        for (int r = 0; r < 3; r++) p[6 + r] = f[r];
       } else {
         T w[3][6];
 #pragma unroll
@@ -432,16 +439,14 @@ __device__ int solve16(const ModelT<T>& m, EnvWork<T>& W, int ng, int nb, T* a, 
       }
     }
     PH(0)
-    // ---- (2) ball-block ground sums (DPP)
+    // ---- (2) ball-block sums of the team-summed ground contacts (DPP)
+    if (gsum) {
 #pragma unroll
-    for (int i = 0; i < 6; i++) gg[i] = tsum(gg[i]);
+      for (int i = 0; i < 6; i++) gg[i] = tsum(gg[i]);
 #pragma unroll
-    for (int i = 0; i < 21; i++) Hg[i] = tsum(Hg[i]);
-    if (tl == 0) {  // identical in every lane: the ball-row owners read their row from LDS
-#pragma unroll
-      for (int i = 0; i < 21; i++) W.u.hes.hg[i] = Hg[i];
+      for (int i = 0; i < 21; i++) Hg[i] = tsum(Hg[i]);
     }
-    team_sync();  // cj, wf, hg visible to every row owner
+    team_sync();  // contact f and C visible to every row owner
     PH(1)
     // ---- (3) gradient, row i: (M a)_i - qfs_i - sum_w J_w[:,i]' f_w (+ ground)
     T h[NV];
@@ -457,32 +462,44 @@ __device__ int solve16(const ModelT<T>& m, EnvWork<T>& W, int ng, int nb, T* a, 
       const int p = wheel_pos(row, w);
       if (p >= 0) {
         const WheelCon<T>& C = W.wc[w];
-        gi -= C.J[0][p] * W.u.hes.wf[w][0] + C.J[1][p] * W.u.hes.wf[w][1] + C.J[2][p] * W.u.hes.wf[w][2];
+        const T* q = wCf + 9 * w + 6;
+        gi -= C.J[0][p] * q[0] + C.J[1][p] * q[1] + C.J[2][p] * q[2];
       }
     });
+    if (gsum) {
 #pragma unroll
-    for (int i = 0; i < 6; i++) gi += row == 9 + i ? gg[i] : T(0);
+      for (int i = 0; i < 6; i++) gi += row == 9 + i ? gg[i] : T(0);
+    }
     gi = rowl ? gi + gb : T(0);
     const T gn = tsum(gi * gi);
     if (m.scale * m.scale * gn < m.tol * m.tol) break;  // scale * ||g|| < tol without the sqrt
     PH(2)
     // ---- (4) Hessian row: M row + wheel blocks + ground block
+    // J[:, p]' C J for a contact: w = C J[:, p] (C packed xx,yy,zz,xy,xz,yz)
+    auto cw = [](const T* C, T j0, T j1, T j2, T& w0, T& w1, T& w2) {
+      w0 = C[0] * j0 + C[3] * j1 + C[4] * j2;
+      w1 = C[3] * j0 + C[1] * j1 + C[5] * j2;
+      w2 = C[4] * j0 + C[5] * j1 + C[2] * j2;
+    };
     static_for<3>([&](auto wc_) {
       constexpr int w = decltype(wc_)::value;
       const int p = wheel_pos(row, w);
       if (p >= 0) {
         const WheelCon<T>& C = W.wc[w];
-        const T j0 = C.J[0][p], j1 = C.J[1][p], j2 = C.J[2][p];
+        T w0, w1, w2;
+        cw(wCf + 9 * w, C.J[0][p], C.J[1][p], C.J[2][p], w0, w1, w2);
 #pragma unroll
-        for (int q = 0; q < 13; q++) {
-          const int k = wheel_col(q, w);
-          h[k] += j0 * W.u.hes.cj[w][0][q] + j1 * W.u.hes.cj[w][1][q] + j2 * W.u.hes.cj[w][2][q];
-        }
+        for (int q = 0; q < 13; q++) h[wheel_col(q, w)] += w0 * C.J[0][q] + w1 * C.J[1][q] + w2 * C.J[2][q];
       }
     });
-    if (gcol >= 0) {
+    if (gsum) {
 #pragma unroll
-      for (int b = 0; b < 6; b++) h[9 + b] += W.u.hes.hg[gcol >= b ? gcol * (gcol + 1) / 2 + b : b * (b + 1) / 2 + gcol];
+      for (int ai = 0; ai < 6; ai++)
+#pragma unroll
+        for (int b = 0; b < 6; b++) {
+          const T v = Hg[ai >= b ? ai * (ai + 1) / 2 + b : b * (b + 1) / 2 + ai];
+          h[9 + b] += row == 9 + ai ? v : T(0);
+        }
     }
     if constexpr (BODY) {
 #pragma unroll
