@@ -38,6 +38,7 @@ int main(int argc, char** argv) {
   long fwd = 0, newton = 0, ls0 = 0, resets = 0;
   long hist[32] = {0};
   long nghist[32] = {0};  // ball-terrain contacts at the last RK stage
+  FILE* dump = getenv("BB_DUMP_ITERS") ? fopen(getenv("BB_DUMP_ITERS"), "w") : nullptr;
   for (int t = 0; t < steps; t++) {
     for (int e = 0; e < n; e++) {
       float a[3] = {U(rng), U(rng), U(rng)}, obs[15], r, p2[2];
@@ -45,6 +46,7 @@ int main(int argc, char** argv) {
       const long lsb = g_ls_evals;
       int fl = env_step<double, false>(m, cfg, &q[e * NQ], &v[e * NV], &w[e * NV], st[e], a, tr, W, obs, r, p2, &it,
                                        Team{1, 0});
+      if (dump && t >= skip) fprintf(dump, "%d %d %d\n", t, e, it);
       if (t >= skip) {
         nghist[W.so.ng < 31 ? W.so.ng : 31]++;
         fwd += 4; newton += it; ls0 += g_ls_evals - lsb;
