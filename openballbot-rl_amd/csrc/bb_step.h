@@ -107,6 +107,11 @@ BB_HD int forward(const ModelT<T>& m, const T* q, const T* v, const T* ctrl, T* 
 #endif
     // W.H is free until mass_dense_team below: it holds the SAT candidate list
     static_assert(sizeof(W.H) >= t16::CAND_CAP * sizeof(int), "candidate list does not fit W.H");
+#ifdef BB_EXP_DUP_BODYCOL  // timing experiment (tools/lib_bench): the base-tree collision twice
+    { int ov2 = 0; (void)t16::collide_body_team(m, k, tr.hf, tr.size_z, tr.hz, W.bc, W.bspill, &ov2, tm.tl,
+                                                 reinterpret_cast<int*>(W.H)); }
+    asm volatile("" ::: "memory");
+#endif
     nb = t16::collide_body_team(m, k, tr.hf, tr.size_z, tr.hz, W.bc, W.bspill, &overflow, tm.tl,
                                 reinterpret_cast<int*>(W.H));
 #if defined(BB_PHASE_CLOCKS)
@@ -169,6 +174,16 @@ BB_HD int forward(const ModelT<T>& m, const T* q, const T* v, const T* ctrl, T* 
 
 #if defined(BB_PHASE_CLOCKS)
   const unsigned long long s_t0 = clock64();
+#endif
+#ifdef BB_EXP_DUP_SOLVE_FULL  // timing experiment: the full kernel's constraint solve twice
+  if constexpr (BODY) {
+    T acc2[NV];
+#pragma unroll
+    for (int i = 0; i < NV; i++) acc2[i] = acc[i];
+    (void)t16::solve16<BODY>(m, W, ng, nb, acc2, tm.tl);
+    asm volatile("" ::: "memory");
+    team_sync();
+  }
 #endif
   const int it = t16::solve16<BODY>(m, W, ng, nb, acc, tm.tl);
 #if defined(BB_PHASE_CLOCKS)

@@ -407,29 +407,31 @@ __device__ int solve16(const ModelT<T>& m, EnvWork<T>& W, int ng, int nb, T* a, 
           constexpr int j = decltype(jc_)::value;
           if (j < cnt) {  // team-uniform
             const int hj = __builtin_amdgcn_update_dpp(0, hinge, 0x150 + j, 0xF, 0xF, false);
-            T Jb[3][13], Cb[6], fb[3];
-#pragma unroll
-            for (int r = 0; r < 3; r++)
-#pragma unroll
-              for (int q = 0; q < 13; q++) Jb[r][q] = bcast<j>(J[r][q]);
+            T Cb[6], fb[3];
 #pragma unroll
             for (int r = 0; r < 6; r++) Cb[r] = bcast<j>(Cc[r]);
 #pragma unroll
             for (int r = 0; r < 3; r++) fb[r] = bcast<j>(f[r]);
-            // this row's column of J_b (dof row -> column position, or none)
+            // this row's column of J_b (dof row -> column position, or none),
+            // picked from the broadcast Jacobian; the Jacobian is broadcast a
+            // second time for the row accumulation instead of being held (a
+            // held 3x13 copy spilled the full kernel to scratch)
             const int prow = row < 6 ? row : (row < 9 ? (row == 6 + hj ? 6 : -1) : row - 2);
             T jc[3] = {0, 0, 0};
 #pragma unroll
             for (int q = 0; q < 13; q++)
 #pragma unroll
-              for (int r = 0; r < 3; r++) jc[r] = prow == q ? Jb[r][q] : jc[r];
+              for (int r = 0; r < 3; r++) {
+                const T v = bcast<j>(J[r][q]);
+                jc[r] = prow == q ? v : jc[r];
+              }
             gb -= jc[0] * fb[0] + jc[1] * fb[1] + jc[2] * fb[2];
             const T w0 = Cb[0] * jc[0] + Cb[3] * jc[1] + Cb[4] * jc[2];
             const T w1 = Cb[3] * jc[0] + Cb[1] * jc[1] + Cb[5] * jc[2];
             const T w2 = Cb[4] * jc[0] + Cb[5] * jc[1] + Cb[2] * jc[2];
 #pragma unroll
             for (int q = 0; q < 13; q++) {
-              const T add = w0 * Jb[0][q] + w1 * Jb[1][q] + w2 * Jb[2][q];
+              const T add = w0 * bcast<j>(J[0][q]) + w1 * bcast<j>(J[1][q]) + w2 * bcast<j>(J[2][q]);
               if (q < 6) hb[q] += add;
               else if (q == 6) { hb[6] += hj == 0 ? add : T(0); hb[7] += hj == 1 ? add : T(0); hb[8] += hj == 2 ? add : T(0); }
               else hb[q + 2] += add;
@@ -481,6 +483,28 @@ __device__ int solve16(const ModelT<T>& m, EnvWork<T>& W, int ng, int nb, T* a, 
       w1 = C[3] * j0 + C[1] * j1 + C[5] * j2;
       w2 = C[4] * j0 + C[5] * j1 + C[2] * j2;
     };
+#ifdef BB_EXP_DUP_HESS  // timing experiment: the wheel blocks of the Hessian row twice
+    {
+      T h2[NV];
+#pragma unroll
+      for (int k = 0; k < NV; k++) h2[k] = h[k] * T(0.5);
+      static_for<3>([&](auto wc_) {
+        constexpr int w = decltype(wc_)::value;
+        const int p = wheel_pos(row, w);
+        if (p >= 0) {
+          const WheelCon<T>& C = W.wc[w];
+          T w0, w1, w2;
+          cw(wCf + 9 * w, C.J[0][p], C.J[1][p], C.J[2][p], w0, w1, w2);
+#pragma unroll
+          for (int q = 0; q < 13; q++) h2[wheel_col(q, w)] += w0 * C.J[0][q] + w1 * C.J[1][q] + w2 * C.J[2][q];
+        }
+      });
+      T acc = 0;
+#pragma unroll
+      for (int k = 0; k < NV; k++) acc += h2[k];
+      asm volatile("" :: "v"(acc) : "memory");
+    }
+#endif
     static_for<3>([&](auto wc_) {
       constexpr int w = decltype(wc_)::value;
       const int p = wheel_pos(row, w);
@@ -511,8 +535,25 @@ __device__ int solve16(const ModelT<T>& m, EnvWork<T>& W, int ng, int nb, T* a, 
     PH(3)
     // ---- (5) factorise and solve
     T diag[NV], s[NV], sown;
+#ifdef BB_EXP_DUP_CHOL  // timing experiment (tools/lib_bench): the factorisation twice
+    {
+      T h2[NV], d2[NV];
+#pragma unroll
+      for (int k = 0; k < NV; k++) h2[k] = h[k];
+      chol_rows(h2, hdi, d2, tl);
+      asm volatile("" :: "v"(d2[NV - 1]), "v"(h2[NV - 2]) : "memory");
+    }
+#endif
     chol_rows(h, hdi, diag, tl);
     PH(4)
+#ifdef BB_EXP_DUP_TRSV  // timing experiment: the two triangular sweeps twice
+    {
+      T s2[NV], so2;
+      chol_solve_rows(h, diag, gi, s2, so2, tl, &W.u.hes.cj[0][0][0]);
+      asm volatile("" :: "v"(s2[0]), "v"(so2) : "memory");
+      team_sync();
+    }
+#endif
     chol_solve_rows(h, diag, gi, s, sown, tl, &W.u.hes.cj[0][0][0]);  // cj is dead after the Hessian
     T d0 = tsum(sown * gi);
     bool fin = true;

@@ -34,7 +34,8 @@ def run_one(lib, precision, terrain, steps, warmup):
     from ballbot_gym.envs import BallbotVecEnv
 
     _native.use_diagnostic_library(lib)
-    env = BallbotVecEnv(4096, device="cuda:0", precision=precision, terrain_config={"type": terrain, "config": {}})
+    env = BallbotVecEnv(4096, device="cuda:0", precision=precision, terrain_config={"type": terrain, "config": {}},
+                        n_terrains=None if terrain == "perlin" else 16)
     pool = torch.rand(64, 4096, 3, device="cuda:0") * 2 - 1
     for i in range(warmup):
         env.step_async_raw(pool[i % 64])
