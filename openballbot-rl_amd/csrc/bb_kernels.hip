@@ -184,6 +184,9 @@ __global__ __launch_bounds__(64) void step_kernel(ModelT<T> mg, EnvCfg cfg, Dev 
   }
   if (e >= d.n) return;
   const bool lead = tm.tl == 0;
+#ifdef BB_PHASE_CLOCKS
+  const unsigned long long t_env0 = clock64();
+#endif
   EnvWork<T>& W = team_work<T>(smem, team);
   if (BODY && lead) W.bspill = body_spill_of<T>(d, e);  // read after the forward's first team_sync
   // the env state lives in the team's workspace (every lane writes the same
@@ -233,6 +236,14 @@ __global__ __launch_bounds__(64) void step_kernel(ModelT<T> mg, EnvCfg cfg, Dev 
   if (fl & F_DIVERGED) atomicAdd(&d.stats[1], 1ull);
   if (fl & F_OVERFLOW) atomicAdd(&d.stats[2], 1ull);
   atomicAdd(&d.stats[4], (unsigned long long)iters);
+#ifdef BB_PHASE_CLOCKS
+  {  // per-env step duration: max, sum and count per kernel (full 34-36, fast 37-39)
+    const unsigned long long dt = clock64() - t_env0;
+    atomicMax(&bb_phase_cycles[BODY ? 34 : 37], dt);
+    atomicAdd(&bb_phase_cycles[BODY ? 35 : 38], dt);
+    atomicAdd(&bb_phase_cycles[BODY ? 36 : 39], 1ull);
+  }
+#endif
 }
 
 template <typename T>

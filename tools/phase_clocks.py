@@ -72,6 +72,9 @@ def main():
                               "prisms_per_forward": out[17] / out[12],
                               "prism_rounds_per_forward": out[18] / out[12],
                               "sat_runs_per_forward": out[19] / out[12]}
+    for name, k in (("full", 34), ("fast", 37)):  # per-env step durations (s_memtime cycles)
+        if out[k + 2]:
+            res[f"{name}_env_step_cycles"] = {"max": out[k], "mean": out[k + 1] / out[k + 2], "count": out[k + 2]}
     print(json.dumps(res, indent=1))
 
 
