@@ -29,7 +29,7 @@
 using namespace bb;
 
 #ifdef BB_PHASE_CLOCKS
-namespace bb { __device__ unsigned long long bb_phase_cycles[40]; }
+namespace bb { __device__ unsigned long long bb_phase_cycles[80]; }
 #endif
 
 namespace {
@@ -188,6 +188,9 @@ __global__ __launch_bounds__(64) void step_kernel(ModelT<T> mg, EnvCfg cfg, Dev 
   const unsigned long long t_env0 = clock64();
 #endif
   EnvWork<T>& W = team_work<T>(smem, team);
+#ifdef BB_PHASE_CLOCKS
+  if (lead) W.dbg_nb = 0;
+#endif
   if (BODY && lead) W.bspill = body_spill_of<T>(d, e);  // read after the forward's first team_sync
   // the env state lives in the team's workspace (every lane writes the same
   // values): 47 values held in registers across four solves would spill
@@ -242,6 +245,15 @@ __global__ __launch_bounds__(64) void step_kernel(ModelT<T> mg, EnvCfg cfg, Dev 
     atomicMax(&bb_phase_cycles[BODY ? 34 : 37], dt);
     atomicAdd(&bb_phase_cycles[BODY ? 35 : 38], dt);
     atomicAdd(&bb_phase_cycles[BODY ? 36 : 39], 1ull);
+    // full kernel: step-duration histogram (bins of 2^20 cycles) with the base-tree
+    // contacts and Newton iterations of the envs in each bin
+    if (BODY) {
+      const int bin = int(dt >> 20) < 9 ? int(dt >> 20) : 9;
+      atomicAdd(&bb_phase_cycles[40 + bin], 1ull);
+      atomicAdd(&bb_phase_cycles[50 + bin], (unsigned long long)W.dbg_nb);
+      atomicAdd(&bb_phase_cycles[60 + bin], (unsigned long long)iters);
+      atomicMax(&bb_phase_cycles[70 + bin], (unsigned long long)W.dbg_nb);
+    }
   }
 #endif
 }
@@ -931,8 +943,8 @@ int bb_get_config(bb_handle* h, int32_t* out5) {
 // diagnostic build only: read and clear the per-phase cycle counters
 int bb_debug_phase_cycles(unsigned long long* out16) {
   HIPCHK(hipDeviceSynchronize());
-  HIPCHK(hipMemcpyFromSymbol(out16, HIP_SYMBOL(bb::bb_phase_cycles), sizeof(unsigned long long) * 40));
-  unsigned long long z[40] = {0};
+  HIPCHK(hipMemcpyFromSymbol(out16, HIP_SYMBOL(bb::bb_phase_cycles), sizeof(unsigned long long) * 80));
+  unsigned long long z[80] = {0};
   HIPCHK(hipMemcpyToSymbol(HIP_SYMBOL(bb::bb_phase_cycles), z, sizeof z));
   return 0;
 }

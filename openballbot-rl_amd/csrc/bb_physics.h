@@ -832,117 +832,89 @@ struct Poses {
   T Rb[9], pb[3], RB[9], pB[3];
 };
 
-// Stored base-tree contact -> 13-column Jacobian rows in the wheel-contact
-// layout (base lin 3, base ang 3, hinge 1, ball lin 3, ball ang 3), the hinge
-// slot's wheel (-1: none), aref and D (isotropic friction: mu = 1).
+// Stored base-tree contact in world form.  Its 13-column Jacobian (the
+// wheel-contact layout: base lin 3, base ang 3, hinge 1, ball lin 3, ball ang 3)
+// is J[r][q] = F_r . w_q with F = (n, t1, t2) and one world vector per column:
+//   base lin i   e_i                      base ang i   Rb_i x db
+//   hinge        hw = uw x da             ball lin i   -ball e_i
+//   ball ang i   -ball RB_i x dB
+// (Rb_i, RB_i: body axes, db/dB: contact point from the base/ball origins, uw
+// and da: the wheel's hinge axis and the point from the hinge anchor), so
+// J x = F V(x) with V(x) = x_lin + (Rb x_ang) x db + hw x_h - ball (x_blin +
+// (RB x_bang) x dB) (body_V), and J' C J = W' (F' C F) W: the solve broadcasts
+// A = F' C F and phi = F' f instead of J.  aref and D: isotropic friction,
+// mu = 1 (mj_makeImpedance / mj_instantiateContact).
 template <typename T>
-BB_HD void body_contact(const ModelT<T>& m, const T* bc, const Poses<T>& P, const T* v, T (&J)[3][13], int& hinge,
-                        T (&aref)[3], T& D) {
+struct BodyFrame {
+  T F[3][3], db[3], dB[3], hw[3], aref[3], D, ball;
+  int hinge;  // wheel of the hinge column (-1: none)
+};
+
+// V(x) of a body contact (see BodyFrame): J x = F V(x)
+template <typename T>
+BB_HD void body_V(const BodyFrame<T>& b, const Poses<T>& P, const T* x, T (&V)[3]) {
+  T om[3], wx[3];
+  mv3(om, P.Rb, x + 3);
+  cross3(wx, om, b.db);
+  const T xh = b.hinge >= 0 ? hinge_sel(b.hinge, x) : T(0);
+  T ob[3], bx[3];
+  mv3(ob, P.RB, x + 12);
+  cross3(bx, ob, b.dB);
+#pragma unroll
+  for (int i = 0; i < 3; i++) V[i] = x[i] + wx[i] + b.hw[i] * xh - b.ball * (x[9 + i] + bx[i]);
+}
+
+// stored contact (BF_* fields) -> BodyFrame at the stage velocity v
+template <typename T>
+BB_HD void body_frame(const ModelT<T>& m, const T* bc, const Poses<T>& P, const T* v, BodyFrame<T>& b) {
   const int code = int(bc[BF_CODE]);
   const int b1 = code >> 3, b2 = code & 7;
   const T n[3] = {bc[BF_N], bc[BF_N + 1], bc[BF_N + 2]};
-  const T p[3] = {bc[BF_P], bc[BF_P + 1], bc[BF_P + 2]};
   const T dist = bc[BF_DIST];
   T t1[3], t2[3];
   frame_from_normal(n, t1, t2);
-  const T* F[3] = {n, t1, t2};
-  const T db[3] = {p[0] - P.pb[0], p[1] - P.pb[1], p[2] - P.pb[2]};
-  const T dB[3] = {p[0] - P.pB[0], p[1] - P.pB[1], p[2] - P.pB[2]};
-  hinge = (b2 >= 4 && b2 <= 6) ? b2 - 4 : -1;
-  T uw[3] = {0, 0, 0}, da[3] = {0, 0, 0};
-  if (hinge >= 0) {
-    T t[3];
-    mv3(uw, P.Rb, m.u[hinge]);
-    mv3(t, P.Rb, m.anchor);
-    da[0] = db[0] - t[0]; da[1] = db[1] - t[1]; da[2] = db[2] - t[2];
-  }
-  const T ball = b1 == 7 ? T(1) : T(0);
 #pragma unroll
-  for (int r = 0; r < 3; r++) {
-    T x1[3], x2[3];
-    J[r][0] = F[r][0]; J[r][1] = F[r][1]; J[r][2] = F[r][2];
-    cross3(x1, db, F[r]);
-    mtv3(x2, P.Rb, x1);
-    J[r][3] = x2[0]; J[r][4] = x2[1]; J[r][5] = x2[2];
-    cross3(x1, da, F[r]);
-    J[r][6] = hinge >= 0 ? dot3(uw, x1) : T(0);
-    J[r][7] = -ball * F[r][0]; J[r][8] = -ball * F[r][1]; J[r][9] = -ball * F[r][2];
-    cross3(x1, dB, F[r]);
-    mtv3(x2, P.RB, x1);
-    J[r][10] = -ball * x2[0]; J[r][11] = -ball * x2[1]; J[r][12] = -ball * x2[2];
+  for (int i = 0; i < 3; i++) {
+    b.F[0][i] = n[i]; b.F[1][i] = t1[i]; b.F[2][i] = t2[i];
+    b.db[i] = bc[BF_P + i] - P.pb[i];
+    b.dB[i] = bc[BF_P + i] - P.pB[i];
+    b.hw[i] = 0;
   }
+  b.hinge = (b2 >= 4 && b2 <= 6) ? b2 - 4 : -1;
+  if (b.hinge >= 0) {
+    T uw[3], t[3], da[3];
+    mv3(uw, P.Rb, m.u[b.hinge]);
+    mv3(t, P.Rb, m.anchor);
+    da[0] = b.db[0] - t[0]; da[1] = b.db[1] - t[1]; da[2] = b.db[2] - t[2];
+    cross3(b.hw, uw, da);
+  }
+  b.ball = b1 == 7 ? T(1) : T(0);
   const T iw2 = b2 == 1 ? m.iw_base : (b2 <= 3 ? m.iw_cam[b2 - 2] : m.iw_wheel[b2 - 4]);
   const T tran = iw2 + (b1 == 7 ? m.iw_ball : T(0));
   const T imp = clampT(impedance(m, dist), T(0.0001), T(0.9999));
-  D = T(1) / maxT(T(1e-15), (1 - imp) * tran / imp);
+  b.D = T(1) / maxT(T(1e-15), (1 - imp) * tran / imp);
+  T V[3];
+  body_V(b, P, v, V);
 #pragma unroll
-  for (int r = 0; r < 3; r++) {
-    T vel = 0;
-#pragma unroll
-    for (int q = 0; q < 6; q++) vel += J[r][q] * v[q];
-    vel += hinge >= 0 ? J[r][6] * v[6 + hinge] : T(0);
-#pragma unroll
-    for (int q = 7; q < 13; q++) vel += J[r][q] * v[q + 2];
-    aref[r] = -m.Bd * vel - (r == 0 ? m.K * imp * dist : T(0));
-  }
+  for (int r = 0; r < 3; r++) b.aref[r] = -m.Bd * dot3(b.F[r], V) - (r == 0 ? m.K * imp * dist : T(0));
 }
 
-// line-search terms of a body contact without materialising J: per row r,
-// jar0_r = J_r a - aref_r and J_r s; D returned
+// line-search terms of a body contact: per row r, jar0_r = J_r a - aref_r and
+// J_r s; D returned
 template <typename T>
 BB_HD void body_ls_terms(const ModelT<T>& m, const T* bc, const Poses<T>& P, const T* v, const T* a, const T* s,
                          T (&c6)[6], T& D) {
-  const int code = int(bc[BF_CODE]);
-  const int b1 = code >> 3, b2 = code & 7;
-  const T n[3] = {bc[BF_N], bc[BF_N + 1], bc[BF_N + 2]};
-  const T dist = bc[BF_DIST];
-  T t1[3], t2[3];
-  frame_from_normal(n, t1, t2);
-  const T db[3] = {bc[BF_P] - P.pb[0], bc[BF_P + 1] - P.pb[1], bc[BF_P + 2] - P.pb[2]};
-  const T dB[3] = {bc[BF_P] - P.pB[0], bc[BF_P + 1] - P.pB[1], bc[BF_P + 2] - P.pB[2]};
-  const int hinge = (b2 >= 4 && b2 <= 6) ? b2 - 4 : -1;
-  T uw[3] = {0, 0, 0}, da[3] = {0, 0, 0};
-  if (hinge >= 0) {
-    T t[3];
-    mv3(uw, P.Rb, m.u[hinge]);
-    mv3(t, P.Rb, m.anchor);
-    da[0] = db[0] - t[0]; da[1] = db[1] - t[1]; da[2] = db[2] - t[2];
-  }
-  const T ball = b1 == 7 ? T(1) : T(0);
-  const T iw2 = b2 == 1 ? m.iw_base : (b2 <= 3 ? m.iw_cam[b2 - 2] : m.iw_wheel[b2 - 4]);
-  const T imp = clampT(impedance(m, dist), T(0.0001), T(0.9999));
-  D = T(1) / maxT(T(1e-15), (1 - imp) * (iw2 + (b1 == 7 ? m.iw_ball : T(0))) / imp);
+  BodyFrame<T> b;
+  body_frame(m, bc, P, v, b);
+  T Va[3], Vs[3];
+  body_V(b, P, a, Va);
+  body_V(b, P, s, Vs);
 #pragma unroll
   for (int r = 0; r < 3; r++) {
-    const T* F = r == 0 ? n : (r == 1 ? t1 : t2);
-    T x1[3], wa[3], wB[3];
-    cross3(x1, db, F);
-    mtv3(wa, P.Rb, x1);
-    cross3(x1, da, F);
-    const T jh = hinge >= 0 ? dot3(uw, x1) : T(0);
-    cross3(x1, dB, F);
-    mtv3(wB, P.RB, x1);
-    auto dotJ = [&](const T* x) {
-      T acc = F[0] * x[0] + F[1] * x[1] + F[2] * x[2] + wa[0] * x[3] + wa[1] * x[4] + wa[2] * x[5];
-      acc += hinge >= 0 ? jh * hinge_sel(hinge, x) : T(0);
-      acc -= ball * (F[0] * x[9] + F[1] * x[10] + F[2] * x[11] + wB[0] * x[12] + wB[1] * x[13] + wB[2] * x[14]);
-      return acc;
-    };
-    const T aref = -m.Bd * dotJ(v) - (r == 0 ? m.K * imp * dist : T(0));
-    c6[r] = dotJ(a) - aref;
-    c6[3 + r] = dotJ(s);
+    c6[r] = dot3(b.F[r], Va) - b.aref[r];
+    c6[3 + r] = dot3(b.F[r], Vs);
   }
-}
-
-// J_r x for a body contact in the 13-column layout
-template <typename T>
-BB_HD T body_dot(const T (&J)[3][13], int hinge, int r, const T* x) {
-  T acc = hinge >= 0 ? J[r][6] * hinge_sel(hinge, x) : T(0);
-#pragma unroll
-  for (int q = 0; q < 6; q++) acc += J[r][q] * x[q];
-#pragma unroll
-  for (int q = 7; q < 13; q++) acc += J[r][q] * x[q + 2];
-  return acc;
+  D = b.D;
 }
 
 // mjc_ConvexHField for the ball: sub-grid from the ball AABB, triangular

@@ -27,7 +27,7 @@ static long g_alpha1 = 0;         // Newton iterations whose first evaluation (a
 // Diagnostic build only (-DBB_PHASE_CLOCKS): per-phase s_memtime cycles,
 // summed over teams into bb_phase_cycles[] (read back by tools/phase_clocks).
 #if defined(BB_PHASE_CLOCKS) && defined(__HIP_DEVICE_COMPILE__)
-extern __device__ unsigned long long bb_phase_cycles[40];
+extern __device__ unsigned long long bb_phase_cycles[80];
 #define PH_DECL unsigned long long ph_t = clock64(), ph_acc[10] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
 #define PH(k) { unsigned long long n_ = clock64(); ph_acc[k] += n_ - ph_t; ph_t = n_; }
 // phases 0-7 -> slots 0-7; 8 (line-search setup) -> 32, 9 (line-search loop) -> 33
@@ -37,11 +37,15 @@ extern __device__ unsigned long long bb_phase_cycles[40];
 // ISA analysis build: phase boundaries as assembler comments
 #define PH_DECL
 #define PH(k) asm volatile("; PHASE_MARK " #k);
+#define PH_TOP asm volatile("; PHASE_MARK 10");
 #define PH_FLUSH(tm)
 #else
 #define PH_DECL
 #define PH(k)
 #define PH_FLUSH(tm)
+#endif
+#ifndef PH_TOP
+#define PH_TOP
 #endif
 
 struct Team {
@@ -109,6 +113,9 @@ struct EnvWork {
   T g[MAXG * NGF];                           // ball-terrain contacts (compact, GF_*)
   T bc[MAXB_LDS * NBF];                      // base-tree geom contacts 0..MAXB_LDS-1 (compact, BF_*)
   T* bspill;                                 // contacts MAXB_LDS..MAXB-1: this env's HBM block (full kernel)
+#ifdef BB_PHASE_CLOCKS
+  int dbg_nb;                                // diagnostic build: base-tree contacts summed over the step's forwards
+#endif
   Poses<T> P;                                // body poses for the Jacobian rebuilds
   T H[NH];                                   // Hessian / Cholesky factor (packed lower); dense M on the GPU
   union U {
@@ -216,6 +223,17 @@ BB_HD void chol_team(T* H, const T* hd, const Team& tm) {
 template <typename T>
 struct LsTerm {
   T u0[3], du[3], mu, Dm, b0, b1, vv, kink;
+#ifdef BB_IMPROVE
+  T c0;
+  BB_HD T cost(T alpha) const {
+    const T N = u0[0] + alpha * du[0], U1 = u0[1] + alpha * du[1], U2 = u0[2] + alpha * du[2];
+    const T Tn = sqrt(U1 * U1 + U2 * U2);
+    const bool top = N >= mu * Tn;
+    const bool bot = !top && mu * N + Tn <= 0;
+    const T g = N - mu * Tn;
+    return top ? T(0) : (bot ? c0 + alpha * (b0 + T(0.5) * alpha * b1) : T(0.5) * Dm * g * g);
+  }
+#endif
   BB_HD void prep(const T* j0, const T* x, T mu_, T f1, T f2, const T* D, T Dm_) {
     mu = mu_;
     Dm = Dm_;
@@ -223,6 +241,9 @@ struct LsTerm {
     du[0] = mu * x[0]; du[1] = f1 * x[1]; du[2] = f2 * x[2];
     b0 = D[0] * j0[0] * x[0] + D[1] * j0[1] * x[1] + D[2] * j0[2] * x[2];
     b1 = D[0] * x[0] * x[0] + D[1] * x[1] * x[1] + D[2] * x[2] * x[2];
+#ifdef BB_IMPROVE
+    c0 = T(0.5) * (D[0] * j0[0] * j0[0] + D[1] * j0[1] * j0[1] + D[2] * j0[2] * j0[2]);
+#endif
     vv = du[1] * du[1] + du[2] * du[2];
     kink = T(-1);
     if (vv > 0) {
@@ -533,11 +554,18 @@ BB_HD int solve_team(const ModelT<T>& m, EnvWork<T>& W, const T* qfs, int ng, T*
            double(lsr.lo), double(lsr.hi), double(lsr.dlo), double(lsr.dhi));
 #endif
     if (!(alpha > 0)) break;
+#ifdef BB_IMPROVE
+    T dcost = alpha * (gs + T(0.5) * alpha * sMs);
+    for (int c = 0; c < nc; c++) dcost += lst[c].cost(alpha) - lst[c].cost(T(0));
+#endif
     T sn = 0, an2 = 0;
 #pragma unroll
     for (int i = 0; i < NV; i++) { a[i] += alpha * s[i]; sn += s[i] * s[i]; an2 += a[i] * a[i]; }
     PH(6)
     if (alpha * alpha * sn <= T(1e-30) + m.step_rel2 * (1 + an2)) { it++; break; }
+#ifdef BB_IMPROVE
+    if (-m.scale * dcost < m.tol) { it++; break; }
+#endif
   }
   PH(7)
   PH_FLUSH(tm)

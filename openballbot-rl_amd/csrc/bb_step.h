@@ -119,6 +119,7 @@ BB_HD int forward(const ModelT<T>& m, const T* q, const T* v, const T* ctrl, T* 
       atomicAdd(&bb_phase_cycles[12], 1ull);
       atomicAdd(&bb_phase_cycles[13], (unsigned long long)nb);
       atomicAdd(&bb_phase_cycles[14], clock64() - b_t0);
+      W.dbg_nb += nb;
     }
 #endif
   } else {

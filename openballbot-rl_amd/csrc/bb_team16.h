@@ -189,6 +189,22 @@ __device__ __forceinline__ void chol_solve_rows(const T (&h)[NV], const T (&diag
   sown = own;
 }
 
+// stored base-tree contact b into registers: LDS slot or the env's HBM spill
+// block, each through its own address space (a pointer select between the two
+// compiles to generic flat loads)
+template <typename T>
+__device__ __forceinline__ void body_load(const EnvWork<T>& W, int b, T (&o)[NBF]) {
+  if (b < MAXB_LDS) {
+    const T* p = W.bc + b * NBF;
+#pragma unroll
+    for (int i = 0; i < NBF; i++) o[i] = p[i];
+  } else {
+    const T* p = W.bspill + (b - MAXB_LDS) * NBF;
+#pragma unroll
+    for (int i = 0; i < NBF; i++) o[i] = p[i];
+  }
+}
+
 // line-search terms of contact c: jar(0) = J a - aref, J s and the contact's
 // D (isotropic contacts) -- zeros when c >= nc
 template <bool BODY, typename T>
@@ -208,7 +224,9 @@ __device__ __forceinline__ void ls_terms(const ModelT<T>& m, const EnvWork<T>& W
 #pragma unroll
     for (int r = 0; r < 3; r++) { c6[r] = ground_dot(J, r, a) - ar[r]; c6[3 + r] = ground_dot(J, r, s); }
   } else if constexpr (BODY) {
-    body_ls_terms(m, body_slot(const_cast<T*>(W.bc), W.bspill, c - 3 - ng), W.P, W.vi, a, s, c6, D);
+    T bcv[NBF];
+    body_load(W, c - 3 - ng, bcv);
+    body_ls_terms(m, bcv, W.P, W.vi, a, s, c6, D);
   }
 }
 
@@ -325,6 +343,7 @@ __device__ int solve16(const ModelT<T>& m, EnvWork<T>& W, int ng, int nb, T* a, 
   int it = 0;
   for (; it < m.maxiter; it++) {
     team_sync();
+    PH_TOP
     // ---- (1) contact pass, contact-parallel (c = tl, tl + 16, ...): the
     // wheels' cone force f and Hessian C (3x3, packed) into LDS for the row
     // owners; ball-terrain contacts add ball-block gradient and C-weighted J'J
@@ -377,68 +396,120 @@ __device__ int solve16(const ModelT<T>& m, EnvWork<T>& W, int ng, int nb, T* a, 
           for (int j = 0; j <= i; j++) Hg[i * (i + 1) / 2 + j] += Jg[0][i] * w[0][j] + Jg[1][i] * w[1][j] + Jg[2][i] * w[2][j];
       }
     }
-    // base-tree contacts (full kernel), contact-parallel: lane tl rebuilds
-    // contact b0 + tl (Jacobian, cone force and Hessian); the 16 contacts of
-    // the round are then broadcast over the row (DPP) so that every lane adds
-    // its own Hessian row sum_b J_b[:, row]' C_b J_b and gradient entry
-    // -J_b[:, row]' f_b
+    // base-tree contacts (full kernel), contact-parallel in world form
+    // (BodyFrame): lane tl rebuilds contact b0 + tl's frame and cone force and
+    // forms A = F' C F and phi = F' f; each contact's A, phi and its column
+    // vectors' parameters (db, dB, hw, ball, hinge: 18 values, not the 39 of
+    // J) are then broadcast over the row (DPP), and every lane adds its own
+    // Hessian row sum_b w_b,row' A_b w_b,q and gradient entry -w_b,row' phi_b.
+    // The row is accumulated in world vectors (base lin, Rb-frame lever sum,
+    // hinge slots, ball lin, RB-frame lever sum) and turned into dof entries
+    // once per iteration.
     T hb[NV], gb = 0;
 #pragma unroll
     for (int i = 0; i < NV; i++) hb[i] = 0;
     if constexpr (BODY) {
+#ifdef BB_EXP_DUP_FBODY  // timing experiment: the base-tree contact pass twice
+     for (int rep = 0; rep < 2; rep++) {
+      if (rep == 1) { T z = 0; for (int i = 0; i < NV; i++) z += hb[i]; asm volatile("" :: "v"(z), "v"(gb) : "memory");
+                      for (int i = 0; i < NV; i++) hb[i] = 0; gb = 0; }
+#endif
+      // this row's column vector w_row = ev + [ang] rc x (db | dB) + [hinge slot] hw, times -ball on ball rows
+      const bool r_ang = (row >= 3 && row < 6) || row >= 12, r_ball = row >= 9;
+      const int r_h = (row >= 6 && row < 9) ? row - 6 : -2;
+      const int r_e = row < 3 ? row : ((row >= 9 && row < 12) ? row - 9 : -1);
+      T rc[3] = {0, 0, 0};
+      if (r_ang) {
+        const T* R = row < 6 ? W.P.Rb : W.P.RB;
+        const int k = row < 6 ? row - 3 : row - 12;
+        rc[0] = R[k]; rc[1] = R[3 + k]; rc[2] = R[6 + k];
+      }
+      T Ul[3] = {0, 0, 0}, Yb[3] = {0, 0, 0}, Ub[3] = {0, 0, 0}, YB[3] = {0, 0, 0}, hs[3] = {0, 0, 0};
       for (int b0 = 0; b0 < nb; b0 += L) {  // team-uniform
-        T J[3][13], f[3] = {0, 0, 0}, Cc[6] = {0, 0, 0, 0, 0, 0};
-#pragma unroll
-        for (int r = 0; r < 3; r++)
-#pragma unroll
-          for (int q = 0; q < 13; q++) J[r][q] = 0;
+        T A[6] = {0, 0, 0, 0, 0, 0}, ph[3] = {0, 0, 0}, db[3] = {0, 0, 0}, dB[3] = {0, 0, 0}, hw[3] = {0, 0, 0};
+        T mb = 0;  // -ball
         int hinge = -1;
         if (b0 + tl < nb) {
-          T ar[3], Dc;
-          body_contact(m, body_slot(W.bc, W.bspill, b0 + tl), W.P, W.vi, J, hinge, ar, Dc);
-          T jar[3];
+          T bcv[NBF];
+          body_load(W, b0 + tl, bcv);
+          BodyFrame<T> bf;
+          body_frame(m, bcv, W.P, W.vi, bf);
+          T V[3], jar[3];
+          body_V(bf, W.P, a, V);
 #pragma unroll
-          for (int r = 0; r < 3; r++) jar[r] = body_dot(J, hinge, r, a) - ar[r];
-          const T D[3] = {Dc, Dc, Dc};
-          cone_sel(jar, T(1), T(1), T(1), D, Dc * T(0.5), f, Cc);
+          for (int r = 0; r < 3; r++) jar[r] = dot3(bf.F[r], V) - bf.aref[r];
+          const T D[3] = {bf.D, bf.D, bf.D};
+          T f[3], Cc[6];
+          cone_sel(jar, T(1), T(1), T(1), D, bf.D * T(0.5), f, Cc);
+          // G = C F (rows r), A = F' G, phi = F' f
+          T G[3][3];
+#pragma unroll
+          for (int i = 0; i < 3; i++) {
+            G[0][i] = Cc[0] * bf.F[0][i] + Cc[3] * bf.F[1][i] + Cc[4] * bf.F[2][i];
+            G[1][i] = Cc[3] * bf.F[0][i] + Cc[1] * bf.F[1][i] + Cc[5] * bf.F[2][i];
+            G[2][i] = Cc[4] * bf.F[0][i] + Cc[5] * bf.F[1][i] + Cc[2] * bf.F[2][i];
+            ph[i] = bf.F[0][i] * f[0] + bf.F[1][i] * f[1] + bf.F[2][i] * f[2];
+          }
+          auto Aij = [&](int i, int j) { return bf.F[0][i] * G[0][j] + bf.F[1][i] * G[1][j] + bf.F[2][i] * G[2][j]; };
+          A[0] = Aij(0, 0); A[1] = Aij(1, 1); A[2] = Aij(2, 2); A[3] = Aij(0, 1); A[4] = Aij(0, 2); A[5] = Aij(1, 2);
+#pragma unroll
+          for (int i = 0; i < 3; i++) { db[i] = bf.db[i]; dB[i] = bf.dB[i]; hw[i] = bf.hw[i]; }
+          mb = -bf.ball;
+          hinge = bf.hinge;
         }
         const int cnt = nb - b0;
         static_for<L>([&](auto jc_) {
           constexpr int j = decltype(jc_)::value;
           if (j < cnt) {  // team-uniform
             const int hj = __builtin_amdgcn_update_dpp(0, hinge, 0x150 + j, 0xF, 0xF, false);
-            T Cb[6], fb[3];
+            T Ab[6], pb[3], dbb[3], dBb[3], hwb[3];
 #pragma unroll
-            for (int r = 0; r < 6; r++) Cb[r] = bcast<j>(Cc[r]);
+            for (int r = 0; r < 6; r++) Ab[r] = bcast<j>(A[r]);
 #pragma unroll
-            for (int r = 0; r < 3; r++) fb[r] = bcast<j>(f[r]);
-            // this row's column of J_b (dof row -> column position, or none),
-            // picked from the broadcast Jacobian; the Jacobian is broadcast a
-            // second time for the row accumulation instead of being held (a
-            // held 3x13 copy spilled the full kernel to scratch)
-            const int prow = row < 6 ? row : (row < 9 ? (row == 6 + hj ? 6 : -1) : row - 2);
-            T jc[3] = {0, 0, 0};
-#pragma unroll
-            for (int q = 0; q < 13; q++)
-#pragma unroll
-              for (int r = 0; r < 3; r++) {
-                const T v = bcast<j>(J[r][q]);
-                jc[r] = prow == q ? v : jc[r];
-              }
-            gb -= jc[0] * fb[0] + jc[1] * fb[1] + jc[2] * fb[2];
-            const T w0 = Cb[0] * jc[0] + Cb[3] * jc[1] + Cb[4] * jc[2];
-            const T w1 = Cb[3] * jc[0] + Cb[1] * jc[1] + Cb[5] * jc[2];
-            const T w2 = Cb[4] * jc[0] + Cb[5] * jc[1] + Cb[2] * jc[2];
-#pragma unroll
-            for (int q = 0; q < 13; q++) {
-              const T add = w0 * bcast<j>(J[0][q]) + w1 * bcast<j>(J[1][q]) + w2 * bcast<j>(J[2][q]);
-              if (q < 6) hb[q] += add;
-              else if (q == 6) { hb[6] += hj == 0 ? add : T(0); hb[7] += hj == 1 ? add : T(0); hb[8] += hj == 2 ? add : T(0); }
-              else hb[q + 2] += add;
+            for (int r = 0; r < 3; r++) {
+              pb[r] = bcast<j>(ph[r]); dbb[r] = bcast<j>(db[r]); dBb[r] = bcast<j>(dB[r]); hwb[r] = bcast<j>(hw[r]);
             }
+            const T mbb = bcast<j>(mb);
+            T w[3], cx[3], wx[3];
+#pragma unroll
+            for (int r = 0; r < 3; r++) cx[r] = row < 6 ? dbb[r] : dBb[r];
+            cross3(wx, rc, cx);
+#pragma unroll
+            for (int r = 0; r < 3; r++) {
+              T x = (r_e == r ? T(1) : T(0)) + (r_ang ? wx[r] : T(0)) + (r_h == hj ? hwb[r] : T(0));
+              w[r] = r_ball ? mbb * x : x;
+            }
+            const T u[3] = {Ab[0] * w[0] + Ab[3] * w[1] + Ab[4] * w[2], Ab[3] * w[0] + Ab[1] * w[1] + Ab[5] * w[2],
+                            Ab[4] * w[0] + Ab[5] * w[1] + Ab[2] * w[2]};
+            gb -= w[0] * pb[0] + w[1] * pb[1] + w[2] * pb[2];
+            T y[3], yB[3];
+            cross3(y, dbb, u);
+            cross3(yB, dBb, u);
+#pragma unroll
+            for (int r = 0; r < 3; r++) {
+              Ul[r] += u[r];
+              Yb[r] += y[r];
+              Ub[r] += mbb * u[r];
+              YB[r] += mbb * yB[r];
+            }
+            const T hu = hwb[0] * u[0] + hwb[1] * u[1] + hwb[2] * u[2];
+#pragma unroll
+            for (int r = 0; r < 3; r++) hs[r] += hj == r ? hu : T(0);
           }
         });
       }
+      // dof entries: base ang k = Rb_k . Yb, ball ang k = RB_k . YB
+#pragma unroll
+      for (int k = 0; k < 3; k++) {
+        hb[k] = Ul[k];
+        hb[3 + k] = W.P.Rb[k] * Yb[0] + W.P.Rb[3 + k] * Yb[1] + W.P.Rb[6 + k] * Yb[2];
+        hb[6 + k] = hs[k];
+        hb[9 + k] = Ub[k];
+        hb[12 + k] = W.P.RB[k] * YB[0] + W.P.RB[3 + k] * YB[1] + W.P.RB[6 + k] * YB[2];
+      }
+#ifdef BB_EXP_DUP_FBODY
+     }
+#endif
     }
     PH(0)
     // ---- (2) ball-block sums of the team-summed ground contacts (DPP)

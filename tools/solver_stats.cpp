@@ -46,7 +46,7 @@ int main(int argc, char** argv) {
       const long lsb = g_ls_evals;
       int fl = env_step<double, false>(m, cfg, &q[e * NQ], &v[e * NV], &w[e * NV], st[e], a, tr, W, obs, r, p2, &it,
                                        Team{1, 0});
-      if (dump && t >= skip) fprintf(dump, "%d %d %d\n", t, e, it);
+      if (dump && t >= skip) fprintf(dump, "%d %d %d %d\n", t, e, it, st[e]);
       if (t >= skip) {
         nghist[W.so.ng < 31 ? W.so.ng : 31]++;
         fwd += 4; newton += it; ls0 += g_ls_evals - lsb;
