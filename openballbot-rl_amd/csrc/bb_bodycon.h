@@ -60,9 +60,21 @@ BB_HD T prism_support(const PrismG<T>& P, const T* n) {
   return m;
 }
 
-// closest points of segments p0p1 and q0q1 (Ericson 5.1.9)
+// max and min of n . V over the prism's vertices (support along n and -n)
 template <typename T>
-BB_HD T seg_seg(const T* p0, const T* p1, const T* q0, const T* q1, T* cp, T* cq) {
+BB_HD void prism_extent(const PrismG<T>& P, const T* n, T& mx, T& mn) {
+  mx = mn = dot3(n, P.V[0]);
+#pragma unroll
+  for (int i = 1; i < 6; i++) {
+    const T d = dot3(n, P.V[i]);
+    mx = maxT(mx, d);
+    mn = minT(mn, d);
+  }
+}
+
+// closest points of segments p0p1 and q0q1 (Ericson 5.1.9); squared distance
+template <typename T>
+BB_HD T seg_seg2(const T* p0, const T* p1, const T* q0, const T* q1, T* cp, T* cq) {
   T d1[3] = {p1[0] - p0[0], p1[1] - p0[1], p1[2] - p0[2]};
   T d2[3] = {q1[0] - q0[0], q1[1] - q0[1], q1[2] - q0[2]};
   T r[3] = {p0[0] - q0[0], p0[1] - q0[1], p0[2] - q0[2]};
@@ -84,7 +96,12 @@ BB_HD T seg_seg(const T* p0, const T* p1, const T* q0, const T* q1, T* cp, T* cq
 #pragma unroll
   for (int i = 0; i < 3; i++) { cp[i] = p0[i] + s * d1[i]; cq[i] = q0[i] + t * d2[i]; }
   T d[3] = {cp[0] - cq[0], cp[1] - cq[1], cp[2] - cq[2]};
-  return sqrt(dot3(d, d));
+  return dot3(d, d);
+}
+
+template <typename T>
+BB_HD T seg_seg(const T* p0, const T* p1, const T* q0, const T* q1, T* cp, T* cq) {
+  return sqrt(seg_seg2(p0, p1, q0, q1, cp, cq));
 }
 
 // distance of segment p0p1 to triangle abc (0 if they intersect)
@@ -201,14 +218,16 @@ BB_HD bool capsule_prism(const Seg<T>& g, const PrismG<T>& P, T& dist, T* n, T* 
   }
   // intersecting: minimum over the separating-axis candidates
   T bestd = T(1e30), bn[3] = {0, 0, 1};
+  // both signs of an axis from one set of dot products: support(-a) =
+  // -min(a.V), min(-a.p) = -max(a.p) (negation is exact: same values as
+  // evaluating -a directly)
   auto test = [&](const T* ax) {
-#pragma unroll
-    for (int sg = 0; sg < 2; sg++) {
-      const T s = sg ? T(-1) : T(1);
-      const T a[3] = {s * ax[0], s * ax[1], s * ax[2]};
-      const T d = prism_support(P, a) - minT(dot3(a, p0), dot3(a, p1));
-      if (d < bestd) { bestd = d; bn[0] = a[0]; bn[1] = a[1]; bn[2] = a[2]; }
-    }
+    T mx, mn;
+    prism_extent(P, ax, mx, mn);
+    const T e0 = dot3(ax, p0), e1 = dot3(ax, p1);
+    const T dp = mx - minT(e0, e1), dm = -mn + maxT(e0, e1);
+    if (dp < bestd) { bestd = dp; bn[0] = ax[0]; bn[1] = ax[1]; bn[2] = ax[2]; }
+    if (dm < bestd) { bestd = dm; bn[0] = -ax[0]; bn[1] = -ax[1]; bn[2] = -ax[2]; }
   };
 #pragma unroll
   for (int f = 0; f < 5; f++) test(P.pn[f]);
@@ -257,15 +276,21 @@ template <typename T>
 BB_HD bool cylinder_prism(const Seg<T>& g, const PrismG<T>& P, T& dist, T* n, T* pos) {
   T bestd = T(1e30), bn[3] = {0, 0, 1};
   bool sep = false;
+  // both signs of an axis from one set of dot products (see capsule_prism):
+  // cyl_support(-a) = -a.c + hh |a.u| + r sqrt(1 - (a.u)^2)
   auto test = [&](const T* ax) {
-#pragma unroll
-    for (int sg = 0; sg < 2; sg++) {
-      const T s = sg ? T(-1) : T(1);
-      const T a[3] = {s * ax[0], s * ax[1], s * ax[2]}, ma[3] = {-a[0], -a[1], -a[2]};
-      const T d = prism_support(P, a) + cyl_support(g, ma);
-      if (d <= 0) sep = true;
-      if (d < bestd) { bestd = d; bn[0] = a[0]; bn[1] = a[1]; bn[2] = a[2]; }
-    }
+    T mx, mn;
+    prism_extent(P, ax, mx, mn);
+    const T na = dot3(ax, g.a);
+    const T rad = T(1) - na * na;
+    const T sr = sqrt(rad > 0 ? rad : T(0));
+    const T ac = dot3(ax, g.c);
+    const T csm = -ac + g.hh * fabs(na) + g.r * sr, csp = ac + g.hh * fabs(na) + g.r * sr;  // cyl_support(-a), (a)
+    const T dp = mx + csm, dm = -mn + csp;
+    if (dp <= 0) sep = true;
+    if (dp < bestd) { bestd = dp; bn[0] = ax[0]; bn[1] = ax[1]; bn[2] = ax[2]; }
+    if (dm <= 0) sep = true;
+    if (dm < bestd) { bestd = dm; bn[0] = -ax[0]; bn[1] = -ax[1]; bn[2] = -ax[2]; }
   };
 #pragma unroll
   for (int f = 0; f < 5; f++) test(P.pn[f]);

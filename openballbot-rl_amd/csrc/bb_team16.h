@@ -968,6 +968,13 @@ __device__ int collide_body_team(const ModelT<T>& m, const Kin<T>& k, const floa
           vertices(rr, p, V);
           PrismG<T> Pr;
           prism_build(Pr, V, -zb);
+#ifdef BB_EXP_DUP_SAT  // timing experiment: the exact prism tests twice
+          {
+            T d2 = 0, n2[3], p2[3];
+            const bool h2 = gi == 0 ? cylinder_prism(g, Pr, d2, n2, p2) : capsule_prism(g, Pr, d2, n2, p2);
+            asm volatile("" :: "v"(d2), "v"(n2[0]), "v"(p2[0]), "v"(int(h2)) : "memory");
+          }
+#endif
           hit = gi == 0 ? cylinder_prism(g, Pr, dist, n, pos) : capsule_prism(g, Pr, dist, n, pos);
           b2 = gi + 1;  // body ids: tower 1, sticks 2-3, wheels 4-6
         }
@@ -1009,6 +1016,20 @@ __device__ int collide_body_team(const ModelT<T>& m, const Kin<T>& k, const floa
       rmin = rmin < 0 ? 0 : rmin; rmax = rmax > N1 ? N1 : rmax;
       const int np = 2 * (cmax - cmin + 1) - 2;
       const int total = (rmax - rmin) * (np > 0 ? np : 0);
+#ifdef BB_EXP_DUP_PRUNE  // timing experiment: the prune walk twice (first pass discarded)
+      for (int base = 0; base < total; base += L) {
+        const int P = base + tl;
+        bool ch = false;
+        if (P < total) {
+          const int rr = rmin + P / np, p = 2 * cmin + P % np;
+          T V[3][3];
+          vertices(rr, p, V);
+          ch = !(V[0][2] < lo[2] && V[1][2] < lo[2] && V[2][2] < lo[2]) && prism_may_hit(gr, V);
+        }
+        const unsigned long long bal = __ballot(ch);
+        asm volatile("" :: "s"(bal) : "memory");
+      }
+#endif
       for (int base = 0; base < total; base += L) {
         const int P = base + tl;
         bool cand_hit = false;
