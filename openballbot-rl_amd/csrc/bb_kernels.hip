@@ -303,16 +303,21 @@ __global__ __launch_bounds__(64) void forward_kernel(ModelT<T> mg, Dev d, const 
 
 // Which envs should take the full kernel this step: a base-tree geom within a
 // margin of the ball or of a heightfield vertex under it (the fast kernel's
-// exact per-stage test stays the arbiter; this only routes work).  One lane
-// per env.
+// exact per-stage test stays the arbiter; this only routes work).  One
+// 16-lane team per env (4 per wave): the per-geom setup is replicated, the
+// cells under each geom's grown AABB are dealt over the lanes and the hits
+// reduced with a ballot.  (One lane per env was 64 waves walking ~230 cells
+// each: 93 us per step on perlin, on the critical path of the full kernel.)
 template <typename T>
 __global__ __launch_bounds__(64) void predict_kernel(ModelT<T> mg, Dev d) {
   __shared__ ModelT<T> ms;
   if (threadIdx.x == 0) ms = mg;
   __syncthreads();
   const ModelT<T>& m = ms;
-  const int e = blockIdx.x * 64 + threadIdx.x;
-  if (e >= d.n) return;
+  constexpr int PL = 16;
+  const int tl = int(threadIdx.x) & (PL - 1), team_shift = int(threadIdx.x) & ~(PL - 1);
+  const int e = blockIdx.x * (WAVE / PL) + int(threadIdx.x) / PL;
+  if (e >= d.n) return;  // team-uniform
   const T* Q = (const T*)d.qpos;
   const T* V = (const T*)d.qvel;
   T pb[3], qb[4], pB[3], qB[4];
@@ -402,22 +407,29 @@ __global__ __launch_bounds__(64) void predict_kernel(ModelT<T> mg, Dev d) {
     t16::Reach<T> sr;
     t16::make_reach(sg, sr);
 #endif
-    for (int r = rmin; r < rmax && !slow; r++)
-      for (int c = cmin; c < cmax; c++) {
-        const T x0 = dx * c - sx, x1 = dx * (c + 1) - sx, y0 = dy * r - sy, y1 = dy * (r + 1) - sy;
-        const T z00 = T(hf[r * HF_N + c]) * size_z, z10 = T(hf[(r + 1) * HF_N + c]) * size_z;
-        const T z01 = T(hf[r * HF_N + c + 1]) * size_z, z11 = T(hf[(r + 1) * HF_N + c + 1]) * size_z;
-        if (maxT(maxT(z00, z10), maxT(z01, z11)) < lo) continue;
-        const T A[3][3] = {{x0, y0, z00}, {x0, y1, z10}, {x1, y0, z01}};
-        const T B[3][3] = {{x0, y1, z10}, {x1, y0, z01}, {x1, y1, z11}};
+    const int nc = cmax - cmin, total = (rmax - rmin) * nc;
+    bool hit = false;
+    for (int i = tl; i < total && !hit; i += PL) {  // cell i of the sub-grid, row-major
+      const int r = rmin + i / nc, c = cmin + i % nc;
+      const T x0 = dx * c - sx, x1 = dx * (c + 1) - sx, y0 = dy * r - sy, y1 = dy * (r + 1) - sy;
+      const T z00 = T(hf[r * HF_N + c]) * size_z, z10 = T(hf[(r + 1) * HF_N + c]) * size_z;
+      const T z01 = T(hf[r * HF_N + c + 1]) * size_z, z11 = T(hf[(r + 1) * HF_N + c + 1]) * size_z;
+      if (maxT(maxT(z00, z10), maxT(z01, z11)) < lo) continue;
+      const T A[3][3] = {{x0, y0, z00}, {x0, y1, z10}, {x1, y0, z01}};
+      const T B[3][3] = {{x0, y1, z10}, {x1, y0, z01}, {x1, y1, z11}};
 #ifdef __HIP_DEVICE_COMPILE__
-        if (t16::prism_may_hit(sr, A) || t16::prism_may_hit(sr, B)) { slow = true; break; }
+      hit = t16::prism_may_hit(sr, A) || t16::prism_may_hit(sr, B);
 #else
-        (void)A; (void)B; slow = true;  // host pass of the kernel: never run
+      (void)A; (void)B; hit = true;  // host pass of the kernel: never run
 #endif
-      }
+    }
+#ifdef __HIP_DEVICE_COMPILE__
+    slow = ((__ballot(hit) >> team_shift) & 0xFFFFull) != 0;  // team-uniform
+#else
+    (void)team_shift; slow = hit;
+#endif
   }
-  d.pred_mark[e] = slow ? 1 : 0;
+  if (tl == 0) d.pred_mark[e] = slow ? 1 : 0;
 }
 
 // Stable split of 0..n-1 by pred_mark into fast_envs / pred_envs (one block).
@@ -525,7 +537,7 @@ int launch_step(bb_handle* h, const float* a, float* o, float* r, uint8_t* dn, f
   }
   // route: envs near a base-tree contact -> full kernel (side stream,
   // concurrent); the rest -> fast kernel; its hand-overs -> full kernel after
-  hipLaunchKernelGGL(predict_kernel<T>, dim3((h->n + 63) / 64), dim3(64), 0, s, m, h->d);
+  hipLaunchKernelGGL(predict_kernel<T>, dim3((h->n + WAVE / 16 - 1) / (WAVE / 16)), dim3(WAVE), 0, s, m, h->d);
   hipLaunchKernelGGL(split_kernel, dim3(1), dim3(1024), 0, s, h->d);
   HIPCHK(hipEventRecord(h->fork, s));
   HIPCHK(hipStreamWaitEvent(h->side, h->fork, 0));

@@ -22,6 +22,7 @@ namespace bb {
 static long g_ls_evals = 0;
 static long g_ls_hist[16] = {0};  // line-search evaluations per Newton iteration
 static long g_alpha1 = 0;         // Newton iterations whose first evaluation (alpha = 1) was accepted
+static int g_stage_iters[4] = {0, 0, 0, 0};  // Newton iterations of each RK stage of the last step
 #endif
 
 // Diagnostic build only (-DBB_PHASE_CLOCKS): per-phase s_memtime cycles,

@@ -265,6 +265,9 @@ BB_HD int rk4_step(const ModelT<T>& m, T* q, T* v, T* warm, const T* ctrl, const
 #pragma unroll
     for (int i = 0; i < NV; i++) warm[i] = acc[i];
     iters += fit;
+#if defined(BB_SOLVE_STATS) && !defined(__HIP_DEVICE_COMPILE__)
+    g_stage_iters[stage] = fit;
+#endif
     const T b = (stage == 0 || stage == 3) ? T(1.0 / 6) : T(1.0 / 3);  // RK4 weights B
     team_sync();
     if (stage == 0) {

@@ -46,7 +46,9 @@ int main(int argc, char** argv) {
       const long lsb = g_ls_evals;
       int fl = env_step<double, false>(m, cfg, &q[e * NQ], &v[e * NV], &w[e * NV], st[e], a, tr, W, obs, r, p2, &it,
                                        Team{1, 0});
-      if (dump && t >= skip) fprintf(dump, "%d %d %d %d\n", t, e, it, st[e]);
+      if (dump && t >= skip)
+        fprintf(dump, "%d %d %d %d %d %d %d %d\n", t, e, it, st[e], g_stage_iters[0], g_stage_iters[1], g_stage_iters[2],
+                g_stage_iters[3]);
       if (t >= skip) {
         nghist[W.so.ng < 31 ? W.so.ng : 31]++;
         fwd += 4; newton += it; ls0 += g_ls_evals - lsb;
