@@ -166,6 +166,65 @@ BB_HD void prism_centroid(const PrismG<T>& P, T* cen) {
     for (int i = 0; i < 3; i++) cen[i] += P.V[v][i] * T(1.0 / 6);
 }
 
+// capsule_prism when the axis segment misses the prism: the separation
+// distance and closest pair.  The closest pair is an endpoint and a face
+// interior point (the endpoint in front of the face, its projection inside
+// every other face plane), or a point of the segment and one of the 9 prism
+// edges: the minimum over the 8 boundary triangles (the oracle's seg_tri
+// loop) from 9 segment pairs and 10 projections instead of 16 point-triangle
+// and 24 segment pairs.
+template <typename T>
+#ifdef __HIP_DEVICE_COMPILE__
+__attribute__((noinline))
+#endif
+BB_HD bool capsule_prism_apart(const Seg<T>& g, const PrismG<T>& P, const T* p0, const T* p1, T& dist, T* n, T* pos) {
+  T best2 = T(1e30), bp[3] = {0, 0, 0}, bq[3] = {0, 0, 0};
+  T h0[5], h1[5];
+#pragma unroll
+  for (int f = 0; f < 5; f++) { h0[f] = dot3(P.pn[f], p0) - P.pd[f]; h1[f] = dot3(P.pn[f], p1) - P.pd[f]; }
+#pragma unroll
+  for (int f = 0; f < 5; f++) {
+#pragma unroll
+    for (int k = 0; k < 2; k++) {
+      const T* x = k ? p1 : p0;
+      const T hf = k ? h1[f] : h0[f];
+      bool inside = hf > 0;
+#pragma unroll
+      for (int g2 = 0; g2 < 5; g2++)
+        if (g2 != f) inside = inside && (k ? h1[g2] : h0[g2]) - hf * dot3(P.pn[g2], P.pn[f]) <= T(1e-12);
+      if (inside && hf * hf < best2) {
+        best2 = hf * hf;
+#pragma unroll
+        for (int i = 0; i < 3; i++) { bp[i] = x[i]; bq[i] = x[i] - hf * P.pn[f][i]; }
+      }
+    }
+  }
+  const int E[9][2] = {{0, 1}, {1, 2}, {2, 0}, {3, 4}, {4, 5}, {5, 3}, {0, 3}, {1, 4}, {2, 5}};
+#pragma unroll
+  for (int e = 0; e < 9; e++) {
+    T cp[3], cq[3];
+    const T d2 = seg_seg2(p0, p1, P.V[E[e][0]], P.V[E[e][1]], cp, cq);
+    if (d2 < best2) {
+      best2 = d2;
+#pragma unroll
+      for (int i = 0; i < 3; i++) { bp[i] = cp[i]; bq[i] = cq[i]; }
+    }
+  }
+  const T best = sqrt(best2);
+  if (best >= g.r) return false;
+  if (best > T(1e-12)) {
+    const T ib = T(1) / best;
+#pragma unroll
+    for (int i = 0; i < 3; i++) n[i] = (bp[i] - bq[i]) * ib;
+  } else {
+    n[0] = P.pn[0][0]; n[1] = P.pn[0][1]; n[2] = P.pn[0][2];
+  }
+  dist = best - g.r;
+#pragma unroll
+  for (int i = 0; i < 3; i++) pos[i] = bp[i] - n[i] * (g.r + dist * T(0.5));
+  return true;
+}
+
 // capsule vs prism; normal from prism to capsule.  Returns 1 on contact.
 template <typename T>
 BB_HD bool capsule_prism(const Seg<T>& g, const PrismG<T>& P, T& dist, T* n, T* pos) {
@@ -191,31 +250,7 @@ BB_HD bool capsule_prism(const Seg<T>& g, const PrismG<T>& P, T& dist, T* n, T* 
     }
   }
   if (t0 > t1) inter = false;
-  if (!inter) {
-    const int tri[8][3] = {{0, 1, 2}, {3, 4, 5}, {0, 1, 4}, {0, 4, 3}, {1, 2, 5}, {1, 5, 4}, {2, 0, 3}, {2, 3, 5}};
-    T best = T(1e30), bp[3] = {0, 0, 0}, bq[3] = {0, 0, 0};
-#pragma unroll
-    for (int f = 0; f < 8; f++) {
-      T cp[3], cq[3];
-      const T d = seg_tri(p0, p1, P.V[tri[f][0]], P.V[tri[f][1]], P.V[tri[f][2]], cp, cq);
-      if (d < best) {
-        best = d;
-#pragma unroll
-        for (int i = 0; i < 3; i++) { bp[i] = cp[i]; bq[i] = cq[i]; }
-      }
-    }
-    if (best >= g.r) return false;
-    if (best > T(1e-12)) {
-#pragma unroll
-      for (int i = 0; i < 3; i++) n[i] = (bp[i] - bq[i]) / best;
-    } else {
-      n[0] = P.pn[0][0]; n[1] = P.pn[0][1]; n[2] = P.pn[0][2];
-    }
-    dist = best - g.r;
-#pragma unroll
-    for (int i = 0; i < 3; i++) pos[i] = bp[i] - n[i] * (g.r + dist * T(0.5));
-    return true;
-  }
+  if (!inter) return capsule_prism_apart(g, P, p0, p1, dist, n, pos);
   // intersecting: minimum over the separating-axis candidates
   T bestd = T(1e30), bn[3] = {0, 0, 1};
   // both signs of an axis from one set of dot products: support(-a) =
