@@ -52,6 +52,9 @@ def lib():
         L.hc_forward.argtypes = [dp, dp, dp, dp, fp, C.c_double, C.c_int, dp]
         L.hc_env_step.argtypes = [C.POINTER(EnvCfg), dp, dp, dp, ip, fp, fp, C.c_double, fp, fp, fp, C.c_int]
         L.hc_model.argtypes = [dp]
+        L.hc_body_jacobian_check.argtypes = [C.c_int, C.c_uint]
+        L.hc_body_jacobian_check.restype = C.c_double
+        L.hc_capsule_apart_check.argtypes = [C.c_int, C.c_uint, dp]
         _lib = L
     return _lib
 

@@ -78,3 +78,33 @@ def test_step_parity_on_perlin(oracle):
     rec = traj.record(n_envs=128, n_steps=60, hfield=hf, seed=9)
     _teacher_forced(env, rec, TOL["fp64"])
     env.close()
+
+
+NUMPY_TERRAINS = ["stepped", "ramp", "sinusoidal", "ridge_valley", "bowl", "gradient", "terraced", "wavy", "spiral",
+                  "mixed"]
+
+
+@pytest.mark.parametrize("ttype", NUMPY_TERRAINS)
+def test_step_parity_terrain_generators(oracle, ttype):
+    """Teacher-forced fp64 steps on every other terrain generator of the
+    registry (terrain/__init__.py:18-36) with its default config vs the oracle
+    on the same field and vertical scale (ramp and gradient rescale size_z,
+    ballbot_env.py:486-495).  The relief takes the predict/split route, so
+    ball-terrain and base-tree contacts on each generator's shapes (steps,
+    ramps, ridges, bowls, spirals) go through both step kernels."""
+    import traj
+    from ballbot_gym.envs import BallbotVecEnv
+    from ballbot_gym.envs.config import terrain_bank
+    from test_gpu_parity import TOL, _teacher_forced
+
+    cfg = {"type": ttype, "config": {}}
+    if ttype == "mixed":  # needs components (terrain/mixed.py)
+        cfg["config"] = {"components": [{"type": "hills", "weight": 0.6}, {"type": "stepped", "weight": 0.4}],
+                         "blend_mode": "additive"}
+    hfs, seeds, size_z = terrain_bank(cfg, 1, seed=5)
+    hf = np.asarray(hfs[0], np.float32).ravel()
+    env = BallbotVecEnv(32, device="cuda:0", terrain_config=cfg, n_terrains=1, seed=5, auto_reset=False)
+    assert np.array_equal(env.hfield(0), hf)
+    rec = traj.record(n_envs=32, n_steps=40, hfield=hf, size_z=size_z, seed=17)
+    _teacher_forced(env, rec, TOL["fp64"])
+    env.close()
