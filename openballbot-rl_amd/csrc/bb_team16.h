@@ -666,6 +666,27 @@ __device__ int solve16(const ModelT<T>& m, EnvWork<T>& W, int ng, int nb, T* a, 
     } else {
       ls_term<BODY>(m, W, tl, ng, nc, a, s, kdw, lt);  // a base-tree contact (rebuilt), or none
     }
+#ifdef BB_EXP_DUP_LS  // timing experiment: the line-search evaluations twice (first result discarded)
+    {
+      LineSearch<T> l2;
+      l2.init(d0);
+      for (int ls = 1; ls <= m.ls_maxiter; ls++) {
+        T d1p = 0, d2p = 0, dmp = 0;
+        lt.eval(l2.alpha, d1p, d2p, dmp);
+        for (int c = tl + L; c < nc; c += L) {
+          LsTerm<T> lc;
+          ls_term<BODY>(m, W, c, ng, nc, a, s, kdw, lc);
+          lc.eval(l2.alpha, d1p, d2p, dmp);
+        }
+        const T d1 = gs + l2.alpha * sMs + tsum(d1p), d2 = sMs + tsum(d2p);
+        const T dmag = fabs(gs) + fabs(l2.alpha * sMs) + tsum(dmp);
+        if (fabs(d1) <= m.ls_tol * fabs(d0) || fabs(d1) <= T(32) * eps_of<T>() * dmag) break;
+        if (!(d1 == d1)) break;
+        l2.update(d1, d2);
+      }
+      asm volatile("" :: "v"(l2.alpha) : "memory");
+    }
+#endif
     LineSearch<T> lsr;
     lsr.init(d0);
     bool ls_ok = false;
