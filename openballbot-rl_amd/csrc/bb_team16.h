@@ -354,6 +354,18 @@ __device__ int solve16(const ModelT<T>& m, EnvWork<T>& W, int ng, int nb, T* a, 
 #pragma unroll
     for (int i = 0; i < 21; i++) Hg[i] = 0;
     T jar0[3] = {0, 0, 0};  // this lane's first contact, kept for the line search
+#ifdef BB_EXP_DUP_CPASS  // timing experiment: the wheel / ball-terrain contact pass twice
+    for (int rep = 0; rep < 2; rep++) {
+      if (rep == 1) {
+        T z = 0;
+        for (int i = 0; i < 6; i++) z += gg[i];
+        for (int i = 0; i < 21; i++) z += Hg[i];
+        asm volatile("" :: "v"(z) : "memory");
+        for (int i = 0; i < 6; i++) gg[i] = 0;
+        for (int i = 0; i < 21; i++) Hg[i] = 0;
+        team_sync();
+      }
+#endif
     for (int c = tl; c < ngc; c += L) {
       const bool wheel = c < 3;
       T jar[3], Dc = 0, Jg[3][6];
@@ -396,6 +408,9 @@ __device__ int solve16(const ModelT<T>& m, EnvWork<T>& W, int ng, int nb, T* a, 
           for (int j = 0; j <= i; j++) Hg[i * (i + 1) / 2 + j] += Jg[0][i] * w[0][j] + Jg[1][i] * w[1][j] + Jg[2][i] * w[2][j];
       }
     }
+#ifdef BB_EXP_DUP_CPASS
+    }
+#endif
     // base-tree contacts (full kernel), contact-parallel in world form
     // (BodyFrame): lane tl rebuilds contact b0 + tl's frame and cone force and
     // forms A = F' C F and phi = F' f; each contact's A, phi and its column
@@ -514,6 +529,16 @@ __device__ int solve16(const ModelT<T>& m, EnvWork<T>& W, int ng, int nb, T* a, 
     PH(0)
     // ---- (2) ball-block sums of the team-summed ground contacts (DPP)
     if (gsum) {
+#ifdef BB_EXP_DUP_GSUM  // timing experiment: the 27 team sums twice
+      {
+        T z = 0;
+#pragma unroll
+        for (int i = 0; i < 6; i++) z += tsum(gg[i] * T(0.5));
+#pragma unroll
+        for (int i = 0; i < 21; i++) z += tsum(Hg[i] * T(0.5));
+        asm volatile("" :: "v"(z) : "memory");
+      }
+#endif
 #pragma unroll
       for (int i = 0; i < 6; i++) gg[i] = tsum(gg[i]);
 #pragma unroll
@@ -666,30 +691,45 @@ __device__ int solve16(const ModelT<T>& m, EnvWork<T>& W, int ng, int nb, T* a, 
     } else {
       ls_term<BODY>(m, W, tl, ng, nc, a, s, kdw, lt);  // a base-tree contact (rebuilt), or none
     }
-#ifdef BB_EXP_DUP_LS  // timing experiment: the line-search evaluations twice (first result discarded)
-    {
-      LineSearch<T> l2;
-      l2.init(d0);
+    LineSearch<T> lsr;
+    bool ls_ok = false;
+#ifdef BB_EXP_DUP_LS  // timing experiment: the line search twice (first result discarded)
+    auto line_search = [&](LineSearch<T>& lsr, bool& ls_ok) {
+      lsr.init(d0);
+      ls_ok = false;
       for (int ls = 1; ls <= m.ls_maxiter; ls++) {
+        const T alpha = lsr.alpha;
         T d1p = 0, d2p = 0, dmp = 0;
-        lt.eval(l2.alpha, d1p, d2p, dmp);
+        lt.eval(alpha, d1p, d2p, dmp);
         for (int c = tl + L; c < nc; c += L) {
           LsTerm<T> lc;
           ls_term<BODY>(m, W, c, ng, nc, a, s, kdw, lc);
-          lc.eval(l2.alpha, d1p, d2p, dmp);
+          lc.eval(alpha, d1p, d2p, dmp);
         }
-        const T d1 = gs + l2.alpha * sMs + tsum(d1p), d2 = sMs + tsum(d2p);
-        const T dmag = fabs(gs) + fabs(l2.alpha * sMs) + tsum(dmp);
-        if (fabs(d1) <= m.ls_tol * fabs(d0) || fabs(d1) <= T(32) * eps_of<T>() * dmag) break;
+        const T d1 = gs + alpha * sMs + tsum(d1p);
+        const T d2 = sMs + tsum(d2p);
+        const T dmag = fabs(gs) + fabs(alpha * sMs) + tsum(dmp);
+        if (fabs(d1) <= m.ls_tol * fabs(d0) || fabs(d1) <= T(32) * eps_of<T>() * dmag) { ls_ok = true; break; }
         if (!(d1 == d1)) break;
-        l2.update(d1, d2);
+        lsr.update(d1, d2);
+        const bool up = lsr.alpha > lsr.prev;
+        const T big = T(1e30);
+        const T kv = tmin(lsr.crosses(lt.kink) ? (up ? lt.kink : -lt.kink) : big);
+        const T ks = up ? kv : -kv;
+        lsr.dx = kv < big ? fabs(ks - lsr.prev) : lsr.dx;
+        lsr.alpha = kv < big ? ks : lsr.alpha;
       }
-      asm volatile("" :: "v"(l2.alpha) : "memory");
+    };
+    {
+      LineSearch<T> l2;
+      bool ok2;
+      line_search(l2, ok2);
+      asm volatile("" :: "v"(l2.alpha), "v"(int(ok2)) : "memory");
     }
-#endif
-    LineSearch<T> lsr;
+    PH(8)
+    line_search(lsr, ls_ok);
+#else
     lsr.init(d0);
-    bool ls_ok = false;
     PH(8)
     for (int ls = 1; ls <= m.ls_maxiter; ls++) {
       const T alpha = lsr.alpha;
@@ -700,11 +740,14 @@ __device__ int solve16(const ModelT<T>& m, EnvWork<T>& W, int ng, int nb, T* a, 
         ls_term<BODY>(m, W, c, ng, nc, a, s, kdw, lc);
         lc.eval(alpha, d1p, d2p, dmp);
       }
+      // phi' decides most evaluations: the magnitude bound (roundoff test) and
+      // phi'' (the next trial) are summed only when it does not
       const T d1 = gs + alpha * sMs + tsum(d1p);
-      const T d2 = sMs + tsum(d2p);
+      if (fabs(d1) <= m.ls_tol * fabs(d0)) { ls_ok = true; break; }
       const T dmag = fabs(gs) + fabs(alpha * sMs) + tsum(dmp);
-      if (fabs(d1) <= m.ls_tol * fabs(d0) || fabs(d1) <= T(32) * eps_of<T>() * dmag) { ls_ok = true; break; }
+      if (fabs(d1) <= T(32) * eps_of<T>() * dmag) { ls_ok = true; break; }
       if (!(d1 == d1)) break;
+      const T d2 = sMs + tsum(d2p);
       lsr.update(d1, d2);
       const bool up = lsr.alpha > lsr.prev;
       const T big = T(1e30);
@@ -713,6 +756,7 @@ __device__ int solve16(const ModelT<T>& m, EnvWork<T>& W, int ng, int nb, T* a, 
       lsr.dx = kv < big ? fabs(ks - lsr.prev) : lsr.dx;
       lsr.alpha = kv < big ? ks : lsr.alpha;
     }
+#endif
     if (!ls_ok) lsr.alpha = lsr.fallback();
     PH(9)
     const T alpha = lsr.alpha;
