@@ -526,7 +526,12 @@ BB_HD int solve_team(const ModelT<T>& m, EnvWork<T>& W, const T* qfs, int ng, T*
       const T d2 = sMs + team_sum(tm, d2p);
       const T dmag = fabs(gs) + fabs(alpha * sMs) + team_sum(tm, dmp);
 #ifdef BB_LS_TRACE
-      printf("    ls %d alpha %.17g d1 %.6e d2 %.6e d0 %.6e\n", ls, double(alpha), double(d1), double(d2), double(d0));
+      printf("    ls %d alpha %.17g d1 %.6e d2 %.6e d0 %.6e", ls, double(alpha), double(d1), double(d2), double(d0));
+      if (ls == 1) {
+        printf(" kinks");
+        for (int c = 0; c < nc; c++) if (lst[c].kink > 0) printf(" %d:%.4g", c, double(lst[c].kink));
+      }
+      printf("\n");
 #endif
       if (fabs(d1) <= m.ls_tol * fabs(d0) || fabs(d1) <= T(32) * eps_of<T>() * dmag) {
         ls_ok = true;
