@@ -15,6 +15,8 @@
  *   bb_render_depth  RGBDInputs depth cams (_get_obs)           sensors/rgbd.py:46-82
  *   bb_ppo_loss      SB3 PPO.train minibatch loss + grads
  *   bb_adamw_clip    SB3 PPO.train clip_grad_norm_ + AdamW step
+ *   bb_ppo_mlp_step  SB3 PPO.train minibatch (forward, loss, backward, clip,
+ *                    AdamW) of the reference's proprio MLP policy, fused
  *   bb_gae           SB3 RolloutBuffer.compute_returns_and_advantage (PPO)
  *   bb_forward       mujoco.mj_forward (diagnostic)             ballbot_env.py:525,620
  *   bb_get_state/    read/write qpos/qvel/qacc_warmstart        ballbot_env.py:616-617
@@ -42,7 +44,7 @@
 extern "C" {
 #endif
 
-#define BB_ABI_VERSION 8
+#define BB_ABI_VERSION 9
 #define BB_NQ 17
 #define BB_NV 15
 #define BB_OBS 15
@@ -144,6 +146,53 @@ int bb_ppo_loss(const float* mean_dev, const float* values_dev, const float* log
 int bb_adamw_clip(float* param_dev, const float* grad_dev, float* exp_avg_dev, float* exp_avg_sq_dev, int64_t n,
                   const float* lr_dev, float* step_dev, float* coef_dev, double beta1, double beta2, double eps,
                   double weight_decay, double max_norm, void* stream);
+/* One SB3 PPO.train minibatch of the reference's proprio policy, fused:
+ * SB3 MultiInputPolicy with net_arch pi = vf = [128]*4, LeakyReLU (0.01),
+ * the Extractor's 15-d sorted-key proprio features, a 3-d diagonal Gaussian
+ * action head with state-independent log_std and a value head
+ * (ballbot_rl/policies/mlp_policy.py:143-163, ballbot_rl/training/train.py:39-56);
+ * per minibatch it does what PPO.train does between `for rollout_data in
+ * get(batch_size)` and `optimizer.step()` (model.learn, train.py:284): the
+ * forward pass, the loss of bb_ppo_loss, loss.backward(), clip_grad_norm_ and
+ * AdamW.  The minibatch is perm[mb_counter][0..B) of the rollout arrays; the
+ * loss terms go to log[row_counter][6] (loss, pg, vf, entropy loss, approx_kl,
+ * clip_fraction); both counters are incremented on the device, so a captured
+ * graph replays consecutive minibatches.  offsets: float offsets of the 21
+ * parameter tensors in the flat buffer, each a multiple of 4, in the order
+ * pi W0..W3, pi b0..b3, vf W0..W3, vf b0..b3, action W, action b, value W,
+ * value b, log_std.  grad has the flat layout; entries outside the tensors are
+ * never written (keep them 0).  B: a multiple of 32 and of 256 (>= 256).
+ * workspace: >= bb_ppo_mlp_workspace_bytes(B) bytes of device memory.
+ * Five launches on stream; graph-capturable. */
+typedef struct bb_ppo_mlp_args {
+  float* params;
+  float* grad;
+  float* exp_avg;
+  float* exp_avg_sq;
+  int64_t n_params;
+  int32_t offsets[21];
+  const float* obs;          /* [n][15] */
+  const float* actions;      /* [n][3] unclipped */
+  const float* old_logp;     /* [n] */
+  const float* advantages;   /* [n] */
+  const float* returns;      /* [n] */
+  const int64_t* perm;       /* [n / B][B] */
+  int64_t* mb_counter;
+  int64_t* row_counter;
+  float* log;
+  const float* clip;         /* device scalars: clip range, learning rate */
+  const float* lr;
+  float* step;               /* AdamW step counter (float, as torch) */
+  float* coef;               /* 4 floats of scratch */
+  int32_t B;
+  int32_t normalize_advantage;
+  float ent_coef, vf_coef;
+  double beta1, beta2, eps, weight_decay, max_grad_norm;
+  float* workspace;
+  int64_t workspace_bytes;
+} bb_ppo_mlp_args;
+int bb_ppo_mlp_workspace_bytes(int B, int64_t* bytes);
+int bb_ppo_mlp_step(const bb_ppo_mlp_args* args, void* stream);
 /* copy terrain bank slot terrain_id (float32[293*293]) to host memory */
 int bb_get_hfield(bb_handle* h, int terrain_id, float* data_host);
 /* per-env terrain ids (device int32[n]) applied at the next reset */

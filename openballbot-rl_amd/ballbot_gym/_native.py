@@ -54,20 +54,37 @@ class PerlinCfg(C.Structure):
     ]
 
 
+class PPOMlpArgs(C.Structure):
+    """bb_ppo_mlp_args (include/ballbot_mi355x.h)."""
+    _fields_ = [(name, C.c_void_p) for name in ("params", "grad", "exp_avg", "exp_avg_sq")] + [
+        ("n_params", C.c_int64),
+        ("offsets", C.c_int32 * 21),
+    ] + [(name, C.c_void_p) for name in ("obs", "actions", "old_logp", "advantages", "returns", "perm",
+                                         "mb_counter", "row_counter", "log", "clip", "lr", "step", "coef")] + [
+        ("B", C.c_int32),
+        ("normalize_advantage", C.c_int32),
+        ("ent_coef", C.c_float),
+        ("vf_coef", C.c_float),
+    ] + [(name, C.c_double) for name in ("beta1", "beta2", "eps", "weight_decay", "max_grad_norm")] + [
+        ("workspace", C.c_void_p),
+        ("workspace_bytes", C.c_int64),
+    ]
+
+
 EXPORTS = [
     "bb_abi_version", "bb_last_error", "bb_default_params", "bb_create", "bb_destroy", "bb_set_hfield",
     "bb_assign_terrain", "bb_reset", "bb_step", "bb_get_state", "bb_set_state", "bb_forward", "bb_get_stats",
     "bb_get_offsets", "bb_get_config", "bb_time_kernel", "bb_kernel_ms", "bb_generate_perlin", "bb_get_hfield",
-    "bb_gae", "bb_render_depth", "bb_ppo_loss", "bb_adamw_clip",
+    "bb_gae", "bb_render_depth", "bb_ppo_loss", "bb_adamw_clip", "bb_ppo_mlp_workspace_bytes", "bb_ppo_mlp_step",
 ]
 
-ABI_VERSION = 8  # include/ballbot_mi355x.h BB_ABI_VERSION
+ABI_VERSION = 9  # include/ballbot_mi355x.h BB_ABI_VERSION
 
 _lib = None
 
 
 def build(force: bool = False, verbose: bool = False) -> Path:
-    """Compile csrc/bb_kernels.hip + bb_terrain.hip + bb_rollout.hip + bb_render.hip + bb_ppo.hip for gfx950 into _lib/libbb_mi355x.so."""
+    """Compile csrc/bb_kernels.hip + bb_terrain.hip + bb_rollout.hip + bb_render.hip + bb_ppo.hip + bb_mlp.hip for gfx950 into _lib/libbb_mi355x.so."""
     import subprocess
 
     srcs = list(CSRC.glob("*.h")) + list(CSRC.glob("*.hip")) + list(INCLUDE.glob("*.h"))
@@ -78,7 +95,7 @@ def build(force: bool = False, verbose: bool = False) -> Path:
     cmd = ["hipcc", "--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC", "-shared",
            "-o", str(tmp), str(CSRC / "bb_kernels.hip"), str(CSRC / "bb_terrain.hip"),
            str(CSRC / "bb_rollout.hip"), str(CSRC / "bb_render.hip"),
-           str(CSRC / "bb_ppo.hip")]
+           str(CSRC / "bb_ppo.hip"), str(CSRC / "bb_mlp.hip")]
     if verbose:
         print(" ".join(cmd))
     subprocess.run(cmd, check=True)
@@ -132,6 +149,8 @@ def _load(path: Path):
     L.bb_ppo_loss.argtypes = [vp] * 8 + [C.c_int, C.c_int, C.c_float, C.c_float, vp, vp, vp, vp]
     L.bb_adamw_clip.argtypes = [vp, vp, vp, vp, C.c_int64, vp, vp, vp] + [C.c_double] * 5 + [vp]
     L.bb_gae.argtypes = [vp, vp, vp, vp, vp, C.c_int, C.c_int, C.c_double, C.c_double, vp, vp, vp]
+    L.bb_ppo_mlp_workspace_bytes.argtypes = [C.c_int, C.POINTER(C.c_int64)]
+    L.bb_ppo_mlp_step.argtypes = [C.POINTER(PPOMlpArgs), vp]
     L.bb_kernel_ms.argtypes = [vp, C.POINTER(C.c_double), C.POINTER(C.c_int32)]
     for name in [n for n in EXPORTS if n not in ("bb_default_params", "bb_abi_version")]:
         getattr(L, name).restype = C.c_int

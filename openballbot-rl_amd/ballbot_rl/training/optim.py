@@ -7,7 +7,8 @@ On the GPU that is ~60 small PyTorch launches per minibatch (per-tensor norms,
 the foreach clip, capturable AdamW's per-tensor weight decay and bias
 corrections).  `FlatAdamW` keeps the trainable parameters, exp_avg and
 exp_avg_sq in three flat fp32 buffers (the parameters become views of the
-first), gathers the gradients with one concatenation and runs the clip and
+first, each starting on a 16-byte boundary), copies the gradients into a
+fourth (one foreach launch) and runs the clip and
 the AdamW update in `bb_adamw_clip`: a single-workgroup norm/scalars launch and
 one elementwise pass.  The math is torch.optim.AdamW's (amsgrad off) with
 clip_grad_norm_'s factor min(1, max_norm / (||g|| + 1e-6)).
@@ -44,9 +45,16 @@ class FlatAdamW:
         dev = self.params[0].device
         if dev.type != "cuda" or any(p.device != dev or p.dtype != torch.float32 for p in self.params):
             raise ValueError("FlatAdamW: fp32 parameters on one GPU expected")
-        n = sum(p.numel() for p in self.params)
+        # every tensor starts on a 16-byte boundary (float4 loads in bb_ppo_mlp_step);
+        # the gaps hold zeros in the parameter and gradient buffers
+        self.offsets = []
+        n = 0
+        for p in self.params:
+            self.offsets.append(n)
+            n += (p.numel() + 3) // 4 * 4
         self.n = n
-        self.flat = torch.empty(n, device=dev)
+        self.flat = torch.zeros(n, device=dev)
+        self.grad = torch.zeros(n, device=dev)
         self.exp_avg = torch.zeros(n, device=dev)
         self.exp_avg_sq = torch.zeros(n, device=dev)
         self.step_t = torch.zeros(1, device=dev)
@@ -55,15 +63,15 @@ class FlatAdamW:
         self.beta1, self.beta2 = float(betas[0]), float(betas[1])
         self.eps, self.weight_decay, self.max_grad_norm = float(eps), float(weight_decay), float(max_grad_norm)
         self.state = {}
-        off = 0
+        self._gviews = []
         with torch.no_grad():
-            for p in self.params:
+            for p, off in zip(self.params, self.offsets):
                 k = p.numel()
                 self.flat[off:off + k].copy_(p.detach().reshape(-1))
                 p.data = self.flat[off:off + k].view_as(p)
                 self.state[p] = {"exp_avg": self.exp_avg[off:off + k].view_as(p),
                                  "exp_avg_sq": self.exp_avg_sq[off:off + k].view_as(p), "step": self.step_t}
-                off += k
+                self._gviews.append(self.grad[off:off + k].view_as(p))
         self.param_groups = [{"lr": self.lr, "params": self.params, "weight_decay": self.weight_decay,
                               "betas": (self.beta1, self.beta2), "eps": self.eps}]
 
@@ -77,8 +85,13 @@ class FlatAdamW:
                 p.grad.zero_()
 
     def step(self) -> None:
-        grads = [p.grad if p.grad is not None else torch.zeros_like(p) for p in self.params]
-        g = torch.cat([t.reshape(-1) for t in grads])
+        have = [(v, p.grad) for v, p in zip(self._gviews, self.params) if p.grad is not None]
+        if have:
+            torch._foreach_copy_([v for v, _ in have], [g for _, g in have])
+        for v, p in zip(self._gviews, self.params):
+            if p.grad is None:
+                v.zero_()
+        g = self.grad
         stream = torch.cuda.current_stream(self.flat.device).cuda_stream
         self._check(self._lib.bb_adamw_clip(_ptr(self.flat), _ptr(g), _ptr(self.exp_avg), _ptr(self.exp_avg_sq),
                                             int(self.n), _ptr(self.lr), _ptr(self.step_t), _ptr(self.coef),

@@ -151,6 +151,47 @@ def policy_obs(obs15: torch.Tensor, depth: Optional[torch.Tensor] = None,
     return d
 
 
+def fused_mlp_slots(ppo: "BatchedPPO"):
+    """Flat-buffer offsets of the 21 tensors bb_ppo_mlp_step reads, or None when
+    the policy/optimiser is not the reference's proprio MLP on FlatAdamW
+    (pi = vf = [128]*4 LeakyReLU(0.01) over the 15-d obs, 3-d action head).
+    BB_PPO_FUSED=0 disables the fused update (A/B runs)."""
+    import os
+
+    from ballbot_rl.training.optim import FlatAdamW
+
+    if os.environ.get("BB_PPO_FUSED", "1") == "0" or ppo.cameras or ppo.device.type != "cuda":
+        return None
+    opt, pol = ppo.optimizer, ppo.policy
+    if not isinstance(opt, FlatAdamW) or ppo.batch_size % 256:
+        return None
+
+    def trunk(seq):
+        mods = list(seq)
+        if len(mods) != 8:
+            return None
+        lins, acts = mods[0::2], mods[1::2]
+        shapes = [(128, 15), (128, 128), (128, 128), (128, 128)]
+        if any(not isinstance(m, nn.Linear) or m.bias is None or tuple(m.weight.shape) != sh
+               for m, sh in zip(lins, shapes)):
+            return None
+        if any(not isinstance(a, nn.LeakyReLU) or a.negative_slope != 0.01 for a in acts):
+            return None
+        return [m.weight for m in lins] + [m.bias for m in lins]
+
+    pi, vf = trunk(pol.policy_net), trunk(pol.value_net_trunk)
+    if pi is None or vf is None or pol.features_extractor.features_dim != 15:
+        return None
+    if tuple(pol.action_net.weight.shape) != (3, 128) or tuple(pol.value_net.weight.shape) != (1, 128):
+        return None
+    tensors = pi + vf + [pol.action_net.weight, pol.action_net.bias, pol.value_net.weight, pol.value_net.bias,
+                         pol.log_std]
+    where = {id(q): off for q, off in zip(opt.params, opt.offsets)}
+    if len(opt.params) != len(tensors) or any(id(t) not in where for t in tensors):
+        return None
+    return [where[id(t)] for t in tensors]
+
+
 class _UpdateGraphs:
     """PPO.train as ONE captured graph per minibatch, replayed with no host sync.
 
@@ -188,6 +229,65 @@ class _UpdateGraphs:
         p_snap = [p.detach().clone() for p in params]
         st_snap = {id(p): {k: v.clone() for k, v in opt.state[p].items()} for p in params if p in opt.state}
 
+        slots = fused_mlp_slots(ppo)
+        self.fused = slots is not None
+        if self.fused:
+            mb_step = self._fused_step(ppo, slots)
+        else:
+            mb_step = self._autograd_step(ppo, params, opt)
+        self.perm.copy_(torch.arange(self.nb * B, device=dev).view(self.nb, B) % max(n, 1))
+        side = torch.cuda.Stream(device=dev)
+        side.wait_stream(torch.cuda.current_stream(dev))
+        with torch.cuda.stream(side):
+            for _ in range(2):  # warm-up (also creates the AdamW state the graph updates)
+                self.k.zero_(); self.row.zero_()
+                mb_step()
+        torch.cuda.current_stream(dev).wait_stream(side)
+        for p in params:  # backward allocates the grads inside the graph pool (static addresses)
+            p.grad = None
+        self.k.zero_(); self.row.zero_()
+        self.graph = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(self.graph):
+            mb_step()
+        torch.cuda.synchronize(dev)
+        self._restore(opt, [p_snap, {i: st_snap.get(id(p)) for i, p in enumerate(params)}])
+
+    def _fused_step(self, ppo: "BatchedPPO", slots):
+        """bb_ppo_mlp_step: the whole minibatch (forward, loss, backward, clip,
+        AdamW) in five HIP launches; it advances k and row itself."""
+        from ballbot_gym import _native as N
+
+        opt, lib = ppo.optimizer, N.lib()
+        nbytes = C.c_int64()
+        N.check(lib.bb_ppo_mlp_workspace_bytes(int(ppo.batch_size), C.byref(nbytes)), "bb_ppo_mlp_workspace_bytes")
+        self.ws = torch.empty(int(nbytes.value) // 4, device=ppo.device)
+        a = N.PPOMlpArgs()
+        a.params, a.grad, a.exp_avg, a.exp_avg_sq = (t.data_ptr() for t in (opt.flat, opt.grad, opt.exp_avg,
+                                                                            opt.exp_avg_sq))
+        a.n_params = int(opt.n)
+        for i, o in enumerate(slots):
+            a.offsets[i] = int(o)
+        d = self.data
+        a.obs, a.actions, a.old_logp = d["obs"].data_ptr(), d["actions"].data_ptr(), d["log_probs"].data_ptr()
+        a.advantages, a.returns = d["advantages"].data_ptr(), d["returns"].data_ptr()
+        a.perm, a.mb_counter, a.row_counter, a.log = (t.data_ptr() for t in (self.perm, self.k, self.row, self.log))
+        a.clip, a.lr, a.step, a.coef = (t.data_ptr() for t in (self.clip, opt.lr, opt.step_t, opt.coef))
+        a.B = int(ppo.batch_size)
+        a.normalize_advantage = int(ppo.normalize_advantage)
+        a.ent_coef, a.vf_coef = float(ppo.ent_coef), float(ppo.vf_coef)
+        a.beta1, a.beta2, a.eps = opt.beta1, opt.beta2, opt.eps
+        a.weight_decay, a.max_grad_norm = opt.weight_decay, opt.max_grad_norm
+        a.workspace, a.workspace_bytes = self.ws.data_ptr(), int(nbytes.value)
+        self._args = a
+        dev = ppo.device
+
+        def mb_step():
+            stream = C.c_void_p(torch.cuda.current_stream(dev).cuda_stream)
+            N.check(lib.bb_ppo_mlp_step(C.byref(a), stream), "bb_ppo_mlp_step")
+
+        return mb_step
+
+    def _autograd_step(self, ppo: "BatchedPPO", params, opt):
         def mb_step():
             d = self.data
             idx = self.perm.index_select(0, self.k).view(-1)
@@ -205,22 +305,7 @@ class _UpdateGraphs:
                 self.k.add_(1)
                 self.row.add_(1)
 
-        self.perm.copy_(torch.arange(self.nb * B, device=dev).view(self.nb, B) % max(n, 1))
-        side = torch.cuda.Stream(device=dev)
-        side.wait_stream(torch.cuda.current_stream(dev))
-        with torch.cuda.stream(side):
-            for _ in range(2):  # warm-up (also creates the AdamW state the graph updates)
-                self.k.zero_(); self.row.zero_()
-                mb_step()
-        torch.cuda.current_stream(dev).wait_stream(side)
-        for p in params:  # backward allocates the grads inside the graph pool (static addresses)
-            p.grad = None
-        self.k.zero_(); self.row.zero_()
-        self.graph = torch.cuda.CUDAGraph()
-        with torch.cuda.graph(self.graph):
-            mb_step()
-        torch.cuda.synchronize(dev)
-        self._restore(opt, [p_snap, {i: st_snap.get(id(p)) for i, p in enumerate(params)}])
+        return mb_step
 
     def _snapshot(self, opt):
         return [[p.detach().clone() for p in self.params],

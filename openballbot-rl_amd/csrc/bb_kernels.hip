@@ -25,6 +25,7 @@
 #include "bb_rollout.h"
 #include "bb_render.h"
 #include "bb_ppo.h"
+#include "bb_mlp.h"
 
 using namespace bb;
 
@@ -824,9 +825,57 @@ int bb_adamw_clip(float* param, const float* grad, float* exp_avg, float* exp_av
   if (!(eps >= 0.0) || !(max_norm > 0.0)) return fail("bb_adamw_clip: eps must be >= 0 and max_norm > 0");
   if ((reinterpret_cast<uintptr_t>(grad) & 15) != 0) return fail("bb_adamw_clip: grad must be 16-byte aligned");
   AdamWArgs a{param, grad, exp_avg, exp_avg_sq, (long long)n, lr, step, coef, beta1, beta2, weight_decay,
-              float(beta2), float(1.0 - beta1), float(1.0 - beta2), float(eps), float(max_norm)};
+              float(beta2), float(1.0 - beta1), float(1.0 - beta2), float(eps), float(max_norm),
+              nullptr, 0};
   if (launch_adamw_clip(a, (hipStream_t)stream))
     return fail("bb_adamw_clip: launch failed: %s", hipGetErrorString(hipGetLastError()));
+  return 0;
+}
+
+int bb_ppo_mlp_workspace_bytes(int B, int64_t* bytes) {
+  if (!bytes) return fail("bb_ppo_mlp_workspace_bytes: NULL argument");
+  if (B < 256 || B % 256) return fail("bb_ppo_mlp_workspace_bytes: B must be a positive multiple of 256 (got %d)", B);
+  *bytes = mlp_workspace_bytes(B);
+  return 0;
+}
+
+int bb_ppo_mlp_step(const bb_ppo_mlp_args* a, void* stream) {
+  if (!a) return fail("bb_ppo_mlp_step: NULL argument");
+  if (!a->params || !a->grad || !a->exp_avg || !a->exp_avg_sq || !a->obs || !a->actions || !a->old_logp ||
+      !a->advantages || !a->returns || !a->perm || !a->mb_counter || !a->row_counter || !a->log || !a->clip ||
+      !a->lr || !a->step || !a->coef || !a->workspace)
+    return fail("bb_ppo_mlp_step: NULL argument");
+  if (a->B < 256 || a->B % 256) return fail("bb_ppo_mlp_step: B must be a positive multiple of 256 (got %d)", a->B);
+  if (a->workspace_bytes < mlp_workspace_bytes(a->B))
+    return fail("bb_ppo_mlp_step: workspace of %lld bytes < %lld", (long long)a->workspace_bytes,
+                mlp_workspace_bytes(a->B));
+  if (!(a->beta1 >= 0.0 && a->beta1 < 1.0) || !(a->beta2 >= 0.0 && a->beta2 < 1.0) || !(a->eps >= 0.0) ||
+      !(a->max_grad_norm > 0.0))
+    return fail("bb_ppo_mlp_step: bad optimiser hyper-parameters");
+  // sizes of the 21 tensors: their extents must fit the flat buffer, 16-byte aligned
+  static const int sizes[MLP_NSLOTS] = {128 * 15, 128 * 128, 128 * 128, 128 * 128, 128, 128, 128, 128,
+                                        128 * 15, 128 * 128, 128 * 128, 128 * 128, 128, 128, 128, 128,
+                                        3 * 128, 3, 128, 1, 3};
+  for (int i = 0; i < MLP_NSLOTS; i++)
+    if (a->offsets[i] < 0 || a->offsets[i] % 4 || (int64_t)a->offsets[i] + sizes[i] > a->n_params)
+      return fail("bb_ppo_mlp_step: offsets[%d] = %d is not a 4-aligned slot inside the %lld-float buffer", i,
+                  a->offsets[i], (long long)a->n_params);
+  if ((reinterpret_cast<uintptr_t>(a->params) | reinterpret_cast<uintptr_t>(a->grad)) & 15)
+    return fail("bb_ppo_mlp_step: params and grad must be 16-byte aligned");
+  MlpStepArgs m;
+  m.params = a->params; m.grad = a->grad; m.exp_avg = a->exp_avg; m.exp_avg_sq = a->exp_avg_sq;
+  m.n_params = a->n_params;
+  for (int i = 0; i < MLP_NSLOTS; i++) m.off[i] = a->offsets[i];
+  m.obs = a->obs; m.actions = a->actions; m.old_logp = a->old_logp; m.adv = a->advantages; m.returns = a->returns;
+  m.perm = reinterpret_cast<const long long*>(a->perm);
+  m.mb_counter = reinterpret_cast<long long*>(a->mb_counter);
+  m.row_counter = reinterpret_cast<long long*>(a->row_counter);
+  m.log = a->log; m.clip = a->clip; m.lr = a->lr; m.step = a->step; m.coef = a->coef;
+  m.B = a->B; m.normalize = a->normalize_advantage ? 1 : 0; m.ent_coef = a->ent_coef; m.vf_coef = a->vf_coef;
+  m.beta1 = a->beta1; m.beta2 = a->beta2; m.eps = a->eps; m.weight_decay = a->weight_decay;
+  m.max_norm = a->max_grad_norm; m.ws = a->workspace; m.ws_bytes = a->workspace_bytes;
+  const int rc = launch_mlp_step(m, (hipStream_t)stream);
+  if (rc) return fail("bb_ppo_mlp_step: launch failed (%d): %s", rc, hipGetErrorString(hipGetLastError()));
   return 0;
 }
 

@@ -1,0 +1,53 @@
+// bb_mlp.h -- one fused PPO minibatch step of the reference's proprio MLP
+// policy (bb_mlp.hip), shared with the C-ABI.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace bb {
+
+// Parameter slots in the flat fp32 buffer (float offsets, each a multiple of 4).
+enum MlpSlot {
+  MLP_PI_W0 = 0,  // pi trunk weights [128][15], [128][128] x3
+  MLP_PI_B0 = 4,  // pi trunk biases [128] x4
+  MLP_VF_W0 = 8,
+  MLP_VF_B0 = 12,
+  MLP_WA = 16,    // action_net [3][128]
+  MLP_BA = 17,    // [3]
+  MLP_WV = 18,    // value_net [1][128]
+  MLP_BV = 19,    // [1]
+  MLP_LS = 20,    // log_std [3]
+  MLP_NSLOTS = 21
+};
+
+struct MlpStepArgs {
+  float* params;        // flat fp32 parameters (AdamW updates them in place)
+  float* grad;          // flat fp32 gradients, same layout (gaps stay 0)
+  float* exp_avg;
+  float* exp_avg_sq;
+  long long n_params;   // flat length (with the alignment gaps)
+  int off[MLP_NSLOTS];
+  const float* obs;       // [n][15] rollout observations (sorted-key proprio)
+  const float* actions;   // [n][3] unclipped actions
+  const float* old_logp;  // [n]
+  const float* adv;       // [n]
+  const float* returns;   // [n]
+  const long long* perm;  // [nb][B] minibatch sample indices
+  long long* mb_counter;  // minibatch within the epoch (read, then incremented)
+  long long* row_counter; // log row (read, then incremented)
+  float* log;             // [rows][6]: loss, pg, vf, ent, approx_kl, clip_fraction
+  const float* clip;
+  const float* lr;
+  float* step;
+  float* coef;            // [4] AdamW scratch
+  int B, normalize;
+  float ent_coef, vf_coef;
+  double beta1, beta2, eps, weight_decay, max_norm;
+  float* ws;
+  long long ws_bytes;
+};
+
+long long mlp_workspace_bytes(int B);
+int launch_mlp_step(const MlpStepArgs& a, hipStream_t s);
+
+}  // namespace bb

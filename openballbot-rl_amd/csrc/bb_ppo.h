@@ -39,6 +39,10 @@ struct AdamWArgs {
   double weight_decay;
   float b2, omb1, omb2;    // float(beta2), float(1 - beta1), float(1 - beta2)
   float eps, max_norm;
+  // optional: per-workgroup partial sums of g^2 (bb_mlp.hip writes them while
+  // it assembles the gradient); NULL = the prep launch reduces grad itself
+  const float* norm_part;
+  int n_norm_part;
 };
 
 int launch_adamw_clip(const AdamWArgs& a, hipStream_t s);

@@ -135,13 +135,17 @@ constexpr int OPT_THREADS = 1024;
 __global__ __launch_bounds__(OPT_THREADS) void adamw_prep_kernel(AdamWArgs p) {
   __shared__ float red[OPT_THREADS / 64][NACC];
   float v[NACC] = {0, 0, 0, 0, 0, 0, 0, 0};
-  const long long n4 = p.n / 4;
-  const float4* g4 = reinterpret_cast<const float4*>(p.grad);
-  for (long long i = threadIdx.x; i < n4; i += OPT_THREADS) {
-    const float4 g = g4[i];
-    v[0] += g.x * g.x + g.y * g.y + g.z * g.z + g.w * g.w;
+  if (p.norm_part) {
+    for (int i = threadIdx.x; i < p.n_norm_part; i += OPT_THREADS) v[0] += p.norm_part[i];
+  } else {
+    const long long n4 = p.n / 4;
+    const float4* g4 = reinterpret_cast<const float4*>(p.grad);
+    for (long long i = threadIdx.x; i < n4; i += OPT_THREADS) {
+      const float4 g = g4[i];
+      v[0] += g.x * g.x + g.y * g.y + g.z * g.z + g.w * g.w;
+    }
+    for (long long i = n4 * 4 + threadIdx.x; i < p.n; i += OPT_THREADS) v[0] += p.grad[i] * p.grad[i];
   }
-  for (long long i = n4 * 4 + threadIdx.x; i < p.n; i += OPT_THREADS) v[0] += p.grad[i] * p.grad[i];
   block_sums(v, red);
   if (threadIdx.x == 0) {
     const float norm = sqrtf(v[0]);

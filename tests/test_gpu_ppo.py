@@ -274,3 +274,142 @@ def test_adamw_clip_rejects_bad_arguments():
     assert L.bb_adamw_clip(p, p, p, p, 16, p, s.data_ptr(), s.data_ptr(), 1.0, 0.999, 1e-8, 0.01, 0.5, None) < 0
     assert L.bb_adamw_clip(None, p, p, p, 16, p, s.data_ptr(), s.data_ptr(), 0.9, 0.999, 1e-8, 0.01, 0.5, None) < 0
 
+
+
+def _gpu_fake(n=256, ep_len=6):
+    from fake_env import FakeEnv
+
+    dev = torch.device("cuda:0")
+
+    class GpuFake(FakeEnv):
+        def __init__(self):
+            super().__init__(n, ep_len=ep_len)
+            self.device = dev
+
+        def reset(self):
+            o, i = super().reset()
+            return o.to(dev), i
+
+        def step(self, a):
+            o, r, d, t, i = super().step(a.cpu())
+            return o.to(dev), r.to(dev), d.to(dev), t.to(dev), i
+
+    return GpuFake()
+
+
+def _sb3_minibatch_loss(policy, obs, act, old_logp, adv, ret, clip, ent_coef, vf_coef, normalize):
+    """SB3 2.6.0 PPO.train's minibatch loss in plain torch autograd (the checker)."""
+    values, logp, entropy = policy.evaluate_actions(obs, act)
+    if normalize:
+        adv = (adv - adv.mean()) / (adv.std() + 1e-8)
+    lr = logp - old_logp
+    r = torch.exp(lr)
+    pg = -torch.min(adv * r, adv * torch.clamp(r, 1 - clip, 1 + clip)).mean()
+    vf = torch.nn.functional.mse_loss(ret, values)
+    ent = -torch.mean(entropy)
+    with torch.no_grad():
+        kl = torch.mean((r - 1) - lr)
+        cf = torch.mean((torch.abs(r - 1) > clip).float())
+    return pg + ent_coef * ent + vf_coef * vf, pg, vf, ent, kl, cf
+
+
+@pytest.mark.parametrize("normalize", [True, False])
+def test_fused_minibatch_matches_autograd(normalize):
+    """bb_ppo_mlp_step (one graph replay = one minibatch): gradients and log terms
+    vs torch autograd of the SB3 loss on the same parameters and samples (fp32;
+    only summation orders differ), and the AdamW step it applies vs FlatAdamW on
+    the autograd gradients."""
+    import copy
+
+    from ballbot_rl.training.logger import CSVLogger
+    from ballbot_rl.training.optim import FlatAdamW
+    from ballbot_rl.training.ppo import BatchedPPO, _UpdateGraphs
+
+    m = BatchedPPO(_gpu_fake(), n_steps=16, batch_size=512, n_epochs=2, learning_rate=1e-3, clip_range=0.1,
+                   ent_coef=0.01, vf_coef=0.5, normalize_advantage=normalize, seed=5,
+                   logger=CSVLogger(None, stdout=False))
+    m.collect_rollouts()
+    with torch.no_grad():  # spread the log ratio over the clip range
+        m.buf.log_probs.add_(0.1 * torch.randn_like(m.buf.log_probs))
+    d = {k: v.clone() for k, v in m.buf.flat().items()}
+    n = d["obs"].shape[0]
+    gr = _UpdateGraphs(m, n)
+    assert gr.fused
+    for k, v in gr.data.items():
+        v.copy_(d[k])
+    gr.clip.fill_(0.1)
+    perm = torch.randperm(n, device=m.device).view(gr.nb, -1)
+    gr.perm.copy_(perm)
+    gr.k.fill_(3); gr.row.zero_()
+    ref_policy = copy.deepcopy(m.policy)
+    ref_params = [p for p in ref_policy.parameters()]
+    gr.graph.replay()
+    torch.cuda.synchronize()
+    assert int(gr.k) == 4 and int(gr.row) == 1
+    idx = perm[3]
+    loss, pg, vf, ent, kl, cf = _sb3_minibatch_loss(ref_policy, d["obs"][idx], d["actions"][idx], d["log_probs"][idx],
+                                                    d["advantages"][idx], d["returns"][idx], 0.1, 0.01, 0.5, normalize)
+    loss.backward()
+    row = gr.log[0]
+    for got, want in zip(row.tolist(), (loss, pg, vf, ent, kl, cf)):
+        assert got == pytest.approx(float(want.detach()), rel=2e-4, abs=1e-6)
+    opt = m.optimizer
+    names = [nm for nm, _ in m.policy.named_parameters()]
+    where = {id(p): o for p, o in zip(opt.params, opt.offsets)}
+    for nm, p, q in zip(names, m.policy.parameters(), ref_params):
+        off = where[id(p)]
+        g = opt.grad[off:off + p.numel()].view_as(p)
+        scale = float(q.grad.abs().max())
+        err = float((g - q.grad).abs().max())
+        assert err <= 2e-4 * scale + 1e-8, (nm, err, scale)
+    # the AdamW step taken: FlatAdamW (tested against torch) on the autograd gradients
+    ref_opt = FlatAdamW(ref_params, lr=float(opt.lr), weight_decay=opt.weight_decay, max_grad_norm=opt.max_grad_norm)
+    ref_opt.step()
+    for p, q in zip(m.policy.parameters(), ref_params):
+        diff = (p.detach() - q.detach()).abs()
+        # first Adam step ~ lr * sign(g): elements whose gradient is ~0 may flip
+        assert float((diff > 1e-6).float().mean()) < 2e-3, float(diff.max())
+        assert float(diff.max()) <= 2.5e-3
+
+
+@pytest.mark.parametrize("target_kl", [None, 2e-3])
+def test_fused_update_matches_autograd_update(target_kl, monkeypatch):
+    """A whole update (all epochs, device-side KL stop) with the fused minibatch
+    vs the autograd graphs: same number of updates, log terms and parameters
+    within the fp32 reduction-order tolerance."""
+    from ballbot_rl.training.logger import CSVLogger
+    from ballbot_rl.training.ppo import BatchedPPO
+
+    models = []
+    for _ in range(2):
+        m = BatchedPPO(_gpu_fake(), n_steps=16, batch_size=512, n_epochs=3, learning_rate=3e-4, target_kl=target_kl,
+                       normalize_advantage=True, seed=4, logger=CSVLogger(None, stdout=False))
+        m.collect_rollouts()
+        models.append(m)
+    d0 = models[0].buf.flat()
+    for fused, m in zip(("0", "1"), models):  # the update graphs are built (and the path chosen) in _update
+        monkeypatch.setenv("BB_PPO_FUSED", fused)
+        m.shuffle_gen.manual_seed(99)
+        m._update({k: v.clone() for k, v in d0.items()})
+    assert not models[0]._graphs.fused and models[1]._graphs.fused
+    assert models[0]._n_updates == models[1]._n_updates
+    la, lb = models[0].logger.values, models[1].logger.values
+    for k in ("train/policy_gradient_loss", "train/value_loss", "train/approx_kl", "train/clip_fraction"):
+        assert la[k] == pytest.approx(lb[k], rel=5e-3, abs=1e-6), k
+    for a, b in zip(models[0].policy.parameters(), models[1].policy.parameters()):
+        diff = (a - b).abs()
+        assert float((diff > 1e-5).float().mean()) < 1e-2, float(diff.max())
+
+
+def test_ppo_mlp_step_rejects_bad_arguments():
+    import ctypes as C
+
+    from ballbot_gym import _native as N
+
+    L = N.lib()
+    nb = C.c_int64()
+    assert L.bb_ppo_mlp_workspace_bytes(100, C.byref(nb)) < 0
+    assert L.bb_ppo_mlp_workspace_bytes(8192, C.byref(nb)) == 0 and nb.value > 8192 * 2000 * 4
+    a = N.PPOMlpArgs()
+    assert L.bb_ppo_mlp_step(C.byref(a), None) < 0
+    assert "NULL" in N.last_error()
