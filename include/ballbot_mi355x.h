@@ -17,6 +17,8 @@
  *   bb_adamw_clip    SB3 PPO.train clip_grad_norm_ + AdamW step
  *   bb_ppo_mlp_step  SB3 PPO.train minibatch (forward, loss, backward, clip,
  *                    AdamW) of the reference's proprio MLP policy, fused
+ *   bb_ppo_mlp_act   SB3 collect_rollouts policy step (same policy)
+ *   bb_rollout_track SB3 collect_rollouts / Monitor episode bookkeeping
  *   bb_gae           SB3 RolloutBuffer.compute_returns_and_advantage (PPO)
  *   bb_forward       mujoco.mj_forward (diagnostic)             ballbot_env.py:525,620
  *   bb_get_state/    read/write qpos/qvel/qacc_warmstart        ballbot_env.py:616-617
@@ -161,7 +163,7 @@ int bb_adamw_clip(float* param_dev, const float* grad_dev, float* exp_avg_dev, f
  * parameter tensors in the flat buffer, each a multiple of 4, in the order
  * pi W0..W3, pi b0..b3, vf W0..W3, vf b0..b3, action W, action b, value W,
  * value b, log_std.  grad has the flat layout; entries outside the tensors are
- * never written (keep them 0).  B: a multiple of 32 and of 256 (>= 256).
+ * never written (keep them 0).  B: a multiple of 256 in [256, 16384].
  * workspace: >= bb_ppo_mlp_workspace_bytes(B) bytes of device memory.
  * Five launches on stream; graph-capturable. */
 typedef struct bb_ppo_mlp_args {
@@ -193,6 +195,29 @@ typedef struct bb_ppo_mlp_args {
 } bb_ppo_mlp_args;
 int bb_ppo_mlp_workspace_bytes(int B, int64_t* bytes);
 int bb_ppo_mlp_step(const bb_ppo_mlp_args* args, void* stream);
+/* The rollout's policy step for the same proprio MLP policy (SB3
+ * ActorCriticPolicy.forward as called by OnPolicyAlgorithm.collect_rollouts,
+ * model.learn at ballbot_rl/training/train.py:284): for n observation rows
+ * obs_dev [n][15], mean/value from the two trunks, actions = mean +
+ * noise * exp(log_std) (noise_dev [n][3] standard normal; NULL = the mean),
+ * their Gaussian log-probability and the value.  Writes actions_dev [n][3]
+ * (unclipped, as SB3 stores them), values_dev [n], log_prob_dev [n], and
+ * optionally clipped_dev [n][3] (clip to the [-1, 1] action space, what
+ * env.step receives) and obs_copy_dev [n][15] (the rollout buffer's copy).
+ * params_dev/offsets as for bb_ppo_mlp_step.  One launch; graph-capturable. */
+int bb_ppo_mlp_act(const float* params_dev, const int32_t* offsets, const float* obs_dev, const float* noise_dev, int n,
+                   float* obs_copy_dev, float* actions_dev, float* clipped_dev, float* values_dev, float* log_prob_dev,
+                   void* stream);
+/* One rollout step's episode bookkeeping (SB3 collect_rollouts + Monitor,
+ * model.learn at ballbot_rl/training/train.py:284): done = (flags_dev[i] &
+ * done_mask) != 0; rewards_out_dev[i] = reward_dev[i]; the float64 episode
+ * return ep_ret_dev and int64 length ep_len_dev accumulate, finished episodes
+ * are written to ep_r_out_dev (NaN elsewhere) / ep_l_out_dev (0 elsewhere) and
+ * their counters restart; starts_dev (and starts_next_dev unless NULL) get
+ * done as uint8 (episode_starts of the next step).  One launch. */
+int bb_rollout_track(const float* reward_dev, const uint8_t* flags_dev, int done_mask, int n, float* rewards_out_dev,
+                     double* ep_ret_dev, int64_t* ep_len_dev, double* ep_r_out_dev, int64_t* ep_l_out_dev,
+                     uint8_t* starts_dev, uint8_t* starts_next_dev, void* stream);
 /* copy terrain bank slot terrain_id (float32[293*293]) to host memory */
 int bb_get_hfield(bb_handle* h, int terrain_id, float* data_host);
 /* per-env terrain ids (device int32[n]) applied at the next reset */

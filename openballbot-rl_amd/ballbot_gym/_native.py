@@ -76,6 +76,7 @@ EXPORTS = [
     "bb_assign_terrain", "bb_reset", "bb_step", "bb_get_state", "bb_set_state", "bb_forward", "bb_get_stats",
     "bb_get_offsets", "bb_get_config", "bb_time_kernel", "bb_kernel_ms", "bb_generate_perlin", "bb_get_hfield",
     "bb_gae", "bb_render_depth", "bb_ppo_loss", "bb_adamw_clip", "bb_ppo_mlp_workspace_bytes", "bb_ppo_mlp_step",
+    "bb_ppo_mlp_act", "bb_rollout_track",
 ]
 
 ABI_VERSION = 9  # include/ballbot_mi355x.h BB_ABI_VERSION
@@ -151,6 +152,8 @@ def _load(path: Path):
     L.bb_gae.argtypes = [vp, vp, vp, vp, vp, C.c_int, C.c_int, C.c_double, C.c_double, vp, vp, vp]
     L.bb_ppo_mlp_workspace_bytes.argtypes = [C.c_int, C.POINTER(C.c_int64)]
     L.bb_ppo_mlp_step.argtypes = [C.POINTER(PPOMlpArgs), vp]
+    L.bb_ppo_mlp_act.argtypes = [vp, C.POINTER(C.c_int32), vp, vp, C.c_int, vp, vp, vp, vp, vp, vp]
+    L.bb_rollout_track.argtypes = [vp, vp, C.c_int, C.c_int] + [vp] * 8
     L.bb_kernel_ms.argtypes = [vp, C.POINTER(C.c_double), C.POINTER(C.c_int32)]
     for name in [n for n in EXPORTS if n not in ("bb_default_params", "bb_abi_version")]:
         getattr(L, name).restype = C.c_int

@@ -154,6 +154,23 @@ class BallbotVecEnv:
             reward = reward + self._host_reward_batch()
         return self.obs, reward, terminated, torch.zeros_like(terminated), info
 
+    def step_flags(self, actions: torch.Tensor):
+        """env.step without the derived tensors, for the batched trainer's
+        rollout: -> (obs[N,15], reward[N], done_flags[N] uint8, BB_DONE_* bits).
+        Same launch and buffers as step()."""
+        if self._host_reward is not None:
+            obs, reward, _, _, info = self.step(actions)
+            return obs, reward, info["done_flags"]
+        if actions.device != self.device or actions.dtype != torch.float32 or not actions.is_contiguous() \
+                or actions.shape != (self.num_envs, 3):
+            raise ValueError(f"actions must be a contiguous float32 ({self.num_envs}, 3) tensor on {self.device}")
+        N.check(N.lib().bb_step(self._h, _ptr(actions), _ptr(self.obs), _ptr(self.reward), _ptr(self.done),
+                                _ptr(self.terminal_obs), _ptr(self.pos2d), int(self.auto_reset), self._stream()),
+                "bb_step")
+        if self.cameras:
+            self._render(force=False)
+        return self.obs, self.reward, self.done
+
     def capture_step(self, actions: torch.Tensor) -> "torch.cuda.CUDAGraph":
         """Capture one env.step (routing, fast/full step kernels on the env's two
         streams, depth cameras) reading `actions` as ONE HIP graph; replay() then

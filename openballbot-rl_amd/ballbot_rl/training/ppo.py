@@ -151,11 +151,12 @@ def policy_obs(obs15: torch.Tensor, depth: Optional[torch.Tensor] = None,
     return d
 
 
-def fused_mlp_slots(ppo: "BatchedPPO"):
+def fused_mlp_slots(ppo: "BatchedPPO", update: bool = True):
     """Flat-buffer offsets of the 21 tensors bb_ppo_mlp_step reads, or None when
     the policy/optimiser is not the reference's proprio MLP on FlatAdamW
-    (pi = vf = [128]*4 LeakyReLU(0.01) over the 15-d obs, 3-d action head).
-    BB_PPO_FUSED=0 disables the fused update (A/B runs)."""
+    (pi = vf = [128]*4 LeakyReLU(0.01) over the 15-d obs, 3-d action head);
+    update=True also needs a batch size bb_ppo_mlp_step takes.
+    BB_PPO_FUSED=0 disables the fused update and rollout step (A/B runs)."""
     import os
 
     from ballbot_rl.training.optim import FlatAdamW
@@ -163,7 +164,9 @@ def fused_mlp_slots(ppo: "BatchedPPO"):
     if os.environ.get("BB_PPO_FUSED", "1") == "0" or ppo.cameras or ppo.device.type != "cuda":
         return None
     opt, pol = ppo.optimizer, ppo.policy
-    if not isinstance(opt, FlatAdamW) or ppo.batch_size % 256:
+    if not isinstance(opt, FlatAdamW):
+        return None
+    if update and (ppo.batch_size % 256 or ppo.batch_size > 16384):
         return None
 
     def trunk(seq):
@@ -420,6 +423,7 @@ class BatchedPPO:
         self._ep_ret = torch.zeros(self.n_envs, dtype=torch.float64, device=self.device)
         self._ep_len = torch.zeros(self.n_envs, dtype=torch.int64, device=self.device)
         self.progress_remaining = 1.0
+        self._act_slots = None  # fused rollout policy step: slots, False (not eligible) or None (not checked)
 
     # ------------------------------------------------------------ distributed
     def _sync_params(self) -> None:
@@ -435,9 +439,55 @@ class BatchedPPO:
                 off += k
 
     # ---------------------------------------------------------------- rollout
+    def _collect_fused(self, slots) -> tuple:
+        """collect_rollouts with the policy step as bb_ppo_mlp_act and the
+        episode bookkeeping as bb_rollout_track: three launches per env step
+        (policy, bb_step, bookkeeping) instead of ~40.  Same semantics as the
+        torch loop below (tests/test_gpu_ppo.py: test_fused_rollout_matches_torch)."""
+        from ballbot_gym import _native as N
+
+        env, b, dev = self.env, self.buf, self.device
+        lib = N.lib()
+        T, n = self.n_steps, self.n_envs
+        offs = (C.c_int32 * 21)(*slots)
+        flat = C.c_void_p(self.optimizer.flat.data_ptr())
+        if self._last_obs is None:
+            self._last_obs, _ = env.reset()
+        noise = torch.randn(T, n, 3, generator=self.gen, device=dev)
+        clipped = torch.empty(n, 3, device=dev)
+        ep_r = torch.empty(T, n, dtype=torch.float64, device=dev)
+        ep_l = torch.empty(T, n, dtype=torch.int64, device=dev)
+        b.starts[0].copy_(self._last_starts)
+        fast = hasattr(env, "step_flags")
+        stream = C.c_void_p(torch.cuda.current_stream(dev).cuda_stream)
+        for t in range(T):
+            obs_in = self._last_obs.contiguous()
+            N.check(lib.bb_ppo_mlp_act(flat, offs, _ptr(obs_in), _ptr(noise[t]), n, _ptr(b.obs[t]), _ptr(b.actions[t]),
+                                       _ptr(clipped), _ptr(b.values[t]), _ptr(b.log_probs[t]), stream),
+                    "bb_ppo_mlp_act")
+            if fast:
+                obs, reward, flags = env.step_flags(clipped)
+                mask = 5  # BB_DONE_TERMINATED | BB_DONE_DIVERGED (the reference never truncates)
+            else:
+                obs, reward, term, trunc, _info = env.step(clipped)
+                flags, mask = (term | trunc).to(torch.uint8).contiguous(), 1
+            reward = reward.contiguous()
+            nxt = _ptr(b.starts[t + 1]) if t + 1 < T else None
+            N.check(lib.bb_rollout_track(_ptr(reward), _ptr(flags), mask, n, _ptr(b.rewards[t]), _ptr(self._ep_ret),
+                                         _ptr(self._ep_len), _ptr(ep_r[t]), _ptr(ep_l[t]), _ptr(self._last_starts),
+                                         nxt, stream), "bb_rollout_track")
+            self._last_obs = obs
+        return ep_r, ep_l
+
     @torch.no_grad()
     def collect_rollouts(self) -> None:
         env, b = self.env, self.buf
+        if self._act_slots is None and not self.cameras and self.device.type == "cuda":
+            self._act_slots = fused_mlp_slots(self, update=False) or False
+        if self._act_slots:
+            ep_r, ep_l = self._collect_fused(self._act_slots)
+            self._finish_rollout(ep_r, ep_l)
+            return
         self.policy.eval()  # SB3 set_training_mode(False): BatchNorm uses running stats
         if self._last_obs is None:
             self._last_obs, _ = env.reset()
@@ -469,14 +519,19 @@ class BatchedPPO:
             self._ep_len.masked_fill_(done, 0)
             self._last_obs = obs
             self._last_starts = done.to(torch.uint8)
+        self._finish_rollout(torch.stack(ep_r), torch.stack(ep_l))
+
+    def _finish_rollout(self, ep_r: torch.Tensor, ep_l: torch.Tensor) -> None:
+        """GAE and the finished episodes ([T][N] returns, NaN where none ended; lengths)."""
+        env, b = self.env, self.buf
         self.num_timesteps += self.n_envs * self.n_steps * self.world
         last_v = self.policy.predict_values(
             policy_obs(self._last_obs, env.depth, env.rel_ts) if self.cameras else self._last_obs)
         b.advantages, b.returns = self.gae_fn(b.rewards, b.values, b.starts, last_v.contiguous(),
                                               self._last_starts.contiguous(), self.gamma, self.gae_lambda)
         # finished episodes in time order (one host sync per rollout)
-        r = torch.stack(ep_r).cpu().numpy()
-        ln = torch.stack(ep_l).cpu().numpy()
+        r = ep_r.cpu().numpy()
+        ln = ep_l.cpu().numpy()
         mask = ~np.isnan(r)
         finished = list(zip(r[mask].tolist(), ln[mask].tolist()))
         if self.world > 1:

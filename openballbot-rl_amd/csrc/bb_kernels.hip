@@ -834,7 +834,8 @@ int bb_adamw_clip(float* param, const float* grad, float* exp_avg, float* exp_av
 
 int bb_ppo_mlp_workspace_bytes(int B, int64_t* bytes) {
   if (!bytes) return fail("bb_ppo_mlp_workspace_bytes: NULL argument");
-  if (B < 256 || B % 256) return fail("bb_ppo_mlp_workspace_bytes: B must be a positive multiple of 256 (got %d)", B);
+  if (B < 256 || B % 256 || B > 16384)
+    return fail("bb_ppo_mlp_workspace_bytes: B must be a multiple of 256 in [256, 16384] (got %d)", B);
   *bytes = mlp_workspace_bytes(B);
   return 0;
 }
@@ -845,7 +846,8 @@ int bb_ppo_mlp_step(const bb_ppo_mlp_args* a, void* stream) {
       !a->advantages || !a->returns || !a->perm || !a->mb_counter || !a->row_counter || !a->log || !a->clip ||
       !a->lr || !a->step || !a->coef || !a->workspace)
     return fail("bb_ppo_mlp_step: NULL argument");
-  if (a->B < 256 || a->B % 256) return fail("bb_ppo_mlp_step: B must be a positive multiple of 256 (got %d)", a->B);
+  if (a->B < 256 || a->B % 256 || a->B > 16384)
+    return fail("bb_ppo_mlp_step: B must be a multiple of 256 in [256, 16384] (got %d)", a->B);
   if (a->workspace_bytes < mlp_workspace_bytes(a->B))
     return fail("bb_ppo_mlp_step: workspace of %lld bytes < %lld", (long long)a->workspace_bytes,
                 mlp_workspace_bytes(a->B));
@@ -876,6 +878,35 @@ int bb_ppo_mlp_step(const bb_ppo_mlp_args* a, void* stream) {
   m.max_norm = a->max_grad_norm; m.ws = a->workspace; m.ws_bytes = a->workspace_bytes;
   const int rc = launch_mlp_step(m, (hipStream_t)stream);
   if (rc) return fail("bb_ppo_mlp_step: launch failed (%d): %s", rc, hipGetErrorString(hipGetLastError()));
+  return 0;
+}
+
+int bb_ppo_mlp_act(const float* params, const int32_t* offsets, const float* obs, const float* noise, int n,
+                   float* obs_copy, float* actions, float* clipped, float* values, float* log_prob, void* stream) {
+  if (!params || !offsets || !obs || !actions || !values || !log_prob) return fail("bb_ppo_mlp_act: NULL argument");
+  if (n < 0) return fail("bb_ppo_mlp_act: n must be >= 0 (got %d)", n);
+  for (int i = 0; i < MLP_NSLOTS; i++)
+    if (offsets[i] < 0 || offsets[i] % 4) return fail("bb_ppo_mlp_act: offsets[%d] = %d is not 4-aligned", i, offsets[i]);
+  if (reinterpret_cast<uintptr_t>(params) & 15) return fail("bb_ppo_mlp_act: params must be 16-byte aligned");
+  MlpActArgs m;
+  m.params = params;
+  for (int i = 0; i < MLP_NSLOTS; i++) m.off[i] = offsets[i];
+  m.obs = obs; m.noise = noise; m.n = n; m.obs_copy = obs_copy; m.actions = actions; m.clipped = clipped;
+  m.values = values; m.log_prob = log_prob;
+  if (launch_mlp_act(m, (hipStream_t)stream))
+    return fail("bb_ppo_mlp_act: launch failed: %s", hipGetErrorString(hipGetLastError()));
+  return 0;
+}
+
+int bb_rollout_track(const float* reward, const uint8_t* flags, int mask, int n, float* rewards_out, double* ep_ret,
+                     int64_t* ep_len, double* ep_r_out, int64_t* ep_l_out, uint8_t* starts, uint8_t* starts_next,
+                     void* stream) {
+  if (!reward || !flags || !rewards_out || !ep_ret || !ep_len || !ep_r_out || !ep_l_out || !starts)
+    return fail("bb_rollout_track: NULL argument");
+  if (n < 0) return fail("bb_rollout_track: n must be >= 0 (got %d)", n);
+  if (launch_track(reward, flags, mask, n, rewards_out, ep_ret, reinterpret_cast<long long*>(ep_len), ep_r_out,
+                   reinterpret_cast<long long*>(ep_l_out), starts, starts_next, (hipStream_t)stream))
+    return fail("bb_rollout_track: launch failed: %s", hipGetErrorString(hipGetLastError()));
   return 0;
 }
 

@@ -47,7 +47,22 @@ struct MlpStepArgs {
   long long ws_bytes;
 };
 
+// the rollout's policy step (SB3 ActorCriticPolicy.forward) for n obs rows
+struct MlpActArgs {
+  const float* params;
+  int off[MLP_NSLOTS];
+  const float* obs;      // [n][15]
+  const float* noise;    // [n][3] or NULL (deterministic)
+  int n;
+  float* obs_copy;       // [n][15] or NULL
+  float* actions;        // [n][3] unclipped
+  float* clipped;        // [n][3] or NULL
+  float* values;         // [n]
+  float* log_prob;       // [n]
+};
+
 long long mlp_workspace_bytes(int B);
+int launch_mlp_act(const MlpActArgs& a, hipStream_t s);
 int launch_mlp_step(const MlpStepArgs& a, hipStream_t s);
 
 }  // namespace bb

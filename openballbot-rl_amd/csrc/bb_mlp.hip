@@ -47,14 +47,14 @@ constexpr int HID = 128;          // trunk width
 constexpr int IN = 15;            // observation features
 constexpr int XW = 32;            // workspace row width of the padded input
 constexpr int ROWS = 32;          // rows per tile (the MFMA M)
-constexpr int T1 = 256;           // threads per tile workgroup
+constexpr int T1 = 512;           // threads per tile workgroup: 8 waves = 2 trunks x 4 column blocks
 constexpr int LDT = HID + 4;      // LDS row stride (floats): float4 rows, no bank conflicts
 constexpr int LDX = IN + 2;       // input tile stride
-constexpr int NCH = 8;            // K chunks of the weight-gradient GEMMs
-constexpr int BPART = 2 * 4 * HID + 4;  // bias partials per tile: trunk biases, ba[3], bv
+constexpr int MAXCH = 32;         // max K chunks of the weight-gradient GEMMs
 constexpr int LPART = 8;          // loss partials per tile: pg, vf, kl, cf, dls[3], -
 constexpr int NJOB = 10;          // weight-gradient GEMMs: 2 trunks x 4 layers + 2 heads
-constexpr int NSEG = 21;          // gradient segments (weights, biases, log_std)
+constexpr int NSEG = 2 * NJOB;    // gradient segments: weights and biases of each job
+constexpr int SLAB = 32;          // rows per LDS slab in the dW kernel
 constexpr float SLOPE = 0.01f;    // nn.LeakyReLU default negative_slope
 constexpr float HALF_LOG_2PI = 0.91893853320467274f;
 
@@ -65,14 +65,24 @@ __device__ __forceinline__ f32x16 mfma(float a, float b, f32x16 c) {
 __device__ __forceinline__ int crow(int reg, int lane) { return (reg & 3) + 8 * (reg >> 2) + 4 * (lane >> 5); }
 __device__ __forceinline__ float leaky(float z) { return z > 0.f ? z : z * SLOPE; }
 
+// K chunks of the weight-gradient GEMMs: the most (<= 32) whose chunk is a
+// whole number of SLAB-row slabs
+__host__ __device__ inline int n_chunks(int B) {
+  for (int c = MAXCH; c > 1; c >>= 1)
+    if (B % (c * SLAB) == 0) return c;
+  return 1;
+}
+constexpr int WELEMS = 2 * (HID * IN + 3 * HID * HID) + 4 * HID;  // weight elements
+constexpr int BELEMS = 2 * 4 * HID + 4;                           // bias elements
+
 struct Workspace {
   float* x;           // [B][32] padded inputs
   float* h[2][4];     // [B][128] h1..h4 per trunk
   float* dz[2][4];    // [B][128] dL/dz of layers 0..3 per trunk
   float* dhead;       // [B][4] dL/dmean[3], dL/dvalue
-  float* bpart;       // [B/32][BPART]
   float* lpart;       // [B/32][LPART]
-  float* wpart;       // [NCH][weights]
+  float* wpart;       // [nch][weights] per job
+  float* bpart;       // [nch][biases] per job
   float* npart;       // [reduce workgroups]
 };
 
@@ -86,9 +96,9 @@ Workspace carve(float* base, int B, long long* total_floats) {
   for (int t = 0; t < 2; t++)
     for (int l = 0; l < 4; l++) w.dz[t][l] = take((long long)B * HID);
   w.dhead = take((long long)B * 4);
-  w.bpart = take((long long)(B / ROWS) * BPART);
   w.lpart = take((long long)(B / ROWS) * LPART);
-  w.wpart = take((long long)NCH * (2 * (HID * IN + 3 * HID * HID) + 4 * HID));
+  w.wpart = take((long long)MAXCH * WELEMS);
+  w.bpart = take((long long)MAXCH * BELEMS);
   w.npart = take(4096);
   if (total_floats) *total_floats = o;
   return w;
@@ -108,9 +118,17 @@ struct TileArgs {
   int B, normalize;
   float vf_coef;
   Workspace w;
+  // rollout (act) mode: rows r0.. of obs directly, n of them
+  int n;
+  const float* noise;   // [n][3] standard normal draws, NULL = deterministic (the mean)
+  float* obs_copy;      // [n][15] or NULL
+  float* act_out;       // [n][3] unclipped actions
+  float* act_clipped;   // [n][3] actions clipped to [-1, 1] or NULL
+  float* values_out;    // [n]
+  float* logp_out;      // [n]
 };
 
-// block-wide sum over T1 threads, same order in every workgroup
+// block-wide sum over the T1 threads, same order in every workgroup
 __device__ float block_sum(float v, float* red) {
 #pragma unroll
   for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off, 64);
@@ -118,149 +136,192 @@ __device__ float block_sum(float v, float* red) {
   __syncthreads();
   if (lane == 0) red[wid] = v;
   __syncthreads();
-  return (red[0] + red[1]) + (red[2] + red[3]);
+  return ((red[0] + red[1]) + (red[2] + red[3])) + ((red[4] + red[5]) + (red[6] + red[7]));
 }
 
-// store a wave's 32x32 C-layout block: rows of the tile, columns col0..col0+31
+// store a wave's 32x32 C-layout block: rows of the tile, column col
 __device__ __forceinline__ void store_block(const f32x16& v, float* dst, int ld, int col, int lane) {
 #pragma unroll
   for (int r = 0; r < 16; r++) dst[(long long)crow(r, lane) * ld + col] = v[r];
 }
 
-// a layer's output gradient: to the workspace (weight GEMMs) and its column
-// sums over the tile (bias gradient partial)
-__device__ __forceinline__ void dz_out(const f32x16& dz, const Workspace& w, int t, int l, int r0, int tile, int col,
-                                       int lane) {
-  store_block(dz, w.dz[t][l] + (long long)r0 * HID, HID, col, lane);
-  float s = 0.f;
+// one 128->128 product of a 32-row tile for this wave's 32 output columns:
+// acc += A (LDS tile, rows x K) * B, B[k][col] = wk(k) -- forward: W[col][k]
+// (float4 along k), backward: W[k][col]
+template <bool FWD>
+__device__ __forceinline__ f32x16 tile_gemm(f32x16 acc, const float* tile_row, const float* W, int col, int hh) {
+  // every W operand of the layer is requested before the first MFMA (64 VGPRs),
+  // so the L2 latency is paid once per layer, not once per unrolled group
+  const float* arow = tile_row + 4 * hh;
+  float4 b4[HID / 8];
+  if (FWD) {
+    const float* wrow = W + col * HID + 4 * hh;
 #pragma unroll
-  for (int r = 0; r < 16; r++) s += dz[r];
-  s += __shfl_xor(s, 32, 64);
-  if (lane < 32) w.bpart[(long long)tile * BPART + t * 4 * HID + l * HID + col] = s;
+    for (int m = 0; m < HID / 8; m++) b4[m] = *reinterpret_cast<const float4*>(wrow + 8 * m);
+  } else {
+    const float* wcol = W + 4 * hh * HID + col;
+#pragma unroll
+    for (int m = 0; m < HID / 8; m++) {
+      const float* wp = wcol + 8 * m * HID;
+      b4[m] = make_float4(wp[0], wp[HID], wp[2 * HID], wp[3 * HID]);
+    }
+  }
+#pragma unroll
+  for (int m = 0; m < HID / 8; m++) {
+    const float4 a4 = *reinterpret_cast<const float4*>(arow + 8 * m);
+    acc = mfma(a4.x, b4[m].x, acc);
+    acc = mfma(a4.y, b4[m].y, acc);
+    acc = mfma(a4.z, b4[m].z, acc);
+    acc = mfma(a4.w, b4[m].w, acc);
+  }
+  return acc;
 }
 
+// TRAIN: one minibatch tile of the update (forward, loss, backward).
+// !TRAIN: the rollout's policy step, SB3 ActorCriticPolicy.forward over obs rows.
+template <bool TRAIN>
 __global__ __launch_bounds__(T1) void mlp_tile_kernel(TileArgs p) {
-  __shared__ __attribute__((aligned(16))) float xs[2][ROWS][LDT];  // layer-input exchange tiles
+  __shared__ __attribute__((aligned(16))) float xs[2][2][ROWS][LDT];  // [trunk][buffer] exchange tiles
   __shared__ float xin[ROWS][LDX];
   __shared__ float head[ROWS][4];  // dL/dmean[3], dL/dvalue
   __shared__ float hm[ROWS][4];    // mean[3], value
-  __shared__ float red[4];
+  __shared__ float red[8];
   __shared__ int idx[ROWS];
 
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, hh = lane >> 5;
-  const int col = w * 32 + (lane & 31);
+  const int t = w >> 2;                           // trunk: 0 pi, 1 vf
+  const int col = (w & 3) * 32 + (lane & 31);     // this lane's output column
   const int B = p.B, tile = blockIdx.x, r0 = tile * ROWS;
-  const long long* perm = p.perm + (*p.mb_counter) * (long long)B;
+  const long long* perm = TRAIN ? p.perm + (*p.mb_counter) * (long long)B : nullptr;
   const float* P = p.P;
 
-  // advantage normalisation over the minibatch (torch.std: unbiased)
+  // advantage normalisation over the minibatch (torch.std: unbiased), one pass
+  // over memory: each thread keeps its samples in registers
   float amean = 0.f, ainv = 1.f;
-  if (p.normalize && B > 1) {
+  if (TRAIN && p.normalize && B > 1) {
+    constexpr int MAXPT = 32;  // B <= 16384 keeps every sample in registers
+    float v[MAXPT];
     float s = 0.f;
-    for (int i = tid; i < B; i += T1) s += p.adv[perm[i]];
+#pragma unroll
+    for (int j = 0; j < MAXPT; j++) {
+      const int i = tid + j * T1;
+      v[j] = i < B ? p.adv[perm[i]] : 0.f;
+      s += v[j];
+    }
+    for (int i = tid + MAXPT * T1; i < B; i += T1) s += p.adv[perm[i]];
     amean = block_sum(s, red) / float(B);
     float q = 0.f;
-    for (int i = tid; i < B; i += T1) { const float d = p.adv[perm[i]] - amean; q += d * d; }
+#pragma unroll
+    for (int j = 0; j < MAXPT; j++) {
+      const float d = v[j] - amean;
+      q += tid + j * T1 < B ? d * d : 0.f;
+    }
+    for (int i = tid + MAXPT * T1; i < B; i += T1) { const float d = p.adv[perm[i]] - amean; q += d * d; }
     ainv = 1.f / (sqrtf(block_sum(q, red) / float(B - 1)) + 1e-8f);
   }
 
-  if (tid < ROWS) idx[tid] = (int)perm[r0 + tid];
+  if (tid < ROWS) idx[tid] = TRAIN ? (int)perm[r0 + tid] : (r0 + tid < p.n ? r0 + tid : -1);
   __syncthreads();
   for (int e = tid; e < ROWS * XW; e += T1) {
-    const int r = e >> 5, c = e & 31;
-    const float v = c < IN ? p.obs[(long long)idx[r] * IN + c] : 0.f;
+    const int r = e >> 5, c = e & 31, i = idx[r];
+    const float v = c < IN && i >= 0 ? p.obs[(long long)i * IN + c] : 0.f;
     if (c < LDX) xin[r][c] = v;
-    p.w.x[(long long)(r0 + r) * XW + c] = v;
+    if (TRAIN) p.w.x[(long long)(r0 + r) * XW + c] = v;
+    if (!TRAIN && p.obs_copy && c < IN && i >= 0) p.obs_copy[(long long)i * IN + c] = v;
   }
   __syncthreads();
 
-  // ---------------- forward: both trunks, activations kept in C layout
-  f32x16 hreg[2][4];
+  // ---------------- forward: waves 0-3 the pi trunk, 4-7 the vf trunk, in lockstep
+  const int wbase = t ? MLP_VF_W0 : MLP_PI_W0, bbase = t ? MLP_VF_B0 : MLP_PI_B0;
+  f32x16 hreg[4];
   int cur = 0;
+  {  // layer 0, K = 15 (padded to 16)
+    f32x16 acc;
+    const float bias = P[p.off[bbase] + col];
 #pragma unroll
-  for (int t = 0; t < 2; t++) {
-    const int ow = p.off[t ? MLP_VF_W0 : MLP_PI_W0], ob = p.off[t ? MLP_VF_B0 : MLP_PI_B0];
-    {  // layer 0, K = 15 (padded to 16)
-      f32x16 acc;
-      const float bias = P[ob + col];
+    for (int r = 0; r < 16; r++) acc[r] = bias;
+    const float* W0 = P + p.off[wbase] + col * IN;
 #pragma unroll
-      for (int r = 0; r < 16; r++) acc[r] = bias;
-#pragma unroll
-      for (int s = 0; s < 8; s++) {
-        const int k = 2 * s + hh;
-        const float a = xin[lane & 31][k];
-        const float b = k < IN ? P[ow + col * IN + k] : 0.f;
-        acc = mfma(a, b, acc);
-      }
-#pragma unroll
-      for (int r = 0; r < 16; r++) acc[r] = leaky(acc[r]);
-      hreg[t][0] = acc;
-      store_block(acc, p.w.h[t][0] + (long long)r0 * HID, HID, col, lane);
-      store_block(acc, &xs[cur][0][0], LDT, col, lane);
-      __syncthreads();
+    for (int s = 0; s < 8; s++) {
+      const int k = 2 * s + hh;
+      acc = mfma(xin[lane & 31][k], k < IN ? W0[k] : 0.f, acc);
     }
 #pragma unroll
-    for (int l = 1; l < 4; l++) {
-      const float* W = P + p.off[(t ? MLP_VF_W0 : MLP_PI_W0) + l];
-      f32x16 acc;
-      const float bias = P[p.off[(t ? MLP_VF_B0 : MLP_PI_B0) + l] + col];
-#pragma unroll
-      for (int r = 0; r < 16; r++) acc[r] = bias;
-      const float* arow = &xs[cur][lane & 31][4 * hh];
-      const float* wrow = W + col * HID + 4 * hh;
-#pragma unroll 4
-      for (int m = 0; m < HID / 8; m++) {
-        const float4 a4 = *reinterpret_cast<const float4*>(arow + 8 * m);
-        const float4 b4 = *reinterpret_cast<const float4*>(wrow + 8 * m);
-        acc = mfma(a4.x, b4.x, acc);
-        acc = mfma(a4.y, b4.y, acc);
-        acc = mfma(a4.z, b4.z, acc);
-        acc = mfma(a4.w, b4.w, acc);
-      }
-#pragma unroll
-      for (int r = 0; r < 16; r++) acc[r] = leaky(acc[r]);
-      hreg[t][l] = acc;
-      store_block(acc, p.w.h[t][l] + (long long)r0 * HID, HID, col, lane);
-      store_block(acc, &xs[cur ^ 1][0][0], LDT, col, lane);
-      cur ^= 1;
-      __syncthreads();
-    }
-    // head on h4 (xs[cur]): thread (row tid>>3, part tid&7) sums 16 columns
-    {
-      const int r = tid >> 3, part = tid & 7;
-      const float* hrow = &xs[cur][r][part * 16];
-      float s0 = 0.f, s1 = 0.f, s2 = 0.f;
-      if (t == 0) {
-        const float* Wa = P + p.off[MLP_WA] + part * 16;
-#pragma unroll
-        for (int c = 0; c < 16; c++) {
-          const float h = hrow[c];
-          s0 += h * Wa[c];
-          s1 += h * Wa[HID + c];
-          s2 += h * Wa[2 * HID + c];
-        }
-      } else {
-        const float* Wv = P + p.off[MLP_WV] + part * 16;
-#pragma unroll
-        for (int c = 0; c < 16; c++) s0 += hrow[c] * Wv[c];
-      }
-#pragma unroll
-      for (int off = 1; off < 8; off <<= 1) {
-        s0 += __shfl_xor(s0, off, 64);
-        s1 += __shfl_xor(s1, off, 64);
-        s2 += __shfl_xor(s2, off, 64);
-      }
-      if (part == 0) {
-        if (t == 0) {
-          hm[r][0] = s0 + P[p.off[MLP_BA]];
-          hm[r][1] = s1 + P[p.off[MLP_BA] + 1];
-          hm[r][2] = s2 + P[p.off[MLP_BA] + 2];
-        } else {
-          hm[r][3] = s0 + P[p.off[MLP_BV]];
-        }
-      }
-    }
+    for (int r = 0; r < 16; r++) acc[r] = leaky(acc[r]);
+    hreg[0] = acc;
+    if (TRAIN) store_block(acc, p.w.h[t][0] + (long long)r0 * HID, HID, col, lane);
+    store_block(acc, &xs[t][cur][0][0], LDT, col, lane);
     __syncthreads();
+  }
+#pragma unroll
+  for (int l = 1; l < 4; l++) {
+    f32x16 acc;
+    const float bias = P[p.off[bbase + l] + col];
+#pragma unroll
+    for (int r = 0; r < 16; r++) acc[r] = bias;
+    acc = tile_gemm<true>(acc, &xs[t][cur][lane & 31][0], P + p.off[wbase + l], col, hh);
+#pragma unroll
+    for (int r = 0; r < 16; r++) acc[r] = leaky(acc[r]);
+    hreg[l] = acc;
+    if (TRAIN) store_block(acc, p.w.h[t][l] + (long long)r0 * HID, HID, col, lane);
+    store_block(acc, &xs[t][cur ^ 1][0][0], LDT, col, lane);
+    cur ^= 1;
+    __syncthreads();
+  }
+  // heads on h4 (xs[t][cur]): threads of trunk t, (row, 16-column part)
+  {
+    const int tt = tid >> 8, r = (tid >> 3) & 31, part = tid & 7;
+    const float* hrow = &xs[tt][cur][r][part * 16];
+    float s0 = 0.f, s1 = 0.f, s2 = 0.f;
+    if (tt == 0) {
+      const float* Wa = P + p.off[MLP_WA] + part * 16;
+#pragma unroll
+      for (int c = 0; c < 16; c++) {
+        const float h = hrow[c];
+        s0 += h * Wa[c];
+        s1 += h * Wa[HID + c];
+        s2 += h * Wa[2 * HID + c];
+      }
+    } else {
+      const float* Wv = P + p.off[MLP_WV] + part * 16;
+#pragma unroll
+      for (int c = 0; c < 16; c++) s0 += hrow[c] * Wv[c];
+    }
+#pragma unroll
+    for (int off = 1; off < 8; off <<= 1) {
+      s0 += __shfl_xor(s0, off, 64);
+      s1 += __shfl_xor(s1, off, 64);
+      s2 += __shfl_xor(s2, off, 64);
+    }
+    if (part == 0) {
+      if (tt == 0) {
+        hm[r][0] = s0 + P[p.off[MLP_BA]];
+        hm[r][1] = s1 + P[p.off[MLP_BA] + 1];
+        hm[r][2] = s2 + P[p.off[MLP_BA] + 2];
+      } else {
+        hm[r][3] = s0 + P[p.off[MLP_BV]];
+      }
+    }
+  }
+  __syncthreads();
+
+  if (!TRAIN) {  // SB3 DiagGaussian: a = mean + eps * exp(log_std); log_prob of a; value
+    if (w != 0 || lane >= ROWS || idx[lane] < 0) return;
+    const int r = lane, i = idx[r];
+    const float* ls = P + p.off[MLP_LS];
+    float lp = 0.f;
+#pragma unroll
+    for (int j = 0; j < 3; j++) {
+      const float mu = hm[r][j];
+      const float a = p.noise ? __fadd_rn(mu, __fmul_rn(p.noise[3LL * i + j], expf(ls[j]))) : mu;
+      const float z = __fmul_rn(__fsub_rn(a, mu), expf(-ls[j]));
+      lp += -0.5f * z * z - ls[j] - 0.5f * (2.f * HALF_LOG_2PI);
+      p.act_out[3LL * i + j] = a;
+      if (p.act_clipped) p.act_clipped[3LL * i + j] = fminf(fmaxf(a, -1.f), 1.f);
+    }
+    p.values_out[i] = hm[r][3];
+    p.logp_out[i] = lp;
+    return;
   }
 
   // ---------------- loss (SB3 PPO.train, bb_ppo.hip) and head gradients: wave 0, lane = row
@@ -271,8 +332,7 @@ __global__ __launch_bounds__(T1) void mlp_tile_kernel(TileArgs p) {
     const float inv_std[3] = {expf(-l0), expf(-l1), expf(-l2)};
     const float lp_const = -(l0 + l1 + l2) - 3.f * HALF_LOG_2PI;
     const float invB = 1.f / float(B);
-    float acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-    float gh[4] = {0, 0, 0, 0};
+    float acc[7] = {0, 0, 0, 0, 0, 0, 0};
     if (lane < ROWS) {
       const int r = lane, i = idx[r];
       float z[3], lp = lp_const;
@@ -294,6 +354,7 @@ __global__ __launch_bounds__(T1) void mlp_tile_kernel(TileArgs p) {
       const bool inside = rho >= 1.f - c && rho <= 1.f + c;
       const float gr = (inside || s1 < s2) ? -A : 0.f;
       const float glp = gr * rho * invB;
+      float gh[4];
 #pragma unroll
       for (int j = 0; j < 3; j++) {
         gh[j] = glp * z[j] * inv_std[j];
@@ -311,135 +372,147 @@ __global__ __launch_bounds__(T1) void mlp_tile_kernel(TileArgs p) {
     for (int off = 1; off < 64; off <<= 1) {
 #pragma unroll
       for (int q = 0; q < 7; q++) acc[q] += __shfl_xor(acc[q], off, 64);
-#pragma unroll
-      for (int j = 0; j < 4; j++) gh[j] += __shfl_xor(gh[j], off, 64);
     }
     if (lane == 0) {
 #pragma unroll
       for (int q = 0; q < 7; q++) p.w.lpart[(long long)tile * LPART + q] = acc[q];
       p.w.lpart[(long long)tile * LPART + 7] = 0.f;
-#pragma unroll
-      for (int j = 0; j < 4; j++) p.w.bpart[(long long)tile * BPART + 2 * 4 * HID + j] = gh[j];
     }
   }
   __syncthreads();
 
-  // ---------------- backward through both trunks
+  // ---------------- backward, both trunks in lockstep
+  f32x16 dz;
+  {
+    const float* Wh = P + p.off[t ? MLP_WV : MLP_WA];
+    const float w0 = Wh[col];
+    const float w1 = t ? 0.f : Wh[HID + col];
+    const float w2 = t ? 0.f : Wh[2 * HID + col];
 #pragma unroll
-  for (int t = 0; t < 2; t++) {
-    f32x16 dz;
-    {
-      const float* Wh = P + p.off[t ? MLP_WV : MLP_WA];
-      const float w0 = Wh[col];
-      const float w1 = t ? 0.f : Wh[HID + col];
-      const float w2 = t ? 0.f : Wh[2 * HID + col];
-#pragma unroll
-      for (int r = 0; r < 16; r++) {
-        const int R = crow(r, lane);
-        const float d = t ? head[R][3] * w0 : (head[R][0] * w0 + head[R][1] * w1) + head[R][2] * w2;
-        dz[r] = hreg[t][3][r] > 0.f ? d : d * SLOPE;
-      }
+    for (int r = 0; r < 16; r++) {
+      const int R = crow(r, lane);
+      const float d = t ? head[R][3] * w0 : (head[R][0] * w0 + head[R][1] * w1) + head[R][2] * w2;
+      dz[r] = hreg[3][r] > 0.f ? d : d * SLOPE;
     }
-#pragma unroll
-    for (int l = 3; l >= 1; l--) {
-      dz_out(dz, p.w, t, l, r0, tile, col, lane);
-      store_block(dz, &xs[cur][0][0], LDT, col, lane);
-      __syncthreads();
-      const float* W = P + p.off[(t ? MLP_VF_W0 : MLP_PI_W0) + l];
-      f32x16 acc;
-#pragma unroll
-      for (int r = 0; r < 16; r++) acc[r] = 0.f;
-      const float* arow = &xs[cur][lane & 31][4 * hh];
-      const float* wcol = W + 4 * hh * HID + col;
-#pragma unroll 4
-      for (int m = 0; m < HID / 8; m++) {
-        const float4 a4 = *reinterpret_cast<const float4*>(arow + 8 * m);
-        const float* wp = wcol + 8 * m * HID;
-        acc = mfma(a4.x, wp[0], acc);
-        acc = mfma(a4.y, wp[HID], acc);
-        acc = mfma(a4.z, wp[2 * HID], acc);
-        acc = mfma(a4.w, wp[3 * HID], acc);
-      }
-#pragma unroll
-      for (int r = 0; r < 16; r++) dz[r] = hreg[t][l - 1][r] > 0.f ? acc[r] : acc[r] * SLOPE;
-      cur ^= 1;
-    }
-    dz_out(dz, p.w, t, 0, r0, tile, col, lane);
   }
+#pragma unroll
+  for (int l = 3; l >= 1; l--) {
+    store_block(dz, p.w.dz[t][l] + (long long)r0 * HID, HID, col, lane);
+    store_block(dz, &xs[t][cur][0][0], LDT, col, lane);
+    __syncthreads();
+    f32x16 acc;
+#pragma unroll
+    for (int r = 0; r < 16; r++) acc[r] = 0.f;
+    acc = tile_gemm<false>(acc, &xs[t][cur][lane & 31][0], P + p.off[wbase + l], col, hh);
+#pragma unroll
+    for (int r = 0; r < 16; r++) dz[r] = hreg[l - 1][r] > 0.f ? acc[r] : acc[r] * SLOPE;
+    cur ^= 1;
+  }
+  store_block(dz, p.w.dz[t][0] + (long long)r0 * HID, HID, col, lane);
 }
 
-// ---------------- weight gradients: dW = dz^T h over row chunks
+// ---------------- weight and bias gradients: dW = dz^T h, db = dz^T 1 over row chunks
 struct GemmJob {
   const float* dz;
   const float* h;
-  float* part;     // [NCH][O][I]
-  int ldz, ldh, O, I, nob, nib, first;
+  float* wpart;    // [nch][O][I]
+  float* bpart;    // [nch][O]
+  int ldz, ldh, O, I;
 };
 struct GemmArgs {
   GemmJob job[NJOB];
-  int nunits, chunk;
+  int order[NJOB];  // grid order of the jobs: the 128x128 layers first
+  int nch, chunk;
 };
 
-constexpr int PF = 16;  // MFMA steps per prefetch batch
-
+// one workgroup per (job, chunk).  The chunk's dz and h rows pass through LDS in
+// 32-row slabs (coalesced loads by all 256 threads, the next slab in flight
+// while the current one feeds the MFMAs); wave w owns output rows 32w..32w+31
+// and all (<= 4) 32-column blocks.
 __global__ __launch_bounds__(256) void mlp_dw_kernel(GemmArgs g) {
-  const int unit = blockIdx.x * 4 + (threadIdx.x >> 6);
-  if (unit >= g.nunits) return;
-  const int lane = threadIdx.x & 63, hh = lane >> 5;
-  int j = 0;
-#pragma unroll
-  for (int q = 1; q < NJOB; q++)
-    if (unit >= g.job[q].first) j = q;
+  __shared__ float za[2][SLAB][LDT];
+  __shared__ float hb[2][SLAB][LDT];
+  const int j = g.order[blockIdx.x / g.nch], chunk = blockIdx.x % g.nch;
   const GemmJob J = g.job[j];
-  const int u = unit - J.first, nblk = J.nob * J.nib;
-  const int chunk = u / nblk, ob = (u % nblk) / J.nib, ib = u % J.nib;
-  const int o = ob * 32 + (lane & 31), i = ib * 32 + (lane & 31);
-  const bool ok_o = o < J.O, ok_i = i < J.I;
-  const long long rb = (long long)chunk * g.chunk + hh;
-  const float* zp = J.dz + rb * J.ldz + (ok_o ? o : 0);
-  const float* hp = J.h + rb * J.ldh + (ok_i ? i : 0);
-  const long long zs = 2LL * J.ldz, hs = 2LL * J.ldh;
-  f32x16 acc;
+  const int tid = threadIdx.x, w = tid >> 6, lane = tid & 63, hh = lane >> 5;
+  const int o = w * 32 + (lane & 31);
+  const bool active = w * 32 < J.O;
+  const int nib = (J.I + 31) / 32;
+  const long long row0 = (long long)chunk * g.chunk;
+  const int nslab = g.chunk / SLAB;
+  // loader: thread tid fills columns c = tid & 127 of rows (tid >> 7) + 2i
+  const int lc = tid & 127, lr = tid >> 7;
+  const bool lz = lc < J.O, lh = lc < J.I;
+  float rz[SLAB / 2], rh[SLAB / 2];
+  auto load = [&](int slab) {
+    const long long rb = row0 + (long long)slab * SLAB + lr;
 #pragma unroll
-  for (int r = 0; r < 16; r++) acc[r] = 0.f;
-  float a[PF], b[PF];
-#pragma unroll
-  for (int s = 0; s < PF; s++) { a[s] = zp[s * zs]; b[s] = hp[s * hs]; }
-  const int steps = g.chunk / 2;
-  for (int s0 = 0; s0 < steps; s0 += PF) {
-    float an[PF], bn[PF];
-    const bool more = s0 + PF < steps;
-#pragma unroll
-    for (int s = 0; s < PF; s++) {
-      an[s] = more ? zp[(s0 + PF + s) * zs] : 0.f;
-      bn[s] = more ? hp[(s0 + PF + s) * hs] : 0.f;
+    for (int i = 0; i < SLAB / 2; i++) {
+      rz[i] = lz ? J.dz[(rb + 2 * i) * J.ldz + lc] : 0.f;
+      rh[i] = lh ? J.h[(rb + 2 * i) * J.ldh + lc] : 0.f;
     }
+  };
+  auto stash = [&](int buf) {
 #pragma unroll
-    for (int s = 0; s < PF; s++) acc = mfma(ok_o ? a[s] : 0.f, ok_i ? b[s] : 0.f, acc);
+    for (int i = 0; i < SLAB / 2; i++) {
+      za[buf][lr + 2 * i][lc] = rz[i];
+      hb[buf][lr + 2 * i][lc] = rh[i];
+    }
+  };
+  f32x16 acc[4];
 #pragma unroll
-    for (int s = 0; s < PF; s++) { a[s] = an[s]; b[s] = bn[s]; }
+  for (int q = 0; q < 4; q++)
+#pragma unroll
+    for (int r = 0; r < 16; r++) acc[q][r] = 0.f;
+  float bsum = 0.f;
+  load(0);
+  stash(0);
+  __syncthreads();
+  for (int sl = 0; sl < nslab; sl++) {
+    const int buf = sl & 1;
+    if (sl + 1 < nslab) load(sl + 1);
+    if (active) {
+#pragma unroll
+      for (int st = 0; st < SLAB / 2; st++) {
+        const int r = 2 * st + hh;
+        const float a = za[buf][r][o];
+        bsum += a;
+#pragma unroll
+        for (int q = 0; q < 4; q++)
+          if (q < nib) acc[q] = mfma(a, hb[buf][r][q * 32 + (lane & 31)], acc[q]);
+      }
+    }
+    if (sl + 1 < nslab) stash(buf ^ 1);
+    __syncthreads();
   }
-  if (!ok_i) return;
+  if (!active) return;
+  const bool ok_o = o < J.O;
+  bsum += __shfl_xor(bsum, 32, 64);
+  if (hh == 0 && ok_o) J.bpart[(long long)chunk * J.O + o] = bsum;
 #pragma unroll
-  for (int r = 0; r < 16; r++) {
-    const int oo = ob * 32 + crow(r, lane);
-    if (oo < J.O) J.part[((long long)chunk * J.O + oo) * J.I + i] = acc[r];
+  for (int q = 0; q < 4; q++) {
+    const int i = q * 32 + (lane & 31);
+    if (q >= nib || i >= J.I) continue;
+#pragma unroll
+    for (int r = 0; r < 16; r++) {
+      const int oo = w * 32 + crow(r, lane);
+      if (oo < J.O) J.wpart[((long long)chunk * J.O + oo) * J.I + i] = acc[q][r];
+    }
   }
 }
 
-// ---------------- gradient assembly, norm partials, log row, counters
+// ---------------- gradient assembly, norm partials, log_std, log row, counters
 struct Seg {
-  const float* src;  // partials: element e of partial c at src[c * stride + e]
-  int n, count, stride, dst, first;
-  float add;
+  const float* src;  // chunk partials: element e of chunk c at src[c * n + e]
+  int n, dst, first;
 };
 struct ReduceArgs {
   Seg seg[NSEG];
-  int total;
+  int total, nch;
   float* grad;
   float* npart;
   const float* lpart;
-  int ntiles, B;
+  int ntiles, B, off_ls;
   const float* ls;
   float ent_coef, vf_coef;
   float* log;
@@ -448,8 +521,23 @@ struct ReduceArgs {
 };
 
 __global__ __launch_bounds__(256) void mlp_reduce_kernel(ReduceArgs a) {
-  __shared__ float red[4][4];
+  __shared__ float red[4];
+  __shared__ float tsum[8];
   const int e = blockIdx.x * 256 + threadIdx.x, lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  if (blockIdx.x == 0) {  // loss partials over the tiles: wave w sums q = w and q = w + 4
+    float v0 = 0.f, v1 = 0.f;
+    for (int t = lane; t < a.ntiles; t += 64) {
+      v0 += a.lpart[(long long)t * LPART + wid];
+      v1 += a.lpart[(long long)t * LPART + wid + 4];
+    }
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) {
+      v0 += __shfl_xor(v0, off, 64);
+      v1 += __shfl_xor(v1, off, 64);
+    }
+    if (lane == 0) { tsum[wid] = v0; tsum[wid + 4] = v1; }
+    __syncthreads();
+  }
   float g2 = 0.f;
   if (e < a.total) {
     int q = 0;
@@ -458,40 +546,38 @@ __global__ __launch_bounds__(256) void mlp_reduce_kernel(ReduceArgs a) {
     const Seg S = a.seg[q];
     const int el = e - S.first;
     float s = 0.f;
-    for (int c = 0; c < S.count; c++) s += S.src[(long long)c * S.stride + el];
-    s += S.add;
+    for (int c = 0; c < a.nch; c++) s += S.src[(long long)c * S.n + el];
     a.grad[S.dst + el] = s;
     g2 = s * s;
   }
+  if (blockIdx.x == 0 && threadIdx.x == 0) {  // d loss / d log_std_j = sum glp (z^2 - 1) - ent_coef
+#pragma unroll
+    for (int j = 0; j < 3; j++) {
+      const float gl = tsum[4 + j] - a.ent_coef;
+      a.grad[a.off_ls + j] = gl;
+      g2 += gl * gl;
+    }
+  }
 #pragma unroll
   for (int off = 32; off > 0; off >>= 1) g2 += __shfl_xor(g2, off, 64);
-  if (lane == 0) red[0][wid] = g2;
+  if (lane == 0) red[wid] = g2;
   __syncthreads();
-  if (threadIdx.x == 0) a.npart[blockIdx.x] = (red[0][0] + red[0][1]) + (red[0][2] + red[0][3]);
+  if (threadIdx.x != 0) return;
+  a.npart[blockIdx.x] = (red[0] + red[1]) + (red[2] + red[3]);
   if (blockIdx.x != 0) return;
-  // log row: wave q < 4 sums loss partial q over the tiles
-  float v = 0.f;
-  for (int t = lane; t < a.ntiles; t += 64) v += a.lpart[(long long)t * LPART + wid];
-#pragma unroll
-  for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off, 64);
-  __syncthreads();
-  if (lane == 0) red[1][wid] = v;
-  __syncthreads();
-  if (threadIdx.x == 0) {
-    const float invB = 1.f / float(a.B);
-    const float pg = red[1][0] * invB, vf = red[1][1] * invB;
-    const float ent = -(3.f * (0.5f + HALF_LOG_2PI) + a.ls[0] + a.ls[1] + a.ls[2]);
-    const long long row = *a.row_counter;
-    float* L = a.log + row * 6;
-    L[0] = pg + a.ent_coef * ent + a.vf_coef * vf;
-    L[1] = pg;
-    L[2] = vf;
-    L[3] = ent;
-    L[4] = red[1][2] * invB;
-    L[5] = red[1][3] * invB;
-    *a.row_counter = row + 1;
-    *a.mb_counter = *a.mb_counter + 1;
-  }
+  const float invB = 1.f / float(a.B);
+  const float pg = tsum[0] * invB, vf = tsum[1] * invB;
+  const float ent = -(3.f * (0.5f + HALF_LOG_2PI) + a.ls[0] + a.ls[1] + a.ls[2]);
+  const long long row = *a.row_counter;
+  float* L = a.log + row * 6;
+  L[0] = pg + a.ent_coef * ent + a.vf_coef * vf;
+  L[1] = pg;
+  L[2] = vf;
+  L[3] = ent;
+  L[4] = tsum[2] * invB;
+  L[5] = tsum[3] * invB;
+  *a.row_counter = row + 1;
+  *a.mb_counter = *a.mb_counter + 1;
 }
 
 }  // namespace
@@ -504,10 +590,10 @@ long long mlp_workspace_bytes(int B) {
 
 int launch_mlp_step(const MlpStepArgs& A, hipStream_t s) {
   const int B = A.B;
-  if (B < 256 || B % ROWS || (B / NCH) % (2 * PF)) return -2;
+  if (B < 256 || B % 256 || B > 16384) return -2;
   if (A.ws_bytes < mlp_workspace_bytes(B)) return -3;
   const Workspace w = carve(A.ws, B, nullptr);
-  const int ntiles = B / ROWS;
+  const int ntiles = B / ROWS, nch = n_chunks(B);
 
   TileArgs t;
   t.P = A.params;
@@ -515,52 +601,41 @@ int launch_mlp_step(const MlpStepArgs& A, hipStream_t s) {
   t.obs = A.obs; t.actions = A.actions; t.old_logp = A.old_logp; t.adv = A.adv; t.returns = A.returns;
   t.perm = A.perm; t.mb_counter = A.mb_counter; t.clip = A.clip;
   t.B = B; t.normalize = A.normalize; t.vf_coef = A.vf_coef; t.w = w;
-  hipLaunchKernelGGL(mlp_tile_kernel, dim3(ntiles), dim3(T1), 0, s, t);
+  t.n = 0; t.noise = nullptr; t.obs_copy = t.act_out = t.act_clipped = t.values_out = t.logp_out = nullptr;
+  hipLaunchKernelGGL(mlp_tile_kernel<true>, dim3(ntiles), dim3(T1), 0, s, t);
 
-  // weight-gradient jobs, in flat-gradient segment order
+  // weight/bias-gradient jobs, in flat-gradient segment order
   GemmArgs g;
-  int nunits = 0, nj = 0;
-  auto add_job = [&](const float* dz, int ldz, int O, const float* h, int ldh, int I, float* part) {
-    GemmJob& J = g.job[nj++];
-    J.dz = dz; J.ldz = ldz; J.O = O; J.h = h; J.ldh = ldh; J.I = I; J.part = part;
-    J.nob = (O + 31) / 32; J.nib = (I + 31) / 32; J.first = nunits;
-    nunits += J.nob * J.nib * NCH;
-  };
-  float* wp = w.wpart;
-  const float* wbase[NJOB];
-  int wsize[NJOB], wdst[NJOB];
-  for (int tr = 0; tr < 2; tr++)
-    for (int l = 0; l < 4; l++) {
-      const int I = l ? HID : IN;
-      wbase[nj] = wp; wsize[nj] = HID * I; wdst[nj] = A.off[(tr ? MLP_VF_W0 : MLP_PI_W0) + l];
-      add_job(w.dz[tr][l], HID, HID, l ? w.h[tr][l - 1] : w.x, l ? HID : XW, I, wp);
-      wp += (long long)NCH * HID * I;
-    }
-  wbase[nj] = wp; wsize[nj] = 3 * HID; wdst[nj] = A.off[MLP_WA];
-  add_job(w.dhead, 4, 3, w.h[0][3], HID, HID, wp);
-  wp += (long long)NCH * 3 * HID;
-  wbase[nj] = wp; wsize[nj] = HID; wdst[nj] = A.off[MLP_WV];
-  add_job(w.dhead + 3, 4, 1, w.h[1][3], HID, HID, wp);
-  g.nunits = nunits;
-  g.chunk = B / NCH;
-  hipLaunchKernelGGL(mlp_dw_kernel, dim3((nunits + 3) / 4), dim3(256), 0, s, g);
-
   ReduceArgs r;
-  int total = 0, ns = 0;
-  auto add_seg = [&](const float* src, int n, int count, int stride, int dst, float add) {
-    Seg& S = r.seg[ns++];
-    S.src = src; S.n = n; S.count = count; S.stride = stride; S.dst = dst; S.first = total; S.add = add;
-    total += n;
+  int nj = 0, ns = 0, total = 0;
+  float* wp = w.wpart;
+  float* bp = w.bpart;
+  auto add_job = [&](const float* dz, int ldz, int O, const float* h, int ldh, int I, int wdst, int bdst) {
+    GemmJob& J = g.job[nj++];
+    J.dz = dz; J.ldz = ldz; J.O = O; J.h = h; J.ldh = ldh; J.I = I; J.wpart = wp; J.bpart = bp;
+    Seg& SW = r.seg[ns++];
+    SW.src = wp; SW.n = O * I; SW.dst = wdst; SW.first = total; total += O * I;
+    Seg& SB = r.seg[ns++];
+    SB.src = bp; SB.n = O; SB.dst = bdst; SB.first = total; total += O;
+    wp += (long long)nch * O * I;
+    bp += (long long)nch * O;
   };
-  for (int j = 0; j < NJOB; j++) add_seg(wbase[j], wsize[j], NCH, wsize[j], wdst[j], 0.f);
   for (int tr = 0; tr < 2; tr++)
     for (int l = 0; l < 4; l++)
-      add_seg(w.bpart + tr * 4 * HID + l * HID, HID, ntiles, BPART, A.off[(tr ? MLP_VF_B0 : MLP_PI_B0) + l], 0.f);
-  add_seg(w.bpart + 2 * 4 * HID, 3, ntiles, BPART, A.off[MLP_BA], 0.f);
-  add_seg(w.bpart + 2 * 4 * HID + 3, 1, ntiles, BPART, A.off[MLP_BV], 0.f);
-  add_seg(w.lpart + 4, 3, ntiles, LPART, A.off[MLP_LS], -A.ent_coef);
-  r.total = total;
-  r.grad = A.grad; r.npart = w.npart; r.lpart = w.lpart; r.ntiles = ntiles; r.B = B;
+      add_job(w.dz[tr][l], HID, HID, l ? w.h[tr][l - 1] : w.x, l ? HID : XW, l ? HID : IN,
+              A.off[(tr ? MLP_VF_W0 : MLP_PI_W0) + l], A.off[(tr ? MLP_VF_B0 : MLP_PI_B0) + l]);
+  add_job(w.dhead, 4, 3, w.h[0][3], HID, HID, A.off[MLP_WA], A.off[MLP_BA]);
+  add_job(w.dhead + 3, 4, 1, w.h[1][3], HID, HID, A.off[MLP_WV], A.off[MLP_BV]);
+  {  // grid order: the six 128x128 layers, then the input layers and the heads
+    const int order[NJOB] = {1, 2, 3, 5, 6, 7, 0, 4, 8, 9};
+    for (int q = 0; q < NJOB; q++) g.order[q] = order[q];
+  }
+  g.nch = nch;
+  g.chunk = B / nch;
+  hipLaunchKernelGGL(mlp_dw_kernel, dim3(NJOB * nch), dim3(256), 0, s, g);
+
+  r.total = total; r.nch = nch;
+  r.grad = A.grad; r.npart = w.npart; r.lpart = w.lpart; r.ntiles = ntiles; r.B = B; r.off_ls = A.off[MLP_LS];
   r.ls = A.params + A.off[MLP_LS]; r.ent_coef = A.ent_coef; r.vf_coef = A.vf_coef; r.log = A.log;
   r.mb_counter = A.mb_counter; r.row_counter = A.row_counter;
   const int nred = (total + 255) / 256;
@@ -571,6 +646,17 @@ int launch_mlp_step(const MlpStepArgs& A, hipStream_t s) {
               A.weight_decay, float(A.beta2), float(1.0 - A.beta1), float(1.0 - A.beta2), float(A.eps),
               float(A.max_norm), w.npart, nred};
   if (launch_adamw_clip(o, s)) return -1;
+  return hipGetLastError() == hipSuccess ? 0 : -1;
+}
+
+int launch_mlp_act(const MlpActArgs& A, hipStream_t s) {
+  if (A.n <= 0) return 0;
+  TileArgs t{};
+  t.P = A.params;
+  for (int i = 0; i < MLP_NSLOTS; i++) t.off[i] = A.off[i];
+  t.obs = A.obs; t.n = A.n; t.noise = A.noise; t.obs_copy = A.obs_copy; t.act_out = A.actions;
+  t.act_clipped = A.clipped; t.values_out = A.values; t.logp_out = A.log_prob;
+  hipLaunchKernelGGL(mlp_tile_kernel<false>, dim3((A.n + ROWS - 1) / ROWS), dim3(T1), 0, s, t);
   return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 

@@ -10,4 +10,9 @@ int launch_gae(const float* rew, const float* val, const uint8_t* start, const f
                const uint8_t* last_done, int T, int N, double gamma, double lam, float* adv, float* ret,
                hipStream_t s);
 
+// one rollout step's episode bookkeeping (SB3 collect_rollouts + Monitor)
+int launch_track(const float* reward, const uint8_t* flags, int mask, int n, float* rewards_out, double* ep_ret,
+                 long long* ep_len, double* ep_r_out, long long* ep_l_out, uint8_t* starts, uint8_t* starts_next,
+                 hipStream_t s);
+
 }  // namespace bb

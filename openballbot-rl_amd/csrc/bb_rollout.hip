@@ -45,7 +45,41 @@ __global__ __launch_bounds__(256) void gae_kernel(const float* __restrict__ rew,
   }
 }
 
+// Episode bookkeeping of one rollout step (SB3 OnPolicyAlgorithm.collect_rollouts
+// + Monitor): store the reward, accumulate the per-env return (float64, as
+// Monitor sums Python floats) and length, record finished episodes (return,
+// length; NaN / 0 elsewhere) and restart the counters, and publish
+// episode_starts for the next step.  done = (flags & mask) != 0.
+__global__ __launch_bounds__(256) void track_kernel(const float* __restrict__ reward, const uint8_t* __restrict__ flags,
+                                                    int mask, int n, float* __restrict__ rewards_out,
+                                                    double* __restrict__ ep_ret, long long* __restrict__ ep_len,
+                                                    double* __restrict__ ep_r_out, long long* __restrict__ ep_l_out,
+                                                    uint8_t* __restrict__ starts, uint8_t* __restrict__ starts_next) {
+  const int e = blockIdx.x * blockDim.x + threadIdx.x;
+  if (e >= n) return;
+  const float r = reward[e];
+  const bool done = (flags[e] & mask) != 0;
+  rewards_out[e] = r;
+  const double ret = ep_ret[e] + double(r);
+  const long long len = ep_len[e] + 1;
+  ep_r_out[e] = done ? ret : __builtin_nan("");
+  ep_l_out[e] = done ? len : 0;
+  ep_ret[e] = done ? 0.0 : ret;
+  ep_len[e] = done ? 0 : len;
+  starts[e] = done ? 1 : 0;
+  if (starts_next) starts_next[e] = done ? 1 : 0;
+}
+
 }  // namespace
+
+int launch_track(const float* reward, const uint8_t* flags, int mask, int n, float* rewards_out, double* ep_ret,
+                 long long* ep_len, double* ep_r_out, long long* ep_l_out, uint8_t* starts, uint8_t* starts_next,
+                 hipStream_t s) {
+  if (n <= 0) return 0;
+  hipLaunchKernelGGL(track_kernel, dim3((n + 255) / 256), dim3(256), 0, s, reward, flags, mask, n, rewards_out, ep_ret,
+                     ep_len, ep_r_out, ep_l_out, starts, starts_next);
+  return hipGetLastError() == hipSuccess ? 0 : -1;
+}
 
 int launch_gae(const float* rew, const float* val, const uint8_t* start, const float* last_val,
                const uint8_t* last_done, int T, int N, double gamma, double lam, float* adv, float* ret,

@@ -75,8 +75,10 @@ def test_train_main_end_to_end(tmp_path):
 
 
 @pytest.mark.parametrize("target_kl", [None, 2e-4])
-def test_graph_update_matches_eager(target_kl):
-    """The graph-replayed update (device-side KL stop) == the eager SB3 update on the same rollout."""
+def test_graph_update_matches_eager(target_kl, monkeypatch):
+    """The graph-replayed update (device-side KL stop) == the eager SB3 update on the same rollout
+    (autograd minibatches on both sides; the fused minibatch has its own tests below)."""
+    monkeypatch.setenv("BB_PPO_FUSED", "0")
     from fake_env import FakeEnv
     from ballbot_rl.training.logger import CSVLogger
     from ballbot_rl.training.ppo import BatchedPPO
@@ -413,3 +415,61 @@ def test_ppo_mlp_step_rejects_bad_arguments():
     a = N.PPOMlpArgs()
     assert L.bb_ppo_mlp_step(C.byref(a), None) < 0
     assert "NULL" in N.last_error()
+
+
+def test_fused_rollout_matches_torch(monkeypatch):
+    """collect_rollouts with bb_ppo_mlp_act + bb_rollout_track vs the torch loop:
+    same noise, same env stream -> the same buffers (fp32 reduction-order
+    tolerance for the network outputs) and the same finished episodes."""
+    from ballbot_rl.training.logger import CSVLogger
+    from ballbot_rl.training.ppo import BatchedPPO
+
+    models = []
+    for fused in ("0", "1"):
+        monkeypatch.setenv("BB_PPO_FUSED", fused)
+        m = BatchedPPO(_gpu_fake(n=300, ep_len=5), n_steps=12, batch_size=256, n_epochs=1, seed=7,
+                       logger=CSVLogger(None, stdout=False))
+        for _ in range(2):
+            m.collect_rollouts()
+        models.append(m)
+    assert models[0]._act_slots is False and models[1]._act_slots
+    a, b = models[0].buf, models[1].buf
+    assert torch.equal(a.obs, b.obs) and torch.equal(a.starts, b.starts)
+    assert torch.allclose(a.actions, b.actions, rtol=1e-5, atol=1e-5), (a.actions - b.actions).abs().max()
+    assert torch.allclose(a.values, b.values, rtol=1e-4, atol=1e-5), (a.values - b.values).abs().max()
+    assert torch.allclose(a.log_probs, b.log_probs, rtol=1e-4, atol=1e-4), (a.log_probs - b.log_probs).abs().max()
+    assert torch.allclose(a.rewards, b.rewards, rtol=1e-4, atol=1e-5)
+    assert torch.allclose(a.advantages, b.advantages, rtol=1e-3, atol=1e-4)
+    ea, eb = list(models[0].ep_info_buffer), list(models[1].ep_info_buffer)
+    assert len(ea) == len(eb) > 0
+    assert [e["l"] for e in ea] == [e["l"] for e in eb]
+    assert np.allclose([e["r"] for e in ea], [e["r"] for e in eb], rtol=1e-4, atol=1e-4)
+    assert models[0].num_timesteps == models[1].num_timesteps
+
+
+def test_fused_act_deterministic_is_the_mean():
+    """bb_ppo_mlp_act with noise NULL: actions = the policy mean (predict(deterministic=True) before the clip)."""
+    import ctypes as C
+
+    from ballbot_gym import _native as N
+    from ballbot_rl.training.logger import CSVLogger
+    from ballbot_rl.training.ppo import BatchedPPO, fused_mlp_slots
+
+    m = BatchedPPO(_gpu_fake(n=100), n_steps=4, batch_size=256, seed=2, logger=CSVLogger(None, stdout=False))
+    slots = fused_mlp_slots(m, update=False)
+    assert slots is not None
+    dev = m.device
+    obs = torch.randn(77, 15, device=dev)
+    act = torch.empty(77, 3, device=dev); val = torch.empty(77, device=dev); lp = torch.empty(77, device=dev)
+    clipped = torch.empty(77, 3, device=dev)
+    ptr = lambda t: C.c_void_p(t.data_ptr())  # noqa: E731
+    N.check(N.lib().bb_ppo_mlp_act(ptr(m.optimizer.flat), (C.c_int32 * 21)(*slots), ptr(obs), None, 77, None, ptr(act),
+                                   ptr(clipped), ptr(val), ptr(lp), None), "bb_ppo_mlp_act")
+    torch.cuda.synchronize()
+    with torch.no_grad():
+        mean, v = m.policy._heads(obs)
+        want_lp = m.policy.log_prob(mean, mean)
+    assert torch.allclose(act, mean, rtol=1e-5, atol=1e-6)
+    assert torch.equal(clipped, act.clamp(-1, 1))
+    assert torch.allclose(val, v, rtol=1e-5, atol=1e-5)
+    assert torch.allclose(lp, want_lp, rtol=1e-6, atol=1e-5)
