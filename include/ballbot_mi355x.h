@@ -19,6 +19,7 @@
  *                    AdamW) of the reference's proprio MLP policy, fused
  *   bb_ppo_mlp_act   SB3 collect_rollouts policy step (same policy)
  *   bb_rollout_track SB3 collect_rollouts / Monitor episode bookkeeping
+ *   bb_depth_encoder frozen rgbd encoder of the camera policy, fused
  *   bb_gae           SB3 RolloutBuffer.compute_returns_and_advantage (PPO)
  *   bb_forward       mujoco.mj_forward (diagnostic)             ballbot_env.py:525,620
  *   bb_get_state/    read/write qpos/qvel/qacc_warmstart        ballbot_env.py:616-617
@@ -218,6 +219,34 @@ int bb_ppo_mlp_act(const float* params_dev, const int32_t* offsets, const float*
 int bb_rollout_track(const float* reward_dev, const uint8_t* flags_dev, int done_mask, int n, float* rewards_out_dev,
                      double* ep_ret_dev, int64_t* ep_len_dev, double* ep_r_out_dev, int64_t* ep_l_out_dev,
                      uint8_t* starts_dev, uint8_t* starts_next_dev, void* stream);
+/* The camera policy's frozen depth encoder (the reference's rgbd branch with a
+ * pretrained encoder: Conv2d(1,32,3,s2,p1) BatchNorm2d LeakyReLU, Conv2d(32,32,3,
+ * s2,p1) BatchNorm2d LeakyReLU, Flatten, Linear(8192,20) BatchNorm1d Tanh;
+ * ballbot_rl/encoders/models.py:6-54 as loaded by policies/mlp_policy.py:51-125)
+ * over n 64x64 depth images (image i at images_dev + i * image_stride floats,
+ * 16-byte aligned).  train != 0: the BatchNorms normalise with the batch's
+ * statistics and update their running statistics and num_batches_tracked
+ * (torch train mode, as SB3's policy.train() leaves them during PPO updates);
+ * train == 0: the running statistics normalise (eval mode, the rollout).
+ * Writes features row i at out_dev + i * out_stride (20 floats).  The pointers
+ * in bb_encoder_params are the module's device tensors (running statistics and
+ * counters are written in train mode; counters may be NULL).  Six launches on
+ * stream; graph-capturable. */
+typedef struct bb_encoder_params {
+  const float *conv1_w, *conv1_b, *bn1_w, *bn1_b;
+  float *bn1_mean, *bn1_var;
+  int64_t* bn1_count;
+  const float *conv2_w, *conv2_b, *bn2_w, *bn2_b;
+  float *bn2_mean, *bn2_var;
+  int64_t* bn2_count;
+  const float *fc_w, *fc_b, *bn3_w, *bn3_b;
+  float *bn3_mean, *bn3_var;
+  int64_t* bn3_count;
+} bb_encoder_params;
+int bb_depth_encoder_workspace_bytes(int64_t n, int64_t* bytes);
+int bb_depth_encoder(const bb_encoder_params* params, const float* images_dev, int64_t image_stride, int64_t n,
+                     int height, int width, int train, float momentum, float eps, float* out_dev, int64_t out_stride,
+                     float* workspace_dev, int64_t workspace_bytes, void* stream);
 /* copy terrain bank slot terrain_id (float32[293*293]) to host memory */
 int bb_get_hfield(bb_handle* h, int terrain_id, float* data_host);
 /* per-env terrain ids (device int32[n]) applied at the next reset */

@@ -71,12 +71,22 @@ class PPOMlpArgs(C.Structure):
     ]
 
 
+ENCODER_FIELDS = ("conv1_w", "conv1_b", "bn1_w", "bn1_b", "bn1_mean", "bn1_var", "bn1_count",
+                  "conv2_w", "conv2_b", "bn2_w", "bn2_b", "bn2_mean", "bn2_var", "bn2_count",
+                  "fc_w", "fc_b", "bn3_w", "bn3_b", "bn3_mean", "bn3_var", "bn3_count")
+
+
+class EncoderParams(C.Structure):
+    """bb_encoder_params (include/ballbot_mi355x.h): device pointers of the encoder's tensors."""
+    _fields_ = [(name, C.c_void_p) for name in ENCODER_FIELDS]
+
+
 EXPORTS = [
     "bb_abi_version", "bb_last_error", "bb_default_params", "bb_create", "bb_destroy", "bb_set_hfield",
     "bb_assign_terrain", "bb_reset", "bb_step", "bb_get_state", "bb_set_state", "bb_forward", "bb_get_stats",
     "bb_get_offsets", "bb_get_config", "bb_time_kernel", "bb_kernel_ms", "bb_generate_perlin", "bb_get_hfield",
     "bb_gae", "bb_render_depth", "bb_ppo_loss", "bb_adamw_clip", "bb_ppo_mlp_workspace_bytes", "bb_ppo_mlp_step",
-    "bb_ppo_mlp_act", "bb_rollout_track",
+    "bb_ppo_mlp_act", "bb_rollout_track", "bb_depth_encoder_workspace_bytes", "bb_depth_encoder",
 ]
 
 ABI_VERSION = 9  # include/ballbot_mi355x.h BB_ABI_VERSION
@@ -85,7 +95,7 @@ _lib = None
 
 
 def build(force: bool = False, verbose: bool = False) -> Path:
-    """Compile csrc/bb_kernels.hip + bb_terrain.hip + bb_rollout.hip + bb_render.hip + bb_ppo.hip + bb_mlp.hip for gfx950 into _lib/libbb_mi355x.so."""
+    """Compile csrc/bb_kernels.hip + bb_terrain.hip + bb_rollout.hip + bb_render.hip + bb_ppo.hip + bb_mlp.hip + bb_encoder.hip for gfx950 into _lib/libbb_mi355x.so."""
     import subprocess
 
     srcs = list(CSRC.glob("*.h")) + list(CSRC.glob("*.hip")) + list(INCLUDE.glob("*.h"))
@@ -96,7 +106,7 @@ def build(force: bool = False, verbose: bool = False) -> Path:
     cmd = ["hipcc", "--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC", "-shared",
            "-o", str(tmp), str(CSRC / "bb_kernels.hip"), str(CSRC / "bb_terrain.hip"),
            str(CSRC / "bb_rollout.hip"), str(CSRC / "bb_render.hip"),
-           str(CSRC / "bb_ppo.hip"), str(CSRC / "bb_mlp.hip")]
+           str(CSRC / "bb_ppo.hip"), str(CSRC / "bb_mlp.hip"), str(CSRC / "bb_encoder.hip")]
     if verbose:
         print(" ".join(cmd))
     subprocess.run(cmd, check=True)
@@ -154,6 +164,9 @@ def _load(path: Path):
     L.bb_ppo_mlp_step.argtypes = [C.POINTER(PPOMlpArgs), vp]
     L.bb_ppo_mlp_act.argtypes = [vp, C.POINTER(C.c_int32), vp, vp, C.c_int, vp, vp, vp, vp, vp, vp]
     L.bb_rollout_track.argtypes = [vp, vp, C.c_int, C.c_int] + [vp] * 8
+    L.bb_depth_encoder_workspace_bytes.argtypes = [C.c_int64, C.POINTER(C.c_int64)]
+    L.bb_depth_encoder.argtypes = [C.POINTER(EncoderParams), vp, C.c_int64, C.c_int64, C.c_int, C.c_int, C.c_int,
+                                   C.c_float, C.c_float, vp, C.c_int64, vp, C.c_int64, vp]
     L.bb_kernel_ms.argtypes = [vp, C.POINTER(C.c_double), C.POINTER(C.c_int32)]
     for name in [n for n in EXPORTS if n not in ("bb_default_params", "bb_abi_version")]:
         getattr(L, name).restype = C.c_int

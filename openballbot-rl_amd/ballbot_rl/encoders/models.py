@@ -66,3 +66,58 @@ def load_frozen_encoder(path: str, device="cpu") -> nn.Sequential:
     for p in enc.parameters():
         p.requires_grad = False
     return enc.to(device).eval()
+
+
+def fusable_encoder(enc: nn.Module) -> bool:
+    """True when `enc` is the reference's frozen rgbd encoder layout (the encoder of
+    TinyAutoencoder(64, 64): conv 1->32, BN, LeakyReLU(0.01), conv 32->32, BN,
+    LeakyReLU, Flatten, Linear(8192 -> 20), BN1d, Tanh) with frozen fp32 weights
+    and one BatchNorm momentum/eps, i.e. what bb_depth_encoder computes."""
+    m = list(enc) if isinstance(enc, nn.Sequential) else []
+    kinds = (nn.Conv2d, nn.BatchNorm2d, nn.LeakyReLU, nn.Conv2d, nn.BatchNorm2d, nn.LeakyReLU, nn.Flatten, nn.Linear,
+             nn.BatchNorm1d, nn.Tanh)
+    if len(m) != len(kinds) or any(type(x) is not k for x, k in zip(m, kinds)):
+        return False
+    c1, b1, a1, c2, b2, a2, _, fc, b3, _ = m
+    conv_ok = all(c.bias is not None and c.kernel_size == (3, 3) and c.stride == (2, 2) and c.padding == (1, 1)
+                  and c.dilation == (1, 1) and c.groups == 1 for c in (c1, c2))
+    shapes_ok = (c1.in_channels, c1.out_channels, c2.in_channels, c2.out_channels) == (1, 32, 32, 32) and \
+        (fc.in_features, fc.out_features) == (8192, 20) and fc.bias is not None
+    bns = (b1, b2, b3)
+    bn_ok = all(b.affine and b.track_running_stats and b.momentum is not None for b in bns) and \
+        len({(float(b.momentum), float(b.eps)) for b in bns}) == 1 and (b1.num_features, b3.num_features) == (32, 20)
+    act_ok = all(a.negative_slope == 0.01 for a in (a1, a2))
+    frozen = all(not p.requires_grad for p in enc.parameters())
+    dtypes = all(t.dtype == torch.float32 for t in list(enc.parameters()) + [b.running_mean for b in bns])
+    return conv_ok and shapes_ok and bn_ok and act_ok and frozen and dtypes
+
+
+def fused_encoder_forward(enc: nn.Sequential, x: torch.Tensor) -> torch.Tensor:
+    """bb_depth_encoder on x [n, 1, 64, 64] (cuda, fp32; a channel slice of the
+    [n, 2, 64, 64] camera tensor is fine): the frozen encoder's output [n, 20] with
+    torch's BatchNorm semantics for enc.training (train: batch statistics and a
+    running-statistics update; eval: running statistics).  No autograd graph."""
+    import ctypes as C
+
+    from ballbot_gym import _native as N
+
+    c1, b1, _, c2, b2, _, _, fc, b3, _ = list(enc)
+    n = x.shape[0]
+    if x.dim() != 4 or tuple(x.shape[1:]) != (1, 64, 64) or x.stride(3) != 1 or x.stride(2) != 64 \
+            or x.stride(0) % 4 or x.data_ptr() % 16 or x.dtype != torch.float32:
+        x = x.contiguous()
+    ptr = lambda t: t.data_ptr()  # noqa: E731
+    vals = [c1.weight, c1.bias, b1.weight, b1.bias, b1.running_mean, b1.running_var, b1.num_batches_tracked,
+            c2.weight, c2.bias, b2.weight, b2.bias, b2.running_mean, b2.running_var, b2.num_batches_tracked,
+            fc.weight, fc.bias, b3.weight, b3.bias, b3.running_mean, b3.running_var, b3.num_batches_tracked]
+    p = N.EncoderParams(*[ptr(t.data if isinstance(t, nn.Parameter) else t) for t in vals])
+    nbytes = C.c_int64()
+    L = N.lib()
+    N.check(L.bb_depth_encoder_workspace_bytes(int(n), C.byref(nbytes)), "bb_depth_encoder_workspace_bytes")
+    ws = torch.empty(int(nbytes.value) // 4 + 4, device=x.device)
+    out = torch.empty(n, 20, device=x.device)
+    stream = C.c_void_p(torch.cuda.current_stream(x.device).cuda_stream)
+    N.check(L.bb_depth_encoder(C.byref(p), C.c_void_p(x.data_ptr()), int(x.stride(0)), int(n), 64, 64,
+                               int(bool(enc.training)), float(b1.momentum), float(b1.eps), C.c_void_p(out.data_ptr()),
+                               20, C.c_void_p(ws.data_ptr()), int(nbytes.value), stream), "bb_depth_encoder")
+    return out

@@ -80,13 +80,26 @@ class Extractor(nn.Module):
         self.keys = list(observation_space.keys())
         self.features_dim = total
         self._proprio_only = all(k in PROPRIO_KEYS for k in self.keys)
+        # frozen encoders of the reference's layout run as bb_depth_encoder on the GPU
+        self._frozen_keys = set()
+        if frozen_encoder is not None:
+            from ballbot_rl.encoders.models import fusable_encoder
+
+            self._frozen_keys = {k for k in self.keys if "rgbd_" in k and fusable_encoder(ex[k])}
 
     def forward(self, observations: Obs) -> torch.Tensor:
         if isinstance(observations, torch.Tensor):
             if not self._proprio_only:
                 raise ValueError("a packed observation tensor only carries the proprio keys")
             return observations.reshape(observations.shape[0], -1)
-        return torch.cat([self.extractors[k](observations[k]) for k in self.keys], dim=1)
+        return torch.cat([self._extract(k, observations[k]) for k in self.keys], dim=1)
+
+    def _extract(self, key: str, x: torch.Tensor) -> torch.Tensor:
+        if key in self._frozen_keys and x.is_cuda and os.environ.get("BB_FUSED_ENCODER", "1") != "0":
+            from ballbot_rl.encoders.models import fused_encoder_forward
+
+            return fused_encoder_forward(self.extractors[key], x)
+        return self.extractors[key](x)
 
 
 class _SplitKLinearFn(torch.autograd.Function):

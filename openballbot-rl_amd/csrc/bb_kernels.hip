@@ -26,6 +26,7 @@
 #include "bb_render.h"
 #include "bb_ppo.h"
 #include "bb_mlp.h"
+#include "bb_encoder.h"
 
 using namespace bb;
 
@@ -907,6 +908,40 @@ int bb_rollout_track(const float* reward, const uint8_t* flags, int mask, int n,
   if (launch_track(reward, flags, mask, n, rewards_out, ep_ret, reinterpret_cast<long long*>(ep_len), ep_r_out,
                    reinterpret_cast<long long*>(ep_l_out), starts, starts_next, (hipStream_t)stream))
     return fail("bb_rollout_track: launch failed: %s", hipGetErrorString(hipGetLastError()));
+  return 0;
+}
+
+int bb_depth_encoder_workspace_bytes(int64_t n, int64_t* bytes) {
+  if (!bytes) return fail("bb_depth_encoder_workspace_bytes: NULL argument");
+  if (n < 0) return fail("bb_depth_encoder_workspace_bytes: n must be >= 0");
+  *bytes = encoder_workspace_bytes(n);
+  return 0;
+}
+
+int bb_depth_encoder(const bb_encoder_params* p, const float* images, int64_t image_stride, int64_t n, int height,
+                     int width, int train, float momentum, float eps, float* out, int64_t out_stride, float* ws,
+                     int64_t ws_bytes, void* stream) {
+  if (!p || !images || !out || !ws) return fail("bb_depth_encoder: NULL argument");
+  if (!p->conv1_w || !p->conv1_b || !p->bn1_w || !p->bn1_b || !p->bn1_mean || !p->bn1_var || !p->conv2_w ||
+      !p->conv2_b || !p->bn2_w || !p->bn2_b || !p->bn2_mean || !p->bn2_var || !p->fc_w || !p->fc_b || !p->bn3_w ||
+      !p->bn3_b || !p->bn3_mean || !p->bn3_var)
+    return fail("bb_depth_encoder: NULL parameter pointer");
+  if (height != 64 || width != 64) return fail("bb_depth_encoder: only 64x64 images (got %dx%d)", height, width);
+  if (n < 0 || (train && n < 2)) return fail("bb_depth_encoder: need n >= 2 in train mode (got %lld)", (long long)n);
+  if ((reinterpret_cast<uintptr_t>(images) & 15) || image_stride % 4 || image_stride < 64 * 64)
+    return fail("bb_depth_encoder: images must be 16-byte aligned with a stride of >= 4096 floats, a multiple of 4");
+  if (out_stride < 20) return fail("bb_depth_encoder: out_stride must be >= 20");
+  if (ws_bytes < encoder_workspace_bytes(n))
+    return fail("bb_depth_encoder: workspace of %lld bytes < %lld", (long long)ws_bytes, encoder_workspace_bytes(n));
+  EncArgs a{};
+  a.p = EncParams{p->conv1_w, p->conv1_b, p->bn1_w, p->bn1_b, p->bn1_mean, p->bn1_var,
+                  reinterpret_cast<long long*>(p->bn1_count), p->conv2_w, p->conv2_b, p->bn2_w, p->bn2_b,
+                  p->bn2_mean, p->bn2_var, reinterpret_cast<long long*>(p->bn2_count), p->fc_w, p->fc_b, p->bn3_w,
+                  p->bn3_b, p->bn3_mean, p->bn3_var, reinterpret_cast<long long*>(p->bn3_count)};
+  a.images = images; a.image_stride = image_stride; a.n = n; a.train = train ? 1 : 0;
+  a.momentum = momentum; a.eps = eps; a.out = out; a.out_stride = out_stride;
+  if (launch_encoder(a, ws, (hipStream_t)stream))
+    return fail("bb_depth_encoder: launch failed: %s", hipGetErrorString(hipGetLastError()));
   return 0;
 }
 

@@ -473,3 +473,72 @@ def test_fused_act_deterministic_is_the_mean():
     assert torch.equal(clipped, act.clamp(-1, 1))
     assert torch.allclose(val, v, rtol=1e-5, atol=1e-5)
     assert torch.allclose(lp, want_lp, rtol=1e-6, atol=1e-5)
+
+
+def _random_frozen_encoder(seed=0):
+    from ballbot_rl.encoders import TinyAutoencoder
+
+    g = torch.Generator().manual_seed(seed)
+    enc = TinyAutoencoder(64, 64).encoder
+    with torch.no_grad():
+        for mod in enc:
+            if isinstance(mod, (torch.nn.BatchNorm1d, torch.nn.BatchNorm2d)):
+                nf = mod.num_features
+                mod.weight.copy_(1 + 0.2 * torch.randn(nf, generator=g))
+                mod.bias.copy_(0.1 * torch.randn(nf, generator=g))
+                mod.running_mean.copy_(0.1 * torch.randn(nf, generator=g))
+                mod.running_var.copy_(0.5 + torch.rand(nf, generator=g))
+    for p in enc.parameters():
+        p.requires_grad = False
+    return enc.to("cuda:0")
+
+
+@pytest.mark.parametrize("train", [False, True])
+def test_fused_encoder_matches_torch(train):
+    """bb_depth_encoder vs the torch module (MIOpen convolutions) on a strided camera
+    slice: features, and in train mode the running statistics and counters torch's
+    BatchNorm updates (fp32; reduction orders differ)."""
+    import copy
+
+    from ballbot_rl.encoders.models import fusable_encoder, fused_encoder_forward
+
+    ref = _random_frozen_encoder(3)
+    mine = copy.deepcopy(ref)
+    assert fusable_encoder(mine)
+    ref.train(train); mine.train(train)
+    g = torch.Generator(device="cuda:0").manual_seed(1)
+    cams = torch.rand(300, 2, 64, 64, device="cuda:0", generator=g) * 1.0
+    for cam in (0, 1):
+        x = cams[:, cam:cam + 1]
+        with torch.no_grad():
+            want = ref(x)
+        got = fused_encoder_forward(mine, x)
+        torch.cuda.synchronize()
+        assert got.shape == (300, 20)
+        assert torch.allclose(got, want, rtol=1e-4, atol=2e-4), (got - want).abs().max()
+    for a, b in zip(ref.modules(), mine.modules()):
+        if isinstance(a, (torch.nn.BatchNorm1d, torch.nn.BatchNorm2d)):
+            assert torch.allclose(a.running_mean, b.running_mean, rtol=1e-4, atol=1e-5)
+            assert torch.allclose(a.running_var, b.running_var, rtol=1e-4, atol=1e-5)
+            assert int(a.num_batches_tracked) == int(b.num_batches_tracked) == (2 if train else 0)
+
+
+def test_fused_encoder_in_extractor(monkeypatch):
+    """The camera policy's Extractor with a frozen encoder: fused vs BB_FUSED_ENCODER=0."""
+    from ballbot_rl.policies.mlp_policy import ActorCriticPolicy, obs_spaces
+
+    enc = _random_frozen_encoder(4)
+    pol = ActorCriticPolicy(obs_spaces(cameras=True), frozen_encoder=enc).to("cuda:0")
+    assert pol.features_extractor._frozen_keys == {"rgbd_0", "rgbd_1"}
+    n = 256
+    obs = {k: torch.randn(n, 3, device="cuda:0") for k in ("actions", "angular_vel", "motor_state", "orientation",
+                                                            "vel")}
+    cams = torch.rand(n, 2, 64, 64, device="cuda:0")
+    obs["rgbd_0"], obs["rgbd_1"] = cams[:, 0:1], cams[:, 1:2]
+    obs["relative_image_timestamp"] = torch.rand(n, 1, device="cuda:0") * 0.01
+    pol.eval()
+    with torch.no_grad():
+        fused = pol.features_extractor(obs)
+        monkeypatch.setenv("BB_FUSED_ENCODER", "0")
+        plain = pol.features_extractor(obs)
+    assert torch.allclose(fused, plain, rtol=1e-4, atol=2e-4), (fused - plain).abs().max()
