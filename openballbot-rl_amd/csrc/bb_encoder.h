@@ -18,12 +18,13 @@ struct EncParams {
 };
 
 struct EncWorkspace {
-  double* part1;  // conv1 channel sums per workgroup
+  double* part1;  // conv1 input-window moments per workgroup
   double* part2;  // conv2 channel sums per workgroup
   float* ss1;     // BN1 scale, shift
   float* ss2;     // BN2 scale, shift
   float* out2;    // [n][8192] raw conv2 output
   float* z;       // [n][20] raw linear output
+  double* part3;  // BatchNorm1d sums per 32-image block
 };
 
 struct EncArgs {

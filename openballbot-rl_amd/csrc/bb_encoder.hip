@@ -11,10 +11,11 @@
 // Nothing downstream needs gradients through it.
 //
 // Launches per camera (n images):
-//   train: conv1_stats -> bn_finish(1) -> conv2 -> bn_finish(2) -> linear -> head
-//   eval:                bn_finish(1) -> conv2 -> bn_finish(2) -> linear -> head
-// conv1 is recomputed where it is consumed (9 MACs per output): conv1_stats only
-// accumulates its per-channel sums, conv2 rebuilds 16 channels at a time in LDS.
+//   train: conv1_moments -> bn1_moments -> conv2 -> bn_finish(2) -> linear -> head
+//   eval:                   bn_finish(1) -> conv2 -> bn_finish(2) -> linear -> head
+// conv1 is linear in its 3x3 input window, so its batch statistics come from
+// the windows' 9 means and 45 products (conv1_moments); conv2 recomputes conv1
+// where it consumes it (9 MACs per output), 16 channels at a time in LDS.
 // conv2 is an implicit GEMM on v_mfma_f32_32x32x2_f32 (M = 32 output positions,
 // N = 32 channels, K = 288 taps x channels); the linear layer is a 32-image x
 // 32-output (20 used) MFMA GEMM over K = 8192.  Batch statistics accumulate in
@@ -46,62 +47,110 @@ __device__ __forceinline__ f32x16 mfma(float a, float b, f32x16 c) {
 __device__ __forceinline__ int crow(int reg, int lane) { return (reg & 3) + 8 * (reg >> 2) + 4 * (lane >> 5); }
 __device__ __forceinline__ float leaky(float z) { return z > 0.f ? z : z * SLOPE; }
 
-// conv1 output (pre-BN) at channel oc, position (oy, ox) from the LDS image
-__device__ __forceinline__ float conv1_at(const float (*x)[IW], const float* w1, float b1, int oy, int ox) {
-  float v = b1;
-#pragma unroll
-  for (int ky = 0; ky < 3; ky++) {
-    const int iy = 2 * oy + ky - 1;
-#pragma unroll
-    for (int kx = 0; kx < 3; kx++) {
-      const int ix = 2 * ox + kx - 1;
-      const float xv = (iy >= 0 && ix >= 0) ? x[iy][ix] : 0.f;  // iy, ix <= 63 always
-      v = fmaf(w1[ky * 3 + kx], xv, v);
-    }
-  }
-  return v;
-}
-
 __device__ __forceinline__ void stage_image(float (*x)[IW], const float* img) {
   for (int e = threadIdx.x; e < IH * IW / 4; e += 256)
     reinterpret_cast<float4*>(&x[0][0])[e] = reinterpret_cast<const float4*>(img)[e];
 }
 
-// ---- 1. conv1 batch statistics: one workgroup per 8 images; thread (oc, group)
-__global__ __launch_bounds__(256) void conv1_stats_kernel(EncArgs a) {
-  __shared__ __attribute__((aligned(16))) float x[IH][IW];
-  __shared__ double red[8][C1][2];
-  const int t = threadIdx.x, oc = t & 31, g = t >> 5;
-  float w1[9];
+// the 3x3 stride-2 input window of conv1 output position pos (zero padded)
+__device__ __forceinline__ void window(const float (*x)[IW], int pos, float (&xv)[9]) {
+  const int oy = pos >> 5, ox = pos & 31;
 #pragma unroll
-  for (int k = 0; k < 9; k++) w1[k] = a.p.w1[oc * 9 + k];
-  const float b1 = a.p.b1[oc];
-  double s = 0.0, s2 = 0.0;
-  for (int i = 0; i < 8; i++) {
-    const long long b = (long long)blockIdx.x * 8 + i;
+  for (int ky = 0; ky < 3; ky++)
+#pragma unroll
+    for (int kx = 0; kx < 3; kx++) {
+      const int iy = 2 * oy + ky - 1, ix = 2 * ox + kx - 1;
+      xv[ky * 3 + kx] = (iy >= 0 && ix >= 0) ? x[iy][ix] : 0.f;  // iy, ix <= 63 always
+    }
+}
+
+__device__ __forceinline__ float conv1_win(const float (&xv)[9], const float* w1, float b1) {
+  float v = b1;
+#pragma unroll
+  for (int k = 0; k < 9; k++) v = fmaf(w1[k], xv[k], v);
+  return v;
+}
+
+// ---- 1. conv1 batch statistics from the input windows.  conv1 is linear in its
+// 3x3 window x: v_c = b_c + w_c . x, so over the batch
+//   E[v_c] = b_c + w_c . E[x],  E[v_c^2] = b_c^2 + 2 b_c w_c . E[x] + w_c' E[x x'] w_c
+// and the 32 channels need only the 9 window means and 45 window products.
+// One workgroup per 32 images; a thread owns 4 output positions (fp32 sums of
+// 128 terms), the workgroup and grid sums are fp64.
+constexpr int NMOM = 9 + 45;
+constexpr int MOM_IMGS = 32;  // images per conv1_moments workgroup
+
+__global__ __launch_bounds__(256) void conv1_moments_kernel(EncArgs a) {
+  __shared__ __attribute__((aligned(16))) float x[IH][IW];
+  __shared__ double red[4][NMOM];
+  const int t = threadIdx.x, lane = t & 63, w = t >> 6;
+  float m[NMOM];
+#pragma unroll
+  for (int k = 0; k < NMOM; k++) m[k] = 0.f;
+  for (int i = 0; i < MOM_IMGS; i++) {
+    const long long b = (long long)blockIdx.x * MOM_IMGS + i;
     if (b >= a.n) break;
     __syncthreads();
     stage_image(x, a.images + b * a.image_stride);
     __syncthreads();
-    float fs = 0.f, fs2 = 0.f;
-    for (int q = 0; q < H1 * H1 / 8; q++) {
-      const int pos = g + 8 * q;
-      const float v = conv1_at(x, w1, b1, pos >> 5, pos & 31);
-      fs += v;
-      fs2 += v * v;
+#pragma unroll
+    for (int j = 0; j < H1 * H1 / 256; j++) {
+      float xv[9];
+      window(x, t + 256 * j, xv);
+      int q = 9;
+#pragma unroll
+      for (int k = 0; k < 9; k++) {
+        m[k] += xv[k];
+#pragma unroll
+        for (int l = k; l < 9; l++) m[q++] += xv[k] * xv[l];
+      }
     }
-    s += fs;
-    s2 += fs2;
   }
-  red[g][oc][0] = s;
-  red[g][oc][1] = s2;
+#pragma unroll
+  for (int k = 0; k < NMOM; k++) {
+    double d = m[k];
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) d += __shfl_xor(d, off, 64);
+    if (lane == 0) red[w][k] = d;
+  }
   __syncthreads();
-  if (t < 2 * C1) {
-    const int c = t >> 1, k = t & 1;
-    double v = 0.0;
-    for (int gg = 0; gg < 8; gg++) v += red[gg][c][k];
-    a.ws.part1[((long long)blockIdx.x * C1 + c) * 2 + k] = v;
+  if (t < NMOM) a.ws.part1[(long long)blockIdx.x * NMOM + t] = (red[0][t] + red[1][t]) + (red[2][t] + red[3][t]);
+}
+
+// BN1 from the window moments (train mode): scale/shift and the running update
+__global__ __launch_bounds__(256) void bn1_moments_kernel(EncArgs a, int nparts) {
+  __shared__ double red[4][NMOM];
+  __shared__ double mom[NMOM];
+  const int t = threadIdx.x;
+  if (t < 4 * NMOM) {
+    const int k = t % NMOM, sub = t / NMOM;
+    double s = 0.0;
+    for (int p = sub; p < nparts; p += 4) s += a.ws.part1[(long long)p * NMOM + k];
+    red[sub][k] = s;
   }
+  __syncthreads();
+  const double cnt = double(a.n) * (H1 * H1);
+  if (t < NMOM) mom[t] = ((red[0][t] + red[1][t]) + (red[2][t] + red[3][t])) / cnt;
+  __syncthreads();
+  if (t >= C1) return;
+  const int c = t;
+  double wv[9];
+  for (int k = 0; k < 9; k++) wv[k] = a.p.w1[c * 9 + k];
+  const double b = a.p.b1[c];
+  double wmu = 0.0, wMw = 0.0;
+  int q = 9;
+  for (int k = 0; k < 9; k++) {
+    wmu += wv[k] * mom[k];
+    for (int l = k; l < 9; l++) wMw += (k == l ? 1.0 : 2.0) * wv[k] * wv[l] * mom[q++];
+  }
+  const double mean = b + wmu;
+  const double var = fmax(b * b + 2.0 * b * wmu + wMw - mean * mean, 0.0);
+  a.p.rm1[c] = (1.f - a.momentum) * a.p.rm1[c] + a.momentum * float(mean);
+  a.p.rv1[c] = (1.f - a.momentum) * a.p.rv1[c] + a.momentum * float(var * cnt / (cnt - 1.0));
+  if (c == 0 && a.p.nbt1) *a.p.nbt1 += 1;
+  const float sc = a.p.g1[c] / sqrtf(float(var) + a.eps);
+  a.ws.ss1[c] = sc;
+  a.ws.ss1[C1 + c] = a.p.be1[c] - float(mean) * sc;
 }
 
 // ---- 2. BN finish: batch (train) or running (eval) statistics -> scale/shift
@@ -110,15 +159,24 @@ __global__ __launch_bounds__(256) void bn_finish_kernel(const double* part, int 
                                                         const float* gamma, const float* beta, float* rmean,
                                                         float* rvar, long long* nbt, int train, float momentum,
                                                         float eps, float* scale_shift) {
-  const int c = threadIdx.x;
-  if (c >= C) return;
+  __shared__ double red[8][32][2];
+  const int c = threadIdx.x & 31, sub = threadIdx.x >> 5;  // C <= 32; 8 interleaved sub-sums
+  if (train) {
+    double s = 0.0, s2 = 0.0;
+    if (c < C)
+      for (int p = sub; p < nparts; p += 8) {
+        s += part[((long long)p * C + c) * 2];
+        s2 += part[((long long)p * C + c) * 2 + 1];
+      }
+    red[sub][c][0] = s;
+    red[sub][c][1] = s2;
+  }
+  __syncthreads();
+  if (sub != 0 || c >= C) return;
   float mean, var;
   if (train) {
     double s = 0.0, s2 = 0.0;
-    for (int p = 0; p < nparts; p++) {
-      s += part[((long long)p * C + c) * 2];
-      s2 += part[((long long)p * C + c) * 2 + 1];
-    }
+    for (int q = 0; q < 8; q++) { s += red[q][c][0]; s2 += red[q][c][1]; }
     const double m = s / double(count);
     const double v = fmax(s2 / double(count) - m * m, 0.0);
     mean = float(m);
@@ -135,25 +193,28 @@ __global__ __launch_bounds__(256) void bn_finish_kernel(const double* part, int 
   scale_shift[C + c] = beta[c] - mean * sc;
 }
 
-// ---- 3. conv2 as an implicit GEMM; grid-stride over images.  Per image: the
-// image in LDS, then twice (input channels 0-15, 16-31): conv1 + BN1 + LeakyReLU
-// of those channels into LDS, and 72 MFMA steps per 32-position block.
-// Wave w owns position blocks 2w, 2w+1 (rows 4w..4w+3 of the 16x16 output).
-__global__ __launch_bounds__(256) void conv2_kernel(EncArgs a) {
-  __shared__ __attribute__((aligned(16))) float x[IH][IW];
-  __shared__ float a1[16 * CS];       // 16 channels of the activated conv1 output
+// ---- 3. conv2 as an implicit GEMM; two images per workgroup (waves 0-3 and
+// 4-7, 2 waves per SIMD to hide each other's latency), grid-stride over image
+// pairs.  Per image: the image in LDS, then four times (input channels 8q..8q+7):
+// conv1 + BN1 + LeakyReLU of those channels into LDS, and 36 MFMA steps per
+// 32-position block.  Wave w of an image owns position blocks 2w, 2w+1.
+constexpr int QCH = 8;  // conv1 channels per LDS pass
+
+__global__ __launch_bounds__(512) void conv2_kernel(EncArgs a) {
+  __shared__ __attribute__((aligned(16))) float x[2][IH][IW];
+  __shared__ float a1[2][QCH * CS];   // QCH channels of the activated conv1 output, per image
   __shared__ float w2t[K2][C1];       // conv2 weights, [ic*9 + tap][oc]
   __shared__ float ss1[2 * C1];
-  __shared__ double red[4][C1][2];
-  const int t = threadIdx.x, lane = t & 63, w = t >> 6, hh = lane >> 5, oc = lane & 31;
-  for (int e = t; e < K2 * C1; e += 256) {
+  __shared__ double red[8][C1][2];
+  const int t = threadIdx.x, sub = t >> 8, t8 = t & 255, lane = t & 63, w = (t >> 6) & 3, hh = lane >> 5;
+  const int oc = lane & 31;
+  for (int e = t; e < K2 * C1; e += 512) {
     const int o = e / K2, k = e % K2;
     w2t[k][o] = a.p.w2[e];
   }
   if (t < 2 * C1) ss1[t] = a.ws.ss1[t];
   const float b2 = a.p.b2[oc];
   double s = 0.0, s2 = 0.0;
-  // this lane's two output positions (A rows) in its wave's blocks
   int py[2], px[2];
 #pragma unroll
   for (int q = 0; q < 2; q++) {
@@ -161,33 +222,37 @@ __global__ __launch_bounds__(256) void conv2_kernel(EncArgs a) {
     py[q] = pos >> 4;
     px[q] = pos & 15;
   }
-  for (long long b = blockIdx.x; b < a.n; b += gridDim.x) {
+  for (long long base = 2LL * blockIdx.x; base < a.n; base += 2LL * gridDim.x) {
+    const long long b = base + sub;
+    const bool valid = b < a.n;
     __syncthreads();
-    stage_image(x, a.images + b * a.image_stride);
+    if (valid)
+      for (int e = t8; e < IH * IW / 4; e += 256)
+        reinterpret_cast<float4*>(&x[sub][0][0])[e] = reinterpret_cast<const float4*>(a.images + b * a.image_stride)[e];
     f32x16 acc[2];
 #pragma unroll
     for (int q = 0; q < 2; q++)
 #pragma unroll
       for (int r = 0; r < 16; r++) acc[q][r] = b2;
-    for (int half = 0; half < 2; half++) {
-      __syncthreads();  // image staged / previous half consumed
-      for (int icl = 0; icl < 16; icl++) {  // the channel is uniform: its weights are scalar loads
-        const int ic = 16 * half + icl;
-        float w1[9];
+    for (int quarter = 0; quarter < C1 / QCH; quarter++) {
+      __syncthreads();  // image staged / previous pass consumed
 #pragma unroll
-        for (int k = 0; k < 9; k++) w1[k] = a.p.w1[ic * 9 + k];
-        const float b1 = a.p.b1[ic], sc = ss1[ic], sh = ss1[C1 + ic];
+      for (int j = 0; j < H1 * H1 / 256; j++) {  // 4 positions per thread, each window read once
+        const int pos = t8 + 256 * j;
+        float xv[9];
+        window(x[sub], pos, xv);
 #pragma unroll
-        for (int j = 0; j < H1 * H1 / 256; j++) {
-          const int pos = t + 256 * j;
-          a1[icl * CS + pos] = leaky(fmaf(conv1_at(x, w1, b1, pos >> 5, pos & 31), sc, sh));
+        for (int icl = 0; icl < QCH; icl++) {  // uniform channel: scalar weight loads
+          const int ic = QCH * quarter + icl;
+          a1[sub][icl * CS + pos] = leaky(fmaf(conv1_win(xv, a.p.w1 + ic * 9, a.p.b1[ic]), ss1[ic], ss1[C1 + ic]));
         }
       }
       __syncthreads();
       // K order: step (icp, tap): lane half hh takes input channel 2 icp + hh
-      for (int icp = 0; icp < 8; icp++) {
-        const int icl = 2 * icp + hh, ic = 16 * half + icl;
-        const float* ach = a1 + icl * CS;
+#pragma unroll
+      for (int icp = 0; icp < QCH / 2; icp++) {
+        const int icl = 2 * icp + hh, ic = QCH * quarter + icl;
+        const float* ach = a1[sub] + icl * CS;
 #pragma unroll
         for (int tap = 0; tap < 9; tap++) {
           const int ky = tap / 3, kx = tap % 3;
@@ -201,6 +266,7 @@ __global__ __launch_bounds__(256) void conv2_kernel(EncArgs a) {
         }
       }
     }
+    if (!valid) continue;
     // raw conv2 output, flattened (C, H, W): column = channel, rows = positions
     float* out = a.ws.out2 + b * FL;
 #pragma unroll
@@ -221,11 +287,13 @@ __global__ __launch_bounds__(256) void conv2_kernel(EncArgs a) {
   if (a.train) {
     s += __shfl_xor(s, 32, 64);
     s2 += __shfl_xor(s2, 32, 64);
-    if (hh == 0) { red[w][oc][0] = s; red[w][oc][1] = s2; }
+    if (hh == 0) { red[t >> 6][oc][0] = s; red[t >> 6][oc][1] = s2; }
     __syncthreads();
     if (t < 2 * C1) {
       const int c = t >> 1, k = t & 1;
-      a.ws.part2[((long long)blockIdx.x * C1 + c) * 2 + k] = (red[0][c][k] + red[1][c][k]) + (red[2][c][k] + red[3][c][k]);
+      double v = 0.0;
+      for (int ww = 0; ww < 8; ww++) v += red[ww][c][k];
+      a.ws.part2[((long long)blockIdx.x * C1 + c) * 2 + k] = v;
     }
   }
 }
@@ -271,35 +339,48 @@ __global__ __launch_bounds__(256) void linear_kernel(EncArgs a) {
   for (int e = t; e < 32 * NZ; e += 256) {
     const int i = e / NZ, j = e % NZ;
     const long long im = (long long)blockIdx.x * 32 + i;
-    if (im >= a.n) continue;
-    a.ws.z[im * NZ + j] = ((tile[0][i][j] + tile[1][i][j]) + (tile[2][i][j] + tile[3][i][j])) + a.p.bl[j];
+    const float v = ((tile[0][i][j] + tile[1][i][j]) + (tile[2][i][j] + tile[3][i][j])) + a.p.bl[j];
+    tile[0][i][j] = im < a.n ? v : 0.f;
+    if (im < a.n) a.ws.z[im * NZ + j] = v;
+  }
+  if (!a.train) return;
+  __syncthreads();
+  if (t < 2 * NZ) {  // this block's BatchNorm1d sums (fp64)
+    const int j = t >> 1, k = t & 1;
+    double sum = 0.0;
+    for (int i = 0; i < 32; i++) {
+      const double v = tile[0][i][j];
+      sum += k ? v * v : v;
+    }
+    a.ws.part3[((long long)blockIdx.x * NZ + j) * 2 + k] = sum;
   }
 }
 
-// ---- 5. BatchNorm1d(20) + Tanh -> features; one 1024-thread workgroup
-__global__ __launch_bounds__(1024) void head_kernel(EncArgs a) {
-  __shared__ double red[32][NZ][2];
+// ---- 5. BatchNorm1d(20) + Tanh -> features.  Every workgroup forms the
+// statistics from the linear kernel's per-block sums (same order, same bits);
+// block 0 alone moves the running statistics.
+__global__ __launch_bounds__(256) void head_kernel(EncArgs a, int nparts) {
+  __shared__ double red[4][NZ][2];
   __shared__ float sc[NZ], sh[NZ];
-  const int t = threadIdx.x, lane = t & 31, grp = t >> 5;  // 32 groups of 32 threads
+  const int t = threadIdx.x;
   if (a.train) {
-    // thread (grp, lane): channel j = lane (< 20), images grp, grp + 32, ...
-    double s = 0.0, s2 = 0.0;
-    if (lane < NZ)
-      for (long long i = grp; i < a.n; i += 32) {
-        const double v = a.ws.z[i * NZ + lane];
-        s += v;
-        s2 += v * v;
-      }
-    if (lane < NZ) { red[grp][lane][0] = s; red[grp][lane][1] = s2; }
+    if (t < 4 * 2 * NZ) {
+      const int jk = t % (2 * NZ), sub = t / (2 * NZ);
+      double s = 0.0;
+      for (int p = sub; p < nparts; p += 4) s += a.ws.part3[(long long)p * 2 * NZ + jk];
+      red[sub][jk >> 1][jk & 1] = s;
+    }
     __syncthreads();
     if (t < NZ) {
       double S = 0.0, S2 = 0.0;
-      for (int g = 0; g < 32; g++) { S += red[g][t][0]; S2 += red[g][t][1]; }
+      for (int g = 0; g < 4; g++) { S += red[g][t][0]; S2 += red[g][t][1]; }
       const double cnt = double(a.n);
       const double m = S / cnt, v = fmax(S2 / cnt - m * m, 0.0);
-      a.p.rm3[t] = (1.f - a.momentum) * a.p.rm3[t] + a.momentum * float(m);
-      a.p.rv3[t] = (1.f - a.momentum) * a.p.rv3[t] + a.momentum * float(v * cnt / (a.n > 1 ? cnt - 1.0 : 1.0));
-      if (t == 0 && a.p.nbt3) *a.p.nbt3 += 1;
+      if (blockIdx.x == 0) {
+        a.p.rm3[t] = (1.f - a.momentum) * a.p.rm3[t] + a.momentum * float(m);
+        a.p.rv3[t] = (1.f - a.momentum) * a.p.rv3[t] + a.momentum * float(v * cnt / (cnt - 1.0));
+        if (t == 0 && a.p.nbt3) *a.p.nbt3 += 1;
+      }
       const float s_ = a.p.g3[t] / sqrtf(float(v) + a.eps);
       sc[t] = s_;
       sh[t] = a.p.be3[t] - float(m) * s_;
@@ -310,7 +391,8 @@ __global__ __launch_bounds__(1024) void head_kernel(EncArgs a) {
     sh[t] = a.p.be3[t] - a.p.rm3[t] * s_;
   }
   __syncthreads();
-  for (long long e = t; e < a.n * NZ; e += 1024) {
+  const long long e = (long long)blockIdx.x * 256 + t;
+  if (e < a.n * NZ) {
     const int j = int(e % NZ);
     a.out[(e / NZ) * a.out_stride + j] = tanhf(fmaf(a.ws.z[e], sc[j], sh[j]));
   }
@@ -320,13 +402,14 @@ EncWorkspace carve(float* base, long long n, long long* total) {
   EncWorkspace w;
   long long o = 0;
   auto take = [&](long long nfloats) { float* p = base ? base + o : nullptr; o += (nfloats + 63) & ~63LL; return p; };
-  const long long g1 = (n + 7) / 8;
-  w.part1 = reinterpret_cast<double*>(take(g1 * C1 * 2 * 2));
+  const long long g1 = (n + 31) / 32;
+  w.part1 = reinterpret_cast<double*>(take(g1 * NMOM * 2));
   w.part2 = reinterpret_cast<double*>(take(256LL * C1 * 2 * 2));
   w.ss1 = take(2 * C1);
   w.ss2 = take(2 * C1);
   w.out2 = take(n * FL);
   w.z = take(n * NZ);
+  w.part3 = reinterpret_cast<double*>(take(((n + 31) / 32) * NZ * 2 * 2));
   if (total) *total = o;
   return w;
 }
@@ -342,16 +425,21 @@ long long encoder_workspace_bytes(long long n) {
 int launch_encoder(EncArgs a, float* ws, hipStream_t s) {
   if (a.n <= 0) return 0;
   a.ws = carve(ws, a.n, nullptr);
-  const int g1 = int((a.n + 7) / 8);
-  const int g2 = int(a.n < 256 ? a.n : 256);
-  if (a.train) hipLaunchKernelGGL(conv1_stats_kernel, dim3(g1), dim3(256), 0, s, a);
-  hipLaunchKernelGGL(bn_finish_kernel, dim3(1), dim3(256), 0, s, (const double*)a.ws.part1, g1, a.n * H1 * H1, C1,
-                     a.p.g1, a.p.be1, a.p.rm1, a.p.rv1, a.p.nbt1, a.train, a.momentum, a.eps, a.ws.ss1);
-  hipLaunchKernelGGL(conv2_kernel, dim3(g2), dim3(256), 0, s, a);
+  const int g1 = int((a.n + MOM_IMGS - 1) / MOM_IMGS);
+  const long long pairs = (a.n + 1) / 2;
+  const int g2 = int(pairs < 256 ? pairs : 256);
+  if (a.train) {
+    hipLaunchKernelGGL(conv1_moments_kernel, dim3(g1), dim3(256), 0, s, a);
+    hipLaunchKernelGGL(bn1_moments_kernel, dim3(1), dim3(256), 0, s, a, g1);
+  } else {
+    hipLaunchKernelGGL(bn_finish_kernel, dim3(1), dim3(256), 0, s, (const double*)a.ws.part1, g1, a.n * H1 * H1, C1,
+                       a.p.g1, a.p.be1, a.p.rm1, a.p.rv1, a.p.nbt1, 0, a.momentum, a.eps, a.ws.ss1);
+  }
+  hipLaunchKernelGGL(conv2_kernel, dim3(g2), dim3(512), 0, s, a);
   hipLaunchKernelGGL(bn_finish_kernel, dim3(1), dim3(256), 0, s, (const double*)a.ws.part2, g2, a.n * H2 * H2, C1,
                      a.p.g2, a.p.be2, a.p.rm2, a.p.rv2, a.p.nbt2, a.train, a.momentum, a.eps, a.ws.ss2);
   hipLaunchKernelGGL(linear_kernel, dim3(int((a.n + 31) / 32)), dim3(256), 0, s, a);
-  hipLaunchKernelGGL(head_kernel, dim3(1), dim3(1024), 0, s, a);
+  hipLaunchKernelGGL(head_kernel, dim3(int((a.n * NZ + 255) / 256)), dim3(256), 0, s, a, int((a.n + 31) / 32));
   return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 

@@ -1,0 +1,16 @@
+#!/bin/bash
+# rocprofv3 kernel summary of a short camera PPO run with the fused frozen encoder.
+set -o pipefail
+mkdir -p gpurun_out
+export TMPDIR=/tmp
+timeout -k 10 300 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_cam -o run --output-format csv -- \
+  python -u tools/bench_ppo.py --cameras --frozen-encoder --timesteps 1e6 > gpurun_out/prof_cam.log 2>&1 || { tail gpurun_out/prof_cam.log; exit 1; }
+python - <<'PY'
+import csv, glob
+f = glob.glob("gpurun_out/prof_cam/**/*kernel_stats.csv", recursive=True)[0]
+rows = list(csv.DictReader(open(f)))
+tot = sum(float(r["TotalDurationNs"]) for r in rows)
+for r in sorted(rows, key=lambda r: -float(r["TotalDurationNs"]))[:22]:
+    print(f"{float(r['TotalDurationNs'])/1e6:8.1f} ms {int(r['Calls']):6d} {float(r['AverageNs'])/1e3:8.1f} us  {r['Name'][:100]}")
+print("total ms", tot / 1e6)
+PY
