@@ -47,7 +47,7 @@
 extern "C" {
 #endif
 
-#define BB_ABI_VERSION 9
+#define BB_ABI_VERSION 10
 #define BB_NQ 17
 #define BB_NV 15
 #define BB_OBS 15
@@ -174,7 +174,7 @@ typedef struct bb_ppo_mlp_args {
   float* exp_avg_sq;
   int64_t n_params;
   int32_t offsets[21];
-  const float* obs;          /* [n][15] */
+  const float* obs;          /* [n][obs_dim] */
   const float* actions;      /* [n][3] unclipped */
   const float* old_logp;     /* [n] */
   const float* advantages;   /* [n] */
@@ -189,6 +189,8 @@ typedef struct bb_ppo_mlp_args {
   float* coef;               /* 4 floats of scratch */
   int32_t B;
   int32_t normalize_advantage;
+  int32_t obs_dim;           /* 15 (proprio) or 56 (+ relative_image_timestamp, rgbd_0/1 features) */
+  int32_t obs_direct;        /* 0: obs rows are perm-indexed rollout rows; 1: the minibatch's rows in order */
   float ent_coef, vf_coef;
   double beta1, beta2, eps, weight_decay, max_grad_norm;
   float* workspace;
@@ -199,14 +201,15 @@ int bb_ppo_mlp_step(const bb_ppo_mlp_args* args, void* stream);
 /* The rollout's policy step for the same proprio MLP policy (SB3
  * ActorCriticPolicy.forward as called by OnPolicyAlgorithm.collect_rollouts,
  * model.learn at ballbot_rl/training/train.py:284): for n observation rows
- * obs_dev [n][15], mean/value from the two trunks, actions = mean +
+ * obs_dev [n][obs_dim] (15, or 56 with the camera features), mean/value from the two trunks, actions = mean +
  * noise * exp(log_std) (noise_dev [n][3] standard normal; NULL = the mean),
  * their Gaussian log-probability and the value.  Writes actions_dev [n][3]
  * (unclipped, as SB3 stores them), values_dev [n], log_prob_dev [n], and
  * optionally clipped_dev [n][3] (clip to the [-1, 1] action space, what
  * env.step receives) and obs_copy_dev [n][15] (the rollout buffer's copy).
  * params_dev/offsets as for bb_ppo_mlp_step.  One launch; graph-capturable. */
-int bb_ppo_mlp_act(const float* params_dev, const int32_t* offsets, const float* obs_dev, const float* noise_dev, int n,
+int bb_ppo_mlp_act(const float* params_dev, const int32_t* offsets, const float* obs_dev, int obs_dim,
+                   const float* noise_dev, int n,
                    float* obs_copy_dev, float* actions_dev, float* clipped_dev, float* values_dev, float* log_prob_dev,
                    void* stream);
 /* One rollout step's episode bookkeeping (SB3 collect_rollouts + Monitor,

@@ -63,6 +63,8 @@ class PPOMlpArgs(C.Structure):
                                          "mb_counter", "row_counter", "log", "clip", "lr", "step", "coef")] + [
         ("B", C.c_int32),
         ("normalize_advantage", C.c_int32),
+        ("obs_dim", C.c_int32),
+        ("obs_direct", C.c_int32),
         ("ent_coef", C.c_float),
         ("vf_coef", C.c_float),
     ] + [(name, C.c_double) for name in ("beta1", "beta2", "eps", "weight_decay", "max_grad_norm")] + [
@@ -89,7 +91,7 @@ EXPORTS = [
     "bb_ppo_mlp_act", "bb_rollout_track", "bb_depth_encoder_workspace_bytes", "bb_depth_encoder",
 ]
 
-ABI_VERSION = 9  # include/ballbot_mi355x.h BB_ABI_VERSION
+ABI_VERSION = 10  # include/ballbot_mi355x.h BB_ABI_VERSION
 
 _lib = None
 
@@ -162,7 +164,7 @@ def _load(path: Path):
     L.bb_gae.argtypes = [vp, vp, vp, vp, vp, C.c_int, C.c_int, C.c_double, C.c_double, vp, vp, vp]
     L.bb_ppo_mlp_workspace_bytes.argtypes = [C.c_int, C.POINTER(C.c_int64)]
     L.bb_ppo_mlp_step.argtypes = [C.POINTER(PPOMlpArgs), vp]
-    L.bb_ppo_mlp_act.argtypes = [vp, C.POINTER(C.c_int32), vp, vp, C.c_int, vp, vp, vp, vp, vp, vp]
+    L.bb_ppo_mlp_act.argtypes = [vp, C.POINTER(C.c_int32), vp, C.c_int, vp, C.c_int, vp, vp, vp, vp, vp, vp]
     L.bb_rollout_track.argtypes = [vp, vp, C.c_int, C.c_int] + [vp] * 8
     L.bb_depth_encoder_workspace_bytes.argtypes = [C.c_int64, C.POINTER(C.c_int64)]
     L.bb_depth_encoder.argtypes = [C.POINTER(EncoderParams), vp, C.c_int64, C.c_int64, C.c_int, C.c_int, C.c_int,

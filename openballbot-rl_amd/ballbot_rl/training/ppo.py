@@ -153,15 +153,16 @@ def policy_obs(obs15: torch.Tensor, depth: Optional[torch.Tensor] = None,
 
 def fused_mlp_slots(ppo: "BatchedPPO", update: bool = True):
     """Flat-buffer offsets of the 21 tensors bb_ppo_mlp_step reads, or None when
-    the policy/optimiser is not the reference's proprio MLP on FlatAdamW
-    (pi = vf = [128]*4 LeakyReLU(0.01) over the 15-d obs, 3-d action head);
+    the policy/optimiser is not the reference's MLP on FlatAdamW (pi = vf =
+    [128]*4 LeakyReLU(0.01) over the 15-d proprio obs, or the 56-d features of
+    the camera policy with fused frozen encoders; 3-d action head);
     update=True also needs a batch size bb_ppo_mlp_step takes.
     BB_PPO_FUSED=0 disables the fused update and rollout step (A/B runs)."""
     import os
 
     from ballbot_rl.training.optim import FlatAdamW
 
-    if os.environ.get("BB_PPO_FUSED", "1") == "0" or ppo.cameras or ppo.device.type != "cuda":
+    if os.environ.get("BB_PPO_FUSED", "1") == "0" or ppo.device.type != "cuda":
         return None
     opt, pol = ppo.optimizer, ppo.policy
     if not isinstance(opt, FlatAdamW):
@@ -169,12 +170,21 @@ def fused_mlp_slots(ppo: "BatchedPPO", update: bool = True):
     if update and (ppo.batch_size % 256 or ppo.batch_size > 16384):
         return None
 
+    ext = pol.features_extractor
+    fd = ext.features_dim
+    if ppo.cameras:  # the camera features must come from fused frozen encoders (no trainable extractor)
+        rgbd = {k for k in ext.keys if "rgbd_" in k}
+        if fd != 56 or ext._frozen_keys != rgbd or any(p.requires_grad for p in ext.parameters()):
+            return None
+    elif fd != 15:
+        return None
+
     def trunk(seq):
         mods = list(seq)
         if len(mods) != 8:
             return None
         lins, acts = mods[0::2], mods[1::2]
-        shapes = [(128, 15), (128, 128), (128, 128), (128, 128)]
+        shapes = [(128, fd), (128, 128), (128, 128), (128, 128)]
         if any(not isinstance(m, nn.Linear) or m.bias is None or tuple(m.weight.shape) != sh
                for m, sh in zip(lins, shapes)):
             return None
@@ -183,7 +193,7 @@ def fused_mlp_slots(ppo: "BatchedPPO", update: bool = True):
         return [m.weight for m in lins] + [m.bias for m in lins]
 
     pi, vf = trunk(pol.policy_net), trunk(pol.value_net_trunk)
-    if pi is None or vf is None or pol.features_extractor.features_dim != 15:
+    if pi is None or vf is None:
         return None
     if tuple(pol.action_net.weight.shape) != (3, 128) or tuple(pol.value_net.weight.shape) != (1, 128):
         return None
@@ -271,7 +281,13 @@ class _UpdateGraphs:
         for i, o in enumerate(slots):
             a.offsets[i] = int(o)
         d = self.data
-        a.obs, a.actions, a.old_logp = d["obs"].data_ptr(), d["actions"].data_ptr(), d["log_probs"].data_ptr()
+        cams = "depth" in d
+        fd = ppo.policy.features_extractor.features_dim
+        if cams:  # the minibatch's features (frozen encoders in train mode) land here, in minibatch order
+            self.feats = torch.zeros(ppo.batch_size, fd, device=ppo.device)
+        a.obs = self.feats.data_ptr() if cams else d["obs"].data_ptr()
+        a.obs_dim, a.obs_direct = int(fd), int(cams)
+        a.actions, a.old_logp = d["actions"].data_ptr(), d["log_probs"].data_ptr()
         a.advantages, a.returns = d["advantages"].data_ptr(), d["returns"].data_ptr()
         a.perm, a.mb_counter, a.row_counter, a.log = (t.data_ptr() for t in (self.perm, self.k, self.row, self.log))
         a.clip, a.lr, a.step, a.coef = (t.data_ptr() for t in (self.clip, opt.lr, opt.step_t, opt.coef))
@@ -285,6 +301,10 @@ class _UpdateGraphs:
         dev = ppo.device
 
         def mb_step():
+            if cams:
+                idx = self.perm.index_select(0, self.k).view(-1)
+                with torch.no_grad():
+                    self.feats.copy_(ppo.policy.features_extractor(ppo._mb_obs(d, idx)))
             stream = C.c_void_p(torch.cuda.current_stream(dev).cuda_stream)
             N.check(lib.bb_ppo_mlp_step(C.byref(a), stream), "bb_ppo_mlp_step")
 
@@ -440,6 +460,48 @@ class BatchedPPO:
 
     # ---------------------------------------------------------------- rollout
     def _collect_fused(self, slots) -> tuple:
+        if self.cameras:
+            return self._collect_fused_cameras(slots)
+        return self._collect_fused_proprio(slots)
+
+    def _collect_fused_cameras(self, slots) -> tuple:
+        """The camera policy's rollout: features from the Extractor (fused frozen
+        encoders, eval mode), then bb_ppo_mlp_act on the 56-d features and
+        bb_rollout_track; the rollout buffer keeps obs, images and timestamps."""
+        from ballbot_gym import _native as N
+
+        env, b, dev = self.env, self.buf, self.device
+        lib = N.lib()
+        T, n = self.n_steps, self.n_envs
+        offs = (C.c_int32 * 21)(*slots)
+        flat = C.c_void_p(self.optimizer.flat.data_ptr())
+        ext = self.policy.features_extractor
+        self.policy.eval()
+        if self._last_obs is None:
+            self._last_obs, _ = env.reset()
+        noise = torch.randn(T, n, 3, generator=self.gen, device=dev)
+        clipped = torch.empty(n, 3, device=dev)
+        ep_r = torch.empty(T, n, dtype=torch.float64, device=dev)
+        ep_l = torch.empty(T, n, dtype=torch.int64, device=dev)
+        b.starts[0].copy_(self._last_starts)
+        stream = C.c_void_p(torch.cuda.current_stream(dev).cuda_stream)
+        for t in range(T):
+            b.obs[t].copy_(self._last_obs)
+            b.depth[t].copy_(env.depth)
+            b.rel_ts[t].copy_(env.rel_ts)
+            feats = ext(policy_obs(b.obs[t], b.depth[t], b.rel_ts[t])).contiguous()
+            N.check(lib.bb_ppo_mlp_act(flat, offs, _ptr(feats), int(feats.shape[1]), _ptr(noise[t]), n, None,
+                                       _ptr(b.actions[t]), _ptr(clipped), _ptr(b.values[t]), _ptr(b.log_probs[t]),
+                                       stream), "bb_ppo_mlp_act")
+            obs, reward, flags = env.step_flags(clipped)
+            nxt = _ptr(b.starts[t + 1]) if t + 1 < T else None
+            N.check(lib.bb_rollout_track(_ptr(reward.contiguous()), _ptr(flags), 5, n, _ptr(b.rewards[t]),
+                                         _ptr(self._ep_ret), _ptr(self._ep_len), _ptr(ep_r[t]), _ptr(ep_l[t]),
+                                         _ptr(self._last_starts), nxt, stream), "bb_rollout_track")
+            self._last_obs = obs
+        return ep_r, ep_l
+
+    def _collect_fused_proprio(self, slots) -> tuple:
         """collect_rollouts with the policy step as bb_ppo_mlp_act and the
         episode bookkeeping as bb_rollout_track: three launches per env step
         (policy, bb_step, bookkeeping) instead of ~40.  Same semantics as the
@@ -462,7 +524,7 @@ class BatchedPPO:
         stream = C.c_void_p(torch.cuda.current_stream(dev).cuda_stream)
         for t in range(T):
             obs_in = self._last_obs.contiguous()
-            N.check(lib.bb_ppo_mlp_act(flat, offs, _ptr(obs_in), _ptr(noise[t]), n, _ptr(b.obs[t]), _ptr(b.actions[t]),
+            N.check(lib.bb_ppo_mlp_act(flat, offs, _ptr(obs_in), 15, _ptr(noise[t]), n, _ptr(b.obs[t]), _ptr(b.actions[t]),
                                        _ptr(clipped), _ptr(b.values[t]), _ptr(b.log_probs[t]), stream),
                     "bb_ppo_mlp_act")
             if fast:
@@ -482,9 +544,9 @@ class BatchedPPO:
     @torch.no_grad()
     def collect_rollouts(self) -> None:
         env, b = self.env, self.buf
-        if self._act_slots is None and not self.cameras and self.device.type == "cuda":
+        if self._act_slots is None and self.device.type == "cuda":
             self._act_slots = fused_mlp_slots(self, update=False) or False
-        if self._act_slots:
+        if self._act_slots and (not self.cameras or hasattr(env, "step_flags")):
             ep_r, ep_l = self._collect_fused(self._act_slots)
             self._finish_rollout(ep_r, ep_l)
             return

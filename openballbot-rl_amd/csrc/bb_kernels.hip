@@ -856,9 +856,10 @@ int bb_ppo_mlp_step(const bb_ppo_mlp_args* a, void* stream) {
       !(a->max_grad_norm > 0.0))
     return fail("bb_ppo_mlp_step: bad optimiser hyper-parameters");
   // sizes of the 21 tensors: their extents must fit the flat buffer, 16-byte aligned
-  static const int sizes[MLP_NSLOTS] = {128 * 15, 128 * 128, 128 * 128, 128 * 128, 128, 128, 128, 128,
-                                        128 * 15, 128 * 128, 128 * 128, 128 * 128, 128, 128, 128, 128,
-                                        3 * 128, 3, 128, 1, 3};
+  if (a->obs_dim != 15 && a->obs_dim != 56) return fail("bb_ppo_mlp_step: obs_dim must be 15 or 56 (got %d)", a->obs_dim);
+  const int sizes[MLP_NSLOTS] = {128 * a->obs_dim, 128 * 128, 128 * 128, 128 * 128, 128, 128, 128, 128,
+                                 128 * a->obs_dim, 128 * 128, 128 * 128, 128 * 128, 128, 128, 128, 128,
+                                 3 * 128, 3, 128, 1, 3};
   for (int i = 0; i < MLP_NSLOTS; i++)
     if (a->offsets[i] < 0 || a->offsets[i] % 4 || (int64_t)a->offsets[i] + sizes[i] > a->n_params)
       return fail("bb_ppo_mlp_step: offsets[%d] = %d is not a 4-aligned slot inside the %lld-float buffer", i,
@@ -874,7 +875,7 @@ int bb_ppo_mlp_step(const bb_ppo_mlp_args* a, void* stream) {
   m.mb_counter = reinterpret_cast<long long*>(a->mb_counter);
   m.row_counter = reinterpret_cast<long long*>(a->row_counter);
   m.log = a->log; m.clip = a->clip; m.lr = a->lr; m.step = a->step; m.coef = a->coef;
-  m.B = a->B; m.normalize = a->normalize_advantage ? 1 : 0; m.ent_coef = a->ent_coef; m.vf_coef = a->vf_coef;
+  m.B = a->B; m.normalize = a->normalize_advantage ? 1 : 0; m.in_dim = a->obs_dim; m.obs_direct = a->obs_direct ? 1 : 0; m.ent_coef = a->ent_coef; m.vf_coef = a->vf_coef;
   m.beta1 = a->beta1; m.beta2 = a->beta2; m.eps = a->eps; m.weight_decay = a->weight_decay;
   m.max_norm = a->max_grad_norm; m.ws = a->workspace; m.ws_bytes = a->workspace_bytes;
   const int rc = launch_mlp_step(m, (hipStream_t)stream);
@@ -882,17 +883,18 @@ int bb_ppo_mlp_step(const bb_ppo_mlp_args* a, void* stream) {
   return 0;
 }
 
-int bb_ppo_mlp_act(const float* params, const int32_t* offsets, const float* obs, const float* noise, int n,
+int bb_ppo_mlp_act(const float* params, const int32_t* offsets, const float* obs, int obs_dim, const float* noise, int n,
                    float* obs_copy, float* actions, float* clipped, float* values, float* log_prob, void* stream) {
   if (!params || !offsets || !obs || !actions || !values || !log_prob) return fail("bb_ppo_mlp_act: NULL argument");
   if (n < 0) return fail("bb_ppo_mlp_act: n must be >= 0 (got %d)", n);
+  if (obs_dim != 15 && obs_dim != 56) return fail("bb_ppo_mlp_act: obs_dim must be 15 or 56 (got %d)", obs_dim);
   for (int i = 0; i < MLP_NSLOTS; i++)
     if (offsets[i] < 0 || offsets[i] % 4) return fail("bb_ppo_mlp_act: offsets[%d] = %d is not 4-aligned", i, offsets[i]);
   if (reinterpret_cast<uintptr_t>(params) & 15) return fail("bb_ppo_mlp_act: params must be 16-byte aligned");
   MlpActArgs m;
   m.params = params;
   for (int i = 0; i < MLP_NSLOTS; i++) m.off[i] = offsets[i];
-  m.obs = obs; m.noise = noise; m.n = n; m.obs_copy = obs_copy; m.actions = actions; m.clipped = clipped;
+  m.obs = obs; m.in_dim = obs_dim; m.noise = noise; m.n = n; m.obs_copy = obs_copy; m.actions = actions; m.clipped = clipped;
   m.values = values; m.log_prob = log_prob;
   if (launch_mlp_act(m, (hipStream_t)stream))
     return fail("bb_ppo_mlp_act: launch failed: %s", hipGetErrorString(hipGetLastError()));

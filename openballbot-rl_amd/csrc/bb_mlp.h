@@ -27,7 +27,9 @@ struct MlpStepArgs {
   float* exp_avg_sq;
   long long n_params;   // flat length (with the alignment gaps)
   int off[MLP_NSLOTS];
-  const float* obs;       // [n][15] rollout observations (sorted-key proprio)
+  const float* obs;       // [n][in_dim] rollout observations (sorted-key proprio), or with
+                          // obs_direct the minibatch's [B][in_dim] features in order
+  int in_dim, obs_direct; // 15 (proprio) or 56 (+ relative_image_timestamp and the two camera features)
   const float* actions;   // [n][3] unclipped actions
   const float* old_logp;  // [n]
   const float* adv;       // [n]
@@ -51,10 +53,11 @@ struct MlpStepArgs {
 struct MlpActArgs {
   const float* params;
   int off[MLP_NSLOTS];
-  const float* obs;      // [n][15]
+  const float* obs;      // [n][in_dim]
+  int in_dim;            // 15 or 56
   const float* noise;    // [n][3] or NULL (deterministic)
   int n;
-  float* obs_copy;       // [n][15] or NULL
+  float* obs_copy;       // [n][in_dim] or NULL
   float* actions;        // [n][3] unclipped
   float* clipped;        // [n][3] or NULL
   float* values;         // [n]

@@ -44,12 +44,11 @@ namespace {
 typedef float f32x16 __attribute__((ext_vector_type(16)));
 
 constexpr int HID = 128;          // trunk width
-constexpr int IN = 15;            // observation features
-constexpr int XW = 32;            // workspace row width of the padded input
+constexpr int IN_MAX = 56;        // policy input features: 15 (proprio) or 56 (with the camera features)
+constexpr int XW_MAX = 64;        // workspace row width of the padded input
 constexpr int ROWS = 32;          // rows per tile (the MFMA M)
 constexpr int T1 = 512;           // threads per tile workgroup: 8 waves = 2 trunks x 4 column blocks
 constexpr int LDT = HID + 4;      // LDS row stride (floats): float4 rows, no bank conflicts
-constexpr int LDX = IN + 2;       // input tile stride
 constexpr int MAXCH = 32;         // max K chunks of the weight-gradient GEMMs
 constexpr int LPART = 8;          // loss partials per tile: pg, vf, kl, cf, dls[3], -
 constexpr int NJOB = 10;          // weight-gradient GEMMs: 2 trunks x 4 layers + 2 heads
@@ -72,7 +71,7 @@ __host__ __device__ inline int n_chunks(int B) {
     if (B % (c * SLAB) == 0) return c;
   return 1;
 }
-constexpr int WELEMS = 2 * (HID * IN + 3 * HID * HID) + 4 * HID;  // weight elements
+constexpr int WELEMS = 2 * (HID * IN_MAX + 3 * HID * HID) + 4 * HID;  // weight elements (upper bound)
 constexpr int BELEMS = 2 * 4 * HID + 4;                           // bias elements
 
 struct Workspace {
@@ -90,7 +89,7 @@ Workspace carve(float* base, int B, long long* total_floats) {
   Workspace w;
   long long o = 0;
   auto take = [&](long long n) { float* p = base ? base + o : nullptr; o += (n + 63) & ~63LL; return p; };
-  w.x = take((long long)B * XW);
+  w.x = take((long long)B * XW_MAX);
   for (int t = 0; t < 2; t++)
     for (int l = 0; l < 4; l++) w.h[t][l] = take((long long)B * HID);
   for (int t = 0; t < 2; t++)
@@ -118,6 +117,7 @@ struct TileArgs {
   int B, normalize;
   float vf_coef;
   Workspace w;
+  int obs_direct;  // TRAIN: obs rows are the minibatch in order (not indexed by perm)
   // rollout (act) mode: rows r0.. of obs directly, n of them
   int n;
   const float* noise;   // [n][3] standard normal draws, NULL = deterministic (the mean)
@@ -179,8 +179,12 @@ __device__ __forceinline__ f32x16 tile_gemm(f32x16 acc, const float* tile_row, c
 
 // TRAIN: one minibatch tile of the update (forward, loss, backward).
 // !TRAIN: the rollout's policy step, SB3 ActorCriticPolicy.forward over obs rows.
-template <bool TRAIN>
+// IN: policy input features (15 proprio, 56 with the camera features); the
+// padded input is XW wide in the workspace.
+template <bool TRAIN, int IN>
 __global__ __launch_bounds__(T1) void mlp_tile_kernel(TileArgs p) {
+  constexpr int XW = IN <= 16 ? 32 : 64;
+  constexpr int LDX = IN + 2;
   __shared__ __attribute__((aligned(16))) float xs[2][2][ROWS][LDT];  // [trunk][buffer] exchange tiles
   __shared__ float xin[ROWS][LDX];
   __shared__ float head[ROWS][4];  // dL/dmean[3], dL/dvalue
@@ -223,8 +227,10 @@ __global__ __launch_bounds__(T1) void mlp_tile_kernel(TileArgs p) {
   if (tid < ROWS) idx[tid] = TRAIN ? (int)perm[r0 + tid] : (r0 + tid < p.n ? r0 + tid : -1);
   __syncthreads();
   for (int e = tid; e < ROWS * XW; e += T1) {
-    const int r = e >> 5, c = e & 31, i = idx[r];
-    const float v = c < IN && i >= 0 ? p.obs[(long long)i * IN + c] : 0.f;
+    const int r = e / XW, c = e % XW, i = idx[r];
+    // obs_direct: the input rows are already the minibatch, in order (camera features)
+    const long long src = TRAIN && p.obs_direct ? (long long)(r0 + r) : (long long)i;
+    const float v = c < IN && i >= 0 ? p.obs[src * IN + c] : 0.f;
     if (c < LDX) xin[r][c] = v;
     if (TRAIN) p.w.x[(long long)(r0 + r) * XW + c] = v;
     if (!TRAIN && p.obs_copy && c < IN && i >= 0) p.obs_copy[(long long)i * IN + c] = v;
@@ -235,16 +241,16 @@ __global__ __launch_bounds__(T1) void mlp_tile_kernel(TileArgs p) {
   const int wbase = t ? MLP_VF_W0 : MLP_PI_W0, bbase = t ? MLP_VF_B0 : MLP_PI_B0;
   f32x16 hreg[4];
   int cur = 0;
-  {  // layer 0, K = 15 (padded to 16)
+  {  // layer 0, K = IN (padded to even)
     f32x16 acc;
     const float bias = P[p.off[bbase] + col];
 #pragma unroll
     for (int r = 0; r < 16; r++) acc[r] = bias;
     const float* W0 = P + p.off[wbase] + col * IN;
 #pragma unroll
-    for (int s = 0; s < 8; s++) {
+    for (int s = 0; s < (IN + 1) / 2; s++) {
       const int k = 2 * s + hh;
-      acc = mfma(xin[lane & 31][k], k < IN ? W0[k] : 0.f, acc);
+      acc = mfma(k < IN ? xin[lane & 31][k] : 0.f, k < IN ? W0[k] : 0.f, acc);
     }
 #pragma unroll
     for (int r = 0; r < 16; r++) acc[r] = leaky(acc[r]);
@@ -590,7 +596,7 @@ long long mlp_workspace_bytes(int B) {
 
 int launch_mlp_step(const MlpStepArgs& A, hipStream_t s) {
   const int B = A.B;
-  if (B < 256 || B % 256 || B > 16384) return -2;
+  if (B < 256 || B % 256 || B > 16384 || (A.in_dim != 15 && A.in_dim != 56)) return -2;
   if (A.ws_bytes < mlp_workspace_bytes(B)) return -3;
   const Workspace w = carve(A.ws, B, nullptr);
   const int ntiles = B / ROWS, nch = n_chunks(B);
@@ -602,7 +608,11 @@ int launch_mlp_step(const MlpStepArgs& A, hipStream_t s) {
   t.perm = A.perm; t.mb_counter = A.mb_counter; t.clip = A.clip;
   t.B = B; t.normalize = A.normalize; t.vf_coef = A.vf_coef; t.w = w;
   t.n = 0; t.noise = nullptr; t.obs_copy = t.act_out = t.act_clipped = t.values_out = t.logp_out = nullptr;
-  hipLaunchKernelGGL(mlp_tile_kernel<true>, dim3(ntiles), dim3(T1), 0, s, t);
+  t.obs_direct = A.obs_direct;
+  if (A.in_dim == 15)
+    hipLaunchKernelGGL((mlp_tile_kernel<true, 15>), dim3(ntiles), dim3(T1), 0, s, t);
+  else
+    hipLaunchKernelGGL((mlp_tile_kernel<true, 56>), dim3(ntiles), dim3(T1), 0, s, t);
 
   // weight/bias-gradient jobs, in flat-gradient segment order
   GemmArgs g;
@@ -622,7 +632,8 @@ int launch_mlp_step(const MlpStepArgs& A, hipStream_t s) {
   };
   for (int tr = 0; tr < 2; tr++)
     for (int l = 0; l < 4; l++)
-      add_job(w.dz[tr][l], HID, HID, l ? w.h[tr][l - 1] : w.x, l ? HID : XW, l ? HID : IN,
+      add_job(w.dz[tr][l], HID, HID, l ? w.h[tr][l - 1] : w.x, l ? HID : (A.in_dim <= 16 ? 32 : 64),
+              l ? HID : A.in_dim,
               A.off[(tr ? MLP_VF_W0 : MLP_PI_W0) + l], A.off[(tr ? MLP_VF_B0 : MLP_PI_B0) + l]);
   add_job(w.dhead, 4, 3, w.h[0][3], HID, HID, A.off[MLP_WA], A.off[MLP_BA]);
   add_job(w.dhead + 3, 4, 1, w.h[1][3], HID, HID, A.off[MLP_WV], A.off[MLP_BV]);
@@ -651,12 +662,16 @@ int launch_mlp_step(const MlpStepArgs& A, hipStream_t s) {
 
 int launch_mlp_act(const MlpActArgs& A, hipStream_t s) {
   if (A.n <= 0) return 0;
+  if (A.in_dim != 15 && A.in_dim != 56) return -2;
   TileArgs t{};
   t.P = A.params;
   for (int i = 0; i < MLP_NSLOTS; i++) t.off[i] = A.off[i];
   t.obs = A.obs; t.n = A.n; t.noise = A.noise; t.obs_copy = A.obs_copy; t.act_out = A.actions;
   t.act_clipped = A.clipped; t.values_out = A.values; t.logp_out = A.log_prob;
-  hipLaunchKernelGGL(mlp_tile_kernel<false>, dim3((A.n + ROWS - 1) / ROWS), dim3(T1), 0, s, t);
+  if (A.in_dim == 15)
+    hipLaunchKernelGGL((mlp_tile_kernel<false, 15>), dim3((A.n + ROWS - 1) / ROWS), dim3(T1), 0, s, t);
+  else
+    hipLaunchKernelGGL((mlp_tile_kernel<false, 56>), dim3((A.n + ROWS - 1) / ROWS), dim3(T1), 0, s, t);
   return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 

@@ -463,7 +463,7 @@ def test_fused_act_deterministic_is_the_mean():
     act = torch.empty(77, 3, device=dev); val = torch.empty(77, device=dev); lp = torch.empty(77, device=dev)
     clipped = torch.empty(77, 3, device=dev)
     ptr = lambda t: C.c_void_p(t.data_ptr())  # noqa: E731
-    N.check(N.lib().bb_ppo_mlp_act(ptr(m.optimizer.flat), (C.c_int32 * 21)(*slots), ptr(obs), None, 77, None, ptr(act),
+    N.check(N.lib().bb_ppo_mlp_act(ptr(m.optimizer.flat), (C.c_int32 * 21)(*slots), ptr(obs), 15, None, 77, None, ptr(act),
                                    ptr(clipped), ptr(val), ptr(lp), None), "bb_ppo_mlp_act")
     torch.cuda.synchronize()
     with torch.no_grad():
@@ -542,3 +542,46 @@ def test_fused_encoder_in_extractor(monkeypatch):
         monkeypatch.setenv("BB_FUSED_ENCODER", "0")
         plain = pol.features_extractor(obs)
     assert torch.allclose(fused, plain, rtol=1e-4, atol=2e-4), (fused - plain).abs().max()
+
+
+def test_fused_camera_policy_matches_autograd(monkeypatch):
+    """The camera policy with fused frozen encoders: the fused minibatch over the 56-d
+    features (bb_ppo_mlp_step, obs_direct) vs the autograd minibatch on the same
+    rollout, and the fused rollout step vs the torch one on the first env step."""
+    import copy
+
+    from ballbot_gym.envs import BallbotVecEnv
+    from ballbot_rl.training.logger import CSVLogger
+    from ballbot_rl.training.ppo import BatchedPPO
+
+    enc = _random_frozen_encoder(5)
+    envs = [BallbotVecEnv(256, device="cuda:0", seed=5, disable_cameras=False) for _ in range(2)]
+    models = []
+    for fused, env in zip(("0", "1"), envs):
+        monkeypatch.setenv("BB_PPO_FUSED", fused)
+        m = BatchedPPO(env, n_steps=8, batch_size=512, n_epochs=2, learning_rate=3e-4, seed=3,
+                       frozen_encoder=copy.deepcopy(enc), logger=CSVLogger(None, stdout=False))
+        m.collect_rollouts()
+        models.append(m)
+    assert models[0]._act_slots is False and models[1]._act_slots
+    a, b = models[0].buf, models[1].buf
+    assert torch.equal(a.obs[0], b.obs[0]) and torch.equal(a.depth[0], b.depth[0])
+    assert torch.allclose(a.actions[0], b.actions[0], rtol=1e-4, atol=1e-5), (a.actions[0] - b.actions[0]).abs().max()
+    assert torch.allclose(a.values[0], b.values[0], rtol=1e-4, atol=1e-5)
+    assert torch.allclose(a.log_probs[0], b.log_probs[0], rtol=1e-4, atol=1e-4)
+    d0 = models[0].buf.flat()
+    for fused, m in zip(("0", "1"), models):
+        monkeypatch.setenv("BB_PPO_FUSED", fused)
+        m.shuffle_gen.manual_seed(99)
+        m._update({k: v.clone() for k, v in d0.items()})
+    assert not models[0]._graphs.fused and models[1]._graphs.fused
+    la, lb = models[0].logger.values, models[1].logger.values
+    for k in ("train/policy_gradient_loss", "train/value_loss", "train/approx_kl"):
+        assert la[k] == pytest.approx(lb[k], rel=5e-3, abs=1e-6), k
+    for p, q in zip(models[0].policy.parameters(), models[1].policy.parameters()):
+        diff = (p - q).abs()
+        assert float((diff > 1e-5).float().mean()) < 1e-2, float(diff.max())
+    for p, q in zip(models[0].policy.features_extractor.buffers(), models[1].policy.features_extractor.buffers()):
+        assert torch.allclose(p.double(), q.double(), rtol=1e-4, atol=1e-5)
+    for env in envs:
+        env.close()
