@@ -47,7 +47,7 @@
 extern "C" {
 #endif
 
-#define BB_ABI_VERSION 10
+#define BB_ABI_VERSION 11
 #define BB_NQ 17
 #define BB_NV 15
 #define BB_OBS 15
@@ -226,8 +226,9 @@ int bb_rollout_track(const float* reward_dev, const uint8_t* flags_dev, int done
  * pretrained encoder: Conv2d(1,32,3,s2,p1) BatchNorm2d LeakyReLU, Conv2d(32,32,3,
  * s2,p1) BatchNorm2d LeakyReLU, Flatten, Linear(8192,20) BatchNorm1d Tanh;
  * ballbot_rl/encoders/models.py:6-54 as loaded by policies/mlp_policy.py:51-125)
- * over n 64x64 depth images (image i at images_dev + i * image_stride floats,
- * 16-byte aligned).  train != 0: the BatchNorms normalise with the batch's
+ * over n 64x64 depth images (image i at images_dev + j * image_stride floats,
+ * 16-byte aligned, with j = i, or j = index_dev[i] when index_dev is not NULL:
+ * a minibatch read straight from the rollout buffer).  train != 0: the BatchNorms normalise with the batch's
  * statistics and update their running statistics and num_batches_tracked
  * (torch train mode, as SB3's policy.train() leaves them during PPO updates);
  * train == 0: the running statistics normalise (eval mode, the rollout).
@@ -247,9 +248,9 @@ typedef struct bb_encoder_params {
   int64_t* bn3_count;
 } bb_encoder_params;
 int bb_depth_encoder_workspace_bytes(int64_t n, int64_t* bytes);
-int bb_depth_encoder(const bb_encoder_params* params, const float* images_dev, int64_t image_stride, int64_t n,
-                     int height, int width, int train, float momentum, float eps, float* out_dev, int64_t out_stride,
-                     float* workspace_dev, int64_t workspace_bytes, void* stream);
+int bb_depth_encoder(const bb_encoder_params* params, const float* images_dev, int64_t image_stride,
+                     const int64_t* index_dev, int64_t n, int height, int width, int train, float momentum, float eps,
+                     float* out_dev, int64_t out_stride, float* workspace_dev, int64_t workspace_bytes, void* stream);
 /* copy terrain bank slot terrain_id (float32[293*293]) to host memory */
 int bb_get_hfield(bb_handle* h, int terrain_id, float* data_host);
 /* per-env terrain ids (device int32[n]) applied at the next reset */

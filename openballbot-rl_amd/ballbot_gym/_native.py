@@ -91,7 +91,7 @@ EXPORTS = [
     "bb_ppo_mlp_act", "bb_rollout_track", "bb_depth_encoder_workspace_bytes", "bb_depth_encoder",
 ]
 
-ABI_VERSION = 10  # include/ballbot_mi355x.h BB_ABI_VERSION
+ABI_VERSION = 11  # include/ballbot_mi355x.h BB_ABI_VERSION
 
 _lib = None
 
@@ -167,7 +167,7 @@ def _load(path: Path):
     L.bb_ppo_mlp_act.argtypes = [vp, C.POINTER(C.c_int32), vp, C.c_int, vp, C.c_int, vp, vp, vp, vp, vp, vp]
     L.bb_rollout_track.argtypes = [vp, vp, C.c_int, C.c_int] + [vp] * 8
     L.bb_depth_encoder_workspace_bytes.argtypes = [C.c_int64, C.POINTER(C.c_int64)]
-    L.bb_depth_encoder.argtypes = [C.POINTER(EncoderParams), vp, C.c_int64, C.c_int64, C.c_int, C.c_int, C.c_int,
+    L.bb_depth_encoder.argtypes = [C.POINTER(EncoderParams), vp, C.c_int64, vp, C.c_int64, C.c_int, C.c_int, C.c_int,
                                    C.c_float, C.c_float, vp, C.c_int64, vp, C.c_int64, vp]
     L.bb_kernel_ms.argtypes = [vp, C.POINTER(C.c_double), C.POINTER(C.c_int32)]
     for name in [n for n in EXPORTS if n not in ("bb_default_params", "bb_abi_version")]:

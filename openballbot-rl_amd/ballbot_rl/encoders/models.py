@@ -92,17 +92,21 @@ def fusable_encoder(enc: nn.Module) -> bool:
     return conv_ok and shapes_ok and bn_ok and act_ok and frozen and dtypes
 
 
-def fused_encoder_forward(enc: nn.Sequential, x: torch.Tensor) -> torch.Tensor:
+def fused_encoder_forward(enc: nn.Sequential, x: torch.Tensor, index: "torch.Tensor | None" = None) -> torch.Tensor:
     """bb_depth_encoder on x [n, 1, 64, 64] (cuda, fp32; a channel slice of the
     [n, 2, 64, 64] camera tensor is fine): the frozen encoder's output [n, 20] with
     torch's BatchNorm semantics for enc.training (train: batch statistics and a
-    running-statistics update; eval: running statistics).  No autograd graph."""
+    running-statistics update; eval: running statistics).  No autograd graph.
+    index (int64 [m], on the device): encode rows index[i] of x instead (a
+    minibatch gathered inside the kernel); the output has m rows."""
     import ctypes as C
 
     from ballbot_gym import _native as N
 
     c1, b1, _, c2, b2, _, _, fc, b3, _ = list(enc)
-    n = x.shape[0]
+    n = x.shape[0] if index is None else index.shape[0]
+    if index is not None and (index.dtype != torch.int64 or not index.is_contiguous() or index.device != x.device):
+        index = index.to(device=x.device, dtype=torch.int64).contiguous()
     if x.dim() != 4 or tuple(x.shape[1:]) != (1, 64, 64) or x.stride(3) != 1 or x.stride(2) != 64 \
             or x.stride(0) % 4 or x.data_ptr() % 16 or x.dtype != torch.float32:
         x = x.contiguous()
@@ -117,7 +121,8 @@ def fused_encoder_forward(enc: nn.Sequential, x: torch.Tensor) -> torch.Tensor:
     ws = torch.empty(int(nbytes.value) // 4 + 4, device=x.device)
     out = torch.empty(n, 20, device=x.device)
     stream = C.c_void_p(torch.cuda.current_stream(x.device).cuda_stream)
-    N.check(L.bb_depth_encoder(C.byref(p), C.c_void_p(x.data_ptr()), int(x.stride(0)), int(n), 64, 64,
+    N.check(L.bb_depth_encoder(C.byref(p), C.c_void_p(x.data_ptr()), int(x.stride(0)),
+                               None if index is None else C.c_void_p(index.data_ptr()), int(n), 64, 64,
                                int(bool(enc.training)), float(b1.momentum), float(b1.eps), C.c_void_p(out.data_ptr()),
                                20, C.c_void_p(ws.data_ptr()), int(nbytes.value), stream), "bb_depth_encoder")
     return out

@@ -174,7 +174,9 @@ def fused_mlp_slots(ppo: "BatchedPPO", update: bool = True):
     fd = ext.features_dim
     if ppo.cameras:  # the camera features must come from fused frozen encoders (no trainable extractor)
         rgbd = {k for k in ext.keys if "rgbd_" in k}
-        if fd != 56 or ext._frozen_keys != rgbd or any(p.requires_grad for p in ext.parameters()):
+        order = ["actions", "angular_vel", "motor_state", "orientation", "relative_image_timestamp", "rgbd_0", "rgbd_1",
+                 "vel"]  # the feature layout _UpdateGraphs assembles for the fused minibatch
+        if fd != 56 or ext.keys != order or ext._frozen_keys != rgbd or any(p.requires_grad for p in ext.parameters()):
             return None
     elif fd != 15:
         return None
@@ -300,11 +302,21 @@ class _UpdateGraphs:
         self._args = a
         dev = ppo.device
 
+        ext = ppo.policy.features_extractor
+
         def mb_step():
-            if cams:
+            if cams:  # the Extractor's sorted-key concatenation, the images read through idx by the kernel
+                from ballbot_rl.encoders.models import fused_encoder_forward
+
                 idx = self.perm.index_select(0, self.k).view(-1)
-                with torch.no_grad():
-                    self.feats.copy_(ppo.policy.features_extractor(ppo._mb_obs(d, idx)))
+                o15 = d["obs"][idx]
+                f = self.feats
+                f[:, 0:12].copy_(o15[:, 0:12])              # actions, angular_vel, motor_state, orientation
+                f[:, 12].copy_(d["rel_ts"][idx])            # relative_image_timestamp
+                for c, key in enumerate(("rgbd_0", "rgbd_1")):
+                    f[:, 13 + 20 * c:33 + 20 * c].copy_(
+                        fused_encoder_forward(ext.extractors[key], d["depth"][:, c:c + 1], index=idx))
+                f[:, 53:56].copy_(o15[:, 12:15])            # vel
             stream = C.c_void_p(torch.cuda.current_stream(dev).cuda_stream)
             N.check(lib.bb_ppo_mlp_step(C.byref(a), stream), "bb_ppo_mlp_step")
 

@@ -31,6 +31,7 @@ struct EncArgs {
   EncParams p;
   const float* images;     // image i at images + i * image_stride, 64x64 row-major
   long long image_stride;  // floats
+  const long long* index;  // NULL, or image i is row index[i] of images (a minibatch gather)
   long long n;
   int train;
   float momentum, eps;

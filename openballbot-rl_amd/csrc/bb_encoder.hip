@@ -47,6 +47,11 @@ __device__ __forceinline__ f32x16 mfma(float a, float b, f32x16 c) {
 __device__ __forceinline__ int crow(int reg, int lane) { return (reg & 3) + 8 * (reg >> 2) + 4 * (lane >> 5); }
 __device__ __forceinline__ float leaky(float z) { return z > 0.f ? z : z * SLOPE; }
 
+// image b of the batch: row index[b] of the image array when an index is given
+__device__ __forceinline__ const float* image_of(const EncArgs& a, long long b) {
+  return a.images + (a.index ? a.index[b] : b) * a.image_stride;
+}
+
 __device__ __forceinline__ void stage_image(float (*x)[IW], const float* img) {
   for (int e = threadIdx.x; e < IH * IW / 4; e += 256)
     reinterpret_cast<float4*>(&x[0][0])[e] = reinterpret_cast<const float4*>(img)[e];
@@ -91,7 +96,7 @@ __global__ __launch_bounds__(256) void conv1_moments_kernel(EncArgs a) {
     const long long b = (long long)blockIdx.x * MOM_IMGS + i;
     if (b >= a.n) break;
     __syncthreads();
-    stage_image(x, a.images + b * a.image_stride);
+    stage_image(x, image_of(a, b));
     __syncthreads();
 #pragma unroll
     for (int j = 0; j < H1 * H1 / 256; j++) {
@@ -228,7 +233,7 @@ __global__ __launch_bounds__(512) void conv2_kernel(EncArgs a) {
     __syncthreads();
     if (valid)
       for (int e = t8; e < IH * IW / 4; e += 256)
-        reinterpret_cast<float4*>(&x[sub][0][0])[e] = reinterpret_cast<const float4*>(a.images + b * a.image_stride)[e];
+        reinterpret_cast<float4*>(&x[sub][0][0])[e] = reinterpret_cast<const float4*>(image_of(a, b))[e];
     f32x16 acc[2];
 #pragma unroll
     for (int q = 0; q < 2; q++)

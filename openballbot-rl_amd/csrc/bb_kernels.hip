@@ -920,9 +920,9 @@ int bb_depth_encoder_workspace_bytes(int64_t n, int64_t* bytes) {
   return 0;
 }
 
-int bb_depth_encoder(const bb_encoder_params* p, const float* images, int64_t image_stride, int64_t n, int height,
-                     int width, int train, float momentum, float eps, float* out, int64_t out_stride, float* ws,
-                     int64_t ws_bytes, void* stream) {
+int bb_depth_encoder(const bb_encoder_params* p, const float* images, int64_t image_stride, const int64_t* index,
+                     int64_t n, int height, int width, int train, float momentum, float eps, float* out,
+                     int64_t out_stride, float* ws, int64_t ws_bytes, void* stream) {
   if (!p || !images || !out || !ws) return fail("bb_depth_encoder: NULL argument");
   if (!p->conv1_w || !p->conv1_b || !p->bn1_w || !p->bn1_b || !p->bn1_mean || !p->bn1_var || !p->conv2_w ||
       !p->conv2_b || !p->bn2_w || !p->bn2_b || !p->bn2_mean || !p->bn2_var || !p->fc_w || !p->fc_b || !p->bn3_w ||
@@ -940,7 +940,8 @@ int bb_depth_encoder(const bb_encoder_params* p, const float* images, int64_t im
                   reinterpret_cast<long long*>(p->bn1_count), p->conv2_w, p->conv2_b, p->bn2_w, p->bn2_b,
                   p->bn2_mean, p->bn2_var, reinterpret_cast<long long*>(p->bn2_count), p->fc_w, p->fc_b, p->bn3_w,
                   p->bn3_b, p->bn3_mean, p->bn3_var, reinterpret_cast<long long*>(p->bn3_count)};
-  a.images = images; a.image_stride = image_stride; a.n = n; a.train = train ? 1 : 0;
+  a.images = images; a.image_stride = image_stride; a.index = reinterpret_cast<const long long*>(index);
+  a.n = n; a.train = train ? 1 : 0;
   a.momentum = momentum; a.eps = eps; a.out = out; a.out_stride = out_stride;
   if (launch_encoder(a, ws, (hipStream_t)stream))
     return fail("bb_depth_encoder: launch failed: %s", hipGetErrorString(hipGetLastError()));

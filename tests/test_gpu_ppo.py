@@ -585,3 +585,22 @@ def test_fused_camera_policy_matches_autograd(monkeypatch):
         assert torch.allclose(p.double(), q.double(), rtol=1e-4, atol=1e-5)
     for env in envs:
         env.close()
+
+
+def test_fused_encoder_index_gather():
+    """bb_depth_encoder reading a minibatch through an index == encoding the gathered images."""
+    import copy
+
+    from ballbot_rl.encoders.models import fused_encoder_forward
+
+    enc = _random_frozen_encoder(6)
+    enc2 = copy.deepcopy(enc)
+    enc.train(); enc2.train()
+    cams = torch.rand(700, 2, 64, 64, device="cuda:0")
+    idx = torch.randperm(700, device="cuda:0")[:512]
+    a = fused_encoder_forward(enc, cams[:, 1:2], index=idx)
+    b = fused_encoder_forward(enc2, cams[idx][:, 1:2].contiguous())
+    torch.cuda.synchronize()
+    assert torch.equal(a, b)
+    for p, q in zip(enc.buffers(), enc2.buffers()):
+        assert torch.equal(p, q)
