@@ -198,27 +198,33 @@ __global__ __launch_bounds__(256) void bn_finish_kernel(const double* part, int 
   scale_shift[C + c] = beta[c] - mean * sc;
 }
 
-// ---- 3. conv2 as an implicit GEMM; two images per workgroup (waves 0-3 and
-// 4-7, 2 waves per SIMD to hide each other's latency), grid-stride over image
-// pairs.  Per image: the image in LDS, then four times (input channels 8q..8q+7):
-// conv1 + BN1 + LeakyReLU of those channels into LDS, and 36 MFMA steps per
-// 32-position block.  Wave w of an image owns position blocks 2w, 2w+1.
-constexpr int QCH = 8;  // conv1 channels per LDS pass
+// ---- 3. conv2 as an implicit GEMM, producer/consumer.  One 512-thread
+// workgroup per CU walks its images (grid-stride) in items of 8 input channels
+// (4 items per image).  Waves 0-3 produce: conv1 + BN1 + LeakyReLU of item s's
+// channels into LDS buffer s&1, each thread keeping its 4 positions' 3x3 input
+// windows in registers for the whole image (read from global/L2, no LDS copy of
+// the image).  Waves 4-7 consume item s-1 from buffer (s-1)&1 with MFMA: wave w
+// owns position blocks 2w, 2w+1 (36 MFMA steps each per item).  A producer and a
+// consumer wave share each SIMD, so the VALU work hides under the MFMAs.
+constexpr int QCH = 8;  // conv1 channels per item
 
 __global__ __launch_bounds__(512) void conv2_kernel(EncArgs a) {
-  __shared__ __attribute__((aligned(16))) float x[2][IH][IW];
-  __shared__ float a1[2][QCH * CS];   // QCH channels of the activated conv1 output, per image
+  __shared__ float a1[2][QCH * CS];   // the activated conv1 output of one item, double-buffered
   __shared__ float w2t[K2][C1];       // conv2 weights, [ic*9 + tap][oc]
   __shared__ float ss1[2 * C1];
-  __shared__ double red[8][C1][2];
-  const int t = threadIdx.x, sub = t >> 8, t8 = t & 255, lane = t & 63, w = (t >> 6) & 3, hh = lane >> 5;
-  const int oc = lane & 31;
+  __shared__ double red[4][C1][2];
+  const int t = threadIdx.x, lane = t & 63, wv = t >> 6, hh = lane >> 5, oc = lane & 31;
+  const bool producer = wv < 4;
+  const int w = wv & 3, t8 = t & 255;
   for (int e = t; e < K2 * C1; e += 512) {
     const int o = e / K2, k = e % K2;
     w2t[k][o] = a.p.w2[e];
   }
   if (t < 2 * C1) ss1[t] = a.ws.ss1[t];
+  __syncthreads();
   const float b2 = a.p.b2[oc];
+  const long long nimg = a.n > blockIdx.x ? (a.n - 1 - blockIdx.x) / gridDim.x + 1 : 0;
+  const long long nitems = 4 * nimg;
   double s = 0.0, s2 = 0.0;
   int py[2], px[2];
 #pragma unroll
@@ -227,37 +233,51 @@ __global__ __launch_bounds__(512) void conv2_kernel(EncArgs a) {
     py[q] = pos >> 4;
     px[q] = pos & 15;
   }
-  for (long long base = 2LL * blockIdx.x; base < a.n; base += 2LL * gridDim.x) {
-    const long long b = base + sub;
-    const bool valid = b < a.n;
-    __syncthreads();
-    if (valid)
-      for (int e = t8; e < IH * IW / 4; e += 256)
-        reinterpret_cast<float4*>(&x[sub][0][0])[e] = reinterpret_cast<const float4*>(image_of(a, b))[e];
-    f32x16 acc[2];
+  float xw[H1 * H1 / 256][9];  // producer: the input windows of its 4 positions
+  f32x16 acc[2];
+  for (long long st = 0; st <= nitems; st++) {
+    if (producer && st < nitems) {
+      const long long b = blockIdx.x + (st >> 2) * (long long)gridDim.x;
+      const int quarter = int(st & 3), buf = int(st & 1);
+      if (quarter == 0) {
+        const float* img = image_of(a, b);
 #pragma unroll
-    for (int q = 0; q < 2; q++)
+        for (int j = 0; j < H1 * H1 / 256; j++) {
+          const int pos = t8 + 256 * j, oy = pos >> 5, ox = pos & 31;
 #pragma unroll
-      for (int r = 0; r < 16; r++) acc[q][r] = b2;
-    for (int quarter = 0; quarter < C1 / QCH; quarter++) {
-      __syncthreads();  // image staged / previous pass consumed
+          for (int ky = 0; ky < 3; ky++)
 #pragma unroll
-      for (int j = 0; j < H1 * H1 / 256; j++) {  // 4 positions per thread, each window read once
+            for (int kx = 0; kx < 3; kx++) {
+              const int iy = 2 * oy + ky - 1, ix = 2 * ox + kx - 1;
+              xw[j][ky * 3 + kx] = (iy >= 0 && ix >= 0) ? img[iy * IW + ix] : 0.f;
+            }
+        }
+      }
+#pragma unroll
+      for (int j = 0; j < H1 * H1 / 256; j++) {
         const int pos = t8 + 256 * j;
-        float xv[9];
-        window(x[sub], pos, xv);
 #pragma unroll
         for (int icl = 0; icl < QCH; icl++) {  // uniform channel: scalar weight loads
           const int ic = QCH * quarter + icl;
-          a1[sub][icl * CS + pos] = leaky(fmaf(conv1_win(xv, a.p.w1 + ic * 9, a.p.b1[ic]), ss1[ic], ss1[C1 + ic]));
+          a1[buf][icl * CS + pos] = leaky(fmaf(conv1_win(xw[j], a.p.w1 + ic * 9, a.p.b1[ic]), ss1[ic], ss1[C1 + ic]));
         }
       }
-      __syncthreads();
+    }
+    if (!producer && st >= 1) {
+      const long long it = st - 1;
+      const long long b = blockIdx.x + (it >> 2) * (long long)gridDim.x;
+      const int quarter = int(it & 3), buf = int(it & 1);
+      if (quarter == 0) {
+#pragma unroll
+        for (int q = 0; q < 2; q++)
+#pragma unroll
+          for (int r = 0; r < 16; r++) acc[q][r] = b2;
+      }
       // K order: step (icp, tap): lane half hh takes input channel 2 icp + hh
 #pragma unroll
       for (int icp = 0; icp < QCH / 2; icp++) {
         const int icl = 2 * icp + hh, ic = QCH * quarter + icl;
-        const float* ach = a1[sub] + icl * CS;
+        const float* ach = a1[buf] + icl * CS;
 #pragma unroll
         for (int tap = 0; tap < 9; tap++) {
           const int ky = tap / 3, kx = tap % 3;
@@ -270,35 +290,36 @@ __global__ __launch_bounds__(512) void conv2_kernel(EncArgs a) {
           }
         }
       }
-    }
-    if (!valid) continue;
-    // raw conv2 output, flattened (C, H, W): column = channel, rows = positions
-    float* out = a.ws.out2 + b * FL;
+      if (quarter == 3) {  // raw conv2 output, flattened (C, H, W): column = channel, rows = positions
+        float* out = a.ws.out2 + b * FL;
 #pragma unroll
-    for (int q = 0; q < 2; q++) {
-      float fs = 0.f, fs2 = 0.f;
+        for (int q = 0; q < 2; q++) {
+          float fs = 0.f, fs2 = 0.f;
 #pragma unroll
-      for (int r = 0; r < 16; r++) {
-        const int pos = (2 * w + q) * 32 + crow(r, lane);
-        const float v = acc[q][r];
-        out[oc * (H2 * H2) + pos] = v;
-        fs += v;
-        fs2 += v * v;
+          for (int r = 0; r < 16; r++) {
+            const int pos = (2 * w + q) * 32 + crow(r, lane);
+            const float v = acc[q][r];
+            out[oc * (H2 * H2) + pos] = v;
+            fs += v;
+            fs2 += v * v;
+          }
+          s += fs;
+          s2 += fs2;
+        }
       }
-      s += fs;
-      s2 += fs2;
     }
+    __syncthreads();
   }
   if (a.train) {
-    s += __shfl_xor(s, 32, 64);
-    s2 += __shfl_xor(s2, 32, 64);
-    if (hh == 0) { red[t >> 6][oc][0] = s; red[t >> 6][oc][1] = s2; }
+    if (!producer) {
+      s += __shfl_xor(s, 32, 64);
+      s2 += __shfl_xor(s2, 32, 64);
+      if (hh == 0) { red[w][oc][0] = s; red[w][oc][1] = s2; }
+    }
     __syncthreads();
     if (t < 2 * C1) {
       const int c = t >> 1, k = t & 1;
-      double v = 0.0;
-      for (int ww = 0; ww < 8; ww++) v += red[ww][c][k];
-      a.ws.part2[((long long)blockIdx.x * C1 + c) * 2 + k] = v;
+      a.ws.part2[((long long)blockIdx.x * C1 + c) * 2 + k] = (red[0][c][k] + red[1][c][k]) + (red[2][c][k] + red[3][c][k]);
     }
   }
 }
@@ -431,8 +452,7 @@ int launch_encoder(EncArgs a, float* ws, hipStream_t s) {
   if (a.n <= 0) return 0;
   a.ws = carve(ws, a.n, nullptr);
   const int g1 = int((a.n + MOM_IMGS - 1) / MOM_IMGS);
-  const long long pairs = (a.n + 1) / 2;
-  const int g2 = int(pairs < 256 ? pairs : 256);
+  const int g2 = int(a.n < 256 ? a.n : 256);
   if (a.train) {
     hipLaunchKernelGGL(conv1_moments_kernel, dim3(g1), dim3(256), 0, s, a);
     hipLaunchKernelGGL(bn1_moments_kernel, dim3(1), dim3(256), 0, s, a, g1);
