@@ -5,8 +5,9 @@
 // ~50 PyTorch/hipBLASLt launches of the autograd path.
 //
 // The policy (ballbot_rl/policies/mlp_policy.py:143-163, train.py:39-56):
-//   f = obs (15 floats, sorted-key proprio)
-//   pi: h1..h4 = leaky(h W^T + b), 15->128->128->128->128;  mean = h4 Wa^T + ba (3)
+//   f = obs: 15 sorted-key proprio floats, or the camera policy's 56 features
+//       (proprio, relative_image_timestamp, the two frozen-encoder outputs)
+//   pi: h1..h4 = leaky(h W^T + b), IN->128->128->128->128;  mean = h4 Wa^T + ba (3)
 //   vf: the same trunk shape;                               value = h4 Wv^T + bv (1)
 // The loss is bb_ppo.hip's (clipped surrogate, MSE value loss, entropy of a
 // state-independent log_std); its per-sample gradient needs only the
@@ -14,21 +15,23 @@
 // the same bits), so the gradient flows back through the tile that formed it.
 //
 // Launches (B = minibatch rows, tiles of 32 rows):
-//   1. mlp_tile_kernel   B/32 workgroups x 4 waves.  Wave w owns columns
-//      32w..32w+31 of every 128-wide layer; a layer is 64 (K=128) or 8 (K=16)
-//      v_mfma_f32_32x32x2_f32 per wave with the layer input read from an LDS
-//      tile (float4 per lane, k order permuted identically for A and B) and
-//      W from L2.  Activations stay in registers in the MFMA C layout (h1..h4
-//      of both trunks: 128 VGPRs) for the LeakyReLU backward; the heads and the
-//      loss run on the VALU.  Backward: dh_l = dz_{l+1} W_l (MFMA again).
-//      Layer inputs h_l and output gradients dz_{l+1} go to a workspace for
-//      launch 2; bias gradients and loss terms leave as per-tile partials.
-//   2. mlp_dw_kernel     dW_l = dz_{l+1}^T h_l as 32x32 MFMA blocks over
-//      K = B/8 row chunks, one wave per (layer, block, chunk): 896 waves at
-//      B = 8192.
-//   3. mlp_reduce_kernel sums the chunk/tile partials in a fixed order into the
-//      flat gradient buffer, g^2 per workgroup for the clip, the log row, and
-//      advances the minibatch/log-row counters (graph replays).
+//   1. mlp_tile_kernel<TRAIN, IN>  B/32 workgroups x 8 waves: waves 0-3 the pi
+//      trunk, 4-7 the vf trunk; wave w owns columns 32(w%4)..+31 of every
+//      128-wide layer.  A 128->128 layer is 64 v_mfma_f32_32x32x2_f32 per wave
+//      with the layer input read from an LDS tile (float4 per lane, k order
+//      permuted identically for A and B) and W from L2; the input layer takes
+//      (IN+1)/2 steps.  Activations stay in registers in the MFMA C layout for
+//      the LeakyReLU backward; the heads and the loss run on the VALU.
+//      Backward: dh_l = dz_{l+1} W_l (MFMA again).  Layer inputs h_l and output
+//      gradients dz_{l+1} go to a workspace for launch 2; loss terms leave as
+//      per-tile partials.  TRAIN = false is the rollout's policy step.
+//   2. mlp_dw_kernel     dW_l = dz_{l+1}^T h_l and db_l = dz_{l+1}^T 1 over
+//      row chunks: one workgroup per (layer, chunk) stages 32-row slabs of dz
+//      and h in LDS; wave w owns output rows 32w..32w+31, all columns.
+//   3. mlp_reduce_kernel sums the chunk partials in a fixed order into the
+//      flat gradient buffer, g^2 per workgroup for the clip, the log_std
+//      gradient, the log row, and advances the minibatch/log-row counters
+//      (graph replays).
 //   4-5. bb_ppo.hip's adamw_prep/adamw_update (clip factor from the partials).
 // fp32 throughout (the MFMA is exact f32); only summation orders differ from
 // autograd (tests/test_gpu_ppo.py: test_fused_minibatch_matches_autograd).
