@@ -30,6 +30,7 @@ broadcasts the new parameters.
 from __future__ import annotations
 
 import ctypes as C
+import os
 import time
 from collections import deque
 from typing import Any, Callable, Dict, Optional, Union
@@ -497,11 +498,30 @@ class BatchedPPO:
         ep_l = torch.empty(T, n, dtype=torch.int64, device=dev)
         b.starts[0].copy_(self._last_starts)
         stream = C.c_void_p(torch.cuda.current_stream(dev).cuda_stream)
+        # The cameras re-render an env every 6 steps (and at its reset): exactly the envs whose
+        # relative_image_timestamp is 0.  In eval mode the encoder is a fixed function of the
+        # image, so the other envs keep last step's camera features (bit-identical); the cache
+        # is rebuilt at every rollout start (the update moved the BatchNorm statistics).
+        from ballbot_rl.encoders.models import fused_encoder_forward
+
+        cache = os.environ.get("BB_ENC_CACHE", "1") != "0"
+        feats = torch.empty(n, 56, device=dev)
+        encs = (ext.extractors["rgbd_0"], ext.extractors["rgbd_1"])
         for t in range(T):
             b.obs[t].copy_(self._last_obs)
             b.depth[t].copy_(env.depth)
             b.rel_ts[t].copy_(env.rel_ts)
-            feats = ext(policy_obs(b.obs[t], b.depth[t], b.rel_ts[t])).contiguous()
+            feats[:, 0:12].copy_(b.obs[t][:, 0:12])
+            feats[:, 12].copy_(b.rel_ts[t])
+            feats[:, 53:56].copy_(b.obs[t][:, 12:15])
+            idx = None if (t == 0 or not cache) else torch.nonzero(b.rel_ts[t] == 0).view(-1)
+            if idx is None:
+                for c, enc in enumerate(encs):
+                    feats[:, 13 + 20 * c:33 + 20 * c].copy_(fused_encoder_forward(enc, b.depth[t][:, c:c + 1]))
+            elif idx.numel():
+                for c, enc in enumerate(encs):
+                    f = fused_encoder_forward(enc, b.depth[t][:, c:c + 1], index=idx)
+                    feats[:, 13 + 20 * c:33 + 20 * c].index_copy_(0, idx, f)
             N.check(lib.bb_ppo_mlp_act(flat, offs, _ptr(feats), int(feats.shape[1]), _ptr(noise[t]), n, None,
                                        _ptr(b.actions[t]), _ptr(clipped), _ptr(b.values[t]), _ptr(b.log_probs[t]),
                                        stream), "bb_ppo_mlp_act")

@@ -604,3 +604,28 @@ def test_fused_encoder_index_gather():
     assert torch.equal(a, b)
     for p, q in zip(enc.buffers(), enc2.buffers()):
         assert torch.equal(p, q)
+
+
+def test_camera_feature_cache_is_exact(monkeypatch):
+    """The camera rollout re-encodes only the envs whose cameras re-rendered this step
+    (relative_image_timestamp 0); the rollout buffers equal a full re-encode every step."""
+    import copy
+
+    from ballbot_gym.envs import BallbotVecEnv
+    from ballbot_rl.training.logger import CSVLogger
+    from ballbot_rl.training.ppo import BatchedPPO
+
+    enc = _random_frozen_encoder(7)
+    bufs = []
+    for cache in ("1", "0"):
+        monkeypatch.setenv("BB_ENC_CACHE", cache)
+        env = BallbotVecEnv(256, device="cuda:0", seed=9, disable_cameras=False, max_ep_steps=5)
+        m = BatchedPPO(env, n_steps=14, batch_size=512, seed=3, frozen_encoder=copy.deepcopy(enc),
+                       logger=CSVLogger(None, stdout=False))
+        m.collect_rollouts()
+        assert m._act_slots
+        bufs.append((m.buf.actions.clone(), m.buf.values.clone(), m.buf.rel_ts.clone()))
+        env.close()
+    (a0, v0, r0), (a1, v1, r1) = bufs
+    assert float((r0 == 0).float().mean()) < 0.5  # most steps reuse cached features
+    assert torch.equal(r0, r1) and torch.equal(a0, a1) and torch.equal(v0, v1)
