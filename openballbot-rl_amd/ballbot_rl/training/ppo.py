@@ -265,6 +265,14 @@ class _UpdateGraphs:
         self.graph = torch.cuda.CUDAGraph()
         with torch.cuda.graph(self.graph):
             mb_step()
+        # the fused proprio minibatch advances its own device counters, so a whole epoch
+        # (nb minibatches) is one graph as well: one host launch per epoch instead of nb
+        self.graph_epoch = None
+        if self.fused and "depth" not in self.data and self.nb > 1:
+            self.graph_epoch = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(self.graph_epoch):
+                for _ in range(self.nb):
+                    mb_step()
         torch.cuda.synchronize(dev)
         self._restore(opt, [p_snap, {i: st_snap.get(id(p)) for i, p in enumerate(params)}])
 
@@ -367,6 +375,10 @@ class _UpdateGraphs:
                 break
             self.perm.copy_(self.perms[e])
             self.k.zero_()
+            if self.graph_epoch is not None and rows - done >= self.nb:
+                self.graph_epoch.replay()
+                done += self.nb
+                continue
             for _ in range(min(self.nb, rows - done)):
                 self.graph.replay()
                 done += 1
