@@ -52,7 +52,7 @@ constexpr int XW_MAX = 64;        // workspace row width of the padded input
 constexpr int ROWS = 32;          // rows per tile (the MFMA M)
 constexpr int T1 = 512;           // threads per tile workgroup: 8 waves = 2 trunks x 4 column blocks
 constexpr int LDT = HID + 4;      // LDS row stride (floats): float4 rows, no bank conflicts
-constexpr int MAXCH = 32;         // max K chunks of the weight-gradient GEMMs
+constexpr int MAXCH = 64;         // max K chunks of the weight-gradient GEMMs
 constexpr int LPART = 8;          // loss partials per tile: pg, vf, kl, cf, dls[3], -
 constexpr int NJOB = 10;          // weight-gradient GEMMs: 2 trunks x 4 layers + 2 heads
 constexpr int NSEG = 2 * NJOB;    // gradient segments: weights and biases of each job
@@ -67,7 +67,7 @@ __device__ __forceinline__ f32x16 mfma(float a, float b, f32x16 c) {
 __device__ __forceinline__ int crow(int reg, int lane) { return (reg & 3) + 8 * (reg >> 2) + 4 * (lane >> 5); }
 __device__ __forceinline__ float leaky(float z) { return z > 0.f ? z : z * SLOPE; }
 
-// K chunks of the weight-gradient GEMMs: the most (<= 32) whose chunk is a
+// K chunks of the weight-gradient GEMMs: the most (<= MAXCH) whose chunk is a
 // whole number of SLAB-row slabs
 __host__ __device__ inline int n_chunks(int B) {
   for (int c = MAXCH; c > 1; c >>= 1)
@@ -554,8 +554,15 @@ __global__ __launch_bounds__(256) void mlp_reduce_kernel(ReduceArgs a) {
       if (e >= a.seg[k].first) q = k;
     const Seg S = a.seg[q];
     const int el = e - S.first;
-    float s = 0.f;
-    for (int c = 0; c < a.nch; c++) s += S.src[(long long)c * S.n + el];
+    // eight independent partial sums keep eight loads in flight (fixed order)
+    float p8[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+    int c = 0;
+    for (; c + 8 <= a.nch; c += 8) {
+#pragma unroll
+      for (int u = 0; u < 8; u++) p8[u] += S.src[(long long)(c + u) * S.n + el];
+    }
+    for (; c < a.nch; c++) p8[c & 7] += S.src[(long long)c * S.n + el];
+    const float s = ((p8[0] + p8[1]) + (p8[2] + p8[3])) + ((p8[4] + p8[5]) + (p8[6] + p8[7]));
     a.grad[S.dst + el] = s;
     g2 = s * s;
   }
