@@ -103,3 +103,30 @@ def test_argument_errors_without_gpu(native):
                       (lambda: L.bb_get_stats(None, None), "NULL argument")):
         assert call() < 0
         assert msg in _err(native), (msg, _err(native))
+
+
+def test_ctypes_structs_match_the_header(tmp_path, native):
+    """The ctypes mirrors of the header's structs (bb_ppo_mlp_args, bb_encoder_params)
+    have the C compiler's size and field offsets (gcc on the header, no GPU)."""
+    import shutil
+    import subprocess
+
+    if shutil.which("gcc") is None:
+        pytest.skip("gcc not available")
+    structs = {"bb_ppo_mlp_args": native.PPOMlpArgs, "bb_encoder_params": native.EncoderParams}
+    lines = ['#include <stdio.h>', '#include <stddef.h>', '#include "ballbot_mi355x.h"', 'int main(void) {']
+    for cname, py in structs.items():
+        lines.append(f'printf("{cname} size %zu\\n", sizeof({cname}));')
+        for field, _ in py._fields_:
+            lines.append(f'printf("{cname} {field} %zu\\n", offsetof({cname}, {field}));')
+    lines += ["return 0;", "}"]
+    src = tmp_path / "layout.c"
+    src.write_text("\n".join(lines))
+    exe = tmp_path / "layout"
+    subprocess.run(["gcc", "-I", str(ROOT / "include"), str(src), "-o", str(exe)], check=True)
+    out = subprocess.run([str(exe)], check=True, capture_output=True, text=True).stdout.split("\n")
+    got = {tuple(line.split()[:2]): int(line.split()[2]) for line in out if line.strip()}
+    for cname, py in structs.items():
+        assert got[(cname, "size")] == C.sizeof(py), cname
+        for field, _ in py._fields_:
+            assert got[(cname, field)] == getattr(py, field).offset, (cname, field)
