@@ -92,7 +92,7 @@ def parity_probe(env, n_probe: int = 64) -> dict:
     for e in range(min(n_probe, env.num_envs)):
         qe, ve, we, se = q[e].copy(), v[e].copy(), w[e].copy(), np.array([st[e]], np.int32)
         _, _, fl, _, _ = O.env_step(cfg, qe, ve, we, se, a[e], hf)
-        if fl & 5:  # terminated / diverged: reset on the GPU
+        if fl & 1:  # terminated: reset on the GPU
             continue
         eq.append(float(np.linalg.norm(q1[e] - qe)))
         ev.append(float(np.linalg.norm(v1[e] - ve)))
@@ -142,12 +142,12 @@ def main() -> None:
     dev = torch.device("cuda", gpu)
     torch.cuda.set_device(dev)
 
-    from ballbot_gym.distributed import env_shard, max_over_ranks, rank_seed
+    from ballbot_gym.distributed import env_shard, max_over_ranks
     from ballbot_gym.envs import BallbotVecEnv
 
     # weak scaling: every rank owns a contiguous block of `--envs` global env ids
     first_env, n = env_shard(args.envs * world, rank, world)
-    env = BallbotVecEnv(n, device=dev, precision=args.precision, seed=rank_seed(1000, first_env),
+    env = BallbotVecEnv(n, device=dev, precision=args.precision, seed=1000,  # one shared stream (train.py:82-89)
                         terrain_config={"type": args.terrain, "config": {}}, n_terrains=args.n_terrains,
                         disable_cameras=not args.cameras)
 

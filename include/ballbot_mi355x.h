@@ -8,7 +8,9 @@
  *                    (+ hfield_size[2] rescale                  ballbot_env.py:486-495)
  *                    (+ init height offset                      ballbot_env.py:527-565)
  *   bb_generate_perlin  generate_perlin_terrain per seed       terrain/perlin.py:8-74
- *   bb_assign_terrain   choice of terrain per env at reset      ballbot_env.py:501-513
+ *   bb_set_terrain_stream  r_seed = _np_random.integers(0, 10000) ballbot_env.py:378-384,
+ *                    at every reset, one generator per env        :505-510 (train.py:82-89)
+ *   bb_assign_terrain   pin a terrain per env (config seed)     ballbot_env.py:505-510
  *   bb_reset         mj_resetData + height offset + mj_forward  ballbot_env.py:612-620
  *   bb_step          ctrl = -clip(10a); mj_step; _get_obs;      ballbot_env.py:903-1036
  *                    reward plugin; termination
@@ -27,8 +29,12 @@
  *
  * Conventions
  *   - every function returns int: 0 ok, <0 error (bb_last_error has the text);
- *     per-env physics divergence is NOT an error, it is reported in done[]
- *     (bit 2) and the env is auto-reset, mirroring mj_checkPos/Vel/Acc.
+ *     per-env physics divergence is NOT an error.  As MuJoCo's mj_step does
+ *     (mj_checkPos/Vel at its start, mj_checkAcc after the first forward), a
+ *     NaN or |x| > 1e10 in qpos, qvel or qacc resets that env's data to qpos0
+ *     (no terrain height offset, zero velocity, warm start and ctrl) and the
+ *     step integrates from there; the episode goes on (no done), done[] bit 2
+ *     reports it.  A NaN ctrl zeroes all three controls (mjWARN_BADCTRL).
  *   - device pointers belong to the caller (e.g. torch tensors); the library
  *     never frees them.  Work is enqueued on the caller's stream (hipStream_t
  *     passed as void*); bb_step/bb_reset are graph-capturable.
@@ -47,22 +53,25 @@
 extern "C" {
 #endif
 
-#define BB_ABI_VERSION 11
+#define BB_ABI_VERSION 12
 #define BB_NQ 17
 #define BB_NV 15
 #define BB_OBS 15
 #define BB_HF_N 293
 
-/* done[] bits */
+/* done[] bits (only TERMINATED ends an episode) */
 #define BB_DONE_TERMINATED 1
 #define BB_DONE_FAILURE 2
-#define BB_DONE_DIVERGED 4
+#define BB_DONE_DIVERGED 4 /* MuJoCo's divergence reset ran inside this step (informational) */
 #define BB_DONE_OVERFLOW 8
+#define BB_NSTATS 7
 
 /* reward kinds (built-in reward plugins, ballbot_gym/rewards) */
 #define BB_REWARD_DIRECTIONAL 0 /* rewards/directional.py:33-54 */
 #define BB_REWARD_DISTANCE 1    /* rewards/distance.py:33-50 (pos2d-based) */
-#define BB_REWARD_NONE 2        /* custom plugin evaluated host-side */
+#define BB_REWARD_NONE 2        /* custom plugin evaluated host-side: reward_dev gets the action penalty
+                                   only; the caller adds plugin * scale, then the survival bonus when
+                                   done bit 1 (failure) is clear (ballbot_env.py:929-937, 1019-1020) */
 
 typedef struct bb_handle bb_handle;
 
@@ -79,7 +88,7 @@ typedef struct {
   float goal[2];               /* distance reward goal */
   float goal_scale;            /* distance reward scale */
   int n_terrains;              /* terrain bank size (>= 1) */
-  uint64_t seed;               /* per-env terrain draws at auto-reset */
+  uint64_t seed;               /* unused since ABI 12 (terrain draws: bb_set_terrain_stream) */
   int fp64;                    /* 1 (default): fp64 arithmetic, 0: fp32 */
   int solver_maxiter;          /* 0 = default */
   double solver_tol;           /* 0 = default */
@@ -207,8 +216,9 @@ int bb_ppo_mlp_step(const bb_ppo_mlp_args* args, void* stream);
  * (unclipped, as SB3 stores them), values_dev [n], log_prob_dev [n], and
  * optionally clipped_dev [n][3] (clip to the [-1, 1] action space, what
  * env.step receives) and obs_copy_dev [n][15] (the rollout buffer's copy).
- * params_dev/offsets as for bb_ppo_mlp_step.  One launch; graph-capturable. */
-int bb_ppo_mlp_act(const float* params_dev, const int32_t* offsets, const float* obs_dev, int obs_dim,
+ * params_dev/offsets/n_params as for bb_ppo_mlp_step (every slot must lie inside
+ * the n_params-float buffer).  One launch; graph-capturable. */
+int bb_ppo_mlp_act(const float* params_dev, const int32_t* offsets, int64_t n_params, const float* obs_dev, int obs_dim,
                    const float* noise_dev, int n,
                    float* obs_copy_dev, float* actions_dev, float* clipped_dev, float* values_dev, float* log_prob_dev,
                    void* stream);
@@ -253,8 +263,24 @@ int bb_depth_encoder(const bb_encoder_params* params, const float* images_dev, i
                      float* out_dev, int64_t out_stride, float* workspace_dev, int64_t workspace_bytes, void* stream);
 /* copy terrain bank slot terrain_id (float32[293*293]) to host memory */
 int bb_get_hfield(bb_handle* h, int terrain_id, float* data_host);
-/* per-env terrain ids (device int32[n]) applied at the next reset */
+/* pin per-env terrain ids (device int32[n]) for every later reset; an id
+ * outside [0, n_terrains) (e.g. -1) unpins the env (it draws from its stream
+ * again).  A pinned reset takes no stream draw (a fixed config seed,
+ * ballbot_env.py:505-510). */
 int bb_assign_terrain(bb_handle* h, const int32_t* ids_dev, void* stream);
+/* terrain seed streams (ballbot_env.py:378-384, 505-510): each reset of env e
+ * that is not pinned takes the next draw of stream env_stream_host[e] (NULL:
+ * all envs stream 0, n_streams must be 1): the k-th reset of the env (k = 0 at
+ * the first reset after this call) gets bank slot slots_host[s * length + k],
+ * i.e. the slot holding the terrain of the k-th value of the stream's
+ * np_random(seed).integers(0, 10000).  Past `length` draws the stream wraps
+ * around (counted in stats[5]).  Resets every env's draw counter to 0.
+ * n_streams = 0 removes the streams (unpinned envs then reset onto slot 0).
+ * Synchronous; a HIP graph captured before this call keeps the old streams. */
+int bb_set_terrain_stream(bb_handle* h, const int32_t* slots_host, int n_streams, int length,
+                          const int32_t* env_stream_host);
+/* current bank slot and number of stream draws of every env (host int32[n] each, may be NULL) */
+int bb_get_env_terrain(bb_handle* h, int32_t* terrain_host, int32_t* draws_host);
 
 /* reset envs where mask_dev[i] != 0 (mask NULL = all); writes reset obs */
 int bb_reset(bb_handle* h, const uint8_t* mask_dev, float* obs_dev, void* stream);
@@ -270,11 +296,13 @@ int bb_step(bb_handle* h, const float* actions_dev, float* obs_dev, float* rewar
 int bb_get_state(bb_handle* h, double* qpos, double* qvel, double* warm, int32_t* steps);
 int bb_set_state(bb_handle* h, const double* qpos, const double* qvel, const double* warm, const int32_t* steps);
 int bb_forward(bb_handle* h, const double* ctrl, double* qacc, int32_t* ncontact);
-/* counters since create: [resets, diverged, overflow (env-steps where a geom pair hit MuJoCo's
- * mjMAXCONPAIR = 50 contacts and was truncated, as MuJoCo does), slow-path env-steps (envs the fast
- * kernel handed to the full kernel: base-tree geom contacts possible), solver_iters_lo,
- * solver_iters_hi] */
-int bb_get_stats(bb_handle* h, int64_t* out6);
+/* the first n (<= BB_NSTATS) counters since create: [auto-resets, divergence resets (env-steps
+ * with done bit 2), overflow (env-steps where a geom pair hit MuJoCo's mjMAXCONPAIR = 50 contacts and
+ * was truncated, as MuJoCo does), slow-path env-steps (envs the fast kernel handed to the full
+ * kernel: base-tree geom contacts possible), Newton iterations, resets past the end of their
+ * terrain stream, env-steps whose last RK stage stored base-tree contacts past the 32 LDS slots
+ * (the per-env HBM spill block)] */
+int bb_get_stats(bb_handle* h, int64_t* out, int n);
 /* launch configuration: [n_envs, envs_per_wave, fp64, lds_bytes_per_workgroup,
  * lanes_per_env] */
 int bb_get_config(bb_handle* h, int32_t* out5);

@@ -16,6 +16,7 @@ INCLUDE = PKG.parent.parent / "include"
 
 NQ, NV, NOBS, HF_N = 17, 15, 15, 293
 DONE_TERMINATED, DONE_FAILURE, DONE_DIVERGED, DONE_OVERFLOW = 1, 2, 4, 8
+NSTATS = 7  # BB_NSTATS
 REWARD_DIRECTIONAL, REWARD_DISTANCE, REWARD_NONE = 0, 1, 2
 
 
@@ -89,9 +90,10 @@ EXPORTS = [
     "bb_get_offsets", "bb_get_config", "bb_time_kernel", "bb_kernel_ms", "bb_generate_perlin", "bb_get_hfield",
     "bb_gae", "bb_render_depth", "bb_ppo_loss", "bb_adamw_clip", "bb_ppo_mlp_workspace_bytes", "bb_ppo_mlp_step",
     "bb_ppo_mlp_act", "bb_rollout_track", "bb_depth_encoder_workspace_bytes", "bb_depth_encoder",
+    "bb_set_terrain_stream", "bb_get_env_terrain",
 ]
 
-ABI_VERSION = 11  # include/ballbot_mi355x.h BB_ABI_VERSION
+ABI_VERSION = 12  # include/ballbot_mi355x.h BB_ABI_VERSION
 
 _lib = None
 
@@ -152,7 +154,9 @@ def _load(path: Path):
     L.bb_get_state.argtypes = [vp, dp, dp, dp, C.POINTER(C.c_int32)]
     L.bb_set_state.argtypes = [vp, dp, dp, dp, C.POINTER(C.c_int32)]
     L.bb_forward.argtypes = [vp, dp, dp, C.POINTER(C.c_int32)]
-    L.bb_get_stats.argtypes = [vp, C.POINTER(C.c_int64)]
+    L.bb_get_stats.argtypes = [vp, C.POINTER(C.c_int64), C.c_int]
+    L.bb_set_terrain_stream.argtypes = [vp, C.POINTER(C.c_int32), C.c_int, C.c_int, C.POINTER(C.c_int32)]
+    L.bb_get_env_terrain.argtypes = [vp, C.POINTER(C.c_int32), C.POINTER(C.c_int32)]
     L.bb_get_offsets.argtypes = [vp, fp]
     L.bb_get_config.argtypes = [vp, C.POINTER(C.c_int32)]
     L.bb_time_kernel.argtypes = [vp, C.c_int]
@@ -164,7 +168,8 @@ def _load(path: Path):
     L.bb_gae.argtypes = [vp, vp, vp, vp, vp, C.c_int, C.c_int, C.c_double, C.c_double, vp, vp, vp]
     L.bb_ppo_mlp_workspace_bytes.argtypes = [C.c_int, C.POINTER(C.c_int64)]
     L.bb_ppo_mlp_step.argtypes = [C.POINTER(PPOMlpArgs), vp]
-    L.bb_ppo_mlp_act.argtypes = [vp, C.POINTER(C.c_int32), vp, C.c_int, vp, C.c_int, vp, vp, vp, vp, vp, vp]
+    L.bb_ppo_mlp_act.argtypes = [vp, C.POINTER(C.c_int32), C.c_int64, vp, C.c_int, vp, C.c_int, vp, vp, vp, vp, vp,
+                                 vp]
     L.bb_rollout_track.argtypes = [vp, vp, C.c_int, C.c_int] + [vp] * 8
     L.bb_depth_encoder_workspace_bytes.argtypes = [C.c_int64, C.POINTER(C.c_int64)]
     L.bb_depth_encoder.argtypes = [C.POINTER(EncoderParams), vp, C.c_int64, vp, C.c_int64, C.c_int, C.c_int, C.c_int,

@@ -8,7 +8,7 @@ benchmark and the gather of rollout buffers at a PPO update.
 """
 from __future__ import annotations
 
-from typing import Tuple
+from typing import List, Optional, Tuple
 
 import torch
 import torch.distributed as dist
@@ -25,9 +25,16 @@ def env_shard(num_envs_total: int, rank: int, world: int) -> Tuple[int, int]:
     return start, base + (1 if rank < extra else 0)
 
 
-def rank_seed(seed: int, first_env: int) -> int:
-    """Seed of a rank's env block: offset by its first global env id."""
-    return int(seed) + int(first_env)
+def shard_stream_seeds(seed: int, first_env: int, count: int, per_env: bool = False) -> Optional[List[int]]:
+    """Terrain seed streams of a rank's env block (BallbotVecEnv stream_seeds).
+
+    Training envs all draw from np_random(seed) (eval_env=[True, seed] for every
+    env, train.py:82-89): None, i.e. every local env on that one stream, the
+    same on every rank.  per_env: global env g draws from np_random(seed + g),
+    the eval VecEnv's seed + N_ENVS + env_i (train.py:90-97) with seed the base."""
+    if not per_env:
+        return None
+    return [int(seed) + int(first_env) + i for i in range(int(count))]
 
 
 def max_over_ranks(value: float, device=None) -> float:

@@ -10,7 +10,7 @@ GPU; `step` takes and returns torch tensors on `device`.
 from __future__ import annotations
 
 import ctypes as C
-from typing import Any, Dict, Optional
+from typing import Any, Dict, Optional, Sequence
 
 import numpy as np
 import torch
@@ -29,9 +29,19 @@ class BallbotVecEnv:
 
     Args mirror BBotSimulation (ballbot_env.py:157-231) plus `num_envs`,
     `device`, `precision` ("fp32" | "fp64") and the terrain bank size.
+
+    Terrain seeds follow the reference's per-reset draw r_seed =
+    _np_random.integers(0, 10000) (ballbot_env.py:505-510) with the generator
+    fixed at construction (eval_env=[True, seed], :378-384): by default every
+    env shares np_random(seed), as train.py:82-89 builds all training envs, so
+    the k-th reset of every env gets the k-th draw; `stream_seeds` gives env i
+    its own generator np_random(stream_seeds[i]) (an eval VecEnv: seed + N + i,
+    train.py:90-97).  `n_terrains` is the number of draws per stream kept
+    resident (perlin default: the whole seed space on the GPU, 65536 draws).
     """
 
     metadata = {"render_modes": []}
+    render_mode = None
 
     def __init__(
         self,
@@ -46,8 +56,10 @@ class BallbotVecEnv:
         n_terrains: Optional[int] = None,
         auto_reset: bool = True,
         disable_cameras: bool = True,
+        stream_seeds: Optional[Sequence[int]] = None,
+        terrain_draws: Optional[Sequence[int]] = None,
     ):
-        from .config import TERRAIN_SEED_HIGH, gpu_perlin_plan, np_random, params_from_configs, terrain_bank
+        from .config import bank_fields, gpu_perlin_plan, params_from_configs, terrain_plan
 
         if not torch.cuda.is_available():
             raise RuntimeError("BallbotVecEnv needs a ROCm GPU (torch.cuda.is_available() is False)")
@@ -71,14 +83,18 @@ class BallbotVecEnv:
         p, self.reward_obj, self._host_reward = params_from_configs(self.reward_config, env_config, max_ep_steps,
                                                                     precision, seed)
         self.max_ep_steps = int(p.max_ep_steps)
-        plan = gpu_perlin_plan(self.terrain_config, n_terrains, seed)
-        if plan is None:
-            hfields, self.terrain_seeds, size_z = terrain_bank(self.terrain_config, n_terrains, seed)
-            bank = [(h, size_z) for h in hfields]
+        gp = gpu_perlin_plan(self.terrain_config, n_terrains, seed, self.num_envs, stream_seeds, terrain_draws)
+        if gp is None:
+            plan = terrain_plan(self.terrain_config, n_terrains, seed, self.num_envs, stream_seeds,
+                                draws=terrain_draws)
+            bank = [(h, plan.size_z) for h in bank_fields(self.terrain_config, plan)]
         else:  # perlin: generated on the GPU below
-            self.terrain_seeds, pcfg, size_z = plan
+            plan, pcfg = gp
             bank = []
-        p.n_terrains = len(bank) or len(self.terrain_seeds)
+        self.terrain_plan = plan
+        self.terrain_seeds = plan.seeds
+        size_z = plan.size_z
+        p.n_terrains = len(plan.seeds)
         self.precision = "fp64" if p.fp64 else "fp32"
         self._params = p
         L = N.lib()
@@ -88,7 +104,7 @@ class BallbotVecEnv:
         for i, (data, size_z) in enumerate(bank):
             arr = np.ascontiguousarray(data, dtype=np.float32)
             N.check(L.bb_set_hfield(h, i, arr.ctypes.data_as(C.POINTER(C.c_float)), float(size_z)), "bb_set_hfield")
-        if plan is not None:
+        if gp is not None:
             sd = np.ascontiguousarray(self.terrain_seeds, dtype=np.int32)
             N.check(L.bb_generate_perlin(h, 0, len(sd), sd.ctypes.data_as(C.POINTER(C.c_int32)), C.byref(pcfg),
                                          float(size_z)), "bb_generate_perlin")
@@ -102,16 +118,19 @@ class BallbotVecEnv:
         if self.cameras:
             self.depth = torch.ones(n, 2, self.cam_h, self.cam_w, dtype=torch.float32, device=dev)
             self.rel_ts = torch.zeros(n, dtype=torch.float32, device=dev)
-        if plan is not None and self.n_terrains == TERRAIN_SEED_HIGH:
-            # whole seed space resident (slot == seed): the first reset draws the
-            # reference's seed stream, integers(0, 10000) (ballbot_env.py:505-510)
-            ids = torch.from_numpy(np_random(seed).integers(0, TERRAIN_SEED_HIGH, size=n).astype(np.int32)).to(dev)
-            N.check(L.bb_assign_terrain(h, _ptr(ids), self._stream()), "bb_assign_terrain")
-        elif self.n_terrains > 1:
-            g = torch.Generator(device="cpu").manual_seed(int(seed))
-            ids = torch.randint(0, self.n_terrains, (n,), generator=g, dtype=torch.int32).to(dev)
-            N.check(L.bb_assign_terrain(h, _ptr(ids), self._stream()), "bb_assign_terrain")
-        self.reset()
+        if plan.streams is not None:  # every later reset takes its stream's next draw
+            st = np.ascontiguousarray(plan.streams, dtype=np.int32)
+            es = None if plan.env_stream is None else np.ascontiguousarray(plan.env_stream, dtype=np.int32)
+            ip = C.POINTER(C.c_int32)
+            N.check(L.bb_set_terrain_stream(h, st.ctypes.data_as(ip), st.shape[0], st.shape[1],
+                                            None if es is None else es.ctypes.data_as(ip)), "bb_set_terrain_stream")
+        from .. import spaces
+
+        # SB3 VecEnv / gymnasium attributes (ballbot_env.py:235-256)
+        self.action_space = spaces.action_space()
+        self.observation_space = spaces.observation_space({"h": self.cam_h, "w": self.cam_w}, 1, not self.cameras)
+        self._pending_actions: Optional[torch.Tensor] = None
+        self.reset()  # the first reset: draw 0 of every env's stream
 
     # --------------------------------------------------------------------- api
     def _stream(self):
@@ -151,7 +170,7 @@ class BallbotVecEnv:
                 "failure": (self.done & N.DONE_FAILURE) != 0}
         reward = self.reward
         if self._host_reward is not None:
-            reward = reward + self._host_reward_batch()
+            reward = self._plugin_reward(info["failure"])
         return self.obs, reward, terminated, torch.zeros_like(terminated), info
 
     def step_flags(self, actions: torch.Tensor):
@@ -198,17 +217,81 @@ class BallbotVecEnv:
         N.lib().bb_step(self._h, _ptr(actions), _ptr(self.obs), _ptr(self.reward), _ptr(self.done),
                         None, None, int(self.auto_reset), self._stream())
 
-    def _host_reward_batch(self) -> torch.Tensor:
-        """Custom reward plugins (BaseReward.__call__(state) -> float) evaluated
-        per env on the host from the terminal observation dict."""
-        obs = self.terminal_obs.cpu().numpy()
-        pos = self.pos2d.cpu().numpy()
-        out = np.zeros(self.num_envs, dtype=np.float32)
+    def _plugin_reward(self, failure: torch.Tensor) -> torch.Tensor:
+        """Reward of a custom plugin, in the reference's float32 order
+        (ballbot_env.py:929-937, 1019-1020): plugin(obs) * scale + action penalty
+        (the kernel's reward for BB_REWARD_NONE), then + survival bonus unless failed.
+        The plugin sees this step's observation (before any auto-reset) and pos2d."""
+        f32 = np.float32
+        hb = getattr(type(self._host_reward), "has_batched", None)
+        if hb is not None and hb():  # device path: one call, no host sync
+            st = {k: self.terminal_obs[:, 3 * i:3 * i + 3] for i, k in enumerate(OBS_KEYS)}
+            st["pos2d"] = self.pos2d
+            v = torch.as_tensor(self._host_reward.batched(st), device=self.device).to(torch.float32).reshape(-1)
+            if v.shape[0] != self.num_envs:
+                raise ValueError(f"{type(self._host_reward).__name__}.batched returned {v.shape[0]} rewards "
+                                 f"for {self.num_envs} envs")
+        else:  # compatibility path: BaseReward.__call__(state) per env on the host
+            obs = self.terminal_obs.cpu().numpy()
+            pos = self.pos2d.cpu().numpy()
+            out = np.zeros(self.num_envs, dtype=f32)
+            for i in range(self.num_envs):
+                state = split_obs(obs[i])
+                state["pos2d"] = pos[i]
+                out[i] = f32(self._host_reward(state))
+            v = torch.from_numpy(out).to(self.device)
+        r = v * f32(self._params.reward_scale) + self.reward
+        return torch.where(failure, r, r + f32(self._params.survival_bonus))
+
+    # ------------------------------------------------- SB3 VecEnv interface
+    def step_async(self, actions) -> None:
+        """VecEnv.step_async: remember the actions (torch [N,3] or numpy); step_wait runs the step."""
+        self._pending_actions = torch.as_tensor(actions, dtype=torch.float32, device=self.device)
+
+    def step_wait(self):
+        """VecEnv.step_wait -> (obs dict of [N,...] tensors, rewards [N], dones [N] bool, infos list).
+
+        dones = terminated (the reference never truncates); done envs were reset
+        in the same launch, their last observation is infos[i]["terminal_observation"]
+        (SB3's convention).  The per-env info dicts are host objects: the batched
+        trainer reads the tensors of step() instead."""
+        if self._pending_actions is None:
+            raise RuntimeError("step_wait() without step_async()")
+        obs, reward, term, trunc, info = self.step(self._pending_actions)
+        self._pending_actions = None
+        done = term | trunc
+        d_h = done.cpu().numpy()
+        fail = info["failure"].cpu().numpy()
+        p2 = info["pos2d"].cpu().numpy()
+        tob = info["terminal_observation"].cpu().numpy()
+        infos = []
         for i in range(self.num_envs):
-            state = split_obs(obs[i])
-            state["pos2d"] = pos[i]
-            out[i] = np.float32(self._host_reward(state)) * np.float32(self._params.reward_scale)
-        return torch.from_numpy(out).to(self.device)
+            inf = {"TimeLimit.truncated": False, "failure": bool(fail[i]), "success": False, "pos2d": p2[i]}
+            if d_h[i]:
+                inf["terminal_observation"] = split_obs(tob[i])
+            infos.append(inf)
+        return self.obs_dict(obs), reward, done, infos
+
+    def seed(self, seed: Optional[int] = None):
+        """VecEnv.seed: terrain streams are fixed at construction (the reference's eval_env
+        generators ignore reset seeds, ballbot_env.py:378-384, 596-599); seeds the action space."""
+        self.action_space.seed(seed)
+        return [seed] * self.num_envs
+
+    def get_attr(self, name: str, indices=None):
+        n = self.num_envs if indices is None else len(list(indices))
+        return [getattr(self, name)] * n
+
+    def set_attr(self, name: str, value, indices=None) -> None:
+        setattr(self, name, value)
+
+    def env_method(self, name: str, *args, indices=None, **kwargs):
+        n = self.num_envs if indices is None else len(list(indices))
+        return [getattr(self, name)(*args, **kwargs)] * n
+
+    def env_is_wrapped(self, wrapper_class, indices=None):
+        n = self.num_envs if indices is None else len(list(indices))
+        return [False] * n
 
     def obs_dict(self, obs: Optional[torch.Tensor] = None) -> Dict[str, torch.Tensor]:
         o = self.obs if obs is None else obs
@@ -254,10 +337,24 @@ class BallbotVecEnv:
         return qacc, ncon
 
     def stats(self) -> Dict[str, int]:
-        out = (C.c_int64 * 6)()
-        N.check(N.lib().bb_get_stats(self._h, out), "bb_get_stats")
+        out = (C.c_int64 * N.NSTATS)()
+        N.check(N.lib().bb_get_stats(self._h, out, N.NSTATS), "bb_get_stats")
         return {"resets": out[0], "diverged": out[1], "overflow": out[2], "slow_path": out[3],
-                "solver_iters": out[4] + (out[5] << 32)}
+                "solver_iters": out[4], "stream_wraps": out[5], "spill": out[6]}
+
+    def env_terrain(self):
+        """(bank slot of every env's current terrain, stream draws each env made) as int32[N] arrays."""
+        t = np.zeros(self.num_envs, np.int32)
+        k = np.zeros(self.num_envs, np.int32)
+        ip = C.POINTER(C.c_int32)
+        N.check(N.lib().bb_get_env_terrain(self._h, t.ctypes.data_as(ip), k.ctypes.data_as(ip)), "bb_get_env_terrain")
+        return t, k
+
+    def assign_terrain(self, ids) -> None:
+        """Pin env i to bank slot ids[i] for its later resets (-1 unpins: back to its stream)."""
+        t = torch.as_tensor(np.asarray(ids, np.int32)).to(self.device)
+        N.check(N.lib().bb_assign_terrain(self._h, _ptr(t), self._stream()), "bb_assign_terrain")
+        torch.cuda.current_stream(self.device).synchronize()
 
     def hfield(self, terrain_id: int) -> np.ndarray:
         """Terrain bank slot `terrain_id` as float32[293*293] (host copy)."""

@@ -32,7 +32,7 @@ def evaluate_policy(policy, env, n_eval_episodes: int = 8, deterministic: bool =
         a = policy.predict(obs, deterministic=deterministic)
         obs, r, term, trunc, info = env.step(a)
         flags = info.get("done_flags") if isinstance(info, dict) else None
-        done = (term | trunc) if flags is None else ((flags & 5) != 0) | trunc
+        done = (term | trunc) if flags is None else ((flags & 1) != 0) | trunc
         ret += torch.where(active, r.double(), torch.zeros_like(ret))
         length += active.long()
         active &= ~done

@@ -95,7 +95,11 @@ class Extractor(nn.Module):
         return torch.cat([self._extract(k, observations[k]) for k in self.keys], dim=1)
 
     def _extract(self, key: str, x: torch.Tensor) -> torch.Tensor:
-        if key in self._frozen_keys and x.is_cuda and os.environ.get("BB_FUSED_ENCODER", "1") != "0":
+        # the fused encoder has no autograd graph: an encoder unfrozen after construction
+        # (fine-tuning) goes through its torch modules so its gradients are kept
+        trainable = torch.is_grad_enabled() and any(p.requires_grad for p in self.extractors[key].parameters())
+        if (key in self._frozen_keys and x.is_cuda and not trainable
+                and os.environ.get("BB_FUSED_ENCODER", "1") != "0"):
             from ballbot_rl.encoders.models import fused_encoder_forward
 
             return fused_encoder_forward(self.extractors[key], x)

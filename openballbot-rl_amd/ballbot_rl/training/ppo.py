@@ -174,10 +174,13 @@ def fused_mlp_slots(ppo: "BatchedPPO", update: bool = True):
     ext = pol.features_extractor
     fd = ext.features_dim
     if ppo.cameras:  # the camera features must come from fused frozen encoders (no trainable extractor)
-        rgbd = {k for k in ext.keys if "rgbd_" in k}
+        keys, frozen = getattr(ext, "keys", None), getattr(ext, "_frozen_keys", None)
+        if keys is None or frozen is None:  # a custom extractor: the autograd path
+            return None
+        rgbd = {k for k in keys if "rgbd_" in k}
         order = ["actions", "angular_vel", "motor_state", "orientation", "relative_image_timestamp", "rgbd_0", "rgbd_1",
                  "vel"]  # the feature layout _UpdateGraphs assembles for the fused minibatch
-        if fd != 56 or ext.keys != order or ext._frozen_keys != rgbd or any(p.requires_grad for p in ext.parameters()):
+        if fd != 56 or keys != order or frozen != rgbd or any(p.requires_grad for p in ext.parameters()):
             return None
     elif fd != 15:
         return None
@@ -241,9 +244,14 @@ class _UpdateGraphs:
         self.clip = torch.zeros((), device=dev)
         self.log = torch.zeros(ppo.n_epochs * self.nb, self.LOG_COLS, device=dev)
         self.params = params = [p for p in ppo.policy.parameters() if p.requires_grad]
+        # BatchNorm running statistics and num_batches_tracked of the (frozen) encoders: a
+        # train-mode minibatch moves them, so the warm-up/capture below and the KL-stop
+        # replay must restore them with the parameters
+        self.buffers = [b for b in ppo.policy.buffers()]
         opt = ppo.optimizer
         p_snap = [p.detach().clone() for p in params]
         st_snap = {id(p): {k: v.clone() for k, v in opt.state[p].items()} for p in params if p in opt.state}
+        b_snap = [b.detach().clone() for b in self.buffers]
 
         slots = fused_mlp_slots(ppo)
         self.fused = slots is not None
@@ -274,7 +282,7 @@ class _UpdateGraphs:
                 for _ in range(self.nb):
                     mb_step()
         torch.cuda.synchronize(dev)
-        self._restore(opt, [p_snap, {i: st_snap.get(id(p)) for i, p in enumerate(params)}])
+        self._restore(opt, [p_snap, {i: st_snap.get(id(p)) for i, p in enumerate(params)}, b_snap])
 
     def _fused_step(self, ppo: "BatchedPPO", slots):
         """bb_ppo_mlp_step: the whole minibatch (forward, loss, backward, clip,
@@ -353,7 +361,8 @@ class _UpdateGraphs:
 
     def _snapshot(self, opt):
         return [[p.detach().clone() for p in self.params],
-                {i: {k: v.clone() for k, v in opt.state[p].items()} for i, p in enumerate(self.params)}]
+                {i: {k: v.clone() for k, v in opt.state[p].items()} for i, p in enumerate(self.params)},
+                [b.detach().clone() for b in self.buffers]]
 
     def _restore(self, opt, snap) -> None:
         with torch.no_grad():
@@ -366,6 +375,26 @@ class _UpdateGraphs:
                         v.copy_(prev[k])
                     else:
                         v.zero_()
+            for b, s_ in zip(self.buffers, snap[2]):
+                b.copy_(s_)
+
+    @torch.no_grad()
+    def _stats_forward(self, ppo: "BatchedPPO", row: int) -> None:
+        """SB3 evaluates the minibatch that trips the KL stop (train mode) before it
+        breaks: its BatchNorm statistics move once more, with no optimiser step."""
+        if not self.buffers:
+            return
+        e, k = divmod(row, self.nb)
+        idx = self.perms[e][k]
+        d = self.data
+        if self.fused and "depth" in d:
+            from ballbot_rl.encoders.models import fused_encoder_forward
+
+            ext = ppo.policy.features_extractor
+            for c, key in enumerate(("rgbd_0", "rgbd_1")):
+                fused_encoder_forward(ext.extractors[key], d["depth"][:, c:c + 1], index=idx)
+        else:
+            ppo.policy.features_extractor(ppo._mb_obs(d, idx))
 
     def _replay(self, rows: int) -> None:
         self.row.zero_()
@@ -400,9 +429,71 @@ class _UpdateGraphs:
                 r = int(trip[0])
                 self._restore(ppo.optimizer, snap)
                 self._replay(r)            # the steps before the tripping minibatch
+                self._stats_forward(ppo, r)  # ... and its own forward (BatchNorm statistics)
                 keep = log[:r + 1].copy()  # ... whose own terms SB3 still logs
                 return keep
         return log
+
+
+class _RolloutGraph:
+    """One proprio rollout -- n_steps x (bb_ppo_mlp_act, env.step_flags, bb_rollout_track)
+    -- captured as ONE HIP graph and replayed once per rollout (SB3 collect_rollouts).
+
+    A captured graph keeps the raw device pointers of everything its kernels read
+    and write.  Every such buffer is therefore owned here (the Gaussian noise, the
+    clipped actions, the finished-episode rows) or is a fixed buffer of the env,
+    the rollout buffer or the optimiser that lives as long as the graph.  The eager
+    loop allocates noise / clipped / ep_r / ep_l afresh per rollout: a capture of
+    that loop bakes in the first rollout's addresses, which the caching allocator
+    hands to other tensors -- or unmaps (empty_cache, an allocation retry under
+    memory pressure) -- once the rollout's tensors are freed, so a later replay
+    reads stale memory or faults with an illegal address.  That is how the
+    round-2 per-step capture could fault only when other tests ran beside it.
+    The env's step (routing, both step kernels on two streams) is captured as in
+    BallbotVecEnv.capture_step; the handle's counters and lists are written by
+    the graph's kernels in stream order, as in eager stepping."""
+
+    def __init__(self, ppo: "BatchedPPO", slots):
+        from ballbot_gym import _native as N
+
+        env, b, dev = ppo.env, ppo.buf, ppo.device
+        T, n = ppo.n_steps, ppo.n_envs
+        self.env, self.key = env, (id(env), T, n)
+        self.noise = torch.zeros(T, n, 3, device=dev)
+        self.clipped = torch.zeros(n, 3, device=dev)
+        self.ep_r = torch.zeros(T, n, dtype=torch.float64, device=dev)
+        self.ep_l = torch.zeros(T, n, dtype=torch.int64, device=dev)
+        self.flat = ppo.optimizer.flat
+        self.offs = (C.c_int32 * 21)(*slots)
+        lib = N.lib()
+        obs = env.obs  # step_flags returns the env's own observation buffer: read in place
+        flat, nflat = C.c_void_p(self.flat.data_ptr()), int(self.flat.numel())
+        torch.cuda.synchronize(dev)
+        self.graph = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(self.graph):
+            stream = C.c_void_p(torch.cuda.current_stream(dev).cuda_stream)
+            b.starts[0].copy_(ppo._last_starts)
+            for t in range(T):
+                N.check(lib.bb_ppo_mlp_act(flat, self.offs, nflat, _ptr(obs), 15, _ptr(self.noise[t]), n,
+                                           _ptr(b.obs[t]), _ptr(b.actions[t]), _ptr(self.clipped),
+                                           _ptr(b.values[t]), _ptr(b.log_probs[t]), stream), "bb_ppo_mlp_act")
+                o, reward, flags = env.step_flags(self.clipped)
+                if o.data_ptr() != obs.data_ptr() or not reward.is_contiguous():
+                    raise RuntimeError("rollout graph: env.step_flags must return its fixed buffers")
+                nxt = _ptr(b.starts[t + 1]) if t + 1 < T else None
+                N.check(lib.bb_rollout_track(_ptr(reward), _ptr(flags), 1, n, _ptr(b.rewards[t]),
+                                             _ptr(ppo._ep_ret), _ptr(ppo._ep_len), _ptr(self.ep_r[t]),
+                                             _ptr(self.ep_l[t]), _ptr(ppo._last_starts), nxt, stream),
+                        "bb_rollout_track")
+        torch.cuda.synchronize(dev)
+
+    def run(self, ppo: "BatchedPPO"):
+        if ppo._last_obs.data_ptr() != self.env.obs.data_ptr():
+            self.env.obs.copy_(ppo._last_obs)
+        self.noise.normal_(generator=ppo.gen)  # == torch.randn(T, n, 3, generator=gen): the eager draws
+        self.graph.replay()
+        ppo._last_obs = self.env.obs
+        return self.ep_r, self.ep_l
 
 
 class BatchedPPO:
@@ -469,6 +560,7 @@ class BatchedPPO:
         self._ep_len = torch.zeros(self.n_envs, dtype=torch.int64, device=self.device)
         self.progress_remaining = 1.0
         self._act_slots = None  # fused rollout policy step: slots, False (not eligible) or None (not checked)
+        self._rgraph: Optional[_RolloutGraph] = None
 
     # ------------------------------------------------------------ distributed
     def _sync_params(self) -> None:
@@ -500,6 +592,7 @@ class BatchedPPO:
         T, n = self.n_steps, self.n_envs
         offs = (C.c_int32 * 21)(*slots)
         flat = C.c_void_p(self.optimizer.flat.data_ptr())
+        nflat = int(self.optimizer.flat.numel())
         ext = self.policy.features_extractor
         self.policy.eval()
         if self._last_obs is None:
@@ -534,12 +627,12 @@ class BatchedPPO:
                 for c, enc in enumerate(encs):
                     f = fused_encoder_forward(enc, b.depth[t][:, c:c + 1], index=idx)
                     feats[:, 13 + 20 * c:33 + 20 * c].index_copy_(0, idx, f)
-            N.check(lib.bb_ppo_mlp_act(flat, offs, _ptr(feats), int(feats.shape[1]), _ptr(noise[t]), n, None,
+            N.check(lib.bb_ppo_mlp_act(flat, offs, nflat, _ptr(feats), int(feats.shape[1]), _ptr(noise[t]), n, None,
                                        _ptr(b.actions[t]), _ptr(clipped), _ptr(b.values[t]), _ptr(b.log_probs[t]),
                                        stream), "bb_ppo_mlp_act")
             obs, reward, flags = env.step_flags(clipped)
             nxt = _ptr(b.starts[t + 1]) if t + 1 < T else None
-            N.check(lib.bb_rollout_track(_ptr(reward.contiguous()), _ptr(flags), 5, n, _ptr(b.rewards[t]),
+            N.check(lib.bb_rollout_track(_ptr(reward.contiguous()), _ptr(flags), 1, n, _ptr(b.rewards[t]),
                                          _ptr(self._ep_ret), _ptr(self._ep_len), _ptr(ep_r[t]), _ptr(ep_l[t]),
                                          _ptr(self._last_starts), nxt, stream), "bb_rollout_track")
             self._last_obs = obs
@@ -555,10 +648,16 @@ class BatchedPPO:
         env, b, dev = self.env, self.buf, self.device
         lib = N.lib()
         T, n = self.n_steps, self.n_envs
-        offs = (C.c_int32 * 21)(*slots)
-        flat = C.c_void_p(self.optimizer.flat.data_ptr())
         if self._last_obs is None:
             self._last_obs, _ = env.reset()
+        if (self.use_graphs and hasattr(env, "step_flags") and getattr(env, "_host_reward", None) is None
+                and hasattr(env, "obs") and os.environ.get("BB_ROLLOUT_GRAPH", "1") != "0"):
+            if self._rgraph is None or self._rgraph.key != (id(env), T, n):
+                self._rgraph = _RolloutGraph(self, slots)
+            return self._rgraph.run(self)
+        offs = (C.c_int32 * 21)(*slots)
+        flat = C.c_void_p(self.optimizer.flat.data_ptr())
+        nflat = int(self.optimizer.flat.numel())
         noise = torch.randn(T, n, 3, generator=self.gen, device=dev)
         clipped = torch.empty(n, 3, device=dev)
         ep_r = torch.empty(T, n, dtype=torch.float64, device=dev)
@@ -568,12 +667,13 @@ class BatchedPPO:
         stream = C.c_void_p(torch.cuda.current_stream(dev).cuda_stream)
         for t in range(T):
             obs_in = self._last_obs.contiguous()
-            N.check(lib.bb_ppo_mlp_act(flat, offs, _ptr(obs_in), 15, _ptr(noise[t]), n, _ptr(b.obs[t]), _ptr(b.actions[t]),
+            N.check(lib.bb_ppo_mlp_act(flat, offs, nflat, _ptr(obs_in), 15, _ptr(noise[t]), n, _ptr(b.obs[t]),
+                                       _ptr(b.actions[t]),
                                        _ptr(clipped), _ptr(b.values[t]), _ptr(b.log_probs[t]), stream),
                     "bb_ppo_mlp_act")
             if fast:
                 obs, reward, flags = env.step_flags(clipped)
-                mask = 5  # BB_DONE_TERMINATED | BB_DONE_DIVERGED (the reference never truncates)
+                mask = 1  # BB_DONE_TERMINATED (the reference never truncates; a divergence reset ends nothing)
             else:
                 obs, reward, term, trunc, _info = env.step(clipped)
                 flags, mask = (term | trunc).to(torch.uint8).contiguous(), 1
@@ -615,7 +715,7 @@ class BatchedPPO:
             b.log_probs[t].copy_(logp)
             obs, reward, term, trunc, info = env.step(actions.clamp(-1.0, 1.0))
             flags = info.get("done_flags") if isinstance(info, dict) else None
-            done = (term | trunc) if flags is None else ((flags & 5) != 0) | trunc
+            done = (term | trunc) if flags is None else ((flags & 1) != 0) | trunc
             b.rewards[t].copy_(reward)
             self._ep_ret += reward.double()
             self._ep_len += 1

@@ -64,7 +64,7 @@ def experiment_dir(config: Dict[str, Any], out: Optional[str] = None) -> Path:
     return Path("outputs/experiments/runs") / name
 
 
-def make_env(config: Dict[str, Any], num_envs: int, device, seed: int, precision: str = "fp64"):
+def make_env(config: Dict[str, Any], num_envs: int, device, seed: int, precision: str = "fp64", stream_seeds=None):
     from ballbot_gym.envs import BallbotVecEnv
 
     env_cfg = {"camera": config.get("camera", {}), "env": config.get("env", {}), "logging": config.get("logging", {})}
@@ -73,12 +73,13 @@ def make_env(config: Dict[str, Any], num_envs: int, device, seed: int, precision
     cams = bool(config.get("camera")) and not config.get("disable_cameras", False)
     return BallbotVecEnv(num_envs, device=device, reward_config=get_component_config(config, "reward"),
                          terrain_config=get_component_config(config, "terrain"), env_config=env_cfg, seed=seed,
-                         precision=precision, n_terrains=config.get("n_terrains"), disable_cameras=not cams)
+                         precision=precision, n_terrains=config.get("n_terrains"), disable_cameras=not cams,
+                         stream_seeds=stream_seeds)
 
 
 def main(config: Dict[str, Any], seed: int, out: Optional[str] = None, total_timesteps: Optional[int] = None,
          precision: str = "fp64") -> BatchedPPO:
-    from ballbot_gym.distributed import env_shard, rank_seed
+    from ballbot_gym.distributed import env_shard, shard_stream_seeds
     from ballbot_rl.evaluation import evaluate_policy
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -91,10 +92,13 @@ def main(config: Dict[str, Any], seed: int, out: Optional[str] = None, total_tim
     dev = torch.device("cuda", local)
     n_total = int(config["num_envs"])
     first, n_local = env_shard(n_total, rank, world)
-    env = make_env(config, n_local, dev, rank_seed(seed, first), precision)
+    # every training env draws its terrains from np_random(seed) (train.py:82-89)
+    env = make_env(config, n_local, dev, seed, precision, shard_stream_seeds(seed, first, n_local))
     eval_cfg = config.get("evaluation", {}) or {}
     n_eval = int(eval_cfg.get("n_episodes", 8))
-    eval_env = make_env(config, max(n_eval, 1), dev, seed + n_total, precision) if rank == 0 else None
+    # eval env i draws from np_random(seed + N_ENVS + i) (train.py:90-97)
+    eval_env = (make_env(config, max(n_eval, 1), dev, seed + n_total, precision,
+                         shard_stream_seeds(seed + n_total, 0, max(n_eval, 1), per_env=True)) if rank == 0 else None)
 
     out_path = experiment_dir(config, out if out is not None else config.get("out"))
     logger = None

@@ -63,13 +63,6 @@ __device__ __forceinline__ EnvWork<T>& team_work(unsigned char* smem, int team) 
   return *reinterpret_cast<EnvWork<T>*>(smem + size_t(team) * work_stride<T>());
 }
 
-BB_HD uint32_t hash3(uint64_t seed, uint32_t a, uint32_t b) {  // splitmix-style counter hash
-  uint64_t z = seed + 0x9E3779B97F4A7C15ull * (uint64_t(a) * 0x100000001ull + b + 1);
-  z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
-  z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
-  return uint32_t(z ^ (z >> 31));
-}
-
 struct Dev {
   int n;
   void* qpos;
@@ -77,15 +70,17 @@ struct Dev {
   void* warm;
   int* steps;
   int* terrain;
-  int* pending_terrain;
-  int* episodes;
+  int* pending_terrain;       // >= 0: terrain pinned by bb_assign_terrain; < 0: draw from the stream
+  int* episodes;              // terrain-stream draws made by each env so far
+  const int* tstream;         // [n_streams][tlen] bank slot of draw k (bb_set_terrain_stream); NULL: none
+  const int* env_stream;      // [n] stream of each env; NULL: stream 0
+  int tlen;
   const float* bank;
   const float* size_z;
   const float* offset;
   const float* hmax;  // per terrain: max(hfield) (the top height is hmax * size_z)
   int n_terrains;
-  uint64_t seed;
-  unsigned long long* stats;  // resets, diverged, overflow, slow-path env-steps, iters
+  unsigned long long* stats;  // resets, diverged, overflow, slow-path env-steps, iters, draws past the stream table, spill
   int* slow_list;             // envs the fast kernel handed to the full kernel this step
   int* slow_count;            // [0] fast list size, [1] predicted-slow list size, [2] hand-overs
   int* fast_envs;             // this step's fast-kernel env list (ascending)
@@ -126,9 +121,29 @@ __device__ __forceinline__ void store_state(const Dev& d, int e, const T* q, con
   d.steps[e] = step;
 }
 
+// The terrain of env e's next episode.  The reference draws
+// r_seed = _np_random.integers(0, 10000) at every reset (ballbot_env.py:505-510)
+// from a generator fixed at construction for eval_env=[True, seed]
+// (:378-384), which train.py:82-89 uses for every training env: the k-th reset
+// of an env takes the k-th draw of its stream.  The host precomputes each
+// stream's draws as bank slots (bb_set_terrain_stream); this reads draw
+// episodes[e].  A pinned terrain (bb_assign_terrain) takes no draw.
+__device__ __forceinline__ int next_terrain(const Dev& d, int e) {
+  const int pin = d.pending_terrain[e];
+  if (pin >= 0 || !d.tstream) return pin >= 0 ? pin : 0;
+  int k = d.episodes[e];
+  d.episodes[e] = k + 1;
+  if (k >= d.tlen) {  // past the resident draws: reuse them (counted)
+    atomicAdd(&d.stats[5], 1ull);
+    k %= d.tlen;
+  }
+  const int st = d.env_stream ? d.env_stream[e] : 0;
+  return d.tstream[size_t(st) * d.tlen + k];
+}
+
 template <typename T>
 __device__ __forceinline__ void reset_lane(const ModelT<T>& m, const Dev& d, int e, T* q, T* v, T* w, int& step) {
-  int tid = d.pending_terrain[e];
+  const int tid = next_terrain(d, e);
   d.terrain[e] = tid;
   reset_state(m, T(d.offset[tid]), q, v, w);
   step = 0;
@@ -221,12 +236,10 @@ __global__ __launch_bounds__(64) void step_kernel(ModelT<T> mg, EnvCfg cfg, Dev 
     for (int i = 0; i < 15; i++) tobs[15 * e + i] = o[i];
   }
   if (pos2d) { pos2d[2 * e] = p2[0]; pos2d[2 * e + 1] = p2[1]; }
-  const bool reset = auto_reset && (fl & (F_TERMINATED | F_DIVERGED));
+  // SB3 VecEnv auto-reset of a terminated episode; a MuJoCo divergence reset
+  // (F_DIVERGED) already happened inside the step and ends nothing
+  const bool reset = auto_reset && (fl & F_TERMINATED);
   if (reset) {
-    // next terrain for this env: counter-based draw from the bank
-    int ep = d.episodes[e] + 1;
-    d.episodes[e] = ep;
-    if (d.n_terrains > 1) d.pending_terrain[e] = int(hash3(d.seed, uint32_t(e), uint32_t(ep)) % uint32_t(d.n_terrains));
     reset_lane(m, d, e, q, v, w, step);
 #pragma unroll
     for (int i = 0; i < 15; i++) o[i] = 0.f;  // reset obs: identity quat, zero velocities, zero action
@@ -240,6 +253,7 @@ __global__ __launch_bounds__(64) void step_kernel(ModelT<T> mg, EnvCfg cfg, Dev 
   if (reset) atomicAdd(&d.stats[0], 1ull);
   if (fl & F_DIVERGED) atomicAdd(&d.stats[1], 1ull);
   if (fl & F_OVERFLOW) atomicAdd(&d.stats[2], 1ull);
+  if (fl & F_SPILL) atomicAdd(&d.stats[6], 1ull);
   atomicAdd(&d.stats[4], (unsigned long long)iters);
 #ifdef BB_PHASE_CLOCKS
   {  // per-env step duration: max, sum and count per kernel (full 34-36, fast 37-39)
@@ -387,12 +401,14 @@ __global__ __launch_bounds__(64) void predict_kernel(ModelT<T> mg, Dev d) {
     // capsule-hull AABB of the geom, grown by the margin
     const T ext = gr + margin;
     const T lo = minT(p0[2], p1[2]) - ext;
-    if (slow || lo > hz) continue;
+    if (slow || !(lo <= hz)) continue;
     const T x0 = minT(p0[0], p1[0]) - ext, x1 = maxT(p0[0], p1[0]) + ext;
     const T y0 = minT(p0[1], p1[1]) - ext, y1 = maxT(p0[1], p1[1]) + ext;
     const T sx = m.hf_sx, sy = m.hf_sy;
     const int N1 = HF_N - 1;
-    if (x0 > sx || x1 < -sx || y0 > sy || y1 < -sy) continue;
+    // written so that a NaN pose (a diverged state before mj_checkPos resets
+    // it in the step) skips the geom: no cell index is formed from it
+    if (!(x0 <= sx && x1 >= -sx && y0 <= sy && y1 >= -sy)) continue;
     int cmin = (int)floor((x0 + sx) / (2 * sx) * N1), cmax = (int)ceil((x1 + sx) / (2 * sx) * N1);
     int rmin = (int)floor((y0 + sy) / (2 * sy) * N1), rmax = (int)ceil((y1 + sy) / (2 * sy) * N1);
     cmin = cmin < 0 ? 0 : cmin; cmax = cmax > N1 ? N1 : cmax;
@@ -458,8 +474,8 @@ __global__ __launch_bounds__(1024) void split_kernel(Dev d) {
 __global__ void assign_kernel(Dev d, const int32_t* ids) {
   const int e = blockIdx.x * blockDim.x + threadIdx.x;
   if (e >= d.n) return;
-  int t = ids[e];
-  d.pending_terrain[e] = (t >= 0 && t < d.n_terrains) ? t : 0;
+  const int t = ids[e];
+  d.pending_terrain[e] = (t >= 0 && t < d.n_terrains) ? t : -1;  // -1: back to the terrain stream
 }
 
 }  // namespace
@@ -489,6 +505,9 @@ struct bb_handle {
   int route = -1;
   std::vector<uint8_t> relief;  // per terrain: max height > 0
   int n_relief = 0;
+  int* tstream = nullptr;       // device copies of the terrain streams (bb_set_terrain_stream)
+  int* env_stream = nullptr;
+  int n_streams = 0;
   CamRig rig;  // depth cameras in the base body (bb_render_depth)
   void* scenes = nullptr;
 };
@@ -654,7 +673,7 @@ int bb_create(int n_envs, int device, const bb_params* p, bb_handle** out) {
   const size_t n = n_envs, nt = pp.n_terrains;
   Dev& d = h->d;
   memset(&d, 0, sizeof d);
-  d.n = n_envs; d.n_terrains = pp.n_terrains; d.seed = pp.seed;
+  d.n = n_envs; d.n_terrains = pp.n_terrains;
   HIPCHK(hipMalloc(&d.qpos, es * NQ * n));
   HIPCHK(hipMalloc(&d.qvel, es * NV * n));
   HIPCHK(hipMalloc(&d.warm, es * NV * n));
@@ -680,7 +699,7 @@ int bb_create(int n_envs, int device, const bb_params* p, bb_handle** out) {
   HIPCHK(hipEventCreateWithFlags(&h->join, hipEventDisableTiming));
   HIPCHK(hipMemset(d.steps, 0, sizeof(int) * n));
   HIPCHK(hipMemset(d.terrain, 0, sizeof(int) * n));
-  HIPCHK(hipMemset(d.pending_terrain, 0, sizeof(int) * n));
+  HIPCHK(hipMemset(d.pending_terrain, 0xFF, sizeof(int) * n));  // -1: no pin
   HIPCHK(hipMemset(d.episodes, 0, sizeof(int) * n));
   HIPCHK(hipMemset(h->bank, 0, sizeof(float) * nt * HF_N * HF_N));
   HIPCHK(hipMemset(d.stats, 0, sizeof(unsigned long long) * 8));
@@ -718,6 +737,7 @@ int bb_destroy(bb_handle* h) {
   (void)hipFree(h->d.slow_list); (void)hipFree(h->d.slow_count);
   (void)hipFree(h->d.fast_envs); (void)hipFree(h->d.pred_envs); (void)hipFree(h->d.pred_mark);
   (void)hipFree(h->d.body_spill);
+  (void)hipFree(h->tstream); (void)hipFree(h->env_stream);
   (void)hipStreamDestroy(h->side); (void)hipEventDestroy(h->fork); (void)hipEventDestroy(h->join);
   for (hipEvent_t e : h->tev) (void)hipEventDestroy(e);
   (void)hipFree(h->scenes);
@@ -883,13 +903,20 @@ int bb_ppo_mlp_step(const bb_ppo_mlp_args* a, void* stream) {
   return 0;
 }
 
-int bb_ppo_mlp_act(const float* params, const int32_t* offsets, const float* obs, int obs_dim, const float* noise, int n,
-                   float* obs_copy, float* actions, float* clipped, float* values, float* log_prob, void* stream) {
+int bb_ppo_mlp_act(const float* params, const int32_t* offsets, int64_t n_params, const float* obs, int obs_dim,
+                   const float* noise, int n, float* obs_copy, float* actions, float* clipped, float* values,
+                   float* log_prob, void* stream) {
   if (!params || !offsets || !obs || !actions || !values || !log_prob) return fail("bb_ppo_mlp_act: NULL argument");
   if (n < 0) return fail("bb_ppo_mlp_act: n must be >= 0 (got %d)", n);
   if (obs_dim != 15 && obs_dim != 56) return fail("bb_ppo_mlp_act: obs_dim must be 15 or 56 (got %d)", obs_dim);
+  // the same slot check as bb_ppo_mlp_step: every tensor inside the n_params-float buffer
+  const int sizes[MLP_NSLOTS] = {128 * obs_dim, 128 * 128, 128 * 128, 128 * 128, 128, 128, 128, 128,
+                                 128 * obs_dim, 128 * 128, 128 * 128, 128 * 128, 128, 128, 128, 128,
+                                 3 * 128, 3, 128, 1, 3};
   for (int i = 0; i < MLP_NSLOTS; i++)
-    if (offsets[i] < 0 || offsets[i] % 4) return fail("bb_ppo_mlp_act: offsets[%d] = %d is not 4-aligned", i, offsets[i]);
+    if (offsets[i] < 0 || offsets[i] % 4 || (int64_t)offsets[i] + sizes[i] > n_params)
+      return fail("bb_ppo_mlp_act: offsets[%d] = %d is not a 4-aligned slot inside the %lld-float buffer", i,
+                  offsets[i], (long long)n_params);
   if (reinterpret_cast<uintptr_t>(params) & 15) return fail("bb_ppo_mlp_act: params must be 16-byte aligned");
   MlpActArgs m;
   m.params = params;
@@ -1051,13 +1078,58 @@ int bb_forward(bb_handle* h, const double* ctrl, double* qacc, int32_t* ncon) {
   return 0;
 }
 
-int bb_get_stats(bb_handle* h, int64_t* out6) {
-  if (!h || !out6) return fail("bb_get_stats: NULL argument");
+int bb_get_stats(bb_handle* h, int64_t* out, int n) {
+  if (!h || !out) return fail("bb_get_stats: NULL argument");
+  if (n < 0 || n > BB_NSTATS) return fail("bb_get_stats: n must be in [0, %d] (got %d)", BB_NSTATS, n);
   HIPCHK(hipSetDevice(h->device));
   unsigned long long s[8];
   HIPCHK(hipMemcpy(s, h->d.stats, sizeof s, hipMemcpyDeviceToHost));
-  out6[0] = (int64_t)s[0]; out6[1] = (int64_t)s[1]; out6[2] = (int64_t)s[2];
-  out6[3] = (int64_t)s[3]; out6[4] = (int64_t)(s[4] & 0xffffffffull); out6[5] = (int64_t)(s[4] >> 32);
+  const int64_t v[BB_NSTATS] = {(int64_t)s[0], (int64_t)s[1], (int64_t)s[2], (int64_t)s[3], (int64_t)s[4],
+                                (int64_t)s[5], (int64_t)s[6]};
+  for (int i = 0; i < n; i++) out[i] = v[i];
+  return 0;
+}
+
+int bb_set_terrain_stream(bb_handle* h, const int32_t* slots, int n_streams, int length, const int32_t* env_stream) {
+  if (!h) return fail("bb_set_terrain_stream: NULL handle");
+  if (n_streams < 0) return fail("bb_set_terrain_stream: n_streams must be >= 0 (got %d)", n_streams);
+  HIPCHK(hipSetDevice(h->device));
+  HIPCHK(hipDeviceSynchronize());
+  (void)hipFree(h->tstream); (void)hipFree(h->env_stream);
+  h->tstream = nullptr; h->env_stream = nullptr; h->n_streams = 0;
+  h->d.tstream = nullptr; h->d.env_stream = nullptr; h->d.tlen = 0;
+  if (n_streams == 0) return 0;
+  if (!slots) return fail("bb_set_terrain_stream: NULL slots");
+  if (length < 1) return fail("bb_set_terrain_stream: length must be >= 1 (got %d)", length);
+  const size_t cnt = size_t(n_streams) * size_t(length);
+  for (size_t i = 0; i < cnt; i++)
+    if (slots[i] < 0 || slots[i] >= h->p.n_terrains)
+      return fail("bb_set_terrain_stream: slots[%zu] = %d out of range [0,%d)", i, slots[i], h->p.n_terrains);
+  if (env_stream) {
+    for (int e = 0; e < h->n; e++)
+      if (env_stream[e] < 0 || env_stream[e] >= n_streams)
+        return fail("bb_set_terrain_stream: env_stream[%d] = %d out of range [0,%d)", e, env_stream[e], n_streams);
+  } else if (n_streams != 1) {
+    return fail("bb_set_terrain_stream: %d streams need an env_stream map", n_streams);
+  }
+  HIPCHK(hipMalloc((void**)&h->tstream, sizeof(int) * cnt));
+  HIPCHK(hipMemcpy(h->tstream, slots, sizeof(int) * cnt, hipMemcpyHostToDevice));
+  if (env_stream) {
+    HIPCHK(hipMalloc((void**)&h->env_stream, sizeof(int) * h->n));
+    HIPCHK(hipMemcpy(h->env_stream, env_stream, sizeof(int) * h->n, hipMemcpyHostToDevice));
+  }
+  HIPCHK(hipMemset(h->d.episodes, 0, sizeof(int) * h->n));  // the next reset takes draw 0
+  h->n_streams = n_streams;
+  h->d.tstream = h->tstream; h->d.env_stream = h->env_stream; h->d.tlen = length;
+  return 0;
+}
+
+int bb_get_env_terrain(bb_handle* h, int32_t* terrain, int32_t* draws) {
+  if (!h) return fail("bb_get_env_terrain: NULL handle");
+  HIPCHK(hipSetDevice(h->device));
+  HIPCHK(hipDeviceSynchronize());
+  if (terrain) HIPCHK(hipMemcpy(terrain, h->d.terrain, sizeof(int) * h->n, hipMemcpyDeviceToHost));
+  if (draws) HIPCHK(hipMemcpy(draws, h->d.episodes, sizeof(int) * h->n, hipMemcpyDeviceToHost));
   return 0;
 }
 

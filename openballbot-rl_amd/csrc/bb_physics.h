@@ -927,7 +927,7 @@ BB_HD int collide_ground(const ModelT<T>& m, const Kin<T>& k, const T* v, const 
   const T* c = k.c;
   const T sx = m.hf_sx, sy = m.hf_sy, zb = m.hf_bottom;
   T xmin = c[0] - r, xmax = c[0] + r, ymin = c[1] - r, ymax = c[1] + r, zmin = c[2] - r, zmax = c[2] + r;
-  if (xmin > sx || xmax < -sx || ymin > sy || ymax < -sy || zmin > size_z || zmax < -zb) return 0;
+  if (!(xmin <= sx && xmax >= -sx && ymin <= sy && ymax >= -sy && zmin <= size_z && zmax >= -zb)) return 0;
   const int N1 = HF_N - 1;
   int cmin = (int)floor((xmin + sx) / (2 * sx) * N1);
   int cmax = (int)ceil((xmax + sx) / (2 * sx) * N1);

@@ -125,8 +125,10 @@ __device__ float ray_hfield(const float* o, const float* d, const float* hf, flo
     t0 = fmaxf(t0, ta);
     t1 = fminf(t1, tb);
   }
-  if (t0 > t1) return -1.f;
-  int c = (int)floorf((o[0] + t0 * d[0] + sx) / dx), r = (int)floorf((o[1] + t0 * d[1] + sy) / dy);
+  const float px = o[0] + t0 * d[0], py = o[1] + t0 * d[1];
+  // negated: a NaN camera pose (diverged state) casts no ray into the field
+  if (!(t0 <= t1) || !(fabsf(px) <= 2.f * sx && fabsf(py) <= 2.f * sy)) return -1.f;
+  int c = (int)floorf((px + sx) / dx), r = (int)floorf((py + sy) / dy);
   c = c < 0 ? 0 : (c > N1 - 1 ? N1 - 1 : c);
   r = r < 0 ? 0 : (r > N1 - 1 ? N1 - 1 : r);
   const int stc = d[0] > 0.f ? 1 : -1, str = d[1] > 0.f ? 1 : -1;

@@ -70,6 +70,19 @@ BB_HD void team_sync() {
 #endif
 }
 
+// true in every lane of the team if b holds in any of its lanes (team-uniform branch)
+BB_HD bool team_any(const Team& tm, bool b) {
+#ifdef __HIP_DEVICE_COMPILE__
+  const unsigned long long m = __ballot(b);
+  const int sh = int(threadIdx.x) & ~(tm.L - 1);
+  const unsigned long long mask = tm.L >= 64 ? ~0ull : ((1ull << tm.L) - 1);
+  return ((m >> sh) & mask) != 0;
+#else
+  (void)tm;
+  return b;
+#endif
+}
+
 // packed lower-triangle index e -> (i, j), j <= i
 BB_HD void tri_unpack(int e, int& i, int& j) {
   int r = (int)((sqrtf(8.f * float(e) + 1.f) - 1.f) * 0.5f);

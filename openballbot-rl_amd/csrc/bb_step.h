@@ -204,11 +204,22 @@ BB_HD int forward(const ModelT<T>& m, const T* q, const T* v, const T* ctrl, T* 
   return it;
 }
 
-// mj_step with integrator RK4 = mj_forward + mj_RungeKutta(N=4) + mj_advance.
+template <typename T>
+BB_HD bool vec_bad(const T* x, int n) {  // MuJoCo's mju_isBad over x[0..n): NaN or |x| > mjMAXVAL = 1e10
+  bool bad = false;
+#pragma unroll
+  for (int i = 0; i < n; i++) bad = bad || !(fabs(x[i]) <= T(1e10));
+  return bad;
+}
+
+// mj_step with integrator RK4 = mj_forward + mj_checkAcc + mj_RungeKutta(N=4) + mj_advance.
 // warm: qacc_warmstart (each stage's constraint solve saves its qacc).
+// mj_checkAcc: a bad qacc after the first forward resets the data (qpos0, zero
+// velocity, warm start and ctrl; no height offset) and repeats that forward;
+// *acc_reset reports it.  ctrl is zeroed then, as mj_resetData zeroes d->ctrl.
 template <typename T, bool BODY = true>
-BB_HD int rk4_step(const ModelT<T>& m, T* q, T* v, T* warm, const T* ctrl, const TerrainRef<T>& tr,
-                   EnvWork<T>& W, StageOut<T>& so, const Team& tm) {
+BB_HD int rk4_step(const ModelT<T>& m, T* q, T* v, T* warm, T* ctrl, const TerrainRef<T>& tr,
+                   EnvWork<T>& W, StageOut<T>& so, const Team& tm, bool* acc_reset) {
   const T h = m.h;
   // the RK context lives in the workspace (written identically by every
   // lane of the team); only the stage state and the warm start are in registers
@@ -262,6 +273,19 @@ BB_HD int rk4_step(const ModelT<T>& m, T* q, T* v, T* warm, const T* ctrl, const
     }
     const int fit = forward<T, BODY>(m, W.u.pre.qi, W.vi, ctrl, acc, tr, W, stage == 3 ? &so : (StageOut<T>*)nullptr, tm);
     if (fit < 0) return -1;  // fast path aborted (team-uniform)
+    if (stage == 0 && !*acc_reset && team_any(tm, vec_bad(acc, NV))) {
+      // mj_checkAcc -> mj_resetData + mj_forward (rare: stage 1 again from qpos0)
+      team_sync();
+#pragma unroll
+      for (int i = 0; i < NQ; i++) q0[i] = m.qpos0[i];
+#pragma unroll
+      for (int i = 0; i < NV; i++) { v0[i] = 0; warm[i] = 0; }
+      ctrl[0] = ctrl[1] = ctrl[2] = 0;
+      *acc_reset = true;
+      iters += fit;
+      stage = -1;
+      continue;
+    }
 #pragma unroll
     for (int i = 0; i < NV; i++) warm[i] = acc[i];
     iters += fit;
@@ -291,6 +315,17 @@ BB_HD int rk4_step(const ModelT<T>& m, T* q, T* v, T* warm, const T* ctrl, const
   return iters;
 }
 
+// mj_resetData + height offset (ballbot_env.py:612-620)
+template <typename T>
+BB_HD void reset_state(const ModelT<T>& m, T offset, T* q, T* v, T* warm) {
+#pragma unroll
+  for (int i = 0; i < NQ; i++) q[i] = m.qpos0[i];
+  q[2] += offset;
+  q[12] += offset;
+#pragma unroll
+  for (int i = 0; i < NV; i++) { v[i] = 0; warm[i] = 0; }
+}
+
 // numpy-quaternion as_rotation_vector (quaternion_log, eps 1e-14): no w>=0
 // canonicalisation.
 template <typename T>
@@ -307,19 +342,21 @@ BB_HD void quat_to_rotvec(const T* q, T* rv) {
 
 BB_HD float clipf(float x, float lo, float hi) { return x < lo ? lo : (x > hi ? hi : x); }
 
+// mj_checkPos / mj_checkVel: NaN or |x| > 1e10 anywhere in qpos or qvel
 template <typename T>
 BB_HD bool state_bad(const T* q, const T* v) {
-  bool bad = false;
-#pragma unroll
-  for (int i = 0; i < NQ; i++) bad = bad || !(fabs(q[i]) <= T(1e10));
-#pragma unroll
-  for (int i = 0; i < NV; i++) bad = bad || !(fabs(v[i]) <= T(1e10));
-  return bad;
+  return vec_bad(q, NQ) || vec_bad(v, NV);
 }
 
 // flags returned by env_step; F_SLOWPATH: the fast kernel left this env to
-// the full kernel (nothing was stepped)
-constexpr int F_TERMINATED = 1, F_FAILURE = 2, F_DIVERGED = 4, F_OVERFLOW = 8, F_SLOWPATH = 1 << 16;
+// the full kernel (nothing was stepped).  F_DIVERGED: MuJoCo's divergence
+// auto-reset ran inside this step (mj_checkPos/Vel/Acc -> mj_resetData); it is
+// information, not an episode end: the reference's episode goes on from qpos0
+// (ballbot_env.py:897-899 never fires, mj_step advances time past 0).
+// F_SPILL (internal): the last RK stage stored base-tree contacts past the
+// team's MAXB_LDS LDS slots, in the env's HBM spill block.
+constexpr int F_TERMINATED = 1, F_FAILURE = 2, F_DIVERGED = 4, F_OVERFLOW = 8, F_SPILL = 1 << 9,
+              F_SLOWPATH = 1 << 16;
 
 // One BBotSimulation.step.  obs15 = sorted keys (actions, angular_vel,
 // motor_state, orientation, vel), the order the policy's Extractor consumes.
@@ -331,12 +368,26 @@ BB_HD int env_step(const ModelT<T>& m, const EnvCfg& cfg, T* q, T* v, T* warm, i
   T ctrl[3];
 #pragma unroll
   for (int i = 0; i < 3; i++) ctrl[i] = -T(clipf(action[i] * mwv, -mwv, mwv));  // data.ctrl[:] = -ctrl
+  // mjWARN_BADCTRL (mj_fwdActuation): a bad control zeroes all of them
+  if (vec_bad(ctrl, 3)) ctrl[0] = ctrl[1] = ctrl[2] = 0;
+  int flags = 0;
+  // mj_step's mj_checkPos / mj_checkVel: a bad state is mj_resetData'd (qpos0
+  // without the reset height offset, zero velocity, warm start and ctrl) and
+  // this step integrates from there; step_counter goes on (team-uniform: the
+  // state is the team's shared copy)
+  if (state_bad(q, v)) {
+    reset_state(m, T(0), q, v, warm);
+    ctrl[0] = ctrl[1] = ctrl[2] = 0;
+    flags = F_DIVERGED;
+  }
   StageOut<T>& so = W.so;  // team-shared (LDS): not register-resident across the solves
-  int it = rk4_step<T, BODY>(m, q, v, warm, ctrl, tr, W, so, tm);
+  bool acc_reset = false;
+  int it = rk4_step<T, BODY>(m, q, v, warm, ctrl, tr, W, so, tm, &acc_reset);
   if (it < 0) return F_SLOWPATH;
   if (iters) *iters = it;
-  int flags = state_bad(q, v) ? F_DIVERGED : 0;
+  if (acc_reset) flags |= F_DIVERGED;
   if (so.overflow) flags |= F_OVERFLOW;
+  if (so.nb > MAXB_LDS) flags |= F_SPILL;
   // _get_obs
   T rv[3];
   quat_to_rotvec(so.quat_b, rv);
@@ -378,21 +429,13 @@ BB_HD int env_step(const ModelT<T>& m, const EnvCfg& cfg, T* q, T* v, T* warm, i
   T nn = qw * qw + qx * qx + qy * qy + qz * qz;
   T R22 = T(1) - 2 * (qx * qx + qy * qy) / nn;
   T ang = acos(clampT(R22, T(-1), T(1))) * T(180 / 3.14159265358979323846);
+  // a host-side plugin (reward_kind 2) gets the action penalty only: the host
+  // adds plugin * scale first and the bonus last, the reference's order
+  // (reward_obj(obs) * scale + action_reg, then + survival_bonus)
   if (ang > T(cfg.max_allowed_tilt)) flags |= F_FAILURE | F_TERMINATED;
-  else r = r + cfg.survival_bonus;
+  else if (cfg.reward_kind != 2) r = r + cfg.survival_bonus;
   reward = r;
   return flags;
-}
-
-// mj_resetData + height offset (ballbot_env.py:612-620)
-template <typename T>
-BB_HD void reset_state(const ModelT<T>& m, T offset, T* q, T* v, T* warm) {
-#pragma unroll
-  for (int i = 0; i < NQ; i++) q[i] = m.qpos0[i];
-  q[2] += offset;
-  q[12] += offset;
-#pragma unroll
-  for (int i = 0; i < NV; i++) { v[i] = 0; warm[i] = 0; }
 }
 
 }  // namespace bb

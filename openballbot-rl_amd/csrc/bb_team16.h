@@ -784,7 +784,8 @@ __device__ __forceinline__ int collide_team(const ModelT<T>& m, const Kin<T>& k,
   const T* c = k.c;
   const T sx = m.hf_sx, sy = m.hf_sy, zb = m.hf_bottom;
   const T xmin = c[0] - r, xmax = c[0] + r, ymin = c[1] - r, ymax = c[1] + r, zmin = c[2] - r, zmax = c[2] + r;
-  if (xmin > sx || xmax < -sx || ymin > sy || ymax < -sy || zmin > size_z || zmax < -zb) return 0;
+  // negated form: a NaN ball position (diverged stage state) forms no cell index
+  if (!(xmin <= sx && xmax >= -sx && ymin <= sy && ymax >= -sy && zmin <= size_z && zmax >= -zb)) return 0;
   const int N1 = HF_N - 1;
   int cmin = (int)floor((xmin + sx) / (2 * sx) * N1);
   int cmax = (int)ceil((xmax + sx) / (2 * sx) * N1);
@@ -930,8 +931,9 @@ __device__ bool body_candidates(const ModelT<T>& m, const Kin<T>& k, const float
         const T ext = gi == 0 ? g.hh * ai + g.r * sqrt(rad > 0 ? rad : T(0)) : g.hh * ai + g.r;
         lo[i] = g.c[i] - ext; hi[i] = g.c[i] + ext;
       }
-      if (lo[2] > hz) continue;
-      if (lo[0] > sx || hi[0] < -sx || lo[1] > sy || hi[1] < -sy || lo[2] > size_z || hi[2] < -zb) continue;
+      if (!(lo[2] <= hz)) continue;
+      // negated: a NaN pose skips the geom (no cell index from it)
+      if (!(lo[0] <= sx && hi[0] >= -sx && lo[1] <= sy && hi[1] >= -sy && lo[2] <= size_z && hi[2] >= -zb)) continue;
       int cmin = (int)floor((lo[0] + sx) / (2 * sx) * N1), cmax = (int)ceil((hi[0] + sx) / (2 * sx) * N1);
       int rmin = (int)floor((lo[1] + sy) / (2 * sy) * N1), rmax = (int)ceil((hi[1] + sy) / (2 * sy) * N1);
       cmin = cmin < 0 ? 0 : cmin; cmax = cmax > N1 ? N1 : cmax;
@@ -1073,8 +1075,8 @@ __device__ int collide_body_team(const ModelT<T>& m, const Kin<T>& k, const floa
         const T ext = cyl ? g.hh * ai + g.r * sqrt(rad > 0 ? rad : T(0)) : g.hh * ai + g.r;
         lo[i] = g.c[i] - ext; hi[i] = g.c[i] + ext;
       }
-      if (lo[2] > hz) continue;  // above every vertex of the terrain
-      if (lo[0] > sx || hi[0] < -sx || lo[1] > sy || hi[1] < -sy || lo[2] > size_z || hi[2] < -zb) continue;
+      if (!(lo[2] <= hz)) continue;  // above every vertex of the terrain (or a NaN pose)
+      if (!(lo[0] <= sx && hi[0] >= -sx && lo[1] <= sy && hi[1] >= -sy && lo[2] <= size_z && hi[2] >= -zb)) continue;
       int cmin = (int)floor((lo[0] + sx) / (2 * sx) * N1), cmax = (int)ceil((hi[0] + sx) / (2 * sx) * N1);
       int rmin = (int)floor((lo[1] + sy) / (2 * sy) * N1), rmax = (int)ceil((hi[1] + sy) / (2 * sy) * N1);
       cmin = cmin < 0 ? 0 : cmin; cmax = cmax > N1 ? N1 : cmax;

@@ -1436,18 +1436,47 @@ static void integrate_pos(double* qpos, const double* v, double h) {
   for (int k = 0; k < 3; k++) qpos[7 + k] += h * v[6 + k];
 }
 
-/* mj_step with integrator RK4: mj_forward, then mj_RungeKutta(m, d, 4) */
-void bbo_mj_step(double* qpos, double* qvel, double* warm, const double* ctrl,
-                 const float* hfield, double size_z, bbo_forward_out* stage4) {
+/* MuJoCo's mju_isBad over x[0..n): NaN or |x| > mjMAXVAL (1e10) */
+static int vec_bad(const double* x, int n) {
+  for (int i = 0; i < n; i++) if (!(fabs(x[i]) <= 1e10)) return 1;
+  return 0;
+}
+
+/* mj_resetData for this model: qpos0, zero qvel, qacc_warmstart and ctrl (no
+ * reset height offset: that is the env's, ballbot_env.py:616-617) */
+static void reset_data(double* qpos, double* qvel, double* warm, double* ctrl) {
+  compile_model();
+  memcpy(qpos, M_.qpos0, NQ * sizeof(double));
+  memset(qvel, 0, NV * sizeof(double));
+  if (warm) memset(warm, 0, NV * sizeof(double));
+  ctrl[0] = ctrl[1] = ctrl[2] = 0;
+}
+
+/* mj_step with integrator RK4: mj_checkPos, mj_checkVel, mj_forward,
+ * mj_checkAcc, then mj_RungeKutta(m, d, 4).  A bad qpos/qvel (before the
+ * forward) or qacc (after it) resets the data (mj_resetData; the qacc case
+ * then runs mj_forward again) and the step goes on from qpos0.  A bad ctrl
+ * zeroes every ctrl (mjWARN_BADCTRL, mj_fwdActuation).  Returns 1 if a
+ * divergence reset happened. */
+int bbo_mj_step(double* qpos, double* qvel, double* warm, const double* ctrl_in,
+                const float* hfield, double size_z, bbo_forward_out* stage4) {
   static const double A[3] = {0.5, 0.5, 1.0}; /* RK4 A (sub)diagonal */
   static const double B[4] = {1.0 / 6, 1.0 / 3, 1.0 / 3, 1.0 / 6};
   const double h = TIMESTEP;
-  double q0[NQ], v0[NV], X[4][NV], F[4][NV];
+  double q0[NQ], v0[NV], X[4][NV], F[4][NV], ctrl[3] = {ctrl_in[0], ctrl_in[1], ctrl_in[2]};
+  int reset = 0;
+  if (vec_bad(ctrl, 3)) ctrl[0] = ctrl[1] = ctrl[2] = 0;
+  if (vec_bad(qpos, NQ) || vec_bad(qvel, NV)) { reset_data(qpos, qvel, warm, ctrl); reset = 1; }
   memcpy(q0, qpos, sizeof q0);
   memcpy(v0, qvel, sizeof v0);
   bbo_forward_out tmp;
   bbo_forward_out* o = stage4 ? stage4 : &tmp;
   forward_impl(q0, v0, ctrl, warm, hfield, size_z, o);
+  if (!reset && vec_bad(o->qacc, NV)) {
+    reset_data(q0, v0, warm, ctrl);
+    reset = 1;
+    forward_impl(q0, v0, ctrl, warm, hfield, size_z, o);
+  }
   memcpy(X[0], v0, sizeof v0);
   memcpy(F[0], o->qacc, sizeof F[0]);
   for (int i = 1; i < 4; i++) {
@@ -1469,6 +1498,7 @@ void bbo_mj_step(double* qpos, double* qvel, double* warm, const double* ctrl,
   for (int d = 0; d < NV; d++) qvel[d] = v0[d] + h * da[d];
   memcpy(qpos, q0, sizeof q0);
   integrate_pos(qpos, dv, h);
+  return reset;
 }
 
 /* ---------------------------------------------------------------- env glue */
@@ -1513,12 +1543,6 @@ double bbo_init_offset(const float* hf, double size_z) {
   return mx * size_z + 0.01;
 }
 
-static int state_bad(const double* qpos, const double* qvel) {
-  for (int i = 0; i < NQ; i++) if (!isfinite(qpos[i]) || fabs(qpos[i]) > 1e10) return 1;
-  for (int i = 0; i < NV; i++) if (!isfinite(qvel[i]) || fabs(qvel[i]) > 1e10) return 1;
-  return 0;
-}
-
 int bbo_env_step(const bbo_env_cfg* cfg, double* qpos, double* qvel, double* warm, int* step_counter,
                  const float* action, const float* hfield, double size_z, float* obs15, float* reward,
                  float* pos2d, double* tilt_deg) {
@@ -1531,8 +1555,10 @@ int bbo_env_step(const bbo_env_cfg* cfg, double* qpos, double* qvel, double* war
     ctrl[k] = -(double)c;
   }
   bbo_forward_out s4;
-  bbo_mj_step(qpos, qvel, warm, ctrl, hfield, size_z, &s4);
-  int diverged = state_bad(qpos, qvel);
+  /* mj_step's divergence reset (mj_checkPos/Vel/Acc) happens inside it; the
+   * episode goes on from qpos0 with step_counter unchanged: mj_step advances
+   * time past 0, so the env's time==0 check (ballbot_env.py:897-899) stays off */
+  int diverged = bbo_mj_step(qpos, qvel, warm, ctrl, hfield, size_z, &s4);
 
   /* _get_obs (ballbot_env.py:771-811) from stage-4 xquat/cvel and final qvel */
   double rv[3];
@@ -1589,7 +1615,7 @@ int bbo_env_step_batch(const bbo_env_cfg* cfg, int n, double* qpos, double* qvel
     int f = bbo_env_step(cfg, q, v, w, step_counter + e, actions + 3 * e, hfield, size_z, obs + 15 * e,
                          reward + e, NULL, NULL);
     done[e] = (unsigned char)(f & 7);
-    if (f & 5) { /* terminated or diverged -> auto-reset */
+    if (f & 1) { /* terminated -> auto-reset (a divergence reset ends nothing) */
       bbo_reset_state(offset, q, v, w);
       step_counter[e] = 0;
       nd++;
@@ -1611,7 +1637,7 @@ int bbo_env_step_batch_mt(const bbo_env_cfg* cfg, int n, double* qpos, double* q
     int f = bbo_env_step(cfg, q, v, w, step_counter + e, actions + 3 * e, hfield, size_z, obs + 15 * e,
                          reward + e, NULL, NULL);
     done[e] = (unsigned char)(f & 7);
-    if (f & 5) {
+    if (f & 1) {
       bbo_reset_state(offset, q, v, w);
       step_counter[e] = 0;
       nd++;

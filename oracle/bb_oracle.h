@@ -91,8 +91,12 @@ void bbo_forward(const double* qpos, const double* qvel, const double* ctrl,
 
 /* mj_step with RK4: advances qpos/qvel/warm in place.  stage4 (may be NULL)
  * receives the forward outputs of the last RK stage (what mjData holds after
- * mj_step: xquat/cvel/xpos come from RK stage 4). */
-void bbo_mj_step(double* qpos, double* qvel, double* warm, const double* ctrl,
+ * mj_step: xquat/cvel/xpos come from RK stage 4).  MuJoCo's
+ * divergence handling is restated: a NaN/|x|>1e10 qpos or qvel (mj_checkPos/
+ * Vel) or qacc after the first forward (mj_checkAcc) resets to qpos0 with zero
+ * velocity, warm start and ctrl, and the step integrates from there; a bad
+ * ctrl zeroes all ctrl (mjWARN_BADCTRL).  Returns 1 if such a reset happened. */
+int bbo_mj_step(double* qpos, double* qvel, double* warm, const double* ctrl,
                  const float* hfield, double size_z, bbo_forward_out* stage4);
 
 /* Full env step (ballbot_env.py:854-1036) for one env.

@@ -100,7 +100,11 @@ def test_argument_errors_without_gpu(native):
                       (lambda: L.bb_adamw_clip(16, 16, 16, 16, 0, 16, 16, 16, 0.9, 0.999, 1e-8, 0.01, 0.5, None),
                        "n must be >= 1"),
                       (lambda: L.bb_kernel_ms(None, None, None), "NULL argument"),
-                      (lambda: L.bb_get_stats(None, None), "NULL argument")):
+                      (lambda: L.bb_get_stats(None, None, 6), "NULL argument"),
+                      (lambda: L.bb_ppo_mlp_act(16, (C.c_int32 * 21)(*([0] * 20 + [40000])), 40000, 16, 15, None, 4,
+                                                None, 16, None, 16, 16, None), "inside the 40000-float buffer"),
+                      (lambda: L.bb_set_terrain_stream(None, None, 1, 4, None), "NULL handle"),
+                      (lambda: L.bb_get_env_terrain(None, None, None), "NULL handle")):
         assert call() < 0
         assert msg in _err(native), (msg, _err(native))
 
@@ -113,7 +117,8 @@ def test_ctypes_structs_match_the_header(tmp_path, native):
 
     if shutil.which("gcc") is None:
         pytest.skip("gcc not available")
-    structs = {"bb_ppo_mlp_args": native.PPOMlpArgs, "bb_encoder_params": native.EncoderParams}
+    structs = {"bb_ppo_mlp_args": native.PPOMlpArgs, "bb_encoder_params": native.EncoderParams,
+               "bb_params": native.BBParams, "bb_perlin_cfg": native.PerlinCfg}
     lines = ['#include <stdio.h>', '#include <stddef.h>', '#include "ballbot_mi355x.h"', 'int main(void) {']
     for cname, py in structs.items():
         lines.append(f'printf("{cname} size %zu\\n", sizeof({cname}));')

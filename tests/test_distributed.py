@@ -30,7 +30,7 @@ def _free_port():
 def _worker(rank, world, port, q):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=world)
-    from ballbot_gym.distributed import env_shard, gather_rollouts, max_over_ranks, rank_seed
+    from ballbot_gym.distributed import env_shard, gather_rollouts, max_over_ranks, shard_stream_seeds
 
     start, count = env_shard(10, rank, world)
     t = max_over_ranks(1.0 + rank)
@@ -38,7 +38,7 @@ def _worker(rank, world, port, q):
     buf = torch.arange(start, start + count, dtype=torch.float32).view(1, count, 1).expand(3, count, 4).contiguous()
     out = gather_rollouts(buf)
     if rank == 0:
-        q.put((t, out[0, :, 0].tolist(), rank_seed(5, start)))
+        q.put((t, out[0, :, 0].tolist(), (shard_stream_seeds(5, start, count), shard_stream_seeds(5, start, count, True))))
     dist.destroy_process_group()
 
 
@@ -55,7 +55,7 @@ def test_gloo_world2_gather_and_max():
         assert p.exitcode == 0
     assert t == 2.0
     assert ids == [float(i) for i in range(10)]
-    assert seed0 == 5
+    assert seed0 == (None, [5, 6, 7, 8, 9])  # shared training stream; per-env eval streams from the global id
 
 
 def _ppo_worker(rank, world, port, q):

@@ -386,7 +386,7 @@ def test_full_size_step_properties():
                                             -1, 1)))
         edge = np.abs(tilt - 20.0) < 1e-4
         assert np.array_equal(failed[~edge], tilt[~edge] > 20.0)
-        done = (fl & 5) != 0
+        done = (fl & 1) != 0
         assert np.all(obs.cpu().numpy()[done] == 0)  # auto-reset observation
     q, v, _, _ = env.get_state()
     assert np.allclose(np.linalg.norm(q[:, 3:7], axis=1), 1, atol=1e-9)

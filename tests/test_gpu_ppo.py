@@ -463,8 +463,9 @@ def test_fused_act_deterministic_is_the_mean():
     act = torch.empty(77, 3, device=dev); val = torch.empty(77, device=dev); lp = torch.empty(77, device=dev)
     clipped = torch.empty(77, 3, device=dev)
     ptr = lambda t: C.c_void_p(t.data_ptr())  # noqa: E731
-    N.check(N.lib().bb_ppo_mlp_act(ptr(m.optimizer.flat), (C.c_int32 * 21)(*slots), ptr(obs), 15, None, 77, None, ptr(act),
-                                   ptr(clipped), ptr(val), ptr(lp), None), "bb_ppo_mlp_act")
+    N.check(N.lib().bb_ppo_mlp_act(ptr(m.optimizer.flat), (C.c_int32 * 21)(*slots), m.optimizer.flat.numel(), ptr(obs),
+                                   15, None, 77, None, ptr(act), ptr(clipped), ptr(val), ptr(lp), None),
+            "bb_ppo_mlp_act")
     torch.cuda.synchronize()
     with torch.no_grad():
         mean, v = m.policy._heads(obs)
@@ -629,3 +630,64 @@ def test_camera_feature_cache_is_exact(monkeypatch):
     (a0, v0, r0), (a1, v1, r1) = bufs
     assert float((r0 == 0).float().mean()) < 0.5  # most steps reuse cached features
     assert torch.equal(r0, r1) and torch.equal(a0, a1) and torch.equal(v0, v1)
+
+
+def test_rollout_graph_matches_eager(monkeypatch):
+    """The proprio rollout captured as ONE HIP graph (n_steps x [policy step, bb_step with the
+    two-stream route, bookkeeping]) replays bit-identically to the eager fused rollout -- the
+    same noise, the same env stream -- also after the caching allocator has been churned and
+    emptied between replays (every pointer the graph holds is a fixed buffer, _RolloutGraph)."""
+    from ballbot_gym.envs import BallbotVecEnv
+    from ballbot_rl.training.logger import CSVLogger
+    from ballbot_rl.training.ppo import BatchedPPO
+
+    models = []
+    for graph in ("0", "1"):
+        monkeypatch.setenv("BB_ROLLOUT_GRAPH", graph)
+        env = BallbotVecEnv(512, device="cuda:0", seed=6, terrain_config={"type": "perlin", "config": {}},
+                            n_terrains=8)  # relief bank: the predict/split route on two streams
+        m = BatchedPPO(env, n_steps=16, batch_size=1024, n_epochs=1, seed=4, logger=CSVLogger(None, stdout=False))
+        bufs = []
+        for r in range(3):
+            m.collect_rollouts()
+            bufs.append({k: getattr(m.buf, k).clone() for k in ("obs", "actions", "values", "log_probs", "rewards",
+                                                                 "starts", "advantages", "returns")})
+            junk = [torch.empty(1 << 24, device="cuda:0") for _ in range(8)]  # allocator churn
+            del junk
+            torch.cuda.empty_cache()
+        models.append((m, bufs, env))
+    (ma, ba, ea), (mb, bb, eb) = models
+    assert ma._rgraph is None and mb._rgraph is not None
+    for r in range(3):
+        for k in ba[r]:
+            assert torch.equal(ba[r][k], bb[r][k]), (r, k)
+    assert [e["r"] for e in ma.ep_info_buffer] == [e["r"] for e in mb.ep_info_buffer]
+    assert [e["l"] for e in ma.ep_info_buffer] == [e["l"] for e in mb.ep_info_buffer]
+    qa, va, _, sa = ea.get_state()
+    qb, vb, _, sb = eb.get_state()
+    assert np.array_equal(qa, qb) and np.array_equal(va, vb) and np.array_equal(sa, sb)
+    assert ea.stats()["slow_path"] > 0
+    ea.close()
+    eb.close()
+
+
+def test_update_graph_build_keeps_encoder_statistics(monkeypatch):
+    """Building the update graphs runs warm-up minibatches in train mode on a zero buffer:
+    the frozen encoders' BatchNorm running statistics and num_batches_tracked must be
+    exactly as before the build."""
+    import copy
+
+    from ballbot_gym.envs import BallbotVecEnv
+    from ballbot_rl.training.logger import CSVLogger
+    from ballbot_rl.training.ppo import BatchedPPO
+
+    env = BallbotVecEnv(256, device="cuda:0", seed=5, disable_cameras=False)
+    m = BatchedPPO(env, n_steps=8, batch_size=512, n_epochs=1, seed=3, frozen_encoder=copy.deepcopy(
+        _random_frozen_encoder(7)), logger=CSVLogger(None, stdout=False))
+    m.collect_rollouts()
+    before = [b.clone() for b in m.policy.buffers()]
+    assert len(before) > 0
+    m._graphs_for(256 * 8)
+    for b0, b1 in zip(before, m.policy.buffers()):
+        assert torch.equal(b0, b1)
+    env.close()

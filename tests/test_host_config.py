@@ -17,7 +17,7 @@ def test_directional_reward_maps_to_fused_kernel(reward_config):
     assert (p.max_ep_steps, p.max_allowed_tilt, p.max_wheel_velocity) == (1000, 15.0, 8.0)
     assert p.reward_scale == pytest.approx(0.05) and p.survival_bonus == pytest.approx(0.1)
     assert p.action_reg_coef == pytest.approx(-0.001)
-    assert p.fp64 == 0 and p.seed == 7
+    assert p.fp64 == 0
     p, _, _ = params_from_configs(reward_config)
     assert p.fp64 == 1 and p.max_ep_steps == 4000
 
@@ -100,13 +100,80 @@ def test_gpu_perlin_plan():
 
     assert gpu_perlin_plan({"type": "hills", "config": {}}, None, 0) is None
     assert gpu_perlin_plan({"type": "perlin", "config": {"seed": 5}}, None, 0) is None  # fixed seed: host path
-    seeds, pc, sz = gpu_perlin_plan({"type": "perlin", "config": {"seed": None}}, None, 0)
-    assert seeds == list(range(10000)) and sz == 2.0
+    plan, pc = gpu_perlin_plan({"type": "perlin", "config": {"seed": None}}, None, 0)
+    assert plan.full and plan.seeds == list(range(10000)) and plan.size_z == 2.0
+    assert plan.streams.shape == (1, 65536)  # slot == seed: the draws themselves
     assert (pc.scale, pc.octaves, pc.lacunarity, pc.amplitude) == (25.0, 4, 2.0, 1.0)
     assert abs(pc.persistence - 0.2) < 1e-7
-    seeds, pc, _ = gpu_perlin_plan({"type": "perlin", "config": {"octaves": 5}}, 4, 10)
-    assert seeds == [7765, 9560, 2640, 2076] and pc.octaves == 5
+    plan, pc = gpu_perlin_plan({"type": "perlin", "config": {"octaves": 5}}, 4, 10)
+    assert plan.seeds == [7765, 9560, 2640, 2076] and pc.octaves == 5
+    assert plan.streams.tolist() == [[0, 1, 2, 3]]
     with pytest.raises(ValueError, match="unknown config keys"):
         gpu_perlin_plan({"type": "perlin", "config": {"octave": 3}}, 4, 0)
     with pytest.raises(ValueError):
         gpu_perlin_plan({"type": "perlin", "config": {}}, 0, 0)
+
+
+def test_stream_draws_match_per_reset_scalar_calls():
+    """The reference draws ONE value per reset, _np_random.integers(0, 10000)
+    (ballbot_env.py:505-510); the plan draws a vector at once.  PCG64 buffers
+    its 32-bit outputs in the bit generator, so both give the same stream."""
+    from ballbot_gym.envs.config import np_random, stream_draws
+
+    for seed in (0, 10, 12345):
+        g = np_random(seed)
+        scalar = [int(g.integers(0, 10000)) for _ in range(3000)]
+        assert stream_draws(seed, 3000).tolist() == scalar
+    assert stream_draws(10, 4).tolist() == [7765, 9560, 2640, 2076]  # tests/golden/seeds.json
+
+
+def test_terrain_plan_shared_and_per_env_streams():
+    """train.py:82-89: every training env is built with eval_env=[True, seed]
+    -> all envs share one stream (reset k of every env draws value k);
+    train.py:90-97: eval env i uses seed + N_ENVS + i -> its own stream."""
+    from ballbot_gym.envs.config import stream_draws, terrain_plan
+
+    plan = terrain_plan({"type": "hills", "config": {}}, 32, 10, num_envs=4096)
+    d = stream_draws(10, 32)
+    assert plan.env_stream is None and plan.streams.shape == (1, 32)
+    assert [plan.seeds[s] for s in plan.streams[0]] == d.tolist()
+    assert len(plan.seeds) == len(set(d.tolist()))  # distinct seeds only
+    assert all(plan.seed_of_draw(0, k) == d[k] for k in range(32))
+    seeds = [100 + i % 3 for i in range(7)]
+    plan = terrain_plan({"type": "stepped", "config": {}}, 5, 0, num_envs=7, stream_seeds=seeds)
+    assert plan.streams.shape == (3, 5) and plan.env_stream.tolist() == [0, 1, 2, 0, 1, 2, 0]
+    for i, s in enumerate(seeds):
+        assert [plan.seeds[x] for x in plan.streams[plan.env_stream[i]]] == stream_draws(s, 5).tolist()
+    full = terrain_plan({"type": "perlin", "config": {}}, None, 3, num_envs=2, stream_seeds=[7, 8], full_bank=True)
+    assert full.streams.shape == (2, 1024) and full.streams[1, :5].tolist() == stream_draws(8, 5).tolist()
+    explicit = terrain_plan({"type": "hills", "config": {}}, None, 0, 1, draws=[5, 9, 5])
+    assert explicit.seeds == [5, 9] and explicit.streams.tolist() == [[0, 1, 0]]
+    assert terrain_plan({"type": "flat", "config": {}}, None, 0, 8).streams is None
+    assert terrain_plan({"type": "hills", "config": {"seed": 4}}, 8, 0, 8).seeds == [4]
+    with pytest.raises(ValueError, match="one seed per env"):
+        terrain_plan({"type": "hills", "config": {}}, 4, 0, num_envs=3, stream_seeds=[1, 2])
+
+
+def test_spaces_and_registration():
+    """Gym surface (B1): "ballbot-v0.1" registered (reference __init__.py:47-53),
+    action_space Box(-1, 1, (3,)), observation_space with the reference's keys
+    (envs/observation_spaces.py:9-100), sorted as gymnasium's Dict keeps them."""
+    import ballbot_gym
+    from ballbot_gym import spaces
+
+    assert "ballbot-v0.1" in ballbot_gym.registry.env_specs
+    assert ballbot_gym.registry.env_specs["ballbot-v0.1"].entry_point == "ballbot_gym.envs.ballbot_env:BBotSimulation"
+    a = spaces.action_space()
+    assert a.shape == (3,) and a.dtype == np.float32
+    a.seed(0)
+    for _ in range(100):
+        x = a.sample()
+        assert x.dtype == np.float32 and a.contains(x)
+    assert not a.contains(np.array([0, 0, 1.5], np.float32))
+    o = spaces.observation_space({"h": 64, "w": 64}, 1, disable_cameras=True)
+    assert list(o.keys()) == ["actions", "angular_vel", "motor_state", "orientation", "vel"]
+    o = spaces.observation_space({"h": 64, "w": 64}, 1, disable_cameras=False)
+    assert o["rgbd_0"].shape == (1, 64, 64) and o["relative_image_timestamp"].shape == (1,)
+    assert o.contains(o.sample())
+    with pytest.raises(ValueError, match="No registered env"):
+        ballbot_gym.make("ballbot-v9")

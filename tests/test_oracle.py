@@ -329,3 +329,59 @@ def test_openmp_batch_equals_serial(oracle):
                                   threads=threads)
         states.append((q.copy(), v.copy()))
     assert np.array_equal(states[0][0], states[1][0]) and np.array_equal(states[0][1], states[1][1])
+
+
+def _step_from(oracle, q, v, w, steps, action):
+    q, v, w, sc = q.copy(), v.copy(), w.copy(), np.array([steps], np.int32)
+    obs, r, fl, p2, _ = oracle.env_step(oracle.default_cfg(), q, v, w, sc, np.asarray(action, np.float32),
+                                        oracle.flat_hfield())
+    return q, v, w, int(sc[0]), obs, r, fl
+
+
+@pytest.mark.parametrize("case", ["nan_qpos", "big_qpos", "nan_qvel", "big_qvel", "bad_qacc"])
+def test_divergence_reset_is_mujocos(oracle, case):
+    """A16: mj_step's mj_checkPos / mj_checkVel (NaN or |x| > 1e10) and
+    mj_checkAcc (after the first forward) reset the data -- qpos0 WITHOUT the
+    env's height offset, zero velocity, warm start and ctrl -- and the step
+    integrates from there.  The episode goes on: step_counter continues, no
+    termination (mj_step leaves time = 0.002, so ballbot_env.py:897-899's
+    time == 0 check never fires), done bit 2 reports the reset."""
+    q0 = np.array(oracle.model_info()["qpos0"])
+    rng = np.random.default_rng(4)
+    q, v, w = oracle.reset_state(0.01)
+    q = q + np.r_[rng.normal(0, 0.01, 3), 0, 0, 0, 0, rng.normal(0, 0.1, 10)]
+    v = rng.normal(0, 0.1, 15)
+    w = rng.normal(0, 1.0, 15)
+    if case == "nan_qpos":
+        q[5] = np.nan
+    elif case == "big_qpos":
+        q[11] = 2e10
+    elif case == "nan_qvel":
+        v[2] = np.nan
+    elif case == "big_qvel":
+        v[14] = -1.5e10
+    else:  # finite, |qvel| < 1e10, but the wheel damping alone gives |qacc| >> 1e10
+        v[7] = 5e9
+    a = np.array([0.3, -0.7, 0.5], np.float32)
+    qg, vg, wg, sc, obs, r, fl = _step_from(oracle, q, v, w, 57, a)
+    # expected: one step from qpos0 at rest with zero ctrl (zero action), warm start 0
+    qe, ve, we, _, obs_e, _, fle = _step_from(oracle, q0, np.zeros(15), np.zeros(15), 57, np.zeros(3))
+    np.testing.assert_array_equal(qg, qe)
+    np.testing.assert_array_equal(vg, ve)
+    np.testing.assert_array_equal(obs[3:], obs_e[3:])  # physics part of the observation
+    np.testing.assert_array_equal(obs[:3], a)          # "actions" echoes the command (ballbot_env.py:919)
+    assert fl & 4 and not fle & 4
+    assert (fl & 3) == (fle & 3) == 0 and sc == 58    # the episode goes on
+    assert np.isfinite(r)
+
+
+def test_nan_action_zeroes_ctrl(oracle):
+    """mjWARN_BADCTRL: a NaN control zeroes every control for the step; the
+    observation still echoes the action and the reward's penalty is NaN."""
+    q, v, w = oracle.reset_state(0.01)
+    a = np.array([np.nan, 0.5, 0.5], np.float32)
+    qg, vg, _, _, obs, r, fl = _step_from(oracle, q, v, w, 3, a)
+    qe, ve, _, _, _, _, _ = _step_from(oracle, q, v, w, 3, np.zeros(3))
+    np.testing.assert_array_equal(qg, qe)
+    np.testing.assert_array_equal(vg, ve)
+    assert np.isnan(obs[0]) and np.isnan(r) and not fl & 4

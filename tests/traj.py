@@ -39,7 +39,7 @@ def record(n_envs, n_steps, hfield, size_z=2.0, seed=0, action_scale=1.0, max_ep
             rows["qpos1"].append(q.copy()); rows["qvel1"].append(v.copy()); rows["warm1"].append(w.copy())
             rows["obs"].append(obs); rows["reward"].append(r); rows["flags"].append(fl); rows["pos2d"].append(p2)
             last_obs[e] = obs
-            if fl & 5:
+            if fl & 1:
                 st[e] = O.reset_state(off)
                 sc[e][:] = 0
                 pids[e] = PID(0.002, 20, 15, 2)

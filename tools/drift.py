@@ -45,7 +45,7 @@ def run(precision: str, terrain: str, n: int, T: int, seed: int):
         hf = generate_perlin_terrain(293, seed=s0).astype(np.float32)
         tcfg, nt = {"type": "perlin", "config": {}}, 1
     rec = traj.record(n_envs=n, n_steps=T, hfield=hf, seed=seed)
-    alive = np.cumprod((rec["flags"] & 5) == 0, axis=0).astype(bool)  # still in the first episode after step t
+    alive = np.cumprod((rec["flags"] & 1) == 0, axis=0).astype(bool)  # still in the first episode after step t
     env = BallbotVecEnv(n, device="cuda:0", precision=precision, terrain_config=tcfg, auto_reset=False,
                         n_terrains=nt, seed=0)
     env.set_state(rec["qpos"][0], rec["qvel"][0], rec["warm"][0], rec["steps"][0])
