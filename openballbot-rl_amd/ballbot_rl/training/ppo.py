@@ -50,6 +50,16 @@ def _ptr(t: torch.Tensor):
     return C.c_void_p(t.data_ptr())
 
 
+_DEBUG_GRAPHS = os.environ.get("BB_DEBUG_GRAPHS", "0") != "0"
+
+
+def _dbg(msg: str) -> None:
+    """BB_DEBUG_GRAPHS=1: synchronize and log each graph phase (locates an asynchronous fault)."""
+    if _DEBUG_GRAPHS:
+        torch.cuda.synchronize()
+        print(f"[graphs] ok: {msg}", flush=True)
+
+
 def gae_hip(rewards, values, episode_starts, last_values, last_dones, gamma: float, gae_lambda: float):
     """GAE on device tensors [T][N] through the C-ABI (bb_gae); raises off-GPU."""
     from ballbot_gym import _native as N
@@ -283,6 +293,7 @@ class _UpdateGraphs:
                     mb_step()
         torch.cuda.synchronize(dev)
         self._restore(opt, [p_snap, {i: st_snap.get(id(p)) for i, p in enumerate(params)}, b_snap])
+        _dbg(f"update graphs built (fused={self.fused}, epoch graph={self.graph_epoch is not None})")
 
     def _fused_step(self, ppo: "BatchedPPO", slots):
         """bb_ppo_mlp_step: the whole minibatch (forward, loss, backward, clip,
@@ -421,7 +432,9 @@ class _UpdateGraphs:
             self.perms[e].copy_(torch.randperm(self.n, generator=ppo.shuffle_gen, device=ppo.device).view(self.nb, -1))
         total = ppo.n_epochs * self.nb
         snap = self._snapshot(ppo.optimizer) if ppo.target_kl is not None else None
+        _dbg("update: before replay")
         self._replay(total)
+        _dbg("update: replayed")
         log = self.log.cpu().numpy()
         if ppo.target_kl is not None:
             trip = np.nonzero(log[:, 4] > 1.5 * ppo.target_kl)[0]
@@ -469,6 +482,7 @@ class _RolloutGraph:
         obs = env.obs  # step_flags returns the env's own observation buffer: read in place
         flat, nflat = C.c_void_p(self.flat.data_ptr()), int(self.flat.numel())
         torch.cuda.synchronize(dev)
+        _dbg(f"rollout graph: capture T={T} n={n} obs={obs.data_ptr():#x} flat={self.flat.data_ptr():#x}")
         self.graph = torch.cuda.CUDAGraph()
         with torch.cuda.graph(self.graph):
             stream = C.c_void_p(torch.cuda.current_stream(dev).cuda_stream)
@@ -486,12 +500,15 @@ class _RolloutGraph:
                                              _ptr(self.ep_l[t]), _ptr(ppo._last_starts), nxt, stream),
                         "bb_rollout_track")
         torch.cuda.synchronize(dev)
+        _dbg("rollout graph: captured")
 
     def run(self, ppo: "BatchedPPO"):
         if ppo._last_obs.data_ptr() != self.env.obs.data_ptr():
             self.env.obs.copy_(ppo._last_obs)
         self.noise.normal_(generator=ppo.gen)  # == torch.randn(T, n, 3, generator=gen): the eager draws
+        _dbg("rollout graph: before replay")
         self.graph.replay()
+        _dbg("rollout graph: replayed")
         ppo._last_obs = self.env.obs
         return self.ep_r, self.ep_l
 

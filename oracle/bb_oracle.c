@@ -27,6 +27,13 @@
  */
 #include "bb_oracle.h"
 
+/* phase marks for the FLOP-counting build (oracle/flopcount.cpp); no-ops here:
+ * 0 kinematics, mass matrix, velocities, bias; 1 collision; 2 constraint
+ * assembly (Jacobians, impedance, aref); 3 Newton solver; 4 RK4/glue */
+#ifndef BBO_PHASE
+#define BBO_PHASE(k) ((void)0)
+#endif
+
 #include <math.h>
 #include <string.h>
 #include <float.h>
@@ -46,6 +53,11 @@ static const double PI = 3.14159265358979323846;
 static int g_flags = 0;
 static int g_maxiter = 100;          /* MuJoCo default opt.iterations */
 static double g_tol = 1e-10;         /* tighter than MuJoCo's 1e-8 (oracle) */
+/* line search: the oracle searches to roundoff (|phi'| <= 1e-15 |phi'(0)|, 200
+ * evaluations); MuJoCo stops at ls_tolerance 0.01 within ls_iterations 50
+ * (the FLOP-counting build uses those, oracle/flopcount.cpp) */
+static double g_lstol = 1e-15;
+static int g_lsmax = 200;
 
 int bbo_abi_version(void) { return 3; }
 void bbo_set_flags(int flags) { g_flags = flags; }
@@ -913,7 +925,8 @@ static void body_geoms(const double xpos[NB][3], const double xmat[NB][9], Conve
   Model* m = &M_;
   double t[3];
   /* tower_collision: cylinder r .11 hh .14 at (0,0,0.2) of base (ballbot.xml:41) */
-  m3v(t, xmat[1], (double[3]){0, 0, 0.2});
+  const double tower_c[3] = {0, 0, 0.2};
+  m3v(t, xmat[1], tower_c);
   v3add(g[0].c, xpos[1], t);
   g[0].a[0] = xmat[1][2]; g[0].a[1] = xmat[1][5]; g[0].a[2] = xmat[1][8];
   g[0].hh = 0.14; g[0].r = 0.11; cyl[0] = 1; body[0] = 1;
@@ -1235,7 +1248,7 @@ static int newton(const Efc* e, const double* Mm, const double* a0, double* a, d
     for (int r = 0; r < nr; r++) d0 -= force[r] * Js[r];
     d0 += sMdq;
     if (d0 >= 0) break; /* not a descent direction: converged to roundoff */
-    for (int ls = 0; ls < 200; ls++) {
+    for (int ls = 0; ls < g_lsmax; ls++) {
       for (int r = 0; r < nr; r++) jt[r] = jar[r] + alpha * Js[r];
       total_cost(e, jt, ft, Ht);
       double d1 = sMdq + alpha * sMs, d2 = sMs;
@@ -1245,7 +1258,7 @@ static int newton(const Efc* e, const double* Mm, const double* a0, double* a, d
           for (int q = 0; q < 3; q++) d2 += Js[3 * c + p] * Ht[9 * c + 3 * p + q] * Js[3 * c + q];
         }
       }
-      if (fabs(d1) <= 1e-15 * fabs(d0)) break;
+      if (fabs(d1) <= g_lstol * fabs(d0)) break;
       if (d1 < 0) lo = alpha; else hi = alpha;
       double an = alpha - d1 / d2;
       if (hi < 0) { if (an <= lo) an = 2 * alpha; }
@@ -1276,6 +1289,7 @@ static void forward_impl(const double* qpos, const double* qvel, const double* c
   Model* m = &M_;
   static __thread Work W_;
   Work* w = &W_;
+  BBO_PHASE(0);
   kinematics_all(qpos, w->xpos, w->xquat, w->xmat, w->xipos, w->xI, w->xanchor, w->xaxis);
   build_M(w->xmat, w->xpos, w->xipos, w->xI, w->xanchor, w->xaxis, w->scom, w->cinert, w->cdof, w->M);
 
@@ -1341,7 +1355,9 @@ static void forward_impl(const double* qpos, const double* qvel, const double* c
   Contact con[BBO_MAXCON];
   int nground = 0, nbody = 0, overflow = 0;
   int nc = 0;
+  BBO_PHASE(1);
   if (!(g_flags & BBO_DISABLE_CONTACT)) nc = collide(w->xpos, w->xmat, hf, size_z, con, &nground, &nbody, &overflow);
+  BBO_PHASE(2);
   static __thread Efc E;
   E.nc = nc;
   const double dmax = 0.95, tc = fmax(0.02, 2 * TIMESTEP), dr = 1.0;
@@ -1389,8 +1405,10 @@ static void forward_impl(const double* qpos, const double* qvel, const double* c
   else {
     if (warm_io) memcpy(a, warm_io, sizeof a); else memcpy(a, a0, sizeof a);
     for (int i = 0; i < NV; i++) if (!isfinite(a[i])) { memcpy(a, a0, sizeof a); break; }
+    BBO_PHASE(3);
     niter = newton(&E, w->M, a0, a, 1.0 / (m->meaninertia * NV));
   }
+  BBO_PHASE(4);
   if (warm_io) memcpy(warm_io, a, sizeof a);
 
   if (out) {

@@ -9,8 +9,8 @@ Checks (size-independent, every env-step of 300 steps of random actions):
 the reward is the reference's float32 chain of the returned obs/action, failure
 <=> tilt > 20 deg, clips hold, quaternions stay unit, nothing diverges; then a
 teacher-forced fp64 step of 64 envs -- 8 from each XCD's env range plus
-toppled envs the full kernel must take -- against the oracle on each env's own
-terrain.
+toppled robots (>32 base-tree contacts: the HBM spill block) the full kernel
+must take -- against the oracle on each env's own terrain.
 """
 import numpy as np
 import pytest
@@ -37,6 +37,27 @@ def _props(o, a, r, fl):
     assert np.array_equal(failed[~edge], tilt[~edge] > 20.0)
 
 
+def _toppled(q, env, tid, es, rng):
+    """Robots lying on their own terrain (tower across many prisms): base-tree contacts past
+    the 32 LDS slots, i.e. the per-env HBM spill block (as test_forward_parity_contacts_past_lds)."""
+    N1, hs = 292, 5.0
+    cache = {}
+    for e in es:
+        t = int(tid[e])
+        if t not in cache:
+            cache[t] = env.hfield(t).reshape(293, 293)
+        hf = cache[t]
+        th, yaw = np.radians(rng.uniform(80, 100)), rng.uniform(0, 2 * np.pi)
+        ax = np.array([np.cos(yaw), np.sin(yaw), 0.0])
+        x, y = rng.uniform(-0.5, 0.5, 2)
+        c0, r0 = int(round((x + hs) / (2 * hs) * N1)), int(round((y + hs) / (2 * hs) * N1))
+        top = float(hf[max(r0 - 1, 0):r0 + 2, max(c0 - 1, 0):c0 + 2].max()) * float(env.terrain_plan.size_z)
+        q[e, 0:3] = [x, y, top + rng.uniform(0.08, 0.10)]
+        q[e, 3:7] = [np.cos(th / 2), *(np.sin(th / 2) * ax)]
+        q[e, 10:13] = [x + 0.6 * np.cos(yaw), y + 0.6 * np.sin(yaw), top + 0.5]
+        q[e, 13:17] = [1, 0, 0, 0]
+
+
 @pytest.mark.parametrize("terrain,n_terrains", [("perlin", None), ("hills", 32)], ids=["perlin_full_bank", "hills32"])
 def test_config3_full_size_route0(oracle, terrain, n_terrains, monkeypatch):
     from ballbot_gym.envs import BallbotVecEnv
@@ -54,40 +75,46 @@ def test_config3_full_size_route0(oracle, terrain, n_terrains, monkeypatch):
             _props(info["terminal_observation"].cpu().numpy(), a.cpu().numpy(), rew.cpu().numpy(),
                    info["done_flags"].cpu().numpy())
     st = env.stats()
-    assert st["slow_path"] > 0 and st["diverged"] == 0 and st["resets"] > 0
-    if terrain == "perlin":  # toppled robots on perlin relief: contacts past the 32 LDS slots, in HBM
-        assert st["spill"] > 0, st
+    assert st["diverged"] == 0 and st["resets"] > 0
     q, v, w, s = env.get_state()
     assert np.allclose(np.linalg.norm(q[:, 3:7], axis=1), 1, atol=1e-9)
     assert np.allclose(np.linalg.norm(q[:, 13:17], axis=1), 1, atol=1e-9)
 
-    # teacher-forced spot check: 8 envs from each XCD's contiguous env range (512 envs each)
-    # and the 16 most tilted envs (base-tree contacts: the full kernel)
+    # one teacher-forced step from the current states, with 256 envs (every 16th, all XCD
+    # ranges) replaced by toppled robots: the full kernel's HBM spill block must be reached.
+    # Oracle spot check: 8 envs from each XCD's contiguous env range (512 envs each) and
+    # the 16 toppled envs with the most base-tree contacts
     rng = np.random.default_rng(3)
-    pick = [int(x) for b in range(8) for x in rng.choice(np.arange(512 * b, 512 * (b + 1)), 8, replace=False)]
-    up = 1 - 2 * (q[:, 4] ** 2 + q[:, 5] ** 2)  # R22 of the base quaternion
-    pick += [int(e) for e in np.argsort(up) if int(e) not in pick][:16]
     tid, _ = env.env_terrain()
+    size_z = float(env.terrain_plan.size_z)
+    top = np.arange(5, n, 16)
+    _toppled(q, env, tid, top, rng)
+    v[top] = rng.normal(0, 0.1, (len(top), 15))
+    hfs = {int(t): env.hfield(int(t)) for t in np.unique(tid[top])}
+    nb = np.array([oracle.forward(q[e], v[e], np.zeros(3), None, hfs[int(tid[e])], size_z).nbody for e in top])
+    assert (nb > 0).mean() > 0.5 and (nb > 32).any(), np.bincount(np.minimum(nb, 40))
+    pick = [int(x) for b in range(8) for x in rng.choice(np.setdiff1d(np.arange(512 * b, 512 * (b + 1)), top), 8,
+                                                          replace=False)]
+    pick += [int(e) for e in top[np.argsort(-nb)[:16]]]
     acts = rng.uniform(-1, 1, (n, 3)).astype(np.float32)
-    s0 = env.stats()["slow_path"]
+    s0 = env.stats()
+    env.auto_reset = False  # keep every post-step state (toppled robots terminate) for the comparison
     env.set_state(q, v, w, s)
     obs, rew, term, trunc, info = env.step(torch.tensor(acts, device=env.device))
-    assert env.stats()["slow_path"] - s0 >= 8
+    s1 = env.stats()
+    assert s1["slow_path"] - s0["slow_path"] >= int((nb > 0).sum())  # every touching env took the full kernel
+    assert s1["spill"] - s0["spill"] > 0, s1  # base-tree contacts past the 32 LDS slots, in HBM
     q1, v1, _, _ = env.get_state()
     o1, r1 = info["terminal_observation"].cpu().numpy(), rew.cpu().numpy()
     cfg = oracle.default_cfg()
-    full = 0
+    past = 0
     for e in pick:
         hf = env.hfield(int(tid[e]))
-        size_z = float(env.terrain_plan.size_z)
         qe, ve, we, se = q[e].copy(), v[e].copy(), w[e].copy(), np.array([s[e]], np.int32)
-        fo = oracle.forward(q[e], v[e], np.zeros(3), None, hf, size_z)
-        full += fo.nbody > 0
+        past += oracle.forward(q[e], v[e], np.zeros(3), None, hf, size_z).nbody > 32
         o, r, f, _, _ = oracle.env_step(cfg, qe, ve, we, se, acts[e], hf, size_z)
-        if f & 1:
-            continue  # auto-reset on the GPU: the stored state is the next episode's
+        assert np.abs(o1[e] - o).max() < 1e-6 and abs(r1[e] - r) < 1e-7, e
         assert np.abs(q1[e] - qe).max() < 1e-9, e
         assert np.abs(v1[e] - ve).max() < 1e-6 * max(1.0, np.abs(ve).max()), e
-        assert np.abs(o1[e] - o).max() < 1e-6 and abs(r1[e] - r) < 1e-7, e
-    assert full >= 4  # base-tree contacts among the picked envs
+    assert past >= 1  # toppled envs with more base-tree contacts than LDS slots among the picks
     env.close()

@@ -171,8 +171,10 @@ def _register():
 def test_custom_reward_batched_and_per_env():
     """The reference's reward chain (ballbot_env.py:929-937, 1019-1020) in float32:
     plugin(obs) * scale + action penalty, then + survival bonus unless failed.
-    The per-env host path is bit-exact against numpy's float32 chain; the batched
-    device path (plugin.batched on torch tensors, no host sync) agrees within 1e-8."""
+    The reward config's "scale" is also the env's reward_scale (ballbot_env.py:228-229),
+    so the plugin's 0.1 * |vel| is scaled by 0.1 again.  The per-env host path matches
+    numpy's float32 chain (atol 2e-8: the action-norm rounding, as in the parity tests);
+    the batched device path (plugin.batched on torch tensors, no host sync) agrees within 1e-8."""
     from ballbot_gym.envs import BallbotVecEnv
 
     _register()
@@ -190,7 +192,7 @@ def test_custom_reward_batched_and_per_env():
         ah = a.cpu().numpy()
         p = np.array([f32(0.1 * np.linalg.norm(tob[i, 12:14])) for i in range(n)], f32)
         nrm = np.sqrt((ah * ah).sum(1, dtype=f32), dtype=f32)
-        exp = p * f32(0.01) + f32(-0.0001) * (nrm * nrm)
+        exp = p * f32(0.1) + f32(-0.0001) * (nrm * nrm)
         exp = np.where(fail, exp, exp + f32(0.02)).astype(f32)
         np.testing.assert_allclose(r.cpu().numpy(), exp, rtol=0, atol=2e-8)
         rb = out["velocity_magnitude_batched_test"][1]

@@ -1,0 +1,83 @@
+"""Algorithmic FLOPs per env-step by config, from the
+op-counting build of the oracle (oracle/flopcount.cpp -> oracle/_build/libbb_flops.so).
+
+python tools/flops.py [--envs 64] [--steps 200] [--out profiles/r03_flops.json]
+
+Counts the restated reference algorithm (MuJoCo's mj_step for this model +
+env glue) at MuJoCo's solver tolerance, from the reset state under uniform
+random actions with auto-reset, per terrain config: flat (configs[1]),
+hills and perlin (configs[2]).  FLOP = add/sub + mul + div + sqrt +
+transcendental, one each; per-phase breakdown included.
+"""
+from __future__ import annotations
+
+import argparse
+import ctypes as C
+import json
+import subprocess
+import sys
+import time
+from pathlib import Path
+
+import numpy as np
+
+ROOT = Path(__file__).resolve().parent.parent
+sys.path.insert(0, str(ROOT / "openballbot-rl_amd"))
+
+PHASES = ("kinematics_mass_bias", "collision", "constraint_assembly", "newton_solver", "rk4_glue")
+KINDS = ("add_sub", "mul", "div", "sqrt", "transcendental", "compare")
+LIB = ROOT / "oracle" / "_build" / "libbb_flops.so"
+
+
+def lib():
+    subprocess.run(["make", "-s", "-C", str(ROOT / "oracle")], check=True)
+    L = C.CDLL(str(LIB))
+    L.bbo_count_flops.argtypes = [C.c_int, C.c_int, C.POINTER(C.c_float), C.c_double, C.c_double, C.c_double,
+                                  C.c_uint, C.POINTER(C.c_double)]
+    L.bbo_count_flops.restype = C.c_longlong
+    return L
+
+
+def count(L, hf: np.ndarray, size_z: float, n_envs: int, n_steps: int, seed: int = 1) -> dict:
+    from ballbot_gym.envs.config import init_offset
+
+    hf = np.ascontiguousarray(hf, np.float32).ravel()
+    out = (C.c_double * 30)()
+    t0 = time.perf_counter()
+    steps = L.bbo_count_flops(n_envs, n_steps, hf.ctypes.data_as(C.POINTER(C.c_float)), size_z,
+                              init_offset(hf, size_z), 1.0, seed, out)
+    dt = time.perf_counter() - t0
+    a = np.array(out[:]).reshape(5, 6)
+    per_phase = {p: {k: float(a[i, j]) for j, k in enumerate(KINDS)} for i, p in enumerate(PHASES)}
+    flop_phase = {p: float(a[i, :5].sum()) for i, p in enumerate(PHASES)}
+    return {"env_steps": int(steps), "seconds": round(dt, 2), "flops_per_env_step": float(a[:, :5].sum()),
+            "flops_by_phase": flop_phase, "ops_by_phase": per_phase}
+
+
+def configs():
+    from ballbot_gym.terrain import generate_hills_terrain
+    from ballbot_gym.terrain.perlin import generate_perlin_terrain
+
+    return {"flat": (np.zeros(293 * 293, np.float32), 2.0),
+            "hills_seed7": (generate_hills_terrain(293, seed=7).astype(np.float32), 2.0),
+            "perlin_seed7765": (generate_perlin_terrain(293, seed=7765).astype(np.float32), 2.0)}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--envs", type=int, default=64)
+    ap.add_argument("--steps", type=int, default=200)
+    ap.add_argument("--out", default=str(ROOT / "profiles" / "r03_flops.json"))
+    a = ap.parse_args()
+    L = lib()
+    res = {"what": "algorithmic FLOPs per env-step of the restated reference algorithm (oracle op-counter, "
+                   "MuJoCo tolerance 1e-8, uniform random actions, auto-reset)",
+           "envs": a.envs, "steps": a.steps, "configs": {}}
+    for name, (hf, sz) in configs().items():
+        res["configs"][name] = count(L, hf, sz, a.envs, a.steps)
+        print(name, json.dumps({k: v for k, v in res["configs"][name].items() if k != "ops_by_phase"}), flush=True)
+    Path(a.out).write_text(json.dumps(res, indent=1) + "\n")
+
+
+if __name__ == "__main__":
+    main()
