@@ -25,6 +25,7 @@ for _p in (ROOT / "openballbot-rl_amd", ROOT / "tests"):
         sys.path.insert(0, str(_p))
 
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
+FP64_VECTOR_PEAK_TFLOPS = 78.6  # MI355X spec: half the 157.3 TF FP32 vector rate (MI355X_MICROARCH.md)
 
 
 def algorithmic_bytes(precision: str) -> int:
@@ -69,6 +70,22 @@ def cpu_baseline(seconds: float = 12.0, threads: int = 1) -> dict:
     return {"value": done_steps / dt, "unit": "env-steps/s", "cores": threads, "kind": "port",
             "sample": f"{n} envs x {done_steps // n} steps, flat, random actions, {threads} thread(s) on '{cpu}' "
                       f"(fp64 oracle restating the reference step; MuJoCo itself is not available)"}
+
+
+def flop_count(env, terrain: str, n_envs: int = 16, n_steps: int = 100) -> dict:
+    """Algorithmic FLOPs per env-step of the restated reference algorithm on this
+    workload's terrain (oracle/flopcount.cpp: the oracle compiled over a counting
+    double, MuJoCo's solver settings; the checker's build, in the CPU leg)."""
+    sys.path.insert(0, str(ROOT / "tools"))
+    import flops as F
+
+    plan = env.terrain_plan
+    slot = int(plan.streams[0][0]) if plan.streams is not None else 0  # the first reset's terrain
+    r = F.count(F.lib(), env.hfield(slot), float(plan.size_z), n_envs, n_steps)
+    return {"flops_per_env_step": r["flops_per_env_step"], "by_phase": r["flops_by_phase"],
+            "sample": f"{r['env_steps']} env-steps ({n_envs} envs x {n_steps}) on the first-drawn terrain of the "
+                      f"'{terrain}' bank (seed {plan.seeds[slot]}), uniform random actions, auto-reset; MuJoCo "
+                      "solver settings (tolerance 1e-8, line search 0.01 / 50 evaluations)"}
 
 
 def parity_probe(env, n_probe: int = 64) -> dict:
@@ -171,7 +188,8 @@ def main() -> None:
         dist.barrier()
     torch.cuda.synchronize()
     ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-    env.time_kernel(args.steps)  # HIP events around the dominant (fast step) kernel on the env's stream
+    env.time_kernel(args.steps)  # HIP events around each step kernel, on the stream it is launched on
+    st0 = env.stats()
     t0 = time.perf_counter()
     ev0.record()
     for i in range(args.steps):
@@ -183,20 +201,29 @@ def main() -> None:
     torch.cuda.synchronize()
     elapsed = time.perf_counter() - t0
     step_ms = ev0.elapsed_time(ev1) / args.steps  # whole bb_step sequence per step, torch's stream
+    st1 = env.stats()
     if graph is not None:  # graph replays carry no per-kernel events: time eager steps of the same kernels
         env.time_kernel(min(args.steps, 100))
         for i in range(min(args.steps, 100)):
             env.step_async_raw(pool[i % 64])
         torch.cuda.synchronize()
-    kern_ms, kern_n = env.kernel_ms()  # dominant kernel alone
+    ktimes, kern_n = env.kernel_times()  # fast, predicted-full (side stream), hand-over full
     elapsed = max_over_ranks(elapsed, device=dev)
     stats = env.stats()
+    # envs per launch of each kernel over the timed steps: the full kernel stepped
+    # slow_path env-steps (predicted + handed over), the fast kernel the rest
+    full_per_step = (st1["slow_path"] - st0["slow_path"]) / args.steps
     launch = env.launch_config()
 
     if rank == 0:
         total_steps = n * world * args.steps
         value = total_steps / elapsed
-        abytes = algorithmic_bytes(args.precision) * n
+        # the dominant kernel: on flat banks the fast kernel; on relief banks the longer of
+        # the fast kernel and the concurrent predicted full kernel (the critical path)
+        dom = "fast" if ktimes["fast"] >= ktimes["predicted_full"] else "predicted_full"
+        kern_ms = ktimes[dom]
+        envs_dom = (n - full_per_step) if dom == "fast" else full_per_step
+        abytes = algorithmic_bytes(args.precision) * envs_dom
         achieved = abytes / (kern_ms * 1e-3) / 1e9
         traffic = issue_frac = None
         tj = Path(args.traffic_json)
@@ -232,8 +259,11 @@ def main() -> None:
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
                          "note": "latency/VALU-bound per-lane physics; HBM bytes = algorithmic state I/O "
-                                 f"({algorithmic_bytes(args.precision)} B/env-step)",
-                         "kernel": "step_kernel<T,false> (fast path)", "kernel_ms": kern_ms,
+                                 f"({algorithmic_bytes(args.precision)} B/env-step) x the envs the kernel stepped",
+                         "kernel": ("step_kernel<T,false> (fast path)" if dom == "fast"
+                                    else "step_kernel<T,true> (predicted full kernel, side stream)"),
+                         "kernel_ms": kern_ms, "envs_per_launch": envs_dom, "kernel_ms_all": ktimes,
+                         "full_kernel_envs_per_step": full_per_step,
                          "kernel_launches_timed": kern_n, "step_ms_hip_events": step_ms,
                          # share of the kernel's wave cycles spent issuing (rocprofv3 SQ
                          # counters, profiles/): the bound that binds is instruction issue
@@ -243,6 +273,13 @@ def main() -> None:
         if world == 1 and not args.no_cpu_baseline:
             if args.terrain == "flat":
                 line["parity"] = parity_probe(env)
+            try:  # the compute side of the roofline: reference-algorithm FLOPs at this throughput
+                fl = flop_count(env, args.terrain)
+                tf = fl["flops_per_env_step"] * value / 1e12
+                line["roofline"]["valu_fp64"] = {"achieved": tf, "peak": FP64_VECTOR_PEAK_TFLOPS, "unit": "TFLOP/s",
+                                                 "frac": tf / FP64_VECTOR_PEAK_TFLOPS, **fl}
+            except Exception as e:  # the counting build needs g++ (present here and on the box)
+                line["roofline"]["valu_fp64"] = {"error": repr(e)}
             line["cpu_baseline"] = cpu_baseline(args.cpu_seconds)
             # all host cores granted to this job (OMP_NUM_THREADS; 16 on the GPU box)
             thr = int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or min(16, os.cpu_count() or 1)

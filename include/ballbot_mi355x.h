@@ -314,6 +314,10 @@ int bb_get_offsets(bb_handle* h, float* out);
  * counterpart (bench.py's roofline.achieved). */
 int bb_time_kernel(bb_handle* h, int max_launches);
 int bb_kernel_ms(bb_handle* h, double* avg_ms, int32_t* launches);
+/* the same timed steps, all three step kernels: avg_ms3 = [fast kernel, predicted full
+ * kernel (route 0, concurrent on the handle's side stream; 0 when not launched),
+ * hand-over full kernel (from the later of the two to its end)] */
+int bb_kernel_times(bb_handle* h, double* avg_ms3, int32_t* launches);
 
 #ifdef __cplusplus
 }

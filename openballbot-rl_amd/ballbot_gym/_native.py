@@ -90,7 +90,7 @@ EXPORTS = [
     "bb_get_offsets", "bb_get_config", "bb_time_kernel", "bb_kernel_ms", "bb_generate_perlin", "bb_get_hfield",
     "bb_gae", "bb_render_depth", "bb_ppo_loss", "bb_adamw_clip", "bb_ppo_mlp_workspace_bytes", "bb_ppo_mlp_step",
     "bb_ppo_mlp_act", "bb_rollout_track", "bb_depth_encoder_workspace_bytes", "bb_depth_encoder",
-    "bb_set_terrain_stream", "bb_get_env_terrain",
+    "bb_set_terrain_stream", "bb_get_env_terrain", "bb_kernel_times",
 ]
 
 ABI_VERSION = 12  # include/ballbot_mi355x.h BB_ABI_VERSION
@@ -175,6 +175,7 @@ def _load(path: Path):
     L.bb_depth_encoder.argtypes = [C.POINTER(EncoderParams), vp, C.c_int64, vp, C.c_int64, C.c_int, C.c_int, C.c_int,
                                    C.c_float, C.c_float, vp, C.c_int64, vp, C.c_int64, vp]
     L.bb_kernel_ms.argtypes = [vp, C.POINTER(C.c_double), C.POINTER(C.c_int32)]
+    L.bb_kernel_times.argtypes = [vp, C.POINTER(C.c_double), C.POINTER(C.c_int32)]
     for name in [n for n in EXPORTS if n not in ("bb_default_params", "bb_abi_version")]:
         getattr(L, name).restype = C.c_int
     if L.bb_abi_version() != ABI_VERSION:

@@ -373,6 +373,13 @@ class BallbotVecEnv:
         N.check(N.lib().bb_kernel_ms(self._h, C.byref(ms), C.byref(k)), "bb_kernel_ms")
         return ms.value, k.value
 
+    def kernel_times(self):
+        """Average ms of the fast kernel, the predicted full kernel (route 0, side stream) and
+        the hand-over full kernel over the steps timed since time_kernel(); and the count."""
+        t, k = (C.c_double * 3)(), C.c_int32()
+        N.check(N.lib().bb_kernel_times(self._h, t, C.byref(k)), "bb_kernel_times")
+        return {"fast": t[0], "predicted_full": t[1], "handover_full": t[2]}, k.value
+
     def launch_config(self) -> Dict[str, int]:
         out = (C.c_int32 * 5)()
         N.check(N.lib().bb_get_config(self._h, out), "bb_get_config")

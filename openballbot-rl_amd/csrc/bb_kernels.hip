@@ -471,6 +471,13 @@ __global__ __launch_bounds__(1024) void split_kernel(Dev d) {
   if (t == 1023) { d.slow_count[0] = sf[t]; d.slow_count[1] = ss[t]; d.slow_count[2] = 0; }
 }
 
+// route 1: the hand-over count starts at zero for the fast kernel.  A kernel,
+// not hipMemsetAsync: a captured step then holds only kernel nodes, ordered
+// like any other launch on the stream.
+__global__ void zero_count_kernel(int* c) {
+  if (threadIdx.x == 0) *c = 0;
+}
+
 __global__ void assign_kernel(Dev d, const int32_t* ids) {
   const int e = blockIdx.x * blockDim.x + threadIdx.x;
   if (e >= d.n) return;
@@ -495,8 +502,11 @@ struct bb_handle {
   float* offset;
   float* hmax;
   std::vector<float> h_offset;
-  // optional HIP-event timing of the fast step kernel (bb_time_kernel)
+  // optional HIP-event timing of the step kernels (bb_time_kernel): per timed
+  // step 6 events, pairs around the fast kernel, the predicted full kernel
+  // (route 0, on the side stream) and the hand-over full kernel
   std::vector<hipEvent_t> tev;
+  std::vector<uint8_t> tpred;  // per timed step: the predicted full kernel was launched
   int tcap = 0, tn = 0;
   // step routing: 0 predict + concurrent full kernel; 1 serial fast-then-full;
   // -1 (default) serial while every terrain in the bank is flat, else 0.  On
@@ -545,14 +555,16 @@ int launch_step(bb_handle* h, const float* a, float* o, float* r, uint8_t* dn, f
   if (route == 1) {
     // serial route: the fast kernel over every env, then the full kernel over
     // the envs it handed over (no prediction, no second stream)
-    HIPCHK(hipMemsetAsync(cnt + 2, 0, sizeof(int), s));
+    hipLaunchKernelGGL(zero_count_kernel, dim3(1), dim3(64), 0, s, cnt + 2);
     const bool timed = h->tn < h->tcap;
-    if (timed) HIPCHK(hipEventRecord(h->tev[2 * h->tn], s));
+    hipEvent_t* ev = timed ? &h->tev[6 * h->tn] : nullptr;
+    if (timed) HIPCHK(hipEventRecord(ev[0], s));
     hipLaunchKernelGGL((step_kernel<T, false>), dim3(blocks), dim3(WAVE), lds, s, m, h->cfg, h->d, a, o, r, dn, t,
                        p2, ar, h->team, epw, (const int*)nullptr, (const int*)nullptr);
-    if (timed) { HIPCHK(hipEventRecord(h->tev[2 * h->tn + 1], s)); h->tn++; }
+    if (timed) HIPCHK(hipEventRecord(ev[1], s));
     hipLaunchKernelGGL((step_kernel<T, true>), dim3(fblocks), dim3(WAVE), flds, s, m, h->cfg, h->d, a, o, r, dn, t,
                        p2, ar, h->team, epf, (const int*)h->d.slow_list, (const int*)(cnt + 2));
+    if (timed) { HIPCHK(hipEventRecord(ev[5], s)); h->tpred[h->tn] = 0; h->tn++; }
     HIPCHK(hipGetLastError());
     return 0;
   }
@@ -562,17 +574,21 @@ int launch_step(bb_handle* h, const float* a, float* o, float* r, uint8_t* dn, f
   hipLaunchKernelGGL(split_kernel, dim3(1), dim3(1024), 0, s, h->d);
   HIPCHK(hipEventRecord(h->fork, s));
   HIPCHK(hipStreamWaitEvent(h->side, h->fork, 0));
+  const bool timed = h->tn < h->tcap;
+  hipEvent_t* ev = timed ? &h->tev[6 * h->tn] : nullptr;
+  if (timed) HIPCHK(hipEventRecord(ev[2], h->side));
   hipLaunchKernelGGL((step_kernel<T, true>), dim3(fblocks), dim3(WAVE), flds, h->side, m, h->cfg, h->d, a, o, r, dn,
                      t, p2, ar, h->team, epf, (const int*)h->d.pred_envs, (const int*)(cnt + 1));
-  const bool timed = h->tn < h->tcap;
-  if (timed) HIPCHK(hipEventRecord(h->tev[2 * h->tn], s));
+  if (timed) HIPCHK(hipEventRecord(ev[3], h->side));
+  if (timed) HIPCHK(hipEventRecord(ev[0], s));
   hipLaunchKernelGGL((step_kernel<T, false>), dim3(blocks), dim3(WAVE), lds, s, m, h->cfg, h->d, a, o, r, dn, t, p2,
                      ar, h->team, epw, (const int*)h->d.fast_envs, (const int*)(cnt + 0));
-  if (timed) { HIPCHK(hipEventRecord(h->tev[2 * h->tn + 1], s)); h->tn++; }
+  if (timed) HIPCHK(hipEventRecord(ev[1], s));
   HIPCHK(hipEventRecord(h->join, h->side));
   HIPCHK(hipStreamWaitEvent(s, h->join, 0));
   hipLaunchKernelGGL((step_kernel<T, true>), dim3(fblocks), dim3(WAVE), flds, s, m, h->cfg, h->d, a, o, r, dn, t, p2,
                      ar, h->team, epf, (const int*)h->d.slow_list, (const int*)(cnt + 2));
+  if (timed) { HIPCHK(hipEventRecord(ev[5], s)); h->tpred[h->tn] = 1; h->tn++; }
   HIPCHK(hipGetLastError());
   return 0;
 }
@@ -688,8 +704,8 @@ int bb_create(int n_envs, int device, const bb_params* p, bb_handle** out) {
   HIPCHK(hipMemset(h->hmax, 0, sizeof(float) * nt));
   HIPCHK(hipMalloc((void**)&d.stats, sizeof(unsigned long long) * 8));
   HIPCHK(hipMalloc((void**)&d.slow_list, sizeof(int) * n));
-  HIPCHK(hipMalloc((void**)&d.slow_count, sizeof(int) * 4));
-  HIPCHK(hipMemset(d.slow_count, 0, sizeof(int) * 4));
+  HIPCHK(hipMalloc((void**)&d.slow_count, sizeof(int) * 64));  // 4 used; a 256-B block of its own
+  HIPCHK(hipMemset(d.slow_count, 0, sizeof(int) * 64));
   HIPCHK(hipMalloc((void**)&d.fast_envs, sizeof(int) * n));
   HIPCHK(hipMalloc((void**)&d.pred_envs, sizeof(int) * n));
   HIPCHK(hipMalloc((void**)&d.pred_mark, n));
@@ -1158,25 +1174,49 @@ int bb_time_kernel(bb_handle* h, int max_launches) {
   HIPCHK(hipSetDevice(h->device));
   HIPCHK(hipDeviceSynchronize());
   for (hipEvent_t e : h->tev) (void)hipEventDestroy(e);
-  h->tev.assign(2 * (size_t)max_launches, nullptr);
+  h->tev.assign(6 * (size_t)max_launches, nullptr);
+  h->tpred.assign((size_t)max_launches, 0);
   for (hipEvent_t& e : h->tev) HIPCHK(hipEventCreate(&e));
   h->tcap = max_launches;
   h->tn = 0;
   return 0;
 }
 
+int bb_kernel_times(bb_handle* h, double* avg_ms3, int32_t* launches) {
+  if (!h || !avg_ms3) return fail("bb_kernel_times: NULL argument");
+  HIPCHK(hipSetDevice(h->device));
+  double sum[3] = {0, 0, 0};
+  int npred = 0;
+  for (int i = 0; i < h->tn; i++) {
+    hipEvent_t* ev = &h->tev[6 * i];
+    HIPCHK(hipEventSynchronize(ev[5]));
+    float ms = 0.f;
+    HIPCHK(hipEventElapsedTime(&ms, ev[0], ev[1]));  // fast kernel
+    sum[0] += ms;
+    float a = 0.f, b = 0.f;
+    HIPCHK(hipEventElapsedTime(&a, ev[1], ev[5]));  // hand-over full kernel after the fast kernel ...
+    if (h->tpred[i]) {                              // ... or after the predicted full kernel (side stream)
+      HIPCHK(hipEventElapsedTime(&ms, ev[2], ev[3]));
+      sum[1] += ms;
+      npred++;
+      HIPCHK(hipEventElapsedTime(&b, ev[3], ev[5]));
+      a = a < b ? a : b;
+    }
+    sum[2] += a;
+  }
+  avg_ms3[0] = h->tn ? sum[0] / h->tn : 0.0;
+  avg_ms3[1] = npred ? sum[1] / npred : 0.0;
+  avg_ms3[2] = h->tn ? sum[2] / h->tn : 0.0;
+  if (launches) *launches = h->tn;
+  return 0;
+}
+
 int bb_kernel_ms(bb_handle* h, double* avg_ms, int32_t* launches) {
   if (!h || !avg_ms) return fail("bb_kernel_ms: NULL argument");
-  HIPCHK(hipSetDevice(h->device));
-  double sum = 0.0;
-  for (int i = 0; i < h->tn; i++) {
-    HIPCHK(hipEventSynchronize(h->tev[2 * i + 1]));
-    float ms = 0.f;
-    HIPCHK(hipEventElapsedTime(&ms, h->tev[2 * i], h->tev[2 * i + 1]));
-    sum += ms;
-  }
-  *avg_ms = h->tn ? sum / h->tn : 0.0;
-  if (launches) *launches = h->tn;
+  double t[3];
+  const int rc = bb_kernel_times(h, t, launches);
+  if (rc) return rc;
+  *avg_ms = t[0];
   return 0;
 }
 
