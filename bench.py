@@ -132,6 +132,8 @@ def main() -> None:
     ap.add_argument("--n-terrains", type=int, default=None,
                     help="terrain bank size (default: 16 host-generated seeds; perlin: the whole 10^4 seed space on the GPU)")
     ap.add_argument("--cameras", action="store_true", help="also render the depth cameras (F2) every 6 steps")
+    ap.add_argument("--shared-stream", action="store_true",
+                    help="perlin: all envs on one terrain seed stream (train.py's convention) instead of one per env")
     ap.add_argument("--graph", action="store_true",
                     help="replay the step as one HIP graph (kernel_ms is then timed on eager steps after the run)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
@@ -159,14 +161,21 @@ def main() -> None:
     dev = torch.device("cuda", gpu)
     torch.cuda.set_device(dev)
 
-    from ballbot_gym.distributed import env_shard, max_over_ranks
+    from ballbot_gym.distributed import env_shard, max_over_ranks, shard_stream_seeds
     from ballbot_gym.envs import BallbotVecEnv
 
     # weak scaling: every rank owns a contiguous block of `--envs` global env ids
     first_env, n = env_shard(args.envs * world, rank, world)
-    env = BallbotVecEnv(n, device=dev, precision=args.precision, seed=1000,  # one shared stream (train.py:82-89)
+    # terrain draws: "random uneven heightfield" (configs[2]) -- on the GPU-generated perlin
+    # bank every env draws from its own generator, seed 1000 + global env id (the eval
+    # VecEnv's per-env seeds, train.py:90-97), so the 4096 envs sample 4096 terrain
+    # sequences; the training convention (one shared stream, train.py:82-89) would put
+    # every env on the same terrain at the start.  Host-generated banks: the shared stream.
+    per_env = args.terrain == "perlin" and not args.shared_stream
+    env = BallbotVecEnv(n, device=dev, precision=args.precision, seed=1000,
                         terrain_config={"type": args.terrain, "config": {}}, n_terrains=args.n_terrains,
-                        disable_cameras=not args.cameras)
+                        disable_cameras=not args.cameras,
+                        stream_seeds=shard_stream_seeds(1000, first_env, n, per_env=True) if per_env else None)
 
     static_a = torch.zeros(n, 3, device=dev)
     graph = env.capture_step(static_a) if args.graph else None  # one rollout step = one HIP graph
@@ -252,6 +261,7 @@ def main() -> None:
             "config": {"workload": f"{n} envs/GPU, {args.terrain} terrain, random actions "
                                    f"(BASELINE configs[{1 if args.terrain == 'flat' else 2}])",
                        "n_terrains": env.n_terrains, "depth_cameras": bool(args.cameras),
+                       "terrain_streams": "per env (seed 1000 + env id)" if per_env else "shared (seed 1000)",
                        "hip_graph": graph is not None, "burn_in_steps": args.burn_in,
                        "envs_per_gpu": n, "total_envs": n * world, "precision": args.precision,
                        "parallelism": f"env-sharded x{world} (no collective on the step path)",

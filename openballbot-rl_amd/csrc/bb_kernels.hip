@@ -173,8 +173,11 @@ __global__ __launch_bounds__(64) void step_kernel(ModelT<T> mg, EnvCfg cfg, Dev 
   // instead of piling onto the first few.
   const int nwg = int(gridDim.x), b = int(blockIdx.x);
   int g;
+  // list launches: the count is clamped to the list's size (n), so a count that
+  // was not reset cannot send a workgroup past the list
+  const int ecnt = elist ? min(*ecount, d.n) : 0;
   if (elist) {
-    const int na = (*ecount + epw - 1) / epw, nb = (na + 7) & ~7;
+    const int na = (ecnt + epw - 1) / epw, nb = (na + 7) & ~7;
     if (nb > nwg) {
       g = b;  // too few workgroups in the grid for the rounded-up permutation
     } else {
@@ -196,10 +199,10 @@ __global__ __launch_bounds__(64) void step_kernel(ModelT<T> mg, EnvCfg cfg, Dev 
   if (team >= epw) return;
   int e = g * epw + team;
   if (elist) {  // env list of this launch (ascending env ids)
-    if (e >= *ecount) return;
+    if (e >= ecnt) return;
     e = elist[e];
   }
-  if (e >= d.n) return;
+  if (unsigned(e) >= unsigned(d.n)) return;
   const bool lead = tm.tl == 0;
 #ifdef BB_PHASE_CLOCKS
   const unsigned long long t_env0 = clock64();
@@ -225,7 +228,8 @@ __global__ __launch_bounds__(64) void step_kernel(ModelT<T> mg, EnvCfg cfg, Dev 
   int fl = env_step<T, BODY>(m, cfg, q, v, w, step, a, tr, W, o, r, p2, &iters, tm);
   if (!BODY && (fl & F_SLOWPATH)) {
     if (lead) {
-      d.slow_list[atomicAdd(d.slow_count + 2, 1)] = e;
+      const int at = atomicAdd(d.slow_count + 2, 1);
+      if (at < d.n) d.slow_list[at] = e;  // never past the list, whatever the count holds
     }
     return;
   }
