@@ -175,7 +175,11 @@ BB_HD void prism_centroid(const PrismG<T>& P, T* cen) {
 // and 24 segment pairs.
 template <typename T>
 #ifdef __HIP_DEVICE_COMPILE__
+#ifdef BB_CAPSULE_INLINE  // variant build (tools/lib_bench.py): the same source inlined
+__attribute__((always_inline))
+#else
 __attribute__((noinline))
+#endif
 #endif
 BB_HD bool capsule_prism_apart(const Seg<T>& g, const PrismG<T>& P, const T* p0, const T* p1, T& dist, T* n, T* pos) {
   T best2 = T(1e30), bp[3] = {0, 0, 0}, bq[3] = {0, 0, 0};

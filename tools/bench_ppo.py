@@ -57,7 +57,12 @@ def main():
         from ballbot_rl.encoders import TinyAutoencoder, collect_depth_images, train_autoencoder
 
         t = time.perf_counter()
-        imgs = collect_depth_images(env, 65536, seed=a.seed)
+        # frames from a separate env (>= 1024 envs: fast collection; the training env's terrain
+        # streams stay untouched by the pretraining)
+        penv = BallbotVecEnv(max(a.envs, 1024), device="cuda:0", precision=a.precision, seed=a.seed + 1,
+                             terrain_config={"type": a.terrain, "config": {}}, disable_cameras=False)
+        imgs = collect_depth_images(penv, 65536, seed=a.seed)
+        penv.close()
         ae = TinyAutoencoder(env.cam_h, env.cam_w)
         train_autoencoder(ae, imgs, epochs=2, batch_size=256, log=lambda *_: None)
         frozen = ae.encoder.eval()

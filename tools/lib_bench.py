@@ -23,7 +23,8 @@ def build(name, flags):
     out.parent.mkdir(parents=True, exist_ok=True)
     cmd = ["hipcc", "--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC", "-shared", *flags, "-o", str(out)] + [
         str(ROOT / "openballbot-rl_amd" / "csrc" / f)
-        for f in ("bb_kernels.hip", "bb_terrain.hip", "bb_rollout.hip", "bb_render.hip", "bb_ppo.hip")]
+        for f in ("bb_kernels.hip", "bb_terrain.hip", "bb_rollout.hip", "bb_render.hip", "bb_ppo.hip", "bb_mlp.hip",
+                  "bb_encoder.hip")]
     subprocess.run(cmd, check=True)
     return out
 

@@ -15,11 +15,33 @@ import shutil
 from pathlib import Path
 
 KERNEL = "step_kernel"
+SEL = {"which": "fast"}  # --kernel: fast (step_kernel<T,false>) or pred (the route-0 predicted full kernel)
 
 
 def is_fast(name):
-    """The dominant kernel: the fast step kernel step_kernel<T, false>."""
+    """The fast step kernel step_kernel<T, false>."""
     return KERNEL in name and ", false>" in name
+
+
+def is_full(name):
+    return KERNEL in name and ", true>" in name
+
+
+def select_ids(recs):
+    """Dispatch ids of the selected kernel.  pred: on route 0 the predicted full kernel is
+    the step_kernel<T,true> dispatch launched right before each fast dispatch (the
+    hand-over full kernel comes after it)."""
+    recs = sorted(recs, key=lambda r: int(r["Dispatch_Id"]))
+    if SEL["which"] == "fast":
+        return [int(r["Dispatch_Id"]) for r in recs if is_fast(r["Kernel_Name"])]
+    out, last_full = [], None
+    for r in recs:
+        if is_full(r["Kernel_Name"]):
+            last_full = int(r["Dispatch_Id"])
+        elif is_fast(r["Kernel_Name"]) and last_full is not None:
+            out.append(last_full)
+            last_full = None
+    return out
 
 
 def rows(p):
@@ -29,8 +51,13 @@ def rows(p):
 
 def counters(p, names, last):
     per = {}
-    for r in rows(p):
-        if not is_fast(r["Kernel_Name"]):
+    rr = rows(p)
+    seen = {}
+    for r in rr:
+        seen.setdefault(int(r["Dispatch_Id"]), r)
+    keep = set(select_ids(list(seen.values())))
+    for r in rr:
+        if int(r["Dispatch_Id"]) not in keep:
             continue
         d = per.setdefault(int(r["Dispatch_Id"]), {})
         d[r["Counter_Name"]] = d.get(r["Counter_Name"], 0.0) + float(r["Counter_Value"])
@@ -45,11 +72,16 @@ def main():
     ap.add_argument("--timed", type=int, default=300, help="timed step_kernel dispatches at the end of the trace run")
     ap.add_argument("--pmc-last", type=int, default=20)
     ap.add_argument("--traffic", action="store_true")
+    ap.add_argument("--kernel", default="fast", choices=["fast", "pred"])
+    ap.add_argument("--f64", action="store_true", help="also summarise the FP64 VALU instruction pass (sq64)")
     a = ap.parse_args()
+    SEL["which"] = a.kernel
     src, dst = Path(a.src), Path(a.dst)
     dst.parent.mkdir(parents=True, exist_ok=True)
     shutil.copy(src / "trace" / "run_kernel_stats.csv", str(dst) + "_kernel_stats.csv")
-    tr = [r for r in rows(src / "trace" / "run_kernel_trace.csv") if is_fast(r["Kernel_Name"])]
+    allr = rows(src / "trace" / "run_kernel_trace.csv")
+    keep = set(select_ids(allr))
+    tr = [r for r in allr if int(r["Dispatch_Id"]) in keep]
     tr.sort(key=lambda r: int(r["Start_Timestamp"]))
     timed = tr[-a.timed:]
     durs = [(int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) * 1e-6 for r in timed]
@@ -60,6 +92,7 @@ def main():
         "avg_ms_rocprof": sum(durs) / len(durs),
         "min_ms": min(durs), "max_ms": max(durs),
         "bench_kernel_ms_hip_events": bench["roofline"]["kernel_ms"],
+        "bench_kernel_ms_all": bench["roofline"].get("kernel_ms_all"),
         "bench_value": bench["value"],
         "bench_config": bench["config"],
         "vgpr": timed[0].get("VGPR_Count"), "agpr": timed[0].get("Accum_VGPR_Count"),
@@ -86,6 +119,12 @@ def main():
         "wave_cycles_per_wave": 4 * sq["SQ_WAVE_CYCLES"] / waves,
         "effective_clock_ghz": f["GRBM_GUI_ACTIVE"] / 8 / (out["avg_ms_rocprof"] * 1e-3) / 1e9,
     }
+    if a.f64:  # executed FP64 VALU instructions per wave (x64 lanes: an upper bound on FP64 FLOP, FMA = 2)
+        n64 = ["SQ_INSTS_VALU_ADD_F64", "SQ_INSTS_VALU_MUL_F64", "SQ_INSTS_VALU_FMA_F64", "SQ_INSTS_VALU_TRANS_F64"]
+        c64, n6 = counters(src / "sq64" / "run_counter_collection.csv", n64, a.pmc_last)
+        fl = 64 * (c64[n64[0]] + c64[n64[1]] + 2 * c64[n64[2]] + c64[n64[3]])
+        out["pmc_f64"] = {**c64, "dispatches_averaged": n6, "fp64_flop_upper_bound_per_launch": fl,
+                          "fp64_tflops_upper_bound": fl / (out["avg_ms_rocprof"] * 1e-3) / 1e12}
     (Path(str(dst) + "_summary.json")).write_text(json.dumps(out, indent=1))
     print(json.dumps(out, indent=1))
     if a.traffic:

@@ -5,20 +5,27 @@
 #            busy cycles summed over the 8 XCDs -> effective clock)
 #   write  : --pmc WRITE_SIZE
 #   sq     : SQ instruction / wait counters
+#   sq64   : FP64 VALU instruction counters (F64=1)
 # Each pass is its own process (counters never combined with traces).
+# TERRAIN=perlin profiles configs[2] (the bench's per-env terrain streams).
 set -o pipefail
 TAG=${TAG:-r01}
 PREC=${PREC:-fp64}
-OUT=gpurun_out/prof_${TAG}_${PREC}
+TERRAIN=${TERRAIN:-flat}
+OUT=gpurun_out/prof_${TAG}_${PREC}_${TERRAIN}
 mkdir -p $OUT
 export TMPDIR=/tmp
-B="bench.py --precision $PREC --no-cpu-baseline"
+B="bench.py --precision $PREC --terrain $TERRAIN --no-cpu-baseline"
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/trace -o run -- \
   python3 $B --steps 300 --warmup 300 > $OUT/bench_trace.json || exit $?
-timeout -k 10 300 rocprofv3 --pmc FETCH_SIZE GRBM_GUI_ACTIVE --output-format csv -d $OUT/fetch -o run -- \
+timeout -s KILL 120 rocprofv3 --pmc FETCH_SIZE GRBM_GUI_ACTIVE --output-format csv -d $OUT/fetch -o run -- \
   python3 $B --steps 20 --warmup 300 > $OUT/bench_fetch.json || exit $?
-timeout -k 10 300 rocprofv3 --pmc WRITE_SIZE --output-format csv -d $OUT/write -o run -- \
+timeout -s KILL 120 rocprofv3 --pmc WRITE_SIZE --output-format csv -d $OUT/write -o run -- \
   python3 $B --steps 20 --warmup 300 > $OUT/bench_write.json || exit $?
-timeout -k 10 300 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_WAVE_CYCLES \
+timeout -s KILL 120 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_WAVE_CYCLES \
   --output-format csv -d $OUT/sq -o run -- python3 $B --steps 20 --warmup 300 > $OUT/bench_sq.json || exit $?
+if [ "${F64:-0}" = "1" ]; then
+  timeout -s KILL 120 rocprofv3 --pmc SQ_INSTS_VALU_ADD_F64 SQ_INSTS_VALU_MUL_F64 SQ_INSTS_VALU_FMA_F64 SQ_INSTS_VALU_TRANS_F64 \
+    --output-format csv -d $OUT/sq64 -o run -- python3 $B --steps 20 --warmup 300 > $OUT/bench_sq64.json || exit $?
+fi
 find $OUT -name "*.csv" | head -50
