@@ -72,20 +72,33 @@ def cpu_baseline(seconds: float = 12.0, threads: int = 1) -> dict:
                       f"(fp64 oracle restating the reference step; MuJoCo itself is not available)"}
 
 
-def flop_count(env, terrain: str, n_envs: int = 16, n_steps: int = 100) -> dict:
+def flop_count(env, terrain: str, n_envs: int = 16, n_steps: int = 400, burn_in: int = 400,
+               n_fields: int = 4) -> dict:
     """Algorithmic FLOPs per env-step of the restated reference algorithm on this
     workload's terrain (oracle/flopcount.cpp: the oracle compiled over a counting
-    double, MuJoCo's solver settings; the checker's build, in the CPU leg)."""
+    double, MuJoCo's solver settings; the checker's build, in the CPU leg).
+    Counted after an uncounted burn-in, as the bench times the steady-state mix
+    of episode ages; on a terrain bank, averaged over the first-drawn terrains of
+    the first n_fields streams (the cost per step varies with the terrain: on
+    rough perlin most of an episode is the fall from the reset height)."""
+    import numpy as np
+
     sys.path.insert(0, str(ROOT / "tools"))
     import flops as F
 
     plan = env.terrain_plan
-    slot = int(plan.streams[0][0]) if plan.streams is not None else 0  # the first reset's terrain
-    r = F.count(F.lib(), env.hfield(slot), float(plan.size_z), n_envs, n_steps)
-    return {"flops_per_env_step": r["flops_per_env_step"], "by_phase": r["flops_by_phase"],
-            "sample": f"{r['env_steps']} env-steps ({n_envs} envs x {n_steps}) on the first-drawn terrain of the "
-                      f"'{terrain}' bank (seed {plan.seeds[slot]}), uniform random actions, auto-reset; MuJoCo "
-                      "solver settings (tolerance 1e-8, line search 0.01 / 50 evaluations)"}
+    if plan.streams is None:
+        slots = [0]
+    else:
+        slots = list(dict.fromkeys(int(plan.streams[s][0]) for s in range(min(n_fields, len(plan.streams)))))
+    rs = [F.count(F.lib(), env.hfield(s), float(plan.size_z), n_envs, n_steps, burn_in=burn_in) for s in slots]
+    fl = float(np.mean([r["flops_per_env_step"] for r in rs]))
+    by = {k: float(np.mean([r["flops_by_phase"][k] for r in rs])) for k in rs[0]["flops_by_phase"]}
+    return {"flops_per_env_step": fl, "by_phase": by,
+            "sample": (f"{len(slots)} terrain(s) of the '{terrain}' bank (seeds {[int(plan.seeds[s]) for s in slots]})"
+                       if plan.streams is not None else f"the '{terrain}' terrain") +
+                      f" x {n_envs} envs x {n_steps} counted steps after {burn_in} uncounted, uniform random actions, "
+                      "auto-reset; MuJoCo solver settings (tolerance 1e-8, line search 0.01 / 50 evaluations)"}
 
 
 def parity_probe(env, n_probe: int = 64) -> dict:

@@ -109,14 +109,14 @@ inline bool isnan(FD a) { return ::isnan(a.v); }
 
 extern "C" {
 
-// Run n_steps env-steps of n_envs envs (auto-reset on termination, as the
-// product) from the reset state with actions uniform in [-scale, scale] (a fixed
+// Run n_burn uncounted then n_steps counted env-steps of n_envs envs (auto-reset
+// on termination, as the product) from the reset state with actions uniform in [-scale, scale] (a fixed
 // LCG, seed), on one heightfield, with MuJoCo's solver settings (tolerance 1e-8,
 // line search to 0.01 within 50 evaluations; the oracle's parity runs solve to
 // 1e-10 with a roundoff-exact line search).  out[30] = per env-step means of {add/sub,
 // mul, div, sqrt, transcendental, comparisons} for each of the 5 phases
 // (BBO_PHASE order); returns env-steps run.
-long long bbo_count_flops(int n_envs, int n_steps, const float* hfield, double size_z, double offset,
+long long bbo_count_flops(int n_envs, int n_burn, int n_steps, const float* hfield, double size_z, double offset,
                           double action_scale, unsigned seed, double* out) {
   compile_model();
   const int maxiter0 = g_maxiter, lsmax0 = g_lsmax;
@@ -141,12 +141,16 @@ long long bbo_count_flops(int n_envs, int n_steps, const float* hfield, double s
   int* sc = (int*)calloc((size_t)n_envs, sizeof(int));
   for (int e = 0; e < n_envs; e++) bbo_reset_state(FD(offset), q + e * NQ, v + e * NV, w + e * NV);
   uint64_t st = seed * 6364136223846793005ull + 1442695040888963407ull;
-  fc::g = fc::Counts{};
-  for (auto& c : fc::ph) c = fc::Counts{};
-  fc::cur = 4;
   long long steps = 0;
-  for (int t = 0; t < n_steps; t++)
+  for (int t = 0; t < n_burn + n_steps; t++)
     for (int e = 0; e < n_envs; e++) {
+      if (t == n_burn && e == 0) {  // the steady-state mix of episode ages starts here
+        fc::phase(4);
+        fc::g = fc::Counts{};
+        for (auto& c : fc::ph) c = fc::Counts{};
+        fc::cur = 4;
+        steps = 0;
+      }
       float a[3], obs[15], r, p2[2];
       for (int k = 0; k < 3; k++) {
         st = st * 6364136223846793005ull + 1442695040888963407ull;

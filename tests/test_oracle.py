@@ -385,3 +385,31 @@ def test_nan_action_zeroes_ctrl(oracle):
     np.testing.assert_array_equal(qg, qe)
     np.testing.assert_array_equal(vg, ve)
     assert np.isnan(obs[0]) and np.isnan(r) and not fl & 4
+
+
+def test_flop_counter_counts_the_oracle_step():
+    """oracle/flopcount.cpp (the roofline's algorithmic FLOPs): counted steps
+    exclude the burn-in, counts are deterministic, the Newton solve dominates a
+    flat step, and an env in free fall (no contacts) costs far less."""
+    import sys
+    from pathlib import Path
+
+    sys.path.insert(0, str(Path(__file__).resolve().parents[1] / "tools"))
+    import flops as F
+
+    L = F.lib()
+    flat = np.zeros(293 * 293, np.float32)
+    a = F.count(L, flat, 2.0, 4, 6, burn_in=100)  # landed (the reset height is 4 cm)
+    b = F.count(L, flat, 2.0, 4, 6, burn_in=100)
+    assert a["env_steps"] == 24
+    assert a["flops_per_env_step"] == b["flops_per_env_step"]
+    ph = a["flops_by_phase"]
+    assert max(ph, key=ph.get) == "newton_solver"
+    assert 2e5 < a["flops_per_env_step"] < 3e6
+    assert ph["kinematics_mass_bias"] > 4e4  # per RK4 stage: tree kinematics, CRB mass matrix, RNE bias
+    # a field 1.5 m lower than the reset height computed for it: free fall, no ground contacts
+    high = np.zeros(293 * 293, np.float32)
+    high[140 * 293 + 140] = 0.75  # one tall cell in the footprint window, 0.29 m off: reset height 1.51 m
+    c = F.count(L, high, 2.0, 4, 6, burn_in=100)
+    assert c["flops_by_phase"]["constraint_assembly"] < ph["constraint_assembly"]
+    assert c["flops_per_env_step"] < 0.8 * a["flops_per_env_step"]

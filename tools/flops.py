@@ -4,8 +4,9 @@ op-counting build of the oracle (oracle/flopcount.cpp -> oracle/_build/libbb_flo
 python tools/flops.py [--envs 64] [--steps 200] [--out profiles/r03_flops.json]
 
 Counts the restated reference algorithm (MuJoCo's mj_step for this model +
-env glue) at MuJoCo's solver tolerance, from the reset state under uniform
-random actions with auto-reset, per terrain config: flat (configs[1]),
+env glue) at MuJoCo's solver tolerance, under uniform random actions with
+auto-reset, after an uncounted burn-in from the reset state (the same
+steady-state mix of episode ages bench.py times), per terrain config: flat (configs[1]),
 hills and perlin (configs[2]).  FLOP = add/sub + mul + div + sqrt +
 transcendental, one each; per-phase breakdown included.
 """
@@ -32,19 +33,19 @@ LIB = ROOT / "oracle" / "_build" / "libbb_flops.so"
 def lib():
     subprocess.run(["make", "-s", "-C", str(ROOT / "oracle")], check=True)
     L = C.CDLL(str(LIB))
-    L.bbo_count_flops.argtypes = [C.c_int, C.c_int, C.POINTER(C.c_float), C.c_double, C.c_double, C.c_double,
+    L.bbo_count_flops.argtypes = [C.c_int, C.c_int, C.c_int, C.POINTER(C.c_float), C.c_double, C.c_double, C.c_double,
                                   C.c_uint, C.POINTER(C.c_double)]
     L.bbo_count_flops.restype = C.c_longlong
     return L
 
 
-def count(L, hf: np.ndarray, size_z: float, n_envs: int, n_steps: int, seed: int = 1) -> dict:
+def count(L, hf: np.ndarray, size_z: float, n_envs: int, n_steps: int, seed: int = 1, burn_in: int = 0) -> dict:
     from ballbot_gym.envs.config import init_offset
 
     hf = np.ascontiguousarray(hf, np.float32).ravel()
     out = (C.c_double * 30)()
     t0 = time.perf_counter()
-    steps = L.bbo_count_flops(n_envs, n_steps, hf.ctypes.data_as(C.POINTER(C.c_float)), size_z,
+    steps = L.bbo_count_flops(n_envs, burn_in, n_steps, hf.ctypes.data_as(C.POINTER(C.c_float)), size_z,
                               init_offset(hf, size_z), 1.0, seed, out)
     dt = time.perf_counter() - t0
     a = np.array(out[:]).reshape(5, 6)
@@ -66,15 +67,17 @@ def configs():
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--envs", type=int, default=64)
-    ap.add_argument("--steps", type=int, default=200)
+    ap.add_argument("--burn-in", type=int, default=400, help="uncounted steps first (steady-state episode mix)")
+    ap.add_argument("--steps", type=int, default=400)
     ap.add_argument("--out", default=str(ROOT / "profiles" / "r03_flops.json"))
     a = ap.parse_args()
     L = lib()
     res = {"what": "algorithmic FLOPs per env-step of the restated reference algorithm (oracle op-counter, "
-                   "MuJoCo tolerance 1e-8, uniform random actions, auto-reset)",
-           "envs": a.envs, "steps": a.steps, "configs": {}}
+                   "MuJoCo tolerance 1e-8, uniform random actions, auto-reset, "
+                   "counted after an uncounted burn-in from the reset state)",
+           "envs": a.envs, "burn_in": a.burn_in, "steps": a.steps, "configs": {}}
     for name, (hf, sz) in configs().items():
-        res["configs"][name] = count(L, hf, sz, a.envs, a.steps)
+        res["configs"][name] = count(L, hf, sz, a.envs, a.steps, burn_in=a.burn_in)
         print(name, json.dumps({k: v for k, v in res["configs"][name].items() if k != "ops_by_phase"}), flush=True)
     Path(a.out).write_text(json.dumps(res, indent=1) + "\n")
 
