@@ -149,6 +149,9 @@ def main() -> None:
                     help="perlin: all envs on one terrain seed stream (train.py's convention) instead of one per env")
     ap.add_argument("--graph", action="store_true",
                     help="replay the step as one HIP graph (kernel_ms is then timed on eager steps after the run)")
+    ap.add_argument("--multi-step", type=int, default=0,
+                    help="step M steps per launch (bb_step_multi: the random actions are known in advance, each env "
+                         "runs its M steps back to back); 0: one bb_step launch per step")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
     ap.add_argument("--traffic-json", default=str(ROOT / "profiles" / "traffic.json"))
@@ -203,8 +206,22 @@ def main() -> None:
             env._render(force=False)
     g = torch.Generator(device=dev).manual_seed(1234 + rank)
     pool = torch.rand(64, n, 3, generator=g, device=dev) * 2 - 1  # random actions resident in HBM
-    for i in range(args.burn_in + args.warmup):
-        step(pool[i % 64])
+    M = args.multi_step
+    if M:
+        if args.cameras or args.graph or 64 % M or args.steps % M:
+            raise SystemExit("--multi-step M: M must divide 64 and --steps, without --cameras/--graph")
+        mo = torch.empty(M, n, 15, device=dev)
+        mr = torch.empty(M, n, device=dev)
+        md = torch.empty(M, n, dtype=torch.uint8, device=dev)
+
+    def run(count):  # `count` steps from pool slot 0 on
+        if M:
+            for j in range(0, count, M):
+                env.step_multi_raw(pool[j % 64:j % 64 + M], mo, mr, md)
+        else:
+            for i in range(count):
+                step(pool[i % 64])
+    run(-(-(args.burn_in + args.warmup) // max(M, 1)) * max(M, 1))
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
@@ -214,8 +231,7 @@ def main() -> None:
     st0 = env.stats()
     t0 = time.perf_counter()
     ev0.record()
-    for i in range(args.steps):
-        step(pool[i % 64])
+    run(args.steps)
     ev1.record()
     torch.cuda.synchronize()
     if world > 1:
@@ -245,6 +261,8 @@ def main() -> None:
         dom = "fast" if ktimes["fast"] >= ktimes["predicted_full"] else "predicted_full"
         kern_ms = ktimes[dom]
         envs_dom = (n - full_per_step) if dom == "fast" else full_per_step
+        if M:  # one launch = M steps of every env (hand-overs included, inline)
+            envs_dom = n * M
         abytes = algorithmic_bytes(args.precision) * envs_dom
         achieved = abytes / (kern_ms * 1e-3) / 1e9
         traffic = issue_frac = None
@@ -276,6 +294,7 @@ def main() -> None:
                        "n_terrains": env.n_terrains, "depth_cameras": bool(args.cameras),
                        "terrain_streams": "per env (seed 1000 + env id)" if per_env else "shared (seed 1000)",
                        "hip_graph": graph is not None, "burn_in_steps": args.burn_in,
+                       "steps_per_launch": M or 1,
                        "envs_per_gpu": n, "total_envs": n * world, "precision": args.precision,
                        "parallelism": f"env-sharded x{world} (no collective on the step path)",
                        "launch": launch},
@@ -283,7 +302,8 @@ def main() -> None:
                          "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
                          "note": "latency/VALU-bound per-lane physics; HBM bytes = algorithmic state I/O "
                                  f"({algorithmic_bytes(args.precision)} B/env-step) x the envs the kernel stepped",
-                         "kernel": ("step_kernel<T,false> (fast path)" if dom == "fast"
+                         "kernel": (f"multi_step_kernel<T> ({M} steps per launch)" if M else
+                                    "step_kernel<T,false> (fast path)" if dom == "fast"
                                     else "step_kernel<T,true> (predicted full kernel, side stream)"),
                          "kernel_ms": kern_ms, "envs_per_launch": envs_dom, "kernel_ms_all": ktimes,
                          "full_kernel_envs_per_step": full_per_step,

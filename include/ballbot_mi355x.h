@@ -53,7 +53,7 @@
 extern "C" {
 #endif
 
-#define BB_ABI_VERSION 12
+#define BB_ABI_VERSION 13
 #define BB_NQ 17
 #define BB_NV 15
 #define BB_OBS 15
@@ -291,6 +291,18 @@ int bb_reset(bb_handle* h, const uint8_t* mask_dev, float* obs_dev, void* stream
  * the same launch and obs holds the reset observation (SB3 VecEnv). */
 int bb_step(bb_handle* h, const float* actions_dev, float* obs_dev, float* reward_dev, uint8_t* done_dev,
             float* terminal_obs_dev, float* pos2d_dev, int auto_reset, void* stream);
+/* k_steps consecutive env.steps of all envs in ONE launch, for action
+ * sequences known in advance (open-loop: random-action benchmarks, replayed
+ * actions): the same results as k_steps bb_step calls with actions_dev[k]
+ * (bit-identical outputs, states, counters, auto-resets and terrain draws),
+ * but each env runs its steps back to back instead of waiting at every step
+ * for the slowest env on the GPU.  actions_dev float[k][n][3]; obs_dev
+ * float[k][n][15]; reward_dev float[k][n]; done_dev uint8[k][n];
+ * terminal_obs_dev float[k][n][15] and pos2d_dev float[k][n][2] may be NULL.
+ * No reference counterpart (its VecEnv steps once per call,
+ * ballbot_env.py:854); the per-step semantics are bb_step's. */
+int bb_step_multi(bb_handle* h, const float* actions_dev, int k_steps, float* obs_dev, float* reward_dev,
+                  uint8_t* done_dev, float* terminal_obs_dev, float* pos2d_dev, int auto_reset, void* stream);
 
 /* diagnostics / parity (synchronous, host arrays) */
 int bb_get_state(bb_handle* h, double* qpos, double* qvel, double* warm, int32_t* steps);

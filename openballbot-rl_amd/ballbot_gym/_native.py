@@ -90,10 +90,10 @@ EXPORTS = [
     "bb_get_offsets", "bb_get_config", "bb_time_kernel", "bb_kernel_ms", "bb_generate_perlin", "bb_get_hfield",
     "bb_gae", "bb_render_depth", "bb_ppo_loss", "bb_adamw_clip", "bb_ppo_mlp_workspace_bytes", "bb_ppo_mlp_step",
     "bb_ppo_mlp_act", "bb_rollout_track", "bb_depth_encoder_workspace_bytes", "bb_depth_encoder",
-    "bb_set_terrain_stream", "bb_get_env_terrain", "bb_kernel_times",
+    "bb_set_terrain_stream", "bb_get_env_terrain", "bb_kernel_times", "bb_step_multi",
 ]
 
-ABI_VERSION = 12  # include/ballbot_mi355x.h BB_ABI_VERSION
+ABI_VERSION = 13  # include/ballbot_mi355x.h BB_ABI_VERSION
 
 _lib = None
 
@@ -151,6 +151,7 @@ def _load(path: Path):
     L.bb_assign_terrain.argtypes = [vp, vp, vp]
     L.bb_reset.argtypes = [vp, vp, vp, vp]
     L.bb_step.argtypes = [vp, vp, vp, vp, vp, vp, vp, C.c_int, vp]
+    L.bb_step_multi.argtypes = [vp, vp, C.c_int, vp, vp, vp, vp, vp, C.c_int, vp]
     L.bb_get_state.argtypes = [vp, dp, dp, dp, C.POINTER(C.c_int32)]
     L.bb_set_state.argtypes = [vp, dp, dp, dp, C.POINTER(C.c_int32)]
     L.bb_forward.argtypes = [vp, dp, dp, C.POINTER(C.c_int32)]

@@ -212,6 +212,39 @@ class BallbotVecEnv:
         if self.cameras:
             self._render(force=False)
 
+    def step_multi(self, actions: torch.Tensor, out: Optional[dict] = None) -> dict:
+        """K env.steps of all envs in ONE launch for actions known in advance
+        (bb_step_multi; open-loop sequences such as random-action benchmarks):
+        actions [K, N, 3] -> {"obs" [K,N,15], "reward" [K,N], "done" [K,N] uint8,
+        "terminal_obs" [K,N,15], "pos2d" [K,N,2]}, identical to K step() calls
+        (auto-reset, counters and terrain draws included).  `out` (a dict
+        returned before, same K) is refilled instead of allocating.  The env's
+        obs/reward/done buffers are not updated; cameras are not rendered."""
+        if self.cameras:
+            raise RuntimeError("step_multi does not render the depth cameras; step() does")
+        if self._host_reward is not None:
+            raise RuntimeError("step_multi needs a built-in reward (a host plugin runs per step())")
+        if actions.device != self.device or actions.dtype != torch.float32 or not actions.is_contiguous() \
+                or actions.dim() != 3 or actions.shape[1:] != (self.num_envs, 3):
+            raise ValueError(f"actions must be a contiguous float32 (K, {self.num_envs}, 3) tensor on {self.device}")
+        k = int(actions.shape[0])
+        if out is None or out["reward"].shape[0] != k:
+            n = self.num_envs
+            out = {"obs": torch.empty(k, n, 15, device=self.device), "reward": torch.empty(k, n, device=self.device),
+                   "done": torch.empty(k, n, dtype=torch.uint8, device=self.device),
+                   "terminal_obs": torch.empty(k, n, 15, device=self.device),
+                   "pos2d": torch.empty(k, n, 2, device=self.device)}
+        N.check(N.lib().bb_step_multi(self._h, _ptr(actions), k, _ptr(out["obs"]), _ptr(out["reward"]),
+                                      _ptr(out["done"]), _ptr(out["terminal_obs"]), _ptr(out["pos2d"]),
+                                      int(self.auto_reset), self._stream()), "bb_step_multi")
+        return out
+
+    def step_multi_raw(self, actions: torch.Tensor, obs: torch.Tensor, reward: torch.Tensor,
+                       done: torch.Tensor) -> None:
+        """Launch-only bb_step_multi (benchmarking): caller-owned [K, N, ...] outputs, no terminal obs / pos2d."""
+        N.lib().bb_step_multi(self._h, _ptr(actions), int(actions.shape[0]), _ptr(obs), _ptr(reward), _ptr(done),
+                              None, None, int(self.auto_reset), self._stream())
+
     def step_async_raw(self, actions: torch.Tensor) -> None:
         """Launch-only step (graph capture / benchmarking): no derived tensors."""
         N.lib().bb_step(self._h, _ptr(actions), _ptr(self.obs), _ptr(self.reward), _ptr(self.done),

@@ -278,6 +278,130 @@ __global__ __launch_bounds__(64) void step_kernel(ModelT<T> mg, EnvCfg cfg, Dev 
 #endif
 }
 
+// The full env step of multi_step_kernel's hand-overs.  Inlined (BB_MULTI_MODE
+// 1): as a separate function (0) the call costs the fast path its registers
+// (512 VGPRs + 2.4 KB scratch; 6.33 M against 7.91 M env-steps/s at 4096 flat
+// fp64, 16 steps per launch).  2: full step for every env, 3: no hand-over
+// (timing variants only: 3 is wrong when a hand-over occurs).
+#ifndef BB_MULTI_MODE
+#define BB_MULTI_MODE 1
+#endif
+template <typename T>
+__device__
+#if BB_MULTI_MODE == 0
+__noinline__
+#else
+__forceinline__
+#endif
+int full_env_step(const ModelT<T>& m, const EnvCfg& cfg, T* q, T* v, T* w, int& step,
+                                          const float* a, const TerrainRef<T>& tr, EnvWork<T>& W, float* o,
+                                          float& r, float* p2, int* iters, const Team& tm) {
+  return env_step<T, true>(m, cfg, q, v, w, step, a, tr, W, o, r, p2, iters, tm);
+}
+
+// K env steps of every env in one launch (bb_step_multi): actions [K][n][3]
+// known in advance (open-loop: benchmarks, replayed action sequences).  Each
+// team steps its env K times back to back; no env waits for the slowest env of
+// the chip at every step, only for the slowest of its wave.  Per step the fast
+// path runs first; an env it hands over (F_SLOWPATH: a base-tree geom may
+// touch the terrain) is restored from the team's LDS copy of the step's start
+// state and takes the full step inline.  Per step k the outputs, counters,
+// auto-reset and terrain draws are exactly those of the k-th bb_step call.
+template <typename T>
+__global__ __launch_bounds__(64) void multi_step_kernel(ModelT<T> mg, EnvCfg cfg, Dev d, const float* __restrict__ act,
+                                                        int K, float* __restrict__ obs, float* __restrict__ rew,
+                                                        uint8_t* __restrict__ done, float* __restrict__ tobs,
+                                                        float* __restrict__ pos2d, int auto_reset, int L, int epw) {
+  extern __shared__ __align__(16) unsigned char smem[];
+  const int nwg = int(gridDim.x), b = int(blockIdx.x);
+  const int g = (nwg & 7) ? b : (b & 7) * (nwg >> 3) + (b >> 3);  // XCD-aware order, as step_kernel
+  __shared__ ModelT<T> ms;
+  if (threadIdx.x == 0) ms = mg;
+  __syncthreads();
+  const ModelT<T>& m = ms;
+  const Team tm{L, int(threadIdx.x) & (L - 1)};
+  const int team = threadIdx.x / L;
+  if (team >= epw) return;
+  const int e = g * epw + team;
+  if (unsigned(e) >= unsigned(d.n)) return;
+  const bool lead = tm.tl == 0;
+  EnvWork<T>& W = team_work<T>(smem, team);
+  // the step's start state (qn, vn, wn are contiguous: 47 values), for a hand-over
+  T* bk = reinterpret_cast<T*>(smem + size_t(epw) * work_stride<T>()) + team * (NQ + 2 * NV);
+  if (lead) W.bspill = body_spill_of<T>(d, e);
+  T* q = W.qn;
+  T* v = W.vn;
+  T* w = W.wn;
+  int step;
+  load_state(d, e, q, v, w, step);
+  int tid = d.terrain[e];
+  const size_t n = size_t(d.n);
+#pragma unroll 1
+  for (int k = 0; k < K; k++) {
+    team_sync();
+    for (int i = tm.tl; i < NQ + 2 * NV; i += L) bk[i] = q[i];
+    team_sync();
+    const float* ak = act + size_t(k) * 3 * n;
+    float a[3] = {ak[3 * e], ak[3 * e + 1], ak[3 * e + 2]};
+    const float* hf = d.bank + size_t(tid) * (HF_N * HF_N);
+    float o[15], r, p2[2];
+    int iters = 0;
+    const TerrainRef<T> tr{hf, T(d.size_z[tid]), T(d.hmax[tid]) * T(d.size_z[tid])};
+    const int step0 = step;
+#if BB_MULTI_MODE == 2
+    int fl = F_SLOWPATH;
+#else
+    int fl = env_step<T, false>(m, cfg, q, v, w, step, a, tr, W, o, r, p2, &iters, tm);
+#endif
+    const bool slow = (fl & F_SLOWPATH) != 0;  // team-uniform
+#if BB_MULTI_MODE == 3
+    if (false) {
+#else
+    if (slow) {
+#endif
+      team_sync();
+      for (int i = tm.tl; i < NQ + 2 * NV; i += L) q[i] = bk[i];
+      team_sync();
+      step = step0;
+      fl = full_env_step<T>(m, cfg, q, v, w, step, a, tr, W, o, r, p2, &iters, tm);
+    }
+    const bool reset = auto_reset && (fl & F_TERMINATED);
+    if (lead) {
+      if (slow) atomicAdd(&d.stats[3], 1ull);
+      if (tobs) {
+#pragma unroll
+        for (int i = 0; i < 15; i++) tobs[(size_t(k) * n + e) * 15 + i] = o[i];
+      }
+      if (pos2d) { pos2d[(size_t(k) * n + e) * 2] = p2[0]; pos2d[(size_t(k) * n + e) * 2 + 1] = p2[1]; }
+      if (reset) {
+        tid = next_terrain(d, e);
+        d.terrain[e] = tid;
+      }
+    }
+    if (reset) {
+      tid = __shfl(tid, int(threadIdx.x) & ~(L - 1));  // the lead's draw
+      team_sync();
+      reset_state(m, T(d.offset[tid]), q, v, w);  // every lane writes the same values
+      step = 0;
+#pragma unroll
+      for (int i = 0; i < 15; i++) o[i] = 0.f;
+    }
+    if (lead) {
+#pragma unroll
+      for (int i = 0; i < 15; i++) obs[(size_t(k) * n + e) * 15 + i] = o[i];
+      rew[size_t(k) * n + e] = r;
+      done[size_t(k) * n + e] = uint8_t(fl);
+      if (reset) atomicAdd(&d.stats[0], 1ull);
+      if (fl & F_DIVERGED) atomicAdd(&d.stats[1], 1ull);
+      if (fl & F_OVERFLOW) atomicAdd(&d.stats[2], 1ull);
+      if (fl & F_SPILL) atomicAdd(&d.stats[6], 1ull);
+      atomicAdd(&d.stats[4], (unsigned long long)iters);
+    }
+  }
+  team_sync();
+  if (lead) store_state(d, e, q, v, w, step);
+}
+
 template <typename T>
 __global__ __launch_bounds__(64) void reset_kernel(ModelT<T> m, Dev d, const uint8_t* mask, float* obs) {
   const int e = blockIdx.x * WAVE + threadIdx.x;
@@ -596,6 +720,29 @@ int launch_step(bb_handle* h, const float* a, float* o, float* r, uint8_t* dn, f
   HIPCHK(hipGetLastError());
   return 0;
 }
+// bytes of dynamic LDS of multi_step_kernel: the teams' EnvWork + their step-start copies
+template <typename T>
+size_t multi_lds_bytes(int epw) { return lds_bytes<T>(epw) + size_t(epw) * (NQ + 2 * NV) * sizeof(T); }
+
+template <typename T>
+int launch_multi(bb_handle* h, const float* a, int K, float* o, float* r, uint8_t* dn, float* t, float* p2, int ar,
+                 hipStream_t s) {
+  const int epw = h->epw;
+  const int blocks = (h->n + epw - 1) / epw;
+  const bool timed = h->tn < h->tcap;
+  hipEvent_t* ev = timed ? &h->tev[6 * h->tn] : nullptr;
+  if (timed) HIPCHK(hipEventRecord(ev[0], s));
+  hipLaunchKernelGGL(multi_step_kernel<T>, dim3(blocks), dim3(WAVE), multi_lds_bytes<T>(epw), s, model_of<T>(h),
+                     h->cfg, h->d, a, K, o, r, dn, t, p2, ar, h->team, epw);
+  if (timed) {
+    HIPCHK(hipEventRecord(ev[1], s));
+    HIPCHK(hipEventRecord(ev[5], s));
+    h->tpred[h->tn] = 0;
+    h->tn++;
+  }
+  HIPCHK(hipGetLastError());
+  return 0;
+}
 }  // namespace
 
 extern "C" {
@@ -740,6 +887,9 @@ int bb_create(int n_envs, int device, const bb_params* p, bb_handle** out) {
     const void* fk = h->fp64 ? (const void*)forward_kernel<double> : (const void*)forward_kernel<float>;
     HIPCHK(hipFuncSetAttribute(sk, hipFuncAttributeMaxDynamicSharedMemorySize, lb));
     HIPCHK(hipFuncSetAttribute(fk, hipFuncAttributeMaxDynamicSharedMemorySize, lb));
+    const void* mk = h->fp64 ? (const void*)multi_step_kernel<double> : (const void*)multi_step_kernel<float>;
+    const int mlb = (int)(h->fp64 ? multi_lds_bytes<double>(h->epw) : multi_lds_bytes<float>(h->epw));
+    HIPCHK(hipFuncSetAttribute(mk, hipFuncAttributeMaxDynamicSharedMemorySize, mlb));
   }
   *out = h;
   int rc = bb_reset(h, nullptr, nullptr, nullptr);
@@ -1030,6 +1180,15 @@ int bb_step(bb_handle* h, const float* a, float* o, float* r, uint8_t* dn, float
   if (!a || !o || !r || !dn) return fail("bb_step: actions/obs/reward/done must be non-NULL");
   return h->fp64 ? launch_step<double>(h, a, o, r, dn, t, p2, ar, (hipStream_t)s)
                  : launch_step<float>(h, a, o, r, dn, t, p2, ar, (hipStream_t)s);
+}
+
+int bb_step_multi(bb_handle* h, const float* a, int k, float* o, float* r, uint8_t* dn, float* t, float* p2, int ar,
+                  void* s) {
+  if (!h) return fail("bb_step_multi: NULL handle");
+  if (!a || !o || !r || !dn) return fail("bb_step_multi: actions/obs/reward/done must be non-NULL");
+  if (k < 1) return fail("bb_step_multi: k_steps must be >= 1 (got %d)", k);
+  return h->fp64 ? launch_multi<double>(h, a, k, o, r, dn, t, p2, ar, (hipStream_t)s)
+                 : launch_multi<float>(h, a, k, o, r, dn, t, p2, ar, (hipStream_t)s);
 }
 
 int bb_get_state(bb_handle* h, double* qpos, double* qvel, double* warm, int32_t* steps) {

@@ -104,7 +104,8 @@ def test_argument_errors_without_gpu(native):
                       (lambda: L.bb_ppo_mlp_act(16, (C.c_int32 * 21)(*([0] * 20 + [40000])), 40000, 16, 15, None, 4,
                                                 None, 16, None, 16, 16, None), "inside the 40000-float buffer"),
                       (lambda: L.bb_set_terrain_stream(None, None, 1, 4, None), "NULL handle"),
-                      (lambda: L.bb_get_env_terrain(None, None, None), "NULL handle")):
+                      (lambda: L.bb_get_env_terrain(None, None, None), "NULL handle"),
+                      (lambda: L.bb_step_multi(None, None, 4, None, None, None, None, None, 1, None), "NULL handle")):
         assert call() < 0
         assert msg in _err(native), (msg, _err(native))
 

@@ -1,0 +1,86 @@
+"""bb_step_multi: K env.steps in one launch == K bb_step calls, bit for bit.
+
+Outputs of every step (obs, reward, done flags, terminal obs, pos2d), the
+final states, the counters (resets, Newton iterations, full-path env-steps)
+and the terrain draws of the auto-resets must be identical: the multi-step
+kernel runs the same fast/full step code per env, only without a grid-wide
+barrier between steps.  Flat terrain with short episodes and large actions
+(many auto-resets, toppling robots), and perlin with per-env terrain streams
+(base-tree contacts: the fast path hands envs over to the inline full step).
+"""
+import numpy as np
+import pytest
+
+torch = pytest.importorskip("torch")
+pytestmark = pytest.mark.gpu
+
+
+def _pair(n, terrain, **kw):
+    from ballbot_gym.envs import BallbotVecEnv
+
+    def mk():
+        return BallbotVecEnv(n, device="cuda:0", seed=3, terrain_config={"type": terrain, "config": {}}, **kw)
+    return mk(), mk()
+
+
+def _compare_runs(a, b, actions, k):
+    """a: per-step bb_step; b: bb_step_multi in chunks of k."""
+    T = actions.shape[0]
+    outs = {"obs": [], "reward": [], "done": [], "terminal_obs": [], "pos2d": []}
+    for t in range(T):
+        obs, rew, _, _, info = a.step(actions[t])
+        outs["obs"].append(obs.clone())
+        outs["reward"].append(rew.clone())
+        outs["done"].append(info["done_flags"].clone())
+        outs["terminal_obs"].append(info["terminal_observation"].clone())
+        outs["pos2d"].append(info["pos2d"].clone())
+    ref = {key: torch.stack(v) for key, v in outs.items()}
+    got = {key: [] for key in outs}
+    for t0 in range(0, T, k):
+        o = b.step_multi(actions[t0:t0 + k].contiguous())
+        for key in got:
+            got[key].append(o[key].clone())
+    got = {key: torch.cat(v) for key, v in got.items()}
+    for key in ref:
+        bad = (ref[key] != got[key]).reshape(T, a.num_envs, -1).any(-1).nonzero()
+        assert len(bad) == 0, f"{key}: first (step, env) mismatches {bad[:6].tolist()}"
+    for x, y in zip(a.get_state(), b.get_state()):
+        np.testing.assert_array_equal(x, y)
+    for x, y in zip(a.env_terrain(), b.env_terrain()):
+        np.testing.assert_array_equal(x, y)
+    sa, sb = a.stats(), b.stats()
+    assert sa == sb, (sa, sb)
+    return sa
+
+
+@pytest.mark.parametrize("k", [1, 7, 16])
+def test_multi_step_flat_matches_single_steps(k):
+    n = 1024
+    a, b = _pair(n, "flat", max_ep_steps=25)
+    g = torch.Generator(device="cuda:0").manual_seed(1)
+    actions = torch.rand(48, n, 3, generator=g, device="cuda:0") * 4 - 2  # clipped to [-1, 1]*10 inside: topples
+    st = _compare_runs(a, b, actions, k)
+    assert st["resets"] >= n  # every env's episode ended (step limit or tilt) and auto-reset at least once
+    a.close(), b.close()
+
+
+def test_multi_step_perlin_hand_overs_match():
+    n = 512
+    a, b = _pair(n, "perlin", n_terrains=None, stream_seeds=[50 + i for i in range(n)], max_ep_steps=120)
+    g = torch.Generator(device="cuda:0").manual_seed(2)
+    actions = torch.rand(192, n, 3, generator=g, device="cuda:0") * 2 - 1
+    st = _compare_runs(a, b, actions, 32)
+    assert st["slow_path"] > 0  # base-tree contacts: the inline full step ran
+    assert st["resets"] > 0
+    a.close(), b.close()
+
+
+def test_multi_step_rejects_bad_shapes():
+    from ballbot_gym.envs import BallbotVecEnv
+
+    env = BallbotVecEnv(64, device="cuda:0")
+    with pytest.raises(ValueError):
+        env.step_multi(torch.zeros(4, 32, 3, device="cuda:0"))
+    with pytest.raises(ValueError):
+        env.step_multi(torch.zeros(64, 3, device="cuda:0"))
+    env.close()

@@ -29,7 +29,7 @@ def build(name, flags):
     return out
 
 
-def run_one(lib, precision, terrain, steps, warmup):
+def run_one(lib, precision, terrain, steps, warmup, multi=0):
     import torch
     from ballbot_gym import _native
     from ballbot_gym.envs import BallbotVecEnv
@@ -38,6 +38,20 @@ def run_one(lib, precision, terrain, steps, warmup):
     env = BallbotVecEnv(4096, device="cuda:0", precision=precision, terrain_config={"type": terrain, "config": {}},
                         n_terrains=None if terrain == "perlin" else 16)
     pool = torch.rand(64, 4096, 3, device="cuda:0") * 2 - 1
+    if multi:  # bb_step_multi: `multi` steps per launch
+        assert 64 % multi == 0
+        o = torch.empty(multi, 4096, 15, device="cuda:0")
+        r = torch.empty(multi, 4096, device="cuda:0")
+        dn = torch.empty(multi, 4096, dtype=torch.uint8, device="cuda:0")
+        for i in range(0, warmup, multi):
+            env.step_multi_raw(pool[i % 64:i % 64 + multi], o, r, dn)
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for i in range(0, steps, multi):
+            env.step_multi_raw(pool[i % 64:i % 64 + multi], o, r, dn)
+        torch.cuda.synchronize()
+        dt = (time.perf_counter() - t0) / (steps // multi * multi)
+        return {"ms": dt * 1e3, "env_steps_per_s": 4096 / dt, "multi": multi, "stats": env.stats()}
     for i in range(warmup):
         env.step_async_raw(pool[i % 64])
     torch.cuda.synchronize()
@@ -57,6 +71,7 @@ def main():
     ap.add_argument("--steps", type=int, default=300)
     ap.add_argument("--warmup", type=int, default=300)
     ap.add_argument("--child", default=None)
+    ap.add_argument("--multi", type=int, default=0, help="steps per bb_step_multi launch (0: bb_step per step)")
     ap.add_argument("--no-build", action="store_true", help="use the prebuilt tools/_build/libbb_<NAME>.so")
     ap.add_argument("--build-only", action="store_true", help="compile the variants (here, on the CPU) and exit")
     a = ap.parse_args()
@@ -66,16 +81,17 @@ def main():
             list(ex.map(lambda v: build(v.partition(":")[0], [f for f in v.partition(":")[2].split(",") if f]), a.variant))
         return
     if a.child:
-        print(json.dumps(run_one(a.child, a.precision, a.terrain, a.steps, a.warmup)))
+        print(json.dumps(run_one(a.child, a.precision, a.terrain, a.steps, a.warmup, a.multi)))
         return
     for v in a.variant:
         name, _, fl = v.partition(":")
         lib = (ROOT / "tools" / "_build" / f"libbb_{name}.so") if a.no_build else build(name, [f for f in fl.split(",") if f])
         r = subprocess.run([sys.executable, __file__, "--child", str(lib), "--precision", a.precision,
-                            "--terrain", a.terrain, "--steps", str(a.steps), "--warmup", str(a.warmup)],
+                            "--terrain", a.terrain, "--steps", str(a.steps), "--warmup", str(a.warmup),
+                            "--multi", str(a.multi)],
                            capture_output=True, text=True, timeout=600)
         line = r.stdout.strip().splitlines()[-1] if r.returncode == 0 else r.stderr[-2000:]
-        print(json.dumps({"variant": name, "flags": fl, "precision": a.precision, "terrain": a.terrain,
+        print(json.dumps({"variant": name, "flags": fl, "precision": a.precision, "terrain": a.terrain, "multi": a.multi,
                           "result": json.loads(line) if r.returncode == 0 else line}), flush=True)
 
 
