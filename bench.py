@@ -149,9 +149,10 @@ def main() -> None:
                     help="perlin: all envs on one terrain seed stream (train.py's convention) instead of one per env")
     ap.add_argument("--graph", action="store_true",
                     help="replay the step as one HIP graph (kernel_ms is then timed on eager steps after the run)")
-    ap.add_argument("--multi-step", type=int, default=0,
-                    help="step M steps per launch (bb_step_multi: the random actions are known in advance, each env "
-                         "runs its M steps back to back); 0: one bb_step launch per step")
+    ap.add_argument("--multi-step", type=int, default=64,
+                    help="M steps per launch (bb_step_multi: the benchmark's random actions are known in advance, so "
+                         "each env runs its M steps back to back, bit-identical to M bb_step calls); 0: one bb_step "
+                         "launch per step.  With M > 0 the line also reports the per-launch form under 'per_step'")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
     ap.add_argument("--traffic-json", default=str(ROOT / "profiles" / "traffic.json"))
@@ -207,46 +208,56 @@ def main() -> None:
     g = torch.Generator(device=dev).manual_seed(1234 + rank)
     pool = torch.rand(64, n, 3, generator=g, device=dev) * 2 - 1  # random actions resident in HBM
     M = args.multi_step
+    if M and (args.cameras or args.graph or not 1 <= M <= 64):
+        M = 0  # the cameras render between steps; a captured graph holds one bb_step
     if M:
-        if args.cameras or args.graph or 64 % M or args.steps % M:
-            raise SystemExit("--multi-step M: M must divide 64 and --steps, without --cameras/--graph")
         mo = torch.empty(M, n, 15, device=dev)
         mr = torch.empty(M, n, device=dev)
         md = torch.empty(M, n, dtype=torch.uint8, device=dev)
 
-    def run(count):  # `count` steps from pool slot 0 on
-        if M:
-            for j in range(0, count, M):
-                env.step_multi_raw(pool[j % 64:j % 64 + M], mo, mr, md)
+    def run(count, m):  # `count` steps from pool slot 0 on, m per launch (0: one bb_step per step)
+        if m:
+            for j in range(0, count, m):
+                k = min(m, count - j)
+                env.step_multi_raw(pool[j % 64:j % 64 + k], mo[:k], mr[:k], md[:k])
         else:
             for i in range(count):
                 step(pool[i % 64])
-    run(-(-(args.burn_in + args.warmup) // max(M, 1)) * max(M, 1))
-    torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
-    torch.cuda.synchronize()
-    ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-    env.time_kernel(args.steps)  # HIP events around each step kernel, on the stream it is launched on
-    st0 = env.stats()
-    t0 = time.perf_counter()
-    ev0.record()
-    run(args.steps)
-    ev1.record()
-    torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
-    torch.cuda.synchronize()
-    elapsed = time.perf_counter() - t0
-    step_ms = ev0.elapsed_time(ev1) / args.steps  # whole bb_step sequence per step, torch's stream
-    st1 = env.stats()
-    if graph is not None:  # graph replays carry no per-kernel events: time eager steps of the same kernels
-        env.time_kernel(min(args.steps, 100))
-        for i in range(min(args.steps, 100)):
-            env.step_async_raw(pool[i % 64])
+
+    def timed(m):
+        """args.steps steps, m per launch, bracketed by barrier + synchronize; the MAX over ranks."""
         torch.cuda.synchronize()
-    ktimes, kern_n = env.kernel_times()  # fast, predicted-full (side stream), hand-over full
-    elapsed = max_over_ranks(elapsed, device=dev)
+        if world > 1:
+            dist.barrier()
+        torch.cuda.synchronize()
+        ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        env.time_kernel(-(-args.steps // max(m, 1)))  # HIP events around each step-kernel launch, on its stream
+        st0 = env.stats()
+        t0 = time.perf_counter()
+        ev0.record()
+        run(args.steps, m)
+        ev1.record()
+        torch.cuda.synchronize()
+        if world > 1:
+            dist.barrier()
+        torch.cuda.synchronize()
+        elapsed = time.perf_counter() - t0
+        step_ms = ev0.elapsed_time(ev1) / args.steps  # whole step sequence per step, torch's stream
+        st1 = env.stats()
+        if graph is not None:  # graph replays carry no per-kernel events: time eager steps of the same kernels
+            env.time_kernel(min(args.steps, 100))
+            for i in range(min(args.steps, 100)):
+                env.step_async_raw(pool[i % 64])
+            torch.cuda.synchronize()
+        ktimes, kern_n = env.kernel_times()  # fast (or multi-step), predicted-full (side stream), hand-over full
+        return max_over_ranks(elapsed, device=dev), step_ms, ktimes, kern_n, st0, st1
+
+    run(args.burn_in + args.warmup, M)
+    elapsed, step_ms, ktimes, kern_n, st0, st1 = timed(M)
+    per_step = None
+    if M:  # the same steps with one bb_step launch per step (what a closed-loop rollout uses)
+        run(args.warmup, 0)
+        per_step = timed(0)
     stats = env.stats()
     # envs per launch of each kernel over the timed steps: the full kernel stepped
     # slow_path env-steps (predicted + handed over), the fast kernel the rest
@@ -261,15 +272,16 @@ def main() -> None:
         dom = "fast" if ktimes["fast"] >= ktimes["predicted_full"] else "predicted_full"
         kern_ms = ktimes[dom]
         envs_dom = (n - full_per_step) if dom == "fast" else full_per_step
-        if M:  # one launch = M steps of every env (hand-overs included, inline)
-            envs_dom = n * M
+        if M:  # one launch = up to M steps of every env (hand-overs included, inline)
+            envs_dom = n * args.steps / kern_n
         abytes = algorithmic_bytes(args.precision) * envs_dom
         achieved = abytes / (kern_ms * 1e-3) / 1e9
         traffic = issue_frac = None
         tj = Path(args.traffic_json)
         if tj.exists():
             try:
-                tr = json.loads(tj.read_text()).get(args.precision) or {}
+                key = args.precision if not M else f"{args.precision}_multi{M}"
+                tr = json.loads(tj.read_text()).get(key) or {}
                 if tr.get("envs") == n and tr.get("terrain", "flat") == args.terrain:
                     traffic = tr.get("bytes_per_launch")
                     issue_frac = tr.get("issue_frac")
@@ -288,7 +300,9 @@ def main() -> None:
             "vs_baseline": None,
             "dtype": "f64" if args.precision == "fp64" else "f32",
             "data": "synthetic (uniform random actions in [-1,1], resident in HBM; "
-                    f"{args.burn_in} untimed burn-in steps into the steady-state episode mix before the warmup)",
+                    f"{args.burn_in} untimed burn-in steps into the steady-state episode mix before the warmup"
+                    + (f"; stepped {M} per launch with bb_step_multi, bit-identical to one bb_step per step)" if M
+                       else ")"),
             "config": {"workload": f"{n} envs/GPU, {args.terrain} terrain, random actions "
                                    f"(BASELINE configs[{1 if args.terrain == 'flat' else 2}])",
                        "n_terrains": env.n_terrains, "depth_cameras": bool(args.cameras),
@@ -313,6 +327,13 @@ def main() -> None:
                          "issue_frac": issue_frac},
             "stats": stats,
         }
+        if per_step is not None:
+            pe, pms, pk, pn, _, _ = per_step
+            line["per_step"] = {
+                "value": n * world * args.steps / pe, "ms_per_step": pe / args.steps * 1e3,
+                "step_ms_hip_events": pms, "kernel_ms_all": pk, "kernel_launches_timed": pn,
+                "note": "the same steps with one bb_step launch per step, the form a closed-loop (policy) rollout "
+                        "uses: every step waits for the slowest env of the GPU"}
         if world == 1 and not args.no_cpu_baseline:
             if args.terrain == "flat":
                 line["parity"] = parity_probe(env)

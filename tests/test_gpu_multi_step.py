@@ -82,9 +82,11 @@ def test_multi_step_flat_matches_single_steps(k, monkeypatch):
 def test_multi_step_perlin_hand_overs_match(route, monkeypatch):
     n = 512
     a, b = _pair(n, "perlin", monkeypatch, route=route, n_terrains=None, stream_seeds=[50 + i for i in range(n)],
-                 max_ep_steps=40)
+                 max_ep_steps=200)
     g = torch.Generator(device="cuda:0").manual_seed(2)
-    actions = torch.rand(96, n, 3, generator=g, device="cuda:0") * 2 - 1
+    # rough perlin: most robots fall for ~140 steps from the reset height, then land and topple
+    # (base-tree contacts); episodes end by tilt or at 200 steps
+    actions = torch.rand(256, n, 3, generator=g, device="cuda:0") * 2 - 1
     st = _compare_runs(a, b, actions, 32, exact=route == "1")
     assert st["slow_path"] > 0  # base-tree contacts: the inline full step ran
     assert st["resets"] > 0

@@ -15,7 +15,8 @@ import shutil
 from pathlib import Path
 
 KERNEL = "step_kernel"
-SEL = {"which": "fast"}  # --kernel: fast (step_kernel<T,false>) or pred (the route-0 predicted full kernel)
+SEL = {"which": "fast"}  # --kernel: fast (step_kernel<T,false>), pred (the route-0 predicted full kernel)
+#                          or multi (multi_step_kernel<T>, bb_step_multi)
 
 
 def is_fast(name):
@@ -32,6 +33,8 @@ def select_ids(recs):
     the step_kernel<T,true> dispatch launched right before each fast dispatch (the
     hand-over full kernel comes after it)."""
     recs = sorted(recs, key=lambda r: int(r["Dispatch_Id"]))
+    if SEL["which"] == "multi":
+        return [int(r["Dispatch_Id"]) for r in recs if "multi_step_kernel" in r["Kernel_Name"]]
     if SEL["which"] == "fast":
         return [int(r["Dispatch_Id"]) for r in recs if is_fast(r["Kernel_Name"])]
     out, last_full = [], None
@@ -72,7 +75,7 @@ def main():
     ap.add_argument("--timed", type=int, default=300, help="timed step_kernel dispatches at the end of the trace run")
     ap.add_argument("--pmc-last", type=int, default=20)
     ap.add_argument("--traffic", action="store_true")
-    ap.add_argument("--kernel", default="fast", choices=["fast", "pred"])
+    ap.add_argument("--kernel", default="fast", choices=["fast", "pred", "multi"])
     ap.add_argument("--f64", action="store_true", help="also summarise the FP64 VALU instruction pass (sq64)")
     a = ap.parse_args()
     SEL["which"] = a.kernel
@@ -131,9 +134,12 @@ def main():
         tj = dst.parent / "traffic.json"
         cur = json.loads(tj.read_text()) if tj.exists() else {}
         prec = bench["config"]["precision"]
-        cur[prec] = {"precision": prec, "envs": bench["config"]["envs_per_gpu"],
-                     "bytes_per_launch": fetch_b + write_b, "issue_frac": out["derived"]["issue_frac"],
-                     "source": str(dst) + "_summary.json"}
+        spl = bench["config"].get("steps_per_launch", 1) if a.kernel == "multi" else 1
+        cur[prec if spl == 1 else f"{prec}_multi{spl}"] = {
+            "precision": prec, "envs": bench["config"]["envs_per_gpu"], "steps_per_launch": spl,
+            "bytes_per_launch": fetch_b + write_b, "fetch_raw_bytes_per_launch": f["FETCH_SIZE"] * 1024,
+            "write_bytes_per_launch": write_b, "issue_frac": out["derived"]["issue_frac"],
+            "source": str(dst) + "_summary.json"}
         tj.write_text(json.dumps(cur, indent=1))
 
 
