@@ -21,6 +21,7 @@
  *                    AdamW) of the reference's proprio MLP policy, fused
  *   bb_ppo_mlp_act   SB3 collect_rollouts policy step (same policy)
  *   bb_rollout_track SB3 collect_rollouts / Monitor episode bookkeeping
+ *   bb_rollout       a whole SB3 collect_rollouts (policy + step + bookkeeping) in one launch
  *   bb_depth_encoder frozen rgbd encoder of the camera policy, fused
  *   bb_gae           SB3 RolloutBuffer.compute_returns_and_advantage (PPO)
  *   bb_forward       mujoco.mj_forward (diagnostic)             ballbot_env.py:525,620
@@ -53,7 +54,7 @@
 extern "C" {
 #endif
 
-#define BB_ABI_VERSION 13
+#define BB_ABI_VERSION 14
 #define BB_NQ 17
 #define BB_NV 15
 #define BB_OBS 15
@@ -222,6 +223,37 @@ int bb_ppo_mlp_act(const float* params_dev, const int32_t* offsets, int64_t n_pa
                    const float* noise_dev, int n,
                    float* obs_copy_dev, float* actions_dev, float* clipped_dev, float* values_dev, float* log_prob_dev,
                    void* stream);
+/* One whole PPO rollout of the proprio MLP policy in ONE launch (SB3
+ * OnPolicyAlgorithm.collect_rollouts + Monitor, model.learn at
+ * ballbot_rl/training/train.py:284): every env runs n_steps x (policy forward,
+ * Gaussian sample a = mean + noise * exp(log_std), clip to [-1, 1], env.step,
+ * bookkeeping) back to back -- the parameters are fixed during a rollout and the
+ * envs are independent, so no step waits for the slowest env of the GPU.  The
+ * policy (bb_ppo_mlp_act's, same params/offsets/n_params) runs fp32 on the env's
+ * team, in another summation order than bb_ppo_mlp_act's MFMA tiles (equal to
+ * fp32 rounding); the env step is bb_step_multi's (bit-identical to bb_step's
+ * serial route for the same clipped actions).  Built-in rewards only (not
+ * BB_REWARD_NONE).  One launch; graph-capturable. */
+typedef struct bb_rollout_args {
+  const float* params;      /* flat fp32 policy parameters */
+  int32_t offsets[21];
+  int64_t n_params;
+  const float* noise;       /* [T][n][3] standard normal draws */
+  int n_steps;              /* T */
+  float* obs;               /* [n][15] in: last observation; out: the observation after the rollout */
+  uint8_t* last_starts;     /* [n] in/out: episode_starts */
+  double* ep_ret;           /* [n] in/out: running episode return (float64, as Monitor) */
+  int64_t* ep_len;          /* [n] in/out */
+  float* buf_obs;           /* [T][n][15] */
+  float* buf_actions;       /* [T][n][3] unclipped (as SB3 stores them) */
+  float* buf_values;        /* [T][n] */
+  float* buf_log_prob;      /* [T][n] */
+  float* buf_rewards;       /* [T][n] */
+  uint8_t* buf_starts;      /* [T][n] episode_starts of each step */
+  double* ep_r_out;         /* [T][n] finished episodes' returns, NaN elsewhere */
+  int64_t* ep_l_out;        /* [T][n] their lengths, 0 elsewhere */
+} bb_rollout_args;
+int bb_rollout(bb_handle* h, const bb_rollout_args* args, void* stream);
 /* One rollout step's episode bookkeeping (SB3 collect_rollouts + Monitor,
  * model.learn at ballbot_rl/training/train.py:284): done = (flags_dev[i] &
  * done_mask) != 0; rewards_out_dev[i] = reward_dev[i]; the float64 episode

@@ -74,6 +74,19 @@ class PPOMlpArgs(C.Structure):
     ]
 
 
+class RolloutArgs(C.Structure):
+    """bb_rollout_args (include/ballbot_mi355x.h): one whole PPO rollout in one launch."""
+    _fields_ = [
+        ("params", C.c_void_p),
+        ("offsets", C.c_int32 * 21),
+        ("n_params", C.c_int64),
+        ("noise", C.c_void_p),
+        ("n_steps", C.c_int32),
+    ] + [(name, C.c_void_p) for name in ("obs", "last_starts", "ep_ret", "ep_len", "buf_obs", "buf_actions",
+                                         "buf_values", "buf_log_prob", "buf_rewards", "buf_starts", "ep_r_out",
+                                         "ep_l_out")]
+
+
 ENCODER_FIELDS = ("conv1_w", "conv1_b", "bn1_w", "bn1_b", "bn1_mean", "bn1_var", "bn1_count",
                   "conv2_w", "conv2_b", "bn2_w", "bn2_b", "bn2_mean", "bn2_var", "bn2_count",
                   "fc_w", "fc_b", "bn3_w", "bn3_b", "bn3_mean", "bn3_var", "bn3_count")
@@ -90,10 +103,10 @@ EXPORTS = [
     "bb_get_offsets", "bb_get_config", "bb_time_kernel", "bb_kernel_ms", "bb_generate_perlin", "bb_get_hfield",
     "bb_gae", "bb_render_depth", "bb_ppo_loss", "bb_adamw_clip", "bb_ppo_mlp_workspace_bytes", "bb_ppo_mlp_step",
     "bb_ppo_mlp_act", "bb_rollout_track", "bb_depth_encoder_workspace_bytes", "bb_depth_encoder",
-    "bb_set_terrain_stream", "bb_get_env_terrain", "bb_kernel_times", "bb_step_multi",
+    "bb_set_terrain_stream", "bb_get_env_terrain", "bb_kernel_times", "bb_step_multi", "bb_rollout",
 ]
 
-ABI_VERSION = 13  # include/ballbot_mi355x.h BB_ABI_VERSION
+ABI_VERSION = 14  # include/ballbot_mi355x.h BB_ABI_VERSION
 
 _lib = None
 
@@ -152,6 +165,7 @@ def _load(path: Path):
     L.bb_reset.argtypes = [vp, vp, vp, vp]
     L.bb_step.argtypes = [vp, vp, vp, vp, vp, vp, vp, C.c_int, vp]
     L.bb_step_multi.argtypes = [vp, vp, C.c_int, vp, vp, vp, vp, vp, C.c_int, vp]
+    L.bb_rollout.argtypes = [vp, C.POINTER(RolloutArgs), vp]
     L.bb_get_state.argtypes = [vp, dp, dp, dp, C.POINTER(C.c_int32)]
     L.bb_set_state.argtypes = [vp, dp, dp, dp, C.POINTER(C.c_int32)]
     L.bb_forward.argtypes = [vp, dp, dp, C.POINTER(C.c_int32)]

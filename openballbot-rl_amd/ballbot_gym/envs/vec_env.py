@@ -245,6 +245,15 @@ class BallbotVecEnv:
         N.lib().bb_step_multi(self._h, _ptr(actions), int(actions.shape[0]), _ptr(obs), _ptr(reward), _ptr(done),
                               None, None, int(self.auto_reset), self._stream())
 
+    def run_rollout(self, args) -> None:
+        """One whole PPO rollout in one launch (bb_rollout; args: _native.RolloutArgs
+        filled by the trainer).  Built-in rewards only; the cameras are not rendered."""
+        if self.cameras:
+            raise RuntimeError("bb_rollout steps the proprio policy; the camera policy rolls out per step")
+        if self._host_reward is not None:
+            raise RuntimeError("bb_rollout needs a built-in reward (a host plugin runs per step())")
+        N.check(N.lib().bb_rollout(self._h, C.byref(args), self._stream()), "bb_rollout")
+
     def step_async_raw(self, actions: torch.Tensor) -> None:
         """Launch-only step (graph capture / benchmarking): no derived tensors."""
         N.lib().bb_step(self._h, _ptr(actions), _ptr(self.obs), _ptr(self.reward), _ptr(self.done),

@@ -655,6 +655,38 @@ class BatchedPPO:
             self._last_obs = obs
         return ep_r, ep_l
 
+    def _collect_rollout_kernel(self, slots) -> tuple:
+        """The whole proprio rollout as ONE launch (bb_rollout): every env runs its
+        n_steps of (policy, sample, clip, env step, bookkeeping) back to back on
+        its team.  Same buffers and noise draws as the per-step fused rollout; the
+        policy sums in another fp32 order than bb_ppo_mlp_act's MFMA tiles
+        (tests/test_gpu_rollout.py)."""
+        from ballbot_gym import _native as N
+
+        env, b, dev = self.env, self.buf, self.device
+        T, n = self.n_steps, self.n_envs
+        if self._last_obs is None:
+            self._last_obs, _ = env.reset()
+        obs_io = env.obs
+        if self._last_obs.data_ptr() != obs_io.data_ptr():
+            obs_io.copy_(self._last_obs)
+        noise = torch.randn(T, n, 3, generator=self.gen, device=dev)
+        ep_r = torch.empty(T, n, dtype=torch.float64, device=dev)
+        ep_l = torch.empty(T, n, dtype=torch.int64, device=dev)
+        flat = self.optimizer.flat
+        a = N.RolloutArgs()
+        a.params, a.n_params, a.noise, a.n_steps = flat.data_ptr(), int(flat.numel()), noise.data_ptr(), T
+        for i, o in enumerate(slots):
+            a.offsets[i] = int(o)
+        a.obs, a.last_starts = obs_io.data_ptr(), self._last_starts.data_ptr()
+        a.ep_ret, a.ep_len = self._ep_ret.data_ptr(), self._ep_len.data_ptr()
+        a.buf_obs, a.buf_actions, a.buf_values = b.obs.data_ptr(), b.actions.data_ptr(), b.values.data_ptr()
+        a.buf_log_prob, a.buf_rewards, a.buf_starts = b.log_probs.data_ptr(), b.rewards.data_ptr(), b.starts.data_ptr()
+        a.ep_r_out, a.ep_l_out = ep_r.data_ptr(), ep_l.data_ptr()
+        env.run_rollout(a)
+        self._last_obs = obs_io
+        return ep_r, ep_l
+
     def _collect_fused_proprio(self, slots) -> tuple:
         """collect_rollouts with the policy step as bb_ppo_mlp_act and the
         episode bookkeeping as bb_rollout_track: three launches per env step
@@ -667,6 +699,9 @@ class BatchedPPO:
         T, n = self.n_steps, self.n_envs
         if self._last_obs is None:
             self._last_obs, _ = env.reset()
+        if (hasattr(env, "run_rollout") and getattr(env, "_host_reward", None) is None
+                and os.environ.get("BB_FUSED_ROLLOUT", "1") != "0"):
+            return self._collect_rollout_kernel(slots)
         if (self.use_graphs and hasattr(env, "step_flags") and getattr(env, "_host_reward", None) is None
                 and hasattr(env, "obs") and os.environ.get("BB_ROLLOUT_GRAPH", "1") != "0"):
             if self._rgraph is None or self._rgraph.key != (id(env), T, n):

@@ -299,14 +299,81 @@ int full_env_step(const ModelT<T>& m, const EnvCfg& cfg, T* q, T* v, T* w, int& 
   return env_step<T, true>(m, cfg, q, v, w, step, a, tr, W, o, r, p2, iters, tm);
 }
 
+// One env step of a team inside a multi-step launch (multi_step_kernel,
+// rollout_kernel): the fast path first; an env it hands over (F_SLOWPATH: a
+// base-tree geom may touch the terrain) is restored from the team's LDS copy
+// bk of the step's start state and takes the full step inline.  Auto-reset,
+// terrain draw and counters as step_kernel.  tobs_row / p2_row (may be NULL):
+// this step's terminal obs and pos2d.  On return o holds the obs after any
+// reset; the flags are the step's.
+template <typename T>
+__device__ __forceinline__ int team_step(const ModelT<T>& m, const EnvCfg& cfg, const Dev& d, int e, int& tid,
+                                         T* q, T* v, T* w, int& step, T* bk, const float* a, EnvWork<T>& W, float* o,
+                                         float& r, float* tobs_row, float* p2_row, int auto_reset, const Team& tm) {
+  const int L = tm.L;
+  const bool lead = tm.tl == 0;
+  team_sync();
+  for (int i = tm.tl; i < NQ + 2 * NV; i += L) bk[i] = q[i];
+  team_sync();
+  const float* hf = d.bank + size_t(tid) * (HF_N * HF_N);
+  float p2[2];
+  int iters = 0;
+  const TerrainRef<T> tr{hf, T(d.size_z[tid]), T(d.hmax[tid]) * T(d.size_z[tid])};
+  const int step0 = step;
+#if BB_MULTI_MODE == 2
+  int fl = F_SLOWPATH;
+#else
+  int fl = env_step<T, false>(m, cfg, q, v, w, step, a, tr, W, o, r, p2, &iters, tm);
+#endif
+  const bool slow = (fl & F_SLOWPATH) != 0;  // team-uniform
+#if BB_MULTI_MODE == 3
+  if (false) {
+#else
+  if (slow) {
+#endif
+    team_sync();
+    for (int i = tm.tl; i < NQ + 2 * NV; i += L) q[i] = bk[i];
+    team_sync();
+    step = step0;
+    fl = full_env_step<T>(m, cfg, q, v, w, step, a, tr, W, o, r, p2, &iters, tm);
+  }
+  const bool reset = auto_reset && (fl & F_TERMINATED);
+  if (lead) {
+    if (slow) atomicAdd(&d.stats[3], 1ull);
+    if (tobs_row) {
+#pragma unroll
+      for (int i = 0; i < 15; i++) tobs_row[i] = o[i];
+    }
+    if (p2_row) { p2_row[0] = p2[0]; p2_row[1] = p2[1]; }
+    if (reset) {
+      tid = next_terrain(d, e);
+      d.terrain[e] = tid;
+    }
+  }
+  if (reset) {
+    tid = __shfl(tid, int(threadIdx.x) & ~(L - 1));  // the lead's draw
+    team_sync();
+    reset_state(m, T(d.offset[tid]), q, v, w);  // every lane writes the same values
+    step = 0;
+#pragma unroll
+    for (int i = 0; i < 15; i++) o[i] = 0.f;
+  }
+  if (lead) {
+    if (reset) atomicAdd(&d.stats[0], 1ull);
+    if (fl & F_DIVERGED) atomicAdd(&d.stats[1], 1ull);
+    if (fl & F_OVERFLOW) atomicAdd(&d.stats[2], 1ull);
+    if (fl & F_SPILL) atomicAdd(&d.stats[6], 1ull);
+    atomicAdd(&d.stats[4], (unsigned long long)iters);
+  }
+  return fl;
+}
+
 // K env steps of every env in one launch (bb_step_multi): actions [K][n][3]
 // known in advance (open-loop: benchmarks, replayed action sequences).  Each
-// team steps its env K times back to back; no env waits for the slowest env of
-// the chip at every step, only for the slowest of its wave.  Per step the fast
-// path runs first; an env it hands over (F_SLOWPATH: a base-tree geom may
-// touch the terrain) is restored from the team's LDS copy of the step's start
-// state and takes the full step inline.  Per step k the outputs, counters,
-// auto-reset and terrain draws are exactly those of the k-th bb_step call.
+// team steps its env K times back to back (team_step); no env waits for the
+// slowest env of the chip at every step, only for the slowest of its wave.
+// Per step k the outputs, counters, auto-reset and terrain draws are exactly
+// those of the k-th bb_step call under the serial route.
 template <typename T>
 __global__ __launch_bounds__(64) void multi_step_kernel(ModelT<T> mg, EnvCfg cfg, Dev d, const float* __restrict__ act,
                                                         int K, float* __restrict__ obs, float* __restrict__ rew,
@@ -338,68 +405,225 @@ __global__ __launch_bounds__(64) void multi_step_kernel(ModelT<T> mg, EnvCfg cfg
   const size_t n = size_t(d.n);
 #pragma unroll 1
   for (int k = 0; k < K; k++) {
-    team_sync();
-    for (int i = tm.tl; i < NQ + 2 * NV; i += L) bk[i] = q[i];
-    team_sync();
-    const float* ak = act + size_t(k) * 3 * n;
-    float a[3] = {ak[3 * e], ak[3 * e + 1], ak[3 * e + 2]};
-    const float* hf = d.bank + size_t(tid) * (HF_N * HF_N);
-    float o[15], r, p2[2];
-    int iters = 0;
-    const TerrainRef<T> tr{hf, T(d.size_z[tid]), T(d.hmax[tid]) * T(d.size_z[tid])};
-    const int step0 = step;
-#if BB_MULTI_MODE == 2
-    int fl = F_SLOWPATH;
-#else
-    int fl = env_step<T, false>(m, cfg, q, v, w, step, a, tr, W, o, r, p2, &iters, tm);
-#endif
-    const bool slow = (fl & F_SLOWPATH) != 0;  // team-uniform
-#if BB_MULTI_MODE == 3
-    if (false) {
-#else
-    if (slow) {
-#endif
-      team_sync();
-      for (int i = tm.tl; i < NQ + 2 * NV; i += L) q[i] = bk[i];
-      team_sync();
-      step = step0;
-      fl = full_env_step<T>(m, cfg, q, v, w, step, a, tr, W, o, r, p2, &iters, tm);
-    }
-    const bool reset = auto_reset && (fl & F_TERMINATED);
-    if (lead) {
-      if (slow) atomicAdd(&d.stats[3], 1ull);
-      if (tobs) {
-#pragma unroll
-        for (int i = 0; i < 15; i++) tobs[(size_t(k) * n + e) * 15 + i] = o[i];
-      }
-      if (pos2d) { pos2d[(size_t(k) * n + e) * 2] = p2[0]; pos2d[(size_t(k) * n + e) * 2 + 1] = p2[1]; }
-      if (reset) {
-        tid = next_terrain(d, e);
-        d.terrain[e] = tid;
-      }
-    }
-    if (reset) {
-      tid = __shfl(tid, int(threadIdx.x) & ~(L - 1));  // the lead's draw
-      team_sync();
-      reset_state(m, T(d.offset[tid]), q, v, w);  // every lane writes the same values
-      step = 0;
-#pragma unroll
-      for (int i = 0; i < 15; i++) o[i] = 0.f;
-    }
+    const size_t row = size_t(k) * n + e;
+    const float* ak = act + 3 * row;
+    const float a[3] = {ak[0], ak[1], ak[2]};
+    float o[15], r;
+    const int fl = team_step<T>(m, cfg, d, e, tid, q, v, w, step, bk, a, W, o, r, tobs ? tobs + 15 * row : nullptr,
+                                pos2d ? pos2d + 2 * row : nullptr, auto_reset, tm);
     if (lead) {
 #pragma unroll
-      for (int i = 0; i < 15; i++) obs[(size_t(k) * n + e) * 15 + i] = o[i];
-      rew[size_t(k) * n + e] = r;
-      done[size_t(k) * n + e] = uint8_t(fl);
-      if (reset) atomicAdd(&d.stats[0], 1ull);
-      if (fl & F_DIVERGED) atomicAdd(&d.stats[1], 1ull);
-      if (fl & F_OVERFLOW) atomicAdd(&d.stats[2], 1ull);
-      if (fl & F_SPILL) atomicAdd(&d.stats[6], 1ull);
-      atomicAdd(&d.stats[4], (unsigned long long)iters);
+      for (int i = 0; i < 15; i++) obs[15 * row + i] = o[i];
+      rew[row] = r;
+      done[row] = uint8_t(fl);
     }
   }
   team_sync();
   if (lead) store_state(d, e, q, v, w, step);
+}
+
+// The rollout's policy step for one env on its team: SB3
+// ActorCriticPolicy.forward of the reference's proprio MLP (pi = vf = 4 x 128
+// LeakyReLU trunks over the 15 sorted-key obs; mean = action_net(h_pi), value =
+// value_net(h_vf)), fp32.  Lane tl computes hidden units tl + 16 j (j < 8),
+// each a k-ordered fmaf chain; the layer input is the team's LDS vector.
+// (bb_ppo_mlp_act's MFMA tiles sum in another order: the two agree to fp32
+// rounding, tests/test_gpu_rollout.py.)
+__device__ __forceinline__ float leaky_f(float z) { return z > 0.f ? z : z * 0.01f; }
+__device__ __forceinline__ void team_policy(const float* __restrict__ P, const int* __restrict__ off, const float* x,
+                                            float* hA, float* hB, const Team& tm, float mu[3], float& val) {
+  constexpr int HIDN = 128, IN = 15, PER = HIDN / 16;
+#pragma unroll 1
+  for (int tr = 0; tr < 2; tr++) {
+    const int wb = tr ? MLP_VF_W0 : MLP_PI_W0, bb_ = tr ? MLP_VF_B0 : MLP_PI_B0;
+    {  // layer 0: 15 -> 128
+      const float* W0 = P + off[wb];
+      const float* b0 = P + off[bb_];
+      float acc[PER];
+#pragma unroll
+      for (int j = 0; j < PER; j++) acc[j] = b0[tm.tl + 16 * j];
+#pragma unroll
+      for (int k = 0; k < IN; k++) {
+        const float xk = x[k];
+#pragma unroll
+        for (int j = 0; j < PER; j++) acc[j] = fmaf(xk, W0[(tm.tl + 16 * j) * IN + k], acc[j]);
+      }
+#pragma unroll
+      for (int j = 0; j < PER; j++) hA[tm.tl + 16 * j] = leaky_f(acc[j]);
+      team_sync();
+    }
+    float* hin = hA;
+    float* hout = hB;
+#pragma unroll 1
+    for (int l = 1; l < 4; l++) {  // 128 -> 128
+      const float* Wl = P + off[wb + l];
+      const float* bl = P + off[bb_ + l];
+      float acc[PER];
+#pragma unroll
+      for (int j = 0; j < PER; j++) acc[j] = bl[tm.tl + 16 * j];
+#pragma unroll 2
+      for (int k4 = 0; k4 < HIDN / 4; k4 += 2) {
+        float4 wv[2][PER];
+#pragma unroll
+        for (int u = 0; u < 2; u++)
+#pragma unroll
+          for (int j = 0; j < PER; j++)
+            wv[u][j] = *reinterpret_cast<const float4*>(Wl + (tm.tl + 16 * j) * HIDN + 4 * (k4 + u));
+#pragma unroll
+        for (int u = 0; u < 2; u++) {
+          const float4 h4 = *reinterpret_cast<const float4*>(hin + 4 * (k4 + u));
+#pragma unroll
+          for (int j = 0; j < PER; j++) {
+            acc[j] = fmaf(h4.x, wv[u][j].x, acc[j]);
+            acc[j] = fmaf(h4.y, wv[u][j].y, acc[j]);
+            acc[j] = fmaf(h4.z, wv[u][j].z, acc[j]);
+            acc[j] = fmaf(h4.w, wv[u][j].w, acc[j]);
+          }
+        }
+      }
+#pragma unroll
+      for (int j = 0; j < PER; j++) hout[tm.tl + 16 * j] = leaky_f(acc[j]);
+      team_sync();
+      float* t_ = hin; hin = hout; hout = t_;
+    }
+    // heads on h4 (hin): lane partial sums over its 8 units, then the team sum
+    if (tr == 0) {
+      const float* Wa = P + off[MLP_WA];
+#pragma unroll
+      for (int c = 0; c < 3; c++) {
+        float s = 0.f;
+#pragma unroll
+        for (int j = 0; j < PER; j++) s = fmaf(hin[tm.tl + 16 * j], Wa[c * HIDN + tm.tl + 16 * j], s);
+        mu[c] = team_sum(tm, s) + P[off[MLP_BA] + c];
+      }
+    } else {
+      const float* Wv = P + off[MLP_WV];
+      float s = 0.f;
+#pragma unroll
+      for (int j = 0; j < PER; j++) s = fmaf(hin[tm.tl + 16 * j], Wv[tm.tl + 16 * j], s);
+      val = team_sum(tm, s) + P[off[MLP_BV]];
+    }
+    team_sync();
+  }
+}
+
+struct RolloutDev {
+  const float* P;
+  int off[MLP_NSLOTS];
+  const float* noise;      // [T][n][3]
+  int T;
+  float* obs;              // [n][15] in/out
+  uint8_t* last_starts;    // [n] in/out
+  double* ep_ret;          // [n] in/out
+  long long* ep_len;       // [n] in/out
+  float* b_obs;            // [T][n][15]
+  float* b_act;            // [T][n][3]
+  float* b_val;            // [T][n]
+  float* b_logp;           // [T][n]
+  float* b_rew;            // [T][n]
+  uint8_t* b_starts;       // [T][n]
+  double* ep_r;            // [T][n]
+  long long* ep_l;         // [T][n]
+};
+
+// One whole PPO rollout (SB3 OnPolicyAlgorithm.collect_rollouts + Monitor) in
+// ONE launch (bb_rollout): every env runs its T steps of (policy, sample,
+// clip, env step, bookkeeping) back to back on its team -- the policy's
+// parameters are fixed during a rollout, and envs are independent, so no step
+// needs a grid-wide barrier.  Per step the rollout buffer gets the obs, the
+// unclipped action, value, log-probability, reward and episode start; finished
+// episodes their (float64 return, length).  The step itself is team_step
+// (fast path, inline full-step hand-over, auto-reset).
+template <typename T>
+__global__ __launch_bounds__(64) void rollout_kernel(ModelT<T> mg, EnvCfg cfg, Dev d, RolloutDev ro, int L, int epw) {
+  extern __shared__ __align__(16) unsigned char smem[];
+  const int nwg = int(gridDim.x), b = int(blockIdx.x);
+  const int g = (nwg & 7) ? b : (b & 7) * (nwg >> 3) + (b >> 3);
+  __shared__ ModelT<T> ms;
+  if (threadIdx.x == 0) ms = mg;
+  __syncthreads();
+  const ModelT<T>& m = ms;
+  const Team tm{L, int(threadIdx.x) & (L - 1)};
+  const int team = threadIdx.x / L;
+  if (team >= epw) return;
+  const int e = g * epw + team;
+  if (unsigned(e) >= unsigned(d.n)) return;
+  const bool lead = tm.tl == 0;
+  EnvWork<T>& W = team_work<T>(smem, team);
+  T* bk = reinterpret_cast<T*>(smem + size_t(epw) * work_stride<T>()) + team * (NQ + 2 * NV);
+  // policy scratch after the step-start copies: x[16], hA[128], hB[128] per team
+  float* pol = reinterpret_cast<float*>(smem + size_t(epw) * work_stride<T>() +
+                                        (size_t(epw) * (NQ + 2 * NV) * sizeof(T) + 15) / 16 * 16) + team * 272;
+  float* x = pol;
+  float* hA = pol + 16;
+  float* hB = pol + 144;
+  if (lead) W.bspill = body_spill_of<T>(d, e);
+  T* q = W.qn;
+  T* v = W.vn;
+  T* w = W.wn;
+  int step;
+  load_state(d, e, q, v, w, step);
+  int tid = d.terrain[e];
+  const size_t n = size_t(d.n);
+  float o[15];
+#pragma unroll
+  for (int i = 0; i < 15; i++) o[i] = ro.obs[15 * size_t(e) + i];
+  uint8_t start = ro.last_starts[e];
+  double ret = ro.ep_ret[e];
+  long long len = ro.ep_len[e];
+  const float* ls = ro.P + ro.off[MLP_LS];
+  constexpr float HL2PI = 0.91893853320467274f;
+#pragma unroll 1
+  for (int t = 0; t < ro.T; t++) {
+    const size_t row = size_t(t) * n + e;
+    team_sync();
+    if (tm.tl < 15) x[tm.tl] = o[tm.tl];
+    team_sync();
+    float mu[3], val = 0.f;
+    team_policy(ro.P, ro.off, x, hA, hB, tm, mu, val);
+    // SB3 DiagGaussian (bb_ppo_mlp_act's arithmetic): a = mean + eps * exp(log_std)
+    float a[3], ac[3], lp = 0.f;
+#pragma unroll
+    for (int j = 0; j < 3; j++) {
+      const float ls_j = ls[j];
+      a[j] = __fadd_rn(mu[j], __fmul_rn(ro.noise[3 * row + j], expf(ls_j)));
+      const float z = __fmul_rn(__fsub_rn(a[j], mu[j]), expf(-ls_j));
+      lp += -0.5f * z * z - ls_j - 0.5f * (2.f * HL2PI);
+      ac[j] = fminf(fmaxf(a[j], -1.f), 1.f);
+    }
+    if (lead) {
+#pragma unroll
+      for (int i = 0; i < 15; i++) ro.b_obs[15 * row + i] = o[i];
+#pragma unroll
+      for (int j = 0; j < 3; j++) ro.b_act[3 * row + j] = a[j];
+      ro.b_val[row] = val;
+      ro.b_logp[row] = lp;
+      ro.b_starts[row] = start;
+    }
+    float r;
+    const int fl = team_step<T>(m, cfg, d, e, tid, q, v, w, step, bk, ac, W, o, r, nullptr, nullptr, 1, tm);
+    // collect_rollouts + Monitor bookkeeping (bb_rollout_track): done = terminated
+    const bool dn = (fl & F_TERMINATED) != 0;
+    ret += double(r);
+    len += 1;
+    if (lead) {
+      ro.b_rew[row] = r;
+      ro.ep_r[row] = dn ? ret : __builtin_nan("");
+      ro.ep_l[row] = dn ? len : 0;
+    }
+    ret = dn ? 0.0 : ret;
+    len = dn ? 0 : len;
+    start = dn ? 1 : 0;
+  }
+  team_sync();
+  if (lead) {
+    store_state(d, e, q, v, w, step);
+#pragma unroll
+    for (int i = 0; i < 15; i++) ro.obs[15 * size_t(e) + i] = o[i];
+    ro.last_starts[e] = start;
+    ro.ep_ret[e] = ret;
+    ro.ep_len[e] = len;
+  }
 }
 
 template <typename T>
@@ -724,6 +948,22 @@ int launch_step(bb_handle* h, const float* a, float* o, float* r, uint8_t* dn, f
 template <typename T>
 size_t multi_lds_bytes(int epw) { return lds_bytes<T>(epw) + size_t(epw) * (NQ + 2 * NV) * sizeof(T); }
 
+// dynamic LDS of rollout_kernel: multi_step_kernel's + the teams' policy scratch
+template <typename T>
+size_t rollout_lds_bytes(int epw) {
+  return lds_bytes<T>(epw) + (size_t(epw) * (NQ + 2 * NV) * sizeof(T) + 15) / 16 * 16 + size_t(epw) * 272 * sizeof(float);
+}
+
+template <typename T>
+int launch_rollout(bb_handle* h, const RolloutDev& ro, hipStream_t s) {
+  const int epw = h->epw;
+  const int blocks = (h->n + epw - 1) / epw;
+  hipLaunchKernelGGL(rollout_kernel<T>, dim3(blocks), dim3(WAVE), rollout_lds_bytes<T>(epw), s, model_of<T>(h),
+                     h->cfg, h->d, ro, h->team, epw);
+  HIPCHK(hipGetLastError());
+  return 0;
+}
+
 template <typename T>
 int launch_multi(bb_handle* h, const float* a, int K, float* o, float* r, uint8_t* dn, float* t, float* p2, int ar,
                  hipStream_t s) {
@@ -890,6 +1130,9 @@ int bb_create(int n_envs, int device, const bb_params* p, bb_handle** out) {
     const void* mk = h->fp64 ? (const void*)multi_step_kernel<double> : (const void*)multi_step_kernel<float>;
     const int mlb = (int)(h->fp64 ? multi_lds_bytes<double>(h->epw) : multi_lds_bytes<float>(h->epw));
     HIPCHK(hipFuncSetAttribute(mk, hipFuncAttributeMaxDynamicSharedMemorySize, mlb));
+    const void* rk = h->fp64 ? (const void*)rollout_kernel<double> : (const void*)rollout_kernel<float>;
+    const int rlb = (int)(h->fp64 ? rollout_lds_bytes<double>(h->epw) : rollout_lds_bytes<float>(h->epw));
+    HIPCHK(hipFuncSetAttribute(rk, hipFuncAttributeMaxDynamicSharedMemorySize, rlb));
   }
   *out = h;
   int rc = bb_reset(h, nullptr, nullptr, nullptr);
@@ -1189,6 +1432,33 @@ int bb_step_multi(bb_handle* h, const float* a, int k, float* o, float* r, uint8
   if (k < 1) return fail("bb_step_multi: k_steps must be >= 1 (got %d)", k);
   return h->fp64 ? launch_multi<double>(h, a, k, o, r, dn, t, p2, ar, (hipStream_t)s)
                  : launch_multi<float>(h, a, k, o, r, dn, t, p2, ar, (hipStream_t)s);
+}
+
+int bb_rollout(bb_handle* h, const bb_rollout_args* a, void* stream) {
+  if (!h) return fail("bb_rollout: NULL handle");
+  if (!a || !a->params || !a->noise || !a->obs || !a->last_starts || !a->ep_ret || !a->ep_len || !a->buf_obs ||
+      !a->buf_actions || !a->buf_values || !a->buf_log_prob || !a->buf_rewards || !a->buf_starts || !a->ep_r_out ||
+      !a->ep_l_out)
+    return fail("bb_rollout: NULL argument");
+  if (a->n_steps < 1) return fail("bb_rollout: n_steps must be >= 1 (got %d)", a->n_steps);
+  if (h->cfg.reward_kind == BB_REWARD_NONE)
+    return fail("bb_rollout: the reward is a host-side plugin (BB_REWARD_NONE); step with bb_step instead");
+  const int sizes[MLP_NSLOTS] = {128 * 15, 128 * 128, 128 * 128, 128 * 128, 128, 128, 128, 128,
+                                 128 * 15, 128 * 128, 128 * 128, 128 * 128, 128, 128, 128, 128,
+                                 3 * 128, 3, 128, 1, 3};
+  for (int i = 0; i < MLP_NSLOTS; i++)
+    if (a->offsets[i] < 0 || a->offsets[i] % 4 || (int64_t)a->offsets[i] + sizes[i] > a->n_params)
+      return fail("bb_rollout: offsets[%d] = %d is not a 4-aligned slot inside the %lld-float buffer", i,
+                  a->offsets[i], (long long)a->n_params);
+  if (reinterpret_cast<uintptr_t>(a->params) & 15) return fail("bb_rollout: params must be 16-byte aligned");
+  RolloutDev ro;
+  ro.P = a->params;
+  for (int i = 0; i < MLP_NSLOTS; i++) ro.off[i] = a->offsets[i];
+  ro.noise = a->noise; ro.T = a->n_steps; ro.obs = a->obs; ro.last_starts = a->last_starts; ro.ep_ret = a->ep_ret;
+  ro.ep_len = reinterpret_cast<long long*>(a->ep_len); ro.b_obs = a->buf_obs; ro.b_act = a->buf_actions;
+  ro.b_val = a->buf_values; ro.b_logp = a->buf_log_prob; ro.b_rew = a->buf_rewards; ro.b_starts = a->buf_starts;
+  ro.ep_r = a->ep_r_out; ro.ep_l = reinterpret_cast<long long*>(a->ep_l_out);
+  return h->fp64 ? launch_rollout<double>(h, ro, (hipStream_t)stream) : launch_rollout<float>(h, ro, (hipStream_t)stream);
 }
 
 int bb_get_state(bb_handle* h, double* qpos, double* qvel, double* warm, int32_t* steps) {

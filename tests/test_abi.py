@@ -105,7 +105,8 @@ def test_argument_errors_without_gpu(native):
                                                 None, 16, None, 16, 16, None), "inside the 40000-float buffer"),
                       (lambda: L.bb_set_terrain_stream(None, None, 1, 4, None), "NULL handle"),
                       (lambda: L.bb_get_env_terrain(None, None, None), "NULL handle"),
-                      (lambda: L.bb_step_multi(None, None, 4, None, None, None, None, None, 1, None), "NULL handle")):
+                      (lambda: L.bb_step_multi(None, None, 4, None, None, None, None, None, 1, None), "NULL handle"),
+                      (lambda: L.bb_rollout(None, None, None), "NULL handle")):
         assert call() < 0
         assert msg in _err(native), (msg, _err(native))
 
@@ -119,7 +120,7 @@ def test_ctypes_structs_match_the_header(tmp_path, native):
     if shutil.which("gcc") is None:
         pytest.skip("gcc not available")
     structs = {"bb_ppo_mlp_args": native.PPOMlpArgs, "bb_encoder_params": native.EncoderParams,
-               "bb_params": native.BBParams, "bb_perlin_cfg": native.PerlinCfg}
+               "bb_params": native.BBParams, "bb_perlin_cfg": native.PerlinCfg, "bb_rollout_args": native.RolloutArgs}
     lines = ['#include <stdio.h>', '#include <stddef.h>', '#include "ballbot_mi355x.h"', 'int main(void) {']
     for cname, py in structs.items():
         lines.append(f'printf("{cname} size %zu\\n", sizeof({cname}));')

@@ -641,6 +641,7 @@ def test_rollout_graph_matches_eager(monkeypatch):
     from ballbot_rl.training.logger import CSVLogger
     from ballbot_rl.training.ppo import BatchedPPO
 
+    monkeypatch.setenv("BB_FUSED_ROLLOUT", "0")  # the per-step rollout (bb_rollout is tested in test_gpu_rollout.py)
     models = []
     for graph in ("0", "1"):
         monkeypatch.setenv("BB_ROLLOUT_GRAPH", graph)
