@@ -461,7 +461,11 @@ __device__ __forceinline__ void team_policy(const float* __restrict__ P, const i
       float acc[PER];
 #pragma unroll
       for (int j = 0; j < PER; j++) acc[j] = bl[tm.tl + 16 * j];
+#ifdef BB_POLICY_UNROLL
+#pragma unroll BB_POLICY_UNROLL
+#else
 #pragma unroll 2
+#endif
       for (int k4 = 0; k4 < HIDN / 4; k4 += 2) {
         float4 wv[2][PER];
 #pragma unroll
@@ -551,9 +555,14 @@ __global__ __launch_bounds__(64) void rollout_kernel(ModelT<T> mg, EnvCfg cfg, D
   const bool lead = tm.tl == 0;
   EnvWork<T>& W = team_work<T>(smem, team);
   T* bk = reinterpret_cast<T*>(smem + size_t(epw) * work_stride<T>()) + team * (NQ + 2 * NV);
-  // policy scratch after the step-start copies: x[16], hA[128], hB[128] per team
-  float* pol = reinterpret_cast<float*>(smem + size_t(epw) * work_stride<T>() +
-                                        (size_t(epw) * (NQ + 2 * NV) * sizeof(T) + 15) / 16 * 16) + team * 272;
+  // policy scratch x[16], hA[128], hB[128] in the team's contact stores (g, then
+  // bc): they only hold data inside a step.  (A separate LDS block pushed a
+  // workgroup past 40 KB: 3 instead of 4 workgroups per CU, a quarter of the
+  // waves in a second round.)
+  static_assert(offsetof(EnvWork<T>, bc) == offsetof(EnvWork<T>, g) + sizeof(W.g) &&
+                    sizeof(W.g) + sizeof(W.bc) >= 272 * sizeof(float),
+                "policy scratch must fit in EnvWork::g + bc");
+  float* pol = reinterpret_cast<float*>(W.g);
   float* x = pol;
   float* hA = pol + 16;
   float* hB = pol + 144;
@@ -579,8 +588,10 @@ __global__ __launch_bounds__(64) void rollout_kernel(ModelT<T> mg, EnvCfg cfg, D
     team_sync();
     if (tm.tl < 15) x[tm.tl] = o[tm.tl];
     team_sync();
-    float mu[3], val = 0.f;
+    float mu[3] = {0.f, 0.f, 0.f}, val = 0.f;
+#ifndef BB_ROLLOUT_NO_POLICY
     team_policy(ro.P, ro.off, x, hA, hB, tm, mu, val);
+#endif
     // SB3 DiagGaussian (bb_ppo_mlp_act's arithmetic): a = mean + eps * exp(log_std)
     float a[3], ac[3], lp = 0.f;
 #pragma unroll
@@ -948,11 +959,9 @@ int launch_step(bb_handle* h, const float* a, float* o, float* r, uint8_t* dn, f
 template <typename T>
 size_t multi_lds_bytes(int epw) { return lds_bytes<T>(epw) + size_t(epw) * (NQ + 2 * NV) * sizeof(T); }
 
-// dynamic LDS of rollout_kernel: multi_step_kernel's + the teams' policy scratch
+// dynamic LDS of rollout_kernel: multi_step_kernel's (the policy scratch lives in EnvWork)
 template <typename T>
-size_t rollout_lds_bytes(int epw) {
-  return lds_bytes<T>(epw) + (size_t(epw) * (NQ + 2 * NV) * sizeof(T) + 15) / 16 * 16 + size_t(epw) * 272 * sizeof(float);
-}
+size_t rollout_lds_bytes(int epw) { return multi_lds_bytes<T>(epw); }
 
 template <typename T>
 int launch_rollout(bb_handle* h, const RolloutDev& ro, hipStream_t s) {

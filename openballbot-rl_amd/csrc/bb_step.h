@@ -388,6 +388,11 @@ BB_HD int env_step(const ModelT<T>& m, const EnvCfg& cfg, T* q, T* v, T* warm, i
   if (acc_reset) flags |= F_DIVERGED;
   if (so.overflow) flags |= F_OVERFLOW;
   if (so.nb > MAXB_LDS) flags |= F_SPILL;
+  {
+  // obs, reward and termination without FMA contraction: numpy's float32 /
+  // float64 chains do not fuse, and every kernel that inlines this (step,
+  // multi-step, rollout) then rounds alike
+#pragma clang fp contract(off)
   // _get_obs
   T rv[3];
   quat_to_rotvec(so.quat_b, rv);
@@ -436,6 +441,7 @@ BB_HD int env_step(const ModelT<T>& m, const EnvCfg& cfg, T* q, T* v, T* warm, i
   else if (cfg.reward_kind != 2) r = r + cfg.survival_bonus;
   reward = r;
   return flags;
+  }
 }
 
 }  // namespace bb

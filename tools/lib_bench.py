@@ -29,7 +29,7 @@ def build(name, flags):
     return out
 
 
-def run_one(lib, precision, terrain, steps, warmup, multi=0):
+def run_one(lib, precision, terrain, steps, warmup, multi=0, rollout=False):
     import torch
     from ballbot_gym import _native
     from ballbot_gym.envs import BallbotVecEnv
@@ -38,6 +38,21 @@ def run_one(lib, precision, terrain, steps, warmup, multi=0):
     env = BallbotVecEnv(4096, device="cuda:0", precision=precision, terrain_config={"type": terrain, "config": {}},
                         n_terrains=None if terrain == "perlin" else 16)
     pool = torch.rand(64, 4096, 3, device="cuda:0") * 2 - 1
+    if rollout:  # PPO collect_rollouts (4096 envs x 64 steps), BB_FUSED_ROLLOUT picks bb_rollout or per-step
+        from ballbot_rl.training.logger import CSVLogger
+        from ballbot_rl.training.ppo import BatchedPPO
+
+        m = BatchedPPO(env, n_steps=64, batch_size=8192, n_epochs=1, seed=1, logger=CSVLogger(None, stdout=False))
+        for _ in range(3):
+            m.collect_rollouts()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        reps = max(1, steps // 64)
+        for _ in range(reps):
+            m.collect_rollouts()
+        torch.cuda.synchronize()
+        dt = (time.perf_counter() - t0) / (reps * 64)
+        return {"ms": dt * 1e3, "env_steps_per_s": 4096 / dt, "rollout": True, "stats": env.stats()}
     if multi:  # bb_step_multi: `multi` steps per launch
         assert 64 % multi == 0
         o = torch.empty(multi, 4096, 15, device="cuda:0")
@@ -72,6 +87,7 @@ def main():
     ap.add_argument("--warmup", type=int, default=300)
     ap.add_argument("--child", default=None)
     ap.add_argument("--multi", type=int, default=0, help="steps per bb_step_multi launch (0: bb_step per step)")
+    ap.add_argument("--rollout", action="store_true", help="time PPO collect_rollouts instead of env steps")
     ap.add_argument("--no-build", action="store_true", help="use the prebuilt tools/_build/libbb_<NAME>.so")
     ap.add_argument("--build-only", action="store_true", help="compile the variants (here, on the CPU) and exit")
     a = ap.parse_args()
@@ -81,14 +97,14 @@ def main():
             list(ex.map(lambda v: build(v.partition(":")[0], [f for f in v.partition(":")[2].split(",") if f]), a.variant))
         return
     if a.child:
-        print(json.dumps(run_one(a.child, a.precision, a.terrain, a.steps, a.warmup, a.multi)))
+        print(json.dumps(run_one(a.child, a.precision, a.terrain, a.steps, a.warmup, a.multi, a.rollout)))
         return
     for v in a.variant:
         name, _, fl = v.partition(":")
         lib = (ROOT / "tools" / "_build" / f"libbb_{name}.so") if a.no_build else build(name, [f for f in fl.split(",") if f])
         r = subprocess.run([sys.executable, __file__, "--child", str(lib), "--precision", a.precision,
                             "--terrain", a.terrain, "--steps", str(a.steps), "--warmup", str(a.warmup),
-                            "--multi", str(a.multi)],
+                            "--multi", str(a.multi)] + (["--rollout"] if a.rollout else []),
                            capture_output=True, text=True, timeout=600)
         line = r.stdout.strip().splitlines()[-1] if r.returncode == 0 else r.stderr[-2000:]
         print(json.dumps({"variant": name, "flags": fl, "precision": a.precision, "terrain": a.terrain, "multi": a.multi,
