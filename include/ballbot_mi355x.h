@@ -235,7 +235,9 @@ int bb_ppo_mlp_act(const float* params_dev, const int32_t* offsets, int64_t n_pa
  * serial route for the same clipped actions).  Built-in rewards only (not
  * BB_REWARD_NONE).  One launch; graph-capturable. */
 typedef struct bb_rollout_args {
-  const float* params;      /* flat fp32 policy parameters */
+  const float* params;      /* flat fp32 policy parameters, bb_ppo_mlp_act's slots, except that the eight
+                               trunk weight matrices (slots 0-3, 8-11) are stored input-major (W^T,
+                               [in][128]) so that a team's lanes read whole cache lines */
   int32_t offsets[21];
   int64_t n_params;
   const float* noise;       /* [T][n][3] standard normal draws */

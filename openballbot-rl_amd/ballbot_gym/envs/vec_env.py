@@ -109,6 +109,8 @@ class BallbotVecEnv:
             N.check(L.bb_generate_perlin(h, 0, len(sd), sd.ctypes.data_as(C.POINTER(C.c_int32)), C.byref(pcfg),
                                          float(size_z)), "bb_generate_perlin")
         self.n_terrains = p.n_terrains
+        # any terrain with relief: bb_step routes through the predictor (route 0) on such banks
+        self.relief = gp is not None or any(float(np.max(data)) > 0.0 for data, _ in bank)
         n, dev = self.num_envs, self.device
         self.obs = torch.zeros(n, N.NOBS, dtype=torch.float32, device=dev)
         self.terminal_obs = torch.zeros(n, N.NOBS, dtype=torch.float32, device=dev)

@@ -673,9 +673,18 @@ class BatchedPPO:
         noise = torch.randn(T, n, 3, generator=self.gen, device=dev)
         ep_r = torch.empty(T, n, dtype=torch.float64, device=dev)
         ep_l = torch.empty(T, n, dtype=torch.int64, device=dev)
+        # bb_rollout reads the trunk weights input-major (W^T): a transposed copy per rollout
         flat = self.optimizer.flat
+        if getattr(self, "_pol_t", None) is None or self._pol_t.numel() != flat.numel():
+            self._pol_t = torch.empty_like(flat)
+        pt = self._pol_t
+        pt.copy_(flat)
+        for w0 in (0, 8):  # MLP_PI_W0, MLP_VF_W0 (bb_mlp.h)
+            for l in range(4):
+                o, k = int(slots[w0 + l]), (15 if l == 0 else 128)
+                pt[o:o + 128 * k].view(k, 128).copy_(flat[o:o + 128 * k].view(128, k).t())
         a = N.RolloutArgs()
-        a.params, a.n_params, a.noise, a.n_steps = flat.data_ptr(), int(flat.numel()), noise.data_ptr(), T
+        a.params, a.n_params, a.noise, a.n_steps = pt.data_ptr(), int(pt.numel()), noise.data_ptr(), T
         for i, o in enumerate(slots):
             a.offsets[i] = int(o)
         a.obs, a.last_starts = obs_io.data_ptr(), self._last_starts.data_ptr()
@@ -699,8 +708,12 @@ class BatchedPPO:
         T, n = self.n_steps, self.n_envs
         if self._last_obs is None:
             self._last_obs, _ = env.reset()
-        if (hasattr(env, "run_rollout") and getattr(env, "_host_reward", None) is None
-                and os.environ.get("BB_FUSED_ROLLOUT", "1") != "0"):
+        # bb_rollout on flat banks (default); on relief banks the per-step rollout keeps the
+        # predicted full kernel beside the fast one (bb_rollout's hand-overs run inline and
+        # diverge inside a wave: perlin 4.97 M against 5.15 M rollout env-steps/s)
+        fr = os.environ.get("BB_FUSED_ROLLOUT", "auto")
+        if (hasattr(env, "run_rollout") and getattr(env, "_host_reward", None) is None and fr != "0"
+                and (fr == "1" or not getattr(env, "relief", True))):
             return self._collect_rollout_kernel(slots)
         if (self.use_graphs and hasattr(env, "step_flags") and getattr(env, "_host_reward", None) is None
                 and hasattr(env, "obs") and os.environ.get("BB_ROLLOUT_GRAPH", "1") != "0"):

@@ -425,87 +425,70 @@ __global__ __launch_bounds__(64) void multi_step_kernel(ModelT<T> mg, EnvCfg cfg
 // The rollout's policy step for one env on its team: SB3
 // ActorCriticPolicy.forward of the reference's proprio MLP (pi = vf = 4 x 128
 // LeakyReLU trunks over the 15 sorted-key obs; mean = action_net(h_pi), value =
-// value_net(h_vf)), fp32.  Lane tl computes hidden units tl + 16 j (j < 8),
-// each a k-ordered fmaf chain; the layer input is the team's LDS vector.
+// value_net(h_vf)), fp32.  The trunk weights come INPUT-major (W^T: [in][128],
+// bb_rollout_args), so for each input k the team's 16 lanes read one
+// contiguous 512-B row slice: lane tl owns units 4 tl + c and 64 + 4 tl + c
+// (c < 4) as two float4s, and every fetched cache line is used whole (the
+// output-major rows cost 4x the L2 traffic: 16 lines per load, 16 B used of
+// each).  Each unit is a k-ordered fmaf chain from the layer input in LDS.
 // (bb_ppo_mlp_act's MFMA tiles sum in another order: the two agree to fp32
 // rounding, tests/test_gpu_rollout.py.)
 __device__ __forceinline__ float leaky_f(float z) { return z > 0.f ? z : z * 0.01f; }
 __device__ __forceinline__ void team_policy(const float* __restrict__ P, const int* __restrict__ off, const float* x,
                                             float* hA, float* hB, const Team& tm, float mu[3], float& val) {
-  constexpr int HIDN = 128, IN = 15, PER = HIDN / 16;
+  constexpr int HIDN = 128, IN = 15;
+  const int u0 = 4 * tm.tl;  // this lane's units: u0 + c, 64 + u0 + c
 #pragma unroll 1
   for (int tr = 0; tr < 2; tr++) {
     const int wb = tr ? MLP_VF_W0 : MLP_PI_W0, bb_ = tr ? MLP_VF_B0 : MLP_PI_B0;
-    {  // layer 0: 15 -> 128
-      const float* W0 = P + off[wb];
-      const float* b0 = P + off[bb_];
-      float acc[PER];
-#pragma unroll
-      for (int j = 0; j < PER; j++) acc[j] = b0[tm.tl + 16 * j];
-#pragma unroll
-      for (int k = 0; k < IN; k++) {
-        const float xk = x[k];
-#pragma unroll
-        for (int j = 0; j < PER; j++) acc[j] = fmaf(xk, W0[(tm.tl + 16 * j) * IN + k], acc[j]);
-      }
-#pragma unroll
-      for (int j = 0; j < PER; j++) hA[tm.tl + 16 * j] = leaky_f(acc[j]);
-      team_sync();
-    }
     float* hin = hA;
     float* hout = hB;
 #pragma unroll 1
-    for (int l = 1; l < 4; l++) {  // 128 -> 128
-      const float* Wl = P + off[wb + l];
+    for (int l = 0; l < 4; l++) {
+      const float* WT = P + off[wb + l];  // [K][128]
       const float* bl = P + off[bb_ + l];
-      float acc[PER];
-#pragma unroll
-      for (int j = 0; j < PER; j++) acc[j] = bl[tm.tl + 16 * j];
+      const float* in = l ? hin : x;
+      const int K = l ? HIDN : IN;
+      float4 a0 = *reinterpret_cast<const float4*>(bl + u0);
+      float4 a1 = *reinterpret_cast<const float4*>(bl + 64 + u0);
 #ifdef BB_POLICY_UNROLL
 #pragma unroll BB_POLICY_UNROLL
 #else
-#pragma unroll 2
+#pragma unroll 8
 #endif
-      for (int k4 = 0; k4 < HIDN / 4; k4 += 2) {
-        float4 wv[2][PER];
-#pragma unroll
-        for (int u = 0; u < 2; u++)
-#pragma unroll
-          for (int j = 0; j < PER; j++)
-            wv[u][j] = *reinterpret_cast<const float4*>(Wl + (tm.tl + 16 * j) * HIDN + 4 * (k4 + u));
-#pragma unroll
-        for (int u = 0; u < 2; u++) {
-          const float4 h4 = *reinterpret_cast<const float4*>(hin + 4 * (k4 + u));
-#pragma unroll
-          for (int j = 0; j < PER; j++) {
-            acc[j] = fmaf(h4.x, wv[u][j].x, acc[j]);
-            acc[j] = fmaf(h4.y, wv[u][j].y, acc[j]);
-            acc[j] = fmaf(h4.z, wv[u][j].z, acc[j]);
-            acc[j] = fmaf(h4.w, wv[u][j].w, acc[j]);
-          }
-        }
+      for (int k = 0; k < K; k++) {
+        const float hk = in[k];
+        const float4 w0 = *reinterpret_cast<const float4*>(WT + k * HIDN + u0);
+        const float4 w1 = *reinterpret_cast<const float4*>(WT + k * HIDN + 64 + u0);
+        a0.x = fmaf(hk, w0.x, a0.x); a0.y = fmaf(hk, w0.y, a0.y);
+        a0.z = fmaf(hk, w0.z, a0.z); a0.w = fmaf(hk, w0.w, a0.w);
+        a1.x = fmaf(hk, w1.x, a1.x); a1.y = fmaf(hk, w1.y, a1.y);
+        a1.z = fmaf(hk, w1.z, a1.z); a1.w = fmaf(hk, w1.w, a1.w);
       }
-#pragma unroll
-      for (int j = 0; j < PER; j++) hout[tm.tl + 16 * j] = leaky_f(acc[j]);
+      float* out = l ? hout : hin;  // layer 0 writes hA; later layers alternate
+      *reinterpret_cast<float4*>(out + u0) = make_float4(leaky_f(a0.x), leaky_f(a0.y), leaky_f(a0.z), leaky_f(a0.w));
+      *reinterpret_cast<float4*>(out + 64 + u0) =
+          make_float4(leaky_f(a1.x), leaky_f(a1.y), leaky_f(a1.z), leaky_f(a1.w));
       team_sync();
-      float* t_ = hin; hin = hout; hout = t_;
+      if (l) { float* t_ = hin; hin = hout; hout = t_; }
     }
-    // heads on h4 (hin): lane partial sums over its 8 units, then the team sum
+    // heads on h4 (hin, output-major Wa/Wv): lane partial sums over its 8 units, then the team sum
+    const float4 h0 = *reinterpret_cast<const float4*>(hin + u0);
+    const float4 h1 = *reinterpret_cast<const float4*>(hin + 64 + u0);
+    auto dot8 = [&](const float* w) {
+      const float4 w0 = *reinterpret_cast<const float4*>(w + u0);
+      const float4 w1 = *reinterpret_cast<const float4*>(w + 64 + u0);
+      float s = 0.f;
+      s = fmaf(h0.x, w0.x, s); s = fmaf(h0.y, w0.y, s); s = fmaf(h0.z, w0.z, s); s = fmaf(h0.w, w0.w, s);
+      s = fmaf(h1.x, w1.x, s); s = fmaf(h1.y, w1.y, s); s = fmaf(h1.z, w1.z, s); s = fmaf(h1.w, w1.w, s);
+      return s;
+    };
     if (tr == 0) {
       const float* Wa = P + off[MLP_WA];
 #pragma unroll
-      for (int c = 0; c < 3; c++) {
-        float s = 0.f;
-#pragma unroll
-        for (int j = 0; j < PER; j++) s = fmaf(hin[tm.tl + 16 * j], Wa[c * HIDN + tm.tl + 16 * j], s);
-        mu[c] = team_sum(tm, s) + P[off[MLP_BA] + c];
-      }
+      for (int c = 0; c < 3; c++) mu[c] = team_sum(tm, dot8(Wa + c * HIDN)) + P[off[MLP_BA] + c];
     } else {
-      const float* Wv = P + off[MLP_WV];
-      float s = 0.f;
-#pragma unroll
-      for (int j = 0; j < PER; j++) s = fmaf(hin[tm.tl + 16 * j], Wv[tm.tl + 16 * j], s);
-      val = team_sum(tm, s) + P[off[MLP_BV]];
+      val = team_sum(tm, dot8(P + off[MLP_WV])) + P[off[MLP_BV]];
     }
     team_sync();
   }
