@@ -305,11 +305,13 @@ int full_env_step(const ModelT<T>& m, const EnvCfg& cfg, T* q, T* v, T* w, int& 
 // bk of the step's start state and takes the full step inline.  Auto-reset,
 // terrain draw and counters as step_kernel.  tobs_row / p2_row (may be NULL):
 // this step's terminal obs and pos2d.  On return o holds the obs after any
-// reset; the flags are the step's.
+// reset; the flags are the step's.  full: the predictor routed the env to the
+// full step (relief_multi_kernel): the fast path is not tried.
 template <typename T>
 __device__ __forceinline__ int team_step(const ModelT<T>& m, const EnvCfg& cfg, const Dev& d, int e, int& tid,
                                          T* q, T* v, T* w, int& step, T* bk, const float* a, EnvWork<T>& W, float* o,
-                                         float& r, float* tobs_row, float* p2_row, int auto_reset, const Team& tm) {
+                                         float& r, float* tobs_row, float* p2_row, int auto_reset, const Team& tm,
+                                         bool full = false) {
   const int L = tm.L;
   const bool lead = tm.tl == 0;
   team_sync();
@@ -323,7 +325,7 @@ __device__ __forceinline__ int team_step(const ModelT<T>& m, const EnvCfg& cfg, 
 #if BB_MULTI_MODE == 2
   int fl = F_SLOWPATH;
 #else
-  int fl = env_step<T, false>(m, cfg, q, v, w, step, a, tr, W, o, r, p2, &iters, tm);
+  int fl = full ? F_SLOWPATH : env_step<T, false>(m, cfg, q, v, w, step, a, tr, W, o, r, p2, &iters, tm);
 #endif
   const bool slow = (fl & F_SLOWPATH) != 0;  // team-uniform
 #if BB_MULTI_MODE == 3
@@ -663,30 +665,18 @@ __global__ __launch_bounds__(64) void forward_kernel(ModelT<T> mg, Dev d, const 
   if (ncon) { ncon[2 * e] = so.ng; ncon[2 * e + 1] = so.nb; }
 }
 
-// Which envs should take the full kernel this step: a base-tree geom within a
-// margin of the ball or of a heightfield vertex under it (the fast kernel's
-// exact per-stage test stays the arbiter; this only routes work).  One
-// 16-lane team per env (4 per wave): the per-geom setup is replicated, the
-// cells under each geom's grown AABB are dealt over the lanes and the hits
-// reduced with a ballot.  (One lane per env was 64 waves walking ~230 cells
-// each: 93 us per step on perlin, on the critical path of the full kernel.)
+// The predictor's test for one env (a 16-lane team, lane tl; team_shift = the
+// team's first lane in the wave): may a base-tree geom come within one step's
+// reach of the ball or of a heightfield prism under it?  Team-uniform result.
 template <typename T>
-__global__ __launch_bounds__(64) void predict_kernel(ModelT<T> mg, Dev d) {
-  __shared__ ModelT<T> ms;
-  if (threadIdx.x == 0) ms = mg;
-  __syncthreads();
-  const ModelT<T>& m = ms;
+__device__ __forceinline__ bool predict_env(const ModelT<T>& m, const Dev& d, int tid, const T* Qe, const T* Ve,
+                                            int tl, int team_shift) {
   constexpr int PL = 16;
-  const int tl = int(threadIdx.x) & (PL - 1), team_shift = int(threadIdx.x) & ~(PL - 1);
-  const int e = blockIdx.x * (WAVE / PL) + int(threadIdx.x) / PL;
-  if (e >= d.n) return;  // team-uniform
-  const T* Q = (const T*)d.qpos;
-  const T* V = (const T*)d.qvel;
   T pb[3], qb[4], pB[3], qB[4];
 #pragma unroll
-  for (int i = 0; i < 3; i++) { pb[i] = Q[i * d.n + e]; pB[i] = Q[(10 + i) * d.n + e]; }
+  for (int i = 0; i < 3; i++) { pb[i] = Qe[i]; pB[i] = Qe[10 + i]; }
 #pragma unroll
-  for (int i = 0; i < 4; i++) { qb[i] = Q[(3 + i) * d.n + e]; qB[i] = Q[(13 + i) * d.n + e]; }
+  for (int i = 0; i < 4; i++) { qb[i] = Qe[3 + i]; qB[i] = Qe[13 + i]; }
   qnormalize(qb);
   qnormalize(qB);
   T Rb[9], RB[9];
@@ -695,13 +685,12 @@ __global__ __launch_bounds__(64) void predict_kernel(ModelT<T> mg, Dev d) {
   T vb = 0, wb = 0;
 #pragma unroll
   for (int i = 0; i < 3; i++) {
-    const T a = V[i * d.n + e], b = V[(3 + i) * d.n + e];
+    const T a = Ve[i], b = Ve[3 + i];
     vb += a * a; wb += b * b;
   }
   // one step's reach of any geom point (|v| + 0.5 m |w|) h, x3, + 1 cm
   const T margin = T(3) * m.h * (sqrt(vb) + T(0.5) * sqrt(wb)) + T(0.01);
   const T cB[3] = {pB[0] + RB[2] * m.dz, pB[1] + RB[5] * m.dz, pB[2] + RB[8] * m.dz};  // ball centre
-  const int tid = d.terrain[e];
   const float* hf = d.bank + size_t(tid) * (HF_N * HF_N);
   const T size_z = T(d.size_z[tid]), hz = T(d.hmax[tid]) * size_z;
   bool slow = false;
@@ -793,7 +782,162 @@ __global__ __launch_bounds__(64) void predict_kernel(ModelT<T> mg, Dev d) {
     (void)team_shift; slow = hit;
 #endif
   }
+  return slow;
+}
+
+// Which envs should take the full kernel this step: a base-tree geom within a
+// margin of the ball or of a heightfield vertex under it (the fast kernel's
+// exact per-stage test stays the arbiter; this only routes work).  One
+// 16-lane team per env (4 per wave): the per-geom setup is replicated, the
+// cells under each geom's grown AABB are dealt over the lanes and the hits
+// reduced with a ballot.  (One lane per env was 64 waves walking ~230 cells
+// each: 93 us per step on perlin, on the critical path of the full kernel.)
+template <typename T>
+__global__ __launch_bounds__(64) void predict_kernel(ModelT<T> mg, Dev d) {
+  __shared__ ModelT<T> ms;
+  if (threadIdx.x == 0) ms = mg;
+  __syncthreads();
+  const ModelT<T>& m = ms;
+  constexpr int PL = 16;
+  const int tl = int(threadIdx.x) & (PL - 1), team_shift = int(threadIdx.x) & ~(PL - 1);
+  const int e = blockIdx.x * (WAVE / PL) + int(threadIdx.x) / PL;
+  if (e >= d.n) return;  // team-uniform
+  const T* Q = (const T*)d.qpos;
+  const T* V = (const T*)d.qvel;
+  T Qe[NQ], Ve[6];
+#pragma unroll
+  for (int i = 0; i < NQ; i++) Qe[i] = Q[i * d.n + e];
+#pragma unroll
+  for (int i = 0; i < 6; i++) Ve[i] = V[i * d.n + e];
+  const bool slow = predict_env<T>(m, d, d.terrain[e], Qe, Ve, tl, team_shift);
   if (tl == 0) d.pred_mark[e] = slow ? 1 : 0;
+}
+
+// K steps of every env in one launch on relief banks (bb_step_multi, route 0):
+// a work queue inside each workgroup.  A workgroup of QW waves owns QENV envs
+// (their EnvWork in its LDS).  Each wave repeatedly claims up to 4 envs whose
+// next step is due and that the predictor routes the same way -- all fast or
+// all full -- and steps them, so a wave never runs the fast and the full
+// step one after the other for different teams (the divergence that costs
+// multi_step_kernel its gain on relief).  Per env the result is route 0's:
+// predicted envs take the full step, the others the fast path with the
+// hand-over.  The claims are under an LDS spin lock held by one lane of the
+// claiming wave; a workgroup ends when its QENV x K env-steps are done, which
+// every wave observes.
+constexpr int QW = 4, QENV = 4 * QW;
+
+template <typename T>
+__global__ __launch_bounds__(64 * QW) void relief_multi_kernel(ModelT<T> mg, EnvCfg cfg, Dev d,
+                                                               const float* __restrict__ act, int K,
+                                                               float* __restrict__ obs, float* __restrict__ rew,
+                                                               uint8_t* __restrict__ done, float* __restrict__ tobs,
+                                                               float* __restrict__ pos2d, int auto_reset) {
+  extern __shared__ __align__(16) unsigned char smem[];
+  __shared__ ModelT<T> ms;
+  __shared__ int s_k[QENV], s_busy[QENV], s_kind[QENV], s_tid[QENV], s_step[QENV];
+  __shared__ int s_claim[QW][4], s_fin[QW];
+  __shared__ int s_lock, s_left;
+  const int nwg = int(gridDim.x), b = int(blockIdx.x);
+  const int g = (nwg & 7) ? b : (b & 7) * (nwg >> 3) + (b >> 3);
+  const int e0 = g * QENV;
+  const int nloc = min(QENV, d.n - e0);
+  if (nloc <= 0) return;  // workgroup-uniform
+  const int wave = int(threadIdx.x) >> 6, lane = int(threadIdx.x) & 63;
+  const Team tm{16, lane & 15};
+  const int team = lane >> 4;
+  const bool lead = tm.tl == 0;
+  const size_t n = size_t(d.n);
+  T* bk0 = reinterpret_cast<T*>(smem + size_t(QENV) * work_stride<T>());
+  if (threadIdx.x == 0) {
+    ms = mg;
+    s_lock = 0;
+    s_left = nloc * K;
+  }
+  if (int(threadIdx.x) < nloc) {
+    const int i = int(threadIdx.x), e = e0 + i;
+    EnvWork<T>& W = team_work<T>(smem, i);
+    int step;
+    load_state(d, e, W.qn, W.vn, W.wn, step);
+    W.bspill = body_spill_of<T>(d, e);
+    s_k[i] = 0;
+    s_busy[i] = 0;
+    s_tid[i] = d.terrain[e];
+    s_step[i] = step;
+  }
+  __syncthreads();
+  const ModelT<T>& m = ms;
+  {  // the first step's routes: wave w predicts envs 4w .. 4w + 3
+    const int i = 4 * wave + team;
+    if (i < nloc) {
+      EnvWork<T>& W = team_work<T>(smem, i);
+      const bool sl = predict_env<T>(m, d, s_tid[i], W.qn, W.vn, tm.tl, lane & ~15);
+      if (lead) s_kind[i] = sl ? 1 : 0;
+    }
+  }
+  __syncthreads();
+#pragma unroll 1
+  for (;;) {
+    if (lane == 0) {
+      while (atomicCAS(&s_lock, 0, 1) != 0) __builtin_amdgcn_s_sleep(1);
+      int nf = 0, ns = 0;
+      for (int i = 0; i < nloc; i++)
+        if (!s_busy[i] && s_k[i] < K) (s_kind[i] ? ns : nf)++;
+      // full steps first when a whole wave of them is due (they are the long
+      // ones), else whole waves of fast steps, else the larger group
+      const int kind = ns >= 4 ? 1 : (nf >= 4 ? 0 : (ns >= nf ? 1 : 0));
+      int c = 0;
+      for (int i = 0; i < nloc && c < 4; i++)
+        if (!s_busy[i] && s_k[i] < K && s_kind[i] == kind) { s_busy[i] = 1; s_claim[wave][c++] = i; }
+      for (; c < 4; c++) s_claim[wave][c] = -1;
+      s_fin[wave] = s_left == 0;
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+      atomicExch(&s_lock, 0);
+    }
+    team_sync();  // the wave's lanes see lane 0's claims
+    if (s_fin[wave]) break;
+    const int i = s_claim[wave][team];
+    if (s_claim[wave][0] < 0) {  // nothing due that is not being stepped (wave-uniform)
+      __builtin_amdgcn_s_sleep(2);
+      continue;
+    }
+    if (i >= 0) {
+      EnvWork<T>& W = team_work<T>(smem, i);
+      T* bk = bk0 + i * (NQ + 2 * NV);
+      const int e = e0 + i, k = s_k[i];
+      const size_t row = size_t(k) * n + e;
+      int tid = s_tid[i], step = s_step[i];
+      const bool full = s_kind[i] != 0;
+      const float* ak = act + 3 * row;
+      const float a[3] = {ak[0], ak[1], ak[2]};
+      float o[15], r;
+      const int fl = team_step<T>(m, cfg, d, e, tid, W.qn, W.vn, W.wn, step, bk, a, W, o, r,
+                                  tobs ? tobs + 15 * row : nullptr, pos2d ? pos2d + 2 * row : nullptr, auto_reset,
+                                  tm, full);
+      if (lead) {
+#pragma unroll
+        for (int j = 0; j < 15; j++) obs[15 * row + j] = o[j];
+        rew[row] = r;
+        done[row] = uint8_t(fl);
+      }
+      const bool next = k + 1 < K && predict_env<T>(m, d, tid, W.qn, W.vn, tm.tl, lane & ~15);
+      team_sync();
+      if (lead) {
+        s_tid[i] = tid;
+        s_step[i] = step;
+        s_kind[i] = next ? 1 : 0;
+        s_k[i] = k + 1;
+        atomicSub(&s_left, 1);
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+        s_busy[i] = 0;
+      }
+    }
+  }
+  __syncthreads();
+  if (int(threadIdx.x) < nloc) {
+    const int i = int(threadIdx.x);
+    EnvWork<T>& W = team_work<T>(smem, i);
+    store_state(d, e0 + i, W.qn, W.vn, W.wn, s_step[i]);
+  }
 }
 
 // Stable split of 0..n-1 by pred_mark into fast_envs / pred_envs (one block).
@@ -859,6 +1003,7 @@ struct bb_handle {
   // flat banks hand-overs are rare and the serial route saves the predict and
   // split launches (3.66 M vs 3.57 M env-steps/s at 4096 flat envs)
   int route = -1;
+  int multi_queue = 1;          // bb_step_multi on relief banks: relief_multi_kernel (BB_MULTI_QUEUE=0: off)
   std::vector<uint8_t> relief;  // per terrain: max height > 0
   int n_relief = 0;
   int* tstream = nullptr;       // device copies of the terrain streams (bb_set_terrain_stream)
@@ -956,6 +1101,10 @@ int launch_rollout(bb_handle* h, const RolloutDev& ro, hipStream_t s) {
   return 0;
 }
 
+// dynamic LDS of relief_multi_kernel: QENV EnvWork + their step-start copies
+template <typename T>
+size_t relief_lds_bytes() { return lds_bytes<T>(QENV) + size_t(QENV) * (NQ + 2 * NV) * sizeof(T); }
+
 template <typename T>
 int launch_multi(bb_handle* h, const float* a, int K, float* o, float* r, uint8_t* dn, float* t, float* p2, int ar,
                  hipStream_t s) {
@@ -963,9 +1112,14 @@ int launch_multi(bb_handle* h, const float* a, int K, float* o, float* r, uint8_
   const int blocks = (h->n + epw - 1) / epw;
   const bool timed = h->tn < h->tcap;
   hipEvent_t* ev = timed ? &h->tev[6 * h->tn] : nullptr;
+  const int route = h->route >= 0 ? h->route : (h->n_relief == 0 ? 1 : 0);
   if (timed) HIPCHK(hipEventRecord(ev[0], s));
-  hipLaunchKernelGGL(multi_step_kernel<T>, dim3(blocks), dim3(WAVE), multi_lds_bytes<T>(epw), s, model_of<T>(h),
-                     h->cfg, h->d, a, K, o, r, dn, t, p2, ar, h->team, epw);
+  if (route == 0 && h->team == 16 && h->multi_queue)  // relief banks: the per-workgroup work queue
+    hipLaunchKernelGGL(relief_multi_kernel<T>, dim3((h->n + QENV - 1) / QENV), dim3(64 * QW), relief_lds_bytes<T>(), s,
+                       model_of<T>(h), h->cfg, h->d, a, K, o, r, dn, t, p2, ar);
+  else
+    hipLaunchKernelGGL(multi_step_kernel<T>, dim3(blocks), dim3(WAVE), multi_lds_bytes<T>(epw), s, model_of<T>(h),
+                       h->cfg, h->d, a, K, o, r, dn, t, p2, ar, h->team, epw);
   if (timed) {
     HIPCHK(hipEventRecord(ev[1], s));
     HIPCHK(hipEventRecord(ev[5], s));
@@ -1053,6 +1207,8 @@ int bb_create(int n_envs, int device, const bb_params* p, bb_handle** out) {
     h->epw_full = epf;
     const char* rt = getenv("BB_ROUTE");
     if (rt) h->route = atoi(rt);
+    const char* mq = getenv("BB_MULTI_QUEUE");
+    if (mq) h->multi_queue = atoi(mq) != 0;
   }
   h->md = compile_model(sc);
   h->mf = cast_model<float>(h->md);
@@ -1125,6 +1281,9 @@ int bb_create(int n_envs, int device, const bb_params* p, bb_handle** out) {
     const void* rk = h->fp64 ? (const void*)rollout_kernel<double> : (const void*)rollout_kernel<float>;
     const int rlb = (int)(h->fp64 ? rollout_lds_bytes<double>(h->epw) : rollout_lds_bytes<float>(h->epw));
     HIPCHK(hipFuncSetAttribute(rk, hipFuncAttributeMaxDynamicSharedMemorySize, rlb));
+    const void* qk = h->fp64 ? (const void*)relief_multi_kernel<double> : (const void*)relief_multi_kernel<float>;
+    const int qlb = (int)(h->fp64 ? relief_lds_bytes<double>() : relief_lds_bytes<float>());
+    HIPCHK(hipFuncSetAttribute(qk, hipFuncAttributeMaxDynamicSharedMemorySize, qlb));
   }
   *out = h;
   int rc = bb_reset(h, nullptr, nullptr, nullptr);

@@ -66,7 +66,18 @@ BB_HD T team_sum(const Team& tm, T v) {
 
 BB_HD void team_sync() {
 #ifdef __HIP_DEVICE_COMPILE__
-  __syncthreads();  // one 64-lane wave per workgroup: orders LDS traffic inside the wave
+#ifdef BB_SYNC_BARRIER
+  __syncthreads();
+#else
+  // orders the wave's LDS traffic across its lanes.  A team lives inside one
+  // wave, whose lanes execute together and whose LDS operations complete in
+  // order, so a workgroup fence (wait for the wave's LDS operations) and a
+  // compiler barrier are enough -- no s_barrier, which in a multi-wave
+  // workgroup (relief_multi_kernel) would also wait for the other waves.
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+#endif
 #endif
 }
 

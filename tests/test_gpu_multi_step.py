@@ -87,7 +87,7 @@ def test_multi_step_perlin_hand_overs_match(route, monkeypatch):
     # rough perlin: most robots fall for ~140 steps from the reset height, then land and topple
     # (base-tree contacts); episodes end by tilt or at 200 steps
     actions = torch.rand(256, n, 3, generator=g, device="cuda:0") * 2 - 1
-    st = _compare_runs(a, b, actions, 32, exact=route == "1")
+    st = _compare_runs(a, b, actions, 32)  # route 0: relief_multi_kernel (predictor + work queue), route 1: multi_step_kernel
     assert st["slow_path"] > 0  # base-tree contacts: the inline full step ran
     assert st["resets"] > 0
     a.close(), b.close()
