@@ -316,7 +316,10 @@ def main() -> None:
                          "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
                          "note": "latency/VALU-bound per-lane physics; HBM bytes = algorithmic state I/O "
                                  f"({algorithmic_bytes(args.precision)} B/env-step) x the envs the kernel stepped",
-                         "kernel": (f"multi_step_kernel<T> ({M} steps per launch)" if M else
+                         "kernel": ((f"relief_multi_kernel<T> (work queue, {M} steps per launch)" if env.relief
+                                     and os.environ.get("BB_MULTI_QUEUE", "1") != "0" and
+                                     os.environ.get("BB_ROUTE", "0") == "0"
+                                     else f"multi_step_kernel<T> ({M} steps per launch)") if M else
                                     "step_kernel<T,false> (fast path)" if dom == "fast"
                                     else "step_kernel<T,true> (predicted full kernel, side stream)"),
                          "kernel_ms": kern_ms, "envs_per_launch": envs_dom, "kernel_ms_all": ktimes,

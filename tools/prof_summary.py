@@ -34,7 +34,8 @@ def select_ids(recs):
     hand-over full kernel comes after it)."""
     recs = sorted(recs, key=lambda r: int(r["Dispatch_Id"]))
     if SEL["which"] == "multi":
-        return [int(r["Dispatch_Id"]) for r in recs if "multi_step_kernel" in r["Kernel_Name"]]
+        return [int(r["Dispatch_Id"]) for r in recs
+                if "multi_step_kernel" in r["Kernel_Name"] or "relief_multi_kernel" in r["Kernel_Name"]]
     if SEL["which"] == "fast":
         return [int(r["Dispatch_Id"]) for r in recs if is_fast(r["Kernel_Name"])]
     out, last_full = [], None
