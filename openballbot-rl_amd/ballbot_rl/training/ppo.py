@@ -708,9 +708,9 @@ class BatchedPPO:
         T, n = self.n_steps, self.n_envs
         if self._last_obs is None:
             self._last_obs, _ = env.reset()
-        # bb_rollout on flat banks (default); on relief banks the per-step rollout keeps the
-        # predicted full kernel beside the fast one (bb_rollout's hand-overs run inline and
-        # diverge inside a wave: perlin 4.97 M against 5.15 M rollout env-steps/s)
+        # the whole rollout as one bb_rollout launch on flat banks; on relief banks the per-step
+        # rollout measured faster (perlin PPO, shared terrain stream: 5.13 M rollout env-steps/s
+        # against 4.78 M with bb_rollout's work queue).  BB_FUSED_ROLLOUT=1/0 forces either.
         fr = os.environ.get("BB_FUSED_ROLLOUT", "auto")
         if (hasattr(env, "run_rollout") and getattr(env, "_host_reward", None) is None and fr != "0"
                 and (fr == "1" or not getattr(env, "relief", True))):

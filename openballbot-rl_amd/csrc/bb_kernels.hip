@@ -826,17 +826,26 @@ __global__ __launch_bounds__(64) void predict_kernel(ModelT<T> mg, Dev d) {
 // every wave observes.
 constexpr int QW = 4, QENV = 4 * QW;
 
-template <typename T>
+// RO: the whole PPO rollout (bb_rollout) instead of open-loop steps: each
+// claimed env runs one (policy, sample, clip, step, bookkeeping) step as
+// rollout_kernel does; its observation and episode counters wait in LDS
+// between claims.
+template <typename T, bool RO>
 __global__ __launch_bounds__(64 * QW) void relief_multi_kernel(ModelT<T> mg, EnvCfg cfg, Dev d,
                                                                const float* __restrict__ act, int K,
                                                                float* __restrict__ obs, float* __restrict__ rew,
                                                                uint8_t* __restrict__ done, float* __restrict__ tobs,
-                                                               float* __restrict__ pos2d, int auto_reset) {
+                                                               float* __restrict__ pos2d, int auto_reset, RolloutDev ro) {
   extern __shared__ __align__(16) unsigned char smem[];
   __shared__ ModelT<T> ms;
   __shared__ int s_k[QENV], s_busy[QENV], s_kind[QENV], s_tid[QENV], s_step[QENV];
   __shared__ int s_claim[QW][4], s_fin[QW];
   __shared__ int s_lock, s_left;
+  // RO: per env the observation, episode start and Monitor counters between claims
+  __shared__ float s_obs[RO ? QENV : 1][15];
+  __shared__ int s_start[RO ? QENV : 1];
+  __shared__ double s_ret[RO ? QENV : 1];
+  __shared__ long long s_len[RO ? QENV : 1];
   const int nwg = int(gridDim.x), b = int(blockIdx.x);
   const int g = (nwg & 7) ? b : (b & 7) * (nwg >> 3) + (b >> 3);
   const int e0 = g * QENV;
@@ -863,6 +872,13 @@ __global__ __launch_bounds__(64 * QW) void relief_multi_kernel(ModelT<T> mg, Env
     s_busy[i] = 0;
     s_tid[i] = d.terrain[e];
     s_step[i] = step;
+    if (RO) {
+#pragma unroll
+      for (int j = 0; j < 15; j++) s_obs[i][j] = ro.obs[15 * size_t(e) + j];
+      s_start[i] = ro.last_starts[e];
+      s_ret[i] = ro.ep_ret[e];
+      s_len[i] = ro.ep_len[e];
+    }
   }
   __syncthreads();
   const ModelT<T>& m = ms;
@@ -907,17 +923,59 @@ __global__ __launch_bounds__(64 * QW) void relief_multi_kernel(ModelT<T> mg, Env
       const size_t row = size_t(k) * n + e;
       int tid = s_tid[i], step = s_step[i];
       const bool full = s_kind[i] != 0;
-      const float* ak = act + 3 * row;
-      const float a[3] = {ak[0], ak[1], ak[2]};
-      float o[15], r;
-      const int fl = team_step<T>(m, cfg, d, e, tid, W.qn, W.vn, W.wn, step, bk, a, W, o, r,
-                                  tobs ? tobs + 15 * row : nullptr, pos2d ? pos2d + 2 * row : nullptr, auto_reset,
-                                  tm, full);
-      if (lead) {
+      float a[3], o[15], r;
+      if (RO) {
+        // the policy step of rollout_kernel (scratch: the env's contact stores)
+        float* x = reinterpret_cast<float*>(W.g);
+        if (tm.tl < 15) x[tm.tl] = s_obs[i][tm.tl];
+        team_sync();
+        float mu[3] = {0.f, 0.f, 0.f}, val = 0.f;
+        team_policy(ro.P, ro.off, x, x + 16, x + 144, tm, mu, val);
+        const float* ls = ro.P + ro.off[MLP_LS];
+        float lp = 0.f, araw[3];
 #pragma unroll
-        for (int j = 0; j < 15; j++) obs[15 * row + j] = o[j];
-        rew[row] = r;
-        done[row] = uint8_t(fl);
+        for (int j = 0; j < 3; j++) {
+          const float ls_j = ls[j];
+          araw[j] = __fadd_rn(mu[j], __fmul_rn(ro.noise[3 * row + j], expf(ls_j)));
+          const float z = __fmul_rn(__fsub_rn(araw[j], mu[j]), expf(-ls_j));
+          lp += -0.5f * z * z - ls_j - 0.5f * (2.f * 0.91893853320467274f);
+          a[j] = fminf(fmaxf(araw[j], -1.f), 1.f);
+        }
+        if (lead) {
+#pragma unroll
+          for (int j = 0; j < 15; j++) ro.b_obs[15 * row + j] = s_obs[i][j];
+#pragma unroll
+          for (int j = 0; j < 3; j++) ro.b_act[3 * row + j] = araw[j];
+          ro.b_val[row] = val;
+          ro.b_logp[row] = lp;
+          ro.b_starts[row] = uint8_t(s_start[i]);
+        }
+      } else {
+        const float* ak = act + 3 * row;
+        a[0] = ak[0]; a[1] = ak[1]; a[2] = ak[2];
+      }
+      const int fl = team_step<T>(m, cfg, d, e, tid, W.qn, W.vn, W.wn, step, bk, a, W, o, r,
+                                  (!RO && tobs) ? tobs + 15 * row : nullptr, (!RO && pos2d) ? pos2d + 2 * row : nullptr,
+                                  RO ? 1 : auto_reset, tm, full);
+      if (lead) {
+        if (RO) {  // collect_rollouts + Monitor bookkeeping (bb_rollout_track)
+          const bool dn = (fl & F_TERMINATED) != 0;
+          const double ret = s_ret[i] + double(r);
+          const long long len = s_len[i] + 1;
+          ro.b_rew[row] = r;
+          ro.ep_r[row] = dn ? ret : __builtin_nan("");
+          ro.ep_l[row] = dn ? len : 0;
+          s_ret[i] = dn ? 0.0 : ret;
+          s_len[i] = dn ? 0 : len;
+          s_start[i] = dn ? 1 : 0;
+#pragma unroll
+          for (int j = 0; j < 15; j++) s_obs[i][j] = o[j];
+        } else {
+#pragma unroll
+          for (int j = 0; j < 15; j++) obs[15 * row + j] = o[j];
+          rew[row] = r;
+          done[row] = uint8_t(fl);
+        }
       }
       const bool next = k + 1 < K && predict_env<T>(m, d, tid, W.qn, W.vn, tm.tl, lane & ~15);
       team_sync();
@@ -934,9 +992,16 @@ __global__ __launch_bounds__(64 * QW) void relief_multi_kernel(ModelT<T> mg, Env
   }
   __syncthreads();
   if (int(threadIdx.x) < nloc) {
-    const int i = int(threadIdx.x);
+    const int i = int(threadIdx.x), e = e0 + i;
     EnvWork<T>& W = team_work<T>(smem, i);
-    store_state(d, e0 + i, W.qn, W.vn, W.wn, s_step[i]);
+    store_state(d, e, W.qn, W.vn, W.wn, s_step[i]);
+    if (RO) {
+#pragma unroll
+      for (int j = 0; j < 15; j++) ro.obs[15 * size_t(e) + j] = s_obs[i][j];
+      ro.last_starts[e] = uint8_t(s_start[i]);
+      ro.ep_ret[e] = s_ret[i];
+      ro.ep_len[e] = s_len[i];
+    }
   }
 }
 
@@ -1087,6 +1152,10 @@ int launch_step(bb_handle* h, const float* a, float* o, float* r, uint8_t* dn, f
 template <typename T>
 size_t multi_lds_bytes(int epw) { return lds_bytes<T>(epw) + size_t(epw) * (NQ + 2 * NV) * sizeof(T); }
 
+// dynamic LDS of relief_multi_kernel: QENV EnvWork + their step-start copies
+template <typename T>
+size_t relief_lds_bytes() { return lds_bytes<T>(QENV) + size_t(QENV) * (NQ + 2 * NV) * sizeof(T); }
+
 // dynamic LDS of rollout_kernel: multi_step_kernel's (the policy scratch lives in EnvWork)
 template <typename T>
 size_t rollout_lds_bytes(int epw) { return multi_lds_bytes<T>(epw); }
@@ -1095,15 +1164,17 @@ template <typename T>
 int launch_rollout(bb_handle* h, const RolloutDev& ro, hipStream_t s) {
   const int epw = h->epw;
   const int blocks = (h->n + epw - 1) / epw;
-  hipLaunchKernelGGL(rollout_kernel<T>, dim3(blocks), dim3(WAVE), rollout_lds_bytes<T>(epw), s, model_of<T>(h),
-                     h->cfg, h->d, ro, h->team, epw);
+  const int route = h->route >= 0 ? h->route : (h->n_relief == 0 ? 1 : 0);
+  if (route == 0 && h->team == 16 && h->multi_queue)  // relief banks: the work queue with the policy in it
+    hipLaunchKernelGGL((relief_multi_kernel<T, true>), dim3((h->n + QENV - 1) / QENV), dim3(64 * QW),
+                       relief_lds_bytes<T>(), s, model_of<T>(h), h->cfg, h->d, (const float*)nullptr, ro.T,
+                       (float*)nullptr, (float*)nullptr, (uint8_t*)nullptr, (float*)nullptr, (float*)nullptr, 1, ro);
+  else
+    hipLaunchKernelGGL(rollout_kernel<T>, dim3(blocks), dim3(WAVE), rollout_lds_bytes<T>(epw), s, model_of<T>(h),
+                       h->cfg, h->d, ro, h->team, epw);
   HIPCHK(hipGetLastError());
   return 0;
 }
-
-// dynamic LDS of relief_multi_kernel: QENV EnvWork + their step-start copies
-template <typename T>
-size_t relief_lds_bytes() { return lds_bytes<T>(QENV) + size_t(QENV) * (NQ + 2 * NV) * sizeof(T); }
 
 template <typename T>
 int launch_multi(bb_handle* h, const float* a, int K, float* o, float* r, uint8_t* dn, float* t, float* p2, int ar,
@@ -1115,8 +1186,8 @@ int launch_multi(bb_handle* h, const float* a, int K, float* o, float* r, uint8_
   const int route = h->route >= 0 ? h->route : (h->n_relief == 0 ? 1 : 0);
   if (timed) HIPCHK(hipEventRecord(ev[0], s));
   if (route == 0 && h->team == 16 && h->multi_queue)  // relief banks: the per-workgroup work queue
-    hipLaunchKernelGGL(relief_multi_kernel<T>, dim3((h->n + QENV - 1) / QENV), dim3(64 * QW), relief_lds_bytes<T>(), s,
-                       model_of<T>(h), h->cfg, h->d, a, K, o, r, dn, t, p2, ar);
+    hipLaunchKernelGGL((relief_multi_kernel<T, false>), dim3((h->n + QENV - 1) / QENV), dim3(64 * QW),
+                       relief_lds_bytes<T>(), s, model_of<T>(h), h->cfg, h->d, a, K, o, r, dn, t, p2, ar, RolloutDev{});
   else
     hipLaunchKernelGGL(multi_step_kernel<T>, dim3(blocks), dim3(WAVE), multi_lds_bytes<T>(epw), s, model_of<T>(h),
                        h->cfg, h->d, a, K, o, r, dn, t, p2, ar, h->team, epw);
@@ -1281,9 +1352,12 @@ int bb_create(int n_envs, int device, const bb_params* p, bb_handle** out) {
     const void* rk = h->fp64 ? (const void*)rollout_kernel<double> : (const void*)rollout_kernel<float>;
     const int rlb = (int)(h->fp64 ? rollout_lds_bytes<double>(h->epw) : rollout_lds_bytes<float>(h->epw));
     HIPCHK(hipFuncSetAttribute(rk, hipFuncAttributeMaxDynamicSharedMemorySize, rlb));
-    const void* qk = h->fp64 ? (const void*)relief_multi_kernel<double> : (const void*)relief_multi_kernel<float>;
     const int qlb = (int)(h->fp64 ? relief_lds_bytes<double>() : relief_lds_bytes<float>());
-    HIPCHK(hipFuncSetAttribute(qk, hipFuncAttributeMaxDynamicSharedMemorySize, qlb));
+    const void* qk[2] = {h->fp64 ? (const void*)relief_multi_kernel<double, false>
+                                 : (const void*)relief_multi_kernel<float, false>,
+                         h->fp64 ? (const void*)relief_multi_kernel<double, true>
+                                 : (const void*)relief_multi_kernel<float, true>};
+    for (const void* k : qk) HIPCHK(hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, qlb));
   }
   *out = h;
   int rc = bb_reset(h, nullptr, nullptr, nullptr);

@@ -67,10 +67,12 @@ def test_rollout_policy_matches_mlp_act():
     env.close()
 
 
-@pytest.mark.parametrize("terrain", ["flat", "perlin"])
-def test_rollout_steps_replay_bit_exact(terrain, monkeypatch):
-    """The kernel's env steps == bb_step (serial route) on the kernel's own clipped actions."""
-    monkeypatch.setenv("BB_ROUTE", "1")  # the twin env's bb_step: fast path, hand-over to the full kernel
+@pytest.mark.parametrize("terrain,route", [("flat", "1"), ("perlin", "1"), ("perlin", "0")])
+def test_rollout_steps_replay_bit_exact(terrain, route, monkeypatch):
+    """The kernel's env steps == bb_step on the kernel's own clipped actions.  Route 1 (fast
+    path, hand-over): rollout_kernel; route 0 on perlin (predictor): the relief work queue
+    with the policy in it."""
+    monkeypatch.setenv("BB_ROUTE", route)
     n, T = (1024, 64) if terrain == "flat" else (256, 96)
     kw = {"max_ep_steps": 30} if terrain == "flat" else {"n_terrains": None, "max_ep_steps": 200,
                                                           "stream_seeds": [70 + i for i in range(256)]}
