@@ -87,6 +87,8 @@ struct Dev {
   int* pred_envs;             // envs predicted to need base-tree contacts (full kernel, concurrent)
   uint8_t* pred_mark;
   void* body_spill;           // T[n][MAXB - MAXB_LDS][NBF]: base-tree contacts past the LDS slots
+  int* perm;                  // relief_multi_kernel: env of each workgroup slot (balance_kernel), NULL: identity
+  unsigned long long* cost;   // relief_multi_kernel: shader cycles each env's steps took in the last launch
 };
 
 // env e's spill block for base-tree contacts MAXB_LDS..MAXB-1
@@ -838,7 +840,7 @@ __global__ __launch_bounds__(64 * QW) void relief_multi_kernel(ModelT<T> mg, Env
                                                                float* __restrict__ pos2d, int auto_reset, RolloutDev ro) {
   extern __shared__ __align__(16) unsigned char smem[];
   __shared__ ModelT<T> ms;
-  __shared__ int s_k[QENV], s_busy[QENV], s_kind[QENV], s_tid[QENV], s_step[QENV];
+  __shared__ int s_k[QENV], s_busy[QENV], s_kind[QENV], s_tid[QENV], s_step[QENV], s_env[QENV];
   __shared__ int s_claim[QW][4], s_fin[QW];
   __shared__ int s_lock, s_left;
   // RO: per env the observation, episode start and Monitor counters between claims
@@ -863,11 +865,12 @@ __global__ __launch_bounds__(64 * QW) void relief_multi_kernel(ModelT<T> mg, Env
     s_left = nloc * K;
   }
   if (int(threadIdx.x) < nloc) {
-    const int i = int(threadIdx.x), e = e0 + i;
+    const int i = int(threadIdx.x), e = d.perm ? d.perm[e0 + i] : e0 + i;
     EnvWork<T>& W = team_work<T>(smem, i);
     int step;
     load_state(d, e, W.qn, W.vn, W.wn, step);
     W.bspill = body_spill_of<T>(d, e);
+    s_env[i] = e;
     s_k[i] = 0;
     s_busy[i] = 0;
     s_tid[i] = d.terrain[e];
@@ -919,10 +922,11 @@ __global__ __launch_bounds__(64 * QW) void relief_multi_kernel(ModelT<T> mg, Env
     if (i >= 0) {
       EnvWork<T>& W = team_work<T>(smem, i);
       T* bk = bk0 + i * (NQ + 2 * NV);
-      const int e = e0 + i, k = s_k[i];
+      const int e = s_env[i], k = s_k[i];
       const size_t row = size_t(k) * n + e;
       int tid = s_tid[i], step = s_step[i];
       const bool full = s_kind[i] != 0;
+      const unsigned long long c0 = clock64();
       float a[3], o[15], r;
       if (RO) {
         // the policy step of rollout_kernel (scratch: the env's contact stores)
@@ -980,6 +984,7 @@ __global__ __launch_bounds__(64 * QW) void relief_multi_kernel(ModelT<T> mg, Env
       const bool next = k + 1 < K && predict_env<T>(m, d, tid, W.qn, W.vn, tm.tl, lane & ~15);
       team_sync();
       if (lead) {
+        if (d.cost) d.cost[e] += clock64() - c0;  // this env's cost, for the next launch's balance
         s_tid[i] = tid;
         s_step[i] = step;
         s_kind[i] = next ? 1 : 0;
@@ -992,7 +997,7 @@ __global__ __launch_bounds__(64 * QW) void relief_multi_kernel(ModelT<T> mg, Env
   }
   __syncthreads();
   if (int(threadIdx.x) < nloc) {
-    const int i = int(threadIdx.x), e = e0 + i;
+    const int i = int(threadIdx.x), e = s_env[i];
     EnvWork<T>& W = team_work<T>(smem, i);
     store_state(d, e, W.qn, W.vn, W.wn, s_step[i]);
     if (RO) {
@@ -1003,6 +1008,46 @@ __global__ __launch_bounds__(64 * QW) void relief_multi_kernel(ModelT<T> mg, Env
       ro.ep_len[e] = s_len[i];
     }
   }
+}
+
+// Between relief_multi_kernel launches: deal the envs over its workgroups so
+// that each gets a mix of expensive and cheap ones.  An env's cost in the
+// last launch (shader cycles of its steps) predicts the next one well (its
+// terrain and posture persist for many steps), and a workgroup runs until its
+// last env is done: without this, whole CUs idled for ~40% of a perlin launch
+// while the workgroups holding toppled robots finished.  One workgroup: a
+// 1024-bucket counting sort of the costs (scaled to the maximum), then a
+// snake deal (round r of the sorted envs goes to workgroups 0..nwg-1, the next
+// round back), and the costs restart from 0.  n must be nwg * QENV.
+__global__ __launch_bounds__(1024) void balance_kernel(Dev d, int nwg) {
+  constexpr int NB = 1024;
+  __shared__ unsigned long long s_max;
+  __shared__ int hist[NB];
+  const int t = int(threadIdx.x), n = d.n;
+  if (t == 0) s_max = 1;
+  hist[t] = 0;
+  __syncthreads();
+  unsigned long long mx = 1;
+  for (int e = t; e < n; e += NB) mx = d.cost[e] > mx ? d.cost[e] : mx;
+  atomicMax(&s_max, mx);
+  __syncthreads();
+  const unsigned long long top = s_max;
+  auto bucket = [&](int e) { return int((d.cost[e] * (NB - 1)) / top); };
+  for (int e = t; e < n; e += NB) atomicAdd(&hist[NB - 1 - bucket(e)], 1);  // descending cost
+  __syncthreads();
+  if (t == 0) {  // exclusive scan (1024 entries, once per launch)
+    int acc = 0;
+    for (int b = 0; b < NB; b++) { const int c = hist[b]; hist[b] = acc; acc += c; }
+  }
+  __syncthreads();
+  for (int e = t; e < n; e += NB) {  // position in the sorted order (ties: any order)
+    const int p = atomicAdd(&hist[NB - 1 - bucket(e)], 1);
+    const int r = p / nwg, j = p % nwg;
+    const int wg = (r & 1) ? nwg - 1 - j : j;
+    d.perm[wg * QENV + r] = e;
+  }
+  __syncthreads();
+  for (int e = t; e < n; e += NB) d.cost[e] = 0;
 }
 
 // Stable split of 0..n-1 by pred_mark into fast_envs / pred_envs (one block).
@@ -1069,6 +1114,7 @@ struct bb_handle {
   // split launches (3.66 M vs 3.57 M env-steps/s at 4096 flat envs)
   int route = -1;
   int multi_queue = 1;          // bb_step_multi on relief banks: relief_multi_kernel (BB_MULTI_QUEUE=0: off)
+  int balance = 1;              // relief_multi_kernel: cost-balanced env placement (BB_BALANCE=0: in order)
   std::vector<uint8_t> relief;  // per terrain: max height > 0
   int n_relief = 0;
   int* tstream = nullptr;       // device copies of the terrain streams (bb_set_terrain_stream)
@@ -1094,6 +1140,15 @@ float init_offset(const float* hf, float size_z) {
   for (int i = x0; i < x1; i++)
     for (int j = y0; j < y1; j++) mx = fmax(mx, (double)hf[i * n + j]);
   return float(mx * size_z + 0.01);
+}
+
+Dev balanced_dev(bb_handle* h, hipStream_t s) {
+  Dev dq = h->d;
+  if (h->n % QENV == 0 && h->balance)
+    hipLaunchKernelGGL(balance_kernel, dim3(1), dim3(1024), 0, s, h->d, h->n / QENV);
+  else
+    dq.perm = nullptr;
+  return dq;
 }
 
 template <typename T>
@@ -1152,6 +1207,10 @@ int launch_step(bb_handle* h, const float* a, float* o, float* r, uint8_t* dn, f
 template <typename T>
 size_t multi_lds_bytes(int epw) { return lds_bytes<T>(epw) + size_t(epw) * (NQ + 2 * NV) * sizeof(T); }
 
+// The Dev of a relief_multi_kernel launch: with n a multiple of QENV the envs
+// are dealt by last launch's cost (balance_kernel, on stream s), else in order.
+Dev balanced_dev(bb_handle* h, hipStream_t s);
+
 // dynamic LDS of relief_multi_kernel: QENV EnvWork + their step-start copies
 template <typename T>
 size_t relief_lds_bytes() { return lds_bytes<T>(QENV) + size_t(QENV) * (NQ + 2 * NV) * sizeof(T); }
@@ -1165,11 +1224,12 @@ int launch_rollout(bb_handle* h, const RolloutDev& ro, hipStream_t s) {
   const int epw = h->epw;
   const int blocks = (h->n + epw - 1) / epw;
   const int route = h->route >= 0 ? h->route : (h->n_relief == 0 ? 1 : 0);
-  if (route == 0 && h->team == 16 && h->multi_queue)  // relief banks: the work queue with the policy in it
+  if (route == 0 && h->team == 16 && h->multi_queue) {  // relief banks: the work queue with the policy in it
+    const Dev dq = balanced_dev(h, s);
     hipLaunchKernelGGL((relief_multi_kernel<T, true>), dim3((h->n + QENV - 1) / QENV), dim3(64 * QW),
-                       relief_lds_bytes<T>(), s, model_of<T>(h), h->cfg, h->d, (const float*)nullptr, ro.T,
+                       relief_lds_bytes<T>(), s, model_of<T>(h), h->cfg, dq, (const float*)nullptr, ro.T,
                        (float*)nullptr, (float*)nullptr, (uint8_t*)nullptr, (float*)nullptr, (float*)nullptr, 1, ro);
-  else
+  } else
     hipLaunchKernelGGL(rollout_kernel<T>, dim3(blocks), dim3(WAVE), rollout_lds_bytes<T>(epw), s, model_of<T>(h),
                        h->cfg, h->d, ro, h->team, epw);
   HIPCHK(hipGetLastError());
@@ -1185,10 +1245,11 @@ int launch_multi(bb_handle* h, const float* a, int K, float* o, float* r, uint8_
   hipEvent_t* ev = timed ? &h->tev[6 * h->tn] : nullptr;
   const int route = h->route >= 0 ? h->route : (h->n_relief == 0 ? 1 : 0);
   if (timed) HIPCHK(hipEventRecord(ev[0], s));
-  if (route == 0 && h->team == 16 && h->multi_queue)  // relief banks: the per-workgroup work queue
+  if (route == 0 && h->team == 16 && h->multi_queue) {  // relief banks: the per-workgroup work queue
+    const Dev dq = balanced_dev(h, s);
     hipLaunchKernelGGL((relief_multi_kernel<T, false>), dim3((h->n + QENV - 1) / QENV), dim3(64 * QW),
-                       relief_lds_bytes<T>(), s, model_of<T>(h), h->cfg, h->d, a, K, o, r, dn, t, p2, ar, RolloutDev{});
-  else
+                       relief_lds_bytes<T>(), s, model_of<T>(h), h->cfg, dq, a, K, o, r, dn, t, p2, ar, RolloutDev{});
+  } else
     hipLaunchKernelGGL(multi_step_kernel<T>, dim3(blocks), dim3(WAVE), multi_lds_bytes<T>(epw), s, model_of<T>(h),
                        h->cfg, h->d, a, K, o, r, dn, t, p2, ar, h->team, epw);
   if (timed) {
@@ -1280,6 +1341,8 @@ int bb_create(int n_envs, int device, const bb_params* p, bb_handle** out) {
     if (rt) h->route = atoi(rt);
     const char* mq = getenv("BB_MULTI_QUEUE");
     if (mq) h->multi_queue = atoi(mq) != 0;
+    const char* bl = getenv("BB_BALANCE");
+    if (bl) h->balance = atoi(bl) != 0;
   }
   h->md = compile_model(sc);
   h->mf = cast_model<float>(h->md);
@@ -1320,6 +1383,9 @@ int bb_create(int n_envs, int device, const bb_params* p, bb_handle** out) {
   HIPCHK(hipMalloc((void**)&d.pred_envs, sizeof(int) * n));
   HIPCHK(hipMalloc((void**)&d.pred_mark, n));
   HIPCHK(hipMalloc(&d.body_spill, es * (MAXB - MAXB_LDS) * NBF * size_t(n)));
+  HIPCHK(hipMalloc((void**)&d.perm, sizeof(int) * n));
+  HIPCHK(hipMalloc((void**)&d.cost, sizeof(unsigned long long) * n));
+  HIPCHK(hipMemset(d.cost, 0, sizeof(unsigned long long) * n));
   HIPCHK(hipStreamCreateWithFlags(&h->side, hipStreamNonBlocking));
   HIPCHK(hipEventCreateWithFlags(&h->fork, hipEventDisableTiming));
   HIPCHK(hipEventCreateWithFlags(&h->join, hipEventDisableTiming));
@@ -1374,7 +1440,7 @@ int bb_destroy(bb_handle* h) {
   (void)hipFree(h->bank); (void)hipFree(h->size_z); (void)hipFree(h->offset); (void)hipFree(h->hmax); (void)hipFree(h->d.stats);
   (void)hipFree(h->d.slow_list); (void)hipFree(h->d.slow_count);
   (void)hipFree(h->d.fast_envs); (void)hipFree(h->d.pred_envs); (void)hipFree(h->d.pred_mark);
-  (void)hipFree(h->d.body_spill);
+  (void)hipFree(h->d.body_spill); (void)hipFree(h->d.perm); (void)hipFree(h->d.cost);
   (void)hipFree(h->tstream); (void)hipFree(h->env_stream);
   (void)hipStreamDestroy(h->side); (void)hipEventDestroy(h->fork); (void)hipEventDestroy(h->join);
   for (hipEvent_t e : h->tev) (void)hipEventDestroy(e);
