@@ -25,7 +25,11 @@ rollout for episode statistics and one per minibatch for the KL early stop
 (SB3's semantics need it).  Multi-GPU: each rank
 steps its own env shard; at the update boundary the rollout buffers are
 gathered to rank 0 over RCCL (gather_rollouts), rank 0 runs the update and
-broadcasts the new parameters.
+broadcasts the new parameters (update_mode="gather", north_star's design).
+update_mode="allreduce" instead updates data-parallel: every rank takes its
+minibatches (batch_size / world rows each) from its own shard, the gradients
+are averaged with an RCCL all-reduce before the clip and AdamW step, and the
+KL early stop uses the ranks' mean approx_kl, so no rank waits for rank 0.
 """
 from __future__ import annotations
 
@@ -528,7 +532,8 @@ class BatchedPPO:
                  net_arch: Optional[Dict[str, Any]] = None, activation_fn=nn.LeakyReLU, seed: int = 0,
                  logger: Optional[CSVLogger] = None, stats_window_size: int = 100,
                  gae_fn: Callable = gae_hip, policy: Optional[ActorCriticPolicy] = None,
-                 use_graphs: Optional[bool] = None, frozen_encoder: Optional[nn.Module] = None):
+                 use_graphs: Optional[bool] = None, frozen_encoder: Optional[nn.Module] = None,
+                 update_mode: str = "gather"):
         self.env = env
         self.device = torch.device(env.device)
         self.n_envs = int(env.num_envs)
@@ -542,6 +547,11 @@ class BatchedPPO:
         self.gae_fn = gae_fn
         self.rank = dist.get_rank() if dist.is_available() and dist.is_initialized() else 0
         self.world = dist.get_world_size() if dist.is_available() and dist.is_initialized() else 1
+        if update_mode not in ("gather", "allreduce"):
+            raise ValueError(f"update_mode must be 'gather' or 'allreduce' (got {update_mode!r})")
+        if update_mode == "allreduce" and self.world > 1 and int(batch_size) % self.world:
+            raise ValueError(f"update_mode='allreduce': batch_size {batch_size} must divide by the {self.world} ranks")
+        self.update_mode = update_mode
         torch.manual_seed(int(seed))
         self.cameras = bool(getattr(env, "cameras", False))
         img = (2, env.cam_h, env.cam_w) if self.cameras else None
@@ -833,10 +843,20 @@ class BatchedPPO:
         return self._graphs
 
     def train(self) -> None:
+        if self.world > 1 and self.update_mode == "allreduce":
+            self._update(self.buf.flat(), dp=True)  # every rank, its own shard; parameters stay equal
+            for bf in self.policy.buffers():  # BatchNorm statistics (camera encoder) from rank 0
+                dist.broadcast(bf, src=0)
+            return
         data = self._gathered()
         if data is not None:
             self._update(data)
         self._sync_params()
+
+    def _allreduce_mean(self, t: torch.Tensor) -> torch.Tensor:
+        t = t.detach().clone().float()
+        dist.all_reduce(t)
+        return t / self.world
 
     def _loss(self, obs, act, old_logp, adv, ret, clip):
         """One minibatch of SB3 PPO.train: -> (loss, pg, vf, ent, approx_kl, clip_fraction).
@@ -868,7 +888,12 @@ class BatchedPPO:
             return policy_obs(d["obs"][idx], d["depth"][idx], d["rel_ts"][idx])
         return d["obs"][idx]
 
-    def _update(self, d: Dict[str, torch.Tensor]) -> None:
+    def _update(self, d: Dict[str, torch.Tensor], dp: bool = False) -> None:
+        """SB3 PPO.train over the rollout d.  dp: data-parallel over the ranks
+        (update_mode="allreduce"): local minibatches of batch_size / world rows,
+        gradients averaged over the ranks before the step, the KL stop on the
+        ranks' mean approx_kl (eager minibatches: the all-reduce sits between
+        backward and step)."""
         self.policy.train()
         lr = self.lr_schedule(self.progress_remaining)
         clip = self.clip_schedule(self.progress_remaining)
@@ -878,7 +903,8 @@ class BatchedPPO:
                 g["lr"].fill_(lr)
             else:
                 g["lr"] = lr
-        graphs = self._graphs_for(n) if self.use_graphs else None
+        graphs = self._graphs_for(n) if self.use_graphs and not dp else None
+        bsz = self.batch_size // self.world if dp else self.batch_size
         loss = torch.zeros((), device=self.device)
         ent_l, pg_l, vf_l, clip_f, kls = [], [], [], [], []
         if graphs is not None:
@@ -899,11 +925,13 @@ class BatchedPPO:
             for _epoch in range(self.n_epochs):
                 kls = []
                 perm = torch.randperm(n, generator=self.shuffle_gen, device=self.device)
-                for s in range(0, n, self.batch_size):
-                    idx = perm[s:s + self.batch_size]
+                for s in range(0, n, bsz):
+                    idx = perm[s:s + bsz]
                     loss, pg, vf, ent, kl, cf = self._loss(self._mb_obs(d, idx), d["actions"][idx],
                                                            d["log_probs"][idx], d["advantages"][idx],
                                                            d["returns"][idx], clip)
+                    if dp:  # the global minibatch's terms: the mean over the ranks' local minibatches
+                        pg, vf, ent, kl, cf = (self._allreduce_mean(x) for x in (pg, vf, ent, kl, cf))
                     pg_l.append(pg); vf_l.append(vf); ent_l.append(ent); clip_f.append(cf)
                     approx_kl = float(kl)  # the early stop needs it before the step (host sync)
                     kls.append(approx_kl)
@@ -912,6 +940,13 @@ class BatchedPPO:
                         break
                     self.optimizer.zero_grad(set_to_none=False)
                     loss.backward()
+                    if dp:  # average the gradient over the ranks: one all-reduce (RCCL on the GPU)
+                        gs = [p_.grad for p_ in self.policy.parameters() if p_.grad is not None]
+                        fg = torch._utils._flatten_dense_tensors(gs)
+                        dist.all_reduce(fg)
+                        fg.div_(self.world)
+                        for g_, f_ in zip(gs, torch._utils._unflatten_dense_tensors(fg, gs)):
+                            g_.copy_(f_)
                     if not getattr(self.optimizer, "clips_grad", False):
                         nn.utils.clip_grad_norm_(self.policy.parameters(), self.max_grad_norm)
                     self.optimizer.step()

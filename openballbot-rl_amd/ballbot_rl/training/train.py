@@ -78,7 +78,7 @@ def make_env(config: Dict[str, Any], num_envs: int, device, seed: int, precision
 
 
 def main(config: Dict[str, Any], seed: int, out: Optional[str] = None, total_timesteps: Optional[int] = None,
-         precision: str = "fp64") -> BatchedPPO:
+         precision: str = "fp64", update_mode: str = "gather") -> BatchedPPO:
     from ballbot_gym.distributed import env_shard, shard_stream_seeds
     from ballbot_rl.evaluation import evaluate_policy
 
@@ -124,7 +124,8 @@ def main(config: Dict[str, Any], seed: int, out: Optional[str] = None, total_tim
     elif env.cameras and fc and rank == 0:
         print(f"warning: frozen_cnn {fc!r} is not a safetensors encoder (pickled modules are not loaded); "
               "the rgbd branches train from scratch")
-    model = BatchedPPO(env, seed=seed, logger=logger, frozen_encoder=frozen, **ppo_kwargs(config))
+    model = BatchedPPO(env, seed=seed, logger=logger, frozen_encoder=frozen, update_mode=update_mode,
+                       **ppo_kwargs(config))
     if config.get("resume"):
         model.load_policy(config["resume"])
     eval_freq = int(eval_cfg.get("freq", 5000))
@@ -159,6 +160,8 @@ def cli_main() -> None:
     ap.add_argument("--total-timesteps", type=float, default=None)
     ap.add_argument("--out", default=None)
     ap.add_argument("--precision", default="fp64", choices=["fp32", "fp64"])
+    ap.add_argument("--update-mode", default="gather", choices=["gather", "allreduce"],
+                    help="multi-GPU PPO update: gather the rollouts to rank 0 (north_star) or data-parallel")
     args = ap.parse_args()
     cfg = load_training_config(str(Path(args.config).resolve()))
     seed = int(cfg.get("seed", 0))
@@ -167,7 +170,7 @@ def cli_main() -> None:
         np.random.seed(seed)
         torch.manual_seed(seed)
     main(cfg, seed, out=args.out, total_timesteps=None if args.total_timesteps is None else int(args.total_timesteps),
-         precision=args.precision)
+         precision=args.precision, update_mode=args.update_mode)
     if dist.is_initialized():
         dist.destroy_process_group()
 

@@ -2,6 +2,7 @@
 import os
 import socket
 
+import numpy as np
 import pytest
 import torch
 import torch.distributed as dist
@@ -91,3 +92,59 @@ def test_gloo_world2_ppo_update_boundary():
     assert u0 == 2 and u1 == 0             # SB3 counts epochs: 1 epoch x 2 iterations, on rank 0 only
     assert (v0 == v1).all()
     assert e0 == e1 > 0                    # episode stats gathered from both ranks
+
+
+def _dp_worker(rank, world, port, q, target_kl):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    from fake_env import FakeEnv
+    from test_ppo import _ppo
+
+    torch.manual_seed(100 + rank)  # different local init: the constructor's broadcast aligns them
+    env = FakeEnv(8, seed=5, ep_len=4)  # the same data on both ranks (see the single-process twin)
+    m = _ppo(env, n_steps=4, batch_size=16, n_epochs=2, update_mode="allreduce", target_kl=target_kl)
+    m.gen.manual_seed(77)
+    m.learn(total_timesteps=2 * 8 * 4 * world)
+    vec = torch.nn.utils.parameters_to_vector(m.policy.parameters()).detach()
+    q.put((rank, m._n_updates, vec.numpy(), m.logger.values.get("train/approx_kl")))
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("target_kl", [None, 1e-4])
+def test_gloo_world2_data_parallel_update(target_kl):
+    """update_mode="allreduce": every rank updates on its own shard with batch_size/world rows
+    per minibatch and the gradients averaged over the ranks.  Both ranks holding the same
+    data makes the averaged gradient each rank's own, so the result must equal one process
+    updating that data with batch_size/world (KL early stop on the ranks' mean approx_kl)."""
+    from fake_env import FakeEnv
+    from test_ppo import _ppo
+
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_dp_worker, args=(r, 2, port, q, target_kl)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = sorted([q.get(timeout=180) for _ in range(2)], key=lambda x: x[0])
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    (_, u0, v0, kl0), (_, u1, v1, kl1) = res
+    assert (v0 == v1).all() and u0 == u1  # no parameter broadcast after the update: they stay equal
+    torch.manual_seed(100)  # rank 0's initial parameters
+    m = _ppo(FakeEnv(8, seed=5, ep_len=4), n_steps=4, batch_size=8, n_epochs=2, target_kl=target_kl)
+    m.gen.manual_seed(77)
+    m.learn(total_timesteps=2 * 8 * 4)
+    ref = torch.nn.utils.parameters_to_vector(m.policy.parameters()).detach().numpy()
+    assert m._n_updates == u0
+    np.testing.assert_allclose(v0, ref, rtol=1e-6, atol=1e-7)
+    if target_kl is not None:
+        assert kl0 == pytest.approx(m.logger.values.get("train/approx_kl"), rel=1e-6)
+
+
+def test_data_parallel_needs_divisible_batch():
+    from fake_env import FakeEnv
+    from test_ppo import _ppo
+
+    with pytest.raises(ValueError):
+        _ppo(FakeEnv(8), update_mode="sideways")
