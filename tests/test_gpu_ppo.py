@@ -691,3 +691,48 @@ def test_update_graph_build_keeps_encoder_statistics(monkeypatch):
     for b0, b1 in zip(before, m.policy.buffers()):
         assert torch.equal(b0, b1)
     env.close()
+
+
+def _dp_gpu_worker(rank, world, port, q):
+    import os
+
+    import torch.distributed as dist
+
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world))
+    dist.init_process_group("gloo", rank=rank, world_size=world)  # two ranks sharing the box's GPU
+    from ballbot_gym.envs import BallbotVecEnv
+    from ballbot_rl.training.logger import CSVLogger
+    from ballbot_rl.training.ppo import BatchedPPO
+
+    torch.manual_seed(10 + rank)
+    env = BallbotVecEnv(256, device="cuda:0", seed=3 + rank, max_ep_steps=40)
+    m = BatchedPPO(env, n_steps=16, batch_size=1024, n_epochs=2, seed=5, update_mode="allreduce",
+                   logger=CSVLogger(None, stdout=False))
+    m.learn(total_timesteps=256 * 16 * world * 2)
+    vec = torch.nn.utils.parameters_to_vector(m.policy.parameters()).detach().cpu()
+    q.put((rank, vec.numpy(), m._n_updates, float(m.logger.values["train/value_loss"])))
+    env.close()
+    dist.destroy_process_group()
+
+
+def test_data_parallel_update_on_gpu_ranks():
+    """update_mode="allreduce" with the GPU env, bb_ppo_loss and FlatAdamW (bb_adamw_clip) on
+    two ranks (gloo, one GPU): different env shards, the same parameters after every update."""
+    import socket
+
+    import torch.multiprocessing as mp
+
+    with socket.socket() as s_:
+        s_.bind(("127.0.0.1", 0))
+        port = s_.getsockname()[1]
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    procs = [ctx.Process(target=_dp_gpu_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = sorted([q.get(timeout=240) for _ in range(2)], key=lambda x: x[0])
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    (_, v0, u0, l0), (_, v1, u1, l1) = res
+    assert (v0 == v1).all() and u0 == u1 == 4 and l0 == l1 and np.isfinite(l0)
