@@ -93,6 +93,19 @@ def test_multi_step_perlin_hand_overs_match(route, monkeypatch):
     a.close(), b.close()
 
 
+def test_multi_step_relief_queue_ragged_workgroups(monkeypatch):
+    """200 envs: the last workgroup of the relief work queue holds 8 envs (200 = 12 x 16 + 8),
+    and the cost-balanced placement is off (it needs whole workgroups); route 0 bit-exact."""
+    n = 200
+    a, b = _pair(n, "perlin", monkeypatch, route="0", n_terrains=None, stream_seeds=[900 + i for i in range(n)],
+                 max_ep_steps=200)
+    g = torch.Generator(device="cuda:0").manual_seed(5)
+    actions = torch.rand(224, n, 3, generator=g, device="cuda:0") * 2 - 1
+    st = _compare_runs(a, b, actions, 32)
+    assert st["slow_path"] > 0
+    a.close(), b.close()
+
+
 def test_multi_step_rejects_bad_shapes():
     from ballbot_gym.envs import BallbotVecEnv
 
