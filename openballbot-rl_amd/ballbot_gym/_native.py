@@ -111,22 +111,44 @@ ABI_VERSION = 14  # include/ballbot_mi355x.h BB_ABI_VERSION
 _lib = None
 
 
+HIP_SOURCES = ("bb_kernels.hip", "bb_terrain.hip", "bb_rollout.hip", "bb_render.hip", "bb_ppo.hip", "bb_mlp.hip",
+               "bb_encoder.hip")
+
+
 def build(force: bool = False, verbose: bool = False) -> Path:
-    """Compile csrc/bb_kernels.hip + bb_terrain.hip + bb_rollout.hip + bb_render.hip + bb_ppo.hip + bb_mlp.hip + bb_encoder.hip for gfx950 into _lib/libbb_mi355x.so."""
+    """Compile csrc/*.hip (HIP_SOURCES) for gfx950 into _lib/libbb_mi355x.so: one
+    hipcc -c per source, in parallel (objects under _lib/obj), then one link."""
     import subprocess
+    from concurrent.futures import ThreadPoolExecutor
 
     srcs = list(CSRC.glob("*.h")) + list(CSRC.glob("*.hip")) + list(INCLUDE.glob("*.h"))
     if LIB_PATH.exists() and not force and all(LIB_PATH.stat().st_mtime >= s.stat().st_mtime for s in srcs):
         return LIB_PATH
-    LIB_PATH.parent.mkdir(parents=True, exist_ok=True)
-    tmp = LIB_PATH.with_suffix(".so.tmp")
-    cmd = ["hipcc", "--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC", "-shared",
-           "-o", str(tmp), str(CSRC / "bb_kernels.hip"), str(CSRC / "bb_terrain.hip"),
-           str(CSRC / "bb_rollout.hip"), str(CSRC / "bb_render.hip"),
-           str(CSRC / "bb_ppo.hip"), str(CSRC / "bb_mlp.hip"), str(CSRC / "bb_encoder.hip")]
+    obj_dir = LIB_PATH.parent / "obj"
+    obj_dir.mkdir(parents=True, exist_ok=True)
+    flags = ["--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC"]
+    jobs = []
+    for f in HIP_SOURCES:
+        obj = obj_dir / (f[:-4] + ".o")
+        jobs.append((["hipcc", *flags, "-c", "-o", str(obj), str(CSRC / f)], obj))
     if verbose:
-        print(" ".join(cmd))
-    subprocess.run(cmd, check=True)
+        for cmd, _ in jobs:
+            print(" ".join(cmd))
+
+    def run(job):
+        return subprocess.run(job[0], capture_output=True, text=True)
+
+    workers = max(1, min(len(jobs), os.cpu_count() or 1, 16))
+    with ThreadPoolExecutor(workers) as ex:
+        results = list(ex.map(run, jobs))
+    for (cmd, _), r in zip(jobs, results):
+        if r.returncode != 0:
+            raise subprocess.CalledProcessError(r.returncode, cmd, r.stdout, r.stderr + "\n" + " ".join(cmd))
+    tmp = LIB_PATH.with_suffix(".so.tmp")
+    link = ["hipcc", "--offload-arch=gfx950", "-shared", "-fPIC", "-o", str(tmp), *[str(o) for _, o in jobs]]
+    if verbose:
+        print(" ".join(link))
+    subprocess.run(link, check=True)
     os.replace(tmp, LIB_PATH)
     return LIB_PATH
 

@@ -313,7 +313,7 @@ template <typename T>
 __device__ __forceinline__ int team_step(const ModelT<T>& m, const EnvCfg& cfg, const Dev& d, int e, int& tid,
                                          T* q, T* v, T* w, int& step, T* bk, const float* a, EnvWork<T>& W, float* o,
                                          float& r, float* tobs_row, float* p2_row, int auto_reset, const Team& tm,
-                                         bool full = false) {
+                                         unsigned* cnt, bool full = false) {
   const int L = tm.L;
   const bool lead = tm.tl == 0;
   team_sync();
@@ -343,7 +343,7 @@ __device__ __forceinline__ int team_step(const ModelT<T>& m, const EnvCfg& cfg, 
   }
   const bool reset = auto_reset && (fl & F_TERMINATED);
   if (lead) {
-    if (slow) atomicAdd(&d.stats[3], 1ull);
+    cnt[3] += slow;
     if (tobs_row) {
 #pragma unroll
       for (int i = 0; i < 15; i++) tobs_row[i] = o[i];
@@ -363,13 +363,28 @@ __device__ __forceinline__ int team_step(const ModelT<T>& m, const EnvCfg& cfg, 
     for (int i = 0; i < 15; i++) o[i] = 0.f;
   }
   if (lead) {
-    if (reset) atomicAdd(&d.stats[0], 1ull);
-    if (fl & F_DIVERGED) atomicAdd(&d.stats[1], 1ull);
-    if (fl & F_OVERFLOW) atomicAdd(&d.stats[2], 1ull);
-    if (fl & F_SPILL) atomicAdd(&d.stats[6], 1ull);
-    atomicAdd(&d.stats[4], (unsigned long long)iters);
+    cnt[0] += reset;
+    cnt[1] += (fl & F_DIVERGED) != 0;
+    cnt[2] += (fl & F_OVERFLOW) != 0;
+    cnt[6] += (fl & F_SPILL) != 0;
+    cnt[4] += unsigned(iters);
   }
   return fl;
+}
+
+// A multi-step launch's counters: team_step adds to the team's (or env slot's)
+// LDS row cnt[8] (indices as Dev::stats; 5, the stream wraps, is counted in
+// next_terrain), and the row goes to d.stats once at the end of the launch --
+// not one same-address device atomic per env-step, whose completion every
+// later vector-memory wait of the step would also wait for.
+__device__ __forceinline__ void counts_clear(unsigned* cnt) {
+#pragma unroll
+  for (int i = 0; i < 8; i++) cnt[i] = 0u;
+}
+__device__ __forceinline__ void counts_flush(const Dev& d, const unsigned* cnt) {
+#pragma unroll
+  for (int i = 0; i < 8; i++)
+    if (i != 5 && cnt[i]) atomicAdd(&d.stats[i], (unsigned long long)cnt[i]);
 }
 
 // K env steps of every env in one launch (bb_step_multi): actions [K][n][3]
@@ -399,7 +414,12 @@ __global__ __launch_bounds__(64) void multi_step_kernel(ModelT<T> mg, EnvCfg cfg
   EnvWork<T>& W = team_work<T>(smem, team);
   // the step's start state (qn, vn, wn are contiguous: 47 values), for a hand-over
   T* bk = reinterpret_cast<T*>(smem + size_t(epw) * work_stride<T>()) + team * (NQ + 2 * NV);
-  if (lead) W.bspill = body_spill_of<T>(d, e);
+  __shared__ unsigned s_cnt[WAVE / TEAM][8];
+  unsigned* cnt = s_cnt[team];
+  if (lead) {
+    W.bspill = body_spill_of<T>(d, e);
+    counts_clear(cnt);
+  }
   T* q = W.qn;
   T* v = W.vn;
   T* w = W.wn;
@@ -414,7 +434,7 @@ __global__ __launch_bounds__(64) void multi_step_kernel(ModelT<T> mg, EnvCfg cfg
     const float a[3] = {ak[0], ak[1], ak[2]};
     float o[15], r;
     const int fl = team_step<T>(m, cfg, d, e, tid, q, v, w, step, bk, a, W, o, r, tobs ? tobs + 15 * row : nullptr,
-                                pos2d ? pos2d + 2 * row : nullptr, auto_reset, tm);
+                                pos2d ? pos2d + 2 * row : nullptr, auto_reset, tm, cnt);
     if (lead) {
 #pragma unroll
       for (int i = 0; i < 15; i++) obs[15 * row + i] = o[i];
@@ -423,7 +443,10 @@ __global__ __launch_bounds__(64) void multi_step_kernel(ModelT<T> mg, EnvCfg cfg
     }
   }
   team_sync();
-  if (lead) store_state(d, e, q, v, w, step);
+  if (lead) {
+    store_state(d, e, q, v, w, step);
+    counts_flush(d, cnt);
+  }
 }
 
 // The rollout's policy step for one env on its team: SB3
@@ -553,7 +576,12 @@ __global__ __launch_bounds__(64) void rollout_kernel(ModelT<T> mg, EnvCfg cfg, D
   float* x = pol;
   float* hA = pol + 16;
   float* hB = pol + 144;
-  if (lead) W.bspill = body_spill_of<T>(d, e);
+  __shared__ unsigned s_cnt[WAVE / TEAM][8];
+  unsigned* cnt = s_cnt[team];
+  if (lead) {
+    W.bspill = body_spill_of<T>(d, e);
+    counts_clear(cnt);
+  }
   T* q = W.qn;
   T* v = W.vn;
   T* w = W.wn;
@@ -599,7 +627,7 @@ __global__ __launch_bounds__(64) void rollout_kernel(ModelT<T> mg, EnvCfg cfg, D
       ro.b_starts[row] = start;
     }
     float r;
-    const int fl = team_step<T>(m, cfg, d, e, tid, q, v, w, step, bk, ac, W, o, r, nullptr, nullptr, 1, tm);
+    const int fl = team_step<T>(m, cfg, d, e, tid, q, v, w, step, bk, ac, W, o, r, nullptr, nullptr, 1, tm, cnt);
     // collect_rollouts + Monitor bookkeeping (bb_rollout_track): done = terminated
     const bool dn = (fl & F_TERMINATED) != 0;
     ret += double(r);
@@ -616,6 +644,7 @@ __global__ __launch_bounds__(64) void rollout_kernel(ModelT<T> mg, EnvCfg cfg, D
   team_sync();
   if (lead) {
     store_state(d, e, q, v, w, step);
+    counts_flush(d, cnt);
 #pragma unroll
     for (int i = 0; i < 15; i++) ro.obs[15 * size_t(e) + i] = o[i];
     ro.last_starts[e] = start;
@@ -843,6 +872,7 @@ __global__ __launch_bounds__(64 * QW) void relief_multi_kernel(ModelT<T> mg, Env
   __shared__ int s_k[QENV], s_busy[QENV], s_kind[QENV], s_tid[QENV], s_step[QENV], s_env[QENV];
   __shared__ int s_claim[QW][4], s_fin[QW];
   __shared__ int s_lock, s_left;
+  __shared__ unsigned s_cnt[QENV][8];  // per env slot (team_step's counters)
   // RO: per env the observation, episode start and Monitor counters between claims
   __shared__ float s_obs[RO ? QENV : 1][15];
   __shared__ int s_start[RO ? QENV : 1];
@@ -871,6 +901,7 @@ __global__ __launch_bounds__(64 * QW) void relief_multi_kernel(ModelT<T> mg, Env
     load_state(d, e, W.qn, W.vn, W.wn, step);
     W.bspill = body_spill_of<T>(d, e);
     s_env[i] = e;
+    counts_clear(s_cnt[i]);
     s_k[i] = 0;
     s_busy[i] = 0;
     s_tid[i] = d.terrain[e];
@@ -960,7 +991,7 @@ __global__ __launch_bounds__(64 * QW) void relief_multi_kernel(ModelT<T> mg, Env
       }
       const int fl = team_step<T>(m, cfg, d, e, tid, W.qn, W.vn, W.wn, step, bk, a, W, o, r,
                                   (!RO && tobs) ? tobs + 15 * row : nullptr, (!RO && pos2d) ? pos2d + 2 * row : nullptr,
-                                  RO ? 1 : auto_reset, tm, full);
+                                  RO ? 1 : auto_reset, tm, s_cnt[i], full);
       if (lead) {
         if (RO) {  // collect_rollouts + Monitor bookkeeping (bb_rollout_track)
           const bool dn = (fl & F_TERMINATED) != 0;
@@ -1000,6 +1031,7 @@ __global__ __launch_bounds__(64 * QW) void relief_multi_kernel(ModelT<T> mg, Env
     const int i = int(threadIdx.x), e = s_env[i];
     EnvWork<T>& W = team_work<T>(smem, i);
     store_state(d, e, W.qn, W.vn, W.wn, s_step[i]);
+    counts_flush(d, s_cnt[i]);
     if (RO) {
 #pragma unroll
       for (int j = 0; j < 15; j++) ro.obs[15 * size_t(e) + j] = s_obs[i][j];

@@ -26,11 +26,11 @@ def main():
     ap.add_argument("--build", action="store_true")
     ap.add_argument("--terrain", default="flat")
     a = ap.parse_args()
+    from ballbot_gym import _native
     if a.build or not LIB.exists():
         LIB.parent.mkdir(parents=True, exist_ok=True)
         subprocess.run(["hipcc", "--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC", "-shared", "-DBB_PHASE_CLOCKS",
-                        "-o", str(LIB)] + [str(ROOT / "openballbot-rl_amd" / "csrc" / f) for f in
-                                           ("bb_kernels.hip", "bb_terrain.hip", "bb_rollout.hip", "bb_render.hip", "bb_ppo.hip")],
+                        "-o", str(LIB)] + [str(ROOT / "openballbot-rl_amd" / "csrc" / f) for f in _native.HIP_SOURCES],
                        check=True)
     import torch
     from ballbot_gym import _native
