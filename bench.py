@@ -319,7 +319,9 @@ def main() -> None:
                          "kernel": ((f"relief_multi_kernel<T> (work queue, {M} steps per launch)" if env.relief
                                      and os.environ.get("BB_MULTI_QUEUE", "1") != "0" and
                                      os.environ.get("BB_ROUTE", "0") == "0"
-                                     else f"multi_step_kernel<T> ({M} steps per launch)") if M else
+                                     else f"multi_step_kernel<T,false> ({M} steps per launch; hand-overs parked "
+                                          "for multi_step_kernel<T,true>)" if os.environ.get("BB_MULTI_PARK", "1") != "0"
+                                     else f"multi_step_kernel<T,true> ({M} steps per launch, hand-overs inline)") if M else
                                     "step_kernel<T,false> (fast path)" if dom == "fast"
                                     else "step_kernel<T,true> (predicted full kernel, side stream)"),
                          "kernel_ms": kern_ms, "envs_per_launch": envs_dom, "kernel_ms_all": ktimes,

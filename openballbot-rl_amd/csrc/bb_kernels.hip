@@ -83,6 +83,7 @@ struct Dev {
   unsigned long long* stats;  // resets, diverged, overflow, slow-path env-steps, iters, draws past the stream table, spill
   int* slow_list;             // envs the fast kernel handed to the full kernel this step
   int* slow_count;            // [0] fast list size, [1] predicted-slow list size, [2] hand-overs
+  int* park;                  // bb_step_multi (two launches): the step each env was parked at, K when done
   int* fast_envs;             // this step's fast-kernel env list (ascending)
   int* pred_envs;             // envs predicted to need base-tree contacts (full kernel, concurrent)
   uint8_t* pred_mark;
@@ -309,7 +310,13 @@ int full_env_step(const ModelT<T>& m, const EnvCfg& cfg, T* q, T* v, T* w, int& 
 // this step's terminal obs and pos2d.  On return o holds the obs after any
 // reset; the flags are the step's.  full: the predictor routed the env to the
 // full step (relief_multi_kernel): the fast path is not tried.
-template <typename T>
+// HO = false (multi_step_kernel's first launch): the full step is not compiled
+// in; an env the fast path hands over is restored to the step's start state
+// and F_PARKED returned, without counting the attempt -- the finish launch
+// redoes that step through the hand-over and counts it there.
+constexpr int F_PARKED = 1 << 17;  // internal: never in a done byte
+
+template <typename T, bool HO = true>
 __device__ __forceinline__ int team_step(const ModelT<T>& m, const EnvCfg& cfg, const Dev& d, int e, int& tid,
                                          T* q, T* v, T* w, int& step, T* bk, const float* a, EnvWork<T>& W, float* o,
                                          float& r, float* tobs_row, float* p2_row, int auto_reset, const Team& tm,
@@ -339,7 +346,8 @@ __device__ __forceinline__ int team_step(const ModelT<T>& m, const EnvCfg& cfg, 
     for (int i = tm.tl; i < NQ + 2 * NV; i += L) q[i] = bk[i];
     team_sync();
     step = step0;
-    fl = full_env_step<T>(m, cfg, q, v, w, step, a, tr, W, o, r, p2, &iters, tm);
+    if constexpr (!HO) return F_PARKED;
+    else fl = full_env_step<T>(m, cfg, q, v, w, step, a, tr, W, o, r, p2, &iters, tm);
   }
   const bool reset = auto_reset && (fl & F_TERMINATED);
   if (lead) {
@@ -393,11 +401,21 @@ __device__ __forceinline__ void counts_flush(const Dev& d, const unsigned* cnt) 
 // slowest env of the chip at every step, only for the slowest of its wave.
 // Per step k the outputs, counters, auto-reset and terrain draws are exactly
 // those of the k-th bb_step call under the serial route.
-template <typename T>
+//
+// Two launches (park != NULL): HO = false steps every env until done or until
+// the fast path hands a step over (a base-tree geom may touch the terrain);
+// that env is parked at its step k (park[e] = k, K when done) with the step's
+// start state stored.  HO = true then resumes the parked envs from park[e]
+// with the full step inline and exits at once for the others.  The first
+// launch carries no full step, so it keeps the fast kernel's registers: the
+// full step inlined beside it costs 157-196 spilled VGPRs (scratch traffic on
+// every step, hand-over or not).  park == NULL: one launch, hand-overs inline.
+template <typename T, bool HO>
 __global__ __launch_bounds__(64) void multi_step_kernel(ModelT<T> mg, EnvCfg cfg, Dev d, const float* __restrict__ act,
                                                         int K, float* __restrict__ obs, float* __restrict__ rew,
                                                         uint8_t* __restrict__ done, float* __restrict__ tobs,
-                                                        float* __restrict__ pos2d, int auto_reset, int L, int epw) {
+                                                        float* __restrict__ pos2d, int auto_reset, int L, int epw,
+                                                        int* __restrict__ park) {
   extern __shared__ __align__(16) unsigned char smem[];
   const int nwg = int(gridDim.x), b = int(blockIdx.x);
   const int g = (nwg & 7) ? b : (b & 7) * (nwg >> 3) + (b >> 3);  // XCD-aware order, as step_kernel
@@ -410,6 +428,11 @@ __global__ __launch_bounds__(64) void multi_step_kernel(ModelT<T> mg, EnvCfg cfg
   if (team >= epw) return;
   const int e = g * epw + team;
   if (unsigned(e) >= unsigned(d.n)) return;
+  int k0 = 0;
+  if (HO && park) {  // the finish launch: only parked envs, from their parked step
+    k0 = park[e];
+    if (k0 >= K) return;  // team-uniform
+  }
   const bool lead = tm.tl == 0;
   EnvWork<T>& W = team_work<T>(smem, team);
   // the step's start state (qn, vn, wn are contiguous: 47 values), for a hand-over
@@ -427,14 +450,19 @@ __global__ __launch_bounds__(64) void multi_step_kernel(ModelT<T> mg, EnvCfg cfg
   load_state(d, e, q, v, w, step);
   int tid = d.terrain[e];
   const size_t n = size_t(d.n);
+  int parked = K;
 #pragma unroll 1
-  for (int k = 0; k < K; k++) {
+  for (int k = k0; k < K; k++) {
     const size_t row = size_t(k) * n + e;
     const float* ak = act + 3 * row;
     const float a[3] = {ak[0], ak[1], ak[2]};
     float o[15], r;
-    const int fl = team_step<T>(m, cfg, d, e, tid, q, v, w, step, bk, a, W, o, r, tobs ? tobs + 15 * row : nullptr,
-                                pos2d ? pos2d + 2 * row : nullptr, auto_reset, tm, cnt);
+    const int fl = team_step<T, HO>(m, cfg, d, e, tid, q, v, w, step, bk, a, W, o, r, tobs ? tobs + 15 * row : nullptr,
+                                    pos2d ? pos2d + 2 * row : nullptr, auto_reset, tm, cnt);
+    if (!HO && (fl & F_PARKED)) {  // team-uniform
+      parked = k;
+      break;
+    }
     if (lead) {
 #pragma unroll
       for (int i = 0; i < 15; i++) obs[15 * row + i] = o[i];
@@ -446,6 +474,7 @@ __global__ __launch_bounds__(64) void multi_step_kernel(ModelT<T> mg, EnvCfg cfg
   if (lead) {
     store_state(d, e, q, v, w, step);
     counts_flush(d, cnt);
+    if (!HO) park[e] = parked;
   }
 }
 
@@ -1146,6 +1175,7 @@ struct bb_handle {
   // split launches (3.66 M vs 3.57 M env-steps/s at 4096 flat envs)
   int route = -1;
   int multi_queue = 1;          // bb_step_multi on relief banks: relief_multi_kernel (BB_MULTI_QUEUE=0: off)
+  int multi_park = 1;           // bb_step_multi, serial route: two launches, hand-overs parked (BB_MULTI_PARK=0: one)
   int balance = 1;              // relief_multi_kernel: cost-balanced env placement (BB_BALANCE=0: in order)
   std::vector<uint8_t> relief;  // per terrain: max height > 0
   int n_relief = 0;
@@ -1281,11 +1311,17 @@ int launch_multi(bb_handle* h, const float* a, int K, float* o, float* r, uint8_
     const Dev dq = balanced_dev(h, s);
     hipLaunchKernelGGL((relief_multi_kernel<T, false>), dim3((h->n + QENV - 1) / QENV), dim3(64 * QW),
                        relief_lds_bytes<T>(), s, model_of<T>(h), h->cfg, dq, a, K, o, r, dn, t, p2, ar, RolloutDev{});
+  } else if (h->multi_park) {  // the fast steps, then the parked envs' hand-overs and the rest of their steps
+    hipLaunchKernelGGL((multi_step_kernel<T, false>), dim3(blocks), dim3(WAVE), multi_lds_bytes<T>(epw), s,
+                       model_of<T>(h), h->cfg, h->d, a, K, o, r, dn, t, p2, ar, h->team, epw, h->d.park);
+    if (timed) HIPCHK(hipEventRecord(ev[1], s));
+    hipLaunchKernelGGL((multi_step_kernel<T, true>), dim3(blocks), dim3(WAVE), multi_lds_bytes<T>(epw), s,
+                       model_of<T>(h), h->cfg, h->d, a, K, o, r, dn, t, p2, ar, h->team, epw, h->d.park);
   } else
-    hipLaunchKernelGGL(multi_step_kernel<T>, dim3(blocks), dim3(WAVE), multi_lds_bytes<T>(epw), s, model_of<T>(h),
-                       h->cfg, h->d, a, K, o, r, dn, t, p2, ar, h->team, epw);
+    hipLaunchKernelGGL((multi_step_kernel<T, true>), dim3(blocks), dim3(WAVE), multi_lds_bytes<T>(epw), s,
+                       model_of<T>(h), h->cfg, h->d, a, K, o, r, dn, t, p2, ar, h->team, epw, (int*)nullptr);
   if (timed) {
-    HIPCHK(hipEventRecord(ev[1], s));
+    if (!h->multi_park || (route == 0 && h->team == 16 && h->multi_queue)) HIPCHK(hipEventRecord(ev[1], s));
     HIPCHK(hipEventRecord(ev[5], s));
     h->tpred[h->tn] = 0;
     h->tn++;
@@ -1371,6 +1407,8 @@ int bb_create(int n_envs, int device, const bb_params* p, bb_handle** out) {
     h->epw_full = epf;
     const char* rt = getenv("BB_ROUTE");
     if (rt) h->route = atoi(rt);
+    const char* mp = getenv("BB_MULTI_PARK");
+    if (mp) h->multi_park = atoi(mp) != 0;
     const char* mq = getenv("BB_MULTI_QUEUE");
     if (mq) h->multi_queue = atoi(mq) != 0;
     const char* bl = getenv("BB_BALANCE");
@@ -1409,6 +1447,7 @@ int bb_create(int n_envs, int device, const bb_params* p, bb_handle** out) {
   HIPCHK(hipMemset(h->hmax, 0, sizeof(float) * nt));
   HIPCHK(hipMalloc((void**)&d.stats, sizeof(unsigned long long) * 8));
   HIPCHK(hipMalloc((void**)&d.slow_list, sizeof(int) * n));
+  HIPCHK(hipMalloc((void**)&d.park, sizeof(int) * n));
   HIPCHK(hipMalloc((void**)&d.slow_count, sizeof(int) * 64));  // 4 used; a 256-B block of its own
   HIPCHK(hipMemset(d.slow_count, 0, sizeof(int) * 64));
   HIPCHK(hipMalloc((void**)&d.fast_envs, sizeof(int) * n));
@@ -1444,9 +1483,12 @@ int bb_create(int n_envs, int device, const bb_params* p, bb_handle** out) {
     const void* fk = h->fp64 ? (const void*)forward_kernel<double> : (const void*)forward_kernel<float>;
     HIPCHK(hipFuncSetAttribute(sk, hipFuncAttributeMaxDynamicSharedMemorySize, lb));
     HIPCHK(hipFuncSetAttribute(fk, hipFuncAttributeMaxDynamicSharedMemorySize, lb));
-    const void* mk = h->fp64 ? (const void*)multi_step_kernel<double> : (const void*)multi_step_kernel<float>;
     const int mlb = (int)(h->fp64 ? multi_lds_bytes<double>(h->epw) : multi_lds_bytes<float>(h->epw));
-    HIPCHK(hipFuncSetAttribute(mk, hipFuncAttributeMaxDynamicSharedMemorySize, mlb));
+    const void* mk[2] = {h->fp64 ? (const void*)multi_step_kernel<double, false>
+                                 : (const void*)multi_step_kernel<float, false>,
+                         h->fp64 ? (const void*)multi_step_kernel<double, true>
+                                 : (const void*)multi_step_kernel<float, true>};
+    for (const void* k : mk) HIPCHK(hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, mlb));
     const void* rk = h->fp64 ? (const void*)rollout_kernel<double> : (const void*)rollout_kernel<float>;
     const int rlb = (int)(h->fp64 ? rollout_lds_bytes<double>(h->epw) : rollout_lds_bytes<float>(h->epw));
     HIPCHK(hipFuncSetAttribute(rk, hipFuncAttributeMaxDynamicSharedMemorySize, rlb));
@@ -1470,7 +1512,7 @@ int bb_destroy(bb_handle* h) {
   (void)hipFree(h->d.qpos); (void)hipFree(h->d.qvel); (void)hipFree(h->d.warm);
   (void)hipFree(h->d.steps); (void)hipFree(h->d.terrain); (void)hipFree(h->d.pending_terrain); (void)hipFree(h->d.episodes);
   (void)hipFree(h->bank); (void)hipFree(h->size_z); (void)hipFree(h->offset); (void)hipFree(h->hmax); (void)hipFree(h->d.stats);
-  (void)hipFree(h->d.slow_list); (void)hipFree(h->d.slow_count);
+  (void)hipFree(h->d.slow_list); (void)hipFree(h->d.slow_count); (void)hipFree(h->d.park);
   (void)hipFree(h->d.fast_envs); (void)hipFree(h->d.pred_envs); (void)hipFree(h->d.pred_mark);
   (void)hipFree(h->d.body_spill); (void)hipFree(h->d.perm); (void)hipFree(h->d.cost);
   (void)hipFree(h->tstream); (void)hipFree(h->env_stream);

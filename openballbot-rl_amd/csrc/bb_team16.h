@@ -909,16 +909,40 @@ __device__ __forceinline__ bool prism_may_hit(const Reach<T>& g, const T (&V)[3]
 template <typename T>
 __device__ bool body_candidates(const ModelT<T>& m, const Kin<T>& k, const float* hf, T size_z, T hz, int tl) {
   bool cand = false;
-  if (tl < 3) {
+  // lane gi < 6 places geom gi once (lanes 0..2 also test it against the
+  // ball) and screens it against the terrain: its AABB must reach the
+  // terrain's top (hz) and overlap the grid.  Only the geoms that pass are
+  // walked, by the whole team -- rather than every lane placing all six.
+  bool reach = false;
+  if (tl < 6) {
     Seg<T> g;
     body_geom(m, k, tl, g);
-    T dist, n[3], pos[3];
-    cand = tl == 0 ? sphere_cylinder(k.c, m.ball_r, g, dist, n, pos) : sphere_capsule(k.c, m.ball_r, g, dist, n, pos);
+    if (tl < 3) {
+      T dist, n[3], pos[3];
+      cand = tl == 0 ? sphere_cylinder(k.c, m.ball_r, g, dist, n, pos) : sphere_capsule(k.c, m.ball_r, g, dist, n, pos);
+    }
+    if (hf) {
+      const T sx = m.hf_sx, sy = m.hf_sy, zb = m.hf_bottom;
+      T lo[3], hi[3];
+#pragma unroll
+      for (int i = 0; i < 3; i++) {
+        const T ai = fabs(g.a[i]);
+        const T rad = T(1) - ai * ai;
+        const T ext = tl == 0 ? g.hh * ai + g.r * sqrt(rad > 0 ? rad : T(0)) : g.hh * ai + g.r;
+        lo[i] = g.c[i] - ext; hi[i] = g.c[i] + ext;
+      }
+      // negated: a NaN pose skips the geom (no cell index from it)
+      reach = lo[2] <= hz && lo[0] <= sx && hi[0] >= -sx && lo[1] <= sy && hi[1] >= -sy && lo[2] <= size_z &&
+              hi[2] >= -zb;
+    }
   }
+  unsigned todo = unsigned(__ballot(reach) >> (threadIdx.x & ~(L - 1))) & 0x3Fu;  // team-uniform
   if (hf) {
-    const T sx = m.hf_sx, sy = m.hf_sy, zb = m.hf_bottom;
+    const T sx = m.hf_sx, sy = m.hf_sy;
     const int N1 = HF_N - 1;
-    for (int gi = 0; gi < 6; gi++) {
+    while (todo) {
+      const int gi = __builtin_ctz(todo);
+      todo &= todo - 1;
       Seg<T> g;
       body_geom(m, k, gi, g);
       Reach<T> gr;
@@ -931,9 +955,6 @@ __device__ bool body_candidates(const ModelT<T>& m, const Kin<T>& k, const float
         const T ext = gi == 0 ? g.hh * ai + g.r * sqrt(rad > 0 ? rad : T(0)) : g.hh * ai + g.r;
         lo[i] = g.c[i] - ext; hi[i] = g.c[i] + ext;
       }
-      if (!(lo[2] <= hz)) continue;
-      // negated: a NaN pose skips the geom (no cell index from it)
-      if (!(lo[0] <= sx && hi[0] >= -sx && lo[1] <= sy && hi[1] >= -sy && lo[2] <= size_z && hi[2] >= -zb)) continue;
       int cmin = (int)floor((lo[0] + sx) / (2 * sx) * N1), cmax = (int)ceil((hi[0] + sx) / (2 * sx) * N1);
       int rmin = (int)floor((lo[1] + sy) / (2 * sy) * N1), rmax = (int)ceil((hi[1] + sy) / (2 * sy) * N1);
       cmin = cmin < 0 ? 0 : cmin; cmax = cmax > N1 ? N1 : cmax;

@@ -78,8 +78,11 @@ def test_multi_step_flat_matches_single_steps(k, monkeypatch):
     a.close(), b.close()
 
 
-@pytest.mark.parametrize("route", ["1", "0"])
-def test_multi_step_perlin_hand_overs_match(route, monkeypatch):
+@pytest.mark.parametrize("route,park", [("1", "1"), ("1", "0"), ("0", "1")])
+def test_multi_step_perlin_hand_overs_match(route, park, monkeypatch):
+    """Route 1: multi_step_kernel, hand-overs parked for a second launch (BB_MULTI_PARK=1, the
+    default) or inline in one launch (0); route 0: relief_multi_kernel.  Bit-exact both ways."""
+    monkeypatch.setenv("BB_MULTI_PARK", park)  # read by bb_create
     n = 512
     a, b = _pair(n, "perlin", monkeypatch, route=route, n_terrains=None, stream_seeds=[50 + i for i in range(n)],
                  max_ep_steps=200)
