@@ -577,8 +577,15 @@ struct RolloutDev {
 // unclipped action, value, log-probability, reward and episode start; finished
 // episodes their (float64 return, length).  The step itself is team_step
 // (fast path, inline full-step hand-over, auto-reset).
-template <typename T>
-__global__ __launch_bounds__(64) void rollout_kernel(ModelT<T> mg, EnvCfg cfg, Dev d, RolloutDev ro, int L, int epw) {
+// Two launches (park != NULL), as multi_step_kernel: HO = false parks an env
+// at the step the fast path hands over (its state, observation and episode
+// counters as before that step; the policy rows it wrote are rewritten
+// identically), and HO = true resumes the parked envs from park[e] -- the
+// policy is fixed during a rollout, so an env's remaining steps need nothing
+// from the other envs.
+template <typename T, bool HO>
+__global__ __launch_bounds__(64) void rollout_kernel(ModelT<T> mg, EnvCfg cfg, Dev d, RolloutDev ro, int L, int epw,
+                                                     int* __restrict__ park) {
   extern __shared__ __align__(16) unsigned char smem[];
   const int nwg = int(gridDim.x), b = int(blockIdx.x);
   const int g = (nwg & 7) ? b : (b & 7) * (nwg >> 3) + (b >> 3);
@@ -591,6 +598,11 @@ __global__ __launch_bounds__(64) void rollout_kernel(ModelT<T> mg, EnvCfg cfg, D
   if (team >= epw) return;
   const int e = g * epw + team;
   if (unsigned(e) >= unsigned(d.n)) return;
+  int t0 = 0;
+  if (HO && park) {  // the finish launch: only parked envs, from their parked step
+    t0 = park[e];
+    if (t0 >= ro.T) return;  // team-uniform
+  }
   const bool lead = tm.tl == 0;
   EnvWork<T>& W = team_work<T>(smem, team);
   T* bk = reinterpret_cast<T*>(smem + size_t(epw) * work_stride<T>()) + team * (NQ + 2 * NV);
@@ -626,8 +638,9 @@ __global__ __launch_bounds__(64) void rollout_kernel(ModelT<T> mg, EnvCfg cfg, D
   long long len = ro.ep_len[e];
   const float* ls = ro.P + ro.off[MLP_LS];
   constexpr float HL2PI = 0.91893853320467274f;
+  int parked = ro.T;
 #pragma unroll 1
-  for (int t = 0; t < ro.T; t++) {
+  for (int t = t0; t < ro.T; t++) {
     const size_t row = size_t(t) * n + e;
     team_sync();
     if (tm.tl < 15) x[tm.tl] = o[tm.tl];
@@ -655,8 +668,18 @@ __global__ __launch_bounds__(64) void rollout_kernel(ModelT<T> mg, EnvCfg cfg, D
       ro.b_logp[row] = lp;
       ro.b_starts[row] = start;
     }
-    float r;
-    const int fl = team_step<T>(m, cfg, d, e, tid, q, v, w, step, bk, ac, W, o, r, nullptr, nullptr, 1, tm, cnt);
+    float r, o_prev[15];
+    if (!HO) {
+#pragma unroll
+      for (int i = 0; i < 15; i++) o_prev[i] = o[i];
+    }
+    const int fl = team_step<T, HO>(m, cfg, d, e, tid, q, v, w, step, bk, ac, W, o, r, nullptr, nullptr, 1, tm, cnt);
+    if (!HO && (fl & F_PARKED)) {  // team-uniform: the env resumes at step t in the finish launch
+#pragma unroll
+      for (int i = 0; i < 15; i++) o[i] = o_prev[i];
+      parked = t;
+      break;
+    }
     // collect_rollouts + Monitor bookkeeping (bb_rollout_track): done = terminated
     const bool dn = (fl & F_TERMINATED) != 0;
     ret += double(r);
@@ -674,6 +697,7 @@ __global__ __launch_bounds__(64) void rollout_kernel(ModelT<T> mg, EnvCfg cfg, D
   if (lead) {
     store_state(d, e, q, v, w, step);
     counts_flush(d, cnt);
+    if (!HO) park[e] = parked;
 #pragma unroll
     for (int i = 0; i < 15; i++) ro.obs[15 * size_t(e) + i] = o[i];
     ro.last_starts[e] = start;
@@ -1291,9 +1315,14 @@ int launch_rollout(bb_handle* h, const RolloutDev& ro, hipStream_t s) {
     hipLaunchKernelGGL((relief_multi_kernel<T, true>), dim3((h->n + QENV - 1) / QENV), dim3(64 * QW),
                        relief_lds_bytes<T>(), s, model_of<T>(h), h->cfg, dq, (const float*)nullptr, ro.T,
                        (float*)nullptr, (float*)nullptr, (uint8_t*)nullptr, (float*)nullptr, (float*)nullptr, 1, ro);
+  } else if (h->multi_park) {  // the fast steps, then the parked envs' hand-overs and the rest of their steps
+    hipLaunchKernelGGL((rollout_kernel<T, false>), dim3(blocks), dim3(WAVE), rollout_lds_bytes<T>(epw), s,
+                       model_of<T>(h), h->cfg, h->d, ro, h->team, epw, h->d.park);
+    hipLaunchKernelGGL((rollout_kernel<T, true>), dim3(blocks), dim3(WAVE), rollout_lds_bytes<T>(epw), s,
+                       model_of<T>(h), h->cfg, h->d, ro, h->team, epw, h->d.park);
   } else
-    hipLaunchKernelGGL(rollout_kernel<T>, dim3(blocks), dim3(WAVE), rollout_lds_bytes<T>(epw), s, model_of<T>(h),
-                       h->cfg, h->d, ro, h->team, epw);
+    hipLaunchKernelGGL((rollout_kernel<T, true>), dim3(blocks), dim3(WAVE), rollout_lds_bytes<T>(epw), s,
+                       model_of<T>(h), h->cfg, h->d, ro, h->team, epw, (int*)nullptr);
   HIPCHK(hipGetLastError());
   return 0;
 }
@@ -1489,9 +1518,10 @@ int bb_create(int n_envs, int device, const bb_params* p, bb_handle** out) {
                          h->fp64 ? (const void*)multi_step_kernel<double, true>
                                  : (const void*)multi_step_kernel<float, true>};
     for (const void* k : mk) HIPCHK(hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, mlb));
-    const void* rk = h->fp64 ? (const void*)rollout_kernel<double> : (const void*)rollout_kernel<float>;
     const int rlb = (int)(h->fp64 ? rollout_lds_bytes<double>(h->epw) : rollout_lds_bytes<float>(h->epw));
-    HIPCHK(hipFuncSetAttribute(rk, hipFuncAttributeMaxDynamicSharedMemorySize, rlb));
+    const void* rk[2] = {h->fp64 ? (const void*)rollout_kernel<double, false> : (const void*)rollout_kernel<float, false>,
+                         h->fp64 ? (const void*)rollout_kernel<double, true> : (const void*)rollout_kernel<float, true>};
+    for (const void* k : rk) HIPCHK(hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, rlb));
     const int qlb = (int)(h->fp64 ? relief_lds_bytes<double>() : relief_lds_bytes<float>());
     const void* qk[2] = {h->fp64 ? (const void*)relief_multi_kernel<double, false>
                                  : (const void*)relief_multi_kernel<float, false>,

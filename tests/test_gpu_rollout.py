@@ -67,12 +67,14 @@ def test_rollout_policy_matches_mlp_act():
     env.close()
 
 
-@pytest.mark.parametrize("terrain,route", [("flat", "1"), ("perlin", "1"), ("perlin", "0")])
-def test_rollout_steps_replay_bit_exact(terrain, route, monkeypatch):
+@pytest.mark.parametrize("terrain,route,park", [("flat", "1", "1"), ("perlin", "1", "1"), ("perlin", "1", "0"),
+                                               ("perlin", "0", "1")])
+def test_rollout_steps_replay_bit_exact(terrain, route, park, monkeypatch):
     """The kernel's env steps == bb_step on the kernel's own clipped actions.  Route 1 (fast
-    path, hand-over): rollout_kernel; route 0 on perlin (predictor): the relief work queue
-    with the policy in it."""
+    path, hand-over): rollout_kernel, hand-overs parked for a finish launch (BB_MULTI_PARK=1)
+    or inline (0); route 0 on perlin (predictor): the relief work queue with the policy in it."""
     monkeypatch.setenv("BB_ROUTE", route)
+    monkeypatch.setenv("BB_MULTI_PARK", park)
     n, T = (1024, 64) if terrain == "flat" else (256, 96)
     kw = {"max_ep_steps": 30} if terrain == "flat" else {"n_terrains": None, "max_ep_steps": 200,
                                                           "stream_seeds": [70 + i for i in range(256)]}
