@@ -28,11 +28,15 @@ HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
 FP64_VECTOR_PEAK_TFLOPS = 78.6  # MI355X spec: half the 157.3 TF FP32 vector rate (MI355X_MICROARCH.md)
 
 
-def algorithmic_bytes(precision: str) -> int:
-    """HBM bytes one env-step must move (state in and out, action, outputs)."""
+def algorithmic_bytes(precision: str, steps_per_launch: float = 1) -> float:
+    """HBM bytes one env-step must move: action in, obs/reward/done out, and the
+    env's state (qpos, qvel, qacc_warmstart, step counter, terrain id) read and
+    written once per launch -- every step with one bb_step launch per step, once
+    per K steps with bb_step_multi (the state stays on chip between its steps)."""
     es = 8 if precision == "fp64" else 4
     state = (17 + 15 + 15) * es      # qpos, qvel, qacc_warmstart
-    return 2 * state + 12 + 60 + 4 + 1 + 8 + 4  # r/w state, action, obs, reward, done, step r/w, terrain id
+    per_launch = 2 * state + 8 + 4   # r/w state, step counter r/w, terrain id
+    return per_launch / steps_per_launch + 12 + 60 + 4 + 1  # + action, obs, reward, done
 
 
 def cpu_baseline(seconds: float = 12.0, threads: int = 1) -> dict:
@@ -272,9 +276,11 @@ def main() -> None:
         dom = "fast" if ktimes["fast"] >= ktimes["predicted_full"] else "predicted_full"
         kern_ms = ktimes[dom]
         envs_dom = (n - full_per_step) if dom == "fast" else full_per_step
-        if M:  # one launch = up to M steps of every env (hand-overs included, inline)
+        spl = 1
+        if M:  # one launch = up to M steps of every env (hand-overs included)
             envs_dom = n * args.steps / kern_n
-        abytes = algorithmic_bytes(args.precision) * envs_dom
+            spl = args.steps / kern_n
+        abytes = algorithmic_bytes(args.precision, spl) * envs_dom
         achieved = abytes / (kern_ms * 1e-3) / 1e9
         traffic = issue_frac = None
         tj = Path(args.traffic_json)
@@ -314,8 +320,10 @@ def main() -> None:
                        "launch": launch},
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
-                         "note": "latency/VALU-bound per-lane physics; HBM bytes = algorithmic state I/O "
-                                 f"({algorithmic_bytes(args.precision)} B/env-step) x the envs the kernel stepped",
+                         "note": "latency/VALU-bound per-lane physics; HBM bytes = algorithmic I/O "
+                                 f"({algorithmic_bytes(args.precision, spl):.1f} B/env-step: state once per "
+                                 f"launch of {spl:g} steps, action and outputs every step) x the env-steps "
+                                 "of one launch",
                          "kernel": ((f"relief_multi_kernel<T> (work queue, {M} steps per launch)" if env.relief
                                      and os.environ.get("BB_MULTI_QUEUE", "1") != "0" and
                                      os.environ.get("BB_ROUTE", "0") == "0"

@@ -34,8 +34,13 @@ def select_ids(recs):
     hand-over full kernel comes after it)."""
     recs = sorted(recs, key=lambda r: int(r["Dispatch_Id"]))
     if SEL["which"] == "multi":
+        # multi_step_kernel<T, false> (the fast launch; the finish launch <T, true> only reads park[]
+        # on flat), or the single inline launch <T, true> under BB_MULTI_PARK=0, or relief_multi_kernel
+        ms = [r for r in recs if "multi_step_kernel" in r["Kernel_Name"]]
+        if any(", false>" in r["Kernel_Name"] for r in ms):
+            ms = [r for r in ms if ", false>" in r["Kernel_Name"]]
         return [int(r["Dispatch_Id"]) for r in recs
-                if "multi_step_kernel" in r["Kernel_Name"] or "relief_multi_kernel" in r["Kernel_Name"]]
+                if r in ms or "relief_multi_kernel" in r["Kernel_Name"]]
     if SEL["which"] == "fast":
         return [int(r["Dispatch_Id"]) for r in recs if is_fast(r["Kernel_Name"])]
     out, last_full = [], None
