@@ -37,8 +37,12 @@ template <int CTRL>
 __device__ __forceinline__ float dpp(float v) {
   return __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), CTRL, 0xF, 0xF, true));
 }
+// doubles: row_newbcast (0x150 + j) is the one DPP control gfx950 applies to a
+// 64-bit move (v_mov_b64_dpp, DPP64); the other patterns move two 32-bit halves
 template <int CTRL>
 __device__ __forceinline__ double dpp(double v) {
+  if constexpr (CTRL >= 0x150 && CTRL <= 0x15F)
+    return __longlong_as_double(__builtin_amdgcn_mov_dpp(__double_as_longlong(v), CTRL, 0xF, 0xF, true));
   const unsigned long long u = (unsigned long long)__double_as_longlong(v);
   const int lo = __builtin_amdgcn_mov_dpp((int)(unsigned)u, CTRL, 0xF, 0xF, true);
   const int hi = __builtin_amdgcn_mov_dpp((int)(unsigned)(u >> 32), CTRL, 0xF, 0xF, true);
