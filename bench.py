@@ -153,7 +153,7 @@ def main() -> None:
                     help="perlin: all envs on one terrain seed stream (train.py's convention) instead of one per env")
     ap.add_argument("--graph", action="store_true",
                     help="replay the step as one HIP graph (kernel_ms is then timed on eager steps after the run)")
-    ap.add_argument("--multi-step", type=int, default=64,
+    ap.add_argument("--multi-step", type=int, default=256,
                     help="M steps per launch (bb_step_multi: the benchmark's random actions are known in advance, so "
                          "each env runs its M steps back to back, bit-identical to M bb_step calls); 0: one bb_step "
                          "launch per step.  With M > 0 the line also reports the per-launch form under 'per_step'")
@@ -210,23 +210,32 @@ def main() -> None:
         if args.cameras:
             env._render(force=False)
     g = torch.Generator(device=dev).manual_seed(1234 + rank)
-    pool = torch.rand(64, n, 3, generator=g, device=dev) * 2 - 1  # random actions resident in HBM
+    PS = 256  # action pool slots: random actions resident in HBM, reused cyclically
+    pool = torch.rand(PS, n, 3, generator=g, device=dev) * 2 - 1
     M = args.multi_step
-    if M and (args.cameras or args.graph or not 1 <= M <= 64):
+    if M and (args.cameras or args.graph or not 1 <= M <= PS):
         M = 0  # the cameras render between steps; a captured graph holds one bb_step
     if M:
         mo = torch.empty(M, n, 15, device=dev)
         mr = torch.empty(M, n, device=dev)
         md = torch.empty(M, n, dtype=torch.uint8, device=dev)
 
+    def chunks(count, m):  # launch sizes: up to m steps each, none crossing the end of the pool
+        out, j = [], 0
+        while j < count:
+            out.append(min(m, count - j, PS - j % PS))
+            j += out[-1]
+        return out
+
     def run(count, m):  # `count` steps from pool slot 0 on, m per launch (0: one bb_step per step)
         if m:
-            for j in range(0, count, m):
-                k = min(m, count - j)
-                env.step_multi_raw(pool[j % 64:j % 64 + k], mo[:k], mr[:k], md[:k])
+            j = 0
+            for k in chunks(count, m):
+                env.step_multi_raw(pool[j % PS:j % PS + k], mo[:k], mr[:k], md[:k])
+                j += k
         else:
             for i in range(count):
-                step(pool[i % 64])
+                step(pool[i % PS])
 
     def timed(m):
         """args.steps steps, m per launch, bracketed by barrier + synchronize; the MAX over ranks."""
@@ -235,7 +244,7 @@ def main() -> None:
             dist.barrier()
         torch.cuda.synchronize()
         ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-        env.time_kernel(-(-args.steps // max(m, 1)))  # HIP events around each step-kernel launch, on its stream
+        env.time_kernel(len(chunks(args.steps, m)) if m else args.steps)  # HIP events around each launch, on its stream
         st0 = env.stats()
         t0 = time.perf_counter()
         ev0.record()
@@ -251,7 +260,7 @@ def main() -> None:
         if graph is not None:  # graph replays carry no per-kernel events: time eager steps of the same kernels
             env.time_kernel(min(args.steps, 100))
             for i in range(min(args.steps, 100)):
-                env.step_async_raw(pool[i % 64])
+                env.step_async_raw(pool[i % PS])
             torch.cuda.synchronize()
         ktimes, kern_n = env.kernel_times()  # fast (or multi-step), predicted-full (side stream), hand-over full
         return max_over_ranks(elapsed, device=dev), step_ms, ktimes, kern_n, st0, st1

@@ -334,7 +334,11 @@ int bb_step(bb_handle* h, const float* actions_dev, float* obs_dev, float* rewar
  * float[k][n][15]; reward_dev float[k][n]; done_dev uint8[k][n];
  * terminal_obs_dev float[k][n][15] and pos2d_dev float[k][n][2] may be NULL.
  * No reference counterpart (its VecEnv steps once per call,
- * ballbot_env.py:854); the per-step semantics are bb_step's. */
+ * ballbot_env.py:854); the per-step semantics are bb_step's.  On banks
+ * without relief this is two launches on `stream`: the fast steps, with envs
+ * whose step the fast path hands over parked at that step, then a finish
+ * launch that resumes the parked envs (BB_MULTI_PARK=0 at bb_create: one
+ * launch, hand-overs inline); relief banks use one work-queue launch. */
 int bb_step_multi(bb_handle* h, const float* actions_dev, int k_steps, float* obs_dev, float* reward_dev,
                   uint8_t* done_dev, float* terminal_obs_dev, float* pos2d_dev, int auto_reset, void* stream);
 

@@ -5,8 +5,10 @@ set -o pipefail
 O=gpurun_out/final
 mkdir -p $O
 export TMPDIR=/tmp
+if [ "${SKIP_TESTS:-0}" != "1" ]; then
 timeout -k 10 600 python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread > $O/pytest_gpu.log 2>&1 || { tail -30 $O/pytest_gpu.log; exit 1; }
 tail -2 $O/pytest_gpu.log
+fi
 timeout -k 10 200 python -u -c "import __graft_entry__ as g; g.smoke()" > $O/smoke.log 2>&1 || { cat $O/smoke.log; exit 1; }
 cat $O/smoke.log | tail -1
 run() {  # name, args...
