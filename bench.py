@@ -39,6 +39,17 @@ def algorithmic_bytes(precision: str, steps_per_launch: float = 1) -> float:
     return per_launch / steps_per_launch + 12 + 60 + 4 + 1  # + action, obs, reward, done
 
 
+def launch_chunks(count: int, m: int, pool_slots: int) -> list:
+    """bb_step_multi launch sizes for `count` steps from action-pool slot 0 on: up
+    to m steps each, none crossing the end of the pool (actions are reused
+    cyclically from a pool of `pool_slots` steps)."""
+    out, j = [], 0
+    while j < count:
+        out.append(min(m, count - j, pool_slots - j % pool_slots))
+        j += out[-1]
+    return out
+
+
 def cpu_baseline(seconds: float = 12.0, threads: int = 1) -> dict:
     """The fp64 oracle (a port of the reference step semantics, not MuJoCo) on
     `threads` host cores (one env per OpenMP thread), random actions, flat terrain."""
@@ -220,12 +231,8 @@ def main() -> None:
         mr = torch.empty(M, n, device=dev)
         md = torch.empty(M, n, dtype=torch.uint8, device=dev)
 
-    def chunks(count, m):  # launch sizes: up to m steps each, none crossing the end of the pool
-        out, j = [], 0
-        while j < count:
-            out.append(min(m, count - j, PS - j % PS))
-            j += out[-1]
-        return out
+    def chunks(count, m):
+        return launch_chunks(count, m, PS)
 
     def run(count, m):  # `count` steps from pool slot 0 on, m per launch (0: one bb_step per step)
         if m:

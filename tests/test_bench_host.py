@@ -1,0 +1,42 @@
+"""bench.py host logic (CPU): the algorithmic-byte model behind roofline.achieved
+and the launch chunking of the multi-step bench."""
+import sys
+from pathlib import Path
+
+import pytest
+
+sys.path.insert(0, str(Path(__file__).resolve().parents[1]))
+import bench  # noqa: E402
+
+
+def test_algorithmic_bytes_one_step_per_launch():
+    # fp64 841 B per env-step (state r/w 752, action 12, obs 60, reward 4, done 1,
+    # step counter r/w 8, terrain id 4); fp32 465 B
+    assert bench.algorithmic_bytes("fp64") == 841
+    assert bench.algorithmic_bytes("fp32") == 465
+
+
+@pytest.mark.parametrize("k", [2, 20, 64, 256])
+def test_algorithmic_bytes_multi_step_moves_state_once(k):
+    per_launch = 2 * 47 * 8 + 8 + 4
+    assert bench.algorithmic_bytes("fp64", k) == pytest.approx(per_launch / k + 77)
+    # K steps of one env in one launch move less than K single-step launches
+    assert k * bench.algorithmic_bytes("fp64", k) < k * bench.algorithmic_bytes("fp64")
+
+
+@pytest.mark.parametrize("count,m,pool", [(500, 256, 256), (500, 64, 256), (20, 256, 256), (700, 200, 256),
+                                          (1, 1, 256), (513, 256, 256)])
+def test_launch_chunks_cover_the_steps_within_the_pool(count, m, pool):
+    ch = bench.launch_chunks(count, m, pool)
+    assert sum(ch) == count
+    assert all(1 <= k <= m for k in ch)
+    j = 0
+    for k in ch:  # no launch reads past the end of the action pool
+        assert j % pool + k <= pool
+        j += k
+
+
+def test_launch_chunks_driver_window_is_one_launch():
+    # the driver's --steps 20 --warmup 5: one 20-step launch
+    assert bench.launch_chunks(20, 256, 256) == [20]
+    assert bench.launch_chunks(500, 256, 256) == [256, 244]
