@@ -21,3 +21,7 @@ run bench_flat_fp64_short --steps 20 --warmup 5 --no-cpu-baseline
 run bench_flat_fp32 --precision fp32 --no-cpu-baseline
 run bench_perlin --terrain perlin --no-cpu-baseline
 run bench_hills --terrain hills --no-cpu-baseline
+if [ "${QUEUE_AB:-0}" = "1" ]; then  # relief banks through the parked multi-step kernels instead of the work queue
+  BB_MULTI_QUEUE=0 run bench_hills_noqueue --terrain hills --no-cpu-baseline
+  BB_MULTI_QUEUE=0 run bench_perlin_noqueue --terrain perlin --no-cpu-baseline
+fi
