@@ -340,7 +340,11 @@ def main() -> None:
                                  f"({algorithmic_bytes(args.precision, spl):.1f} B/env-step: state once per "
                                  f"launch of {spl:g} steps, action and outputs every step) x the env-steps "
                                  "of one launch",
-                         "kernel": ((f"relief_multi_kernel<T> (work queue, {M} steps per launch)" if env.relief
+                         "kernel": ((f"relief_multi_kernel<T> (work queue) or the parked multi_step_kernel<T,*> "
+                                     f"launches, chosen per launch from the last one's full steps ({M} steps per "
+                                     "launch)" if env.relief and "BB_MULTI_QUEUE" not in os.environ and
+                                     "BB_ROUTE" not in os.environ and os.environ.get("BB_MULTI_ADAPT", "1") != "0"
+                                     else f"relief_multi_kernel<T> (work queue, {M} steps per launch)" if env.relief
                                      and os.environ.get("BB_MULTI_QUEUE", "1") != "0" and
                                      os.environ.get("BB_ROUTE", "0") == "0"
                                      else f"multi_step_kernel<T,false> ({M} steps per launch; hand-overs parked "

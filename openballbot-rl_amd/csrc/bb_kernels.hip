@@ -316,6 +316,11 @@ int full_env_step(const ModelT<T>& m, const EnvCfg& cfg, T* q, T* v, T* w, int& 
 // redoes that step through the hand-over and counts it there.
 constexpr int F_PARKED = 1 << 17;  // internal: never in a done byte
 
+// bb_step_multi on relief banks, adaptive form (slow_count slots): SC_ROUTE holds
+// the next launch's form (0: the work queue, ROUTE_PARK: the parked multi-step
+// launches), SC_TOUCHED counts the envs of the last launch that needed a full step
+constexpr int SC_ROUTE = 8, SC_TOUCHED = 10, ROUTE_PARK = 1;
+
 template <typename T, bool HO = true>
 __device__ __forceinline__ int team_step(const ModelT<T>& m, const EnvCfg& cfg, const Dev& d, int e, int& tid,
                                          T* q, T* v, T* w, int& step, T* bk, const float* a, EnvWork<T>& W, float* o,
@@ -415,7 +420,10 @@ __global__ __launch_bounds__(64) void multi_step_kernel(ModelT<T> mg, EnvCfg cfg
                                                         int K, float* __restrict__ obs, float* __restrict__ rew,
                                                         uint8_t* __restrict__ done, float* __restrict__ tobs,
                                                         float* __restrict__ pos2d, int auto_reset, int L, int epw,
-                                                        int* __restrict__ park) {
+                                                        int* __restrict__ park, const int* __restrict__ gate) {
+  // gate (relief banks, adaptive form): run only when the device flag selects the
+  // parked launches (ROUTE_PARK); workgroup-uniform, before any barrier
+  if (gate && *gate != ROUTE_PARK) return;
   extern __shared__ __align__(16) unsigned char smem[];
   const int nwg = int(gridDim.x), b = int(blockIdx.x);
   const int g = (nwg & 7) ? b : (b & 7) * (nwg >> 3) + (b >> 3);  // XCD-aware order, as step_kernel
@@ -475,6 +483,7 @@ __global__ __launch_bounds__(64) void multi_step_kernel(ModelT<T> mg, EnvCfg cfg
     store_state(d, e, q, v, w, step);
     counts_flush(d, cnt);
     if (!HO) park[e] = parked;
+    if (!HO && gate && parked < K) atomicAdd(d.slow_count + SC_TOUCHED, 1);  // adaptive: an env that needed a full step
   }
 }
 
@@ -919,7 +928,9 @@ __global__ __launch_bounds__(64 * QW) void relief_multi_kernel(ModelT<T> mg, Env
                                                                const float* __restrict__ act, int K,
                                                                float* __restrict__ obs, float* __restrict__ rew,
                                                                uint8_t* __restrict__ done, float* __restrict__ tobs,
-                                                               float* __restrict__ pos2d, int auto_reset, RolloutDev ro) {
+                                                               float* __restrict__ pos2d, int auto_reset, RolloutDev ro,
+                                                               const int* __restrict__ gate) {
+  if (gate && *gate == ROUTE_PARK) return;  // adaptive form: the parked launches run instead
   extern __shared__ __align__(16) unsigned char smem[];
   __shared__ ModelT<T> ms;
   __shared__ int s_k[QENV], s_busy[QENV], s_kind[QENV], s_tid[QENV], s_step[QENV], s_env[QENV];
@@ -1085,6 +1096,7 @@ __global__ __launch_bounds__(64 * QW) void relief_multi_kernel(ModelT<T> mg, Env
     EnvWork<T>& W = team_work<T>(smem, i);
     store_state(d, e, W.qn, W.vn, W.wn, s_step[i]);
     counts_flush(d, s_cnt[i]);
+    if (!RO && gate && s_cnt[i][3]) atomicAdd(d.slow_count + SC_TOUCHED, 1);  // adaptive: an env that took a full step
     if (RO) {
 #pragma unroll
       for (int j = 0; j < 15; j++) ro.obs[15 * size_t(e) + j] = s_obs[i][j];
@@ -1163,6 +1175,19 @@ __global__ void zero_count_kernel(int* c) {
   if (threadIdx.x == 0) *c = 0;
 }
 
+// after an adaptive bb_step_multi on a relief bank: the next launch takes the
+// parked multi-step form when fewer than `max_touched` envs needed a full step
+// in this one (1: none -- hills' flat centre in steady state), else the work
+// queue.  One env parked early already costs the parked form a serial finish
+// launch of nearly K steps, so the queue takes over at the first one.
+// Deterministic: the choice depends on the envs' results only (no host sync).
+__global__ void route_decide_kernel(int* sc, int max_touched) {
+  if (threadIdx.x == 0) {
+    sc[SC_ROUTE] = sc[SC_TOUCHED] < max_touched ? ROUTE_PARK : 0;
+    sc[SC_TOUCHED] = 0;
+  }
+}
+
 __global__ void assign_kernel(Dev d, const int32_t* ids) {
   const int e = blockIdx.x * blockDim.x + threadIdx.x;
   if (e >= d.n) return;
@@ -1200,6 +1225,8 @@ struct bb_handle {
   int route = -1;
   int multi_queue = 1;          // bb_step_multi on relief banks: relief_multi_kernel (BB_MULTI_QUEUE=0: off)
   int multi_park = 1;           // bb_step_multi, serial route: two launches, hand-overs parked (BB_MULTI_PARK=0: one)
+  int multi_adapt = 1;          // bb_step_multi on relief banks: queue or parked launches per launch (BB_MULTI_ADAPT=0:
+                                // always the queue; off when BB_ROUTE or BB_MULTI_QUEUE fixes the form)
   int balance = 1;              // relief_multi_kernel: cost-balanced env placement (BB_BALANCE=0: in order)
   std::vector<uint8_t> relief;  // per terrain: max height > 0
   int n_relief = 0;
@@ -1314,7 +1341,8 @@ int launch_rollout(bb_handle* h, const RolloutDev& ro, hipStream_t s) {
     const Dev dq = balanced_dev(h, s);
     hipLaunchKernelGGL((relief_multi_kernel<T, true>), dim3((h->n + QENV - 1) / QENV), dim3(64 * QW),
                        relief_lds_bytes<T>(), s, model_of<T>(h), h->cfg, dq, (const float*)nullptr, ro.T,
-                       (float*)nullptr, (float*)nullptr, (uint8_t*)nullptr, (float*)nullptr, (float*)nullptr, 1, ro);
+                       (float*)nullptr, (float*)nullptr, (uint8_t*)nullptr, (float*)nullptr, (float*)nullptr, 1, ro,
+                       (const int*)nullptr);
   } else if (h->multi_park) {  // the fast steps, then the parked envs' hand-overs and the rest of their steps
     hipLaunchKernelGGL((rollout_kernel<T, false>), dim3(blocks), dim3(WAVE), rollout_lds_bytes<T>(epw), s,
                        model_of<T>(h), h->cfg, h->d, ro, h->team, epw, h->d.park);
@@ -1336,21 +1364,39 @@ int launch_multi(bb_handle* h, const float* a, int K, float* o, float* r, uint8_
   hipEvent_t* ev = timed ? &h->tev[6 * h->tn] : nullptr;
   const int route = h->route >= 0 ? h->route : (h->n_relief == 0 ? 1 : 0);
   if (timed) HIPCHK(hipEventRecord(ev[0], s));
-  if (route == 0 && h->team == 16 && h->multi_queue) {  // relief banks: the per-workgroup work queue
+  const size_t mlb = multi_lds_bytes<T>(epw);
+  if (route == 0 && h->team == 16 && h->multi_queue && h->multi_adapt && h->multi_park) {
+    // relief banks, adaptive: the parked launches or the work queue, as the
+    // device flag chose after the last launch (the others exit at once)
+    const int* gate = h->d.slow_count + SC_ROUTE;
+    const Dev dq = balanced_dev(h, s);
+    hipLaunchKernelGGL((multi_step_kernel<T, false>), dim3(blocks), dim3(WAVE), mlb, s, model_of<T>(h), h->cfg, h->d,
+                       a, K, o, r, dn, t, p2, ar, h->team, epw, h->d.park, gate);
+    hipLaunchKernelGGL((multi_step_kernel<T, true>), dim3(blocks), dim3(WAVE), mlb, s, model_of<T>(h), h->cfg, h->d,
+                       a, K, o, r, dn, t, p2, ar, h->team, epw, h->d.park, gate);
+    hipLaunchKernelGGL((relief_multi_kernel<T, false>), dim3((h->n + QENV - 1) / QENV), dim3(64 * QW),
+                       relief_lds_bytes<T>(), s, model_of<T>(h), h->cfg, dq, a, K, o, r, dn, t, p2, ar, RolloutDev{},
+                       gate);
+    if (timed) HIPCHK(hipEventRecord(ev[1], s));
+    hipLaunchKernelGGL(route_decide_kernel, dim3(1), dim3(64), 0, s, h->d.slow_count, 1);
+  } else if (route == 0 && h->team == 16 && h->multi_queue) {  // relief banks: the per-workgroup work queue
     const Dev dq = balanced_dev(h, s);
     hipLaunchKernelGGL((relief_multi_kernel<T, false>), dim3((h->n + QENV - 1) / QENV), dim3(64 * QW),
-                       relief_lds_bytes<T>(), s, model_of<T>(h), h->cfg, dq, a, K, o, r, dn, t, p2, ar, RolloutDev{});
-  } else if (h->multi_park) {  // the fast steps, then the parked envs' hand-overs and the rest of their steps
-    hipLaunchKernelGGL((multi_step_kernel<T, false>), dim3(blocks), dim3(WAVE), multi_lds_bytes<T>(epw), s,
-                       model_of<T>(h), h->cfg, h->d, a, K, o, r, dn, t, p2, ar, h->team, epw, h->d.park);
+                       relief_lds_bytes<T>(), s, model_of<T>(h), h->cfg, dq, a, K, o, r, dn, t, p2, ar, RolloutDev{},
+                       (const int*)nullptr);
     if (timed) HIPCHK(hipEventRecord(ev[1], s));
-    hipLaunchKernelGGL((multi_step_kernel<T, true>), dim3(blocks), dim3(WAVE), multi_lds_bytes<T>(epw), s,
-                       model_of<T>(h), h->cfg, h->d, a, K, o, r, dn, t, p2, ar, h->team, epw, h->d.park);
-  } else
-    hipLaunchKernelGGL((multi_step_kernel<T, true>), dim3(blocks), dim3(WAVE), multi_lds_bytes<T>(epw), s,
-                       model_of<T>(h), h->cfg, h->d, a, K, o, r, dn, t, p2, ar, h->team, epw, (int*)nullptr);
+  } else if (h->multi_park) {  // the fast steps, then the parked envs' hand-overs and the rest of their steps
+    hipLaunchKernelGGL((multi_step_kernel<T, false>), dim3(blocks), dim3(WAVE), mlb, s, model_of<T>(h), h->cfg, h->d,
+                       a, K, o, r, dn, t, p2, ar, h->team, epw, h->d.park, (const int*)nullptr);
+    if (timed) HIPCHK(hipEventRecord(ev[1], s));
+    hipLaunchKernelGGL((multi_step_kernel<T, true>), dim3(blocks), dim3(WAVE), mlb, s, model_of<T>(h), h->cfg, h->d,
+                       a, K, o, r, dn, t, p2, ar, h->team, epw, h->d.park, (const int*)nullptr);
+  } else {
+    hipLaunchKernelGGL((multi_step_kernel<T, true>), dim3(blocks), dim3(WAVE), mlb, s, model_of<T>(h), h->cfg, h->d,
+                       a, K, o, r, dn, t, p2, ar, h->team, epw, (int*)nullptr, (const int*)nullptr);
+    if (timed) HIPCHK(hipEventRecord(ev[1], s));
+  }
   if (timed) {
-    if (!h->multi_park || (route == 0 && h->team == 16 && h->multi_queue)) HIPCHK(hipEventRecord(ev[1], s));
     HIPCHK(hipEventRecord(ev[5], s));
     h->tpred[h->tn] = 0;
     h->tn++;
@@ -1436,6 +1482,8 @@ int bb_create(int n_envs, int device, const bb_params* p, bb_handle** out) {
     h->epw_full = epf;
     const char* rt = getenv("BB_ROUTE");
     if (rt) h->route = atoi(rt);
+    const char* ad = getenv("BB_MULTI_ADAPT");
+    if ((ad && atoi(ad) == 0) || rt || getenv("BB_MULTI_QUEUE")) h->multi_adapt = 0;
     const char* mp = getenv("BB_MULTI_PARK");
     if (mp) h->multi_park = atoi(mp) != 0;
     const char* mq = getenv("BB_MULTI_QUEUE");

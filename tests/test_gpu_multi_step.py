@@ -109,6 +109,30 @@ def test_multi_step_relief_queue_ragged_workgroups(monkeypatch):
     a.close(), b.close()
 
 
+@pytest.mark.parametrize("terrain", ["hills", "perlin"])
+def test_multi_step_adaptive_relief_route(terrain, monkeypatch):
+    """Relief banks with no route fixed: each bb_step_multi runs the work queue (route 0) or the
+    parked launches (route 1), as the device flag chose from the previous launch's full steps
+    (hills: rarely any, the parked form; perlin: many, the queue).  Against one bb_step per step
+    on the serial route the results agree to rounding, launch after launch."""
+    from ballbot_gym.envs import BallbotVecEnv
+
+    n = 512 if terrain == "hills" else 256
+    kw = dict(device="cuda:0", seed=3, terrain_config={"type": terrain, "config": {}}, max_ep_steps=50)
+    if terrain == "perlin":
+        kw.update(n_terrains=None, stream_seeds=[60 + i for i in range(n)])
+    monkeypatch.setenv("BB_ROUTE", "1")
+    a = BallbotVecEnv(n, **kw)
+    for var in ("BB_ROUTE", "BB_MULTI_QUEUE", "BB_MULTI_ADAPT"):
+        monkeypatch.delenv(var, raising=False)
+    b = BallbotVecEnv(n, **kw)  # adaptive
+    g = torch.Generator(device="cuda:0").manual_seed(7)
+    actions = torch.rand(192, n, 3, generator=g, device="cuda:0") * 2 - 1
+    st = _compare_runs(a, b, actions, 32, exact=False)
+    assert st["resets"] > 0
+    a.close(), b.close()
+
+
 def test_multi_step_rejects_bad_shapes():
     from ballbot_gym.envs import BallbotVecEnv
 
