@@ -36,11 +36,15 @@ def select_ids(recs):
     if SEL["which"] == "multi":
         # multi_step_kernel<T, false> (the fast launch; the finish launch <T, true> only reads park[]
         # on flat), or the single inline launch <T, true> under BB_MULTI_PARK=0, or relief_multi_kernel
+        # relief banks: relief_multi_kernel (with the adaptive route the gated multi-step launches
+        # of a queue launch exit at once; a parked launch would show as multi_step_kernel<T, false>)
+        rq = [int(r["Dispatch_Id"]) for r in recs if "relief_multi_kernel" in r["Kernel_Name"]]
+        if rq:
+            return rq
         ms = [r for r in recs if "multi_step_kernel" in r["Kernel_Name"]]
         if any(", false>" in r["Kernel_Name"] for r in ms):
             ms = [r for r in ms if ", false>" in r["Kernel_Name"]]
-        return [int(r["Dispatch_Id"]) for r in recs
-                if r in ms or "relief_multi_kernel" in r["Kernel_Name"]]
+        return [int(r["Dispatch_Id"]) for r in ms]
     if SEL["which"] == "fast":
         return [int(r["Dispatch_Id"]) for r in recs if is_fast(r["Kernel_Name"])]
     out, last_full = [], None
