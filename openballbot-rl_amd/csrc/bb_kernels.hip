@@ -1621,6 +1621,7 @@ int bb_set_hfield(bb_handle* h, int terrain_id, const float* data, float size_z)
   for (int i = 0; i < HF_N * HF_N; i++) hm = data[i] > hm ? data[i] : hm;
   HIPCHK(hipMemcpy(h->hmax + terrain_id, &hm, sizeof(float), hipMemcpyHostToDevice));
   set_relief(h, terrain_id, hm > 0.f);
+  HIPCHK(hipMemset(h->d.slow_count + SC_ROUTE, 0, sizeof(int)));  // a new bank: the adaptive route restarts at the queue
   HIPCHK(hipMemcpy(h->size_z + terrain_id, &size_z, sizeof(float), hipMemcpyHostToDevice));
   HIPCHK(hipMemcpy(h->offset + terrain_id, &off, sizeof(float), hipMemcpyHostToDevice));
   return 0;
@@ -1651,6 +1652,7 @@ int bb_generate_perlin(bb_handle* h, int first, int count, const int32_t* seeds,
   std::vector<float> hm(count);
   HIPCHK(hipMemcpy(hm.data(), h->hmax + first, sizeof(float) * count, hipMemcpyDeviceToHost));
   for (int i = 0; i < count; i++) set_relief(h, first + i, hm[i] > 0.f);
+  HIPCHK(hipMemset(h->d.slow_count + SC_ROUTE, 0, sizeof(int)));  // a new bank: the adaptive route restarts at the queue
   return 0;
 }
 
