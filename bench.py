@@ -28,15 +28,19 @@ HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
 FP64_VECTOR_PEAK_TFLOPS = 78.6  # MI355X spec: half the 157.3 TF FP32 vector rate (MI355X_MICROARCH.md)
 
 
-def algorithmic_bytes(precision: str, steps_per_launch: float = 1) -> float:
-    """HBM bytes one env-step must move: action in, obs/reward/done out, and the
-    env's state (qpos, qvel, qacc_warmstart, step counter, terrain id) read and
-    written once per launch -- every step with one bb_step launch per step, once
-    per K steps with bb_step_multi (the state stays on chip between its steps)."""
+def algorithmic_bytes(precision: str, steps_per_launch: float = 1, relief: bool = False) -> float:
+    """HBM bytes one env-step must move: action in, obs/reward/done/terminal
+    obs/pos2d out, and the env's state (qpos, qvel, qacc_warmstart, step
+    counter, terrain id) read and written once per launch -- every step with one
+    bb_step launch per step, once per K steps with bb_step_multi (the state
+    stays on chip between its steps).  relief: + the heightfield vertices under
+    the ball's AABB, 7 x 7 float32 per forward read once per env-step (SURVEY.md
+    §8 D4: +196 B on uneven terrain)."""
     es = 8 if precision == "fp64" else 4
     state = (17 + 15 + 15) * es      # qpos, qvel, qacc_warmstart
     per_launch = 2 * state + 8 + 4   # r/w state, step counter r/w, terrain id
-    return per_launch / steps_per_launch + 12 + 60 + 4 + 1  # + action, obs, reward, done
+    out = 60 + 4 + 1 + 60 + 8        # obs, reward, done, terminal obs, pos2d
+    return per_launch / steps_per_launch + 12 + out + (196 if relief else 0)
 
 
 def launch_chunks(count: int, m: int, pool_slots: int) -> list:
@@ -101,17 +105,21 @@ def flop_count(env, terrain: str, n_envs: int = 16, n_steps: int = 400, burn_in:
     sys.path.insert(0, str(ROOT / "tools"))
     import flops as F
 
+    from ballbot_gym.envs.config import stream_draws
+
     plan = env.terrain_plan
-    if plan.streams is None:
+    drawn = plan.stream_seeds is not None
+    if not drawn:
         slots = [0]
-    else:
-        slots = list(dict.fromkeys(int(plan.streams[s][0]) for s in range(min(n_fields, len(plan.streams)))))
+    else:  # the first terrains drawn by the first n_fields generators
+        firsts = [int(stream_draws(s, 1)[0]) for s in list(dict.fromkeys(plan.stream_seeds))[:n_fields]]
+        slots = list(dict.fromkeys(max(plan.slot_of(s), 0) for s in firsts))
     rs = [F.count(F.lib(), env.hfield(s), float(plan.size_z), n_envs, n_steps, burn_in=burn_in) for s in slots]
     fl = float(np.mean([r["flops_per_env_step"] for r in rs]))
     by = {k: float(np.mean([r["flops_by_phase"][k] for r in rs])) for k in rs[0]["flops_by_phase"]}
     return {"flops_per_env_step": fl, "by_phase": by,
             "sample": (f"{len(slots)} terrain(s) of the '{terrain}' bank (seeds {[int(plan.seeds[s]) for s in slots]})"
-                       if plan.streams is not None else f"the '{terrain}' terrain") +
+                       if drawn else f"the '{terrain}' terrain") +
                       f" x {n_envs} envs x {n_steps} counted steps after {burn_in} uncounted, uniform random actions, "
                       "auto-reset; MuJoCo solver settings (tolerance 1e-8, line search 0.01 / 50 evaluations)"}
 
@@ -158,10 +166,11 @@ def main() -> None:
     ap.add_argument("--precision", default="fp64", choices=["fp32", "fp64"])
     ap.add_argument("--terrain", default="flat")
     ap.add_argument("--n-terrains", type=int, default=None,
-                    help="terrain bank size (default: 16 host-generated seeds; perlin: the whole 10^4 seed space on the GPU)")
+                    help="draws per generator whose terrains the bank holds (default: the whole 10^4 seed space for "
+                         "per-env generators -- perlin generated on the GPU, others on a host process pool)")
     ap.add_argument("--cameras", action="store_true", help="also render the depth cameras (F2) every 6 steps")
     ap.add_argument("--shared-stream", action="store_true",
-                    help="perlin: all envs on one terrain seed stream (train.py's convention) instead of one per env")
+                    help="all envs on one terrain seed generator np_random(1000) instead of np_random(1000 + env id)")
     ap.add_argument("--graph", action="store_true",
                     help="replay the step as one HIP graph (kernel_ms is then timed on eager steps after the run)")
     ap.add_argument("--multi-step", type=int, default=256,
@@ -198,16 +207,15 @@ def main() -> None:
 
     # weak scaling: every rank owns a contiguous block of `--envs` global env ids
     first_env, n = env_shard(args.envs * world, rank, world)
-    # terrain draws: "random uneven heightfield" (configs[2]) -- on the GPU-generated perlin
-    # bank every env draws from its own generator, seed 1000 + global env id (the eval
-    # VecEnv's per-env seeds, train.py:90-97), so the 4096 envs sample 4096 terrain
-    # sequences; the training convention (one shared stream, train.py:82-89) would put
-    # every env on the same terrain at the start.  Host-generated banks: the shared stream.
-    per_env = args.terrain == "perlin" and not args.shared_stream
+    # terrain draws: global env g draws its terrain seeds from np_random(1000 + g) on the GPU
+    # (SB3's seeding of a training VecEnv, train.py:126-141), so 4096 envs sample 4096
+    # terrain sequences -- configs[2]'s "random uneven heightfield"; --shared-stream puts
+    # every env on np_random(1000) (all envs start on the same terrain)
+    per_env = not args.shared_stream
     env = BallbotVecEnv(n, device=dev, precision=args.precision, seed=1000,
                         terrain_config={"type": args.terrain, "config": {}}, n_terrains=args.n_terrains,
-                        disable_cameras=not args.cameras,
-                        stream_seeds=shard_stream_seeds(1000, first_env, n, per_env=True) if per_env else None)
+                        disable_cameras=not args.cameras, shared_stream=not per_env,
+                        stream_seeds=shard_stream_seeds(1000, first_env, n) if per_env else None)
 
     static_a = torch.zeros(n, 3, device=dev)
     graph = env.capture_step(static_a) if args.graph else None  # one rollout step = one HIP graph
@@ -217,7 +225,7 @@ def main() -> None:
             static_a.copy_(a)
             graph.replay()
             return
-        env.step_async_raw(a)
+        env.step_async_raw(a, full_outputs=True)
         if args.cameras:
             env._render(force=False)
     g = torch.Generator(device=dev).manual_seed(1234 + rank)
@@ -226,10 +234,12 @@ def main() -> None:
     M = args.multi_step
     if M and (args.cameras or args.graph or not 1 <= M <= PS):
         M = 0  # the cameras render between steps; a captured graph holds one bb_step
-    if M:
+    if M:  # every output of the step: obs, reward, done, terminal obs and pos2d (A11's info)
         mo = torch.empty(M, n, 15, device=dev)
         mr = torch.empty(M, n, device=dev)
         md = torch.empty(M, n, dtype=torch.uint8, device=dev)
+        mt = torch.empty(M, n, 15, device=dev)
+        mp = torch.empty(M, n, 2, device=dev)
 
     def chunks(count, m):
         return launch_chunks(count, m, PS)
@@ -238,7 +248,7 @@ def main() -> None:
         if m:
             j = 0
             for k in chunks(count, m):
-                env.step_multi_raw(pool[j % PS:j % PS + k], mo[:k], mr[:k], md[:k])
+                env.step_multi_raw(pool[j % PS:j % PS + k], mo[:k], mr[:k], md[:k], mt[:k], mp[:k])
                 j += k
         else:
             for i in range(count):
@@ -296,7 +306,7 @@ def main() -> None:
         if M:  # one launch = up to M steps of every env (hand-overs included)
             envs_dom = n * args.steps / kern_n
             spl = args.steps / kern_n
-        abytes = algorithmic_bytes(args.precision, spl) * envs_dom
+        abytes = algorithmic_bytes(args.precision, spl, env.relief) * envs_dom
         achieved = abytes / (kern_ms * 1e-3) / 1e9
         traffic = issue_frac = None
         tj = Path(args.traffic_json)
@@ -337,9 +347,10 @@ def main() -> None:
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
                          "note": "latency/VALU-bound per-lane physics; HBM bytes = algorithmic I/O "
-                                 f"({algorithmic_bytes(args.precision, spl):.1f} B/env-step: state once per "
-                                 f"launch of {spl:g} steps, action and outputs every step) x the env-steps "
-                                 "of one launch",
+                                 f"({algorithmic_bytes(args.precision, spl, env.relief):.1f} B/env-step: state "
+                                 f"once per launch of {spl:g} steps, action and all five outputs every step"
+                                 + (", 7x7 hfield vertices per step" if env.relief else "") +
+                                 ") x the env-steps of one launch",
                          "kernel": ((f"relief_multi_kernel<T> (work queue) or the parked multi_step_kernel<T,*> "
                                      f"launches, chosen per launch from the last one's full steps ({M} steps per "
                                      "launch)" if env.relief and "BB_MULTI_QUEUE" not in os.environ and

@@ -8,8 +8,10 @@
  *                    (+ hfield_size[2] rescale                  ballbot_env.py:486-495)
  *                    (+ init height offset                      ballbot_env.py:527-565)
  *   bb_generate_perlin  generate_perlin_terrain per seed       terrain/perlin.py:8-74
- *   bb_set_terrain_stream  r_seed = _np_random.integers(0, 10000) ballbot_env.py:378-384,
- *                    at every reset, one generator per env        :505-510 (train.py:82-89)
+ *   bb_set_terrain_rng     r_seed = _np_random.integers(0, 10000) ballbot_env.py:505-510,
+ *                    at every reset, numpy's PCG64 per env on the    :378-384, 596 (SB3 reset(seed=seed+i),
+ *                    GPU (gymnasium np_random)                       train.py:82-97, 126-141)
+ *   bb_set_terrain_stream  the same draws as a host-made table   ballbot_env.py:505-510
  *   bb_assign_terrain   pin a terrain per env (config seed)     ballbot_env.py:505-510
  *   bb_reset         mj_resetData + height offset + mj_forward  ballbot_env.py:612-620
  *   bb_step          ctrl = -clip(10a); mj_step; _get_obs;      ballbot_env.py:903-1036
@@ -54,7 +56,7 @@
 extern "C" {
 #endif
 
-#define BB_ABI_VERSION 14
+#define BB_ABI_VERSION 15
 #define BB_NQ 17
 #define BB_NV 15
 #define BB_OBS 15
@@ -89,7 +91,7 @@ typedef struct {
   float goal[2];               /* distance reward goal */
   float goal_scale;            /* distance reward scale */
   int n_terrains;              /* terrain bank size (>= 1) */
-  uint64_t seed;               /* unused since ABI 12 (terrain draws: bb_set_terrain_stream) */
+  uint64_t seed;               /* unused since ABI 12 (terrain draws: bb_set_terrain_rng / _stream) */
   int fp64;                    /* 1 (default): fp64 arithmetic, 0: fp32 */
   int solver_maxiter;          /* 0 = default */
   double solver_tol;           /* 0 = default */
@@ -302,17 +304,43 @@ int bb_get_hfield(bb_handle* h, int terrain_id, float* data_host);
  * again).  A pinned reset takes no stream draw (a fixed config seed,
  * ballbot_env.py:505-510). */
 int bb_assign_terrain(bb_handle* h, const int32_t* ids_dev, void* stream);
-/* terrain seed streams (ballbot_env.py:378-384, 505-510): each reset of env e
+/* terrain seed streams as host tables (ballbot_env.py:378-384, 505-510): each reset of env e
  * that is not pinned takes the next draw of stream env_stream_host[e] (NULL:
  * all envs stream 0, n_streams must be 1): the k-th reset of the env (k = 0 at
  * the first reset after this call) gets bank slot slots_host[s * length + k],
  * i.e. the slot holding the terrain of the k-th value of the stream's
  * np_random(seed).integers(0, 10000).  Past `length` draws the stream wraps
- * around (counted in stats[5]).  Resets every env's draw counter to 0.
- * n_streams = 0 removes the streams (unpinned envs then reset onto slot 0).
- * Synchronous; a HIP graph captured before this call keeps the old streams. */
+ * around (counted in stats[5]).  Resets every env's draw counter to 0 and
+ * turns off the device generators of bb_set_terrain_rng.  n_streams = 0
+ * removes the streams (unpinned envs then reset onto slot 0).  Synchronous.
+ * The table is refilled in place while n_streams * length fits the allocation
+ * of an earlier call (a HIP graph captured before then reads the new table); a
+ * larger table is a new allocation, and replaying a graph captured before that
+ * call is invalid. */
 int bb_set_terrain_stream(bb_handle* h, const int32_t* slots_host, int n_streams, int length,
                           const int32_t* env_stream_host);
+/* terrain seed draws on the GPU, one numpy PCG64 generator per env
+ * (gymnasium.utils.seeding.np_random = Generator(PCG64(SeedSequence(seed)))):
+ * every reset of env e that is not pinned draws r_seed = integers(0, 10000)
+ * from env e's generator (ballbot_env.py:505-510), bit-exact and without an
+ * end, and resets onto bank slot seed_slot_host[r_seed] (seed_slot_host NULL:
+ * slot == seed, the bank must hold all 10000 seeds; an entry of -1 marks a seed
+ * that is not resident: such a draw is counted in stats[5] and takes slot
+ * r_seed % n_terrains).  words_host uint64[n][5] is each generator's state as
+ * numpy's PCG64.state holds it: state >> 64, state & (2^64-1), inc >> 64,
+ * inc & (2^64-1), and (has_uint32 << 32) | uinteger.  words_host NULL turns
+ * the device generators off.  Resets every env's draw counter to 0.
+ * Synchronous; the buffers are allocated at the first call and refilled in
+ * place, so a graph captured before a later call reads the new generators.
+ * Replaces the per-env _np_random of BBotSimulation as SB3 seeds it: VecEnv.seed(seed)
+ * then reset(seed=seed+i) (gymnasium Env.reset replaces _np_random,
+ * ballbot_env.py:596; train.py:126-141), and an eval env's np_random(seed + N_ENVS + i)
+ * (:378-384, train.py:90-97). */
+int bb_set_terrain_rng(bb_handle* h, const uint64_t* words_host, const int32_t* seed_slot_host);
+/* the device generators (uint64[n][5], as bb_set_terrain_rng takes them; may be
+ * NULL) and the terrain seed of each env's last device draw (int32[n], -1 before
+ * the first; may be NULL) */
+int bb_get_terrain_rng(bb_handle* h, uint64_t* words_host, int32_t* last_seed_host);
 /* current bank slot and number of stream draws of every env (host int32[n] each, may be NULL) */
 int bb_get_env_terrain(bb_handle* h, int32_t* terrain_host, int32_t* draws_host);
 
@@ -352,7 +380,7 @@ int bb_forward(bb_handle* h, const double* ctrl, double* qacc, int32_t* ncontact
  * with done bit 2), overflow (env-steps where a geom pair hit MuJoCo's mjMAXCONPAIR = 50 contacts and
  * was truncated, as MuJoCo does), slow-path env-steps (envs the fast kernel handed to the full
  * kernel: base-tree geom contacts possible), Newton iterations, resets past the end of their
- * terrain stream, env-steps whose last RK stage stored base-tree contacts past the 32 LDS slots
+ * terrain stream table or onto a drawn seed not resident in the bank, env-steps whose last RK stage stored base-tree contacts past the 32 LDS slots
  * (the per-env HBM spill block)] */
 int bb_get_stats(bb_handle* h, int64_t* out, int n);
 /* launch configuration: [n_envs, envs_per_wave, fp64, lds_bytes_per_workgroup,

@@ -25,22 +25,28 @@ def env_shard(num_envs_total: int, rank: int, world: int) -> Tuple[int, int]:
     return start, base + (1 if rank < extra else 0)
 
 
-def shard_stream_seeds(seed: int, first_env: int, count: int, per_env: bool = False) -> Optional[List[int]]:
-    """Terrain seed streams of a rank's env block (BallbotVecEnv stream_seeds).
+def shard_stream_seeds(seed: int, first_env: int, count: int, per_env: bool = True) -> Optional[List[int]]:
+    """Terrain generator seeds of a rank's env block (BallbotVecEnv stream_seeds).
 
-    Training envs all draw from np_random(seed) (eval_env=[True, seed] for every
-    env, train.py:82-89): None, i.e. every local env on that one stream, the
-    same on every rank.  per_env: global env g draws from np_random(seed + g),
-    the eval VecEnv's seed + N_ENVS + env_i (train.py:90-97) with seed the base."""
+    per_env (default): global env g draws from np_random(seed + g) -- SB3 seeds
+    training env g with reset(seed=seed+g) (VecEnv.seed, train.py:126-141;
+    ballbot_env.py:596), and the eval VecEnv gives env i seed + N_ENVS + i
+    (train.py:90-97, with seed the eval base).  per_env=False: None, every
+    local env on the one generator np_random(seed) (BallbotVecEnv(...,
+    shared_stream=True); the convention an unseeded PPO would leave)."""
     if not per_env:
         return None
-    return [int(seed) + int(first_env) + i for i in range(int(count))]
+    from .envs.config import sb3_stream_seeds
+
+    return sb3_stream_seeds(seed, count, first_env)
 
 
 def max_over_ranks(value: float, device=None) -> float:
     """All-reduce MAX of a scalar (elapsed time); identity without a process group."""
     if not (dist.is_available() and dist.is_initialized()) or dist.get_world_size() == 1:
         return float(value)
+    if dist.get_backend() == "gloo":  # host tensors on gloo (rehearsals sharing one GPU)
+        device = None
     t = torch.tensor([float(value)], dtype=torch.float64, device=device)
     dist.all_reduce(t, op=dist.ReduceOp.MAX)
     return float(t.item())

@@ -13,9 +13,14 @@ reference's keys; camera keys when cameras are on), the reward a Python float
 
 Terrain seeds as the reference draws them (:378-384, :505-510, :596-599,
 :658-661): eval_env=[True, s] fixes _np_random = np_random(s) at
-construction; otherwise the generator is np_random(seed) of the FIRST reset,
-and that first reset also draws the log-dir permutation after its terrain
-draw.  Every later reset draws the next value of integers(0, 10000).
+construction; reset(seed=s) with s not None replaces it by np_random(s)
+(gymnasium's Env.reset, :596), in eval mode too; a reset with no generator yet
+seeds one from OS entropy (:597-599).  Every reset draws r_seed =
+integers(0, 10000) from it (unless the terrain config fixes a seed), and a
+non-eval env's first reset then draws the log-dir permutation (:655-661).  The
+host runs that generator and generates the drawn terrain into a small ring of
+bank slots (the GPU perlin generator, or the registered plugin), as the
+reference regenerates the heightfield at every reset (:501-513).
 
 Not provided: the MuJoCo viewer (GUI), RGB video rendering (`render()`) and
 the per-episode log files (_save_logs) -- outside the hot path.
@@ -23,6 +28,7 @@ the per-episode log files (_save_logs) -- outside the hot path.
 from __future__ import annotations
 
 import string
+from collections import OrderedDict
 from typing import Any, Dict, Optional
 
 import numpy as np
@@ -31,6 +37,7 @@ from .. import spaces
 from .config import np_random
 
 DT = 0.002  # ballbot.xml:3 (opt.timestep)
+RING_SLOTS = 4  # bank slots of the single env: the terrains of its latest draws
 
 
 class BBotSimulation:
@@ -40,7 +47,7 @@ class BBotSimulation:
                  log_options=None, max_ep_steps=None, terrain_type: str = "perlin", eval_env=(False, None),
                  reward_config=None, terrain_config=None, env_config=None, render_mode: Optional[str] = None,
                  viewer_title: Optional[str] = None, device: str = "cuda:0", precision: str = "fp64",
-                 n_terrains: Optional[int] = None):
+                 n_terrains: Optional[int] = None, reward_compat: str = "reference"):
         if render_mode is not None and render_mode not in self.metadata["render_modes"]:
             raise ValueError(f"Invalid render_mode: {render_mode}. Supported modes: {self.metadata['render_modes']}")
         if GUI:
@@ -59,7 +66,6 @@ class BBotSimulation:
         cam["disable_rgb"] = True
         env_config["camera"] = cam
         self._env_config = env_config
-        self._max_ep_steps_arg = max_ep_steps
         self.max_ep_steps = int((env_config.get("env", {}) or {}).get(
             "max_ep_steps", max_ep_steps if max_ep_steps is not None else 4000))
         self.disable_cameras = bool(disable_cameras)
@@ -72,53 +78,73 @@ class BBotSimulation:
         self.action_space = spaces.action_space()
         self.observation_space = spaces.observation_space({"h": cam["height"], "w": cam["width"]}, 1,
                                                           self.disable_cameras)
-        self._device, self._precision, self._n_terrains = device, precision, n_terrains
         self.eval_env = bool(eval_env[0])
-        self._eval_seed = eval_env[1]
-        self._env = None
         self.step_counter = 0
         self.num_episodes = -1
         self.last_r_seed = None
-        if self.eval_env:  # _np_random fixed now (ballbot_env.py:378-384); the first reset draws from it
-            self._build(np_random(self._eval_seed), first_permutation=False)
+        self._log_drawn = False  # the non-eval log-dir permutation (first reset only, ballbot_env.py:655-661)
+        # eval mode: _np_random fixed now (ballbot_env.py:378-384); else seeded by the first reset
+        self._np_random = np_random(eval_env[1]) if self.eval_env else None
+        # a ring of bank slots holding the terrains of the latest draws (n_terrains slots, default 4)
+        from .vec_env import BallbotVecEnv
+
+        self._ring = max(1, int(n_terrains or RING_SLOTS))
+        self._slot_of: "OrderedDict[int, int]" = OrderedDict()
+        self._env = BallbotVecEnv(1, device=device, reward_config=self.reward_config,
+                                  terrain_config=self.terrain_config, env_config=self._env_config,
+                                  max_ep_steps=max_ep_steps, precision=precision, auto_reset=False,
+                                  disable_cameras=self.disable_cameras, terrain_slots=self._ring,
+                                  reward_compat=reward_compat)
 
     @property
     def opt_timestep(self) -> float:
         return DT
 
-    # ------------------------------------------------------------------ setup
-    def _build(self, gen: np.random.Generator, first_permutation: bool) -> None:
-        """The backing one-env BallbotVecEnv, with this env's terrain stream."""
-        from .config import FULL_BANK_DRAWS_PER_ENV, NUMPY_BANK_DRAWS, TERRAIN_SEED_HIGH
-        from .vec_env import BallbotVecEnv
+    @property
+    def np_random(self) -> np.random.Generator:
+        """gymnasium's Env.np_random: the terrain generator (seeded from OS entropy if unset)."""
+        if self._np_random is None:
+            self._np_random = np_random(None)
+        return self._np_random
 
-        k = self._n_terrains or (FULL_BANK_DRAWS_PER_ENV if self.terrain_type == "perlin" else NUMPY_BANK_DRAWS)
-        draws = [int(gen.integers(0, TERRAIN_SEED_HIGH))]
-        if first_permutation:  # the log-dir name of a non-eval env's first reset (ballbot_env.py:658-661)
-            gen.permutation(list(string.ascii_letters + string.digits))
-        draws += [int(x) for x in gen.integers(0, TERRAIN_SEED_HIGH, size=k - 1)]
-        self._draws = draws
-        self._env = BallbotVecEnv(1, device=self._device, reward_config=self.reward_config,
-                                  terrain_config=self.terrain_config, env_config=self._env_config,
-                                  max_ep_steps=self._max_ep_steps_arg, precision=self._precision,
-                                  n_terrains=k,  # the bank holds the distinct seeds of these draws
-                                  auto_reset=False, disable_cameras=self.disable_cameras,
-                                  terrain_draws=draws)
-        self._fresh = True  # constructed = reset once (draw 0)
+    # ------------------------------------------------------------------ setup
+    def _slot(self, r_seed) -> int:
+        """Bank slot holding the terrain of r_seed, generated into the least
+        recently used ring slot if it is not resident (ballbot_env.py:501-513)."""
+        from .config import terrain_is_seedless
+
+        tc = self.terrain_config
+        key = -1 if (tc.get("type", "flat") == "flat" or terrain_is_seedless(tc)) else int(r_seed)
+        if key in self._slot_of:
+            self._slot_of.move_to_end(key)
+            return self._slot_of[key]
+        if len(self._slot_of) < self._ring:
+            slot = len(self._slot_of)
+        else:
+            _, slot = self._slot_of.popitem(last=False)
+        self._env.load_terrain(slot, None if key == -1 and tc.get("type", "flat") == "flat" else int(r_seed))
+        self._slot_of[key] = slot
+        return slot
 
     # -------------------------------------------------------------------- api
     def reset(self, seed=None, goal: str = "random", **kwargs):
-        """ballbot_env.py:567-671: next terrain draw, init height offset, zero state -> (obs, info)."""
-        if self._env is None:  # non-eval: _np_random = np_random(seed of the first reset)
-            self._build(np_random(seed), first_permutation=True)
-        if self._fresh:
-            self._fresh = False
-        else:
-            self._env.reset()
+        """ballbot_env.py:567-671: (re)seed the generator, draw the terrain seed,
+        init height offset, zero state -> (obs, info)."""
+        from .config import TERRAIN_SEED_HIGH
+
+        if seed is not None:  # gymnasium Env.reset(seed) replaces _np_random (ballbot_env.py:596)
+            self._np_random = np_random(seed)
+        gen = self.np_random
+        cfg_seed = (self.terrain_config.get("config", {}) or {}).get("seed")
+        r_seed = int(gen.integers(0, TERRAIN_SEED_HIGH)) if cfg_seed is None else int(cfg_seed)
+        self.last_r_seed = r_seed
+        if not self.eval_env and not self._log_drawn:  # the /tmp/log_<12 chars> name (ballbot_env.py:655-661)
+            gen.permutation(list(string.ascii_letters + string.digits))
+            self._log_drawn = True
+        self._env.assign_terrain(np.array([self._slot(r_seed)], np.int32))
+        self._env.reset()
         self.num_episodes += 1
         self.step_counter = 0
-        cfg_seed = (self.terrain_config.get("config", {}) or {}).get("seed")
-        self.last_r_seed = cfg_seed if cfg_seed is not None else self._draws[self.num_episodes % len(self._draws)]
         obs = self._obs()
         return obs, self._info(np.zeros(2, np.float32), False)
 

@@ -31,13 +31,18 @@ class BallbotVecEnv:
     `device`, `precision` ("fp32" | "fp64") and the terrain bank size.
 
     Terrain seeds follow the reference's per-reset draw r_seed =
-    _np_random.integers(0, 10000) (ballbot_env.py:505-510) with the generator
-    fixed at construction (eval_env=[True, seed], :378-384): by default every
-    env shares np_random(seed), as train.py:82-89 builds all training envs, so
-    the k-th reset of every env gets the k-th draw; `stream_seeds` gives env i
-    its own generator np_random(stream_seeds[i]) (an eval VecEnv: seed + N + i,
-    train.py:90-97).  `n_terrains` is the number of draws per stream kept
-    resident (perlin default: the whole seed space on the GPU, 65536 draws).
+    _np_random.integers(0, 10000) (ballbot_env.py:505-510), drawn on the GPU
+    from numpy's PCG64 per env (bb_set_terrain_rng).  By default env i draws
+    from np_random(seed + i): SB3 seeds the training VecEnv that way
+    (VecEnv.seed(seed), then reset(seed=seed+i) in learn(); gymnasium's
+    Env.reset replaces _np_random, ballbot_env.py:596; train.py:126-141).
+    `stream_seeds` gives env i np_random(stream_seeds[i]) (an eval VecEnv:
+    seed + N_ENVS + i, train.py:90-97); `shared_stream=True` puts every env on
+    np_random(seed).  `seed(s)` re-seeds env i to np_random(s + i) at the next
+    reset(), as SB3's VecEnv.seed does.  `n_terrains`: the draws per generator
+    whose terrains a host-generated bank holds (perlin default: the whole
+    10^4-seed space, generated on the GPU).  `terrain_draws`: an explicit list
+    of terrain seeds that every env walks instead (a replayed draw log).
     """
 
     metadata = {"render_modes": []}
@@ -58,8 +63,11 @@ class BallbotVecEnv:
         disable_cameras: bool = True,
         stream_seeds: Optional[Sequence[int]] = None,
         terrain_draws: Optional[Sequence[int]] = None,
+        shared_stream: bool = False,
+        terrain_slots: Optional[int] = None,
+        reward_compat: str = "reference",
     ):
-        from .config import bank_fields, gpu_perlin_plan, params_from_configs, terrain_plan
+        from .config import params_from_configs
 
         if not torch.cuda.is_available():
             raise RuntimeError("BallbotVecEnv needs a ROCm GPU (torch.cuda.is_available() is False)")
@@ -81,36 +89,27 @@ class BallbotVecEnv:
         self.terrain_config = terrain_config or {"type": "flat", "config": {}}
         self.reward_config = reward_config or {"type": "directional", "config": {"target_direction": [0.0, 1.0]}}
         p, self.reward_obj, self._host_reward = params_from_configs(self.reward_config, env_config, max_ep_steps,
-                                                                    precision, seed)
+                                                                    precision, seed, reward_compat=reward_compat)
+        from .config import reward_error
+
+        # reward_compat="reference": a DistanceReward raises at the first step, as
+        # in the reference env (its obs lacks pos2d); "fused": the kernel computes it
+        self._reward_error = reward_error(self.reward_obj, reward_compat)
         self.max_ep_steps = int(p.max_ep_steps)
-        gp = gpu_perlin_plan(self.terrain_config, n_terrains, seed, self.num_envs, stream_seeds, terrain_draws)
-        if gp is None:
-            plan = terrain_plan(self.terrain_config, n_terrains, seed, self.num_envs, stream_seeds,
-                                draws=terrain_draws)
-            bank = [(h, plan.size_z) for h in bank_fields(self.terrain_config, plan)]
-        else:  # perlin: generated on the GPU below
-            plan, pcfg = gp
-            bank = []
-        self.terrain_plan = plan
-        self.terrain_seeds = plan.seeds
-        size_z = plan.size_z
-        p.n_terrains = len(plan.seeds)
         self.precision = "fp64" if p.fp64 else "fp32"
         self._params = p
-        L = N.lib()
-        h = C.c_void_p()
-        N.check(L.bb_create(self.num_envs, self.device.index or 0, C.byref(p), C.byref(h)), "bb_create")
-        self._h = h
-        for i, (data, size_z) in enumerate(bank):
-            arr = np.ascontiguousarray(data, dtype=np.float32)
-            N.check(L.bb_set_hfield(h, i, arr.ctypes.data_as(C.POINTER(C.c_float)), float(size_z)), "bb_set_hfield")
-        if gp is not None:
-            sd = np.ascontiguousarray(self.terrain_seeds, dtype=np.int32)
-            N.check(L.bb_generate_perlin(h, 0, len(sd), sd.ctypes.data_as(C.POINTER(C.c_int32)), C.byref(pcfg),
-                                         float(size_z)), "bb_generate_perlin")
-        self.n_terrains = p.n_terrains
-        # any terrain with relief: bb_step routes through the predictor (route 0) on such banks
-        self.relief = gp is not None or any(float(np.max(data)) > 0.0 for data, _ in bank)
+        self._seed = int(seed)
+        self._n_terrains_arg = n_terrains
+        self._shared_stream = bool(shared_stream)
+        self._pending_seeds: Optional[list] = None
+        self._h = None
+        if terrain_slots is not None:  # host-driven terrains (load_terrain + assign_terrain), e.g. BBotSimulation
+            from .config import TerrainPlan, terrain_size_z
+
+            plan = TerrainPlan([-1] * int(terrain_slots), None, None, False, terrain_size_z(self.terrain_config))
+            self._install(plan, generate=False)
+        else:
+            self._install(self._plan(stream_seeds, terrain_draws))
         n, dev = self.num_envs, self.device
         self.obs = torch.zeros(n, N.NOBS, dtype=torch.float32, device=dev)
         self.terminal_obs = torch.zeros(n, N.NOBS, dtype=torch.float32, device=dev)
@@ -120,25 +119,109 @@ class BallbotVecEnv:
         if self.cameras:
             self.depth = torch.ones(n, 2, self.cam_h, self.cam_w, dtype=torch.float32, device=dev)
             self.rel_ts = torch.zeros(n, dtype=torch.float32, device=dev)
-        if plan.streams is not None:  # every later reset takes its stream's next draw
-            st = np.ascontiguousarray(plan.streams, dtype=np.int32)
-            es = None if plan.env_stream is None else np.ascontiguousarray(plan.env_stream, dtype=np.int32)
-            ip = C.POINTER(C.c_int32)
-            N.check(L.bb_set_terrain_stream(h, st.ctypes.data_as(ip), st.shape[0], st.shape[1],
-                                            None if es is None else es.ctypes.data_as(ip)), "bb_set_terrain_stream")
         from .. import spaces
 
         # SB3 VecEnv / gymnasium attributes (ballbot_env.py:235-256)
         self.action_space = spaces.action_space()
         self.observation_space = spaces.observation_space({"h": self.cam_h, "w": self.cam_w}, 1, not self.cameras)
         self._pending_actions: Optional[torch.Tensor] = None
-        self.reset()  # the first reset: draw 0 of every env's stream
+        self.reset()  # the first reset: draw 0 of every env's generator
+
+    # ------------------------------------------------------------ terrain bank
+    def _plan(self, stream_seeds=None, terrain_draws=None):
+        from .config import gpu_perlin_plan, terrain_plan
+
+        gp = gpu_perlin_plan(self.terrain_config, self._n_terrains_arg, self._seed, self.num_envs, stream_seeds,
+                             terrain_draws, shared=self._shared_stream)
+        if gp is not None:
+            return gp[0]
+        return terrain_plan(self.terrain_config, self._n_terrains_arg, self._seed, self.num_envs, stream_seeds,
+                            draws=terrain_draws, shared=self._shared_stream)
+
+    def _install(self, plan, generate: bool = True) -> None:
+        """A handle whose bank holds the plan's terrains, with its generators
+        (bb_set_terrain_rng) or draw table (bb_set_terrain_stream) installed."""
+        from .config import bank_fields, perlin_cfg
+
+        perlin = self._gpu_perlin()
+        bank = []
+        if generate and not perlin:
+            bank = [(h, plan.size_z) for h in bank_fields(self.terrain_config, plan)]
+        p = self._params
+        p.n_terrains = len(plan.seeds)
+        L = N.lib()
+        if self._h is not None:
+            L.bb_destroy(self._h)
+            self._h = None
+        h = C.c_void_p()
+        N.check(L.bb_create(self.num_envs, self.device.index or 0, C.byref(p), C.byref(h)), "bb_create")
+        self._h = h
+        for i, (data, size_z) in enumerate(bank):
+            arr = np.ascontiguousarray(data, dtype=np.float32)
+            N.check(L.bb_set_hfield(h, i, arr.ctypes.data_as(C.POINTER(C.c_float)), float(size_z)), "bb_set_hfield")
+        if generate and perlin:
+            sd = np.ascontiguousarray(plan.seeds, dtype=np.int32)
+            N.check(L.bb_generate_perlin(h, 0, len(sd), sd.ctypes.data_as(C.POINTER(C.c_int32)),
+                                         C.byref(perlin_cfg(self.terrain_config)), float(plan.size_z)),
+                    "bb_generate_perlin")
+        self.terrain_plan = plan
+        self.terrain_seeds = plan.seeds
+        self.n_terrains = p.n_terrains
+        # any terrain with relief: bb_step routes through the predictor (route 0) on such banks
+        self.relief = (generate and perlin) or any(float(np.max(data)) > 0.0 for data, _ in bank)
+        self._set_draws(plan)
+
+    def _gpu_perlin(self) -> bool:
+        tc = self.terrain_config
+        return tc.get("type", "flat") == "perlin" and (tc.get("config", {}) or {}).get("seed") is None
+
+    def _set_draws(self, plan) -> None:
+        L, ip = N.lib(), C.POINTER(C.c_int32)
+        if plan.stream_seeds is not None:  # one PCG64 per env on the device
+            words = np.ascontiguousarray(plan.rng_words())
+            ss = None if plan.seed_slot is None else np.ascontiguousarray(plan.seed_slot, dtype=np.int32)
+            N.check(L.bb_set_terrain_rng(self._h, words.ctypes.data_as(C.POINTER(C.c_uint64)),
+                                         None if ss is None else ss.ctypes.data_as(ip)), "bb_set_terrain_rng")
+        elif plan.streams is not None:  # an explicit draw table
+            st = np.ascontiguousarray(plan.streams, dtype=np.int32)
+            es = None if plan.env_stream is None else np.ascontiguousarray(plan.env_stream, dtype=np.int32)
+            N.check(L.bb_set_terrain_stream(self._h, st.ctypes.data_as(ip), st.shape[0], st.shape[1],
+                                            None if es is None else es.ctypes.data_as(ip)), "bb_set_terrain_stream")
+
+    def _reseed(self, stream_seeds) -> None:
+        """Put env i on np_random(stream_seeds[i]) from its next reset on (its draw
+        counter restarts).  A bank that lacks the new generators' first draws is
+        regenerated, on a new handle: HIP graphs captured before this are invalid."""
+        from .config import stream_draws, terrain_plan
+
+        plan = self.terrain_plan
+        if plan.stream_seeds is None and plan.streams is None:
+            return  # one fixed terrain (flat or a config seed): nothing is drawn
+        stream_seeds = [int(x) for x in stream_seeds]
+        if len(stream_seeds) != self.num_envs:
+            raise ValueError(f"need one seed per env ({self.num_envs}), got {len(stream_seeds)}")
+        k = self._n_terrains_arg or 8
+        need = {int(v) for s in dict.fromkeys(stream_seeds) for v in stream_draws(s, k)}
+        if plan.stream_seeds is not None and plan.covers(need):
+            from .config import TerrainPlan
+
+            new = TerrainPlan(plan.seeds, stream_seeds, plan.seed_slot, plan.full, plan.size_z, seedless=plan.seedless)
+            self.terrain_plan = new
+            self._set_draws(new)
+            return
+        self._install(self._plan(stream_seeds))
 
     # --------------------------------------------------------------------- api
     def _stream(self):
         return C.c_void_p(torch.cuda.current_stream(self.device).cuda_stream)
 
     def reset(self, mask: Optional[torch.Tensor] = None):
+        """Reset every env (mask None) or the masked ones -> (obs, {}).  A full
+        reset first applies the seeds of seed(), as SB3's VecEnv.reset passes
+        seed + i to env i's reset (then forgets them)."""
+        if mask is None and self._pending_seeds is not None:
+            pending, self._pending_seeds = self._pending_seeds, None
+            self._reseed(pending)
         m = None if mask is None else mask.to(device=self.device, dtype=torch.uint8).contiguous()
         N.check(N.lib().bb_reset(self._h, _ptr(m), _ptr(self.obs), self._stream()), "bb_reset")
         if self.cameras:
@@ -167,6 +250,8 @@ class BallbotVecEnv:
                 "bb_step")
         if self.cameras:  # envs whose counter hit the frame interval (incl. auto-resets) re-render
             self._render(force=False)
+        if self._reward_error:  # after mj_step, as the reference's reward call (ballbot_env.py:912, 929)
+            raise ValueError(self._reward_error)
         terminated = (self.done & N.DONE_TERMINATED) != 0
         info = {"done_flags": self.done, "terminal_observation": self.terminal_obs, "pos2d": self.pos2d,
                 "failure": (self.done & N.DONE_FAILURE) != 0}
@@ -182,6 +267,8 @@ class BallbotVecEnv:
         if self._host_reward is not None:
             obs, reward, _, _, info = self.step(actions)
             return obs, reward, info["done_flags"]
+        if self._reward_error:
+            raise ValueError(self._reward_error)
         if actions.device != self.device or actions.dtype != torch.float32 or not actions.is_contiguous() \
                 or actions.shape != (self.num_envs, 3):
             raise ValueError(f"actions must be a contiguous float32 ({self.num_envs}, 3) tensor on {self.device}")
@@ -198,6 +285,8 @@ class BallbotVecEnv:
         steps every env with whatever `actions` holds (one launch per rollout step)."""
         if actions.shape != (self.num_envs, 3) or actions.dtype != torch.float32 or not actions.is_contiguous():
             raise ValueError("capture_step needs a contiguous float32 [num_envs, 3] action buffer")
+        if self._reward_error:
+            raise ValueError(self._reward_error)
         graph = torch.cuda.CUDAGraph()
         side = torch.cuda.Stream(device=self.device)
         side.wait_stream(torch.cuda.current_stream(self.device))
@@ -226,6 +315,8 @@ class BallbotVecEnv:
             raise RuntimeError("step_multi does not render the depth cameras; step() does")
         if self._host_reward is not None:
             raise RuntimeError("step_multi needs a built-in reward (a host plugin runs per step())")
+        if self._reward_error:
+            raise ValueError(self._reward_error)
         if actions.device != self.device or actions.dtype != torch.float32 or not actions.is_contiguous() \
                 or actions.dim() != 3 or actions.shape[1:] != (self.num_envs, 3):
             raise ValueError(f"actions must be a contiguous float32 (K, {self.num_envs}, 3) tensor on {self.device}")
@@ -242,10 +333,12 @@ class BallbotVecEnv:
         return out
 
     def step_multi_raw(self, actions: torch.Tensor, obs: torch.Tensor, reward: torch.Tensor,
-                       done: torch.Tensor) -> None:
-        """Launch-only bb_step_multi (benchmarking): caller-owned [K, N, ...] outputs, no terminal obs / pos2d."""
+                       done: torch.Tensor, terminal_obs: Optional[torch.Tensor] = None,
+                       pos2d: Optional[torch.Tensor] = None) -> None:
+        """Launch-only bb_step_multi (benchmarking): caller-owned [K, N, ...] outputs
+        (terminal obs / pos2d optional)."""
         N.lib().bb_step_multi(self._h, _ptr(actions), int(actions.shape[0]), _ptr(obs), _ptr(reward), _ptr(done),
-                              None, None, int(self.auto_reset), self._stream())
+                              _ptr(terminal_obs), _ptr(pos2d), int(self.auto_reset), self._stream())
 
     def run_rollout(self, args) -> None:
         """One whole PPO rollout in one launch (bb_rollout; args: _native.RolloutArgs
@@ -254,12 +347,16 @@ class BallbotVecEnv:
             raise RuntimeError("bb_rollout steps the proprio policy; the camera policy rolls out per step")
         if self._host_reward is not None:
             raise RuntimeError("bb_rollout needs a built-in reward (a host plugin runs per step())")
+        if self._reward_error:
+            raise ValueError(self._reward_error)
         N.check(N.lib().bb_rollout(self._h, C.byref(args), self._stream()), "bb_rollout")
 
-    def step_async_raw(self, actions: torch.Tensor) -> None:
-        """Launch-only step (graph capture / benchmarking): no derived tensors."""
+    def step_async_raw(self, actions: torch.Tensor, full_outputs: bool = False) -> None:
+        """Launch-only step (graph capture / benchmarking): no derived tensors;
+        full_outputs: also the terminal obs and pos2d buffers."""
         N.lib().bb_step(self._h, _ptr(actions), _ptr(self.obs), _ptr(self.reward), _ptr(self.done),
-                        None, None, int(self.auto_reset), self._stream())
+                        _ptr(self.terminal_obs) if full_outputs else None, _ptr(self.pos2d) if full_outputs else None,
+                        int(self.auto_reset), self._stream())
 
     def _plugin_reward(self, failure: torch.Tensor) -> torch.Tensor:
         """Reward of a custom plugin, in the reference's float32 order
@@ -317,10 +414,43 @@ class BallbotVecEnv:
         return self.obs_dict(obs), reward, done, infos
 
     def seed(self, seed: Optional[int] = None):
-        """VecEnv.seed: terrain streams are fixed at construction (the reference's eval_env
-        generators ignore reset seeds, ballbot_env.py:378-384, 596-599); seeds the action space."""
+        """VecEnv.seed (SB3 2.x): env i re-seeds to np_random(seed + i) at the next
+        reset() -- the terrain generator, as reset(seed=seed+i) replaces the
+        reference env's _np_random (ballbot_env.py:596) -- and the action space is
+        seeded.  seed None: a random base, as SB3 draws one.  -> the seeds."""
+        if seed is None:
+            seed = int(np.random.randint(0, np.iinfo(np.uint32).max, dtype=np.uint32))
+        self._pending_seeds = [int(seed) + i for i in range(self.num_envs)]
         self.action_space.seed(seed)
-        return [seed] * self.num_envs
+        return list(self._pending_seeds)
+
+    def load_terrain(self, slot: int, seed: Optional[int]) -> None:
+        """Generate the terrain of `seed` (the registered plugin, or the GPU perlin
+        generator) into bank slot `slot` (terrain_slots mode; ballbot_env.py:501-513)."""
+        from .config import _gen_chunk, perlin_cfg
+
+        L = N.lib()
+        size_z = self.terrain_plan.size_z
+        if self._gpu_perlin() and seed is not None:
+            sd = np.array([int(seed)], np.int32)
+            N.check(L.bb_generate_perlin(self._h, int(slot), 1, sd.ctypes.data_as(C.POINTER(C.c_int32)),
+                                         C.byref(perlin_cfg(self.terrain_config)), float(size_z)),
+                    "bb_generate_perlin")
+        else:
+            arr = np.ascontiguousarray(_gen_chunk(self.terrain_config, [seed], N.HF_N)[0], dtype=np.float32)
+            N.check(L.bb_set_hfield(self._h, int(slot), arr.ctypes.data_as(C.POINTER(C.c_float)), float(size_z)),
+                    "bb_set_hfield")
+        self.terrain_seeds[int(slot)] = seed if seed is not None else -1
+
+    def terrain_rng(self):
+        """(uint64[N][5] device generators in pcg64_words form (None without generators), int32[N] terrain seed of
+        each env's last device draw, -1 before the first)."""
+        gen = self.terrain_plan.stream_seeds is not None
+        w = np.zeros((self.num_envs, 5), np.uint64) if gen else None
+        s = np.zeros(self.num_envs, np.int32)
+        N.check(N.lib().bb_get_terrain_rng(self._h, None if w is None else w.ctypes.data_as(C.POINTER(C.c_uint64)),
+                                           s.ctypes.data_as(C.POINTER(C.c_int32))), "bb_get_terrain_rng")
+        return w, s
 
     def get_attr(self, name: str, indices=None):
         n = self.num_envs if indices is None else len(list(indices))

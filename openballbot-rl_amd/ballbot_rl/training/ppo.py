@@ -551,7 +551,18 @@ class BatchedPPO:
             raise ValueError(f"update_mode must be 'gather' or 'allreduce' (got {update_mode!r})")
         if update_mode == "allreduce" and self.world > 1 and int(batch_size) % self.world:
             raise ValueError(f"update_mode='allreduce': batch_size {batch_size} must divide by the {self.world} ranks")
+        if update_mode == "allreduce" and self.world > 1:
+            # every rank must run the same number of minibatches (one all-reduce each): equal
+            # shards, or the collectives stop matching (gloo errors, RCCL hangs)
+            dev = torch.device("cpu") if dist.get_backend() == "gloo" else self.device
+            t = torch.tensor([self.n_envs, -self.n_envs], dtype=torch.int64, device=dev)
+            dist.all_reduce(t, op=dist.ReduceOp.MAX)
+            if int(t[0]) != self.n_envs or int(-t[1]) != self.n_envs:
+                raise ValueError(f"update_mode='allreduce' needs the same number of envs on every rank (this rank "
+                                 f"has {self.n_envs}, the ranks range over [{int(-t[1])}, {int(t[0])}]): make "
+                                 "num_envs divisible by the world size")
         self.update_mode = update_mode
+        self._dp_adv_hook = None  # tests: called with each data-parallel minibatch's normalised advantages
         torch.manual_seed(int(seed))
         self.cameras = bool(getattr(env, "cameras", False))
         img = (2, env.cam_h, env.cam_w) if self.cameras else None
@@ -853,24 +864,44 @@ class BatchedPPO:
             self._update(data)
         self._sync_params()
 
-    def _allreduce_mean(self, t: torch.Tensor) -> torch.Tensor:
-        t = t.detach().clone().float()
+    def _allreduce_mean(self, ts) -> list:
+        """The ranks' mean of several scalars, in ONE all-reduce."""
+        t = torch.stack([x.detach().float().reshape(()) for x in ts])
         dist.all_reduce(t)
-        return t / self.world
+        return list(t / self.world)
 
-    def _loss(self, obs, act, old_logp, adv, ret, clip):
+    def _global_normalized(self, adv: torch.Tensor) -> torch.Tensor:
+        """SB3's per-minibatch advantage normalisation, (adv - mean) / (std + 1e-8)
+        with the unbiased std, over the GLOBAL minibatch: the union of the ranks'
+        local minibatches (one all-reduce of count, sum and sum of squares)."""
+        a64 = adv.detach().double()
+        t = torch.stack([torch.tensor(float(a64.numel()), dtype=torch.float64, device=adv.device), a64.sum(),
+                         (a64 * a64).sum()])
+        dist.all_reduce(t)
+        n, s1, s2 = float(t[0]), t[1], t[2]
+        mean = s1 / n
+        var = (s2 - n * mean * mean) / max(n - 1.0, 1.0)
+        std = torch.sqrt(torch.clamp(var, min=0.0))
+        out = ((a64 - mean) / (std + 1e-8)).to(adv.dtype)
+        if self._dp_adv_hook is not None:
+            self._dp_adv_hook(adv, out)
+        return out
+
+    def _loss(self, obs, act, old_logp, adv, ret, clip, normalize: Optional[bool] = None):
         """One minibatch of SB3 PPO.train: -> (loss, pg, vf, ent, approx_kl, clip_fraction).
 
         On the GPU the loss and its gradients are one bb_ppo_loss launch; the
-        torch expression below is the CPU stand-in path of the host tests."""
+        torch expression below is the CPU stand-in path of the host tests.
+        normalize: override of normalize_advantage (False: adv is normalised already)."""
+        norm = self.normalize_advantage if normalize is None else bool(normalize)
         if self.device.type == "cuda":
             mean, values = self.policy._heads(obs)
             clip_t = clip if isinstance(clip, torch.Tensor) else torch.tensor(float(clip), device=self.device)
             loss, t = _PPOLossHIP.apply(mean, values, self.policy.log_std, act, old_logp, adv, ret, clip_t,
-                                        self.normalize_advantage, self.ent_coef, self.vf_coef)
+                                        norm, self.ent_coef, self.vf_coef)
             return loss, t[0], t[1], t[2], t[3], t[4]
         values, logp, entropy = self.policy.evaluate_actions(obs, act)
-        if self.normalize_advantage and adv.shape[0] > 1:
+        if norm and adv.shape[0] > 1:
             adv = (adv - adv.mean()) / (adv.std() + 1e-8)
         log_ratio = logp - old_logp
         ratio = torch.exp(log_ratio)
@@ -927,11 +958,15 @@ class BatchedPPO:
                 perm = torch.randperm(n, generator=self.shuffle_gen, device=self.device)
                 for s in range(0, n, bsz):
                     idx = perm[s:s + bsz]
+                    adv = d["advantages"][idx]
+                    norm = None
+                    if dp and self.normalize_advantage:  # SB3 normalises over the (global) minibatch
+                        adv, norm = self._global_normalized(adv), False
                     loss, pg, vf, ent, kl, cf = self._loss(self._mb_obs(d, idx), d["actions"][idx],
-                                                           d["log_probs"][idx], d["advantages"][idx],
-                                                           d["returns"][idx], clip)
+                                                           d["log_probs"][idx], adv, d["returns"][idx], clip,
+                                                           normalize=norm)
                     if dp:  # the global minibatch's terms: the mean over the ranks' local minibatches
-                        pg, vf, ent, kl, cf = (self._allreduce_mean(x) for x in (pg, vf, ent, kl, cf))
+                        pg, vf, ent, kl, cf = self._allreduce_mean((pg, vf, ent, kl, cf))
                     pg_l.append(pg); vf_l.append(vf); ent_l.append(ent); clip_f.append(cf)
                     approx_kl = float(kl)  # the early stop needs it before the step (host sync)
                     kls.append(approx_kl)

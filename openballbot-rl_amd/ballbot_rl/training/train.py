@@ -65,6 +65,7 @@ def experiment_dir(config: Dict[str, Any], out: Optional[str] = None) -> Path:
 
 
 def make_env(config: Dict[str, Any], num_envs: int, device, seed: int, precision: str = "fp64", stream_seeds=None):
+    """One rank's BallbotVecEnv.  stream_seeds None: every env on np_random(seed)."""
     from ballbot_gym.envs import BallbotVecEnv
 
     env_cfg = {"camera": config.get("camera", {}), "env": config.get("env", {}), "logging": config.get("logging", {})}
@@ -74,7 +75,8 @@ def make_env(config: Dict[str, Any], num_envs: int, device, seed: int, precision
     return BallbotVecEnv(num_envs, device=device, reward_config=get_component_config(config, "reward"),
                          terrain_config=get_component_config(config, "terrain"), env_config=env_cfg, seed=seed,
                          precision=precision, n_terrains=config.get("n_terrains"), disable_cameras=not cams,
-                         stream_seeds=stream_seeds)
+                         stream_seeds=stream_seeds, shared_stream=stream_seeds is None,
+                         reward_compat=str(config.get("reward_compat", "reference")))
 
 
 def main(config: Dict[str, Any], seed: int, out: Optional[str] = None, total_timesteps: Optional[int] = None,
@@ -92,8 +94,12 @@ def main(config: Dict[str, Any], seed: int, out: Optional[str] = None, total_tim
     dev = torch.device("cuda", local)
     n_total = int(config["num_envs"])
     first, n_local = env_shard(n_total, rank, world)
-    # every training env draws its terrains from np_random(seed) (train.py:82-89)
-    env = make_env(config, n_local, dev, seed, precision, shard_stream_seeds(seed, first, n_local))
+    # training env g draws its terrains from np_random(seed + g): PPO(seed=seed) seeds the
+    # VecEnv (env i -> seed + i) and learn()'s first reset re-seeds every env's _np_random
+    # with it (train.py:126-141, ballbot_env.py:596); config terrain_streams: shared keeps
+    # one np_random(seed) for every env instead
+    shared = str(config.get("terrain_streams", "per_env")) == "shared"
+    env = make_env(config, n_local, dev, seed, precision, shard_stream_seeds(seed, first, n_local, per_env=not shared))
     eval_cfg = config.get("evaluation", {}) or {}
     n_eval = int(eval_cfg.get("n_episodes", 8))
     # eval env i draws from np_random(seed + N_ENVS + i) (train.py:90-97)

@@ -75,6 +75,9 @@ struct Dev {
   const int* tstream;         // [n_streams][tlen] bank slot of draw k (bb_set_terrain_stream); NULL: none
   const int* env_stream;      // [n] stream of each env; NULL: stream 0
   int tlen;
+  unsigned long long* rng;    // [5][n] per-env PCG64 (bb_set_terrain_rng): state hi/lo, inc hi/lo, 32-bit buffer
+  const int* seed_slot;       // [TERRAIN_SEEDS] bank slot holding each terrain seed (-1: not resident); NULL: slot == seed
+  int* tseed;                 // [n] terrain seed of each env's last device draw (-1: none)
   const float* bank;
   const float* size_z;
   const float* offset;
@@ -124,16 +127,84 @@ __device__ __forceinline__ void store_state(const Dev& d, int e, const T* q, con
   d.steps[e] = step;
 }
 
+// numpy's PCG64 (the bit generator of gymnasium's np_random, Generator(PCG64(
+// SeedSequence(seed)))): a 128-bit LCG, state = state * M + inc, output
+// XSL-RR of the new state.  Generator.integers(0, 10000) takes 32-bit draws
+// (the bit generator buffers the high half of each 64-bit output for the next
+// one) through Lemire's bounded multiply with rejection.  Integer work,
+// bit-exact against numpy (tests/test_host_config.py restates it on the host,
+// tests/test_gpu_terrain_stream.py checks the device draws).
+struct Pcg64 {
+  unsigned long long sh, sl, ih, il, buf;  // state, increment (hi, lo); buf: bit 32 = has_uint32, low 32 = uinteger
+};
+constexpr int TERRAIN_SEEDS = 10000;  // ballbot_env.py:505-510 integers(0, 10000)
+
+__device__ __forceinline__ unsigned long long pcg64_next64(Pcg64& g) {
+  constexpr unsigned long long MH = 0x2360ED051FC65DA4ull, ML = 0x4385DF649FCCF645ull;
+  const unsigned long long lo = g.sl * ML;
+  unsigned long long hi = __umul64hi(g.sl, ML) + g.sl * MH + g.sh * ML;
+  const unsigned long long lo2 = lo + g.il;
+  hi += g.ih + (lo2 < lo ? 1ull : 0ull);
+  g.sl = lo2;
+  g.sh = hi;
+  const unsigned rot = unsigned(hi >> 58);
+  const unsigned long long x = hi ^ lo2;
+  return (x >> rot) | (x << ((64u - rot) & 63u));
+}
+__device__ __forceinline__ unsigned pcg64_next32(Pcg64& g) {
+  if (g.buf >> 32) {  // the buffered half; numpy clears has_uint32 and keeps the value
+    const unsigned u = unsigned(g.buf);
+    g.buf = u;
+    return u;
+  }
+  const unsigned long long x = pcg64_next64(g);
+  g.buf = (1ull << 32) | (x >> 32);
+  return unsigned(x);
+}
+// Generator.integers(0, 10000): buffered_bounded_lemire_uint32 with rng = 9999
+__device__ __forceinline__ int pcg64_terrain_seed(Pcg64& g) {
+  constexpr unsigned EXCL = TERRAIN_SEEDS;
+  unsigned long long m = (unsigned long long)pcg64_next32(g) * EXCL;
+  unsigned left = unsigned(m);
+  if (left < EXCL) {
+    constexpr unsigned THRESHOLD = (0xFFFFFFFFu - (EXCL - 1u)) % EXCL;
+    while (left < THRESHOLD) {
+      m = (unsigned long long)pcg64_next32(g) * EXCL;
+      left = unsigned(m);
+    }
+  }
+  return int(m >> 32);
+}
+
 // The terrain of env e's next episode.  The reference draws
 // r_seed = _np_random.integers(0, 10000) at every reset (ballbot_env.py:505-510)
-// from a generator fixed at construction for eval_env=[True, seed]
-// (:378-384), which train.py:82-89 uses for every training env: the k-th reset
-// of an env takes the k-th draw of its stream.  The host precomputes each
-// stream's draws as bank slots (bb_set_terrain_stream); this reads draw
-// episodes[e].  A pinned terrain (bb_assign_terrain) takes no draw.
+// from the env's own generator: SB3 seeds training env i with reset(seed=seed+i)
+// (VecEnv.seed, then the first reset of learn(); gymnasium's Env.reset(seed)
+// replaces _np_random, :596), an eval env keeps np_random(seed + N_ENVS + i) from
+// construction (:378-384, train.py:90-97).  With bb_set_terrain_rng each env runs
+// that generator here (unbounded, exact); the drawn seed's bank slot comes from
+// seed_slot (a draw whose seed is not resident is counted in stats[5] and takes
+// slot seed % n_terrains).  Otherwise the host's precomputed draws per stream
+// (bb_set_terrain_stream): draw episodes[e] of the table.  A pinned terrain
+// (bb_assign_terrain) takes no draw.  Called by one lane per env.
 __device__ __forceinline__ int next_terrain(const Dev& d, int e) {
   const int pin = d.pending_terrain[e];
-  if (pin >= 0 || !d.tstream) return pin >= 0 ? pin : 0;
+  if (pin >= 0) return pin;
+  if (d.rng) {
+    const size_t n = size_t(d.n);
+    Pcg64 g{d.rng[e], d.rng[n + e], d.rng[2 * n + e], d.rng[3 * n + e], d.rng[4 * n + e]};
+    const int s = pcg64_terrain_seed(g);
+    d.rng[e] = g.sh; d.rng[n + e] = g.sl; d.rng[4 * n + e] = g.buf;
+    d.episodes[e] += 1;
+    d.tseed[e] = s;
+    int slot = d.seed_slot ? d.seed_slot[s] : s;
+    if (unsigned(slot) >= unsigned(d.n_terrains)) {
+      atomicAdd(&d.stats[5], 1ull);
+      slot = s % d.n_terrains;
+    }
+    return slot;
+  }
+  if (!d.tstream) return 0;
   int k = d.episodes[e];
   d.episodes[e] = k + 1;
   if (k >= d.tlen) {  // past the resident draws: reuse them (counted)
@@ -368,7 +439,7 @@ __device__ __forceinline__ int team_step(const ModelT<T>& m, const EnvCfg& cfg, 
     }
   }
   if (reset) {
-    tid = __shfl(tid, int(threadIdx.x) & ~(L - 1));  // the lead's draw
+    tid = __shfl(tid, team_shift_of(L));  // the lead's draw
     team_sync();
     reset_state(m, T(d.offset[tid]), q, v, w);  // every lane writes the same values
     step = 0;
@@ -892,7 +963,7 @@ __global__ __launch_bounds__(64) void predict_kernel(ModelT<T> mg, Dev d) {
   __syncthreads();
   const ModelT<T>& m = ms;
   constexpr int PL = 16;
-  const int tl = int(threadIdx.x) & (PL - 1), team_shift = int(threadIdx.x) & ~(PL - 1);
+  const int tl = int(threadIdx.x) & (PL - 1), team_shift = team_shift_of(PL);
   const int e = blockIdx.x * (WAVE / PL) + int(threadIdx.x) / PL;
   if (e >= d.n) return;  // team-uniform
   const T* Q = (const T*)d.qpos;
@@ -984,7 +1055,7 @@ __global__ __launch_bounds__(64 * QW) void relief_multi_kernel(ModelT<T> mg, Env
     const int i = 4 * wave + team;
     if (i < nloc) {
       EnvWork<T>& W = team_work<T>(smem, i);
-      const bool sl = predict_env<T>(m, d, s_tid[i], W.qn, W.vn, tm.tl, lane & ~15);
+      const bool sl = predict_env<T>(m, d, s_tid[i], W.qn, W.vn, tm.tl, team_shift_of(16));
       if (lead) s_kind[i] = sl ? 1 : 0;
     }
   }
@@ -1076,7 +1147,7 @@ __global__ __launch_bounds__(64 * QW) void relief_multi_kernel(ModelT<T> mg, Env
           done[row] = uint8_t(fl);
         }
       }
-      const bool next = k + 1 < K && predict_env<T>(m, d, tid, W.qn, W.vn, tm.tl, lane & ~15);
+      const bool next = k + 1 < K && predict_env<T>(m, d, tid, W.qn, W.vn, tm.tl, team_shift_of(16));
       team_sync();
       if (lead) {
         if (d.cost) d.cost[e] += clock64() - c0;  // this env's cost, for the next launch's balance
@@ -1232,7 +1303,10 @@ struct bb_handle {
   int n_relief = 0;
   int* tstream = nullptr;       // device copies of the terrain streams (bb_set_terrain_stream)
   int* env_stream = nullptr;
+  size_t tstream_cap = 0;       // ints allocated at tstream (refilled in place while the table fits)
   int n_streams = 0;
+  unsigned long long* rng = nullptr;  // per-env PCG64 words [5][n] (bb_set_terrain_rng), allocated once
+  int* seed_slot = nullptr;           // [TERRAIN_SEEDS], allocated once
   CamRig rig;  // depth cameras in the base body (bb_render_depth)
   void* scenes = nullptr;
 };
@@ -1517,6 +1591,8 @@ int bb_create(int n_envs, int device, const bb_params* p, bb_handle** out) {
   HIPCHK(hipMalloc((void**)&d.terrain, sizeof(int) * n));
   HIPCHK(hipMalloc((void**)&d.pending_terrain, sizeof(int) * n));
   HIPCHK(hipMalloc((void**)&d.episodes, sizeof(int) * n));
+  HIPCHK(hipMalloc((void**)&d.tseed, sizeof(int) * n));
+  HIPCHK(hipMemset(d.tseed, 0xFF, sizeof(int) * n));  // -1: no device draw yet
   HIPCHK(hipMalloc((void**)&h->bank, sizeof(float) * nt * HF_N * HF_N));
   HIPCHK(hipMalloc((void**)&h->size_z, sizeof(float) * nt));
   HIPCHK(hipMalloc((void**)&h->offset, sizeof(float) * nt));
@@ -1593,7 +1669,8 @@ int bb_destroy(bb_handle* h) {
   (void)hipFree(h->d.slow_list); (void)hipFree(h->d.slow_count); (void)hipFree(h->d.park);
   (void)hipFree(h->d.fast_envs); (void)hipFree(h->d.pred_envs); (void)hipFree(h->d.pred_mark);
   (void)hipFree(h->d.body_spill); (void)hipFree(h->d.perm); (void)hipFree(h->d.cost);
-  (void)hipFree(h->tstream); (void)hipFree(h->env_stream);
+  (void)hipFree(h->tstream); (void)hipFree(h->env_stream); (void)hipFree(h->rng); (void)hipFree(h->seed_slot);
+  (void)hipFree(h->d.tseed);
   (void)hipStreamDestroy(h->side); (void)hipEventDestroy(h->fork); (void)hipEventDestroy(h->join);
   for (hipEvent_t e : h->tev) (void)hipEventDestroy(e);
   (void)hipFree(h->scenes);
@@ -1989,10 +2066,11 @@ int bb_set_terrain_stream(bb_handle* h, const int32_t* slots, int n_streams, int
   if (n_streams < 0) return fail("bb_set_terrain_stream: n_streams must be >= 0 (got %d)", n_streams);
   HIPCHK(hipSetDevice(h->device));
   HIPCHK(hipDeviceSynchronize());
-  (void)hipFree(h->tstream); (void)hipFree(h->env_stream);
-  h->tstream = nullptr; h->env_stream = nullptr; h->n_streams = 0;
-  h->d.tstream = nullptr; h->d.env_stream = nullptr; h->d.tlen = 0;
-  if (n_streams == 0) return 0;
+  if (n_streams == 0) {
+    h->n_streams = 0;
+    h->d.tstream = nullptr; h->d.env_stream = nullptr; h->d.tlen = 0;
+    return 0;
+  }
   if (!slots) return fail("bb_set_terrain_stream: NULL slots");
   if (length < 1) return fail("bb_set_terrain_stream: length must be >= 1 (got %d)", length);
   const size_t cnt = size_t(n_streams) * size_t(length);
@@ -2006,15 +2084,75 @@ int bb_set_terrain_stream(bb_handle* h, const int32_t* slots, int n_streams, int
   } else if (n_streams != 1) {
     return fail("bb_set_terrain_stream: %d streams need an env_stream map", n_streams);
   }
-  HIPCHK(hipMalloc((void**)&h->tstream, sizeof(int) * cnt));
+  // refill in place while the table fits, so a graph captured before this call
+  // reads the new table; a larger table is a new allocation
+  if (cnt > h->tstream_cap) {
+    (void)hipFree(h->tstream);
+    h->tstream = nullptr;
+    h->tstream_cap = 0;
+    HIPCHK(hipMalloc((void**)&h->tstream, sizeof(int) * cnt));
+    h->tstream_cap = cnt;
+  }
   HIPCHK(hipMemcpy(h->tstream, slots, sizeof(int) * cnt, hipMemcpyHostToDevice));
   if (env_stream) {
-    HIPCHK(hipMalloc((void**)&h->env_stream, sizeof(int) * h->n));
+    if (!h->env_stream) HIPCHK(hipMalloc((void**)&h->env_stream, sizeof(int) * h->n));
     HIPCHK(hipMemcpy(h->env_stream, env_stream, sizeof(int) * h->n, hipMemcpyHostToDevice));
   }
   HIPCHK(hipMemset(h->d.episodes, 0, sizeof(int) * h->n));  // the next reset takes draw 0
   h->n_streams = n_streams;
-  h->d.tstream = h->tstream; h->d.env_stream = h->env_stream; h->d.tlen = length;
+  h->d.tstream = h->tstream; h->d.env_stream = env_stream ? h->env_stream : nullptr; h->d.tlen = length;
+  h->d.rng = nullptr;  // the table replaces any device generators
+  return 0;
+}
+
+int bb_set_terrain_rng(bb_handle* h, const uint64_t* words, const int32_t* seed_slot) {
+  if (!h) return fail("bb_set_terrain_rng: NULL handle");
+  HIPCHK(hipSetDevice(h->device));
+  HIPCHK(hipDeviceSynchronize());
+  if (!words) {
+    h->d.rng = nullptr;
+    return 0;
+  }
+  if (seed_slot)
+    for (int s = 0; s < TERRAIN_SEEDS; s++)
+      if (seed_slot[s] >= h->p.n_terrains)
+        return fail("bb_set_terrain_rng: seed_slot[%d] = %d out of range [-1,%d)", s, seed_slot[s], h->p.n_terrains);
+  if (!seed_slot && h->p.n_terrains < TERRAIN_SEEDS)
+    return fail("bb_set_terrain_rng: slot == seed needs a bank of %d terrains (have %d): pass seed_slot",
+                TERRAIN_SEEDS, h->p.n_terrains);
+  const size_t n = h->n;
+  for (size_t e = 0; e < n; e++)
+    if ((words[5 * e + 4] >> 32) > 1)
+      return fail("bb_set_terrain_rng: env %zu: buffer word has bits above 32 other than has_uint32", e);
+  std::vector<unsigned long long> soa(5 * n);
+  for (size_t e = 0; e < n; e++)
+    for (int j = 0; j < 5; j++) soa[j * n + e] = words[5 * e + j];
+  if (!h->rng) HIPCHK(hipMalloc((void**)&h->rng, sizeof(unsigned long long) * 5 * n));
+  HIPCHK(hipMemcpy(h->rng, soa.data(), sizeof(unsigned long long) * 5 * n, hipMemcpyHostToDevice));
+  if (seed_slot) {
+    if (!h->seed_slot) HIPCHK(hipMalloc((void**)&h->seed_slot, sizeof(int) * TERRAIN_SEEDS));
+    HIPCHK(hipMemcpy(h->seed_slot, seed_slot, sizeof(int) * TERRAIN_SEEDS, hipMemcpyHostToDevice));
+  }
+  HIPCHK(hipMemset(h->d.episodes, 0, sizeof(int) * n));
+  HIPCHK(hipMemset(h->d.tseed, 0xFF, sizeof(int) * n));
+  h->d.rng = h->rng;
+  h->d.seed_slot = seed_slot ? h->seed_slot : nullptr;
+  return 0;
+}
+
+int bb_get_terrain_rng(bb_handle* h, uint64_t* words, int32_t* last_seed) {
+  if (!h) return fail("bb_get_terrain_rng: NULL handle");
+  HIPCHK(hipSetDevice(h->device));
+  HIPCHK(hipDeviceSynchronize());
+  const size_t n = h->n;
+  if (words) {
+    if (!h->d.rng) return fail("bb_get_terrain_rng: no device generators (bb_set_terrain_rng)");
+    std::vector<unsigned long long> soa(5 * n);
+    HIPCHK(hipMemcpy(soa.data(), h->rng, sizeof(unsigned long long) * 5 * n, hipMemcpyDeviceToHost));
+    for (size_t e = 0; e < n; e++)
+      for (int j = 0; j < 5; j++) words[5 * e + j] = soa[j * n + e];
+  }
+  if (last_seed) HIPCHK(hipMemcpy(last_seed, h->d.tseed, sizeof(int) * n, hipMemcpyDeviceToHost));
   return 0;
 }
 

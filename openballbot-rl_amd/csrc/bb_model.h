@@ -56,7 +56,7 @@ struct SolverCfg {
 inline SolverCfg default_solver(bool fp64) {
   // MuJoCo: tolerance 1e-8, iterations 100, ls_iterations 50.  The minimiser is
   // unique, so the fp32 build stops at its roundoff floor instead.
-  if (fp64) return SolverCfg{1e-8, 1e-2, 1e-14, 40, 40};  // MuJoCo tolerance / ls_tolerance
+  if (fp64) return SolverCfg{1e-8, 1e-2, 1e-14, 100, 50};  // MuJoCo tolerance / ls_tolerance / iterations
   return SolverCfg{2e-6, 1e-3, 3e-7, 16, 16};
 }
 

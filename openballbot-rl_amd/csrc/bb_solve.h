@@ -81,11 +81,18 @@ BB_HD void team_sync() {
 #endif
 }
 
+#ifdef __HIPCC__
+// bit offset of this lane's team in a 64-bit wave ballot: the team's first lane
+// WITHIN THE WAVE.  (threadIdx.x & ~(L-1) is that only in one-wave workgroups;
+// in relief_multi_kernel's 4-wave workgroups it reaches 240, a shift past 63.)
+__device__ __forceinline__ int team_shift_of(int L) { return (int(threadIdx.x) & 63) & ~(L - 1); }
+#endif
+
 // true in every lane of the team if b holds in any of its lanes (team-uniform branch)
 BB_HD bool team_any(const Team& tm, bool b) {
 #ifdef __HIP_DEVICE_COMPILE__
   const unsigned long long m = __ballot(b);
-  const int sh = int(threadIdx.x) & ~(tm.L - 1);
+  const int sh = team_shift_of(tm.L);
   const unsigned long long mask = tm.L >= 64 ? ~0ull : ((1ull << tm.L) - 1);
   return ((m >> sh) & mask) != 0;
 #else
@@ -248,8 +255,8 @@ BB_HD void chol_team(T* H, const T* hd, const Team& tm) {
 template <typename T>
 struct LsTerm {
   T u0[3], du[3], mu, Dm, b0, b1, vv, kink;
-#ifdef BB_IMPROVE
-  T c0;
+  T c0;  // the contact's cost at alpha = 0 in the bottom zone (0.5 sum D_r jar_r^2)
+  // phi_c(alpha): the contact's constraint cost (mj_constraintUpdate's zones)
   BB_HD T cost(T alpha) const {
     const T N = u0[0] + alpha * du[0], U1 = u0[1] + alpha * du[1], U2 = u0[2] + alpha * du[2];
     const T Tn = sqrt(U1 * U1 + U2 * U2);
@@ -258,7 +265,6 @@ struct LsTerm {
     const T g = N - mu * Tn;
     return top ? T(0) : (bot ? c0 + alpha * (b0 + T(0.5) * alpha * b1) : T(0.5) * Dm * g * g);
   }
-#endif
   BB_HD void prep(const T* j0, const T* x, T mu_, T f1, T f2, const T* D, T Dm_) {
     mu = mu_;
     Dm = Dm_;
@@ -266,9 +272,7 @@ struct LsTerm {
     du[0] = mu * x[0]; du[1] = f1 * x[1]; du[2] = f2 * x[2];
     b0 = D[0] * j0[0] * x[0] + D[1] * j0[1] * x[1] + D[2] * j0[2] * x[2];
     b1 = D[0] * x[0] * x[0] + D[1] * x[1] * x[1] + D[2] * x[2] * x[2];
-#ifdef BB_IMPROVE
     c0 = T(0.5) * (D[0] * j0[0] * j0[0] + D[1] * j0[1] * j0[1] + D[2] * j0[2] * j0[2]);
-#endif
     vv = du[1] * du[1] + du[2] * du[2];
     kink = T(-1);
     if (vv > 0) {
@@ -281,7 +285,7 @@ struct LsTerm {
   BB_HD void none() {
     u0[0] = u0[1] = u0[2] = du[0] = du[1] = du[2] = T(0);
     u0[0] = T(1);  // separated: top zone at every alpha
-    mu = Dm = b0 = b1 = vv = T(0);
+    mu = Dm = b0 = b1 = vv = c0 = T(0);
     kink = T(-1);
   }
   // adds phi_c'(alpha), phi_c''(alpha) and a magnitude bound of the terms of phi_c'
@@ -463,7 +467,9 @@ BB_HD int solve_team(const ModelT<T>& m, EnvWork<T>& W, const T* qfs, int ng, T*
 #ifdef BB_SOLVE_TRACE
     printf("it %d |g| %.3e\n", it, double(m.scale * sqrt(gn)));
 #endif
-    if (m.scale * sqrt(gn) < m.tol) break;
+    // MuJoCo's gradient stop (mj_solPrimal: scale * ||grad|| < tolerance after an
+    // iteration; the first iteration always runs)
+    if (it > 0 && m.scale * sqrt(gn) < m.tol) break;
     PH(2)
     // ---- (4) Hessian entries, entry-parallel
     for (int e = tm.tl; e < NH; e += tm.L) {
@@ -584,18 +590,18 @@ BB_HD int solve_team(const ModelT<T>& m, EnvWork<T>& W, const T* qfs, int ng, T*
            double(lsr.lo), double(lsr.hi), double(lsr.dlo), double(lsr.dhi));
 #endif
     if (!(alpha > 0)) break;
-#ifdef BB_IMPROVE
-    T dcost = alpha * (gs + T(0.5) * alpha * sMs);
-    for (int c = 0; c < nc; c++) dcost += lst[c].cost(alpha) - lst[c].cost(T(0));
-#endif
+    // the cost change of the step, closed form on the line: the Gauss term
+    // alpha (s'(Ma - qfs)) + alpha^2 s'Ms / 2, plus each contact's phi_c(alpha) - phi_c(0)
+    T dc = 0;
+    for (int c = tm.tl; c < nc; c += tm.L) dc += lst[c].cost(alpha) - lst[c].cost(T(0));
+    const T dcost = alpha * (gs + T(0.5) * alpha * sMs) + team_sum(tm, dc);
     T sn = 0, an2 = 0;
 #pragma unroll
     for (int i = 0; i < NV; i++) { a[i] += alpha * s[i]; sn += s[i] * s[i]; an2 += a[i] * a[i]; }
     PH(6)
     if (alpha * alpha * sn <= T(1e-30) + m.step_rel2 * (1 + an2)) { it++; break; }
-#ifdef BB_IMPROVE
+    // MuJoCo's improvement stop (mj_solPrimal: scale * (oldcost - cost) < tolerance)
     if (-m.scale * dcost < m.tol) { it++; break; }
-#endif
   }
   PH(7)
   PH_FLUSH(tm)

@@ -574,7 +574,9 @@ __device__ int solve16(const ModelT<T>& m, EnvWork<T>& W, int ng, int nb, T* a, 
     }
     gi = rowl ? gi + gb : T(0);
     const T gn = tsum(gi * gi);
-    if (m.scale * m.scale * gn < m.tol * m.tol) break;  // scale * ||g|| < tol without the sqrt
+    // MuJoCo's gradient stop (mj_solPrimal: scale * ||grad|| < tolerance after an
+    // iteration; the first iteration always runs), without the sqrt
+    if (it > 0 && m.scale * m.scale * gn < m.tol * m.tol) break;
     PH(2)
     // ---- (4) Hessian row: M row + wheel blocks + ground block
     // J[:, p]' C J for a contact: w = C J[:, p] (C packed xx,yy,zz,xy,xz,yz)
@@ -765,11 +767,22 @@ __device__ int solve16(const ModelT<T>& m, EnvWork<T>& W, int ng, int nb, T* a, 
     PH(9)
     const T alpha = lsr.alpha;
     if (!(alpha > 0)) break;
+    // the cost change of the step (MuJoCo's improvement test below), closed form on
+    // the line: alpha s'(Ma - qfs) + alpha^2 s'Ms / 2 + sum_c phi_c(alpha) - phi_c(0)
+    T dc = lt.cost(alpha) - lt.cost(T(0));
+    for (int c = tl + L; c < nc; c += L) {  // contacts past the team's lanes (full kernel only)
+      LsTerm<T> lc;
+      ls_term<BODY>(m, W, c, ng, nc, a, s, kdw, lc);
+      dc += lc.cost(alpha) - lc.cost(T(0));
+    }
+    const T dcost = alpha * (gs + T(0.5) * alpha * sMs) + tsum(dc);
     T sn = 0, an2 = 0;
 #pragma unroll
     for (int i = 0; i < NV; i++) { a[i] += alpha * s[i]; sn += s[i] * s[i]; an2 += a[i] * a[i]; }
     PH(6)
     if (alpha * alpha * sn <= T(1e-30) + m.step_rel2 * (1 + an2)) { it++; break; }
+    // MuJoCo's improvement stop (mj_solPrimal: scale * (oldcost - cost) < tolerance)
+    if (-m.scale * dcost < m.tol) { it++; break; }
   }
   PH(7)
   PH_FLUSH((Team{L, tl}))
@@ -804,7 +817,7 @@ __device__ __forceinline__ int collide_team(const ModelT<T>& m, const Kin<T>& k,
   const int total = (rmax - rmin) * (np > 0 ? np : 0);
   const T dx = 2 * sx / N1, dy = 2 * sy / N1;
   (void)v;
-  const int team_shift = threadIdx.x & ~(L - 1);
+  const int team_shift = team_shift_of(L);
   int ng = 0;
   for (int base = 0; base < total; base += L) {
     const int P = base + tl;
@@ -940,7 +953,7 @@ __device__ bool body_candidates(const ModelT<T>& m, const Kin<T>& k, const float
               hi[2] >= -zb;
     }
   }
-  unsigned todo = unsigned(__ballot(reach) >> (threadIdx.x & ~(L - 1))) & 0x3Fu;  // team-uniform
+  unsigned todo = unsigned(__ballot(reach) >> team_shift_of(L)) & 0x3Fu;  // team-uniform
   if (hf) {
     const T sx = m.hf_sx, sy = m.hf_sy;
     const int N1 = HF_N - 1;
@@ -982,7 +995,7 @@ __device__ bool body_candidates(const ModelT<T>& m, const Kin<T>& k, const float
       }
     }
   }
-  const unsigned bits = unsigned(__ballot(cand) >> (threadIdx.x & ~(L - 1))) & 0xFFFFu;
+  const unsigned bits = unsigned(__ballot(cand) >> team_shift_of(L)) & 0xFFFFu;
   return bits != 0;
 }
 
@@ -1002,7 +1015,7 @@ constexpr int CAND_CAP = 80;
 template <typename T>
 __device__ int collide_body_team(const ModelT<T>& m, const Kin<T>& k, const float* hf, T size_z, T hz, T* bc,
                                  T* spill, int* overflow, int tl, int* cand) {
-  const int team_shift = threadIdx.x & ~(L - 1);
+  const int team_shift = team_shift_of(L);
   const unsigned below = (1u << tl) - 1u;
   int nb = 0;
   auto compact = [&](bool hit) -> int {  // -> this lane's slot (valid if hit)

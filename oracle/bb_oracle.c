@@ -52,17 +52,21 @@ static const double PI = 3.14159265358979323846;
 /* ------------------------------------------------------------------ options */
 static int g_flags = 0;
 static int g_maxiter = 100;          /* MuJoCo default opt.iterations */
-static double g_tol = 1e-10;         /* tighter than MuJoCo's 1e-8 (oracle) */
-/* line search: the oracle searches to roundoff (|phi'| <= 1e-15 |phi'(0)|, 200
- * evaluations); MuJoCo stops at ls_tolerance 0.01 within ls_iterations 50
- * (the FLOP-counting build uses those, oracle/flopcount.cpp) */
-static double g_lstol = 1e-15;
-static int g_lsmax = 200;
+static double g_tol = 1e-8;          /* MuJoCo default opt.tolerance */
+/* line search: MuJoCo's criterion |phi'| <= ls_tolerance |phi'(0)| within
+ * ls_iterations evaluations, on the kernel's 1-D search (newton(); MuJoCo's own
+ * search path is not restated: parity unpinned).  bbo_set_flags(2048) selects
+ * the earlier rounds' exact search instead (Newton/bisection to g_lstol; with
+ * g_lstol 0.01 that simple search leaves rare steps far from the minimiser, up
+ * to 1e-4 in qpos against the kernel). */
+static double g_lstol = 0.01;        /* MuJoCo default opt.ls_tolerance */
+static int g_lsmax = 50;             /* MuJoCo default opt.ls_iterations */
 
 int bbo_abi_version(void) { return 3; }
 void bbo_set_flags(int flags) { g_flags = flags; }
 int bbo_get_flags(void) { return g_flags; }
 void bbo_set_solver(int maxiter, double tol) { g_maxiter = maxiter; g_tol = tol; }
+void bbo_set_linesearch(int ls_iterations, double ls_tolerance) { g_lsmax = ls_iterations; g_lstol = ls_tolerance; }
 
 /* ------------------------------------------------------------- small maths */
 static void v3copy(double* r, const double* a) { r[0] = a[0]; r[1] = a[1]; r[2] = a[2]; }
@@ -1194,6 +1198,99 @@ static double total_cost(const Efc* e, const double* jar, double* force, double*
   return cost;
 }
 
+/* One contact's terms of phi(alpha) = f(a + alpha s) along the search line:
+ * the cone variables U(alpha) = u0 + alpha du (U0 = mu jar0, U1 = f1 jar1,
+ * U2 = f2 jar2, as cone_eval), phi_c' and phi_c'' in closed form per zone, and
+ * the alpha of the contact's near-kink (the smallest T on the line, when the
+ * contact is in the middle zone there).  The kernel's LsTerm (bb_solve.h). */
+typedef struct { double u0[3], du[3], mu, Dm, b0, b1, vv, kink, c0; } LsTerm;
+
+static void ls_prep(LsTerm* t, const double* j0, const double* x, double mu, double f1, double f2,
+                    const double* D, double Dm) {
+  t->mu = mu; t->Dm = Dm;
+  t->u0[0] = mu * j0[0]; t->u0[1] = f1 * j0[1]; t->u0[2] = f2 * j0[2];
+  t->du[0] = mu * x[0]; t->du[1] = f1 * x[1]; t->du[2] = f2 * x[2];
+  t->b0 = D[0] * j0[0] * x[0] + D[1] * j0[1] * x[1] + D[2] * j0[2] * x[2];
+  t->b1 = D[0] * x[0] * x[0] + D[1] * x[1] * x[1] + D[2] * x[2] * x[2];
+  t->c0 = 0.5 * (D[0] * j0[0] * j0[0] + D[1] * j0[1] * j0[1] + D[2] * j0[2] * j0[2]);
+  t->vv = t->du[1] * t->du[1] + t->du[2] * t->du[2];
+  t->kink = -1;
+  if (t->vv > 0) {
+    const double ak = -(t->u0[1] * t->du[1] + t->u0[2] * t->du[2]) / t->vv;
+    const double N = t->u0[0] + ak * t->du[0], U1 = t->u0[1] + ak * t->du[1], U2 = t->u0[2] + ak * t->du[2];
+    const double Tn = sqrt(U1 * U1 + U2 * U2);
+    if (ak > 0 && N < mu * Tn && mu * N + Tn > 0) t->kink = ak;
+  }
+}
+
+static void ls_eval(const LsTerm* t, double alpha, double* d1, double* d2, double* dm) {
+  const double N = t->u0[0] + alpha * t->du[0], U1 = t->u0[1] + alpha * t->du[1], U2 = t->u0[2] + alpha * t->du[2];
+  const double t2 = U1 * U1 + U2 * U2;
+  const double rt = t2 > 0 ? 1 / sqrt(t2) : 0;
+  const double Tn = t2 * rt, mu = t->mu;
+  const int top = (N >= mu * Tn) || (Tn <= 0 && N >= 0);
+  const int bot = !top && ((mu * N + Tn <= 0) || (Tn <= 0 && N < 0));
+  const double g = N - mu * Tn;
+  const double tp = (U1 * t->du[1] + U2 * t->du[2]) * rt;
+  const double gp = t->du[0] - mu * tp;
+  const double tpp = (t->vv - tp * tp) * rt;
+  const double Dg = t->Dm * g;
+  if (top) return;
+  if (bot) { *d1 += t->b0 + alpha * t->b1; *d2 += t->b1; *dm += fabs(t->b0) + fabs(alpha * t->b1); return; }
+  *d1 += Dg * gp;
+  *d2 += t->Dm * gp * gp - mu * Dg * tpp;
+  *dm += fabs(Dg) * (fabs(t->du[0]) + mu * fabs(tp));
+}
+
+/* the contact's constraint cost phi_c(alpha) (cone_eval's zones) */
+static double ls_cost(const LsTerm* t, double alpha) {
+  const double N = t->u0[0] + alpha * t->du[0], U1 = t->u0[1] + alpha * t->du[1], U2 = t->u0[2] + alpha * t->du[2];
+  const double Tn = sqrt(U1 * U1 + U2 * U2);
+  const int top = N >= t->mu * Tn;
+  const int bot = !top && t->mu * N + Tn <= 0;
+  const double g = N - t->mu * Tn;
+  return top ? 0 : (bot ? t->c0 + alpha * (t->b0 + 0.5 * alpha * t->b1) : 0.5 * t->Dm * g * g);
+}
+
+/* The 1-D search on phi' (convex phi): bracket [lo, hi], 1-D Newton from the
+ * latest point while it lands inside the bracket and its step is under half
+ * the step before the last one, else Illinois false position; a step that would
+ * cross a contact's kink stops at it.  The kernel's LineSearch (bb_solve.h). */
+typedef struct { double lo, dlo, hi, dhi, alpha, flo, fhi, prev, dx, dxold; int side, same; } LineSearch;
+
+static void lsr_init(LineSearch* L, double d0) {
+  L->lo = 0; L->dlo = d0; L->hi = -1; L->dhi = 0; L->alpha = 1; L->flo = d0; L->fhi = 0; L->prev = 0;
+  L->dx = L->dxold = 1e30;
+  L->side = 0; L->same = 0;
+}
+static int lsr_crosses(const LineSearch* L, double k) {
+  const int between = L->alpha > L->prev ? (k > L->prev && k < L->alpha) : (k < L->prev && k > L->alpha);
+  return between && k > L->lo && (L->hi < 0 || k < L->hi);
+}
+static void lsr_update(LineSearch* L, double d1, double d2) {
+  L->prev = L->alpha;
+  const int neg = d1 < 0, sd = neg ? -1 : 1;
+  L->same = sd == L->side ? L->same + 1 : 0;
+  L->side = sd;
+  const int rep = L->same > 0;
+  const double hlo = (!neg && rep) ? 0.5 : 1, hhi = (neg && rep && L->hi >= 0) ? 0.5 : 1;
+  if (neg) { L->lo = L->alpha; L->dlo = d1; L->flo = d1; L->fhi *= hhi; }
+  else { L->flo *= hlo; L->hi = L->alpha; L->dhi = d1; L->fhi = d1; }
+  const double an_n = L->alpha - d1 / (d2 > 1e-30 ? d2 : 1e-30);
+  const double fp = L->lo - L->flo * (L->hi - L->lo) / (L->fhi - L->flo);
+  const double an_f = (fp > L->lo && fp < L->hi) ? fp : 0.5 * (L->lo + L->hi);
+  const double an_o = an_n > L->lo ? an_n : (L->lo > 0 ? 2 * L->lo : 1);
+  const int nw = an_n > L->lo && an_n < L->hi && fabs(an_n - L->alpha) <= 0.5 * L->dxold;
+  const double an = L->hi < 0 ? an_o : (nw ? an_n : an_f);
+  L->dxold = L->dx;
+  L->dx = fabs(an - L->alpha);
+  L->alpha = an;
+}
+static void lsr_snap(LineSearch* L, double k) { L->alpha = k; L->dx = fabs(k - L->prev); }
+static double lsr_fallback(const LineSearch* L) {
+  return L->lo > 0 ? L->lo : (L->hi > 0 ? L->hi * L->dlo / (L->dlo - L->dhi) : 0);
+}
+
 /* Newton solve of min 0.5(a-a0)'M(a-a0) + s(Ja - aref) (mj_solNewton) */
 static int newton(const Efc* e, const double* Mm, const double* a0, double* a, double scale) {
   int nr = 3 * e->nc, it;
@@ -1218,7 +1315,9 @@ static int newton(const Efc* e, const double* Mm, const double* a0, double* a, d
     for (int i = 0; i < NV; i++) gn += grad[i] * grad[i];
     if (g_flags & 256) fprintf(stderr, "it %d gn %.3e\n", it, scale * sqrt(gn));
     if (g_flags & 512) fprintf(stderr, "G %d %.17g\n", it, scale * sqrt(gn));
-    if (scale * sqrt(gn) < g_tol) break;
+    /* MuJoCo's gradient stop: scale * ||grad|| < opt.tolerance, tested after an
+     * iteration (mj_solPrimal, engine_solver.c; the first iteration always runs) */
+    if (it > 0 && scale * sqrt(gn) < g_tol) break;
     double H[NV * NV];
     memcpy(H, Mm, sizeof H);
     for (int c = 0; c < e->nc; c++) {
@@ -1238,39 +1337,92 @@ static int newton(const Efc* e, const double* Mm, const double* a0, double* a, d
     double s[NV];
     for (int i = 0; i < NV; i++) s[i] = -grad[i];
     chol_solve(H, NV, s);
-    /* exact line search on phi(alpha) */
+    /* line search on phi(alpha) = f(a + alpha s) */
     double Ms[NV], sMs = 0, sMdq = 0, Js[BBO_MAXCON * 3];
     for (int i = 0; i < NV; i++) { double t = 0; for (int j = 0; j < NV; j++) t += Mm[i * NV + j] * s[j]; Ms[i] = t; }
     for (int i = 0; i < NV; i++) { sMs += s[i] * Ms[i]; sMdq += Ms[i] * dq[i]; }
     for (int r = 0; r < nr; r++) { double t = 0; for (int d = 0; d < NV; d++) t += e->J[r][d] * s[d]; Js[r] = t; }
-    double lo = 0, hi = -1, alpha = 1, d0 = 0;
-    double jt[BBO_MAXCON * 3], ft[BBO_MAXCON * 3], Ht[BBO_MAXCON * 9];
+    double d0 = 0, alpha;
+    double jt[BBO_MAXCON * 3], ft[BBO_MAXCON * 3];
+    static __thread LsTerm lt[BBO_MAXCON];
+    const int exact = (g_flags & 2048) != 0;
     for (int r = 0; r < nr; r++) d0 -= force[r] * Js[r];
     d0 += sMdq;
     if (d0 >= 0) break; /* not a descent direction: converged to roundoff */
-    for (int ls = 0; ls < g_lsmax; ls++) {
-      for (int r = 0; r < nr; r++) jt[r] = jar[r] + alpha * Js[r];
-      total_cost(e, jt, ft, Ht);
-      double d1 = sMdq + alpha * sMs, d2 = sMs;
-      for (int c = 0; c < e->nc; c++) {
-        for (int p = 0; p < 3; p++) {
-          d1 -= ft[3 * c + p] * Js[3 * c + p];
-          for (int q = 0; q < 3; q++) d2 += Js[3 * c + p] * Ht[9 * c + 3 * p + q] * Js[3 * c + q];
+    if (exact) { /* the exact search of earlier rounds: Newton/bisection on phi' to g_lstol */
+      double lo = 0, hi = -1, Ht[BBO_MAXCON * 9];
+      alpha = 1;
+      for (int ls = 0; ls < g_lsmax; ls++) {
+        for (int r = 0; r < nr; r++) jt[r] = jar[r] + alpha * Js[r];
+        total_cost(e, jt, ft, Ht);
+        double d1 = sMdq + alpha * sMs, d2 = sMs;
+        for (int c = 0; c < e->nc; c++) {
+          for (int p = 0; p < 3; p++) {
+            d1 -= ft[3 * c + p] * Js[3 * c + p];
+            for (int q = 0; q < 3; q++) d2 += Js[3 * c + p] * Ht[9 * c + 3 * p + q] * Js[3 * c + q];
+          }
         }
+        if (fabs(d1) <= g_lstol * fabs(d0)) break;
+        if (d1 < 0) lo = alpha; else hi = alpha;
+        double an = alpha - d1 / d2;
+        if (hi < 0) { if (an <= lo) an = 2 * alpha; }
+        else if (!(an > lo && an < hi)) an = 0.5 * (lo + hi);
+        if (hi >= 0 && hi - lo <= 1e-16 * hi) break;
+        alpha = an;
       }
-      if (fabs(d1) <= g_lstol * fabs(d0)) break;
-      if (d1 < 0) lo = alpha; else hi = alpha;
-      double an = alpha - d1 / d2;
-      if (hi < 0) { if (an <= lo) an = 2 * alpha; }
-      else if (!(an > lo && an < hi)) an = 0.5 * (lo + hi);
-      if (hi >= 0 && hi - lo <= 1e-16 * hi) break;
-      alpha = an;
+    } else {
+      /* MuJoCo stops its line search at |phi'| <= ls_tolerance |phi'(0)| within
+       * ls_iterations; its search path is not restated (parity unpinned).  The
+       * oracle runs the kernel's 1-D search (bb_solve.h LineSearch: safeguarded
+       * Newton / Illinois false position, steps stopped at contact kinks) to that
+       * criterion, so that the Newton iterates, and with them MuJoCo's
+       * improvement stop below, are the kernel's up to roundoff */
+      for (int c = 0; c < e->nc; c++)
+        ls_prep(&lt[c], jar + 3 * c, Js + 3 * c, e->mu[c], e->fr[c][0], e->fr[c][1], e->D + 3 * c,
+                e->D[3 * c] / (e->mu[c] * e->mu[c] * (1 + e->mu[c] * e->mu[c])));
+      LineSearch L;
+      lsr_init(&L, d0);
+      int ok = 0;
+      for (int ls = 1; ls <= g_lsmax; ls++) {
+        double d1p = 0, d2p = 0, dmp = 0;
+        for (int c = 0; c < e->nc; c++) ls_eval(&lt[c], L.alpha, &d1p, &d2p, &dmp);
+        const double d1 = sMdq + L.alpha * sMs + d1p;
+        if (fabs(d1) <= g_lstol * fabs(d0)) { ok = 1; break; }
+        const double dmag = fabs(sMdq) + fabs(L.alpha * sMs) + dmp;
+        if (fabs(d1) <= 32 * DBL_EPSILON * dmag) { ok = 1; break; }
+        if (d1 != d1) break;
+        lsr_update(&L, d1, sMs + d2p);
+        const int up = L.alpha > L.prev;
+        double kn = -1;
+        for (int c = 0; c < e->nc; c++)
+          if (lsr_crosses(&L, lt[c].kink) && (kn < 0 || (up ? lt[c].kink < kn : lt[c].kink > kn))) kn = lt[c].kink;
+        if (kn > 0) lsr_snap(&L, kn);
+      }
+      if (!ok) L.alpha = lsr_fallback(&L);
+      alpha = L.alpha;
+      if (!(alpha > 0)) break;
     }
     if (g_flags & 256) fprintf(stderr, "   alpha %.6e d0 %.3e\n", alpha, d0);
+    /* the cost change of the step: Gauss term alpha s'M(a - a0) + alpha^2 s'Ms / 2
+     * (closed form on the line) plus the constraint cost at a + alpha s minus at a */
+    double dcost = alpha * (sMdq + 0.5 * alpha * sMs);
+    if (exact) {
+      for (int r = 0; r < nr; r++) jt[r] = jar[r] + alpha * Js[r];
+      dcost += total_cost(e, jt, ft, NULL) - ccost;
+    } else { /* per contact, as the kernel sums it (phi_c(alpha) - phi_c(0), bb_team16.h solve16) */
+      double dc = 0;
+      for (int c = 0; c < e->nc; c++) dc += ls_cost(&lt[c], alpha) - ls_cost(&lt[c], 0);
+      dcost += dc;
+    }
     double snorm = 0, anorm = 0;
     for (int i = 0; i < NV; i++) { a[i] += alpha * s[i]; snorm += (alpha * s[i]) * (alpha * s[i]); anorm += a[i] * a[i]; }
     /* roundoff floor: the step no longer moves qacc */
     if (sqrt(snorm) <= 1e-15 * (1 + sqrt(anorm))) { it++; break; }
+    /* MuJoCo's improvement stop: scale * (oldcost - cost) < opt.tolerance after the
+     * iteration (mj_solPrimal, engine_solver.c, MuJoCo 99490163 as pinned by the
+     * reference, Readme.md:101-103): the Newton solve ends when either the scaled
+     * cost decrease or the scaled gradient falls below the tolerance */
+    if (-scale * dcost < g_tol) { it++; break; }
   }
   return it;
 }

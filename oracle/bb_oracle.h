@@ -82,6 +82,8 @@ int  bbo_abi_version(void);
 void bbo_set_flags(int flags);
 int  bbo_get_flags(void);
 void bbo_set_solver(int maxiter, double tol);
+/* line search: at most ls_iterations evaluations, stop at |phi'| <= ls_tolerance |phi'(0)| */
+void bbo_set_linesearch(int ls_iterations, double ls_tolerance);
 void bbo_model_info(double* out);   /* masses, invweight0, meaninertia, qpos0 ... (see .c) */
 
 /* mj_forward at (qpos, qvel) with ctrl; warm = qacc_warmstart (may be NULL). */

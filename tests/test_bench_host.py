@@ -10,16 +10,18 @@ import bench  # noqa: E402
 
 
 def test_algorithmic_bytes_one_step_per_launch():
-    # fp64 841 B per env-step (state r/w 752, action 12, obs 60, reward 4, done 1,
-    # step counter r/w 8, terrain id 4); fp32 465 B
-    assert bench.algorithmic_bytes("fp64") == 841
-    assert bench.algorithmic_bytes("fp32") == 465
+    # fp64 909 B per env-step (state r/w 752, action 12, obs 60, reward 4, done 1,
+    # terminal obs 60, pos2d 8, step counter r/w 8, terrain id 4); fp32 533 B; relief terrain
+    # + the 7 x 7 float32 hfield vertices under the ball (+196 B)
+    assert bench.algorithmic_bytes("fp64") == 909
+    assert bench.algorithmic_bytes("fp32") == 533
+    assert bench.algorithmic_bytes("fp64", 1, relief=True) == 909 + 196
 
 
 @pytest.mark.parametrize("k", [2, 20, 64, 256])
 def test_algorithmic_bytes_multi_step_moves_state_once(k):
     per_launch = 2 * 47 * 8 + 8 + 4
-    assert bench.algorithmic_bytes("fp64", k) == pytest.approx(per_launch / k + 77)
+    assert bench.algorithmic_bytes("fp64", k) == pytest.approx(per_launch / k + 145)
     # K steps of one env in one launch move less than K single-step launches
     assert k * bench.algorithmic_bytes("fp64", k) < k * bench.algorithmic_bytes("fp64")
 

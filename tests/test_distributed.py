@@ -39,7 +39,7 @@ def _worker(rank, world, port, q):
     buf = torch.arange(start, start + count, dtype=torch.float32).view(1, count, 1).expand(3, count, 4).contiguous()
     out = gather_rollouts(buf)
     if rank == 0:
-        q.put((t, out[0, :, 0].tolist(), (shard_stream_seeds(5, start, count), shard_stream_seeds(5, start, count, True))))
+        q.put((t, out[0, :, 0].tolist(), (shard_stream_seeds(5, start, count, per_env=False), shard_stream_seeds(5, start, count))))
     dist.destroy_process_group()
 
 
@@ -56,7 +56,7 @@ def test_gloo_world2_gather_and_max():
         assert p.exitcode == 0
     assert t == 2.0
     assert ids == [float(i) for i in range(10)]
-    assert seed0 == (None, [5, 6, 7, 8, 9])  # shared training stream; per-env eval streams from the global id
+    assert seed0 == (None, [5, 6, 7, 8, 9])  # shared stream on request; per-env generators from the global id
 
 
 def _ppo_worker(rank, world, port, q):
@@ -140,6 +140,82 @@ def test_gloo_world2_data_parallel_update(target_kl):
     np.testing.assert_allclose(v0, ref, rtol=1e-6, atol=1e-7)
     if target_kl is not None:
         assert kl0 == pytest.approx(m.logger.values.get("train/approx_kl"), rel=1e-6)
+
+
+def _dp_norm_worker(rank, world, port, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    from fake_env import FakeEnv
+    from test_ppo import _ppo
+
+    env = FakeEnv(8, seed=5 + 11 * rank, ep_len=3 + rank)  # different data on the two ranks
+    m = _ppo(env, n_steps=4, batch_size=16, n_epochs=2, update_mode="allreduce", normalize_advantage=True)
+    seen = []
+    m._dp_adv_hook = lambda raw, out: seen.append((raw.detach().numpy().copy(), out.detach().numpy().copy()))
+    m.learn(total_timesteps=2 * 8 * 4 * world)
+    q.put((rank, seen))
+    dist.destroy_process_group()
+
+
+def test_gloo_world2_data_parallel_global_advantage_normalisation():
+    """update_mode="allreduce" normalises each minibatch's advantages as SB3 does --
+    (adv - mean) / (std + 1e-8), unbiased std -- over the GLOBAL minibatch, the union of
+    the ranks' local minibatches (one all-reduce of count, sum and sum of squares), not
+    per local minibatch.  Ranks hold different data; every minibatch's normalised
+    advantages are checked against the statistics of the two ranks' raw slices."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_dp_norm_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = dict(q.get(timeout=180) for _ in range(2))
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    a, b = res[0], res[1]
+    assert len(a) == len(b) > 0  # the same number of minibatches on both ranks
+    local_differs = False
+    for (ra, na), (rb, nb) in zip(a, b):
+        raw = np.concatenate([ra, rb]).astype(np.float64)
+        mean, std = raw.mean(), raw.std(ddof=1)
+        np.testing.assert_allclose(na, (ra - mean) / (std + 1e-8), rtol=1e-5, atol=1e-6)
+        np.testing.assert_allclose(nb, (rb - mean) / (std + 1e-8), rtol=1e-5, atol=1e-6)
+        union = np.concatenate([na, nb]).astype(np.float64)
+        assert abs(union.mean()) < 1e-5 and abs(union.std(ddof=1) - 1) < 1e-4
+        local = (ra - ra.mean()) / (ra.std(ddof=1) + 1e-8)
+        local_differs |= not np.allclose(local, na, atol=1e-3)
+    assert local_differs  # the global statistics are not each rank's own
+
+
+def _uneven_worker(rank, world, port, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    from fake_env import FakeEnv
+    from test_ppo import _ppo
+
+    try:
+        _ppo(FakeEnv(8 + rank), n_steps=4, batch_size=16, update_mode="allreduce")
+        q.put((rank, "built"))
+    except ValueError as e:
+        q.put((rank, str(e)))
+    dist.destroy_process_group()
+
+
+def test_gloo_world2_allreduce_rejects_uneven_shards():
+    """9 + 8 envs (env_shard of an odd total): the data-parallel update would run a
+    different number of minibatch all-reduces per rank and deadlock; both ranks raise."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_uneven_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = dict(q.get(timeout=120) for _ in range(2))
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    assert all("same number of envs" in v for v in res.values()), res
 
 
 def test_data_parallel_needs_divisible_batch():

@@ -64,8 +64,10 @@ def test_config3_full_size_route0(oracle, terrain, n_terrains, monkeypatch):
 
     monkeypatch.setenv("BB_ROUTE", "0")
     n = 4096
+    # perlin: SB3-seeded generators over the whole seed space; hills: one shared generator,
+    # so the host-generated bank stays at 32 draws' seeds
     env = BallbotVecEnv(n, device="cuda:0", seed=21, terrain_config={"type": terrain, "config": {}},
-                        n_terrains=n_terrains)
+                        n_terrains=n_terrains, shared_stream=terrain == "hills")
     assert env.launch_config()["envs_per_wave"] == 4
     g = torch.Generator(device="cuda:0").manual_seed(9)
     for t in range(300):

@@ -107,38 +107,6 @@ def test_cameras_in_observation():
     env.close()
 
 
-def test_terrain_seeds_follow_the_reference_generators():
-    """eval_env=[True, s]: _np_random = np_random(s) from construction (ballbot_env.py:378-384);
-    otherwise np_random(seed of the first reset), which that reset also advances by the
-    log-dir permutation (:658-661) after its terrain draw."""
-    import string
-
-    from ballbot_gym.envs.config import np_random
-
-    env = _make(terrain_type="hills", eval_env=[True, 10], n_terrains=8)
-    seen = []
-    for _ in range(3):
-        env.reset(seed=999)  # ignored for the terrain stream in eval mode
-        seen.append(int(env.last_r_seed))
-    assert seen == [7765, 9560, 2640]
-    env.close()
-    env = _make(terrain_type="hills", n_terrains=8)
-    g = np_random(42)
-    exp = [int(g.integers(0, 10000))]
-    g.permutation(list(string.ascii_letters + string.digits))
-    exp += [int(g.integers(0, 10000)) for _ in range(2)]
-    seen = []
-    for _ in range(3):
-        env.reset(seed=42)
-        seen.append(int(env.last_r_seed))
-    assert seen == exp
-    hf = env._env.hfield(env._env.env_terrain()[0][0])
-    from ballbot_gym.terrain import generate_hills_terrain
-
-    assert np.array_equal(hf, generate_hills_terrain(293, seed=exp[2]).astype(np.float32))
-    env.close()
-
-
 # --- B2: custom reward plugins -------------------------------------------------
 class VelocityMagnitudeReward:
     """examples/02_custom_reward.py:19-45 (scale * |vel[:2]|), per-env ABI."""

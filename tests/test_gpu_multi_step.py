@@ -119,6 +119,8 @@ def test_multi_step_adaptive_relief_route(terrain, monkeypatch):
 
     n = 512 if terrain == "hills" else 256
     kw = dict(device="cuda:0", seed=3, terrain_config={"type": terrain, "config": {}}, max_ep_steps=50)
+    if terrain == "hills":
+        kw.update(n_terrains=2)  # the seeds of two draws per generator (later draws: counted misses)
     if terrain == "perlin":
         kw.update(n_terrains=None, stream_seeds=[60 + i for i in range(n)])
     monkeypatch.setenv("BB_ROUTE", "1")
@@ -130,6 +132,58 @@ def test_multi_step_adaptive_relief_route(terrain, monkeypatch):
     actions = torch.rand(192, n, 3, generator=g, device="cuda:0") * 2 - 1
     st = _compare_runs(a, b, actions, 32, exact=False)
     assert st["resets"] > 0
+    a.close(), b.close()
+
+
+def _chunked_equal(a, b, pool, chunks, start=0):
+    """a: one bb_step per step; b: bb_step_multi launches of `chunks` steps, both reading
+    the cyclic action pool from slot `start` -- every output of every step (obs, reward,
+    done, terminal obs, pos2d) bit for bit, chunk by chunk."""
+    PS = pool.shape[0]
+    j = start
+    for k in chunks:
+        assert j % PS + k <= PS
+        acts = pool[j % PS:j % PS + k]
+        out = b.step_multi(acts)
+        for t in range(k):
+            obs, rew, _, _, info = a.step(acts[t])
+            for key, ref in (("obs", obs), ("reward", rew), ("done", info["done_flags"]),
+                             ("terminal_obs", info["terminal_observation"]), ("pos2d", info["pos2d"])):
+                assert torch.equal(out[key][t], ref), (key, j + t)
+        j += k
+    return j
+
+
+@pytest.mark.parametrize("terrain,route", [("flat", "1"), ("perlin", "0")])
+def test_headline_form_k256_and_driver_window(terrain, route, monkeypatch):
+    """The exact form bench.py times: a 256-slot action pool resident in HBM, a burn-in of
+    400 steps, 300 warm-up steps, then the timed 500 steps as two launches of 256 + 244
+    (bench.launch_chunks); and the driver's window, one 20-step launch after the burn-in.
+    Against one bb_step per step, bit for bit (flat: 4096 envs, configs[1]; perlin: 1024
+    envs on per-env generators over the whole seed space, route 0: the work queue)."""
+    import sys
+    from pathlib import Path
+
+    sys.path.insert(0, str(Path(__file__).resolve().parents[1]))
+    import bench
+
+    n = 4096 if terrain == "flat" else 1024
+    kw = {} if terrain == "flat" else {"n_terrains": None}
+    a, b = _pair(n, terrain, monkeypatch, route=route, **kw)
+    g = torch.Generator(device="cuda:0").manual_seed(1234)
+    PS = 256
+    pool = torch.rand(PS, n, 3, generator=g, device="cuda:0") * 2 - 1
+    assert bench.launch_chunks(500, 256, PS) == [256, 244]
+    j = _chunked_equal(a, b, pool, bench.launch_chunks(700, 256, PS))  # burn-in + warm-up
+    _chunked_equal(a, b, pool, bench.launch_chunks(500, 256, PS), start=0)  # the timed window
+    j = _chunked_equal(a, b, pool, [20], start=0)  # the driver's --steps 20 window, post burn-in
+    for x, y in zip(a.get_state(), b.get_state()):
+        np.testing.assert_array_equal(x, y)
+    for x, y in zip(a.terrain_rng(), b.terrain_rng()):  # (generators on perlin; None on flat), last draws
+        assert (x is None and y is None) or np.array_equal(x, y)
+    sa, sb = a.stats(), b.stats()
+    assert sa == sb, (sa, sb)
+    assert sa["resets"] > n // 2
     a.close(), b.close()
 
 

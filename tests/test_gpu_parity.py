@@ -221,6 +221,66 @@ def test_forward_parity_contacts_past_lds(oracle, terrain):
 
 
 @pytest.mark.parametrize("terrain", ["flat", "hills"])
+def test_ball_hfield_contact_cap(oracle, terrain):
+    """The ball pressed into the terrain (its centre within ~3 cm of the surface)
+    intersects more prisms than MuJoCo keeps for one geom pair (mjMAXCONPAIR = 50,
+    bb_team16.h collide_team MAXG, oracle/bb_oracle.c BBO_MAXGROUND): both keep the
+    first 50 in prism order.  Contact counts and qacc of the forward, then one
+    teacher-forced step (state, obs, reward) vs the oracle, and the step's
+    overflow counter."""
+    from ballbot_gym.terrain import generate_hills_terrain
+
+    n = 48
+    if terrain == "flat":
+        hf, tcfg, top = oracle.flat_hfield(), {"type": "flat", "config": {}}, 0.0
+    else:
+        hf = generate_hills_terrain(293, seed=7).astype(np.float32)
+        tcfg = {"type": "hills", "config": {"seed": 7}}
+    rng = np.random.default_rng(8)
+    qs, vs = [], []
+    H = hf.reshape(293, 293)
+    for i in range(n):
+        q, v, _ = oracle.reset_state(0.01)
+        x, y = rng.uniform(-0.3, 0.3, 2)
+        if terrain != "flat":  # the terrain's height under the ball centre (nearest vertex)
+            r, c = int(round((y + 5) / 10 * 292)), int(round((x + 5) / 10 * 292))
+            top = float(H[r, c]) * 2.0
+        q[10:13] = [x, y, top + 0.14 + rng.uniform(-0.03, 0.08)]  # ball body: geom centre 0.14 below
+        q[0:3] = [x, y, top + 1.0]  # the base well above (no base-tree contact)
+        v[:] = rng.normal(0, 0.05, 15)
+        qs.append(q)
+        vs.append(v)
+    qs, vs = np.array(qs), np.array(vs)
+    env = _make_env(n, "fp64", tcfg)
+    ctrl = rng.uniform(-10, 10, (n, 3))
+    env.set_state(qs, vs, np.zeros((n, 15)))
+    qacc, ncon = env.forward(ctrl)
+    capped = 0
+    for e in range(n):
+        fo = oracle.forward(qs[e], vs[e], ctrl[e], np.zeros(15), hf)
+        assert (ncon[e, 0], ncon[e, 1]) == (fo.nground, fo.nbody), e
+        capped += fo.ground_overflow != 0
+        ref = np.array(fo.qacc)
+        err = np.abs(qacc[e] - ref).max() / max(1.0, np.abs(ref).max())
+        assert err < 1e-7, (e, err, fo.nground)
+    assert capped >= n // 4 and (ncon[:, 0] == 50).sum() == capped, (capped, np.bincount(ncon[:, 0]))
+    acts = rng.uniform(-1, 1, (n, 3)).astype(np.float32)
+    s0 = env.stats()
+    env.set_state(qs, vs, np.zeros((n, 15)))
+    obs, rew, _, _, info = env.step(torch.tensor(acts, device="cuda:0"))
+    q1, v1, _, _ = env.get_state()
+    assert env.stats()["overflow"] - s0["overflow"] >= capped
+    cfg = oracle.default_cfg()
+    for e in range(n):
+        qe, ve, we, se = qs[e].copy(), vs[e].copy(), np.zeros(15), np.zeros(1, np.int32)
+        o, r, f, _, _ = oracle.env_step(cfg, qe, ve, we, se, acts[e], hf)
+        assert np.abs(q1[e] - qe).max() < 1e-9, e
+        assert np.abs(v1[e] - ve).max() < 1e-6 * max(1.0, np.abs(ve).max()), e
+        assert np.abs(obs.cpu().numpy()[e] - o).max() < 1e-6 and abs(float(rew[e]) - r) < 1e-7, e
+    env.close()
+
+
+@pytest.mark.parametrize("terrain", ["flat", "hills"])
 def test_step_routes_agree(oracle, terrain, monkeypatch):
     """The two step routes (predict + concurrent full kernel, BB_ROUTE=0; serial
     fast-then-full, BB_ROUTE=1; the default picks serial on flat banks) and the
@@ -328,7 +388,8 @@ def test_c_abi_range_errors_on_gpu():
     from ballbot_gym import _native as N
     from ballbot_gym.envs import BallbotVecEnv
 
-    env = BallbotVecEnv(64, device="cuda:0", n_terrains=2, terrain_config={"type": "hills", "config": {}})
+    env = BallbotVecEnv(64, device="cuda:0", n_terrains=2, terrain_config={"type": "hills", "config": {}},
+                        shared_stream=True)
     L, h = N.lib(), env._h
     hf = np.zeros(293 * 293, np.float32)
     fp = hf.ctypes.data_as(C.POINTER(C.c_float))

@@ -35,7 +35,7 @@ def test_depth_matches_oracle(oracle, terrain):
         tcfg = {"type": "hills", "config": {"seed": 7}}
     else:  # GPU bank slot 0 = the first seed of np_random(0); sloped ground in view
         hf = generate_perlin_terrain(293, seed=int(np_random(0).integers(0, 10000))).astype(np.float32)
-        tcfg, kw = {"type": "perlin", "config": {}}, {"n_terrains": 1}
+        tcfg, kw = {"type": "perlin", "config": {}}, {"n_terrains": 1, "shared_stream": True}
     rec = traj.record(n_envs=32, n_steps=40, hfield=hf, seed=21)
     env = _env(32, tcfg, **kw)
     for t in (0, 13, 39):

@@ -22,7 +22,7 @@ def _env(cfg, n_terrains, n_envs=64, seed=0):
     from ballbot_gym.envs import BallbotVecEnv
 
     return BallbotVecEnv(n_envs, device="cuda:0", terrain_config={"type": "perlin", "config": dict(cfg)},
-                         n_terrains=n_terrains, seed=seed, auto_reset=False)
+                         n_terrains=n_terrains, seed=seed, auto_reset=False, shared_stream=True)
 
 
 @pytest.mark.parametrize("cfg", [{}, HARD, {"amplitude": 1.7, "seed": None}], ids=["default", "hard", "amp"])
@@ -103,7 +103,8 @@ def test_step_parity_terrain_generators(oracle, ttype):
                          "blend_mode": "additive"}
     hfs, seeds, size_z = terrain_bank(cfg, 1, seed=5)
     hf = np.asarray(hfs[0], np.float32).ravel()
-    env = BallbotVecEnv(32, device="cuda:0", terrain_config=cfg, n_terrains=1, seed=5, auto_reset=False)
+    env = BallbotVecEnv(32, device="cuda:0", terrain_config=cfg, n_terrains=1, seed=5, auto_reset=False,
+                        shared_stream=True)
     assert np.array_equal(env.hfield(0), hf)
     rec = traj.record(n_envs=32, n_steps=40, hfield=hf, size_z=size_z, seed=17)
     _teacher_forced(env, rec, TOL["fp64"])
