@@ -67,7 +67,7 @@ extern "C" {
 #define BB_DONE_FAILURE 2
 #define BB_DONE_DIVERGED 4 /* MuJoCo's divergence reset ran inside this step (informational) */
 #define BB_DONE_OVERFLOW 8
-#define BB_NSTATS 7
+#define BB_NSTATS 8
 
 /* reward kinds (built-in reward plugins, ballbot_gym/rewards) */
 #define BB_REWARD_DIRECTIONAL 0 /* rewards/directional.py:33-54 */

@@ -16,7 +16,7 @@ INCLUDE = PKG.parent.parent / "include"
 
 NQ, NV, NOBS, HF_N = 17, 15, 15, 293
 DONE_TERMINATED, DONE_FAILURE, DONE_DIVERGED, DONE_OVERFLOW = 1, 2, 4, 8
-NSTATS = 7  # BB_NSTATS
+NSTATS = 8  # BB_NSTATS
 REWARD_DIRECTIONAL, REWARD_DISTANCE, REWARD_NONE = 0, 1, 2
 
 

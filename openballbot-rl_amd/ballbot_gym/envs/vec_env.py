@@ -514,7 +514,7 @@ class BallbotVecEnv:
         out = (C.c_int64 * N.NSTATS)()
         N.check(N.lib().bb_get_stats(self._h, out, N.NSTATS), "bb_get_stats")
         return {"resets": out[0], "diverged": out[1], "overflow": out[2], "slow_path": out[3],
-                "solver_iters": out[4], "stream_wraps": out[5], "spill": out[6]}
+                "solver_iters": out[4], "stream_wraps": out[5], "spill": out[6], "pair_budget": out[7]}
 
     def env_terrain(self):
         """(bank slot of every env's current terrain, stream draws each env made) as int32[N] arrays."""

@@ -1004,14 +1004,22 @@ class BatchedPPO:
 
     # ------------------------------------------------------------------ learn
     def learn(self, total_timesteps: int, callback: Optional[Callable[["BatchedPPO"], bool]] = None,
-              log_interval: int = 1) -> "BatchedPPO":
-        """SB3 OnPolicyAlgorithm.learn: rollout -> (logs) -> update until total_timesteps."""
+              log_interval: int = 1,
+              rollout_callback: Optional[Callable[["BatchedPPO", int, int], None]] = None) -> "BatchedPPO":
+        """SB3 OnPolicyAlgorithm.learn: rollout -> (logs) -> update until total_timesteps.
+        rollout_callback(self, first_vec_step, last_vec_step): after each rollout and
+        before its update, with the parameters the rollout ran with -- where SB3's
+        per-step callbacks (EvalCallback's _on_step) see them; callback(self): after
+        the update."""
         total = int(total_timesteps)
         t0 = time.perf_counter()
         start_steps = self.num_timesteps
         iteration = 0
         while self.num_timesteps < total:
+            v0 = self.num_timesteps // max(self.n_envs * self.world, 1)
             self.collect_rollouts()
+            if rollout_callback is not None:
+                rollout_callback(self, v0 + 1, v0 + self.n_steps)
             iteration += 1
             self.progress_remaining = 1.0 - float(self.num_timesteps) / float(total)
             if log_interval and iteration % log_interval == 0 and self.rank == 0:

@@ -102,9 +102,11 @@ def main(config: Dict[str, Any], seed: int, out: Optional[str] = None, total_tim
     env = make_env(config, n_local, dev, seed, precision, shard_stream_seeds(seed, first, n_local, per_env=not shared))
     eval_cfg = config.get("evaluation", {}) or {}
     n_eval = int(eval_cfg.get("n_episodes", 8))
-    # eval env i draws from np_random(seed + N_ENVS + i) (train.py:90-97)
-    eval_env = (make_env(config, max(n_eval, 1), dev, seed + n_total, precision,
-                         shard_stream_seeds(seed + n_total, 0, max(n_eval, 1), per_env=True)) if rank == 0 else None)
+    # the eval VecEnv: N_ENVS envs, env i on np_random(seed + N_ENVS + i) (train.py:90-97);
+    # evaluation.num_envs overrides its size for GPU-sized runs (thousands of training envs)
+    n_eval_envs = int(eval_cfg.get("num_envs", n_total))
+    eval_env = (make_env(config, n_eval_envs, dev, seed + n_total, precision,
+                         shard_stream_seeds(seed + n_total, 0, n_eval_envs, per_env=True)) if rank == 0 else None)
 
     out_path = experiment_dir(config, out if out is not None else config.get("out"))
     logger = None
@@ -135,22 +137,15 @@ def main(config: Dict[str, Any], seed: int, out: Optional[str] = None, total_tim
     if config.get("resume"):
         model.load_policy(config["resume"])
     eval_freq = int(eval_cfg.get("freq", 5000))
-    state = {"best": -np.inf, "next_eval": eval_freq}
+    on_rollout = None
+    if rank == 0 and eval_env is not None:
+        from ballbot_rl.training.callbacks import EvalCallback
 
-    def on_rollout(m: BatchedPPO) -> bool:
-        vec_steps = m.num_timesteps // n_total  # SB3 EvalCallback counts vec-env steps
-        if rank == 0 and eval_env is not None and vec_steps >= state["next_eval"]:
-            state["next_eval"] = (vec_steps // eval_freq + 1) * eval_freq
-            r = evaluate_policy(m.policy, eval_env, n_eval_episodes=n_eval, deterministic=True)
-            m.logger.record("eval/mean_reward", r["mean_reward"])
-            m.logger.record("eval/mean_ep_length", r["mean_ep_length"])
-            if r["mean_reward"] > state["best"]:
-                state["best"] = r["mean_reward"]
-                m.save(str(out_path / "best_model.safetensors"))
-        return True
+        on_rollout = EvalCallback(eval_env, n_eval_episodes=n_eval, eval_freq=eval_freq, n_total_envs=n_total,
+                                  log_path=out_path / "results", best_model_save_path=out_path)
 
     total = int(float(total_timesteps if total_timesteps is not None else config["total_timesteps"]))
-    model.learn(total_timesteps=total, callback=on_rollout)
+    model.learn(total_timesteps=total, rollout_callback=on_rollout)
     if rank == 0:
         model.save(str(out_path / "final_model.safetensors"))
     env.close()

@@ -92,6 +92,7 @@ struct Dev {
   uint8_t* pred_mark;
   void* body_spill;           // T[n][MAXB - MAXB_LDS][NBF]: base-tree contacts past the LDS slots
   int* perm;                  // relief_multi_kernel: env of each workgroup slot (balance_kernel), NULL: identity
+  int* ring;                  // relief_pair_kernel: [2][n] FIFO rings of env ids ready for a fast / full step (-1: empty)
   unsigned long long* cost;   // relief_multi_kernel: shader cycles each env's steps took in the last launch
 };
 
@@ -392,25 +393,31 @@ constexpr int F_PARKED = 1 << 17;  // internal: never in a done byte
 // launches), SC_TOUCHED counts the envs of the last launch that needed a full step
 constexpr int SC_ROUTE = 8, SC_TOUCHED = 10, ROUTE_PARK = 1;
 
-template <typename T, bool HO = true>
+template <typename T, bool HO = true, bool FULLONLY = false>
 __device__ __forceinline__ int team_step(const ModelT<T>& m, const EnvCfg& cfg, const Dev& d, int e, int& tid,
                                          T* q, T* v, T* w, int& step, T* bk, const float* a, EnvWork<T>& W, float* o,
                                          float& r, float* tobs_row, float* p2_row, int auto_reset, const Team& tm,
                                          unsigned* cnt, bool full = false) {
+  // FULLONLY (relief_pair_kernel<T, true>): the full step only -- the fast path is
+  // not compiled in, so the launch keeps the full step's registers
   const int L = tm.L;
   const bool lead = tm.tl == 0;
-  team_sync();
-  for (int i = tm.tl; i < NQ + 2 * NV; i += L) bk[i] = q[i];
-  team_sync();
+  if constexpr (!FULLONLY) {
+    team_sync();
+    for (int i = tm.tl; i < NQ + 2 * NV; i += L) bk[i] = q[i];
+    team_sync();
+  }
   const float* hf = d.bank + size_t(tid) * (HF_N * HF_N);
   float p2[2];
   int iters = 0;
   const TerrainRef<T> tr{hf, T(d.size_z[tid]), T(d.hmax[tid]) * T(d.size_z[tid])};
   const int step0 = step;
+  int fl;
 #if BB_MULTI_MODE == 2
-  int fl = F_SLOWPATH;
+  fl = F_SLOWPATH;
 #else
-  int fl = full ? F_SLOWPATH : env_step<T, false>(m, cfg, q, v, w, step, a, tr, W, o, r, p2, &iters, tm);
+  if constexpr (FULLONLY) fl = F_SLOWPATH;
+  else fl = full ? F_SLOWPATH : env_step<T, false>(m, cfg, q, v, w, step, a, tr, W, o, r, p2, &iters, tm);
 #endif
   const bool slow = (fl & F_SLOWPATH) != 0;  // team-uniform
 #if BB_MULTI_MODE == 3
@@ -418,10 +425,12 @@ __device__ __forceinline__ int team_step(const ModelT<T>& m, const EnvCfg& cfg, 
 #else
   if (slow) {
 #endif
-    team_sync();
-    for (int i = tm.tl; i < NQ + 2 * NV; i += L) q[i] = bk[i];
-    team_sync();
-    step = step0;
+    if constexpr (!FULLONLY) {
+      team_sync();
+      for (int i = tm.tl; i < NQ + 2 * NV; i += L) q[i] = bk[i];
+      team_sync();
+      step = step0;
+    }
     if constexpr (!HO) return F_PARKED;
     else fl = full_env_step<T>(m, cfg, q, v, w, step, a, tr, W, o, r, p2, &iters, tm);
   }
@@ -1178,6 +1187,244 @@ __global__ __launch_bounds__(64 * QW) void relief_multi_kernel(ModelT<T> mg, Env
   }
 }
 
+// ---- bb_step_multi on relief banks: the relief pair --------------------------
+// relief_multi_kernel holds both steps, and the union of their registers spills
+// (512 VGPRs, ~1 KB of scratch per lane, 21.5 GB of HBM traffic per 256-step
+// launch on perlin).  The pair runs them as two PERSISTENT launches at the same
+// time, on two streams: relief_pair_kernel<T, false> takes the steps the
+// predictor routes to the fast path (only the fast step compiled in: no
+// scratch) and relief_pair_kernel<T, true> the full steps (only the full step).
+// An env moves between them through two FIFO rings of env ids in HBM (d.ring:
+// fast, full; head/tail counters in slow_count) with its state in HBM; d.park[e]
+// counts its steps.  Per env the steps are route 0's, as in relief_multi_kernel
+// and bb_step (bit-identical): a predicted env takes the full step, the others
+// the fast path, and an env the fast path hands over goes to the full launch,
+// which redoes that step.  A team holds an env for at most `seg` steps and
+// requeues it, so every env progresses evenly and the launch ends within a
+// few segments of its last env.  Of each launch's grid of pair_cap one-wave
+// workgroups (the chip's resident capacity) the first SC_ACTIVE[kind] work and
+// the rest exit at once; the two counts add up to pair_cap, so the working
+// workgroups of both launches are resident together and neither waits for the
+// other to be scheduled.  pair_adapt_kernel moves workgroups between the kinds
+// after each launch from the idle time each kind measured.  A wall-clock budget
+// ends both launches with an error flag (stats[7]) should a launch ever wait
+// for work that cannot come -- no hang.
+constexpr int SC_RHEAD = 16, SC_RTAIL = 18, SC_DONE = 20, SC_ERR = 21, SC_ACTIVE = 22, SC_IDLE = 24;
+
+__device__ __forceinline__ int ld_agent(const int* p) {
+  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// take the next env from ring `kind` (lead lane): -1 when the ring is empty
+__device__ __forceinline__ int ring_pop(const Dev& d, int kind) {
+  int* sc = d.slow_count;
+  int* ring = d.ring + size_t(kind) * d.n;
+  for (int att = 0; att < 4; att++) {
+    const int h = ld_agent(sc + SC_RHEAD + kind), t = ld_agent(sc + SC_RTAIL + kind);
+    if (h >= t) return -1;
+    if (atomicCAS(sc + SC_RHEAD + kind, h, h + 1) == h) {
+      int* slot = ring + (unsigned(h) % unsigned(d.n));
+      int e;
+      // the pusher reserved the slot before filling it: wait for the fill (a few cycles)
+      for (int spin = 0; (e = ld_agent(slot)) < 0 && spin < (1 << 20); spin++) __builtin_amdgcn_s_sleep(1);
+      __hip_atomic_store(slot, -1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      return e;
+    }
+  }
+  return -1;
+}
+
+// append env e to ring `kind` (lead lane; the env's state is stored and released)
+__device__ __forceinline__ void ring_push(const Dev& d, int kind, int e) {
+  int* sc = d.slow_count;
+  const int t = atomicAdd(sc + SC_RTAIL + kind, 1);
+  __hip_atomic_store(d.ring + size_t(kind) * d.n + (unsigned(t) % unsigned(d.n)), e, __ATOMIC_RELAXED,
+                     __HIP_MEMORY_SCOPE_AGENT);
+}
+
+template <typename T, bool FULL>
+__global__ __launch_bounds__(64) void relief_pair_kernel(ModelT<T> mg, EnvCfg cfg, Dev d, const float* __restrict__ act,
+                                                         int K, float* __restrict__ obs, float* __restrict__ rew,
+                                                         uint8_t* __restrict__ done, float* __restrict__ tobs,
+                                                         float* __restrict__ pos2d, int auto_reset, int seg,
+                                                         unsigned long long budget, const int* __restrict__ gate) {
+  int* sc = d.slow_count;
+  // adaptive form: the parked launches run instead; else only the active workgroups
+  // (workgroup-uniform, before any barrier)
+  if ((gate && *gate == ROUTE_PARK) || int(blockIdx.x) >= sc[SC_ACTIVE + FULL]) return;
+  extern __shared__ __align__(16) unsigned char smem[];
+  __shared__ ModelT<T> ms;
+  __shared__ unsigned s_cnt[WAVE / TEAM][8];
+  if (threadIdx.x == 0) ms = mg;
+  if (threadIdx.x < 32) s_cnt[threadIdx.x >> 3][threadIdx.x & 7] = 0u;
+  __syncthreads();
+  const ModelT<T>& m = ms;
+  const Team tm{TEAM, int(threadIdx.x) & (TEAM - 1)};
+  const int team = int(threadIdx.x) / TEAM;
+  const bool lead = tm.tl == 0;
+  const int n = d.n;
+  EnvWork<T>& W = team_work<T>(smem, team);
+  T* bk = reinterpret_cast<T*>(smem + size_t(WAVE / TEAM) * work_stride<T>()) + team * (NQ + 2 * NV);
+  unsigned* cnt = s_cnt[team];
+  const int kind = FULL ? 1 : 0;
+  const unsigned long long t0 = wall_clock64();
+  int e = -1, k = 0, tid = 0, step = 0, held = 0;
+  unsigned idle = 0;
+  for (;;) {
+    // a team without an env takes the next one of its kind (the rest of the wave
+    // skips this block); stop when every env has done its K steps
+    int stop = 0;
+    if (e < 0) {
+      int got = -1;
+      if (lead) {
+        if (ld_agent(sc + SC_DONE) >= n || ld_agent(sc + SC_ERR)) {
+          got = -2;
+        } else {
+          got = ring_pop(d, kind);
+          if (got < 0 && wall_clock64() - t0 > budget) {
+            if (atomicExch(sc + SC_ERR, 1) == 0) atomicAdd(&d.stats[7], 1ull);
+            got = -2;
+          }
+        }
+      }
+      got = __shfl(got, team_shift_of(TEAM));
+      if (got == -2) {
+        stop = 1;
+      } else if (got >= 0) {
+        e = got;
+        __threadfence();  // acquire: the state the releasing team stored
+        load_state(d, e, W.qn, W.vn, W.wn, step);
+        k = d.park[e];
+        tid = d.terrain[e];
+        held = 0;
+        if (lead) W.bspill = body_spill_of<T>(d, e);
+        team_sync();
+      }
+    }
+    if (stop) break;
+    if (e >= 0) {
+      const size_t row = size_t(k) * n + e;
+      const float* ak = act + 3 * row;
+      const float a[3] = {ak[0], ak[1], ak[2]};
+      float o[15], r;
+      const int fl = team_step<T, FULL, FULL>(m, cfg, d, e, tid, W.qn, W.vn, W.wn, step, bk, a, W, o, r,
+                                               tobs ? tobs + 15 * row : nullptr, pos2d ? pos2d + 2 * row : nullptr,
+                                               auto_reset, tm, cnt);
+      int next = kind;
+      if (!FULL && (fl & F_PARKED)) {  // the fast path handed the step over: the full launch redoes it
+        next = 1;
+      } else {
+        if (lead) {
+#pragma unroll
+          for (int i = 0; i < 15; i++) obs[15 * row + i] = o[i];
+          rew[row] = r;
+          done[row] = uint8_t(fl);
+        }
+        k++;
+        held++;
+        if (k < K) next = predict_env<T>(m, d, tid, W.qn, W.vn, tm.tl, team_shift_of(TEAM)) ? 1 : 0;
+      }
+      if (k >= K || next != kind || held >= seg) {  // release the env (team-uniform)
+        team_sync();
+        if (lead) {
+          store_state(d, e, W.qn, W.vn, W.wn, step);
+          d.park[e] = k;
+          __threadfence();  // release: the state before the ring entry
+          if (k >= K) atomicAdd(sc + SC_DONE, 1);
+          else ring_push(d, next, e);
+          if (FULL && gate) atomicAdd(sc + SC_TOUCHED, 1);  // adaptive route: an env took full steps
+        }
+        e = -1;
+      }
+    } else {
+      idle++;
+    }
+    // the wave sleeps only when none of its teams holds an env
+    if (__ballot(e >= 0) == 0ull) __builtin_amdgcn_s_sleep(8);
+  }
+  team_sync();
+  if (lead) {
+    counts_flush(d, cnt);
+    if (idle) atomicAdd(sc + SC_IDLE + kind, int(idle > 1000000u ? 1000000u : idle));
+  }
+}
+
+// before the pair: every env's first route (predict_kernel's test) into the
+// rings in env order, step counts to 0, counters reset.  One workgroup per 4 envs.
+template <typename T>
+__global__ __launch_bounds__(64) void pair_init_kernel(ModelT<T> mg, Dev d, const int* __restrict__ gate) {
+  if (gate && *gate == ROUTE_PARK) return;
+  __shared__ ModelT<T> ms;
+  if (threadIdx.x == 0) ms = mg;
+  __syncthreads();
+  const int tl = int(threadIdx.x) & 15;
+  const int e = blockIdx.x * (WAVE / 16) + int(threadIdx.x) / 16;
+  if (e >= d.n) return;  // team-uniform
+  const T* Q = (const T*)d.qpos;
+  const T* V = (const T*)d.qvel;
+  T Qe[NQ], Ve[6];
+#pragma unroll
+  for (int i = 0; i < NQ; i++) Qe[i] = Q[i * d.n + e];
+#pragma unroll
+  for (int i = 0; i < 6; i++) Ve[i] = V[i * d.n + e];
+  const bool full = predict_env<T>(ms, d, d.terrain[e], Qe, Ve, tl, team_shift_of(16));
+  if (tl == 0) {
+    d.pred_mark[e] = full ? 1 : 0;
+    d.park[e] = 0;
+  }
+}
+
+// after pair_init_kernel: the rings from the marks (stable, in env order; one
+// block, as split_kernel), their counters, and the empty slots
+__global__ __launch_bounds__(1024) void pair_rings_kernel(Dev d, const int* __restrict__ gate) {
+  if (gate && *gate == ROUTE_PARK) return;
+  __shared__ int sf[1024], ss[1024];
+  const int t = threadIdx.x, per = (d.n + 1023) / 1024, b = t * per, e_ = min(d.n, b + per);
+  int nf = 0, ns = 0;
+  for (int e = b; e < e_; e++) { if (d.pred_mark[e]) ns++; else nf++; }
+  sf[t] = nf; ss[t] = ns;
+  __syncthreads();
+  for (int off = 1; off < 1024; off <<= 1) {
+    const int af = t >= off ? sf[t - off] : 0, as = t >= off ? ss[t - off] : 0;
+    __syncthreads();
+    sf[t] += af; ss[t] += as;
+    __syncthreads();
+  }
+  int of = sf[t] - nf, os = ss[t] - ns;
+  int* rf = d.ring;
+  int* rs = d.ring + d.n;
+  for (int e = b; e < e_; e++) {
+    if (d.pred_mark[e]) rs[os++] = e; else rf[of++] = e;
+  }
+  __syncthreads();
+  const int NF = sf[1023], NS = ss[1023];
+  for (int i = NF + t; i < d.n; i += 1024) rf[i] = -1;
+  for (int i = NS + t; i < d.n; i += 1024) rs[i] = -1;
+  if (t == 0) {
+    int* sc = d.slow_count;
+    sc[SC_RHEAD] = 0; sc[SC_RHEAD + 1] = 0;
+    sc[SC_RTAIL] = NF; sc[SC_RTAIL + 1] = NS;
+    sc[SC_DONE] = 0; sc[SC_ERR] = 0;
+    sc[SC_IDLE] = 0; sc[SC_IDLE + 1] = 0;
+  }
+}
+
+// after the pair: move workgroups towards the kind that idled less (per active
+// workgroup), in steps of at most cap / 16, keeping cap / 8 for each kind.  The
+// counts only place work: every env's results are the same whatever they are.
+__global__ void pair_adapt_kernel(int* sc, int cap, const int* __restrict__ gate) {
+  if (threadIdx.x != 0 || (gate && *gate == ROUTE_PARK)) return;
+  const int af = sc[SC_ACTIVE], as = sc[SC_ACTIVE + 1];
+  const double idf = double(sc[SC_IDLE]) / (af > 0 ? af : 1), ids = double(sc[SC_IDLE + 1]) / (as > 0 ? as : 1);
+  const double tot = idf + ids;
+  int shift = tot > 0 ? int((idf - ids) / tot * double(cap / 16)) : 0;  // > 0: fast idled more
+  int nf = af - shift;
+  const int lo = cap / 8;
+  nf = nf < lo ? lo : (nf > cap - lo ? cap - lo : nf);
+  sc[SC_ACTIVE] = nf;
+  sc[SC_ACTIVE + 1] = cap - nf;
+}
+
 // Between relief_multi_kernel launches: deal the envs over its workgroups so
 // that each gets a mix of expensive and cheap ones.  An env's cost in the
 // last launch (shader cycles of its steps) predicts the next one well (its
@@ -1299,6 +1546,13 @@ struct bb_handle {
   int multi_adapt = 1;          // bb_step_multi on relief banks: queue or parked launches per launch (BB_MULTI_ADAPT=0:
                                 // always the queue; off when BB_ROUTE or BB_MULTI_QUEUE fixes the form)
   int balance = 1;              // relief_multi_kernel: cost-balanced env placement (BB_BALANCE=0: in order)
+  int pair = 1;                 // relief banks: bb_step_multi's work queue is the relief pair (BB_RELIEF_PAIR=0:
+                                // relief_multi_kernel, the one-launch queue)
+  int pair_cap = 0;             // one-wave workgroups resident on the chip (4 per CU)
+  int pair_seg = 16;            // steps a team holds an env before requeueing it (BB_PAIR_SEG)
+  unsigned long long pair_budget = 0;  // wall-clock ticks a pair launch may wait for work (20 s)
+  int count_memset = 0;         // diagnostic (BB_COUNT_MEMSET=1): reset the hand-over count with
+                                // hipMemsetAsync instead of zero_count_kernel
   std::vector<uint8_t> relief;  // per terrain: max height > 0
   int n_relief = 0;
   int* tstream = nullptr;       // device copies of the terrain streams (bb_set_terrain_stream)
@@ -1353,7 +1607,10 @@ int launch_step(bb_handle* h, const float* a, float* o, float* r, uint8_t* dn, f
   if (route == 1) {
     // serial route: the fast kernel over every env, then the full kernel over
     // the envs it handed over (no prediction, no second stream)
-    hipLaunchKernelGGL(zero_count_kernel, dim3(1), dim3(64), 0, s, cnt + 2);
+    if (h->count_memset)
+      HIPCHK(hipMemsetAsync(cnt + 2, 0, sizeof(int), s));
+    else
+      hipLaunchKernelGGL(zero_count_kernel, dim3(1), dim3(64), 0, s, cnt + 2);
     const bool timed = h->tn < h->tcap;
     hipEvent_t* ev = timed ? &h->tev[6 * h->tn] : nullptr;
     if (timed) HIPCHK(hipEventRecord(ev[0], s));
@@ -1429,6 +1686,28 @@ int launch_rollout(bb_handle* h, const RolloutDev& ro, hipStream_t s) {
   return 0;
 }
 
+// the relief pair on relief banks (see relief_pair_kernel): routes, rings, the
+// two persistent launches on the caller's stream and the handle's side stream,
+// then the split adaptation.  gate: the adaptive route's flag (NULL: always run)
+template <typename T>
+int launch_pair(bb_handle* h, const float* a, int K, float* o, float* r, uint8_t* dn, float* t, float* p2, int ar,
+                hipStream_t s, const int* gate) {
+  const ModelT<T>& m = model_of<T>(h);
+  const size_t plb = multi_lds_bytes<T>(4);
+  hipLaunchKernelGGL(pair_init_kernel<T>, dim3((h->n + WAVE / 16 - 1) / (WAVE / 16)), dim3(WAVE), 0, s, m, h->d, gate);
+  hipLaunchKernelGGL(pair_rings_kernel, dim3(1), dim3(1024), 0, s, h->d, gate);
+  HIPCHK(hipEventRecord(h->fork, s));
+  HIPCHK(hipStreamWaitEvent(h->side, h->fork, 0));
+  hipLaunchKernelGGL((relief_pair_kernel<T, true>), dim3(h->pair_cap), dim3(WAVE), plb, h->side, m, h->cfg, h->d, a, K,
+                     o, r, dn, t, p2, ar, h->pair_seg, h->pair_budget, gate);
+  hipLaunchKernelGGL((relief_pair_kernel<T, false>), dim3(h->pair_cap), dim3(WAVE), plb, s, m, h->cfg, h->d, a, K, o,
+                     r, dn, t, p2, ar, h->pair_seg, h->pair_budget, gate);
+  HIPCHK(hipEventRecord(h->join, h->side));
+  HIPCHK(hipStreamWaitEvent(s, h->join, 0));
+  hipLaunchKernelGGL(pair_adapt_kernel, dim3(1), dim3(64), 0, s, h->d.slow_count, h->pair_cap, gate);
+  return 0;
+}
+
 template <typename T>
 int launch_multi(bb_handle* h, const float* a, int K, float* o, float* r, uint8_t* dn, float* t, float* p2, int ar,
                  hipStream_t s) {
@@ -1443,21 +1722,29 @@ int launch_multi(bb_handle* h, const float* a, int K, float* o, float* r, uint8_
     // relief banks, adaptive: the parked launches or the work queue, as the
     // device flag chose after the last launch (the others exit at once)
     const int* gate = h->d.slow_count + SC_ROUTE;
-    const Dev dq = balanced_dev(h, s);
     hipLaunchKernelGGL((multi_step_kernel<T, false>), dim3(blocks), dim3(WAVE), mlb, s, model_of<T>(h), h->cfg, h->d,
                        a, K, o, r, dn, t, p2, ar, h->team, epw, h->d.park, gate);
     hipLaunchKernelGGL((multi_step_kernel<T, true>), dim3(blocks), dim3(WAVE), mlb, s, model_of<T>(h), h->cfg, h->d,
                        a, K, o, r, dn, t, p2, ar, h->team, epw, h->d.park, gate);
-    hipLaunchKernelGGL((relief_multi_kernel<T, false>), dim3((h->n + QENV - 1) / QENV), dim3(64 * QW),
-                       relief_lds_bytes<T>(), s, model_of<T>(h), h->cfg, dq, a, K, o, r, dn, t, p2, ar, RolloutDev{},
-                       gate);
+    if (h->pair) {
+      if (launch_pair<T>(h, a, K, o, r, dn, t, p2, ar, s, gate)) return -1;
+    } else {
+      const Dev dq = balanced_dev(h, s);
+      hipLaunchKernelGGL((relief_multi_kernel<T, false>), dim3((h->n + QENV - 1) / QENV), dim3(64 * QW),
+                         relief_lds_bytes<T>(), s, model_of<T>(h), h->cfg, dq, a, K, o, r, dn, t, p2, ar,
+                         RolloutDev{}, gate);
+    }
     if (timed) HIPCHK(hipEventRecord(ev[1], s));
     hipLaunchKernelGGL(route_decide_kernel, dim3(1), dim3(64), 0, s, h->d.slow_count, 1);
-  } else if (route == 0 && h->team == 16 && h->multi_queue) {  // relief banks: the per-workgroup work queue
-    const Dev dq = balanced_dev(h, s);
-    hipLaunchKernelGGL((relief_multi_kernel<T, false>), dim3((h->n + QENV - 1) / QENV), dim3(64 * QW),
-                       relief_lds_bytes<T>(), s, model_of<T>(h), h->cfg, dq, a, K, o, r, dn, t, p2, ar, RolloutDev{},
-                       (const int*)nullptr);
+  } else if (route == 0 && h->team == 16 && h->multi_queue) {  // relief banks: the work queue
+    if (h->pair) {
+      if (launch_pair<T>(h, a, K, o, r, dn, t, p2, ar, s, (const int*)nullptr)) return -1;
+    } else {
+      const Dev dq = balanced_dev(h, s);
+      hipLaunchKernelGGL((relief_multi_kernel<T, false>), dim3((h->n + QENV - 1) / QENV), dim3(64 * QW),
+                         relief_lds_bytes<T>(), s, model_of<T>(h), h->cfg, dq, a, K, o, r, dn, t, p2, ar,
+                         RolloutDev{}, (const int*)nullptr);
+    }
     if (timed) HIPCHK(hipEventRecord(ev[1], s));
   } else if (h->multi_park) {  // the fast steps, then the parked envs' hand-overs and the rest of their steps
     hipLaunchKernelGGL((multi_step_kernel<T, false>), dim3(blocks), dim3(WAVE), mlb, s, model_of<T>(h), h->cfg, h->d,
@@ -1564,6 +1851,17 @@ int bb_create(int n_envs, int device, const bb_params* p, bb_handle** out) {
     if (mq) h->multi_queue = atoi(mq) != 0;
     const char* bl = getenv("BB_BALANCE");
     if (bl) h->balance = atoi(bl) != 0;
+    const char* cm = getenv("BB_COUNT_MEMSET");
+    if (cm) h->count_memset = atoi(cm) != 0;
+    const char* rp = getenv("BB_RELIEF_PAIR");
+    if (rp) h->pair = atoi(rp) != 0;
+    const char* ps = getenv("BB_PAIR_SEG");
+    if (ps && atoi(ps) > 0) h->pair_seg = atoi(ps);
+    h->pair_cap = prop.multiProcessorCount * 4;
+    int wrate = 0;  // kHz
+    if (hipDeviceGetAttribute(&wrate, hipDeviceAttributeWallClockRate, device) != hipSuccess || wrate <= 0)
+      wrate = 100000;
+    h->pair_budget = 20ull * 1000ull * (unsigned long long)wrate;
   }
   h->md = compile_model(sc);
   h->mf = cast_model<float>(h->md);
@@ -1608,6 +1906,11 @@ int bb_create(int n_envs, int device, const bb_params* p, bb_handle** out) {
   HIPCHK(hipMalloc((void**)&d.pred_mark, n));
   HIPCHK(hipMalloc(&d.body_spill, es * (MAXB - MAXB_LDS) * NBF * size_t(n)));
   HIPCHK(hipMalloc((void**)&d.perm, sizeof(int) * n));
+  HIPCHK(hipMalloc((void**)&d.ring, sizeof(int) * 2 * n));
+  {  // the relief pair's initial split of the resident workgroups: 5/8 fast, 3/8 full
+    int act[2] = {h->pair_cap * 5 / 8, h->pair_cap - h->pair_cap * 5 / 8};
+    HIPCHK(hipMemcpy(d.slow_count + SC_ACTIVE, act, sizeof act, hipMemcpyHostToDevice));
+  }
   HIPCHK(hipMalloc((void**)&d.cost, sizeof(unsigned long long) * n));
   HIPCHK(hipMemset(d.cost, 0, sizeof(unsigned long long) * n));
   HIPCHK(hipStreamCreateWithFlags(&h->side, hipStreamNonBlocking));
@@ -1652,6 +1955,12 @@ int bb_create(int n_envs, int device, const bb_params* p, bb_handle** out) {
                          h->fp64 ? (const void*)relief_multi_kernel<double, true>
                                  : (const void*)relief_multi_kernel<float, true>};
     for (const void* k : qk) HIPCHK(hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, qlb));
+    const int plb = (int)(h->fp64 ? multi_lds_bytes<double>(4) : multi_lds_bytes<float>(4));
+    const void* pk[2] = {h->fp64 ? (const void*)relief_pair_kernel<double, false>
+                                 : (const void*)relief_pair_kernel<float, false>,
+                         h->fp64 ? (const void*)relief_pair_kernel<double, true>
+                                 : (const void*)relief_pair_kernel<float, true>};
+    for (const void* k : pk) HIPCHK(hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, plb));
   }
   *out = h;
   int rc = bb_reset(h, nullptr, nullptr, nullptr);
@@ -1668,7 +1977,7 @@ int bb_destroy(bb_handle* h) {
   (void)hipFree(h->bank); (void)hipFree(h->size_z); (void)hipFree(h->offset); (void)hipFree(h->hmax); (void)hipFree(h->d.stats);
   (void)hipFree(h->d.slow_list); (void)hipFree(h->d.slow_count); (void)hipFree(h->d.park);
   (void)hipFree(h->d.fast_envs); (void)hipFree(h->d.pred_envs); (void)hipFree(h->d.pred_mark);
-  (void)hipFree(h->d.body_spill); (void)hipFree(h->d.perm); (void)hipFree(h->d.cost);
+  (void)hipFree(h->d.body_spill); (void)hipFree(h->d.perm); (void)hipFree(h->d.cost); (void)hipFree(h->d.ring);
   (void)hipFree(h->tstream); (void)hipFree(h->env_stream); (void)hipFree(h->rng); (void)hipFree(h->seed_slot);
   (void)hipFree(h->d.tseed);
   (void)hipStreamDestroy(h->side); (void)hipEventDestroy(h->fork); (void)hipEventDestroy(h->join);
@@ -2056,7 +2365,7 @@ int bb_get_stats(bb_handle* h, int64_t* out, int n) {
   unsigned long long s[8];
   HIPCHK(hipMemcpy(s, h->d.stats, sizeof s, hipMemcpyDeviceToHost));
   const int64_t v[BB_NSTATS] = {(int64_t)s[0], (int64_t)s[1], (int64_t)s[2], (int64_t)s[3], (int64_t)s[4],
-                                (int64_t)s[5], (int64_t)s[6]};
+                                (int64_t)s[5], (int64_t)s[6], (int64_t)s[7]};
   for (int i = 0; i < n; i++) out[i] = v[i];
   return 0;
 }

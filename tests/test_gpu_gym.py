@@ -167,3 +167,42 @@ def test_custom_reward_batched_and_per_env():
         assert torch.allclose(rb, r, rtol=0, atol=1e-8)
     for e in envs.values():
         e.close()
+
+
+# --- A12: DistanceReward through the env -----------------------------------------
+def test_distance_reward_raises_like_the_reference_and_fused_on_request():
+    """reward_compat="reference" (default): construction and reset work, the first
+    step raises the reference's ValueError (its obs dict lacks pos2d,
+    ballbot_env.py:929, rewards/distance.py:43-44) -- batched env and gym.make alike.
+    reward_compat="fused": the kernel's reward is the reference chain on the step's
+    pos2d: (-scale * |goal - pos2d|) * scale + action penalty (+ survival bonus)."""
+    from ballbot_gym.envs import BallbotVecEnv
+
+    cfg = {"type": "distance", "config": {"goal_position": [1.0, -2.0], "scale": 0.5}}
+    n = 128
+    env = BallbotVecEnv(n, device="cuda:0", reward_config=cfg)
+    env.reset()
+    with pytest.raises(ValueError, match="pos2d"):
+        env.step(torch.zeros(n, 3, device="cuda:0"))
+    with pytest.raises(ValueError, match="pos2d"):
+        env.step_multi(torch.zeros(2, n, 3, device="cuda:0"))
+    env.close()
+    single = _make(terrain_type="flat", reward_config=cfg, disable_cameras=True)
+    single.reset()
+    with pytest.raises(ValueError, match="pos2d"):
+        single.step(np.zeros(3, np.float32))
+    single.close()
+    env = BallbotVecEnv(n, device="cuda:0", reward_config=cfg, reward_compat="fused")
+    g = torch.Generator(device="cuda:0").manual_seed(3)
+    f32 = np.float32
+    for _ in range(30):
+        a = torch.rand(n, 3, generator=g, device="cuda:0") * 2 - 1
+        _, r, _, _, info = env.step(a)
+        p2 = info["pos2d"].cpu().numpy()
+        ah = a.cpu().numpy()
+        dist = np.sqrt(((np.array([1.0, -2.0], f32) - p2) ** 2).sum(1, dtype=f32), dtype=f32)
+        nrm = np.sqrt((ah * ah).sum(1, dtype=f32), dtype=f32)
+        exp = (-f32(0.5) * dist) * f32(0.5) + f32(-0.0001) * (nrm * nrm)
+        exp = np.where(info["failure"].cpu().numpy(), exp, exp + f32(0.02)).astype(f32)
+        np.testing.assert_allclose(r.cpu().numpy(), exp, rtol=0, atol=2e-7)
+    env.close()

@@ -45,6 +45,26 @@ def test_distance_and_custom_rewards():
     assert p.reward_kind == N.REWARD_NONE and host is plugin and plugin.weight == 2.0
 
 
+def test_distance_reward_compat_switch():
+    """The reference env never puts pos2d into the reward's state (ballbot_env.py:929
+    calls reward_obj(obs)), so DistanceReward raises ValueError at the first step
+    (rewards/distance.py:43-44): reward_compat="reference" (the default) keeps that;
+    "fused" computes it in the kernel from the step's pos2d."""
+    from ballbot_gym.envs.config import DISTANCE_REWARD_ERROR, params_from_configs, reward_error
+    from ballbot_gym.rewards.distance import DistanceReward
+
+    cfg = {"type": "distance", "config": {"goal_position": [1.0, -2.0], "scale": 3.0}}
+    _, plugin, _ = params_from_configs(cfg)
+    assert reward_error(plugin) == DISTANCE_REWARD_ERROR
+    assert reward_error(plugin, "fused") is None
+    with pytest.raises(ValueError, match="pos2d"):  # the reference plugin itself, on the reference's obs dict
+        DistanceReward([1.0, -2.0])({"vel": np.zeros(3, np.float32)})
+    _, d, _ = params_from_configs({"type": "directional", "config": {"target_direction": [0.0, 1.0]}})
+    assert reward_error(d) is None
+    with pytest.raises(ValueError, match="reward_compat"):
+        params_from_configs(cfg, reward_compat="maybe")
+
+
 def test_config_errors():
     from ballbot_gym.envs.config import params_from_configs
 

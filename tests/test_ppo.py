@@ -188,3 +188,38 @@ def test_encoder_roundtrip_and_frozen_extractor(tmp_path):
     open(path + ".json", "w").write(json.dumps(meta))
     with pytest.raises(ValueError, match="corrupted"):
         load_frozen_encoder(path)
+
+
+def test_eval_callback_sb3_timing_targets_and_npz(tmp_path):
+    """EvalCallback (callbacks.py:607-617 of the reference; SB3 semantics): an evaluation at
+    every eval_freq-th vec-env step with the rollout's parameters, before its update; env i
+    of the eval VecEnv counts (n_eval_episodes + i) // n_envs episodes, in finishing order;
+    evaluations.npz as SB3 writes it (allow_pickle=False loads it); a progress.csv row with
+    eval/* and time/total_timesteps."""
+    from fake_env import FakeEnv
+    from ballbot_rl.evaluation import evaluate_policy
+    from ballbot_rl.training.callbacks import EvalCallback
+    from ballbot_rl.training.logger import read_progress
+
+    # targets over 10 envs and 8 episodes: [0, 0, 1, ..., 1] (SB3 evaluate_policy)
+    ev = FakeEnv(10, seed=3, ep_len=4)
+    policy = _ppo(FakeEnv(10), n_steps=4, batch_size=8).policy
+    r = evaluate_policy(policy, ev, n_eval_episodes=8)
+    assert len(r["episode_rewards"]) == 8 and len(r["episode_lengths"]) == 8
+    assert all(l >= 1 for l in r["episode_lengths"])
+    # staggered episodes: env i (i >= 2) ends its first episode after 4 - i % 4 steps; finishing order
+    exp_len = sorted(((4 - i % 4) or 4, i) for i in range(2, 10))
+    assert r["episode_lengths"] == [l for l, _ in exp_len]
+    m = _ppo(FakeEnv(16, ep_len=5), n_steps=8, batch_size=32, log_dir=str(tmp_path))
+    cb = EvalCallback(FakeEnv(16, seed=9, ep_len=6), n_eval_episodes=8, eval_freq=12, n_total_envs=16,
+                      log_path=tmp_path / "results", best_model_save_path=tmp_path)
+    calls = []
+    m.learn(total_timesteps=16 * 8 * 5, rollout_callback=lambda mm, a, b: (calls.append((a, b)), cb(mm, a, b)))
+    assert calls == [(1, 8), (9, 16), (17, 24), (25, 32), (33, 40)]
+    d = np.load(tmp_path / "results" / "evaluations.npz", allow_pickle=False)
+    assert d["timesteps"].tolist() == [12 * 16, 24 * 16, 36 * 16]  # vec-steps 12, 24, 36 x 16 envs
+    assert d["results"].shape == (3, 8) and d["ep_lengths"].shape == (3, 8)
+    cols = read_progress(str(tmp_path / "progress.csv"))
+    evals = [v for v in cols["eval/mean_reward"] if v is not None]
+    np.testing.assert_allclose(evals, d["results"].mean(1), rtol=1e-9)
+    assert (tmp_path / "best_model.safetensors").exists()

@@ -38,6 +38,10 @@ def main():
     ap.add_argument("--conv-benchmark", action="store_true", help="MIOpen kernel search for the CNN")
     ap.add_argument("--frozen-encoder", action="store_true",
                     help="with --cameras: pretrain a TinyAutoencoder on GPU frames first and freeze it (reference setup)")
+    ap.add_argument("--eval-freq", type=int, default=0,
+                    help="EvalCallback every N vec-env steps (the reference: 5000) on an eval VecEnv of --envs envs, "
+                         "env i on np_random(seed + envs + i); writes <out>/results/evaluations.npz")
+    ap.add_argument("--eval-episodes", type=int, default=8)
     a = ap.parse_args()
 
     import torch
@@ -95,13 +99,29 @@ def main():
             print(f"iter {iters[0]} t={_m.num_timesteps} ep_rew={_eprew(_m):.3f}", file=sys.stderr, flush=True)
         return True
 
+    ecb, t_eval = None, [0.0]
+    if a.eval_freq:
+        from ballbot_gym.distributed import shard_stream_seeds
+        from ballbot_rl.training.callbacks import EvalCallback
+
+        eenv = BallbotVecEnv(a.envs, device="cuda:0", precision=a.precision, seed=a.seed + a.envs,
+                             stream_seeds=shard_stream_seeds(a.seed + a.envs, 0, a.envs),
+                             terrain_config={"type": a.terrain, "config": {}}, disable_cameras=not a.cameras)
+        inner = EvalCallback(eenv, n_eval_episodes=a.eval_episodes, eval_freq=a.eval_freq, n_total_envs=a.envs,
+                             log_path=Path(a.out) / "results" if a.out else None)
+
+        def ecb(_m, first, last):
+            torch.cuda.synchronize(); t = time.perf_counter()
+            inner(_m, first, last); torch.cuda.synchronize(); t_eval[0] += time.perf_counter() - t
+
     t0 = time.perf_counter()
-    m.learn(total_timesteps=int(a.timesteps), callback=cb)
+    m.learn(total_timesteps=int(a.timesteps), callback=cb, rollout_callback=ecb)
     torch.cuda.synchronize()
     el = time.perf_counter() - t0
     out = {"metric": "PPO env-steps/sec (rollout + GAE + update)", "value": m.num_timesteps / el,
            "unit": "env-steps/s", "timesteps": m.num_timesteps, "iterations": iters[0], "wall_s": el,
-           "rollout_s": t_roll, "update_s": t_upd, "rollout_env_steps_per_s": m.num_timesteps / max(t_roll, 1e-9),
+           "rollout_s": t_roll, "update_s": t_upd, "eval_s": t_eval[0],
+           "rollout_env_steps_per_s": m.num_timesteps / max(t_roll, 1e-9),
            "config": {"envs": a.envs, "n_steps": a.n_steps, "batch_size": a.batch, "n_epochs": a.epochs,
                       "terrain": a.terrain, "precision": a.precision, "cameras": a.cameras,
                       "frozen_encoder": frozen is not None, "encoder_pretrain_s": pre_s},
