@@ -284,6 +284,7 @@ def main() -> None:
 
     run(args.burn_in + args.warmup, M)
     elapsed, step_ms, ktimes, kern_n, st0, st1 = timed(M)
+    pair = env.pair_counters() if (M and env.relief) else None  # the last timed launch (relief pair)
     per_step = None
     if M:  # the same steps with one bb_step launch per step (what a closed-loop rollout uses)
         run(args.warmup, 0)
@@ -371,6 +372,8 @@ def main() -> None:
                          "issue_frac": issue_frac},
             "stats": stats,
         }
+        if pair is not None and pair["claims_fast"] + pair["claims_full"] > 0:
+            line["pair"] = pair
         if per_step is not None:
             pe, pms, pk, pn, _, _ = per_step
             line["per_step"] = {

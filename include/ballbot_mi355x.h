@@ -56,7 +56,7 @@
 extern "C" {
 #endif
 
-#define BB_ABI_VERSION 15
+#define BB_ABI_VERSION 16
 #define BB_NQ 17
 #define BB_NV 15
 #define BB_OBS 15
@@ -68,6 +68,7 @@ extern "C" {
 #define BB_DONE_DIVERGED 4 /* MuJoCo's divergence reset ran inside this step (informational) */
 #define BB_DONE_OVERFLOW 8
 #define BB_NSTATS 8
+#define BB_NPAIR 11
 
 /* reward kinds (built-in reward plugins, ballbot_gym/rewards) */
 #define BB_REWARD_DIRECTIONAL 0 /* rewards/directional.py:33-54 */
@@ -383,6 +384,11 @@ int bb_forward(bb_handle* h, const double* ctrl, double* qacc, int32_t* ncontact
  * terrain stream table or onto a drawn seed not resident in the bank, env-steps whose last RK stage stored base-tree contacts past the 32 LDS slots
  * (the per-env HBM spill block)] */
 int bb_get_stats(bb_handle* h, int64_t* out, int n);
+/* diagnostics of the last relief-pair launch of bb_step_multi (waits for the device): the first
+ * n (<= BB_NPAIR) of [team-cycles stepping (fast, full), idle loop passes (fast, full), working
+ * workgroups of the next launch (fast, full), env claims (fast, full), completed env-steps (fast,
+ * full), fast-path hand-overs to the full launch].  No reference counterpart (tools/). */
+int bb_pair_counters(bb_handle* h, int64_t* out, int n);
 /* launch configuration: [n_envs, envs_per_wave, fp64, lds_bytes_per_workgroup,
  * lanes_per_env] */
 int bb_get_config(bb_handle* h, int32_t* out5);

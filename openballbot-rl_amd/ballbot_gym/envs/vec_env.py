@@ -516,6 +516,14 @@ class BallbotVecEnv:
         return {"resets": out[0], "diverged": out[1], "overflow": out[2], "slow_path": out[3],
                 "solver_iters": out[4], "stream_wraps": out[5], "spill": out[6], "pair_budget": out[7]}
 
+    def pair_counters(self) -> Dict[str, int]:
+        """Diagnostics of the last relief-pair launch of step_multi (bb_pair_counters; waits for the device)."""
+        keys = ("busy_fast", "busy_full", "idle_fast", "idle_full", "active_fast", "active_full", "claims_fast",
+                "claims_full", "steps_fast", "steps_full", "handovers")
+        out = (C.c_int64 * len(keys))()
+        N.check(N.lib().bb_pair_counters(self._h, out, len(keys)), "bb_pair_counters")
+        return dict(zip(keys, out))
+
     def env_terrain(self):
         """(bank slot of every env's current terrain, stream draws each env made) as int32[N] arrays."""
         t = np.zeros(self.num_envs, np.int32)

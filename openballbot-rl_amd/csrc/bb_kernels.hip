@@ -93,6 +93,7 @@ struct Dev {
   void* body_spill;           // T[n][MAXB - MAXB_LDS][NBF]: base-tree contacts past the LDS slots
   int* perm;                  // relief_multi_kernel: env of each workgroup slot (balance_kernel), NULL: identity
   int* ring;                  // relief_pair_kernel: [2][n] FIFO rings of env ids ready for a fast / full step (-1: empty)
+  unsigned long long* pair_busy;  // relief_pair_kernel: [2] team-cycles spent stepping (fast, full) in the last launch
   unsigned long long* cost;   // relief_multi_kernel: shader cycles each env's steps took in the last launch
 };
 
@@ -102,18 +103,46 @@ __device__ __forceinline__ T* body_spill_of(const Dev& d, int e) {
   return reinterpret_cast<T*>(d.body_spill) + size_t(e) * ((MAXB - MAXB_LDS) * NBF);
 }
 
-template <typename T>
+// Device-coherent (agent-scope) loads and stores: `sc1` accesses, which the
+// per-XCD L2s do not serve stale nor hold dirty.  Data that moves between
+// workgroups on different XCDs inside one launch (the relief pair's env
+// hand-over) goes through these instead of __threadfence(), which on gfx950 is
+// buffer_wbl2 + buffer_inv of the WHOLE L2 of the XCD: every hand-over then
+// cost every wave on that XCD its cached lines (kernel code included).
+template <typename V>
+__device__ __forceinline__ V ld_coh(const V* p) {
+  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+template <typename V>
+__device__ __forceinline__ void st_coh(V* p, V v) {
+  __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+// the wave's earlier stores complete (device-coherent ones are then visible to
+// every XCD) before its later memory operations: the release of a hand-over
+// whose data went through st_coh
+__device__ __forceinline__ void stores_done() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
+
+// COH: through ld_coh / st_coh (the relief pair's hand-over)
+template <typename T, bool COH = false>
 __device__ __forceinline__ void load_state(const Dev& d, int e, T* q, T* v, T* w, int& step) {
   const T* Q = (const T*)d.qpos;
   const T* V = (const T*)d.qvel;
   const T* W = (const T*)d.warm;
+  if constexpr (COH) {
 #pragma unroll
-  for (int i = 0; i < NQ; i++) q[i] = Q[i * d.n + e];
+    for (int i = 0; i < NQ; i++) q[i] = ld_coh(Q + i * d.n + e);
 #pragma unroll
-  for (int i = 0; i < NV; i++) { v[i] = V[i * d.n + e]; w[i] = W[i * d.n + e]; }
-  step = d.steps[e];
+    for (int i = 0; i < NV; i++) { v[i] = ld_coh(V + i * d.n + e); w[i] = ld_coh(W + i * d.n + e); }
+    step = ld_coh(d.steps + e);
+  } else {
+#pragma unroll
+    for (int i = 0; i < NQ; i++) q[i] = Q[i * d.n + e];
+#pragma unroll
+    for (int i = 0; i < NV; i++) { v[i] = V[i * d.n + e]; w[i] = W[i * d.n + e]; }
+    step = d.steps[e];
+  }
 }
-template <typename T>
+template <typename T, bool COH = false>
 __device__ __forceinline__ void store_state(const Dev& d, int e, const T* q, const T* v, const T* w, int step) {
   // e opaque here: otherwise the 47 per-element addresses of load_state are
   // kept live (94 VGPRs) across the whole step and spill to scratch
@@ -121,11 +150,19 @@ __device__ __forceinline__ void store_state(const Dev& d, int e, const T* q, con
   T* Q = (T*)d.qpos;
   T* V = (T*)d.qvel;
   T* W = (T*)d.warm;
+  if constexpr (COH) {
 #pragma unroll
-  for (int i = 0; i < NQ; i++) Q[i * d.n + e] = q[i];
+    for (int i = 0; i < NQ; i++) st_coh(Q + i * d.n + e, q[i]);
 #pragma unroll
-  for (int i = 0; i < NV; i++) { V[i * d.n + e] = v[i]; W[i * d.n + e] = w[i]; }
-  d.steps[e] = step;
+    for (int i = 0; i < NV; i++) { st_coh(V + i * d.n + e, v[i]); st_coh(W + i * d.n + e, w[i]); }
+    st_coh(d.steps + e, step);
+  } else {
+#pragma unroll
+    for (int i = 0; i < NQ; i++) Q[i * d.n + e] = q[i];
+#pragma unroll
+    for (int i = 0; i < NV; i++) { V[i * d.n + e] = v[i]; W[i * d.n + e] = w[i]; }
+    d.steps[e] = step;
+  }
 }
 
 // numpy's PCG64 (the bit generator of gymnasium's np_random, Generator(PCG64(
@@ -187,17 +224,20 @@ __device__ __forceinline__ int pcg64_terrain_seed(Pcg64& g) {
 // seed_slot (a draw whose seed is not resident is counted in stats[5] and takes
 // slot seed % n_terrains).  Otherwise the host's precomputed draws per stream
 // (bb_set_terrain_stream): draw episodes[e] of the table.  A pinned terrain
-// (bb_assign_terrain) takes no draw.  Called by one lane per env.
+// (bb_assign_terrain) takes no draw.  Called by one lane per env.  The env's
+// generator and counters go through ld_coh / st_coh: in the relief pair the
+// env's next reset may run on another XCD within the same launch.
 __device__ __forceinline__ int next_terrain(const Dev& d, int e) {
   const int pin = d.pending_terrain[e];
   if (pin >= 0) return pin;
   if (d.rng) {
     const size_t n = size_t(d.n);
-    Pcg64 g{d.rng[e], d.rng[n + e], d.rng[2 * n + e], d.rng[3 * n + e], d.rng[4 * n + e]};
+    Pcg64 g{ld_coh(d.rng + e), ld_coh(d.rng + n + e), ld_coh(d.rng + 2 * n + e), ld_coh(d.rng + 3 * n + e),
+            ld_coh(d.rng + 4 * n + e)};
     const int s = pcg64_terrain_seed(g);
-    d.rng[e] = g.sh; d.rng[n + e] = g.sl; d.rng[4 * n + e] = g.buf;
-    d.episodes[e] += 1;
-    d.tseed[e] = s;
+    st_coh(d.rng + e, g.sh); st_coh(d.rng + n + e, g.sl); st_coh(d.rng + 4 * n + e, g.buf);
+    st_coh(d.episodes + e, ld_coh(d.episodes + e) + 1);
+    st_coh(d.tseed + e, s);
     int slot = d.seed_slot ? d.seed_slot[s] : s;
     if (unsigned(slot) >= unsigned(d.n_terrains)) {
       atomicAdd(&d.stats[5], 1ull);
@@ -206,8 +246,8 @@ __device__ __forceinline__ int next_terrain(const Dev& d, int e) {
     return slot;
   }
   if (!d.tstream) return 0;
-  int k = d.episodes[e];
-  d.episodes[e] = k + 1;
+  int k = ld_coh(d.episodes + e);
+  st_coh(d.episodes + e, k + 1);
   if (k >= d.tlen) {  // past the resident draws: reuse them (counted)
     atomicAdd(&d.stats[5], 1ull);
     k %= d.tlen;
@@ -444,7 +484,7 @@ __device__ __forceinline__ int team_step(const ModelT<T>& m, const EnvCfg& cfg, 
     if (p2_row) { p2_row[0] = p2[0]; p2_row[1] = p2[1]; }
     if (reset) {
       tid = next_terrain(d, e);
-      d.terrain[e] = tid;
+      st_coh(d.terrain + e, tid);
     }
   }
   if (reset) {
@@ -1210,6 +1250,8 @@ __global__ __launch_bounds__(64 * QW) void relief_multi_kernel(ModelT<T> mg, Env
 // ends both launches with an error flag (stats[7]) should a launch ever wait
 // for work that cannot come -- no hang.
 constexpr int SC_RHEAD = 16, SC_RTAIL = 18, SC_DONE = 20, SC_ERR = 21, SC_ACTIVE = 22, SC_IDLE = 24;
+// diagnostics of the last launch (bb_pair_counters): claims [2], completed steps [2], fast-path hand-overs
+constexpr int SC_CLAIMS = 32, SC_STEPS = 34, SC_PARKED = 36;
 
 __device__ __forceinline__ int ld_agent(const int* p) {
   return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -1266,10 +1308,13 @@ __global__ __launch_bounds__(64) void relief_pair_kernel(ModelT<T> mg, EnvCfg cf
   EnvWork<T>& W = team_work<T>(smem, team);
   T* bk = reinterpret_cast<T*>(smem + size_t(WAVE / TEAM) * work_stride<T>()) + team * (NQ + 2 * NV);
   unsigned* cnt = s_cnt[team];
+  __shared__ int s_diag[WAVE / TEAM][3];  // claims, completed steps, fast-path hand-overs
+  if (lead) { s_diag[team][0] = 0; s_diag[team][1] = 0; s_diag[team][2] = 0; }
   const int kind = FULL ? 1 : 0;
   const unsigned long long t0 = wall_clock64();
   int e = -1, k = 0, tid = 0, step = 0, held = 0;
   unsigned idle = 0;
+  unsigned long long busy = 0;  // this team's cycles stepping envs (the split of the next launch)
   for (;;) {
     // a team without an env takes the next one of its kind (the rest of the wave
     // skips this block); stop when every env has done its K steps
@@ -1291,18 +1336,20 @@ __global__ __launch_bounds__(64) void relief_pair_kernel(ModelT<T> mg, EnvCfg cf
       if (got == -2) {
         stop = 1;
       } else if (got >= 0) {
+        // acquire: the releasing team's device-coherent stores, read device-coherently
+        // (their addresses depend on the popped id, so they issue after it)
         e = got;
-        __threadfence();  // acquire: the state the releasing team stored
-        load_state(d, e, W.qn, W.vn, W.wn, step);
-        k = d.park[e];
-        tid = d.terrain[e];
+        load_state<T, true>(d, e, W.qn, W.vn, W.wn, step);
+        k = ld_coh(d.park + e);
+        tid = ld_coh(d.terrain + e);
         held = 0;
-        if (lead) W.bspill = body_spill_of<T>(d, e);
+        if (lead) { W.bspill = body_spill_of<T>(d, e); s_diag[team][0]++; }
         team_sync();
       }
     }
     if (stop) break;
     if (e >= 0) {
+      const unsigned long long c0 = clock64();
       const size_t row = size_t(k) * n + e;
       const float* ak = act + 3 * row;
       const float a[3] = {ak[0], ak[1], ak[2]};
@@ -1313,8 +1360,10 @@ __global__ __launch_bounds__(64) void relief_pair_kernel(ModelT<T> mg, EnvCfg cf
       int next = kind;
       if (!FULL && (fl & F_PARKED)) {  // the fast path handed the step over: the full launch redoes it
         next = 1;
+        if (lead) s_diag[team][2]++;
       } else {
         if (lead) {
+          s_diag[team][1]++;
 #pragma unroll
           for (int i = 0; i < 15; i++) obs[15 * row + i] = o[i];
           rew[row] = r;
@@ -1324,12 +1373,13 @@ __global__ __launch_bounds__(64) void relief_pair_kernel(ModelT<T> mg, EnvCfg cf
         held++;
         if (k < K) next = predict_env<T>(m, d, tid, W.qn, W.vn, tm.tl, team_shift_of(TEAM)) ? 1 : 0;
       }
+      busy += clock64() - c0;
       if (k >= K || next != kind || held >= seg) {  // release the env (team-uniform)
         team_sync();
         if (lead) {
-          store_state(d, e, W.qn, W.vn, W.wn, step);
-          d.park[e] = k;
-          __threadfence();  // release: the state before the ring entry
+          store_state<T, true>(d, e, W.qn, W.vn, W.wn, step);
+          st_coh(d.park + e, k);
+          stores_done();  // release: the state (and a reset's draw) before the ring entry
           if (k >= K) atomicAdd(sc + SC_DONE, 1);
           else ring_push(d, next, e);
           if (FULL && gate) atomicAdd(sc + SC_TOUCHED, 1);  // adaptive route: an env took full steps
@@ -1346,6 +1396,10 @@ __global__ __launch_bounds__(64) void relief_pair_kernel(ModelT<T> mg, EnvCfg cf
   if (lead) {
     counts_flush(d, cnt);
     if (idle) atomicAdd(sc + SC_IDLE + kind, int(idle > 1000000u ? 1000000u : idle));
+    if (busy) atomicAdd(d.pair_busy + kind, busy);
+    atomicAdd(sc + SC_CLAIMS + kind, s_diag[team][0]);
+    atomicAdd(sc + SC_STEPS + kind, s_diag[team][1]);
+    if (!FULL) atomicAdd(sc + SC_PARKED, s_diag[team][2]);
   }
 }
 
@@ -1406,23 +1460,25 @@ __global__ __launch_bounds__(1024) void pair_rings_kernel(Dev d, const int* __re
     sc[SC_RTAIL] = NF; sc[SC_RTAIL + 1] = NS;
     sc[SC_DONE] = 0; sc[SC_ERR] = 0;
     sc[SC_IDLE] = 0; sc[SC_IDLE + 1] = 0;
+    sc[SC_CLAIMS] = 0; sc[SC_CLAIMS + 1] = 0; sc[SC_STEPS] = 0; sc[SC_STEPS + 1] = 0; sc[SC_PARKED] = 0;
+    d.pair_busy[0] = 0; d.pair_busy[1] = 0;
   }
 }
 
-// after the pair: move workgroups towards the kind that idled less (per active
-// workgroup), in steps of at most cap / 16, keeping cap / 8 for each kind.  The
+// after the pair: the next launch splits the resident workgroups in proportion
+// to the team-cycles each kind spent stepping in this one (the work of the two
+// kinds, whatever this launch's split was), keeping cap / 8 for each.  The
 // counts only place work: every env's results are the same whatever they are.
-__global__ void pair_adapt_kernel(int* sc, int cap, const int* __restrict__ gate) {
+__global__ void pair_adapt_kernel(Dev d, int cap, const int* __restrict__ gate) {
   if (threadIdx.x != 0 || (gate && *gate == ROUTE_PARK)) return;
-  const int af = sc[SC_ACTIVE], as = sc[SC_ACTIVE + 1];
-  const double idf = double(sc[SC_IDLE]) / (af > 0 ? af : 1), ids = double(sc[SC_IDLE + 1]) / (as > 0 ? as : 1);
-  const double tot = idf + ids;
-  int shift = tot > 0 ? int((idf - ids) / tot * double(cap / 16)) : 0;  // > 0: fast idled more
-  int nf = af - shift;
+  int* sc = d.slow_count;
+  const double bf = double(d.pair_busy[0]), bs = double(d.pair_busy[1]);
+  if (bf + bs <= 0) return;
+  int ns = int(double(cap) * bs / (bf + bs) + 0.5);
   const int lo = cap / 8;
-  nf = nf < lo ? lo : (nf > cap - lo ? cap - lo : nf);
-  sc[SC_ACTIVE] = nf;
-  sc[SC_ACTIVE + 1] = cap - nf;
+  ns = ns < lo ? lo : (ns > cap - lo ? cap - lo : ns);
+  sc[SC_ACTIVE] = cap - ns;
+  sc[SC_ACTIVE + 1] = ns;
 }
 
 // Between relief_multi_kernel launches: deal the envs over its workgroups so
@@ -1550,6 +1606,7 @@ struct bb_handle {
                                 // relief_multi_kernel, the one-launch queue)
   int pair_cap = 0;             // one-wave workgroups resident on the chip (4 per CU)
   int pair_seg = 16;            // steps a team holds an env before requeueing it (BB_PAIR_SEG)
+  int pair_adapt = 1;           // split the workgroups by the last launch's work (BB_PAIR_ADAPT=0: keep the first split)
   unsigned long long pair_budget = 0;  // wall-clock ticks a pair launch may wait for work (20 s)
   int count_memset = 0;         // diagnostic (BB_COUNT_MEMSET=1): reset the hand-over count with
                                 // hipMemsetAsync instead of zero_count_kernel
@@ -1704,7 +1761,7 @@ int launch_pair(bb_handle* h, const float* a, int K, float* o, float* r, uint8_t
                      r, dn, t, p2, ar, h->pair_seg, h->pair_budget, gate);
   HIPCHK(hipEventRecord(h->join, h->side));
   HIPCHK(hipStreamWaitEvent(s, h->join, 0));
-  hipLaunchKernelGGL(pair_adapt_kernel, dim3(1), dim3(64), 0, s, h->d.slow_count, h->pair_cap, gate);
+  if (h->pair_adapt) hipLaunchKernelGGL(pair_adapt_kernel, dim3(1), dim3(64), 0, s, h->d, h->pair_cap, gate);
   return 0;
 }
 
@@ -1857,6 +1914,8 @@ int bb_create(int n_envs, int device, const bb_params* p, bb_handle** out) {
     if (rp) h->pair = atoi(rp) != 0;
     const char* ps = getenv("BB_PAIR_SEG");
     if (ps && atoi(ps) > 0) h->pair_seg = atoi(ps);
+    const char* pa = getenv("BB_PAIR_ADAPT");
+    if (pa) h->pair_adapt = atoi(pa) != 0;
     h->pair_cap = prop.multiProcessorCount * 4;
     int wrate = 0;  // kHz
     if (hipDeviceGetAttribute(&wrate, hipDeviceAttributeWallClockRate, device) != hipSuccess || wrate <= 0)
@@ -1907,8 +1966,13 @@ int bb_create(int n_envs, int device, const bb_params* p, bb_handle** out) {
   HIPCHK(hipMalloc(&d.body_spill, es * (MAXB - MAXB_LDS) * NBF * size_t(n)));
   HIPCHK(hipMalloc((void**)&d.perm, sizeof(int) * n));
   HIPCHK(hipMalloc((void**)&d.ring, sizeof(int) * 2 * n));
-  {  // the relief pair's initial split of the resident workgroups: 5/8 fast, 3/8 full
-    int act[2] = {h->pair_cap * 5 / 8, h->pair_cap - h->pair_cap * 5 / 8};
+  HIPCHK(hipMalloc((void**)&d.pair_busy, sizeof(unsigned long long) * 2));
+  {  // the relief pair's first split of the resident workgroups (BB_PAIR_FULL: percent full; default half)
+    const char* pf = getenv("BB_PAIR_FULL");
+    int pct = pf ? atoi(pf) : 50;
+    pct = pct < 13 ? 13 : (pct > 87 ? 87 : pct);
+    const int ns = h->pair_cap * pct / 100;
+    int act[2] = {h->pair_cap - ns, ns};
     HIPCHK(hipMemcpy(d.slow_count + SC_ACTIVE, act, sizeof act, hipMemcpyHostToDevice));
   }
   HIPCHK(hipMalloc((void**)&d.cost, sizeof(unsigned long long) * n));
@@ -1978,6 +2042,7 @@ int bb_destroy(bb_handle* h) {
   (void)hipFree(h->d.slow_list); (void)hipFree(h->d.slow_count); (void)hipFree(h->d.park);
   (void)hipFree(h->d.fast_envs); (void)hipFree(h->d.pred_envs); (void)hipFree(h->d.pred_mark);
   (void)hipFree(h->d.body_spill); (void)hipFree(h->d.perm); (void)hipFree(h->d.cost); (void)hipFree(h->d.ring);
+  (void)hipFree(h->d.pair_busy);
   (void)hipFree(h->tstream); (void)hipFree(h->env_stream); (void)hipFree(h->rng); (void)hipFree(h->seed_slot);
   (void)hipFree(h->d.tseed);
   (void)hipStreamDestroy(h->side); (void)hipEventDestroy(h->fork); (void)hipEventDestroy(h->join);
@@ -2366,6 +2431,22 @@ int bb_get_stats(bb_handle* h, int64_t* out, int n) {
   HIPCHK(hipMemcpy(s, h->d.stats, sizeof s, hipMemcpyDeviceToHost));
   const int64_t v[BB_NSTATS] = {(int64_t)s[0], (int64_t)s[1], (int64_t)s[2], (int64_t)s[3], (int64_t)s[4],
                                 (int64_t)s[5], (int64_t)s[6], (int64_t)s[7]};
+  for (int i = 0; i < n; i++) out[i] = v[i];
+  return 0;
+}
+
+int bb_pair_counters(bb_handle* h, int64_t* out, int n) {
+  if (!h || !out) return fail("bb_pair_counters: NULL argument");
+  if (n < 0 || n > BB_NPAIR) return fail("bb_pair_counters: n must be in [0, %d] (got %d)", BB_NPAIR, n);
+  HIPCHK(hipSetDevice(h->device));
+  HIPCHK(hipDeviceSynchronize());
+  int sc[64];
+  unsigned long long busy[2];
+  HIPCHK(hipMemcpy(sc, h->d.slow_count, sizeof sc, hipMemcpyDeviceToHost));
+  HIPCHK(hipMemcpy(busy, h->d.pair_busy, sizeof busy, hipMemcpyDeviceToHost));
+  const int64_t v[BB_NPAIR] = {(int64_t)busy[0], (int64_t)busy[1], sc[SC_IDLE], sc[SC_IDLE + 1], sc[SC_ACTIVE],
+                               sc[SC_ACTIVE + 1], sc[SC_CLAIMS], sc[SC_CLAIMS + 1], sc[SC_STEPS], sc[SC_STEPS + 1],
+                               sc[SC_PARKED]};
   for (int i = 0; i < n; i++) out[i] = v[i];
   return 0;
 }
