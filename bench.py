@@ -285,6 +285,18 @@ def main() -> None:
     run(args.burn_in + args.warmup, M)
     elapsed, step_ms, ktimes, kern_n, st0, st1 = timed(M)
     pair = env.pair_counters() if (M and env.relief) else None  # the last timed launch (relief pair)
+    if pair is not None and pair["claims_fast"] + pair["claims_full"] > 0:
+        import numpy as np
+
+        cyc, fin = env.pair_env_times()  # per env: cycles stepped, wall tick (100 MHz) of its last step
+        c = cyc.astype(np.float64) / 1e6
+        f = (fin.astype(np.float64) - float(fin.max())) / 1e5
+        pair["env_mcycles"] = {q: float(np.percentile(c, p)) for q, p in (("p0", 0), ("p50", 50), ("p90", 90),
+                                                                          ("p99", 99), ("p100", 100))}
+        pair["env_mcycles"]["mean"] = float(c.mean())
+        pair["env_finish_ms_before_last"] = {q: float(np.percentile(f, p)) for q, p in (("p0", 0), ("p10", 10),
+                                                                                       ("p50", 50), ("p90", 90))}
+        pair["corr_cycles_finish"] = float(np.corrcoef(c, f)[0, 1])
     per_step = None
     if M:  # the same steps with one bb_step launch per step (what a closed-loop rollout uses)
         run(args.warmup, 0)

@@ -104,7 +104,7 @@ EXPORTS = [
     "bb_gae", "bb_render_depth", "bb_ppo_loss", "bb_adamw_clip", "bb_ppo_mlp_workspace_bytes", "bb_ppo_mlp_step",
     "bb_ppo_mlp_act", "bb_rollout_track", "bb_depth_encoder_workspace_bytes", "bb_depth_encoder",
     "bb_set_terrain_stream", "bb_get_env_terrain", "bb_kernel_times", "bb_step_multi", "bb_rollout",
-    "bb_set_terrain_rng", "bb_get_terrain_rng", "bb_pair_counters",
+    "bb_set_terrain_rng", "bb_get_terrain_rng", "bb_pair_counters", "bb_pair_env_times",
 ]
 
 ABI_VERSION = 16  # include/ballbot_mi355x.h BB_ABI_VERSION
@@ -194,6 +194,7 @@ def _load(path: Path):
     L.bb_forward.argtypes = [vp, dp, dp, C.POINTER(C.c_int32)]
     L.bb_get_stats.argtypes = [vp, C.POINTER(C.c_int64), C.c_int]
     L.bb_pair_counters.argtypes = [vp, C.POINTER(C.c_int64), C.c_int]
+    L.bb_pair_env_times.argtypes = [vp, C.POINTER(C.c_uint64)]
     L.bb_set_terrain_stream.argtypes = [vp, C.POINTER(C.c_int32), C.c_int, C.c_int, C.POINTER(C.c_int32)]
     L.bb_set_terrain_rng.argtypes = [vp, C.POINTER(C.c_uint64), C.POINTER(C.c_int32)]
     L.bb_get_terrain_rng.argtypes = [vp, C.POINTER(C.c_uint64), C.POINTER(C.c_int32)]

@@ -519,10 +519,17 @@ class BallbotVecEnv:
     def pair_counters(self) -> Dict[str, int]:
         """Diagnostics of the last relief-pair launch of step_multi (bb_pair_counters; waits for the device)."""
         keys = ("busy_fast", "busy_full", "idle_fast", "idle_full", "active_fast", "active_full", "claims_fast",
-                "claims_full", "steps_fast", "steps_full", "handovers")
+                "claims_full", "steps_fast", "steps_full", "handovers", "life_cycles_fast", "life_cycles_full",
+                "life_wall_fast", "life_wall_full")
         out = (C.c_int64 * len(keys))()
         N.check(N.lib().bb_pair_counters(self._h, out, len(keys)), "bb_pair_counters")
         return dict(zip(keys, out))
+
+    def pair_env_times(self):
+        """Per env, the last relief-pair launch: (shader cycles its steps took, wall tick of its last step)."""
+        out = np.zeros((2, self.num_envs), np.uint64)
+        N.check(N.lib().bb_pair_env_times(self._h, out.ctypes.data_as(C.POINTER(C.c_uint64))), "bb_pair_env_times")
+        return out[0], out[1]
 
     def env_terrain(self):
         """(bank slot of every env's current terrain, stream draws each env made) as int32[N] arrays."""

@@ -92,8 +92,11 @@ struct Dev {
   uint8_t* pred_mark;
   void* body_spill;           // T[n][MAXB - MAXB_LDS][NBF]: base-tree contacts past the LDS slots
   int* perm;                  // relief_multi_kernel: env of each workgroup slot (balance_kernel), NULL: identity
-  int* ring;                  // relief_pair_kernel: [2][n] FIFO rings of env ids ready for a fast / full step (-1: empty)
-  unsigned long long* pair_busy;  // relief_pair_kernel: [2] team-cycles spent stepping (fast, full) in the last launch
+  unsigned long long* ring;   // relief_pair_kernel: [2][ring_len] ticket rings of envs ready for a fast / full step
+  int ring_len;               // n + the resident teams: an entry is never overwritten before it is taken
+  unsigned long long* pair_env;  // relief_pair_kernel, last launch, per env: [n] cycles stepped, [n] wall tick of its last step
+  unsigned long long* pair_busy;  // relief_pair_kernel, last launch: [2] team-cycles stepping, [2] team lifetimes
+                                  // in shader cycles, [2] in wall-clock ticks (fast, full)
   unsigned long long* cost;   // relief_multi_kernel: shader cycles each env's steps took in the last launch
 };
 
@@ -1257,31 +1260,28 @@ __device__ __forceinline__ int ld_agent(const int* p) {
   return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
-// take the next env from ring `kind` (lead lane): -1 when the ring is empty
-__device__ __forceinline__ int ring_pop(const Dev& d, int kind) {
-  int* sc = d.slow_count;
-  int* ring = d.ring + size_t(kind) * d.n;
-  for (int att = 0; att < 4; att++) {
-    const int h = ld_agent(sc + SC_RHEAD + kind), t = ld_agent(sc + SC_RTAIL + kind);
-    if (h >= t) return -1;
-    if (atomicCAS(sc + SC_RHEAD + kind, h, h + 1) == h) {
-      int* slot = ring + (unsigned(h) % unsigned(d.n));
-      int e;
-      // the pusher reserved the slot before filling it: wait for the fill (a few cycles)
-      for (int spin = 0; (e = ld_agent(slot)) < 0 && spin < (1 << 20); spin++) __builtin_amdgcn_s_sleep(1);
-      __hip_atomic_store(slot, -1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      return e;
-    }
-  }
-  return -1;
+// The rings are ticket queues.  A team without an env takes a ticket (one
+// atomicAdd on the ring's head: no compare-and-swap retries between the ~2000
+// teams of a kind) and, at each later pass of its wave's loop, looks whether
+// the entry of that ticket has arrived; a release appends its env with one
+// atomicAdd on the tail.  Entries carry their ticket (ticket << 32 | env), so a
+// slot needs no clearing and a look never takes an older lap's entry; the ring
+// is longer than the envs plus the resident teams, so an entry is never
+// overwritten before its ticket's holder took it.
+__device__ __forceinline__ unsigned long long ring_entry(int ticket, int e) {
+  return (static_cast<unsigned long long>(unsigned(ticket)) << 32) | unsigned(e);
 }
-
+__device__ __forceinline__ int ring_ticket(const Dev& d, int kind) { return atomicAdd(d.slow_count + SC_RHEAD + kind, 1); }
+// the env of `ticket` in ring `kind`, or -1 while it has not been appended
+__device__ __forceinline__ int ring_look(const Dev& d, int kind, int ticket) {
+  const unsigned long long v =
+      ld_coh(d.ring + size_t(kind) * d.ring_len + (unsigned(ticket) % unsigned(d.ring_len)));
+  return unsigned(v >> 32) == unsigned(ticket) ? int(unsigned(v)) : -1;
+}
 // append env e to ring `kind` (lead lane; the env's state is stored and released)
 __device__ __forceinline__ void ring_push(const Dev& d, int kind, int e) {
-  int* sc = d.slow_count;
-  const int t = atomicAdd(sc + SC_RTAIL + kind, 1);
-  __hip_atomic_store(d.ring + size_t(kind) * d.n + (unsigned(t) % unsigned(d.n)), e, __ATOMIC_RELAXED,
-                     __HIP_MEMORY_SCOPE_AGENT);
+  const int t = atomicAdd(d.slow_count + SC_RTAIL + kind, 1);
+  st_coh(d.ring + size_t(kind) * d.ring_len + (unsigned(t) % unsigned(d.ring_len)), ring_entry(t, e));
 }
 
 template <typename T, bool FULL>
@@ -1311,10 +1311,11 @@ __global__ __launch_bounds__(64) void relief_pair_kernel(ModelT<T> mg, EnvCfg cf
   __shared__ int s_diag[WAVE / TEAM][3];  // claims, completed steps, fast-path hand-overs
   if (lead) { s_diag[team][0] = 0; s_diag[team][1] = 0; s_diag[team][2] = 0; }
   const int kind = FULL ? 1 : 0;
-  const unsigned long long t0 = wall_clock64();
-  int e = -1, k = 0, tid = 0, step = 0, held = 0;
+  const unsigned long long t0 = wall_clock64(), c_start = clock64();
+  int e = -1, k = 0, tid = 0, step = 0, held = 0, ticket = -1;  // ticket: the lead's, -1 when none
   unsigned idle = 0;
   unsigned long long busy = 0;  // this team's cycles stepping envs (the split of the next launch)
+  unsigned long long held_busy = 0;  // ... the held env's, since the claim
   for (;;) {
     // a team without an env takes the next one of its kind (the rest of the wave
     // skips this block); stop when every env has done its K steps
@@ -1325,8 +1326,10 @@ __global__ __launch_bounds__(64) void relief_pair_kernel(ModelT<T> mg, EnvCfg cf
         if (ld_agent(sc + SC_DONE) >= n || ld_agent(sc + SC_ERR)) {
           got = -2;
         } else {
-          got = ring_pop(d, kind);
-          if (got < 0 && wall_clock64() - t0 > budget) {
+          if (ticket < 0) ticket = ring_ticket(d, kind);
+          got = ring_look(d, kind, ticket);
+          if (got >= 0) ticket = -1;
+          else if (wall_clock64() - t0 > budget) {
             if (atomicExch(sc + SC_ERR, 1) == 0) atomicAdd(&d.stats[7], 1ull);
             got = -2;
           }
@@ -1343,6 +1346,7 @@ __global__ __launch_bounds__(64) void relief_pair_kernel(ModelT<T> mg, EnvCfg cf
         k = ld_coh(d.park + e);
         tid = ld_coh(d.terrain + e);
         held = 0;
+        held_busy = 0;
         if (lead) { W.bspill = body_spill_of<T>(d, e); s_diag[team][0]++; }
         team_sync();
       }
@@ -1373,12 +1377,16 @@ __global__ __launch_bounds__(64) void relief_pair_kernel(ModelT<T> mg, EnvCfg cf
         held++;
         if (k < K) next = predict_env<T>(m, d, tid, W.qn, W.vn, tm.tl, team_shift_of(TEAM)) ? 1 : 0;
       }
-      busy += clock64() - c0;
+      const unsigned long long dc = clock64() - c0;
+      busy += dc;
+      held_busy += dc;
       if (k >= K || next != kind || held >= seg) {  // release the env (team-uniform)
         team_sync();
         if (lead) {
           store_state<T, true>(d, e, W.qn, W.vn, W.wn, step);
           st_coh(d.park + e, k);
+          st_coh(d.pair_env + e, ld_coh(d.pair_env + e) + held_busy);
+          if (k >= K) st_coh(d.pair_env + n + e, static_cast<unsigned long long>(wall_clock64()));
           stores_done();  // release: the state (and a reset's draw) before the ring entry
           if (k >= K) atomicAdd(sc + SC_DONE, 1);
           else ring_push(d, next, e);
@@ -1397,6 +1405,8 @@ __global__ __launch_bounds__(64) void relief_pair_kernel(ModelT<T> mg, EnvCfg cf
     counts_flush(d, cnt);
     if (idle) atomicAdd(sc + SC_IDLE + kind, int(idle > 1000000u ? 1000000u : idle));
     if (busy) atomicAdd(d.pair_busy + kind, busy);
+    atomicAdd(d.pair_busy + 2 + kind, clock64() - c_start);
+    atomicAdd(d.pair_busy + 4 + kind, wall_clock64() - t0);
     atomicAdd(sc + SC_CLAIMS + kind, s_diag[team][0]);
     atomicAdd(sc + SC_STEPS + kind, s_diag[team][1]);
     if (!FULL) atomicAdd(sc + SC_PARKED, s_diag[team][2]);
@@ -1425,6 +1435,7 @@ __global__ __launch_bounds__(64) void pair_init_kernel(ModelT<T> mg, Dev d, cons
   if (tl == 0) {
     d.pred_mark[e] = full ? 1 : 0;
     d.park[e] = 0;
+    d.pair_env[e] = 0;
   }
 }
 
@@ -1445,15 +1456,15 @@ __global__ __launch_bounds__(1024) void pair_rings_kernel(Dev d, const int* __re
     __syncthreads();
   }
   int of = sf[t] - nf, os = ss[t] - ns;
-  int* rf = d.ring;
-  int* rs = d.ring + d.n;
+  unsigned long long* rf = d.ring;
+  unsigned long long* rs = d.ring + d.ring_len;
   for (int e = b; e < e_; e++) {
-    if (d.pred_mark[e]) rs[os++] = e; else rf[of++] = e;
+    if (d.pred_mark[e]) { rs[os] = ring_entry(os, e); os++; } else { rf[of] = ring_entry(of, e); of++; }
   }
   __syncthreads();
   const int NF = sf[1023], NS = ss[1023];
-  for (int i = NF + t; i < d.n; i += 1024) rf[i] = -1;
-  for (int i = NS + t; i < d.n; i += 1024) rs[i] = -1;
+  for (int i = NF + t; i < d.ring_len; i += 1024) rf[i] = ~0ull;  // no ticket's entry
+  for (int i = NS + t; i < d.ring_len; i += 1024) rs[i] = ~0ull;
   if (t == 0) {
     int* sc = d.slow_count;
     sc[SC_RHEAD] = 0; sc[SC_RHEAD + 1] = 0;
@@ -1461,7 +1472,7 @@ __global__ __launch_bounds__(1024) void pair_rings_kernel(Dev d, const int* __re
     sc[SC_DONE] = 0; sc[SC_ERR] = 0;
     sc[SC_IDLE] = 0; sc[SC_IDLE + 1] = 0;
     sc[SC_CLAIMS] = 0; sc[SC_CLAIMS + 1] = 0; sc[SC_STEPS] = 0; sc[SC_STEPS + 1] = 0; sc[SC_PARKED] = 0;
-    d.pair_busy[0] = 0; d.pair_busy[1] = 0;
+    for (int i = 0; i < 6; i++) d.pair_busy[i] = 0;
   }
 }
 
@@ -1965,8 +1976,11 @@ int bb_create(int n_envs, int device, const bb_params* p, bb_handle** out) {
   HIPCHK(hipMalloc((void**)&d.pred_mark, n));
   HIPCHK(hipMalloc(&d.body_spill, es * (MAXB - MAXB_LDS) * NBF * size_t(n)));
   HIPCHK(hipMalloc((void**)&d.perm, sizeof(int) * n));
-  HIPCHK(hipMalloc((void**)&d.ring, sizeof(int) * 2 * n));
-  HIPCHK(hipMalloc((void**)&d.pair_busy, sizeof(unsigned long long) * 2));
+  d.ring_len = n + WAVE / TEAM * h->pair_cap;
+  HIPCHK(hipMalloc((void**)&d.ring, sizeof(unsigned long long) * 2 * size_t(d.ring_len)));
+  HIPCHK(hipMalloc((void**)&d.pair_busy, sizeof(unsigned long long) * 6));
+  HIPCHK(hipMalloc((void**)&d.pair_env, sizeof(unsigned long long) * 2 * size_t(n)));
+  HIPCHK(hipMemset(d.pair_env, 0, sizeof(unsigned long long) * 2 * size_t(n)));
   {  // the relief pair's first split of the resident workgroups (BB_PAIR_FULL: percent full; default half)
     const char* pf = getenv("BB_PAIR_FULL");
     int pct = pf ? atoi(pf) : 50;
@@ -2042,7 +2056,7 @@ int bb_destroy(bb_handle* h) {
   (void)hipFree(h->d.slow_list); (void)hipFree(h->d.slow_count); (void)hipFree(h->d.park);
   (void)hipFree(h->d.fast_envs); (void)hipFree(h->d.pred_envs); (void)hipFree(h->d.pred_mark);
   (void)hipFree(h->d.body_spill); (void)hipFree(h->d.perm); (void)hipFree(h->d.cost); (void)hipFree(h->d.ring);
-  (void)hipFree(h->d.pair_busy);
+  (void)hipFree(h->d.pair_busy); (void)hipFree(h->d.pair_env);
   (void)hipFree(h->tstream); (void)hipFree(h->env_stream); (void)hipFree(h->rng); (void)hipFree(h->seed_slot);
   (void)hipFree(h->d.tseed);
   (void)hipStreamDestroy(h->side); (void)hipEventDestroy(h->fork); (void)hipEventDestroy(h->join);
@@ -2441,13 +2455,22 @@ int bb_pair_counters(bb_handle* h, int64_t* out, int n) {
   HIPCHK(hipSetDevice(h->device));
   HIPCHK(hipDeviceSynchronize());
   int sc[64];
-  unsigned long long busy[2];
+  unsigned long long busy[6];
   HIPCHK(hipMemcpy(sc, h->d.slow_count, sizeof sc, hipMemcpyDeviceToHost));
   HIPCHK(hipMemcpy(busy, h->d.pair_busy, sizeof busy, hipMemcpyDeviceToHost));
   const int64_t v[BB_NPAIR] = {(int64_t)busy[0], (int64_t)busy[1], sc[SC_IDLE], sc[SC_IDLE + 1], sc[SC_ACTIVE],
                                sc[SC_ACTIVE + 1], sc[SC_CLAIMS], sc[SC_CLAIMS + 1], sc[SC_STEPS], sc[SC_STEPS + 1],
-                               sc[SC_PARKED]};
+                               sc[SC_PARKED], (int64_t)busy[2], (int64_t)busy[3], (int64_t)busy[4],
+                               (int64_t)busy[5]};
   for (int i = 0; i < n; i++) out[i] = v[i];
+  return 0;
+}
+
+int bb_pair_env_times(bb_handle* h, uint64_t* out) {
+  if (!h || !out) return fail("bb_pair_env_times: NULL argument");
+  HIPCHK(hipSetDevice(h->device));
+  HIPCHK(hipDeviceSynchronize());
+  HIPCHK(hipMemcpy(out, h->d.pair_env, sizeof(uint64_t) * 2 * size_t(h->d.n), hipMemcpyDeviceToHost));
   return 0;
 }
 
