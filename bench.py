@@ -325,7 +325,8 @@ def main() -> None:
         tj = Path(args.traffic_json)
         if tj.exists():
             try:
-                key = args.precision if not M else f"{args.precision}_multi{M}"
+                key = (args.precision if not M else f"{args.precision}_multi{M}") + (
+                    "" if args.terrain == "flat" else f"_{args.terrain}")
                 tr = json.loads(tj.read_text()).get(key) or {}
                 if tr.get("envs") == n and tr.get("terrain", "flat") == args.terrain:
                     traffic = tr.get("bytes_per_launch")

@@ -1931,7 +1931,9 @@ int bb_create(int n_envs, int device, const bb_params* p, bb_handle** out) {
     int wrate = 0;  // kHz
     if (hipDeviceGetAttribute(&wrate, hipDeviceAttributeWallClockRate, device) != hipSuccess || wrate <= 0)
       wrate = 100000;
-    h->pair_budget = 20ull * 1000ull * (unsigned long long)wrate;
+    const char* pb = getenv("BB_PAIR_BUDGET_MS");  // diagnostics (profilers that serialise launches)
+    const unsigned long long ms = pb && atoll(pb) > 0 ? (unsigned long long)atoll(pb) : 20000ull;
+    h->pair_budget = ms * (unsigned long long)wrate;
   }
   h->md = compile_model(sc);
   h->mf = cast_model<float>(h->md);

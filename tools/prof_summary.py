@@ -15,8 +15,9 @@ import shutil
 from pathlib import Path
 
 KERNEL = "step_kernel"
-SEL = {"which": "fast"}  # --kernel: fast (step_kernel<T,false>), pred (the route-0 predicted full kernel)
-#                          or multi (multi_step_kernel<T>, bb_step_multi)
+SEL = {"which": "fast"}  # --kernel: fast (step_kernel<T,false>), pred (the route-0 predicted full kernel),
+#                          multi (multi_step_kernel<T>, bb_step_multi) or pair (the relief pair: both
+#                          relief_pair_kernel launches of one bb_step_multi call, summed)
 
 
 def is_fast(name):
@@ -33,6 +34,8 @@ def select_ids(recs):
     the step_kernel<T,true> dispatch launched right before each fast dispatch (the
     hand-over full kernel comes after it)."""
     recs = sorted(recs, key=lambda r: int(r["Dispatch_Id"]))
+    if SEL["which"] == "pair":
+        return [int(r["Dispatch_Id"]) for r in recs if "relief_pair_kernel" in r["Kernel_Name"]]
     if SEL["which"] == "multi":
         # multi_step_kernel<T, false> (the fast launch; the finish launch <T, true> only reads park[]
         # on flat), or the single inline launch <T, true> under BB_MULTI_PARK=0, or relief_multi_kernel
@@ -74,7 +77,11 @@ def counters(p, names, last):
             continue
         d = per.setdefault(int(r["Dispatch_Id"]), {})
         d[r["Counter_Name"]] = d.get(r["Counter_Name"], 0.0) + float(r["Counter_Value"])
-    ids = sorted(per)[-last:]
+    ids = sorted(per)
+    if SEL["which"] == "pair":  # one launch = its two relief_pair_kernel dispatches (full, then fast)
+        grp = [ids[i:i + 2] for i in range(0, len(ids) - 1, 2)][-last:]
+        return {n: sum(sum(per[i].get(n, 0.0) for i in g) for g in grp) / len(grp) for n in names}, len(grp)
+    ids = ids[-last:]
     return {n: sum(per[i].get(n, 0.0) for i in ids) / len(ids) for n in names}, len(ids)
 
 
@@ -85,7 +92,7 @@ def main():
     ap.add_argument("--timed", type=int, default=300, help="timed step_kernel dispatches at the end of the trace run")
     ap.add_argument("--pmc-last", type=int, default=20)
     ap.add_argument("--traffic", action="store_true")
-    ap.add_argument("--kernel", default="fast", choices=["fast", "pred", "multi"])
+    ap.add_argument("--kernel", default="fast", choices=["fast", "pred", "multi", "pair"])
     ap.add_argument("--f64", action="store_true", help="also summarise the FP64 VALU instruction pass (sq64)")
     a = ap.parse_args()
     SEL["which"] = a.kernel
@@ -96,8 +103,15 @@ def main():
     keep = set(select_ids(allr))
     tr = [r for r in allr if int(r["Dispatch_Id"]) in keep]
     tr.sort(key=lambda r: int(r["Start_Timestamp"]))
-    timed = tr[-a.timed:]
-    durs = [(int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) * 1e-6 for r in timed]
+    if a.kernel == "pair":  # a launch: first start to last end of its two dispatches
+        tr.sort(key=lambda r: int(r["Dispatch_Id"]))
+        grp = [tr[i:i + 2] for i in range(0, len(tr) - 1, 2)][-a.timed:]
+        timed = [g[0] for g in grp]
+        durs = [(max(int(r["End_Timestamp"]) for r in g) - min(int(r["Start_Timestamp"]) for r in g)) * 1e-6
+                for g in grp]
+    else:
+        timed = tr[-a.timed:]
+        durs = [(int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) * 1e-6 for r in timed]
     bench = json.loads((src / "bench_trace.json").read_text())
     out = {
         "kernel": timed[0]["Kernel_Name"],
@@ -144,9 +158,11 @@ def main():
         tj = dst.parent / "traffic.json"
         cur = json.loads(tj.read_text()) if tj.exists() else {}
         prec = bench["config"]["precision"]
-        spl = bench["config"].get("steps_per_launch", 1) if a.kernel == "multi" else 1
-        cur[prec if spl == 1 else f"{prec}_multi{spl}"] = {
-            "precision": prec, "envs": bench["config"]["envs_per_gpu"], "steps_per_launch": spl,
+        spl = bench["config"].get("steps_per_launch", 1) if a.kernel in ("multi", "pair") else 1
+        terrain = bench["config"].get("workload", "").split(", ")[1].split(" ")[0] if "workload" in bench["config"] else "flat"
+        key = (prec if spl == 1 else f"{prec}_multi{spl}") + ("" if terrain == "flat" else f"_{terrain}")
+        cur[key] = {
+            "precision": prec, "envs": bench["config"]["envs_per_gpu"], "steps_per_launch": spl, "terrain": terrain,
             "bytes_per_launch": fetch_b + write_b, "fetch_raw_bytes_per_launch": f["FETCH_SIZE"] * 1024,
             "write_bytes_per_launch": write_b, "issue_frac": out["derived"]["issue_frac"],
             "source": str(dst) + "_summary.json"}
