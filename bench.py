@@ -177,6 +177,9 @@ def main() -> None:
                     help="M steps per launch (bb_step_multi: the benchmark's random actions are known in advance, so "
                          "each env runs its M steps back to back, bit-identical to M bb_step calls); 0: one bb_step "
                          "launch per step.  With M > 0 the line also reports the per-launch form under 'per_step'")
+    ap.add_argument("--action-pool", type=int, default=512,
+                    help="steps of random actions resident in HBM ([P][n][3], reused cyclically); a launch never "
+                         "crosses the pool's end")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
     ap.add_argument("--traffic-json", default=str(ROOT / "profiles" / "traffic.json"))
@@ -229,7 +232,7 @@ def main() -> None:
         if args.cameras:
             env._render(force=False)
     g = torch.Generator(device=dev).manual_seed(1234 + rank)
-    PS = 256  # action pool slots: random actions resident in HBM, reused cyclically
+    PS = max(1, args.action_pool)  # action pool slots: random actions resident in HBM, reused cyclically
     pool = torch.rand(PS, n, 3, generator=g, device=dev) * 2 - 1
     M = args.multi_step
     if M and (args.cameras or args.graph or not 1 <= M <= PS):
