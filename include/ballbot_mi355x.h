@@ -68,7 +68,7 @@ extern "C" {
 #define BB_DONE_DIVERGED 4 /* MuJoCo's divergence reset ran inside this step (informational) */
 #define BB_DONE_OVERFLOW 8
 #define BB_NSTATS 8
-#define BB_NPAIR 15
+#define BB_NPAIR 16
 
 /* reward kinds (built-in reward plugins, ballbot_gym/rewards) */
 #define BB_REWARD_DIRECTIONAL 0 /* rewards/directional.py:33-54 */
@@ -388,7 +388,8 @@ int bb_get_stats(bb_handle* h, int64_t* out, int n);
  * n (<= BB_NPAIR) of [team-cycles stepping (fast, full), idle loop passes (fast, full), working
  * workgroups of the next launch (fast, full), env claims (fast, full), completed env-steps (fast,
  * full), fast-path hand-overs to the full launch, team lifetimes in shader cycles (fast, full), team
- * lifetimes in wall-clock ticks (fast, full)].  No reference counterpart (tools/). */
+ * lifetimes in wall-clock ticks (fast, full), envs marked heavy for the solo waves].  No
+ * reference counterpart (tools/). */
 int bb_pair_counters(bb_handle* h, int64_t* out, int n);
 /* per env, the last relief-pair launch (waits for the device): out[0:n] shader cycles its steps
  * took (its team's wave, lockstep included), out[n:2n] the wall-clock tick (bb_step_multi's

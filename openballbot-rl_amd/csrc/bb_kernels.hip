@@ -10,6 +10,14 @@
 // Jacobians, ground-contact store, Hessian/Cholesky factor and phase-local
 // scratch; the constraint solve is team-parallel, the per-env state is
 // replicated in the team's registers and stored by the team's lane 0.
+//
+// FMA contraction per source expression only (a * b + c written as one
+// expression): the backend's contraction of separate multiplies and adds
+// depends on the inlining context, so two kernels inlining the same step
+// (bb_step's, bb_step_multi's, the relief pair's, the rollout's) could round
+// differently.  With contraction fixed by the source, every kernel computes
+// each env's step bit for bit the same.
+#pragma clang fp contract(on)
 #include <hip/hip_runtime.h>
 
 #include <stdarg.h>
@@ -1255,6 +1263,11 @@ __global__ __launch_bounds__(64 * QW) void relief_multi_kernel(ModelT<T> mg, Env
 constexpr int SC_RHEAD = 16, SC_RTAIL = 18, SC_DONE = 20, SC_ERR = 21, SC_ACTIVE = 22, SC_IDLE = 24;
 // diagnostics of the last launch (bb_pair_counters): claims [2], completed steps [2], fast-path hand-overs
 constexpr int SC_CLAIMS = 32, SC_STEPS = 34, SC_PARKED = 36;
+// solo waves: ring 2 (the heavy envs' full steps) counters, the solo workgroup count, the heavy
+// marks of this launch (reset by pair_rings_kernel, which keeps the count in SC_HEAVY_LAST)
+constexpr int SC_RHEAD2 = 40, SC_RTAIL2 = 41, SC_SOLO = 42, SC_HEAVY = 43, SC_HEAVY_LAST = 44, NRING = 3;
+__device__ __forceinline__ int ring_head_slot(int r) { return r < 2 ? SC_RHEAD + r : SC_RHEAD2; }
+__device__ __forceinline__ int ring_tail_slot(int r) { return r < 2 ? SC_RTAIL + r : SC_RTAIL2; }
 
 __device__ __forceinline__ int ld_agent(const int* p) {
   return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -1271,7 +1284,9 @@ __device__ __forceinline__ int ld_agent(const int* p) {
 __device__ __forceinline__ unsigned long long ring_entry(int ticket, int e) {
   return (static_cast<unsigned long long>(unsigned(ticket)) << 32) | unsigned(e);
 }
-__device__ __forceinline__ int ring_ticket(const Dev& d, int kind) { return atomicAdd(d.slow_count + SC_RHEAD + kind, 1); }
+__device__ __forceinline__ int ring_ticket(const Dev& d, int kind) {
+  return atomicAdd(d.slow_count + ring_head_slot(kind), 1);
+}
 // the env of `ticket` in ring `kind`, or -1 while it has not been appended
 __device__ __forceinline__ int ring_look(const Dev& d, int kind, int ticket) {
   const unsigned long long v =
@@ -1280,23 +1295,20 @@ __device__ __forceinline__ int ring_look(const Dev& d, int kind, int ticket) {
 }
 // append env e to ring `kind` (lead lane; the env's state is stored and released)
 __device__ __forceinline__ void ring_push(const Dev& d, int kind, int e) {
-  const int t = atomicAdd(d.slow_count + SC_RTAIL + kind, 1);
+  const int t = atomicAdd(d.slow_count + ring_tail_slot(kind), 1);
   st_coh(d.ring + size_t(kind) * d.ring_len + (unsigned(t) % unsigned(d.ring_len)), ring_entry(t, e));
 }
 
+// one team loop of the relief pair (FULL: the full launch's; wg: this workgroup's index among
+// its kind's working workgroups; the caller checked the gate and the active count)
 template <typename T, bool FULL>
-__global__ __launch_bounds__(64) void relief_pair_kernel(ModelT<T> mg, EnvCfg cfg, Dev d, const float* __restrict__ act,
-                                                         int K, float* __restrict__ obs, float* __restrict__ rew,
-                                                         uint8_t* __restrict__ done, float* __restrict__ tobs,
-                                                         float* __restrict__ pos2d, int auto_reset, int seg,
-                                                         unsigned long long budget, const int* __restrict__ gate) {
+__device__ __forceinline__ void pair_loop(const ModelT<T>& mg, const EnvCfg& cfg, const Dev& d, const float* __restrict__ act,
+                                          int K, float* __restrict__ obs, float* __restrict__ rew,
+                                          uint8_t* __restrict__ done, float* __restrict__ tobs,
+                                          float* __restrict__ pos2d, int auto_reset, int seg,
+                                          unsigned long long budget, const int* __restrict__ gate, int wg,
+                                          unsigned char* smem, ModelT<T>& ms, unsigned (*s_cnt)[8], int (*s_diag)[3]) {
   int* sc = d.slow_count;
-  // adaptive form: the parked launches run instead; else only the active workgroups
-  // (workgroup-uniform, before any barrier)
-  if ((gate && *gate == ROUTE_PARK) || int(blockIdx.x) >= sc[SC_ACTIVE + FULL]) return;
-  extern __shared__ __align__(16) unsigned char smem[];
-  __shared__ ModelT<T> ms;
-  __shared__ unsigned s_cnt[WAVE / TEAM][8];
   if (threadIdx.x == 0) ms = mg;
   if (threadIdx.x < 32) s_cnt[threadIdx.x >> 3][threadIdx.x & 7] = 0u;
   __syncthreads();
@@ -1308,9 +1320,12 @@ __global__ __launch_bounds__(64) void relief_pair_kernel(ModelT<T> mg, EnvCfg cf
   EnvWork<T>& W = team_work<T>(smem, team);
   T* bk = reinterpret_cast<T*>(smem + size_t(WAVE / TEAM) * work_stride<T>()) + team * (NQ + 2 * NV);
   unsigned* cnt = s_cnt[team];
-  __shared__ int s_diag[WAVE / TEAM][3];  // claims, completed steps, fast-path hand-overs
   if (lead) { s_diag[team][0] = 0; s_diag[team][1] = 0; s_diag[team][2] = 0; }
   const int kind = FULL ? 1 : 0;
+  // solo waves (full launch, the first sc[SC_SOLO] workgroups): team 0 alone steps the envs
+  // marked heavy (ring 2), so a heavy env's step never waits for wave-mates' divergent work
+  const bool solo = FULL && wg < sc[SC_SOLO];
+  const int rkind = solo ? 2 : kind;
   const unsigned long long t0 = wall_clock64(), c_start = clock64();
   int e = -1, k = 0, tid = 0, step = 0, held = 0, ticket = -1;  // ticket: the lead's, -1 when none
   unsigned idle = 0;
@@ -1323,11 +1338,11 @@ __global__ __launch_bounds__(64) void relief_pair_kernel(ModelT<T> mg, EnvCfg cf
     if (e < 0) {
       int got = -1;
       if (lead) {
-        if (ld_agent(sc + SC_DONE) >= n || ld_agent(sc + SC_ERR)) {
+        if (ld_agent(sc + SC_DONE) >= n || ld_agent(sc + SC_ERR) || (solo && team > 0)) {
           got = -2;
         } else {
-          if (ticket < 0) ticket = ring_ticket(d, kind);
-          got = ring_look(d, kind, ticket);
+          if (ticket < 0) ticket = ring_ticket(d, rkind);
+          got = ring_look(d, rkind, ticket);
           if (got >= 0) ticket = -1;
           else if (wall_clock64() - t0 > budget) {
             if (atomicExch(sc + SC_ERR, 1) == 0) atomicAdd(&d.stats[7], 1ull);
@@ -1389,7 +1404,7 @@ __global__ __launch_bounds__(64) void relief_pair_kernel(ModelT<T> mg, EnvCfg cf
           if (k >= K) st_coh(d.pair_env + n + e, static_cast<unsigned long long>(wall_clock64()));
           stores_done();  // release: the state (and a reset's draw) before the ring entry
           if (k >= K) atomicAdd(sc + SC_DONE, 1);
-          else ring_push(d, next, e);
+          else ring_push(d, next == 1 && (d.pred_mark[e] & 2) ? 2 : next, e);
           if (FULL && gate) atomicAdd(sc + SC_TOUCHED, 1);  // adaptive route: an env took full steps
         }
         e = -1;
@@ -1413,10 +1428,52 @@ __global__ __launch_bounds__(64) void relief_pair_kernel(ModelT<T> mg, EnvCfg cf
   }
 }
 
+// the pair as two launches (on two streams)
+template <typename T, bool FULL>
+__global__ __launch_bounds__(64) void relief_pair_kernel(ModelT<T> mg, EnvCfg cfg, Dev d, const float* __restrict__ act,
+                                                         int K, float* __restrict__ obs, float* __restrict__ rew,
+                                                         uint8_t* __restrict__ done, float* __restrict__ tobs,
+                                                         float* __restrict__ pos2d, int auto_reset, int seg,
+                                                         unsigned long long budget, const int* __restrict__ gate) {
+  // adaptive form: the parked launches run instead; else only the active workgroups
+  // (workgroup-uniform, before any barrier)
+  if ((gate && *gate == ROUTE_PARK) || int(blockIdx.x) >= d.slow_count[SC_ACTIVE + FULL]) return;
+  extern __shared__ __align__(16) unsigned char smem[];
+  __shared__ ModelT<T> ms;
+  __shared__ unsigned s_cnt[WAVE / TEAM][8];
+  __shared__ int s_diag[WAVE / TEAM][3];  // claims, completed steps, fast-path hand-overs
+  pair_loop<T, FULL>(mg, cfg, d, act, K, obs, rew, done, tobs, pos2d, auto_reset, seg, budget, gate, int(blockIdx.x), smem,
+                     ms, s_cnt, s_diag);
+}
+
+// the pair as ONE launch: the first SC_ACTIVE[0] workgroups run the fast loop, the next
+// SC_ACTIVE[1] the full loop (the two loops are disjoint regions of the kernel, so
+// the kernel keeps the larger one's registers, not their union)
+template <typename T>
+__global__ __launch_bounds__(64) void relief_pair1_kernel(ModelT<T> mg, EnvCfg cfg, Dev d, const float* __restrict__ act,
+                                                          int K, float* __restrict__ obs, float* __restrict__ rew,
+                                                          uint8_t* __restrict__ done, float* __restrict__ tobs,
+                                                          float* __restrict__ pos2d, int auto_reset, int seg,
+                                                          unsigned long long budget, const int* __restrict__ gate) {
+  if (gate && *gate == ROUTE_PARK) return;
+  const int nf = d.slow_count[SC_ACTIVE], ns = d.slow_count[SC_ACTIVE + 1], b = int(blockIdx.x);
+  if (b >= nf + ns) return;
+  extern __shared__ __align__(16) unsigned char smem[];
+  __shared__ ModelT<T> ms;
+  __shared__ unsigned s_cnt[WAVE / TEAM][8];
+  __shared__ int s_diag[WAVE / TEAM][3];
+  if (b < nf)
+    pair_loop<T, false>(mg, cfg, d, act, K, obs, rew, done, tobs, pos2d, auto_reset, seg, budget, gate, b, smem, ms,
+                        s_cnt, s_diag);
+  else
+    pair_loop<T, true>(mg, cfg, d, act, K, obs, rew, done, tobs, pos2d, auto_reset, seg, budget, gate, b - nf, smem, ms,
+                       s_cnt, s_diag);
+}
+
 // before the pair: every env's first route (predict_kernel's test) into the
 // rings in env order, step counts to 0, counters reset.  One workgroup per 4 envs.
 template <typename T>
-__global__ __launch_bounds__(64) void pair_init_kernel(ModelT<T> mg, Dev d, const int* __restrict__ gate) {
+__global__ __launch_bounds__(64) void pair_init_kernel(ModelT<T> mg, Dev d, const int* __restrict__ gate, int heavy_pct) {
   if (gate && *gate == ROUTE_PARK) return;
   __shared__ ModelT<T> ms;
   if (threadIdx.x == 0) ms = mg;
@@ -1433,7 +1490,15 @@ __global__ __launch_bounds__(64) void pair_init_kernel(ModelT<T> mg, Dev d, cons
   for (int i = 0; i < 6; i++) Ve[i] = V[i * d.n + e];
   const bool full = predict_env<T>(ms, d, d.terrain[e], Qe, Ve, tl, team_shift_of(16));
   if (tl == 0) {
-    d.pred_mark[e] = full ? 1 : 0;
+    // heavy: the env's steps took more than heavy_pct % of the mean env's in the last
+    // launch (its full steps then go to the solo waves, at most SC_SOLO envs)
+    const unsigned long long tot = d.pair_busy[0] + d.pair_busy[1];
+    const int nsolo = d.slow_count[SC_SOLO];
+    bool heavy = false;
+    if (nsolo > 0 && tot > 0 &&
+        double(d.pair_env[e]) * double(d.n) > double(tot) * double(heavy_pct) * 0.01)
+      heavy = atomicAdd(d.slow_count + SC_HEAVY, 1) < nsolo;
+    d.pred_mark[e] = uint8_t((full ? 1 : 0) | (heavy ? 2 : 0));
     d.park[e] = 0;
     d.pair_env[e] = 0;
   }
@@ -1443,35 +1508,38 @@ __global__ __launch_bounds__(64) void pair_init_kernel(ModelT<T> mg, Dev d, cons
 // block, as split_kernel), their counters, and the empty slots
 __global__ __launch_bounds__(1024) void pair_rings_kernel(Dev d, const int* __restrict__ gate) {
   if (gate && *gate == ROUTE_PARK) return;
-  __shared__ int sf[1024], ss[1024];
+  __shared__ int sc3[NRING][1024];
   const int t = threadIdx.x, per = (d.n + 1023) / 1024, b = t * per, e_ = min(d.n, b + per);
-  int nf = 0, ns = 0;
-  for (int e = b; e < e_; e++) { if (d.pred_mark[e]) ns++; else nf++; }
-  sf[t] = nf; ss[t] = ns;
+  auto ring_of = [&](int e) { const int mk = d.pred_mark[e]; return (mk & 1) ? ((mk & 2) ? 2 : 1) : 0; };
+  int cnt[NRING] = {0, 0, 0};
+  for (int e = b; e < e_; e++) cnt[ring_of(e)]++;
+  for (int r = 0; r < NRING; r++) sc3[r][t] = cnt[r];
   __syncthreads();
   for (int off = 1; off < 1024; off <<= 1) {
-    const int af = t >= off ? sf[t - off] : 0, as = t >= off ? ss[t - off] : 0;
+    int add[NRING];
+    for (int r = 0; r < NRING; r++) add[r] = t >= off ? sc3[r][t - off] : 0;
     __syncthreads();
-    sf[t] += af; ss[t] += as;
+    for (int r = 0; r < NRING; r++) sc3[r][t] += add[r];
     __syncthreads();
   }
-  int of = sf[t] - nf, os = ss[t] - ns;
-  unsigned long long* rf = d.ring;
-  unsigned long long* rs = d.ring + d.ring_len;
+  int pos[NRING];
+  for (int r = 0; r < NRING; r++) pos[r] = sc3[r][t] - cnt[r];
   for (int e = b; e < e_; e++) {
-    if (d.pred_mark[e]) { rs[os] = ring_entry(os, e); os++; } else { rf[of] = ring_entry(of, e); of++; }
+    const int r = ring_of(e);
+    d.ring[size_t(r) * d.ring_len + pos[r]] = ring_entry(pos[r], e);
+    pos[r]++;
   }
   __syncthreads();
-  const int NF = sf[1023], NS = ss[1023];
-  for (int i = NF + t; i < d.ring_len; i += 1024) rf[i] = ~0ull;  // no ticket's entry
-  for (int i = NS + t; i < d.ring_len; i += 1024) rs[i] = ~0ull;
+  for (int r = 0; r < NRING; r++)
+    for (int i = sc3[r][1023] + t; i < d.ring_len; i += 1024) d.ring[size_t(r) * d.ring_len + i] = ~0ull;  // no ticket's entry
   if (t == 0) {
     int* sc = d.slow_count;
-    sc[SC_RHEAD] = 0; sc[SC_RHEAD + 1] = 0;
-    sc[SC_RTAIL] = NF; sc[SC_RTAIL + 1] = NS;
+    for (int r = 0; r < NRING; r++) { sc[ring_head_slot(r)] = 0; sc[ring_tail_slot(r)] = sc3[r][1023]; }
     sc[SC_DONE] = 0; sc[SC_ERR] = 0;
     sc[SC_IDLE] = 0; sc[SC_IDLE + 1] = 0;
     sc[SC_CLAIMS] = 0; sc[SC_CLAIMS + 1] = 0; sc[SC_STEPS] = 0; sc[SC_STEPS + 1] = 0; sc[SC_PARKED] = 0;
+    sc[SC_HEAVY_LAST] = sc[SC_HEAVY];
+    sc[SC_HEAVY] = 0;
     for (int i = 0; i < 6; i++) d.pair_busy[i] = 0;
   }
 }
@@ -1618,6 +1686,9 @@ struct bb_handle {
   int pair_cap = 0;             // one-wave workgroups resident on the chip (4 per CU)
   int pair_seg = 16;            // steps a team holds an env before requeueing it (BB_PAIR_SEG)
   int pair_adapt = 1;           // split the workgroups by the last launch's work (BB_PAIR_ADAPT=0: keep the first split)
+  int pair_one = 0;             // the pair as one launch (BB_PAIR_ONE=1): one dispatch, profilable per dispatch
+  int pair_solo = 0;            // solo waves for heavy envs' full steps (BB_PAIR_SOLO; <= pair_cap / 8)
+  int pair_heavy_pct = 150;     // heavy: last launch's cycles above this % of the mean env's (BB_PAIR_HEAVY)
   unsigned long long pair_budget = 0;  // wall-clock ticks a pair launch may wait for work (20 s)
   int count_memset = 0;         // diagnostic (BB_COUNT_MEMSET=1): reset the hand-over count with
                                 // hipMemsetAsync instead of zero_count_kernel
@@ -1762,16 +1833,22 @@ int launch_pair(bb_handle* h, const float* a, int K, float* o, float* r, uint8_t
                 hipStream_t s, const int* gate) {
   const ModelT<T>& m = model_of<T>(h);
   const size_t plb = multi_lds_bytes<T>(4);
-  hipLaunchKernelGGL(pair_init_kernel<T>, dim3((h->n + WAVE / 16 - 1) / (WAVE / 16)), dim3(WAVE), 0, s, m, h->d, gate);
+  hipLaunchKernelGGL(pair_init_kernel<T>, dim3((h->n + WAVE / 16 - 1) / (WAVE / 16)), dim3(WAVE), 0, s, m, h->d, gate,
+                     h->pair_heavy_pct);
   hipLaunchKernelGGL(pair_rings_kernel, dim3(1), dim3(1024), 0, s, h->d, gate);
-  HIPCHK(hipEventRecord(h->fork, s));
-  HIPCHK(hipStreamWaitEvent(h->side, h->fork, 0));
-  hipLaunchKernelGGL((relief_pair_kernel<T, true>), dim3(h->pair_cap), dim3(WAVE), plb, h->side, m, h->cfg, h->d, a, K,
-                     o, r, dn, t, p2, ar, h->pair_seg, h->pair_budget, gate);
-  hipLaunchKernelGGL((relief_pair_kernel<T, false>), dim3(h->pair_cap), dim3(WAVE), plb, s, m, h->cfg, h->d, a, K, o,
-                     r, dn, t, p2, ar, h->pair_seg, h->pair_budget, gate);
-  HIPCHK(hipEventRecord(h->join, h->side));
-  HIPCHK(hipStreamWaitEvent(s, h->join, 0));
+  if (h->pair_one) {
+    hipLaunchKernelGGL(relief_pair1_kernel<T>, dim3(h->pair_cap), dim3(WAVE), plb, s, m, h->cfg, h->d, a, K, o, r, dn, t,
+                       p2, ar, h->pair_seg, h->pair_budget, gate);
+  } else {
+    HIPCHK(hipEventRecord(h->fork, s));
+    HIPCHK(hipStreamWaitEvent(h->side, h->fork, 0));
+    hipLaunchKernelGGL((relief_pair_kernel<T, true>), dim3(h->pair_cap), dim3(WAVE), plb, h->side, m, h->cfg, h->d, a,
+                       K, o, r, dn, t, p2, ar, h->pair_seg, h->pair_budget, gate);
+    hipLaunchKernelGGL((relief_pair_kernel<T, false>), dim3(h->pair_cap), dim3(WAVE), plb, s, m, h->cfg, h->d, a, K, o,
+                       r, dn, t, p2, ar, h->pair_seg, h->pair_budget, gate);
+    HIPCHK(hipEventRecord(h->join, h->side));
+    HIPCHK(hipStreamWaitEvent(s, h->join, 0));
+  }
   if (h->pair_adapt) hipLaunchKernelGGL(pair_adapt_kernel, dim3(1), dim3(64), 0, s, h->d, h->pair_cap, gate);
   return 0;
 }
@@ -1931,6 +2008,13 @@ int bb_create(int n_envs, int device, const bb_params* p, bb_handle** out) {
     int wrate = 0;  // kHz
     if (hipDeviceGetAttribute(&wrate, hipDeviceAttributeWallClockRate, device) != hipSuccess || wrate <= 0)
       wrate = 100000;
+    const char* po = getenv("BB_PAIR_ONE");
+    if (po) h->pair_one = atoi(po) != 0;
+    const char* so = getenv("BB_PAIR_SOLO");
+    if (so) h->pair_solo = atoi(so) > 0 ? atoi(so) : 0;
+    if (h->pair_solo > h->pair_cap / 8) h->pair_solo = h->pair_cap / 8;
+    const char* hv = getenv("BB_PAIR_HEAVY");
+    if (hv && atoi(hv) > 0) h->pair_heavy_pct = atoi(hv);
     const char* pb = getenv("BB_PAIR_BUDGET_MS");  // diagnostics (profilers that serialise launches)
     const unsigned long long ms = pb && atoll(pb) > 0 ? (unsigned long long)atoll(pb) : 20000ull;
     h->pair_budget = ms * (unsigned long long)wrate;
@@ -1979,7 +2063,7 @@ int bb_create(int n_envs, int device, const bb_params* p, bb_handle** out) {
   HIPCHK(hipMalloc(&d.body_spill, es * (MAXB - MAXB_LDS) * NBF * size_t(n)));
   HIPCHK(hipMalloc((void**)&d.perm, sizeof(int) * n));
   d.ring_len = n + WAVE / TEAM * h->pair_cap;
-  HIPCHK(hipMalloc((void**)&d.ring, sizeof(unsigned long long) * 2 * size_t(d.ring_len)));
+  HIPCHK(hipMalloc((void**)&d.ring, sizeof(unsigned long long) * NRING * size_t(d.ring_len)));
   HIPCHK(hipMalloc((void**)&d.pair_busy, sizeof(unsigned long long) * 6));
   HIPCHK(hipMalloc((void**)&d.pair_env, sizeof(unsigned long long) * 2 * size_t(n)));
   HIPCHK(hipMemset(d.pair_env, 0, sizeof(unsigned long long) * 2 * size_t(n)));
@@ -1990,6 +2074,7 @@ int bb_create(int n_envs, int device, const bb_params* p, bb_handle** out) {
     const int ns = h->pair_cap * pct / 100;
     int act[2] = {h->pair_cap - ns, ns};
     HIPCHK(hipMemcpy(d.slow_count + SC_ACTIVE, act, sizeof act, hipMemcpyHostToDevice));
+    HIPCHK(hipMemcpy(d.slow_count + SC_SOLO, &h->pair_solo, sizeof(int), hipMemcpyHostToDevice));
   }
   HIPCHK(hipMalloc((void**)&d.cost, sizeof(unsigned long long) * n));
   HIPCHK(hipMemset(d.cost, 0, sizeof(unsigned long long) * n));
@@ -2463,7 +2548,7 @@ int bb_pair_counters(bb_handle* h, int64_t* out, int n) {
   const int64_t v[BB_NPAIR] = {(int64_t)busy[0], (int64_t)busy[1], sc[SC_IDLE], sc[SC_IDLE + 1], sc[SC_ACTIVE],
                                sc[SC_ACTIVE + 1], sc[SC_CLAIMS], sc[SC_CLAIMS + 1], sc[SC_STEPS], sc[SC_STEPS + 1],
                                sc[SC_PARKED], (int64_t)busy[2], (int64_t)busy[3], (int64_t)busy[4],
-                               (int64_t)busy[5]};
+                               (int64_t)busy[5], sc[SC_HEAVY_LAST]};
   for (int i = 0; i < n; i++) out[i] = v[i];
   return 0;
 }
