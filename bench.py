@@ -336,6 +336,9 @@ def main() -> None:
                     issue_frac = tr.get("issue_frac")
             except Exception:
                 traffic = issue_frac = None
+        relief_form = ("relief_multi_kernel<T> (work queue)" if os.environ.get("BB_RELIEF_PAIR", "1") == "0" else
+                       "relief_pair1_kernel<T> (the relief pair, one launch)" if os.environ.get("BB_PAIR_ONE", "1") != "0"
+                       else "relief_pair_kernel<T,false> + <T,true> (the relief pair, two concurrent launches)")
         line = {
             "metric": f"env-steps/sec at {n} envs per GPU ({args.terrain} terrain, random actions)",
             "value": value,
@@ -368,11 +371,11 @@ def main() -> None:
                                  f"once per launch of {spl:g} steps, action and all five outputs every step"
                                  + (", 7x7 hfield vertices per step" if env.relief else "") +
                                  ") x the env-steps of one launch",
-                         "kernel": ((f"relief_multi_kernel<T> (work queue) or the parked multi_step_kernel<T,*> "
+                         "kernel": ((f"{relief_form} or the parked multi_step_kernel<T,*> "
                                      f"launches, chosen per launch from the last one's full steps ({M} steps per "
                                      "launch)" if env.relief and "BB_MULTI_QUEUE" not in os.environ and
                                      "BB_ROUTE" not in os.environ and os.environ.get("BB_MULTI_ADAPT", "1") != "0"
-                                     else f"relief_multi_kernel<T> (work queue, {M} steps per launch)" if env.relief
+                                     else f"{relief_form} ({M} steps per launch)" if env.relief
                                      and os.environ.get("BB_MULTI_QUEUE", "1") != "0" and
                                      os.environ.get("BB_ROUTE", "0") == "0"
                                      else f"multi_step_kernel<T,false> ({M} steps per launch; hand-overs parked "

@@ -174,14 +174,8 @@ BB_HD void prism_centroid(const PrismG<T>& P, T* cen) {
 // loop) from 9 segment pairs and 10 projections instead of 16 point-triangle
 // and 24 segment pairs.
 template <typename T>
-#ifdef __HIP_DEVICE_COMPILE__
-#ifdef BB_CAPSULE_INLINE  // variant build (tools/lib_bench.py): the same source inlined
-__attribute__((always_inline))
-#else
-__attribute__((noinline))
-#endif
-#endif
-BB_HD bool capsule_prism_apart(const Seg<T>& g, const PrismG<T>& P, const T* p0, const T* p1, T& dist, T* n, T* pos) {
+BB_HD inline bool capsule_prism_apart(const Seg<T>& g, const PrismG<T>& P, const T* p0, const T* p1, T& dist, T* n,
+                                      T* pos) {
   T best2 = T(1e30), bp[3] = {0, 0, 0}, bq[3] = {0, 0, 0};
   T h0[5], h1[5];
 #pragma unroll
@@ -229,6 +223,36 @@ BB_HD bool capsule_prism_apart(const Seg<T>& g, const PrismG<T>& P, const T* p0,
   return true;
 }
 
+#ifdef __HIP_DEVICE_COMPILE__
+// On the GPU capsule_prism_apart runs as a call: inlined into the base-tree
+// collision it costs that code its registers (§6b).  The call takes its inputs
+// by value -- the segment ends, the radius, the prism's top triangle and bottom
+// -- and returns its outputs by value (14 dwords, in registers), so nothing
+// goes through the stack: with the prism and the segment passed by reference
+// every call wrote ~470 B per lane to scratch (the relief kernels' write
+// traffic).  The prism is rebuilt from the same inputs by the same code, so it
+// is bit for bit the caller's.  dist = 1e30 when there is no contact.
+template <typename T>
+struct ApartOut {
+  T dist, n[3], pos[3];
+};
+template <typename T>
+__attribute__((noinline)) __device__ ApartOut<T> capsule_prism_apart_call(T p00, T p01, T p02, T p10, T p11, T p12, T r,
+                                                                          T v00, T v01, T v02, T v10, T v11, T v12,
+                                                                          T v20, T v21, T v22, T zb) {
+  const T Tp[3][3] = {{v00, v01, v02}, {v10, v11, v12}, {v20, v21, v22}};
+  PrismG<T> P;
+  prism_build(P, Tp, zb);
+  Seg<T> g;  // capsule_prism_apart reads only the radius
+  g.r = r;
+  const T p0[3] = {p00, p01, p02}, p1[3] = {p10, p11, p12};
+  ApartOut<T> o;
+  T d = T(0);
+  o.dist = capsule_prism_apart(g, P, p0, p1, d, o.n, o.pos) ? d : T(1e30);
+  return o;
+}
+#endif
+
 // capsule vs prism; normal from prism to capsule.  Returns 1 on contact.
 template <typename T>
 BB_HD bool capsule_prism(const Seg<T>& g, const PrismG<T>& P, T& dist, T* n, T* pos) {
@@ -254,7 +278,20 @@ BB_HD bool capsule_prism(const Seg<T>& g, const PrismG<T>& P, T& dist, T* n, T* 
     }
   }
   if (t0 > t1) inter = false;
-  if (!inter) return capsule_prism_apart(g, P, p0, p1, dist, n, pos);
+  if (!inter) {
+#if defined(__HIP_DEVICE_COMPILE__) && !defined(BB_CAPSULE_INLINE)
+    const ApartOut<T> o = capsule_prism_apart_call(p0[0], p0[1], p0[2], p1[0], p1[1], p1[2], g.r, P.V[0][0], P.V[0][1],
+                                                   P.V[0][2], P.V[1][0], P.V[1][1], P.V[1][2], P.V[2][0], P.V[2][1],
+                                                   P.V[2][2], P.V[3][2]);
+    if (o.dist == T(1e30)) return false;  // (a NaN distance is a contact, as in capsule_prism_apart)
+    dist = o.dist;
+#pragma unroll
+    for (int i = 0; i < 3; i++) { n[i] = o.n[i]; pos[i] = o.pos[i]; }
+    return true;
+#else
+    return capsule_prism_apart(g, P, p0, p1, dist, n, pos);
+#endif
+  }
   // intersecting: minimum over the separating-axis candidates
   T bestd = T(1e30), bn[3] = {0, 0, 1};
   // both signs of an axis from one set of dot products: support(-a) =

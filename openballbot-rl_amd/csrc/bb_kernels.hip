@@ -17,7 +17,11 @@
 // (bb_step's, bb_step_multi's, the relief pair's, the rollout's) could round
 // differently.  With contraction fixed by the source, every kernel computes
 // each env's step bit for bit the same.
+#if defined(BB_FP_CONTRACT_OFF)  // variant builds (tools/lib_bench.py): no contraction at all
+#pragma clang fp contract(off)
+#elif !defined(BB_FP_CONTRACT_FAST)  // ... or the compiler default (fast, backend-decided)
 #pragma clang fp contract(on)
+#endif
 #include <hip/hip_runtime.h>
 
 #include <stdarg.h>
@@ -39,7 +43,7 @@
 using namespace bb;
 
 #ifdef BB_PHASE_CLOCKS
-namespace bb { __device__ unsigned long long bb_phase_cycles[80]; }
+namespace bb { __device__ unsigned long long bb_phase_cycles[100]; }
 #endif
 
 namespace {
@@ -2677,8 +2681,8 @@ int bb_get_config(bb_handle* h, int32_t* out5) {
 // diagnostic build only: read and clear the per-phase cycle counters
 int bb_debug_phase_cycles(unsigned long long* out16) {
   HIPCHK(hipDeviceSynchronize());
-  HIPCHK(hipMemcpyFromSymbol(out16, HIP_SYMBOL(bb::bb_phase_cycles), sizeof(unsigned long long) * 80));
-  unsigned long long z[80] = {0};
+  HIPCHK(hipMemcpyFromSymbol(out16, HIP_SYMBOL(bb::bb_phase_cycles), sizeof(unsigned long long) * 100));
+  unsigned long long z[100] = {0};
   HIPCHK(hipMemcpyToSymbol(HIP_SYMBOL(bb::bb_phase_cycles), z, sizeof z));
   return 0;
 }

@@ -28,22 +28,26 @@ static int g_stage_iters[4] = {0, 0, 0, 0};  // Newton iterations of each RK sta
 // Diagnostic build only (-DBB_PHASE_CLOCKS): per-phase s_memtime cycles,
 // summed over teams into bb_phase_cycles[] (read back by tools/phase_clocks).
 #if defined(BB_PHASE_CLOCKS) && defined(__HIP_DEVICE_COMPILE__)
-extern __device__ unsigned long long bb_phase_cycles[80];
+extern __device__ unsigned long long bb_phase_cycles[100];
 #define PH_DECL unsigned long long ph_t = clock64(), ph_acc[10] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
 #define PH(k) { unsigned long long n_ = clock64(); ph_acc[k] += n_ - ph_t; ph_t = n_; }
 // phases 0-7 -> slots 0-7; 8 (line-search setup) -> 32, 9 (line-search loop) -> 33
 #define PH_FLUSH(tm) if ((tm).tl == 0) { for (int k_ = 0; k_ < 8; k_++) atomicAdd(&bb_phase_cycles[k_], ph_acc[k_]); \
                                           atomicAdd(&bb_phase_cycles[32], ph_acc[8]); atomicAdd(&bb_phase_cycles[33], ph_acc[9]); }
+// the full kernel's solves (base-tree contacts) separately: phases 0-9 -> slots 80-89
+#define PH_FLUSH_BODY(tm) if ((tm).tl == 0) { for (int k_ = 0; k_ < 10; k_++) atomicAdd(&bb_phase_cycles[80 + k_], ph_acc[k_]); }
 #elif defined(BB_ISA_MARKS) && defined(__HIP_DEVICE_COMPILE__)
 // ISA analysis build: phase boundaries as assembler comments
 #define PH_DECL
 #define PH(k) asm volatile("; PHASE_MARK " #k);
 #define PH_TOP asm volatile("; PHASE_MARK 10");
 #define PH_FLUSH(tm)
+#define PH_FLUSH_BODY(tm)
 #else
 #define PH_DECL
 #define PH(k)
 #define PH_FLUSH(tm)
+#define PH_FLUSH_BODY(tm)
 #endif
 #ifndef PH_TOP
 #define PH_TOP

@@ -785,7 +785,11 @@ __device__ int solve16(const ModelT<T>& m, EnvWork<T>& W, int ng, int nb, T* a, 
     if (-m.scale * dcost < m.tol) { it++; break; }
   }
   PH(7)
-  PH_FLUSH((Team{L, tl}))
+  if constexpr (BODY) {
+    PH_FLUSH_BODY((Team{L, tl}))
+  } else {
+    PH_FLUSH((Team{L, tl}))
+  }
   return it;
 }
 

@@ -40,7 +40,7 @@ def main():
     from ballbot_gym.envs import BallbotVecEnv
     env = BallbotVecEnv(4096, device="cuda:0", precision=a.precision, terrain_config={"type": a.terrain, "config": {}})
     pool = torch.rand(64, 4096, 3, device="cuda:0") * 2 - 1
-    out = (C.c_ulonglong * 80)()
+    out = (C.c_ulonglong * 100)()
     for i in range(a.warmup):
         env.step_async_raw(pool[i % 64])
     torch.cuda.synchronize()
@@ -75,6 +75,11 @@ def main():
     for name, k in (("full", 34), ("fast", 37)):  # per-env step durations (s_memtime cycles)
         if out[k + 2]:
             res[f"{name}_env_step_cycles"] = {"max": out[k], "mean": out[k + 1] / out[k + 2], "count": out[k + 2]}
+    if out[12]:  # the full kernel's solve by phase (slots 80-89), per full forward and per Newton iteration
+        ph = {NAMES[k]: out[80 + k] for k in range(8)}
+        ph["line_search_setup"], ph["line_search_loop"] = out[88], out[89]
+        res["full_kernel"]["solve_phase_cycles_per_forward"] = {k: v / out[12] for k, v in ph.items()}
+        res["full_kernel"]["solve_phase_cycles_per_newton_iter"] = {k: v / max(out[20], 1) for k, v in ph.items()}
     if out[12]:  # full kernel: per-env step duration histogram, bins of 2^20 cycles
         res["full_env_step_hist"] = [{"bin_Mcyc": b * 1.048576, "envs": out[40 + b],
                                       "body_contacts_per_step": out[50 + b] / max(out[40 + b], 1),

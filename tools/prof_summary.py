@@ -35,7 +35,9 @@ def select_ids(recs):
     hand-over full kernel comes after it)."""
     recs = sorted(recs, key=lambda r: int(r["Dispatch_Id"]))
     if SEL["which"] == "pair":
-        return [int(r["Dispatch_Id"]) for r in recs if "relief_pair_kernel" in r["Kernel_Name"]]
+        one = [int(r["Dispatch_Id"]) for r in recs if "relief_pair1_kernel" in r["Kernel_Name"]]
+        SEL["pair_one"] = bool(one)
+        return one or [int(r["Dispatch_Id"]) for r in recs if "relief_pair_kernel" in r["Kernel_Name"]]
     if SEL["which"] == "multi":
         # multi_step_kernel<T, false> (the fast launch; the finish launch <T, true> only reads park[]
         # on flat), or the single inline launch <T, true> under BB_MULTI_PARK=0, or relief_multi_kernel
@@ -78,7 +80,7 @@ def counters(p, names, last):
         d = per.setdefault(int(r["Dispatch_Id"]), {})
         d[r["Counter_Name"]] = d.get(r["Counter_Name"], 0.0) + float(r["Counter_Value"])
     ids = sorted(per)
-    if SEL["which"] == "pair":  # one launch = its two relief_pair_kernel dispatches (full, then fast)
+    if SEL["which"] == "pair" and not SEL.get("pair_one"):  # one launch = its two relief_pair_kernel dispatches
         grp = [ids[i:i + 2] for i in range(0, len(ids) - 1, 2)][-last:]
         return {n: sum(sum(per[i].get(n, 0.0) for i in g) for g in grp) / len(grp) for n in names}, len(grp)
     ids = ids[-last:]
@@ -103,7 +105,7 @@ def main():
     keep = set(select_ids(allr))
     tr = [r for r in allr if int(r["Dispatch_Id"]) in keep]
     tr.sort(key=lambda r: int(r["Start_Timestamp"]))
-    if a.kernel == "pair":  # a launch: first start to last end of its two dispatches
+    if a.kernel == "pair" and not SEL.get("pair_one"):  # a launch: first start to last end of its two dispatches
         tr.sort(key=lambda r: int(r["Dispatch_Id"]))
         grp = [tr[i:i + 2] for i in range(0, len(tr) - 1, 2)][-a.timed:]
         timed = [g[0] for g in grp]
