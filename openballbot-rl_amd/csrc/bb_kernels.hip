@@ -1690,7 +1690,7 @@ struct bb_handle {
   int pair_cap = 0;             // one-wave workgroups resident on the chip (4 per CU)
   int pair_seg = 16;            // steps a team holds an env before requeueing it (BB_PAIR_SEG)
   int pair_adapt = 1;           // split the workgroups by the last launch's work (BB_PAIR_ADAPT=0: keep the first split)
-  int pair_one = 0;             // the pair as one launch (BB_PAIR_ONE=1): one dispatch, profilable per dispatch
+  int pair_one = 1;             // the pair as one launch (BB_PAIR_ONE=0: two concurrent launches on two streams)
   int pair_solo = 0;            // solo waves for heavy envs' full steps (BB_PAIR_SOLO; <= pair_cap / 8)
   int pair_heavy_pct = 150;     // heavy: last launch's cycles above this % of the mean env's (BB_PAIR_HEAVY)
   unsigned long long pair_budget = 0;  // wall-clock ticks a pair launch may wait for work (20 s)
