@@ -173,7 +173,7 @@ def main() -> None:
                     help="all envs on one terrain seed generator np_random(1000) instead of np_random(1000 + env id)")
     ap.add_argument("--graph", action="store_true",
                     help="replay the step as one HIP graph (kernel_ms is then timed on eager steps after the run)")
-    ap.add_argument("--multi-step", type=int, default=256,
+    ap.add_argument("--multi-step", type=int, default=512,
                     help="M steps per launch (bb_step_multi: the benchmark's random actions are known in advance, so "
                          "each env runs its M steps back to back, bit-identical to M bb_step calls); 0: one bb_step "
                          "launch per step.  With M > 0 the line also reports the per-launch form under 'per_step'")
@@ -181,6 +181,8 @@ def main() -> None:
                     help="steps of random actions resident in HBM ([P][n][3], reused cyclically); a launch never "
                          "crosses the pool's end")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-per-step", action="store_true",
+                    help="skip the one-launch-per-step comparison run (profiler counter passes)")
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
     ap.add_argument("--traffic-json", default=str(ROOT / "profiles" / "traffic.json"))
     args = ap.parse_args()
@@ -301,7 +303,7 @@ def main() -> None:
                                                                                        ("p50", 50), ("p90", 90))}
         pair["corr_cycles_finish"] = float(np.corrcoef(c, f)[0, 1])
     per_step = None
-    if M:  # the same steps with one bb_step launch per step (what a closed-loop rollout uses)
+    if M and not args.no_per_step:  # the same steps with one bb_step launch per step (what a closed-loop rollout uses)
         run(args.warmup, 0)
         per_step = timed(0)
     stats = env.stats()

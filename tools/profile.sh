@@ -20,7 +20,7 @@ MULTI=${MULTI:-0}
 B="bench.py --precision $PREC --terrain $TERRAIN --no-cpu-baseline --multi-step $MULTI"
 # PMC passes: a few launches of the timed shape (multi: whole 64-step launches only)
 S="--steps 20 --warmup 300"
-if [ "$MULTI" != "0" ]; then OUT=${OUT}_multi$MULTI; mkdir -p $OUT; S="--steps $((2 * MULTI)) --burn-in $((6 * MULTI)) --warmup $((4 * MULTI))"; fi
+if [ "$MULTI" != "0" ]; then OUT=${OUT}_multi$MULTI; mkdir -p $OUT; S="--steps $((2 * MULTI)) --burn-in $((2 * MULTI)) --warmup $((2 * MULTI)) --no-per-step"; fi
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/trace -o run -- \
   python3 $B --steps 512 --warmup 256 > $OUT/bench_trace.json || exit $?
 timeout -s KILL 120 rocprofv3 --pmc FETCH_SIZE GRBM_GUI_ACTIVE --output-format csv -d $OUT/fetch -o run -- \
