@@ -112,8 +112,10 @@ ABI_VERSION = 16  # include/ballbot_mi355x.h BB_ABI_VERSION
 _lib = None
 
 
-HIP_SOURCES = ("bb_kernels.hip", "bb_terrain.hip", "bb_rollout.hip", "bb_render.hip", "bb_ppo.hip", "bb_mlp.hip",
-               "bb_encoder.hip")
+HIP_SOURCES = ("bb_kernels.hip", "bb_pair.hip", "bb_terrain.hip", "bb_rollout.hip", "bb_render.hip", "bb_ppo.hip",
+               "bb_mlp.hip", "bb_encoder.hip")
+# per-source flags: the relief pair's unit without MachineLICM (bb_kernels.hip: bb_pair_launch_tu)
+SOURCE_FLAGS = {"bb_pair.hip": ["-mllvm", "-disable-machine-licm"]}
 
 
 def build(force: bool = False, verbose: bool = False) -> Path:
@@ -131,7 +133,7 @@ def build(force: bool = False, verbose: bool = False) -> Path:
     jobs = []
     for f in HIP_SOURCES:
         obj = obj_dir / (f[:-4] + ".o")
-        jobs.append((["hipcc", *flags, "-c", "-o", str(obj), str(CSRC / f)], obj))
+        jobs.append((["hipcc", *flags, *SOURCE_FLAGS.get(f, []), "-c", "-o", str(obj), str(CSRC / f)], obj))
     if verbose:
         for cmd, _ in jobs:
             print(" ".join(cmd))

@@ -43,7 +43,11 @@
 using namespace bb;
 
 #ifdef BB_PHASE_CLOCKS
+#ifdef BB_PAIR_TU
+namespace bb { static __device__ unsigned long long bb_phase_cycles[100]; }  // (not read back)
+#else
 namespace bb { __device__ unsigned long long bb_phase_cycles[100]; }
+#endif
 #endif
 
 namespace {
@@ -1709,8 +1713,8 @@ struct bb_handle {
 };
 
 template <typename T> const ModelT<T>& model_of(const bb_handle* h);
-template <> const ModelT<float>& model_of<float>(const bb_handle* h) { return h->mf; }
-template <> const ModelT<double>& model_of<double>(const bb_handle* h) { return h->md; }
+template <> inline const ModelT<float>& model_of<float>(const bb_handle* h) { return h->mf; }
+template <> inline const ModelT<double>& model_of<double>(const bb_handle* h) { return h->md; }
 
 namespace {
 // init height offset (ballbot_env.py:546-563), incl. cell_size = size/nrows
@@ -1857,6 +1861,36 @@ int launch_pair(bb_handle* h, const float* a, int K, float* o, float* r, uint8_t
   return 0;
 }
 
+}  // namespace
+
+// The relief pair's kernels and their launch are compiled a second time in
+// their own translation unit, bb_pair.hip (this file with BB_PAIR_TU), with
+// -mllvm -disable-machine-licm: in the persistent loop MachineLICM hoists the
+// ocml atan2/acos/sin/cos polynomial constants out of the loop and then
+// spills them, and every call reloads ~20 of them one dependent scratch load
+// at a time (448 B of scratch per lane; 16 B without the hoisting).  The
+// other kernels keep the default (flat's multi-step kernel is 2% slower
+// without it).  Both units compile the same source, so the structures agree.
+extern "C" int bb_pair_launch_tu(bb_handle* h, int fp64, const float* a, int K, float* o, float* r, uint8_t* dn,
+                                 float* t, float* p2, int ar, hipStream_t s, const int* gate);
+#ifdef BB_PAIR_TU
+extern "C" int bb_pair_launch_tu(bb_handle* h, int fp64, const float* a, int K, float* o, float* r, uint8_t* dn,
+                                 float* t, float* p2, int ar, hipStream_t s, const int* gate) {
+  return fp64 ? launch_pair<double>(h, a, K, o, r, dn, t, p2, ar, s, gate)
+              : launch_pair<float>(h, a, K, o, r, dn, t, p2, ar, s, gate);
+}
+#endif
+
+namespace {
+
+template <typename T>
+int pair_entry(bb_handle* h, const float* a, int K, float* o, float* r, uint8_t* dn, float* t, float* p2, int ar,
+               hipStream_t s, const int* gate) {
+  if (bb_pair_launch_tu(h, sizeof(T) == 8, a, K, o, r, dn, t, p2, ar, s, gate))
+    return fail("bb_step_multi: relief pair launch failed");
+  return 0;
+}
+
 template <typename T>
 int launch_multi(bb_handle* h, const float* a, int K, float* o, float* r, uint8_t* dn, float* t, float* p2, int ar,
                  hipStream_t s) {
@@ -1876,7 +1910,7 @@ int launch_multi(bb_handle* h, const float* a, int K, float* o, float* r, uint8_
     hipLaunchKernelGGL((multi_step_kernel<T, true>), dim3(blocks), dim3(WAVE), mlb, s, model_of<T>(h), h->cfg, h->d,
                        a, K, o, r, dn, t, p2, ar, h->team, epw, h->d.park, gate);
     if (h->pair) {
-      if (launch_pair<T>(h, a, K, o, r, dn, t, p2, ar, s, gate)) return -1;
+      if (pair_entry<T>(h, a, K, o, r, dn, t, p2, ar, s, gate)) return -1;
     } else {
       const Dev dq = balanced_dev(h, s);
       hipLaunchKernelGGL((relief_multi_kernel<T, false>), dim3((h->n + QENV - 1) / QENV), dim3(64 * QW),
@@ -1887,7 +1921,7 @@ int launch_multi(bb_handle* h, const float* a, int K, float* o, float* r, uint8_
     hipLaunchKernelGGL(route_decide_kernel, dim3(1), dim3(64), 0, s, h->d.slow_count, 1);
   } else if (route == 0 && h->team == 16 && h->multi_queue) {  // relief banks: the work queue
     if (h->pair) {
-      if (launch_pair<T>(h, a, K, o, r, dn, t, p2, ar, s, (const int*)nullptr)) return -1;
+      if (pair_entry<T>(h, a, K, o, r, dn, t, p2, ar, s, (const int*)nullptr)) return -1;
     } else {
       const Dev dq = balanced_dev(h, s);
       hipLaunchKernelGGL((relief_multi_kernel<T, false>), dim3((h->n + QENV - 1) / QENV), dim3(64 * QW),
@@ -1916,6 +1950,7 @@ int launch_multi(bb_handle* h, const float* a, int K, float* o, float* r, uint8_
 }
 }  // namespace
 
+#ifndef BB_PAIR_TU
 extern "C" {
 
 int bb_abi_version(void) { return BB_ABI_VERSION; }
@@ -2747,3 +2782,4 @@ int bb_get_offsets(bb_handle* h, float* out) {
 }
 
 }  // extern "C"
+#endif  // BB_PAIR_TU

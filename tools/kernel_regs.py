@@ -33,8 +33,13 @@ def demangle(names):
 
 def kernels_of(src: Path, tmp: Path) -> list[dict]:
     co = tmp / (src.stem + ".co")
+    import sys
+    sys.path.insert(0, str(ROOT / "openballbot-rl_amd"))
+    from ballbot_gym._native import SOURCE_FLAGS
+
     subprocess.run(["hipcc", "-O3", "-std=c++17", "--offload-arch=gfx950", "--cuda-device-only",
-                    "--no-gpu-bundle-output", "-c", str(src), "-o", str(co)], check=True)
+                    "--no-gpu-bundle-output", *SOURCE_FLAGS.get(src.name, []), "-c", str(src), "-o", str(co)],
+                   check=True)
     notes = subprocess.run([READELF, "--notes", str(co)], check=True, capture_output=True, text=True).stdout
     out, cur, col = [], None, -1
     for line in notes.splitlines():

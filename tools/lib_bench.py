@@ -21,11 +21,17 @@ def build(name, flags):
     """tools/_build/libbb_<name>.so from csrc/bb_kernels.hip with extra flags (python tools/lib_bench.py --build-only)."""
     out = ROOT / "tools" / "_build" / f"libbb_{name}.so"
     out.parent.mkdir(parents=True, exist_ok=True)
-    cmd = ["hipcc", "--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC", "-shared", *flags, "-o", str(out)] + [
-        str(ROOT / "openballbot-rl_amd" / "csrc" / f)
-        for f in ("bb_kernels.hip", "bb_terrain.hip", "bb_rollout.hip", "bb_render.hip", "bb_ppo.hip", "bb_mlp.hip",
-                  "bb_encoder.hip")]
-    subprocess.run(cmd, check=True)
+    from ballbot_gym import _native
+
+    # one object per source with the product's per-source flags, then one link
+    objs = []
+    for f in _native.HIP_SOURCES:
+        o = out.parent / f"{name}_{f[:-4]}.o"
+        subprocess.run(["hipcc", "--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC", *flags,
+                        *_native.SOURCE_FLAGS.get(f, []), "-c", "-o", str(o),
+                        str(ROOT / "openballbot-rl_amd" / "csrc" / f)], check=True)
+        objs.append(str(o))
+    subprocess.run(["hipcc", "--offload-arch=gfx950", "-shared", "-fPIC", "-o", str(out), *objs], check=True)
     return out
 
 

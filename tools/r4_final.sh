@@ -27,3 +27,6 @@ line $O/bench_flat_fp32.json flat_fp32
 timeout -k 10 300 python -u bench.py --terrain hills --no-cpu-baseline $T > $O/bench_hills.json 2> $O/bench_hills.err || exit $?
 line $O/bench_hills.json hills
 echo FINAL_DONE
+# hills at 256 steps per launch (the adaptive route's parked form needs a launch without full steps)
+timeout -k 10 300 python -u bench.py --terrain hills --multi-step 256 --no-cpu-baseline $T > $O/bench_hills256.json 2> $O/bench_hills256.err || exit $?
+line $O/bench_hills256.json hills256
