@@ -107,9 +107,11 @@ struct Dev {
   int* pred_envs;             // envs predicted to need base-tree contacts (full kernel, concurrent)
   uint8_t* pred_mark;
   void* body_spill;           // T[n][MAXB - MAXB_LDS][NBF]: base-tree contacts past the LDS slots
+  void* hand;                 // relief pair: T[n][HAND] env state between holds (qpos, qvel, warm, step), per env
   int* perm;                  // relief_multi_kernel: env of each workgroup slot (balance_kernel), NULL: identity
-  unsigned long long* ring;   // relief_pair_kernel: [2][ring_len] ticket rings of envs ready for a fast / full step
-  int ring_len;               // n + the resident teams: an entry is never overwritten before it is taken
+  unsigned long long* ring;   // relief pair: [NRINGS][ring_len] ticket rings of envs ready for a step (pair_ring)
+  int* rctr;                  // relief pair: [NRINGS][2] ring head / tail
+  int ring_len;               // an XCD's envs + its resident teams: an entry is never overwritten before it is taken
   unsigned long long* pair_env;  // relief_pair_kernel, last launch, per env: [n] cycles stepped, [n] wall tick of its last step
   unsigned long long* pair_busy;  // relief_pair_kernel, last launch: [2] team-cycles stepping, [2] team lifetimes
                                   // in shader cycles, [2] in wall-clock ticks (fast, full)
@@ -1271,11 +1273,26 @@ __global__ __launch_bounds__(64 * QW) void relief_multi_kernel(ModelT<T> mg, Env
 constexpr int SC_RHEAD = 16, SC_RTAIL = 18, SC_DONE = 20, SC_ERR = 21, SC_ACTIVE = 22, SC_IDLE = 24;
 // diagnostics of the last launch (bb_pair_counters): claims [2], completed steps [2], fast-path hand-overs
 constexpr int SC_CLAIMS = 32, SC_STEPS = 34, SC_PARKED = 36;
+// Between two holds within a launch an env's state lives in d.hand, one contiguous record per env
+// (3 cache lines at fp64), written and read by the team's 16 lanes: in the SoA arrays the same
+// 48 values sit in 48 lines, and each write-through (sc1) store of one value is its own memory
+// request.  park[e] carries PARK_HAND once the record holds the env's state; the SoA arrays
+// hold it at the launch's start and get it back when the env's K steps are done.
+constexpr int HAND = NQ + 2 * NV + 1, PARK_HAND = 1 << 30;
 // solo waves: ring 2 (the heavy envs' full steps) counters, the solo workgroup count, the heavy
 // marks of this launch (reset by pair_rings_kernel, which keeps the count in SC_HEAVY_LAST)
-constexpr int SC_RHEAD2 = 40, SC_RTAIL2 = 41, SC_SOLO = 42, SC_HEAVY = 43, SC_HEAVY_LAST = 44, NRING = 3;
-__device__ __forceinline__ int ring_head_slot(int r) { return r < 2 ? SC_RHEAD + r : SC_RHEAD2; }
-__device__ __forceinline__ int ring_tail_slot(int r) { return r < 2 ? SC_RTAIL + r : SC_RTAIL2; }
+constexpr int SC_SOLO = 42, SC_HEAVY = 43, SC_HEAVY_LAST = 44;
+// Rings per XCD: the fast and full rings are sharded 8 ways by env block, env e belonging to
+// XCD label (e >> 5) & 7 (32 envs: one 128-B line of a [K][n] float output), and a team takes
+// envs from the rings of its workgroup's label, blockIdx & 7 -- the XCD the dispatcher deals
+// that workgroup to.  So an env's steps run on one XCD's L2: the partial output lines of
+// neighbouring envs merge there instead of being written back piecemeal from eight L2s, and
+// its terrain cells stay cached.  The label is only a placement hint: any mapping is correct,
+// since every label has fast and full workgroups (each kind keeps >= pair_cap / 8 >= 8).  The
+// heavy envs' solo ring (kind 2) is one ring: the solo workgroups may cover fewer than 8 labels.
+constexpr int NXCD = 8, NRINGS = 2 * NXCD + 1;
+__device__ __forceinline__ int env_xcd(int e) { return (e >> 5) & (NXCD - 1); }
+__device__ __forceinline__ int pair_ring(int kind, int x) { return kind < 2 ? kind * NXCD + x : 2 * NXCD; }
 
 __device__ __forceinline__ int ld_agent(const int* p) {
   return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -1292,19 +1309,17 @@ __device__ __forceinline__ int ld_agent(const int* p) {
 __device__ __forceinline__ unsigned long long ring_entry(int ticket, int e) {
   return (static_cast<unsigned long long>(unsigned(ticket)) << 32) | unsigned(e);
 }
-__device__ __forceinline__ int ring_ticket(const Dev& d, int kind) {
-  return atomicAdd(d.slow_count + ring_head_slot(kind), 1);
-}
+__device__ __forceinline__ int ring_ticket(const Dev& d, int r) { return atomicAdd(d.rctr + 2 * r, 1); }
 // the env of `ticket` in ring `kind`, or -1 while it has not been appended
-__device__ __forceinline__ int ring_look(const Dev& d, int kind, int ticket) {
-  const unsigned long long v =
-      ld_coh(d.ring + size_t(kind) * d.ring_len + (unsigned(ticket) % unsigned(d.ring_len)));
+__device__ __forceinline__ int ring_look(const Dev& d, int r, int ticket) {
+  const unsigned long long v = ld_coh(d.ring + size_t(r) * d.ring_len + (unsigned(ticket) % unsigned(d.ring_len)));
   return unsigned(v >> 32) == unsigned(ticket) ? int(unsigned(v)) : -1;
 }
 // append env e to ring `kind` (lead lane; the env's state is stored and released)
 __device__ __forceinline__ void ring_push(const Dev& d, int kind, int e) {
-  const int t = atomicAdd(d.slow_count + ring_tail_slot(kind), 1);
-  st_coh(d.ring + size_t(kind) * d.ring_len + (unsigned(t) % unsigned(d.ring_len)), ring_entry(t, e));
+  const int r = pair_ring(kind, env_xcd(e));
+  const int t = atomicAdd(d.rctr + 2 * r + 1, 1);
+  st_coh(d.ring + size_t(r) * d.ring_len + (unsigned(t) % unsigned(d.ring_len)), ring_entry(t, e));
 }
 
 // one team loop of the relief pair (FULL: the full launch's; wg: this workgroup's index among
@@ -1334,6 +1349,7 @@ __device__ __forceinline__ void pair_loop(const ModelT<T>& mg, const EnvCfg& cfg
   // marked heavy (ring 2), so a heavy env's step never waits for wave-mates' divergent work
   const bool solo = FULL && wg < sc[SC_SOLO];
   const int rkind = solo ? 2 : kind;
+  const int myring = pair_ring(rkind, int(blockIdx.x) & (NXCD - 1));  // this team's ring (see env_xcd)
   const unsigned long long t0 = wall_clock64(), c_start = clock64();
   int e = -1, k = 0, tid = 0, step = 0, held = 0, ticket = -1;  // ticket: the lead's, -1 when none
   unsigned idle = 0;
@@ -1349,8 +1365,8 @@ __device__ __forceinline__ void pair_loop(const ModelT<T>& mg, const EnvCfg& cfg
         if (ld_agent(sc + SC_DONE) >= n || ld_agent(sc + SC_ERR) || (solo && team > 0)) {
           got = -2;
         } else {
-          if (ticket < 0) ticket = ring_ticket(d, rkind);
-          got = ring_look(d, rkind, ticket);
+          if (ticket < 0) ticket = ring_ticket(d, myring);
+          got = ring_look(d, myring, ticket);
           if (got >= 0) ticket = -1;
           else if (wall_clock64() - t0 > budget) {
             if (atomicExch(sc + SC_ERR, 1) == 0) atomicAdd(&d.stats[7], 1ull);
@@ -1365,8 +1381,16 @@ __device__ __forceinline__ void pair_loop(const ModelT<T>& mg, const EnvCfg& cfg
         // acquire: the releasing team's device-coherent stores, read device-coherently
         // (their addresses depend on the popped id, so they issue after it)
         e = got;
-        load_state<T, true>(d, e, W.qn, W.vn, W.wn, step);
-        k = ld_coh(d.park + e);
+        const int pk = ld_coh(d.park + e);
+        k = pk & (PARK_HAND - 1);
+        if (pk & PARK_HAND) {  // the record (qn, vn, wn are contiguous in EnvWork)
+          const T* hr = reinterpret_cast<const T*>(d.hand) + size_t(e) * HAND;
+          for (int i = tm.tl; i < HAND - 1; i += TEAM) W.qn[i] = ld_coh(hr + i);
+          step = int(ld_coh(hr + HAND - 1));
+          team_sync();
+        } else {
+          load_state<T, true>(d, e, W.qn, W.vn, W.wn, step);
+        }
         tid = ld_coh(d.terrain + e);
         held = 0;
         held_busy = 0;
@@ -1405,9 +1429,14 @@ __device__ __forceinline__ void pair_loop(const ModelT<T>& mg, const EnvCfg& cfg
       held_busy += dc;
       if (k >= K || next != kind || held >= seg) {  // release the env (team-uniform)
         team_sync();
+        if (k < K) {  // the record, spread over the team's lanes
+          T* hr = reinterpret_cast<T*>(d.hand) + size_t(e) * HAND;
+          for (int i = tm.tl; i < HAND - 1; i += TEAM) st_coh(hr + i, W.qn[i]);
+          if (lead) st_coh(hr + HAND - 1, T(step));
+        }
         if (lead) {
-          store_state<T, true>(d, e, W.qn, W.vn, W.wn, step);
-          st_coh(d.park + e, k);
+          if (k >= K) store_state<T, true>(d, e, W.qn, W.vn, W.wn, step);
+          st_coh(d.park + e, k < K ? k | PARK_HAND : k);
           st_coh(d.pair_env + e, ld_coh(d.pair_env + e) + held_busy);
           if (k >= K) st_coh(d.pair_env + n + e, static_cast<unsigned long long>(wall_clock64()));
           stores_done();  // release: the state (and a reset's draw) before the ring entry
@@ -1509,47 +1538,29 @@ __global__ __launch_bounds__(64) void pair_init_kernel(ModelT<T> mg, Dev d, cons
     d.pred_mark[e] = uint8_t((full ? 1 : 0) | (heavy ? 2 : 0));
     d.park[e] = 0;
     d.pair_env[e] = 0;
+    ring_push(d, full ? (heavy ? 2 : 1) : 0, e);  // the rings were cleared by pair_clear_kernel
   }
 }
 
-// after pair_init_kernel: the rings from the marks (stable, in env order; one
-// block, as split_kernel), their counters, and the empty slots
-__global__ __launch_bounds__(1024) void pair_rings_kernel(Dev d, const int* __restrict__ gate) {
+// before pair_init_kernel: every ring slot empty (no ticket's entry) and the ring counters at 0
+__global__ __launch_bounds__(256) void pair_clear_kernel(Dev d, const int* __restrict__ gate) {
   if (gate && *gate == ROUTE_PARK) return;
-  __shared__ int sc3[NRING][1024];
-  const int t = threadIdx.x, per = (d.n + 1023) / 1024, b = t * per, e_ = min(d.n, b + per);
-  auto ring_of = [&](int e) { const int mk = d.pred_mark[e]; return (mk & 1) ? ((mk & 2) ? 2 : 1) : 0; };
-  int cnt[NRING] = {0, 0, 0};
-  for (int e = b; e < e_; e++) cnt[ring_of(e)]++;
-  for (int r = 0; r < NRING; r++) sc3[r][t] = cnt[r];
-  __syncthreads();
-  for (int off = 1; off < 1024; off <<= 1) {
-    int add[NRING];
-    for (int r = 0; r < NRING; r++) add[r] = t >= off ? sc3[r][t - off] : 0;
-    __syncthreads();
-    for (int r = 0; r < NRING; r++) sc3[r][t] += add[r];
-    __syncthreads();
-  }
-  int pos[NRING];
-  for (int r = 0; r < NRING; r++) pos[r] = sc3[r][t] - cnt[r];
-  for (int e = b; e < e_; e++) {
-    const int r = ring_of(e);
-    d.ring[size_t(r) * d.ring_len + pos[r]] = ring_entry(pos[r], e);
-    pos[r]++;
-  }
-  __syncthreads();
-  for (int r = 0; r < NRING; r++)
-    for (int i = sc3[r][1023] + t; i < d.ring_len; i += 1024) d.ring[size_t(r) * d.ring_len + i] = ~0ull;  // no ticket's entry
-  if (t == 0) {
-    int* sc = d.slow_count;
-    for (int r = 0; r < NRING; r++) { sc[ring_head_slot(r)] = 0; sc[ring_tail_slot(r)] = sc3[r][1023]; }
-    sc[SC_DONE] = 0; sc[SC_ERR] = 0;
-    sc[SC_IDLE] = 0; sc[SC_IDLE + 1] = 0;
-    sc[SC_CLAIMS] = 0; sc[SC_CLAIMS + 1] = 0; sc[SC_STEPS] = 0; sc[SC_STEPS + 1] = 0; sc[SC_PARKED] = 0;
-    sc[SC_HEAVY_LAST] = sc[SC_HEAVY];
-    sc[SC_HEAVY] = 0;
-    for (int i = 0; i < 6; i++) d.pair_busy[i] = 0;
-  }
+  const size_t tot = size_t(NRINGS) * d.ring_len;
+  for (size_t i = size_t(blockIdx.x) * blockDim.x + threadIdx.x; i < tot; i += size_t(gridDim.x) * blockDim.x)
+    d.ring[i] = ~0ull;
+  if (blockIdx.x == 0 && threadIdx.x < 2 * NRINGS) d.rctr[threadIdx.x] = 0;
+}
+
+// after pair_init_kernel (which filled the rings): the launch's counters
+__global__ void pair_rings_kernel(Dev d, const int* __restrict__ gate) {
+  if ((gate && *gate == ROUTE_PARK) || threadIdx.x != 0) return;
+  int* sc = d.slow_count;
+  sc[SC_DONE] = 0; sc[SC_ERR] = 0;
+  sc[SC_IDLE] = 0; sc[SC_IDLE + 1] = 0;
+  sc[SC_CLAIMS] = 0; sc[SC_CLAIMS + 1] = 0; sc[SC_STEPS] = 0; sc[SC_STEPS + 1] = 0; sc[SC_PARKED] = 0;
+  sc[SC_HEAVY_LAST] = sc[SC_HEAVY];
+  sc[SC_HEAVY] = 0;
+  for (int i = 0; i < 6; i++) d.pair_busy[i] = 0;
 }
 
 // after the pair: the next launch splits the resident workgroups in proportion
@@ -1841,9 +1852,10 @@ int launch_pair(bb_handle* h, const float* a, int K, float* o, float* r, uint8_t
                 hipStream_t s, const int* gate) {
   const ModelT<T>& m = model_of<T>(h);
   const size_t plb = multi_lds_bytes<T>(4);
+  hipLaunchKernelGGL(pair_clear_kernel, dim3(64), dim3(256), 0, s, h->d, gate);
   hipLaunchKernelGGL(pair_init_kernel<T>, dim3((h->n + WAVE / 16 - 1) / (WAVE / 16)), dim3(WAVE), 0, s, m, h->d, gate,
                      h->pair_heavy_pct);
-  hipLaunchKernelGGL(pair_rings_kernel, dim3(1), dim3(1024), 0, s, h->d, gate);
+  hipLaunchKernelGGL(pair_rings_kernel, dim3(1), dim3(64), 0, s, h->d, gate);
   if (h->pair_one) {
     hipLaunchKernelGGL(relief_pair1_kernel<T>, dim3(h->pair_cap), dim3(WAVE), plb, s, m, h->cfg, h->d, a, K, o, r, dn, t,
                        p2, ar, h->pair_seg, h->pair_budget, gate);
@@ -2100,9 +2112,13 @@ int bb_create(int n_envs, int device, const bb_params* p, bb_handle** out) {
   HIPCHK(hipMalloc((void**)&d.pred_envs, sizeof(int) * n));
   HIPCHK(hipMalloc((void**)&d.pred_mark, n));
   HIPCHK(hipMalloc(&d.body_spill, es * (MAXB - MAXB_LDS) * NBF * size_t(n)));
+  HIPCHK(hipMalloc(&d.hand, es * HAND * size_t(n)));
   HIPCHK(hipMalloc((void**)&d.perm, sizeof(int) * n));
-  d.ring_len = n + WAVE / TEAM * h->pair_cap;
-  HIPCHK(hipMalloc((void**)&d.ring, sizeof(unsigned long long) * NRING * size_t(d.ring_len)));
+  // per ring: an XCD label's envs (32-env blocks) + its resident teams, with margin (the solo ring
+  // holds at most SC_SOLO envs)
+  d.ring_len = (n + 255) / 256 * 32 + WAVE / TEAM * ((h->pair_cap + NXCD - 1) / NXCD) + 64;
+  HIPCHK(hipMalloc((void**)&d.ring, sizeof(unsigned long long) * NRINGS * size_t(d.ring_len)));
+  HIPCHK(hipMalloc((void**)&d.rctr, sizeof(int) * 2 * NRINGS));
   HIPCHK(hipMalloc((void**)&d.pair_busy, sizeof(unsigned long long) * 6));
   HIPCHK(hipMalloc((void**)&d.pair_env, sizeof(unsigned long long) * 2 * size_t(n)));
   HIPCHK(hipMemset(d.pair_env, 0, sizeof(unsigned long long) * 2 * size_t(n)));
@@ -2181,7 +2197,7 @@ int bb_destroy(bb_handle* h) {
   (void)hipFree(h->bank); (void)hipFree(h->size_z); (void)hipFree(h->offset); (void)hipFree(h->hmax); (void)hipFree(h->d.stats);
   (void)hipFree(h->d.slow_list); (void)hipFree(h->d.slow_count); (void)hipFree(h->d.park);
   (void)hipFree(h->d.fast_envs); (void)hipFree(h->d.pred_envs); (void)hipFree(h->d.pred_mark);
-  (void)hipFree(h->d.body_spill); (void)hipFree(h->d.perm); (void)hipFree(h->d.cost); (void)hipFree(h->d.ring);
+  (void)hipFree(h->d.body_spill); (void)hipFree(h->d.hand); (void)hipFree(h->d.perm); (void)hipFree(h->d.cost); (void)hipFree(h->d.ring); (void)hipFree(h->d.rctr);
   (void)hipFree(h->d.pair_busy); (void)hipFree(h->d.pair_env);
   (void)hipFree(h->tstream); (void)hipFree(h->env_stream); (void)hipFree(h->rng); (void)hipFree(h->seed_slot);
   (void)hipFree(h->d.tseed);
