@@ -343,6 +343,16 @@ __device__ int solve16(const ModelT<T>& m, EnvWork<T>& W, int ng, int nb, T* a, 
                 "wheel f/C scratch needs wf and hg adjacent");
   T* const wCf = &W.u.hes.wf[0][0];
   const bool gsum = ng > 0;  // team-uniform
+#ifdef BB_HROW_REG
+  // this lane's row of the dense mass matrix, held in registers across the Newton
+  // iterations (W.H does not change during the solve) instead of re-read from LDS
+  T hM[NV];
+#pragma unroll
+  for (int k = 0; k < NV; k++) hM[k] = W.H[hidx(row, k)];
+#define BB_HROW(k) hM[k]
+#else
+#define BB_HROW(k) W.H[hidx(row, k)]
+#endif
   PH_DECL
   int it = 0;
   for (; it < m.maxiter; it++) {
@@ -553,7 +563,7 @@ __device__ int solve16(const ModelT<T>& m, EnvWork<T>& W, int ng, int nb, T* a, 
     // ---- (3) gradient, row i: (M a)_i - qfs_i - sum_w J_w[:,i]' f_w (+ ground)
     T h[NV];
 #pragma unroll
-    for (int k = 0; k < NV; k++) h[k] = W.H[hidx(row, k)];  // dense M row
+    for (int k = 0; k < NV; k++) h[k] = BB_HROW(k);  // dense M row
     T Ma = 0;
 #pragma unroll
     for (int k = 0; k < NV; k++) Ma += h[k] * a[k];
@@ -675,7 +685,7 @@ __device__ int solve16(const ModelT<T>& m, EnvWork<T>& W, int ng, int nb, T* a, 
     // ---- (6) exact line search
     T Ms = 0;
 #pragma unroll
-    for (int k = 0; k < NV; k++) Ms += W.H[hidx(row, k)] * s[k];
+    for (int k = 0; k < NV; k++) Ms += BB_HROW(k) * s[k];
     const T sMs = tsum(sown * Ms), gs = tsum(sown * mq);
     // this lane's first contact's term from its jar; later rounds rebuild theirs
     LsTerm<T> lt;
@@ -785,6 +795,7 @@ __device__ int solve16(const ModelT<T>& m, EnvWork<T>& W, int ng, int nb, T* a, 
     if (-m.scale * dcost < m.tol) { it++; break; }
   }
   PH(7)
+#undef BB_HROW
   if constexpr (BODY) {
     PH_FLUSH_BODY((Team{L, tl}))
   } else {
