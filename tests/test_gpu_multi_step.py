@@ -155,12 +155,13 @@ def _chunked_equal(a, b, pool, chunks, start=0):
 
 
 @pytest.mark.parametrize("terrain,route", [("flat", "1"), ("perlin", "0")])
-def test_headline_form_k256_and_driver_window(terrain, route, monkeypatch):
-    """The exact form bench.py times: a 256-slot action pool resident in HBM, a burn-in of
-    400 steps, 300 warm-up steps, then the timed 500 steps as two launches of 256 + 244
-    (bench.launch_chunks); and the driver's window, one 20-step launch after the burn-in.
-    Against one bb_step per step, bit for bit (flat: 4096 envs, configs[1]; perlin: 1024
-    envs on per-env generators over the whole seed space, route 0: the work queue)."""
+def test_headline_form_k512_and_driver_window(terrain, route, monkeypatch):
+    """The exact form bench.py times (its defaults: a 512-slot action pool resident in HBM,
+    512 steps per launch): a burn-in of 400 steps and 300 warm-up steps (launches of 512 +
+    188), then the timed 500 steps as one launch (bench.launch_chunks); and the driver's
+    window, one 20-step launch after the burn-in.  Against one bb_step per step, bit for bit
+    (flat: 4096 envs, configs[1]; perlin: 1024 envs on per-env generators over the whole
+    seed space, route 0: the relief pair)."""
     import sys
     from pathlib import Path
 
@@ -171,11 +172,11 @@ def test_headline_form_k256_and_driver_window(terrain, route, monkeypatch):
     kw = {} if terrain == "flat" else {"n_terrains": None}
     a, b = _pair(n, terrain, monkeypatch, route=route, **kw)
     g = torch.Generator(device="cuda:0").manual_seed(1234)
-    PS = 256
+    PS = M = 512
     pool = torch.rand(PS, n, 3, generator=g, device="cuda:0") * 2 - 1
-    assert bench.launch_chunks(500, 256, PS) == [256, 244]
-    j = _chunked_equal(a, b, pool, bench.launch_chunks(700, 256, PS))  # burn-in + warm-up
-    _chunked_equal(a, b, pool, bench.launch_chunks(500, 256, PS), start=0)  # the timed window
+    assert bench.launch_chunks(500, M, PS) == [500]
+    j = _chunked_equal(a, b, pool, bench.launch_chunks(700, M, PS))  # burn-in + warm-up
+    _chunked_equal(a, b, pool, bench.launch_chunks(500, M, PS), start=0)  # the timed window
     j = _chunked_equal(a, b, pool, [20], start=0)  # the driver's --steps 20 window, post burn-in
     for x, y in zip(a.get_state(), b.get_state()):
         np.testing.assert_array_equal(x, y)
@@ -184,6 +185,28 @@ def test_headline_form_k256_and_driver_window(terrain, route, monkeypatch):
     sa, sb = a.stats(), b.stats()
     assert sa == sb, (sa, sb)
     assert sa["resets"] > n // 2
+    a.close(), b.close()
+
+
+@pytest.mark.parametrize("variant", [{"BB_PAIR_ONE": "0"}, {"BB_PAIR_SOLO": "64", "BB_PAIR_HEAVY": "100"},
+                                     {"BB_PAIR_SEG": "4"}, {"BB_RELIEF_PAIR": "0"}],
+                         ids=["two-launches", "solo-waves", "seg4", "work-queue"])
+def test_relief_pair_forms_match(variant, monkeypatch):
+    """The relief pair's other forms: two concurrent launches instead of one, solo
+    waves for the heavy envs (envs above the mean cost of the last launch, from the second
+    launch on), hand-overs every 4 steps, and round 3's work queue.  Each is route 0 and must
+    equal one bb_step per step bit for bit, launch after launch."""
+    for k, v in variant.items():
+        monkeypatch.setenv(k, v)  # read by bb_create
+    n = 512
+    a, b = _pair(n, "perlin", monkeypatch, route="0", n_terrains=None, stream_seeds=[70 + i for i in range(n)],
+                 max_ep_steps=200)
+    g = torch.Generator(device="cuda:0").manual_seed(11)
+    actions = torch.rand(256, n, 3, generator=g, device="cuda:0") * 2 - 1
+    st = _compare_runs(a, b, actions, 32)
+    assert st["slow_path"] > 0 and st["pair_budget"] == 0
+    if "BB_PAIR_SOLO" in variant:
+        assert b.pair_counters()["heavy"] > 0  # the last launch marked heavy envs for the solo waves
     a.close(), b.close()
 
 
