@@ -556,8 +556,16 @@ __device__ __forceinline__ void counts_flush(const Dev& d, const unsigned* cnt) 
 // launch carries no full step, so it keeps the fast kernel's registers: the
 // full step inlined beside it costs 157-196 spilled VGPRs (scratch traffic on
 // every step, hand-over or not).  park == NULL: one launch, hand-overs inline.
+// variant builds (tools/lib_bench.py): tell the compiler a SIMD holds one wave of the kernel
+// (4096 envs fill the chip at one wave per SIMD whatever the registers), so that it schedules
+// for latency instead of an occupancy it cannot reach
+#ifdef BB_WPE1
+#define BB_WPE __attribute__((amdgpu_waves_per_eu(1, 1)))
+#else
+#define BB_WPE
+#endif
 template <typename T, bool HO>
-__global__ __launch_bounds__(64) void multi_step_kernel(ModelT<T> mg, EnvCfg cfg, Dev d, const float* __restrict__ act,
+__global__ BB_WPE __launch_bounds__(64) void multi_step_kernel(ModelT<T> mg, EnvCfg cfg, Dev d, const float* __restrict__ act,
                                                         int K, float* __restrict__ obs, float* __restrict__ rew,
                                                         uint8_t* __restrict__ done, float* __restrict__ tobs,
                                                         float* __restrict__ pos2d, int auto_reset, int L, int epw,
