@@ -1891,10 +1891,13 @@ int launch_pair(bb_handle* h, const float* a, int K, float* o, float* r, uint8_t
 // at a time (448 B of scratch per lane; 16 B without the hoisting).  The
 // other kernels keep the default (flat's multi-step kernel is 2% slower
 // without it).  Both units compile the same source, so the structures agree.
-extern "C" int bb_pair_launch_tu(bb_handle* h, int fp64, const float* a, int K, float* o, float* r, uint8_t* dn,
-                                 float* t, float* p2, int ar, hipStream_t s, const int* gate);
+// (internal to the library: hidden, not part of the C-ABI)
+extern "C" __attribute__((visibility("hidden"))) int bb_pair_launch_tu(bb_handle* h, int fp64, const float* a, int K,
+                                                                      float* o, float* r, uint8_t* dn, float* t,
+                                                                      float* p2, int ar, hipStream_t s,
+                                                                      const int* gate);
 #ifdef BB_PAIR_TU
-extern "C" int bb_pair_launch_tu(bb_handle* h, int fp64, const float* a, int K, float* o, float* r, uint8_t* dn,
+extern "C" __attribute__((visibility("hidden"))) int bb_pair_launch_tu(bb_handle* h, int fp64, const float* a, int K, float* o, float* r, uint8_t* dn,
                                  float* t, float* p2, int ar, hipStream_t s, const int* gate) {
   return fp64 ? launch_pair<double>(h, a, K, o, r, dn, t, p2, ar, s, gate)
               : launch_pair<float>(h, a, K, o, r, dn, t, p2, ar, s, gate);
