@@ -367,9 +367,12 @@ int bb_step(bb_handle* h, const float* actions_dev, float* obs_dev, float* rewar
  * without relief this is two launches on `stream`: the fast steps, with envs
  * whose step the fast path hands over parked at that step, then a finish
  * launch that resumes the parked envs (BB_MULTI_PARK=0 at bb_create: one
- * launch, hand-overs inline).  Relief banks: a work-queue launch, or after a
- * launch in which no env needed a full step the parked launches; a device flag
- * picks one per call (BB_MULTI_ADAPT=0: always the queue). */
+ * launch, hand-overs inline).  Relief banks: the relief pair -- one persistent
+ * launch whose workgroups run either the fast or the full step, envs handed
+ * between them through ticket rings per XCD label (BB_PAIR_ONE=0: two
+ * concurrent launches; BB_RELIEF_PAIR=0: round 3's work queue) -- or, after a
+ * launch in which no env needed a full step, the parked launches; a device flag
+ * picks one per call (BB_MULTI_ADAPT=0: always the pair).  DESIGN §6d, §6e. */
 int bb_step_multi(bb_handle* h, const float* actions_dev, int k_steps, float* obs_dev, float* reward_dev,
                   uint8_t* done_dev, float* terminal_obs_dev, float* pos2d_dev, int auto_reset, void* stream);
 

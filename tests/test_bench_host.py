@@ -38,6 +38,14 @@ def test_launch_chunks_cover_the_steps_within_the_pool(count, m, pool):
         j += k
 
 
+def test_launch_chunks_bench_defaults_time_one_launch():
+    """bench.py's defaults (512-slot action pool, 512 steps per launch): the 500 timed steps are
+    one launch; burn-in + warm-up (700 steps) are 512 + 188."""
+    assert bench.launch_chunks(500, 512, 512) == [500]
+    assert bench.launch_chunks(700, 512, 512) == [512, 188]
+    assert bench.launch_chunks(20, 512, 512) == [20]
+
+
 def test_launch_chunks_driver_window_is_one_launch():
     # the driver's --steps 20 --warmup 5: one 20-step launch
     assert bench.launch_chunks(20, 256, 256) == [20]
