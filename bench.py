@@ -43,6 +43,30 @@ def algorithmic_bytes(precision: str, steps_per_launch: float = 1, relief: bool 
     return per_launch / steps_per_launch + 12 + out + (196 if relief else 0)
 
 
+def profile_entry(path: Path, precision: str, terrain: str, envs: int, spl: float) -> dict:
+    """The rocprofv3 summary (profiles/traffic.json, written by tools/prof_summary.py) of exactly
+    this launch shape: precision, terrain, envs per GPU and steps per launch must all match, else
+    {} -- a 512-step profile says nothing about a 20-step launch."""
+    try:
+        tab = json.loads(path.read_text())
+    except Exception:
+        return {}
+    for e in tab.values():
+        if (e.get("precision") == precision and e.get("terrain", "flat") == terrain and e.get("envs") == envs
+                and abs(float(e.get("steps_per_launch", -1)) - spl) < 1e-9):
+            return e
+    return {}
+
+
+def committed_flops(terrain: str):
+    """The timed-mix FLOP count committed for this terrain (profiles/flops.json, tools/flops.py)."""
+    try:
+        e = json.loads((ROOT / "profiles" / "flops.json").read_text()).get(terrain)
+        return dict(e, source="profiles/flops.json") if e else None
+    except Exception:
+        return None
+
+
 def launch_chunks(count: int, m: int, pool_slots: int) -> list:
     """bb_step_multi launch sizes for `count` steps from action-pool slot 0 on: up
     to m steps each, none crossing the end of the pool (actions are reused
@@ -54,9 +78,25 @@ def launch_chunks(count: int, m: int, pool_slots: int) -> list:
     return out
 
 
-def cpu_baseline(seconds: float = 12.0, threads: int = 1) -> dict:
+def bench_fields(env, terrain: str, n_fields: int = 4):
+    """The terrains a CPU leg samples for this line's workload: flat, or the first-drawn
+    terrains of the first n_fields per-env generators of the line's bank (host copies of the
+    bank slots, with their vertical scale) -> ([(hfield f32, size_z)], description)."""
+    from ballbot_gym.envs.config import stream_draws
+
+    plan = env.terrain_plan
+    if plan.stream_seeds is None:
+        return [(env.hfield(0), float(plan.size_z))], f"the '{terrain}' terrain"
+    firsts = [int(stream_draws(s, 1)[0]) for s in list(dict.fromkeys(plan.stream_seeds))[:n_fields]]
+    slots = list(dict.fromkeys(max(plan.slot_of(x), 0) for x in firsts))
+    return ([(env.hfield(sl), float(plan.size_z)) for sl in slots],
+            f"{len(slots)} terrain(s) of the '{terrain}' bank (seeds {[int(plan.seeds[sl]) for sl in slots]})")
+
+
+def cpu_baseline(seconds: float = 12.0, threads: int = 1, fields=None, fields_desc: str = "flat") -> dict:
     """The fp64 oracle (a port of the reference step semantics, not MuJoCo) on
-    `threads` host cores (one env per OpenMP thread), random actions, flat terrain."""
+    `threads` host cores (one env per OpenMP thread), random actions, on the line's
+    terrain: a group of envs per sampled terrain (bench_fields), auto-reset onto it."""
     import numpy as np
 
     import oracle_lib as O
@@ -64,19 +104,23 @@ def cpu_baseline(seconds: float = 12.0, threads: int = 1) -> dict:
     O.build()
     n = 32 * threads
     cfg = O.default_cfg()
-    hf = O.flat_hfield()
-    off = O.init_offset(hf)
-    q = np.zeros((n, 17)); v = np.zeros((n, 15)); w = np.zeros((n, 15))
-    for e in range(n):
-        q[e], v[e], w[e] = O.reset_state(off)
-    steps = np.zeros(n, np.int32)
+    if fields is None:
+        fields = [(O.flat_hfield(), 2.0)]
+    groups = []
+    for hf, size_z in fields:
+        off = O.init_offset(hf, size_z)
+        q = np.zeros((n, 17)); v = np.zeros((n, 15)); w = np.zeros((n, 15))
+        for e in range(n):
+            q[e], v[e], w[e] = O.reset_state(off)
+        groups.append((np.ascontiguousarray(hf, np.float32), size_z, off, q, v, w, np.zeros(n, np.int32)))
     rng = np.random.default_rng(0)
     done_steps = 0
     t0 = time.perf_counter()
     while time.perf_counter() - t0 < seconds:
-        a = rng.uniform(-1, 1, (n, 3)).astype(np.float32)
-        O.env_step_batch(cfg, q, v, w, steps, a, hf, 2.0, off, threads=threads)
-        done_steps += n
+        for hf, size_z, off, q, v, w, steps in groups:
+            a = rng.uniform(-1, 1, (n, 3)).astype(np.float32)
+            O.env_step_batch(cfg, q, v, w, steps, a, hf, size_z, off, threads=threads)
+            done_steps += n
     dt = time.perf_counter() - t0
     cpu = platform.processor() or platform.machine()
     try:
@@ -87,41 +131,67 @@ def cpu_baseline(seconds: float = 12.0, threads: int = 1) -> dict:
     except OSError:
         pass
     return {"value": done_steps / dt, "unit": "env-steps/s", "cores": threads, "kind": "port",
-            "sample": f"{n} envs x {done_steps // n} steps, flat, random actions, {threads} thread(s) on '{cpu}' "
-                      f"(fp64 oracle restating the reference step; MuJoCo itself is not available)"}
+            "sample": f"{len(groups)} x {n} envs x {done_steps // (n * len(groups))} steps on {fields_desc}, random "
+                      f"actions, auto-reset, {threads} thread(s) on '{cpu}' (fp64 oracle restating the reference "
+                      f"step; MuJoCo itself is not available)"}
 
 
-def flop_count(env, terrain: str, n_envs: int = 16, n_steps: int = 400, burn_in: int = 400,
-               n_fields: int = 4) -> dict:
-    """Algorithmic FLOPs per env-step of the restated reference algorithm on this
-    workload's terrain (oracle/flopcount.cpp: the oracle compiled over a counting
-    double, MuJoCo's solver settings; the checker's build, in the CPU leg).
-    Counted after an uncounted burn-in, as the bench times the steady-state mix
-    of episode ages; on a terrain bank, averaged over the first-drawn terrains of
-    the first n_fields streams (the cost per step varies with the terrain: on
-    rough perlin most of an episode is the fall from the reset height)."""
+def mix_snapshot(env, pool, steps: int, sample: int = 512, max_ep: int = 12) -> dict:
+    """The timed window's mix, for flop_count: `sample` envs spread over the env ids, their
+    states at the start of the window, the window's actions for them (step t reads pool slot
+    t % P, as run() does), and each env's current terrain plus the next max_ep - 1 its device
+    generator will draw (a seed the bank lacks resets onto slot seed % n_terrains, as the
+    kernel does).  Taken before the timed region (it synchronises)."""
     import numpy as np
+    import torch
 
+    from ballbot_gym.envs.config import pcg64_terrain_draws
+
+    n = env.num_envs
+    idx = np.unique(np.linspace(0, n - 1, min(sample, n)).round().astype(np.int64))
+    q, v, w, sc = env.get_state()
+    slots, _ = env.env_terrain()
+    words, _ = env.terrain_rng()
+    P = pool.shape[0]
+    it = torch.as_tensor(idx, device=pool.device)
+    acts = torch.stack([pool[t % P].index_select(0, it) for t in range(steps)]).cpu().numpy()
+    plan = env.terrain_plan
+    rows = np.zeros((len(idx), max_ep), np.int64)
+    for j, e in enumerate(idx):
+        row = [int(slots[e])]
+        if words is not None:
+            for x in pcg64_terrain_draws([int(u) for u in words[e]], max_ep - 1)[0]:
+                sl = plan.slot_of(int(x))
+                row.append(sl if sl >= 0 else int(x) % env.n_terrains)
+        else:  # one fixed terrain, or a shared / tabled stream: the env stays on its terrain
+            row += [row[0]] * (max_ep - 1)
+        rows[j] = row
+    uniq, inv = np.unique(rows, return_inverse=True)
+    offs = env.offsets()
+    return {"q": q[idx], "v": v[idx], "w": w[idx], "sc": sc[idx].astype(np.int32), "actions": acts,
+            "table": np.stack([env.hfield(int(u)) for u in uniq]), "offsets": offs[uniq].astype(np.float64),
+            "terr": inv.reshape(rows.shape).astype(np.int32), "size_z": float(plan.size_z), "envs": len(idx),
+            "terrains": len(uniq), "per_env_draws": words is not None}
+
+
+def flop_count(mix: dict, terrain: str) -> dict:
+    """Algorithmic FLOPs per env-step of the restated reference algorithm on THIS line's timed
+    mix (oracle/flopcount.cpp: the oracle compiled over a counting double, MuJoCo's solver
+    settings; the checker's build, in the CPU leg): the sampled envs of mix_snapshot replayed
+    from their window-start states with the window's actions and their own terrain draws, on
+    host threads.  The oracle's trajectories drift from the kernel's after falls (chaos), so the
+    mix is the window's in distribution, not step for step."""
     sys.path.insert(0, str(ROOT / "tools"))
     import flops as F
 
-    from ballbot_gym.envs.config import stream_draws
-
-    plan = env.terrain_plan
-    drawn = plan.stream_seeds is not None
-    if not drawn:
-        slots = [0]
-    else:  # the first terrains drawn by the first n_fields generators
-        firsts = [int(stream_draws(s, 1)[0]) for s in list(dict.fromkeys(plan.stream_seeds))[:n_fields]]
-        slots = list(dict.fromkeys(max(plan.slot_of(s), 0) for s in firsts))
-    rs = [F.count(F.lib(), env.hfield(s), float(plan.size_z), n_envs, n_steps, burn_in=burn_in) for s in slots]
-    fl = float(np.mean([r["flops_per_env_step"] for r in rs]))
-    by = {k: float(np.mean([r["flops_by_phase"][k] for r in rs])) for k in rs[0]["flops_by_phase"]}
-    return {"flops_per_env_step": fl, "by_phase": by,
-            "sample": (f"{len(slots)} terrain(s) of the '{terrain}' bank (seeds {[int(plan.seeds[s]) for s in slots]})"
-                       if drawn else f"the '{terrain}' terrain") +
-                      f" x {n_envs} envs x {n_steps} counted steps after {burn_in} uncounted, uniform random actions, "
-                      "auto-reset; MuJoCo solver settings (tolerance 1e-8, line search 0.01 / 50 evaluations)"}
+    thr = int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or min(16, os.cpu_count() or 1)
+    r = F.count_replay(mix["q"].copy(), mix["v"].copy(), mix["w"].copy(), mix["sc"].copy(), mix["actions"],
+                       mix["table"], mix["offsets"], mix["terr"], mix["size_z"], threads=thr)
+    r["sample"] = (f"{mix['envs']} envs (spread over the env ids) x {mix['actions'].shape[0]} steps: the timed "
+                   f"window's own start states, actions and {'per-env terrain draws' if mix['per_env_draws'] else 'terrain'}"
+                   f" ({mix['terrains']} '{terrain}' terrains), auto-reset; MuJoCo solver settings (tolerance 1e-8, "
+                   "PrimalSearch ls_tolerance 0.01 / 50 evaluations)")
+    return r
 
 
 def parity_probe(env, n_probe: int = 64) -> dict:
@@ -288,6 +358,8 @@ def main() -> None:
         return max_over_ranks(elapsed, device=dev), step_ms, ktimes, kern_n, st0, st1
 
     run(args.burn_in + args.warmup, M)
+    # the CPU leg's FLOP count replays the timed window's own mix: snapshot it before the window
+    mix = mix_snapshot(env, pool, args.steps) if (world == 1 and not args.no_cpu_baseline) else None
     elapsed, step_ms, ktimes, kern_n, st0, st1 = timed(M)
     pair = env.pair_counters() if (M and env.relief) else None  # the last timed launch (relief pair)
     if pair is not None and pair["claims_fast"] + pair["claims_full"] > 0:
@@ -307,6 +379,17 @@ def main() -> None:
         run(args.warmup, 0)
         per_step = timed(0)
     stats = env.stats()
+    # Launch status: every launch returned 0 (step_multi_raw / step_async_raw raise otherwise);
+    # bb_check waits for the stream and raises if a relief-pair launch ended on its wall-clock
+    # budget (stale outputs and a fast number); and no env diverged in the timed window.
+    env.check()
+    problems = []
+    if stats["pair_budget"]:
+        problems.append(f"{stats['pair_budget']} relief-pair launch(es) ended on the wall-clock budget")
+    if st1["diverged"] != st0["diverged"]:
+        problems.append(f"{st1['diverged'] - st0['diverged']} env-steps diverged in the timed window")
+    if problems:
+        raise SystemExit(f"bench.py rank {rank}: " + "; ".join(problems))
     # envs per launch of each kernel over the timed steps: the full kernel stepped
     # slow_path env-steps (predicted + handed over), the fast kernel the rest
     full_per_step = (st1["slow_path"] - st0["slow_path"]) / args.steps
@@ -325,22 +408,64 @@ def main() -> None:
             envs_dom = n * args.steps / kern_n
             spl = args.steps / kern_n
         abytes = algorithmic_bytes(args.precision, spl, env.relief) * envs_dom
-        achieved = abytes / (kern_ms * 1e-3) / 1e9
-        traffic = issue_frac = None
-        tj = Path(args.traffic_json)
-        if tj.exists():
-            try:
-                key = (args.precision if not M else f"{args.precision}_multi{M}") + (
-                    "" if args.terrain == "flat" else f"_{args.terrain}")
-                tr = json.loads(tj.read_text()).get(key) or {}
-                if tr.get("envs") == n and tr.get("terrain", "flat") == args.terrain:
-                    traffic = tr.get("bytes_per_launch")
-                    issue_frac = tr.get("issue_frac")
-            except Exception:
-                traffic = issue_frac = None
+        achieved_gbs = abytes / (kern_ms * 1e-3) / 1e9
+        prof = profile_entry(Path(args.traffic_json), args.precision, args.terrain, n, spl)
         relief_form = ("relief_multi_kernel<T> (work queue)" if os.environ.get("BB_RELIEF_PAIR", "1") == "0" else
                        "relief_pair1_kernel<T> (the relief pair, one launch)" if os.environ.get("BB_PAIR_ONE", "1") != "0"
                        else "relief_pair_kernel<T,false> + <T,true> (the relief pair, two concurrent launches)")
+        kernel = ((f"{relief_form} or the parked multi_step_kernel<T,*> "
+                   f"launches, chosen per launch from the last one's full steps ({M} steps per "
+                   "launch)" if env.relief and "BB_MULTI_QUEUE" not in os.environ and
+                   "BB_ROUTE" not in os.environ and os.environ.get("BB_MULTI_ADAPT", "1") != "0"
+                   else f"{relief_form} ({M} steps per launch)" if env.relief
+                   and os.environ.get("BB_MULTI_QUEUE", "1") != "0" and
+                   os.environ.get("BB_ROUTE", "0") == "0"
+                   else f"multi_step_kernel<T,false> ({M} steps per launch; hand-overs parked "
+                        "for multi_step_kernel<T,true>)" if os.environ.get("BB_MULTI_PARK", "1") != "0"
+                   else f"multi_step_kernel<T,true> ({M} steps per launch, hand-overs inline)") if M else
+                  "step_kernel<T,false> (fast path)" if dom == "fast"
+                  else "step_kernel<T,true> (predicted full kernel, side stream)")
+        # the compute side: algorithmic FP64 FLOPs of the reference algorithm per env-step on this
+        # workload (the oracle over a counting double, CPU leg) -- live when the CPU leg runs,
+        # else the committed count for this terrain (profiles/flops.json)
+        fl = None
+        if mix is not None:
+            try:
+                fl = flop_count(mix, args.terrain)
+            except Exception as e:  # the counting build needs g++ (present here and on the box)
+                fl = {"error": repr(e)}
+        if fl is None or "error" in fl:
+            fl = committed_flops(args.terrain) or fl
+        fpe = (fl or {}).get("flops_per_env_step")
+        tf = fpe * envs_dom / (kern_ms * 1e-3) / 1e12 if fpe else None
+        roof = {
+            # the roof that binds: FP64 vector issue and the latency of dependent solves
+            "bound": "valu", "achieved": tf, "peak": FP64_VECTOR_PEAK_TFLOPS, "unit": "TFLOP/s",
+            "frac": tf / FP64_VECTOR_PEAK_TFLOPS if tf else None,
+            # HBM bytes per launch from rocprofv3 PMC passes of THIS launch shape (steps per launch,
+            # envs, terrain, precision), or null (profiles/traffic.json, tools/prof_summary.py)
+            "traffic": prof.get("bytes_per_launch"),
+            "traffic_algorithmic_bytes": abytes,
+            "issue_frac": prof.get("issue_frac"),
+            "profile": prof.get("source"),
+            "kernel": kernel, "kernel_ms": kern_ms, "envs_per_launch": envs_dom, "steps_per_launch": spl,
+            "kernel_ms_all": ktimes, "full_kernel_envs_per_step": full_per_step,
+            "kernel_launches_timed": kern_n, "step_ms_hip_events": step_ms,
+            "flops": fl,
+            # the secondary roof, as BASELINE.json asks: algorithmic HBM bytes per launch over the
+            # kernel's duration against the 8 TB/s peak
+            "hbm": {"achieved": achieved_gbs, "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": achieved_gbs / HBM_PEAK_GBS,
+                    "algorithmic_bytes_per_env_step": algorithmic_bytes(args.precision, spl, env.relief),
+                    "traffic_bytes_per_env_step": (prof["bytes_per_launch"] / envs_dom
+                                                   if prof.get("bytes_per_launch") else None),
+                    "note": "algorithmic I/O: state once per launch of the line's steps, action and all five "
+                            "outputs every step" + (", 7x7 hfield vertices per step" if env.relief else "")},
+        }
+        if prof.get("fp64_flop_executed_per_launch"):
+            ex = prof["fp64_flop_executed_per_launch"]
+            roof["valu_fp64_executed"] = {"flop_per_launch_upper_bound": ex,
+                                          "tflops_upper_bound": ex / (kern_ms * 1e-3) / 1e12,
+                                          "executed_over_counted": ex / (fpe * envs_dom) if fpe else None}
         line = {
             "metric": f"env-steps/sec at {n} envs per GPU ({args.terrain} terrain, random actions)",
             "value": value,
@@ -359,39 +484,16 @@ def main() -> None:
                        else ")"),
             "config": {"workload": f"{n} envs/GPU, {args.terrain} terrain, random actions "
                                    f"(BASELINE configs[{1 if args.terrain == 'flat' else 2}])",
-                       "n_terrains": env.n_terrains, "depth_cameras": bool(args.cameras),
+                       "terrain": args.terrain, "n_terrains": env.n_terrains, "depth_cameras": bool(args.cameras),
                        "terrain_streams": "per env (seed 1000 + env id)" if per_env else "shared (seed 1000)",
                        "hip_graph": graph is not None, "burn_in_steps": args.burn_in,
-                       "steps_per_launch": M or 1,
+                       "multi_step": M, "steps_per_launch": spl,
                        "envs_per_gpu": n, "total_envs": n * world, "precision": args.precision,
                        "parallelism": f"env-sharded x{world} (no collective on the step path)",
                        "launch": launch},
-            "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                         "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
-                         "note": "latency/VALU-bound per-lane physics; HBM bytes = algorithmic I/O "
-                                 f"({algorithmic_bytes(args.precision, spl, env.relief):.1f} B/env-step: state "
-                                 f"once per launch of {spl:g} steps, action and all five outputs every step"
-                                 + (", 7x7 hfield vertices per step" if env.relief else "") +
-                                 ") x the env-steps of one launch",
-                         "kernel": ((f"{relief_form} or the parked multi_step_kernel<T,*> "
-                                     f"launches, chosen per launch from the last one's full steps ({M} steps per "
-                                     "launch)" if env.relief and "BB_MULTI_QUEUE" not in os.environ and
-                                     "BB_ROUTE" not in os.environ and os.environ.get("BB_MULTI_ADAPT", "1") != "0"
-                                     else f"{relief_form} ({M} steps per launch)" if env.relief
-                                     and os.environ.get("BB_MULTI_QUEUE", "1") != "0" and
-                                     os.environ.get("BB_ROUTE", "0") == "0"
-                                     else f"multi_step_kernel<T,false> ({M} steps per launch; hand-overs parked "
-                                          "for multi_step_kernel<T,true>)" if os.environ.get("BB_MULTI_PARK", "1") != "0"
-                                     else f"multi_step_kernel<T,true> ({M} steps per launch, hand-overs inline)") if M else
-                                    "step_kernel<T,false> (fast path)" if dom == "fast"
-                                    else "step_kernel<T,true> (predicted full kernel, side stream)"),
-                         "kernel_ms": kern_ms, "envs_per_launch": envs_dom, "kernel_ms_all": ktimes,
-                         "full_kernel_envs_per_step": full_per_step,
-                         "kernel_launches_timed": kern_n, "step_ms_hip_events": step_ms,
-                         # share of the kernel's wave cycles spent issuing (rocprofv3 SQ
-                         # counters, profiles/): the bound that binds is instruction issue
-                         "issue_frac": issue_frac},
+            "roofline": roof,
             "stats": stats,
+            "status": "ok",
         }
         if pair is not None and pair["claims_fast"] + pair["claims_full"] > 0:
             line["pair"] = pair
@@ -405,18 +507,13 @@ def main() -> None:
         if world == 1 and not args.no_cpu_baseline:
             if args.terrain == "flat":
                 line["parity"] = parity_probe(env)
-            try:  # the compute side of the roofline: reference-algorithm FLOPs at this throughput
-                fl = flop_count(env, args.terrain)
-                tf = fl["flops_per_env_step"] * value / 1e12
-                line["roofline"]["valu_fp64"] = {"achieved": tf, "peak": FP64_VECTOR_PEAK_TFLOPS, "unit": "TFLOP/s",
-                                                 "frac": tf / FP64_VECTOR_PEAK_TFLOPS, **fl}
-            except Exception as e:  # the counting build needs g++ (present here and on the box)
-                line["roofline"]["valu_fp64"] = {"error": repr(e)}
-            line["cpu_baseline"] = cpu_baseline(args.cpu_seconds)
+            fields, desc = bench_fields(env, args.terrain)
+            line["cpu_baseline"] = cpu_baseline(args.cpu_seconds, fields=fields, fields_desc=desc)
             # all host cores granted to this job (OMP_NUM_THREADS; 16 on the GPU box)
             thr = int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or min(16, os.cpu_count() or 1)
             if thr > 1:
-                line["cpu_baseline_multicore"] = cpu_baseline(args.cpu_seconds / 2, threads=thr)
+                line["cpu_baseline_multicore"] = cpu_baseline(args.cpu_seconds / 2, threads=thr, fields=fields,
+                                                              fields_desc=desc)
         print(json.dumps(line), flush=True)
     env.close()
     if world > 1:

@@ -56,7 +56,7 @@
 extern "C" {
 #endif
 
-#define BB_ABI_VERSION 16
+#define BB_ABI_VERSION 17
 #define BB_NQ 17
 #define BB_NV 15
 #define BB_OBS 15
@@ -96,7 +96,15 @@ typedef struct {
   int fp64;                    /* 1 (default): fp64 arithmetic, 0: fp32 */
   int solver_maxiter;          /* 0 = default */
   double solver_tol;           /* 0 = default */
+  /* mjModel.opt overrides (ABI 17; ballbot.xml:3-5): model.opt.timestep (0 = 0.002 s)
+   * and disable flags with MuJoCo's mjtDisableBit values -- BB_DSBL_PASSIVE (joint
+   * damping), BB_DSBL_GRAVITY.  For the physics invariants (tests/test_gpu_invariants.py);
+   * the reference env never changes them. */
+  double opt_timestep;
+  int opt_disableflags;
 } bb_params;
+#define BB_DSBL_PASSIVE 32
+#define BB_DSBL_GRAVITY 64
 
 int bb_abi_version(void);
 int bb_last_error(char* buf, int len);
@@ -375,6 +383,15 @@ int bb_step(bb_handle* h, const float* actions_dev, float* obs_dev, float* rewar
  * picks one per call (BB_MULTI_ADAPT=0: always the pair).  DESIGN §6d, §6e. */
 int bb_step_multi(bb_handle* h, const float* actions_dev, int k_steps, float* obs_dev, float* reward_dev,
                   uint8_t* done_dev, float* terminal_obs_dev, float* pos2d_dev, int auto_reset, void* stream);
+
+/* Wait for `stream` and report the handle's sticky fault: 0, or < 0 when a bb_step_multi
+ * relief-pair launch ended on its wall-clock budget (BB_PAIR_BUDGET_MS, default 20 s: a team
+ * waited that long for an env, which only a grid the device could not seat would cause).  The
+ * launch then left some envs with their state at its start but terrain draws and counters
+ * advanced, so from then on bb_step, bb_step_multi and bb_rollout return the same error at once
+ * (no sync needed: the fault word is host memory mapped into the device) until a full bb_reset
+ * (mask NULL) clears it.  No reference counterpart: MuJoCo's mj_step has no such launch. */
+int bb_check(bb_handle* h, void* stream);
 
 /* diagnostics / parity (synchronous, host arrays) */
 int bb_get_state(bb_handle* h, double* qpos, double* qvel, double* warm, int32_t* steps);

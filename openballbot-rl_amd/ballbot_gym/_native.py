@@ -18,6 +18,7 @@ NQ, NV, NOBS, HF_N = 17, 15, 15, 293
 DONE_TERMINATED, DONE_FAILURE, DONE_DIVERGED, DONE_OVERFLOW = 1, 2, 4, 8
 NSTATS = 8  # BB_NSTATS
 REWARD_DIRECTIONAL, REWARD_DISTANCE, REWARD_NONE = 0, 1, 2
+DSBL_PASSIVE, DSBL_GRAVITY = 32, 64  # bb_params.opt_disableflags (MuJoCo mjtDisableBit values)
 
 
 class NativeLibraryError(RuntimeError):
@@ -41,6 +42,8 @@ class BBParams(C.Structure):
         ("fp64", C.c_int),
         ("solver_maxiter", C.c_int),
         ("solver_tol", C.c_double),
+        ("opt_timestep", C.c_double),
+        ("opt_disableflags", C.c_int),
     ]
 
 
@@ -104,10 +107,10 @@ EXPORTS = [
     "bb_gae", "bb_render_depth", "bb_ppo_loss", "bb_adamw_clip", "bb_ppo_mlp_workspace_bytes", "bb_ppo_mlp_step",
     "bb_ppo_mlp_act", "bb_rollout_track", "bb_depth_encoder_workspace_bytes", "bb_depth_encoder",
     "bb_set_terrain_stream", "bb_get_env_terrain", "bb_kernel_times", "bb_step_multi", "bb_rollout",
-    "bb_set_terrain_rng", "bb_get_terrain_rng", "bb_pair_counters", "bb_pair_env_times",
+    "bb_set_terrain_rng", "bb_get_terrain_rng", "bb_pair_counters", "bb_pair_env_times", "bb_check",
 ]
 
-ABI_VERSION = 16  # include/ballbot_mi355x.h BB_ABI_VERSION
+ABI_VERSION = 17  # include/ballbot_mi355x.h BB_ABI_VERSION
 
 _lib = None
 
@@ -197,6 +200,7 @@ def _load(path: Path):
     L.bb_get_stats.argtypes = [vp, C.POINTER(C.c_int64), C.c_int]
     L.bb_pair_counters.argtypes = [vp, C.POINTER(C.c_int64), C.c_int]
     L.bb_pair_env_times.argtypes = [vp, C.POINTER(C.c_uint64)]
+    L.bb_check.argtypes = [vp, vp]
     L.bb_set_terrain_stream.argtypes = [vp, C.POINTER(C.c_int32), C.c_int, C.c_int, C.POINTER(C.c_int32)]
     L.bb_set_terrain_rng.argtypes = [vp, C.POINTER(C.c_uint64), C.POINTER(C.c_int32)]
     L.bb_get_terrain_rng.argtypes = [vp, C.POINTER(C.c_uint64), C.POINTER(C.c_int32)]

@@ -66,6 +66,8 @@ class BallbotVecEnv:
         shared_stream: bool = False,
         terrain_slots: Optional[int] = None,
         reward_compat: str = "reference",
+        opt_timestep: Optional[float] = None,
+        opt_disableflags: int = 0,
     ):
         from .config import params_from_configs
 
@@ -83,7 +85,7 @@ class BallbotVecEnv:
         cam = ((env_config or {}).get("camera", {}) or {})
         self.cam_h, self.cam_w = int(cam.get("height", 64)), int(cam.get("width", 64))
         fr = float(cam.get("frame_rate", 90))
-        self.cam_every = int(np.ceil((1.0 / fr) / 0.002))  # effective_camera_frame_rate (ballbot_env.py:389-411)
+        self.cam_every = int(np.ceil((1.0 / fr) / float(opt_timestep or 0.002)))  # effective_camera_frame_rate (ballbot_env.py:389-411)
         if self.cameras and not cam.get("disable_rgb", True):
             raise ValueError("only depth cameras are rendered (camera.disable_rgb must be true)")
         self.terrain_config = terrain_config or {"type": "flat", "config": {}}
@@ -95,6 +97,11 @@ class BallbotVecEnv:
         # reward_compat="reference": a DistanceReward raises at the first step, as
         # in the reference env (its obs lacks pos2d); "fused": the kernel computes it
         self._reward_error = reward_error(self.reward_obj, reward_compat)
+        # mjModel.opt overrides (physics invariant tests): timestep and MuJoCo's
+        # mjDSBL_PASSIVE / mjDSBL_GRAVITY bits (_native.DSBL_*); the reference never sets them
+        p.opt_timestep = float(opt_timestep or 0.0)
+        p.opt_disableflags = int(opt_disableflags)
+        self.opt_timestep = float(opt_timestep or 0.002)
         self.max_ep_steps = int(p.max_ep_steps)
         self.precision = "fp64" if p.fp64 else "fp32"
         self._params = p
@@ -337,8 +344,15 @@ class BallbotVecEnv:
                        pos2d: Optional[torch.Tensor] = None) -> None:
         """Launch-only bb_step_multi (benchmarking): caller-owned [K, N, ...] outputs
         (terminal obs / pos2d optional)."""
-        N.lib().bb_step_multi(self._h, _ptr(actions), int(actions.shape[0]), _ptr(obs), _ptr(reward), _ptr(done),
-                              _ptr(terminal_obs), _ptr(pos2d), int(self.auto_reset), self._stream())
+        N.check(N.lib().bb_step_multi(self._h, _ptr(actions), int(actions.shape[0]), _ptr(obs), _ptr(reward),
+                                      _ptr(done), _ptr(terminal_obs), _ptr(pos2d), int(self.auto_reset),
+                                      self._stream()), "bb_step_multi")
+
+    def check(self) -> None:
+        """Wait for the env's stream and raise if a bb_step_multi relief-pair launch ended on its
+        wall-clock budget (bb_check).  The fault is sticky: step(), step_multi() and rollouts raise
+        too, without a sync, until a full reset() clears it."""
+        N.check(N.lib().bb_check(self._h, self._stream()), "bb_check")
 
     def run_rollout(self, args) -> None:
         """One whole PPO rollout in one launch (bb_rollout; args: _native.RolloutArgs
@@ -354,9 +368,10 @@ class BallbotVecEnv:
     def step_async_raw(self, actions: torch.Tensor, full_outputs: bool = False) -> None:
         """Launch-only step (graph capture / benchmarking): no derived tensors;
         full_outputs: also the terminal obs and pos2d buffers."""
-        N.lib().bb_step(self._h, _ptr(actions), _ptr(self.obs), _ptr(self.reward), _ptr(self.done),
-                        _ptr(self.terminal_obs) if full_outputs else None, _ptr(self.pos2d) if full_outputs else None,
-                        int(self.auto_reset), self._stream())
+        N.check(N.lib().bb_step(self._h, _ptr(actions), _ptr(self.obs), _ptr(self.reward), _ptr(self.done),
+                                _ptr(self.terminal_obs) if full_outputs else None,
+                                _ptr(self.pos2d) if full_outputs else None, int(self.auto_reset), self._stream()),
+                "bb_step")
 
     def _plugin_reward(self, failure: torch.Tensor) -> torch.Tensor:
         """Reward of a custom plugin, in the reference's float32 order

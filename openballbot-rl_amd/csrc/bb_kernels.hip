@@ -39,6 +39,7 @@
 #include "bb_ppo.h"
 #include "bb_mlp.h"
 #include "bb_encoder.h"
+#include "bb_pairmap.h"
 
 using namespace bb;
 
@@ -116,6 +117,7 @@ struct Dev {
   unsigned long long* pair_busy;  // relief_pair_kernel, last launch: [2] team-cycles stepping, [2] team lifetimes
                                   // in shader cycles, [2] in wall-clock ticks (fast, full)
   unsigned long long* cost;   // relief_multi_kernel: shader cycles each env's steps took in the last launch
+  int* fault;                 // host-mapped sticky error word (bb_check): a relief-pair launch hit its budget
 };
 
 // env e's spill block for base-tree contacts MAXB_LDS..MAXB-1
@@ -867,6 +869,8 @@ __global__ __launch_bounds__(64) void rollout_kernel(ModelT<T> mg, EnvCfg cfg, D
 template <typename T>
 __global__ __launch_bounds__(64) void reset_kernel(ModelT<T> m, Dev d, const uint8_t* mask, float* obs) {
   const int e = blockIdx.x * WAVE + threadIdx.x;
+  // a full reset gives every env a valid state again: it clears the relief pair's sticky fault
+  if (!mask && e == 0 && d.fault) __hip_atomic_store(d.fault, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
   if (e >= d.n) return;
   if (mask && !mask[e]) return;
   T q[NQ], v[NV], w[NV];
@@ -1298,7 +1302,7 @@ constexpr int SC_SOLO = 42, SC_HEAVY = 43, SC_HEAVY_LAST = 44;
 // its terrain cells stay cached.  The label is only a placement hint: any mapping is correct,
 // since every label has fast and full workgroups (each kind keeps >= pair_cap / 8 >= 8).  The
 // heavy envs' solo ring (kind 2) is one ring: the solo workgroups may cover fewer than 8 labels.
-constexpr int NXCD = 8, NRINGS = 2 * NXCD + 1;
+constexpr int NRINGS = 2 * NXCD + 1;  // NXCD: bb_pairmap.h
 __device__ __forceinline__ int env_xcd(int e) { return (e >> 5) & (NXCD - 1); }
 __device__ __forceinline__ int pair_ring(int kind, int x) { return kind < 2 ? kind * NXCD + x : 2 * NXCD; }
 
@@ -1359,6 +1363,7 @@ __device__ __forceinline__ void pair_loop(const ModelT<T>& mg, const EnvCfg& cfg
   const int rkind = solo ? 2 : kind;
   const int myring = pair_ring(rkind, int(blockIdx.x) & (NXCD - 1));  // this team's ring (see env_xcd)
   const unsigned long long t0 = wall_clock64(), c_start = clock64();
+  unsigned long long tw = t0;  // when this team last became idle: the budget bounds a wait, not the team's life
   int e = -1, k = 0, tid = 0, step = 0, held = 0, ticket = -1;  // ticket: the lead's, -1 when none
   unsigned idle = 0;
   unsigned long long busy = 0;  // this team's cycles stepping envs (the split of the next launch)
@@ -1376,8 +1381,13 @@ __device__ __forceinline__ void pair_loop(const ModelT<T>& mg, const EnvCfg& cfg
           if (ticket < 0) ticket = ring_ticket(d, myring);
           got = ring_look(d, myring, ticket);
           if (got >= 0) ticket = -1;
-          else if (wall_clock64() - t0 > budget) {
-            if (atomicExch(sc + SC_ERR, 1) == 0) atomicAdd(&d.stats[7], 1ull);
+          else if (wall_clock64() - tw > budget) {
+            // no env came for `budget` ticks: end the launch for every team, count it, and
+            // raise the handle's sticky fault (host-mapped: bb_check / the next call reports it)
+            if (atomicExch(sc + SC_ERR, 1) == 0) {
+              atomicAdd(&d.stats[7], 1ull);
+              if (d.fault) __hip_atomic_store(d.fault, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+            }
             got = -2;
           }
         }
@@ -1451,6 +1461,7 @@ __device__ __forceinline__ void pair_loop(const ModelT<T>& mg, const EnvCfg& cfg
           if (k >= K) atomicAdd(sc + SC_DONE, 1);
           else ring_push(d, next == 1 && (d.pred_mark[e] & 2) ? 2 : next, e);
           if (FULL && gate) atomicAdd(sc + SC_TOUCHED, 1);  // adaptive route: an env took full steps
+          tw = wall_clock64();
         }
         e = -1;
       }
@@ -1491,9 +1502,9 @@ __global__ __launch_bounds__(64) void relief_pair_kernel(ModelT<T> mg, EnvCfg cf
                      ms, s_cnt, s_diag);
 }
 
-// the pair as ONE launch: the first SC_ACTIVE[0] workgroups run the fast loop, the next
-// SC_ACTIVE[1] the full loop (the two loops are disjoint regions of the kernel, so
-// the kernel keeps the larger one's registers, not their union)
+// the pair as ONE launch: SC_ACTIVE[0] workgroups run the fast loop and SC_ACTIVE[1] the full
+// loop, interleaved by groups of NXCD blocks (pair_kind_of); the two loops are disjoint regions
+// of the kernel, so it keeps the larger one's registers, not their union
 template <typename T>
 __global__ __launch_bounds__(64) void relief_pair1_kernel(ModelT<T> mg, EnvCfg cfg, Dev d, const float* __restrict__ act,
                                                           int K, float* __restrict__ obs, float* __restrict__ rew,
@@ -1501,17 +1512,18 @@ __global__ __launch_bounds__(64) void relief_pair1_kernel(ModelT<T> mg, EnvCfg c
                                                           float* __restrict__ pos2d, int auto_reset, int seg,
                                                           unsigned long long budget, const int* __restrict__ gate) {
   if (gate && *gate == ROUTE_PARK) return;
-  const int nf = d.slow_count[SC_ACTIVE], ns = d.slow_count[SC_ACTIVE + 1], b = int(blockIdx.x);
-  if (b >= nf + ns) return;
+  int wg = 0;
+  const int kind = pair_kind_of(int(blockIdx.x), d.slow_count[SC_ACTIVE], d.slow_count[SC_ACTIVE + 1], &wg);
+  if (kind < 0) return;  // workgroup-uniform, before any barrier
   extern __shared__ __align__(16) unsigned char smem[];
   __shared__ ModelT<T> ms;
   __shared__ unsigned s_cnt[WAVE / TEAM][8];
   __shared__ int s_diag[WAVE / TEAM][3];
-  if (b < nf)
-    pair_loop<T, false>(mg, cfg, d, act, K, obs, rew, done, tobs, pos2d, auto_reset, seg, budget, gate, b, smem, ms,
+  if (kind == 0)
+    pair_loop<T, false>(mg, cfg, d, act, K, obs, rew, done, tobs, pos2d, auto_reset, seg, budget, gate, wg, smem, ms,
                         s_cnt, s_diag);
   else
-    pair_loop<T, true>(mg, cfg, d, act, K, obs, rew, done, tobs, pos2d, auto_reset, seg, budget, gate, b - nf, smem, ms,
+    pair_loop<T, true>(mg, cfg, d, act, K, obs, rew, done, tobs, pos2d, auto_reset, seg, budget, gate, wg, smem, ms,
                        s_cnt, s_diag);
 }
 
@@ -1580,11 +1592,12 @@ __global__ void pair_adapt_kernel(Dev d, int cap, const int* __restrict__ gate) 
   int* sc = d.slow_count;
   const double bf = double(d.pair_busy[0]), bs = double(d.pair_busy[1]);
   if (bf + bs <= 0) return;
-  int ns = int(double(cap) * bs / (bf + bs) + 0.5);
-  const int lo = cap / 8;
-  ns = ns < lo ? lo : (ns > cap - lo ? cap - lo : ns);
-  sc[SC_ACTIVE] = cap - ns;
-  sc[SC_ACTIVE + 1] = ns;
+  // whole groups of NXCD workgroups (pair_kind_of), at least cap / 8 per kind
+  const int G = cap / NXCD, lo = (G + 7) / 8;
+  int gs = int(double(G) * bs / (bf + bs) + 0.5);
+  gs = gs < lo ? lo : (gs > G - lo ? G - lo : gs);
+  sc[SC_ACTIVE] = (G - gs) * NXCD;
+  sc[SC_ACTIVE + 1] = gs * NXCD;
 }
 
 // Between relief_multi_kernel launches: deal the envs over its workgroups so
@@ -1716,7 +1729,8 @@ struct bb_handle {
   int pair_one = 1;             // the pair as one launch (BB_PAIR_ONE=0: two concurrent launches on two streams)
   int pair_solo = 0;            // solo waves for heavy envs' full steps (BB_PAIR_SOLO; <= pair_cap / 8)
   int pair_heavy_pct = 150;     // heavy: last launch's cycles above this % of the mean env's (BB_PAIR_HEAVY)
-  unsigned long long pair_budget = 0;  // wall-clock ticks a pair launch may wait for work (20 s)
+  unsigned long long pair_budget = 0;  // wall-clock ticks a pair team may wait for an env (20 s)
+  double pair_budget_s = 20;
   int count_memset = 0;         // diagnostic (BB_COUNT_MEMSET=1): reset the hand-over count with
                                 // hipMemsetAsync instead of zero_count_kernel
   std::vector<uint8_t> relief;  // per terrain: max height > 0
@@ -1729,6 +1743,7 @@ struct bb_handle {
   int* seed_slot = nullptr;           // [TERRAIN_SEEDS], allocated once
   CamRig rig;  // depth cameras in the base body (bb_render_depth)
   void* scenes = nullptr;
+  volatile int* fault_host = nullptr;  // Dev.fault's host side (hipHostMalloc, mapped)
 };
 
 template <typename T> const ModelT<T>& model_of(const bb_handle* h);
@@ -1896,7 +1911,28 @@ extern "C" __attribute__((visibility("hidden"))) int bb_pair_launch_tu(bb_handle
                                                                       float* o, float* r, uint8_t* dn, float* t,
                                                                       float* p2, int ar, hipStream_t s,
                                                                       const int* gate);
+// Once per handle, in the unit whose pair kernels are the ones launched: their dynamic-LDS
+// limit, and how many one-wave workgroups of relief_pair1_kernel<T> a CU holds at once
+// (*per_cu; the persistent pair's grid is sized from it, bb_create).
+extern "C" __attribute__((visibility("hidden"))) int bb_pair_setup_tu(int fp64, int* per_cu);
 #ifdef BB_PAIR_TU
+template <typename T>
+int pair_setup(int* per_cu) {  // -> a hipError_t (this unit's error text is not the C-ABI's)
+  const size_t plb = multi_lds_bytes<T>(4);
+  const void* ks[3] = {(const void*)relief_pair1_kernel<T>, (const void*)relief_pair_kernel<T, false>,
+                       (const void*)relief_pair_kernel<T, true>};
+  for (const void* k : ks) {
+    const hipError_t e = hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, int(plb));
+    if (e != hipSuccess) return int(e);
+  }
+  int nb = 0;
+  const hipError_t e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, ks[0], WAVE, plb);
+  *per_cu = nb;
+  return int(e);
+}
+extern "C" __attribute__((visibility("hidden"))) int bb_pair_setup_tu(int fp64, int* per_cu) {
+  return fp64 ? pair_setup<double>(per_cu) : pair_setup<float>(per_cu);
+}
 extern "C" __attribute__((visibility("hidden"))) int bb_pair_launch_tu(bb_handle* h, int fp64, const float* a, int K, float* o, float* r, uint8_t* dn,
                                  float* t, float* p2, int ar, hipStream_t s, const int* gate) {
   return fp64 ? launch_pair<double>(h, a, K, o, r, dn, t, p2, ar, s, gate)
@@ -2006,6 +2042,11 @@ int bb_create(int n_envs, int device, const bb_params* p, bb_handle** out) {
   bb_params pp;
   if (p) pp = *p; else bb_default_params(&pp);
   if (pp.n_terrains < 1) return fail("bb_create: n_terrains must be >= 1");
+  if (!(pp.opt_timestep >= 0 && pp.opt_timestep <= 0.1))
+    return fail("bb_create: opt_timestep %g out of range [0, 0.1] (0: ballbot.xml's 0.002)", pp.opt_timestep);
+  if (pp.opt_disableflags & ~(BB_DSBL_PASSIVE | BB_DSBL_GRAVITY))
+    return fail("bb_create: opt_disableflags 0x%x: only BB_DSBL_PASSIVE and BB_DSBL_GRAVITY are supported",
+                pp.opt_disableflags);
   int ndev = 0;
   HIPCHK(hipGetDeviceCount(&ndev));
   if (device < 0 || device >= ndev) return fail("bb_create: device %d out of range (%d devices)", device, ndev);
@@ -2066,7 +2107,14 @@ int bb_create(int n_envs, int device, const bb_params* p, bb_handle** out) {
     if (ps && atoi(ps) > 0) h->pair_seg = atoi(ps);
     const char* pa = getenv("BB_PAIR_ADAPT");
     if (pa) h->pair_adapt = atoi(pa) != 0;
-    h->pair_cap = prop.multiProcessorCount * 4;
+    // the persistent pair needs its whole grid resident: as many one-wave workgroups as the
+    // CUs hold at once (4 per CU: one 512-VGPR wave per SIMD), whole groups of NXCD
+    int per_cu = 0;
+    const int pe = bb_pair_setup_tu(h->fp64, &per_cu);
+    if (pe) return fail("bb_create: relief pair setup: %s", hipGetErrorString(hipError_t(pe)));
+    if (per_cu > 4) per_cu = 4;
+    h->pair_cap = prop.multiProcessorCount * per_cu / NXCD * NXCD;
+    if (h->pair_cap < 16 * NXCD) h->pair = 0;  // too small a chip for the pair: the one-launch work queue
     int wrate = 0;  // kHz
     if (hipDeviceGetAttribute(&wrate, hipDeviceAttributeWallClockRate, device) != hipSuccess || wrate <= 0)
       wrate = 100000;
@@ -2074,14 +2122,21 @@ int bb_create(int n_envs, int device, const bb_params* p, bb_handle** out) {
     if (po) h->pair_one = atoi(po) != 0;
     const char* so = getenv("BB_PAIR_SOLO");
     if (so) h->pair_solo = atoi(so) > 0 ? atoi(so) : 0;
-    if (h->pair_solo > h->pair_cap / 8) h->pair_solo = h->pair_cap / 8;
+    // the solo workgroups are the first full-kind ones: keep a whole group of non-solo full
+    // workgroups (every XCD label) inside the adapt floor of pair_cap / 8
+    if (h->pair_solo > h->pair_cap / 8 - NXCD) h->pair_solo = h->pair_cap / 8 - NXCD;
+    if (h->pair_solo < 0) h->pair_solo = 0;
     const char* hv = getenv("BB_PAIR_HEAVY");
     if (hv && atoi(hv) > 0) h->pair_heavy_pct = atoi(hv);
     const char* pb = getenv("BB_PAIR_BUDGET_MS");  // diagnostics (profilers that serialise launches)
     const unsigned long long ms = pb && atoll(pb) > 0 ? (unsigned long long)atoll(pb) : 20000ull;
     h->pair_budget = ms * (unsigned long long)wrate;
+    h->pair_budget_s = double(ms) * 1e-3;
   }
-  h->md = compile_model(sc);
+  OptCfg oc;
+  if (pp.opt_timestep > 0) oc.timestep = pp.opt_timestep;
+  oc.disable = pp.opt_disableflags;
+  h->md = compile_model(sc, oc);
   h->mf = cast_model<float>(h->md);
   // cam_k: body cam_k_body (pos (+-0.17, -0.01, -0.06), euler 180 -+30 0) and
   // camera euler 180 0 0 in it (ballbot.xml:44-54)
@@ -2137,12 +2192,19 @@ int bb_create(int n_envs, int device, const bb_params* p, bb_handle** out) {
     const char* pf = getenv("BB_PAIR_FULL");
     int pct = pf ? atoi(pf) : 50;
     pct = pct < 13 ? 13 : (pct > 87 ? 87 : pct);
-    const int ns = h->pair_cap * pct / 100;
-    int act[2] = {h->pair_cap - ns, ns};
+    const int G = h->pair_cap / NXCD, lo = (G + 7) / 8;
+    int gs = G * pct / 100;
+    gs = gs < lo ? lo : (gs > G - lo ? G - lo : gs);
+    int act[2] = {(G - gs) * NXCD, gs * NXCD};  // whole groups (pair_kind_of)
     HIPCHK(hipMemcpy(d.slow_count + SC_ACTIVE, act, sizeof act, hipMemcpyHostToDevice));
     HIPCHK(hipMemcpy(d.slow_count + SC_SOLO, &h->pair_solo, sizeof(int), hipMemcpyHostToDevice));
   }
   HIPCHK(hipMalloc((void**)&d.cost, sizeof(unsigned long long) * n));
+  // sticky fault word in host memory mapped into the device: a relief-pair launch that ends on its
+  // budget sets it, and every later call (and bb_check) reports it without a device sync
+  HIPCHK(hipHostMalloc((void**)&h->fault_host, sizeof(int), hipHostMallocMapped | hipHostMallocCoherent));
+  *h->fault_host = 0;
+  HIPCHK(hipHostGetDevicePointer((void**)&d.fault, (void*)h->fault_host, 0));
   HIPCHK(hipMemset(d.cost, 0, sizeof(unsigned long long) * n));
   HIPCHK(hipStreamCreateWithFlags(&h->side, hipStreamNonBlocking));
   HIPCHK(hipEventCreateWithFlags(&h->fork, hipEventDisableTiming));
@@ -2186,12 +2248,7 @@ int bb_create(int n_envs, int device, const bb_params* p, bb_handle** out) {
                          h->fp64 ? (const void*)relief_multi_kernel<double, true>
                                  : (const void*)relief_multi_kernel<float, true>};
     for (const void* k : qk) HIPCHK(hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, qlb));
-    const int plb = (int)(h->fp64 ? multi_lds_bytes<double>(4) : multi_lds_bytes<float>(4));
-    const void* pk[2] = {h->fp64 ? (const void*)relief_pair_kernel<double, false>
-                                 : (const void*)relief_pair_kernel<float, false>,
-                         h->fp64 ? (const void*)relief_pair_kernel<double, true>
-                                 : (const void*)relief_pair_kernel<float, true>};
-    for (const void* k : pk) HIPCHK(hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, plb));
+    // (the relief pair's kernels get theirs in their own unit: bb_pair_setup_tu)
   }
   *out = h;
   int rc = bb_reset(h, nullptr, nullptr, nullptr);
@@ -2215,6 +2272,7 @@ int bb_destroy(bb_handle* h) {
   (void)hipStreamDestroy(h->side); (void)hipEventDestroy(h->fork); (void)hipEventDestroy(h->join);
   for (hipEvent_t e : h->tev) (void)hipEventDestroy(e);
   (void)hipFree(h->scenes);
+  if (h->fault_host) (void)hipHostFree((void*)h->fault_host);
   delete h;
   return 0;
 }
@@ -2292,7 +2350,7 @@ int bb_render_depth(bb_handle* h, float* depth, float* rel_ts, int height, int w
   HIPCHK(hipSetDevice(h->device));
   RenderDev rd{h->n, h->d.qpos, h->d.steps, h->d.terrain, h->bank, h->size_z, h->hmax};
   if (!h->scenes) HIPCHK(hipMalloc(&h->scenes, scene_bytes(h->n)));
-  if (launch_depth(h->fp64 != 0, h->mf, h->rig, rd, height, width, every, force, 0.002f, h->scenes, depth, rel_ts,
+  if (launch_depth(h->fp64 != 0, h->mf, h->rig, rd, height, width, every, force, float(h->md.h), h->scenes, depth, rel_ts,
                    (hipStream_t)stream))
     return fail("bb_render_depth: launch failed: %s", hipGetErrorString(hipGetLastError()));
   return 0;
@@ -2481,8 +2539,26 @@ int bb_reset(bb_handle* h, const uint8_t* mask, float* obs, void* stream) {
   return 0;
 }
 
+// A relief-pair launch that ended on its wall-clock budget left the envs it had not finished
+// with their state at the launch's start but their terrain draws and counters advanced: the
+// handle refuses to step until a full bb_reset (which clears the fault on the device).
+static int faulted(const bb_handle* h, const char* what) {
+  return fail("%s: a bb_step_multi launch ended on its wall-clock budget (an env waited %.0f s for a step that "
+              "never came); the envs' states are inconsistent -- bb_reset(h, NULL, ...) clears this",
+              what, h->pair_budget_s);
+}
+
+int bb_check(bb_handle* h, void* stream) {
+  if (!h) return fail("bb_check: NULL handle");
+  HIPCHK(hipSetDevice(h->device));
+  HIPCHK(hipStreamSynchronize((hipStream_t)stream));
+  if (*h->fault_host) return faulted(h, "bb_check");
+  return 0;
+}
+
 int bb_step(bb_handle* h, const float* a, float* o, float* r, uint8_t* dn, float* t, float* p2, int ar, void* s) {
   if (!h) return fail("bb_step: NULL handle");
+  if (*h->fault_host) return faulted(h, "bb_step");
   if (!a || !o || !r || !dn) return fail("bb_step: actions/obs/reward/done must be non-NULL");
   return h->fp64 ? launch_step<double>(h, a, o, r, dn, t, p2, ar, (hipStream_t)s)
                  : launch_step<float>(h, a, o, r, dn, t, p2, ar, (hipStream_t)s);
@@ -2491,6 +2567,7 @@ int bb_step(bb_handle* h, const float* a, float* o, float* r, uint8_t* dn, float
 int bb_step_multi(bb_handle* h, const float* a, int k, float* o, float* r, uint8_t* dn, float* t, float* p2, int ar,
                   void* s) {
   if (!h) return fail("bb_step_multi: NULL handle");
+  if (*h->fault_host) return faulted(h, "bb_step_multi");
   if (!a || !o || !r || !dn) return fail("bb_step_multi: actions/obs/reward/done must be non-NULL");
   if (k < 1) return fail("bb_step_multi: k_steps must be >= 1 (got %d)", k);
   return h->fp64 ? launch_multi<double>(h, a, k, o, r, dn, t, p2, ar, (hipStream_t)s)
@@ -2499,6 +2576,7 @@ int bb_step_multi(bb_handle* h, const float* a, int k, float* o, float* r, uint8
 
 int bb_rollout(bb_handle* h, const bb_rollout_args* a, void* stream) {
   if (!h) return fail("bb_rollout: NULL handle");
+  if (*h->fault_host) return faulted(h, "bb_rollout");
   if (!a || !a->params || !a->noise || !a->obs || !a->last_starts || !a->ep_ret || !a->ep_len || !a->buf_obs ||
       !a->buf_actions || !a->buf_values || !a->buf_log_prob || !a->buf_rewards || !a->buf_starts || !a->ep_r_out ||
       !a->ep_l_out)

@@ -60,8 +60,17 @@ inline SolverCfg default_solver(bool fp64) {
   return SolverCfg{2e-6, 1e-3, 3e-7, 16, 16};
 }
 
+// mjModel.opt overrides (bb_params.opt_timestep / opt_disableflags): the step
+// size and MuJoCo's mjDSBL_PASSIVE / mjDSBL_GRAVITY switches, for the physics
+// invariants of SURVEY.md §8 C1 (RK4 order, momentum conservation).  Defaults:
+// ballbot.xml's 0.002 s, everything enabled.
+struct OptCfg {
+  double timestep = 0.002;
+  int disable = 0;  // BB_DSBL_PASSIVE (32), BB_DSBL_GRAVITY (64): MuJoCo's bit values
+};
+
 // Compile ballbot.xml (values cited per line) into a double-precision model.
-inline ModelT<double> compile_model(const SolverCfg& sc) {
+inline ModelT<double> compile_model(const SolverCfg& sc, const OptCfg& opt = OptCfg{}) {
   using namespace detail;
   const double pi = 3.14159265358979323846;
   ModelT<double> m;
@@ -147,7 +156,7 @@ inline ModelT<double> compile_model(const SolverCfg& sc) {
       mv3(m.u[k], R, m.axis);
     }
     m.wheel_r = 0.025; m.wheel_hh = 0.02;
-    m.armature = 0.005; m.damping = 0.8;
+    m.armature = 0.005; m.damping = (opt.disable & 32) ? 0.0 : 0.8;  // mjDSBL_PASSIVE drops the joint damping
   }
   // ---- ball (ballbot.xml:76-79): sphere r .09 density 55 at (0,0,-0.14)
   m.ball_r = 0.09;
@@ -155,8 +164,8 @@ inline ModelT<double> compile_model(const SolverCfg& sc) {
   m.IB = 0.4 * m.mB * 0.09 * 0.09;
   m.dz = -0.14;
   // ---- options (ballbot.xml:3-5) + MuJoCo defaults
-  m.h = 0.002;
-  m.grav = 9.81;
+  m.h = opt.timestep;
+  m.grav = (opt.disable & 64) ? 0.0 : 9.81;  // mjDSBL_GRAVITY
   m.hf_sx = 5; m.hf_sy = 5; m.hf_bottom = 0.1;  // hfield size (ballbot.xml:23)
   m.solimp[0] = 0.9; m.solimp[1] = 0.95; m.solimp[2] = 0.001; m.solimp[3] = 0.5; m.solimp[4] = 2;
   {

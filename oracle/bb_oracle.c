@@ -53,12 +53,8 @@ static const double PI = 3.14159265358979323846;
 static int g_flags = 0;
 static int g_maxiter = 100;          /* MuJoCo default opt.iterations */
 static double g_tol = 1e-8;          /* MuJoCo default opt.tolerance */
-/* line search: MuJoCo's criterion |phi'| <= ls_tolerance |phi'(0)| within
- * ls_iterations evaluations, on the kernel's 1-D search (newton(); MuJoCo's own
- * search path is not restated: parity unpinned).  bbo_set_flags(2048) selects
- * the earlier rounds' exact search instead (Newton/bisection to g_lstol; with
- * g_lstol 0.01 that simple search leaves rare steps far from the minimiser, up
- * to 1e-4 in qpos against the kernel). */
+/* line search: MuJoCo's PrimalSearch (newton() below) with opt.ls_tolerance and
+ * opt.ls_iterations; converged when |phi'| < tolerance * ls_tolerance * |s| / scale */
 static double g_lstol = 0.01;        /* MuJoCo default opt.ls_tolerance */
 static int g_lsmax = 50;             /* MuJoCo default opt.ls_iterations */
 
@@ -67,6 +63,9 @@ void bbo_set_flags(int flags) { g_flags = flags; }
 int bbo_get_flags(void) { return g_flags; }
 void bbo_set_solver(int maxiter, double tol) { g_maxiter = maxiter; g_tol = tol; }
 void bbo_set_linesearch(int ls_iterations, double ls_tolerance) { g_lsmax = ls_iterations; g_lstol = ls_tolerance; }
+/* opt.timestep (the RK4 convergence test; 0 restores ballbot.xml's 0.002) */
+static double TIMESTEP = 0.002;
+void bbo_set_timestep(double h) { TIMESTEP = h > 0 ? h : 0.002; }
 
 /* ------------------------------------------------------------- small maths */
 static void v3copy(double* r, const double* a) { r[0] = a[0]; r[1] = a[1]; r[2] = a[2]; }
@@ -170,7 +169,7 @@ static const double BALL_GPOS[3] = {0, 0, -0.14};
 static const double WHEEL_R = 0.025, WHEEL_HH = 0.02, WHEEL_RHO = 620.0; /* :57 */
 static const double WHEEL_GPOS[3] = {-0.018, -0.08, -0.053};
 static const double HF_SIZE[4] = {5, 5, 2.0, 0.1};            /* ballbot.xml:23 */
-static const double TIMESTEP = 0.002;                         /* ballbot.xml:3 */
+/* TIMESTEP: ballbot.xml:3, 0.002 (defined with the options above; bbo_set_timestep) */
 static const double GRAVITY = 9.81;                           /* MuJoCo default */
 
 typedef struct {
@@ -1198,130 +1197,194 @@ static double total_cost(const Efc* e, const double* jar, double* force, double*
   return cost;
 }
 
-/* One contact's terms of phi(alpha) = f(a + alpha s) along the search line:
- * the cone variables U(alpha) = u0 + alpha du (U0 = mu jar0, U1 = f1 jar1,
- * U2 = f2 jar2, as cone_eval), phi_c' and phi_c'' in closed form per zone, and
- * the alpha of the contact's near-kink (the smallest T on the line, when the
- * contact is in the middle zone there).  The kernel's LsTerm (bb_solve.h). */
-typedef struct { double u0[3], du[3], mu, Dm, b0, b1, vv, kink, c0; } LsTerm;
+/* ------------------------------------------------------------------------
+ * mj_solNewton: MuJoCo's primal solver with flg_Newton (mj_solPrimal,
+ * PrimalUpdateConstraint/-Gradient, PrimalPrepare/-Eval/-Search in
+ * engine_solver.c at the commit the reference pins, 99490163, Readme.md:101-103).
+ * MuJoCo is not in /root/reference, so this restatement of its published source
+ * is PARITY UNPINNED [MJ].  The GPU kernel keeps its own line search (bb_solve.h
+ * LineSearch); tests/ hold the two to a stated tolerance, not to bit equality.
+ *
+ *   cost(a)   = 0.5 (a - a0)' M (a - a0) + sum_c phi_c(J_c a - aref_c)   (Gauss + elliptic cones)
+ *   iteration H = M + sum_c J_c' C_c J_c (cone Hessians, incl. the middle zone's
+ *             cross terms); search s = -H^-1 grad; alpha = PrimalSearch(s); a += alpha s;
+ *             recompute cost and gradient; stop when alpha == 0, or
+ *             scale (oldcost - cost) < tolerance, or scale |grad| < tolerance
+ *             (scale = 1 / (meaninertia max(1, nv)))
+ *   search    MuJoCo's PrimalSearch: p1 = one Newton step from alpha 0 (kept only if it
+ *             lowers the cost); converged when |phi'(alpha)| < gtol with
+ *             gtol = tolerance ls_tolerance |s| / scale; else Newton steps in the
+ *             descent direction until phi' changes sign (the bracket [p2, p1]), then
+ *             rounds of three candidates -- the Newton points of both bracket ends
+ *             and the midpoint -- returning the cheapest converged candidate, or
+ *             moving each bracket end to a candidate with a same-signed, smaller |phi'|;
+ *             every evaluation counts against ls_iterations.
+ * ------------------------------------------------------------------------ */
 
-static void ls_prep(LsTerm* t, const double* j0, const double* x, double mu, double f1, double f2,
-                    const double* D, double Dm) {
-  t->mu = mu; t->Dm = Dm;
+/* One contact along the search line (PrimalPrepare for an elliptic cone): the cone
+ * variables U(alpha) = u0 + alpha du (U0 = mu jar0, U1 = f1 jar1, U2 = f2 jar2, as
+ * cone_eval) and the bottom zone's quadratic in alpha (c0, b0, b1). */
+typedef struct { double u0[3], du[3], mu, Dm, b0, b1, c0, vv; } ConeLine;
+
+static void cone_line_prep(ConeLine* t, const double* j0, const double* x, double mu, double f1, double f2,
+                           const double* D) {
+  t->mu = mu;
+  t->Dm = D[0] / (mu * mu * (1 + mu * mu));
   t->u0[0] = mu * j0[0]; t->u0[1] = f1 * j0[1]; t->u0[2] = f2 * j0[2];
   t->du[0] = mu * x[0]; t->du[1] = f1 * x[1]; t->du[2] = f2 * x[2];
   t->b0 = D[0] * j0[0] * x[0] + D[1] * j0[1] * x[1] + D[2] * j0[2] * x[2];
   t->b1 = D[0] * x[0] * x[0] + D[1] * x[1] * x[1] + D[2] * x[2] * x[2];
   t->c0 = 0.5 * (D[0] * j0[0] * j0[0] + D[1] * j0[1] * j0[1] + D[2] * j0[2] * j0[2]);
   t->vv = t->du[1] * t->du[1] + t->du[2] * t->du[2];
-  t->kink = -1;
-  if (t->vv > 0) {
-    const double ak = -(t->u0[1] * t->du[1] + t->u0[2] * t->du[2]) / t->vv;
-    const double N = t->u0[0] + ak * t->du[0], U1 = t->u0[1] + ak * t->du[1], U2 = t->u0[2] + ak * t->du[2];
-    const double Tn = sqrt(U1 * U1 + U2 * U2);
-    if (ak > 0 && N < mu * Tn && mu * N + Tn > 0) t->kink = ak;
+}
+
+/* the contact's cost phi_c(alpha) and its first two derivatives (PrimalEval), by
+ * cone_eval's zones: top (N >= mu T) nothing; bottom (mu N + T <= 0) the three
+ * rows' quadratics; middle 0.5 Dm (N - mu T)^2 with T(alpha) a hyperbola */
+static void cone_line_eval(const ConeLine* t, double alpha, double* cost, double* d0, double* d1) {
+  const double N = t->u0[0] + alpha * t->du[0], U1 = t->u0[1] + alpha * t->du[1], U2 = t->u0[2] + alpha * t->du[2];
+  const double T = sqrt(U1 * U1 + U2 * U2), mu = t->mu;
+  if (N >= mu * T) return;
+  if (mu * N + T <= 0) {
+    *cost += t->c0 + alpha * (t->b0 + 0.5 * alpha * t->b1);
+    *d0 += t->b0 + alpha * t->b1;
+    *d1 += t->b1;
+    return;
   }
-}
-
-static void ls_eval(const LsTerm* t, double alpha, double* d1, double* d2, double* dm) {
-  const double N = t->u0[0] + alpha * t->du[0], U1 = t->u0[1] + alpha * t->du[1], U2 = t->u0[2] + alpha * t->du[2];
-  const double t2 = U1 * U1 + U2 * U2;
-  const double rt = t2 > 0 ? 1 / sqrt(t2) : 0;
-  const double Tn = t2 * rt, mu = t->mu;
-  const int top = (N >= mu * Tn) || (Tn <= 0 && N >= 0);
-  const int bot = !top && ((mu * N + Tn <= 0) || (Tn <= 0 && N < 0));
-  const double g = N - mu * Tn;
-  const double tp = (U1 * t->du[1] + U2 * t->du[2]) * rt;
+  /* middle zone: T > 0 here (T = 0 would need N < 0 and mu N > 0) */
+  const double g = N - mu * T;
+  const double tp = (U1 * t->du[1] + U2 * t->du[2]) / T;
+  const double tpp = (t->vv - tp * tp) / T;
   const double gp = t->du[0] - mu * tp;
-  const double tpp = (t->vv - tp * tp) * rt;
-  const double Dg = t->Dm * g;
-  if (top) return;
-  if (bot) { *d1 += t->b0 + alpha * t->b1; *d2 += t->b1; *dm += fabs(t->b0) + fabs(alpha * t->b1); return; }
-  *d1 += Dg * gp;
-  *d2 += t->Dm * gp * gp - mu * Dg * tpp;
-  *dm += fabs(Dg) * (fabs(t->du[0]) + mu * fabs(tp));
+  *cost += 0.5 * t->Dm * g * g;
+  *d0 += t->Dm * g * gp;
+  *d1 += t->Dm * (gp * gp - mu * g * tpp);
 }
 
-/* the contact's constraint cost phi_c(alpha) (cone_eval's zones) */
-static double ls_cost(const LsTerm* t, double alpha) {
-  const double N = t->u0[0] + alpha * t->du[0], U1 = t->u0[1] + alpha * t->du[1], U2 = t->u0[2] + alpha * t->du[2];
-  const double Tn = sqrt(U1 * U1 + U2 * U2);
-  const int top = N >= t->mu * Tn;
-  const int bot = !top && t->mu * N + Tn <= 0;
-  const double g = N - t->mu * Tn;
-  return top ? 0 : (bot ? t->c0 + alpha * (t->b0 + 0.5 * alpha * t->b1) : 0.5 * t->Dm * g * g);
+/* a point of the line search (mjPrimalPnt): alpha, cost, phi', phi'' */
+typedef struct { double alpha, cost, d0, d1; } PrimalPnt;
+
+typedef struct {
+  int nc, evals;
+  double q0, q1, q2;  /* Gauss cost on the line: q0 + alpha q1 + alpha^2 q2 */
+  const ConeLine* cl;
+} PrimalLine;
+
+static void primal_eval(PrimalLine* L, PrimalPnt* p) {
+  const double a = p->alpha;
+  double cost = L->q0 + a * (L->q1 + a * L->q2), d0 = L->q1 + 2 * a * L->q2, d1 = 2 * L->q2;
+  for (int c = 0; c < L->nc; c++) cone_line_eval(&L->cl[c], a, &cost, &d0, &d1);
+  p->cost = cost; p->d0 = d0; p->d1 = d1;
+  L->evals++;
 }
 
-/* The 1-D search on phi' (convex phi): bracket [lo, hi], 1-D Newton from the
- * latest point while it lands inside the bracket and its step is under half
- * the step before the last one, else Illinois false position; a step that would
- * cross a contact's kink stops at it.  The kernel's LineSearch (bb_solve.h). */
-typedef struct { double lo, dlo, hi, dhi, alpha, flo, fhi, prev, dx, dxold; int side, same; } LineSearch;
-
-static void lsr_init(LineSearch* L, double d0) {
-  L->lo = 0; L->dlo = d0; L->hi = -1; L->dhi = 0; L->alpha = 1; L->flo = d0; L->fhi = 0; L->prev = 0;
-  L->dx = L->dxold = 1e30;
-  L->side = 0; L->same = 0;
-}
-static int lsr_crosses(const LineSearch* L, double k) {
-  const int between = L->alpha > L->prev ? (k > L->prev && k < L->alpha) : (k < L->prev && k > L->alpha);
-  return between && k > L->lo && (L->hi < 0 || k < L->hi);
-}
-static void lsr_update(LineSearch* L, double d1, double d2) {
-  L->prev = L->alpha;
-  const int neg = d1 < 0, sd = neg ? -1 : 1;
-  L->same = sd == L->side ? L->same + 1 : 0;
-  L->side = sd;
-  const int rep = L->same > 0;
-  const double hlo = (!neg && rep) ? 0.5 : 1, hhi = (neg && rep && L->hi >= 0) ? 0.5 : 1;
-  if (neg) { L->lo = L->alpha; L->dlo = d1; L->flo = d1; L->fhi *= hhi; }
-  else { L->flo *= hlo; L->hi = L->alpha; L->dhi = d1; L->fhi = d1; }
-  const double an_n = L->alpha - d1 / (d2 > 1e-30 ? d2 : 1e-30);
-  const double fp = L->lo - L->flo * (L->hi - L->lo) / (L->fhi - L->flo);
-  const double an_f = (fp > L->lo && fp < L->hi) ? fp : 0.5 * (L->lo + L->hi);
-  const double an_o = an_n > L->lo ? an_n : (L->lo > 0 ? 2 * L->lo : 1);
-  const int nw = an_n > L->lo && an_n < L->hi && fabs(an_n - L->alpha) <= 0.5 * L->dxold;
-  const double an = L->hi < 0 ? an_o : (nw ? an_n : an_f);
-  L->dxold = L->dx;
-  L->dx = fabs(an - L->alpha);
-  L->alpha = an;
-}
-static void lsr_snap(LineSearch* L, double k) { L->alpha = k; L->dx = fabs(k - L->prev); }
-static double lsr_fallback(const LineSearch* L) {
-  return L->lo > 0 ? L->lo : (L->hi > 0 ? L->hi * L->dlo / (L->dlo - L->dhi) : 0);
+/* updateBracket: move bracket end p to a candidate on its side of the minimum
+ * (same sign of phi') with a smaller |phi'|; then its Newton point pnext */
+static int update_bracket(PrimalLine* L, PrimalPnt* p, PrimalPnt* const cand[3], PrimalPnt* pnext) {
+  int flag = 0;
+  for (int i = 0; i < 3; i++) {
+    if (p->d0 < 0 && cand[i]->d0 < 0 && p->d0 < cand[i]->d0) { *p = *cand[i]; flag = 1; }
+    else if (p->d0 > 0 && cand[i]->d0 > 0 && p->d0 > cand[i]->d0) { *p = *cand[i]; flag = 2; }
+  }
+  if (flag) {
+    pnext->alpha = p->alpha - p->d0 / p->d1;
+    primal_eval(L, pnext);
+  }
+  return flag;
 }
 
-/* Newton solve of min 0.5(a-a0)'M(a-a0) + s(Ja - aref) (mj_solNewton) */
-static int newton(const Efc* e, const double* Mm, const double* a0, double* a, double scale) {
-  int nr = 3 * e->nc, it;
+/* PrimalSearch -> alpha (0: no improvement) */
+static double primal_search(PrimalLine* L, double snorm, double scale) {
+  if (snorm < MJMINVAL) return 0;
+  const double gtol = g_tol * g_lstol * snorm / scale;
+  PrimalPnt p0, p1, p2, pmid, p1next, p2next;
+  L->evals = 0;
+  p0.alpha = 0;
+  primal_eval(L, &p0);
+  p1.alpha = p0.alpha - p0.d0 / p0.d1;  /* always attempt one Newton step */
+  primal_eval(L, &p1);
+  if (p0.cost < p1.cost) p1 = p0;
+  if (fabs(p1.d0) < gtol) return p1.alpha;  /* initial convergence (alpha 0: no improvement) */
+  const double dir = p1.d0 < 0 ? 1 : -1;
+  int p2update = 0;
+  while (p1.d0 * dir <= -gtol && L->evals < g_lsmax) {  /* one-sided: Newton steps until phi' changes sign */
+    p2 = p1;
+    p2update = 1;
+    p1.alpha -= p1.d0 / p1.d1;
+    primal_eval(L, &p1);
+    if (fabs(p1.d0) < gtol) return p1.alpha;
+  }
+  if (L->evals >= g_lsmax || !p2update) return p1.alpha;  /* could not bracket */
+  p1next.alpha = p1.alpha - p1.d0 / p1.d1;
+  primal_eval(L, &p1next);
+  p2next.alpha = p2.alpha - p2.d0 / p2.d1;
+  primal_eval(L, &p2next);
+  while (L->evals < g_lsmax) {  /* bracketed */
+    pmid.alpha = 0.5 * (p1.alpha + p2.alpha);
+    primal_eval(L, &pmid);
+    PrimalPnt* const cand[3] = {&p1next, &p2next, &pmid};
+    int best = -1;
+    double bestcost = 0;
+    for (int i = 0; i < 3; i++)
+      if (fabs(cand[i]->d0) < gtol && (best < 0 || cand[i]->cost < bestcost)) { bestcost = cand[i]->cost; best = i; }
+    if (best >= 0) return cand[best]->alpha;
+    /* both ends update from the same three candidates (copies: p1's update must not move p2's) */
+    PrimalPnt c0 = p1next, c1 = p2next, c2 = pmid;
+    PrimalPnt* const cc[3] = {&c0, &c1, &c2};
+    const int b1 = update_bracket(L, &p1, cc, &p1next);
+    const int b2 = update_bracket(L, &p2, cc, &p2next);
+    if (!b1 && !b2) return pmid.alpha;  /* numerical accuracy reached: the midpoint */
+  }
+  /* out of evaluations: the better bracket end, if it improves on alpha 0 */
+  if (p1.cost <= p2.cost && p1.cost < p0.cost) return p1.alpha;
+  if (p2.cost <= p1.cost && p2.cost < p0.cost) return p2.alpha;
+  return 0;
+}
+
+/* the solver's state at qacc a (PrimalUpdateConstraint + PrimalUpdateGradient):
+ * jar = J a - aref, cone forces and Hessians, cost = Gauss + constraint, grad */
+typedef struct {
   double jar[BBO_MAXCON * 3], force[BBO_MAXCON * 3], Hc[BBO_MAXCON * 9];
+  double dq[NV], Mdq[NV], grad[NV], cost;
+} PrimalState;
+
+static void primal_update(const Efc* e, const double* Mm, const double* a0, const double* a, PrimalState* S) {
+  const int nr = 3 * e->nc;
+  for (int r = 0; r < nr; r++) { double s = -e->aref[r]; for (int d = 0; d < NV; d++) s += e->J[r][d] * a[d]; S->jar[r] = s; }
+  const double ccost = total_cost(e, S->jar, S->force, S->Hc);
+  double gauss = 0;
+  for (int d = 0; d < NV; d++) S->dq[d] = a[d] - a0[d];
+  for (int i = 0; i < NV; i++) {
+    double s = 0;
+    for (int j = 0; j < NV; j++) s += Mm[i * NV + j] * S->dq[j];
+    S->Mdq[i] = s;
+    gauss += 0.5 * S->dq[i] * s;
+  }
+  for (int i = 0; i < NV; i++) {
+    double s = S->Mdq[i];
+    for (int r = 0; r < nr; r++) s -= e->J[r][i] * S->force[r];
+    S->grad[i] = s;
+  }
+  S->cost = gauss + ccost;
+}
+
+/* Newton solve of min 0.5(a-a0)'M(a-a0) + s(Ja - aref) from a (the warm start) */
+static int newton(const Efc* e, const double* Mm, const double* a0, double* a, double scale) {
+  const int nr = 3 * e->nc;
+  static __thread PrimalState S;
+  static __thread ConeLine cl[BBO_MAXCON];
+  primal_update(e, Mm, a0, a, &S);
+  int it;
   for (it = 0; it < g_maxiter; it++) {
-    for (int r = 0; r < nr; r++) { double s = -e->aref[r]; for (int d = 0; d < NV; d++) s += e->J[r][d] * a[d]; jar[r] = s; }
-    double ccost = total_cost(e, jar, force, Hc);
-    double grad[NV], dq[NV];
-    for (int d = 0; d < NV; d++) dq[d] = a[d] - a0[d];
-    if (g_flags & 512) {  /* diagnostics: MuJoCo's cost = Gauss + constraint */
-      double gauss = 0;
-      for (int i = 0; i < NV; i++) for (int j = 0; j < NV; j++) gauss += 0.5 * dq[i] * Mm[i * NV + j] * dq[j];
-      fprintf(stderr, "C %d %.17g\n", it, scale * (gauss + ccost));
+    if (g_flags & 256) {
+      double gn = 0;
+      for (int i = 0; i < NV; i++) gn += S.grad[i] * S.grad[i];
+      fprintf(stderr, "it %d cost %.17g grad %.3e\n", it, scale * S.cost, scale * sqrt(gn));
     }
-    for (int i = 0; i < NV; i++) {
-      double s = 0;
-      for (int j = 0; j < NV; j++) s += Mm[i * NV + j] * dq[j];
-      for (int r = 0; r < nr; r++) s -= e->J[r][i] * force[r];
-      grad[i] = s;
-    }
-    double gn = 0;
-    for (int i = 0; i < NV; i++) gn += grad[i] * grad[i];
-    if (g_flags & 256) fprintf(stderr, "it %d gn %.3e\n", it, scale * sqrt(gn));
-    if (g_flags & 512) fprintf(stderr, "G %d %.17g\n", it, scale * sqrt(gn));
-    /* MuJoCo's gradient stop: scale * ||grad|| < opt.tolerance, tested after an
-     * iteration (mj_solPrimal, engine_solver.c; the first iteration always runs) */
-    if (it > 0 && scale * sqrt(gn) < g_tol) break;
     double H[NV * NV];
     memcpy(H, Mm, sizeof H);
     for (int c = 0; c < e->nc; c++) {
-      const double* C = Hc + 9 * c;
+      const double* C = S.Hc + 9 * c;
       for (int p = 0; p < 3; p++)
         for (int q = 0; q < 3; q++) {
           double w = C[3 * p + q];
@@ -1334,97 +1397,44 @@ static int newton(const Efc* e, const double* Mm, const double* a0, double* a, d
         }
     }
     if (chol(H, NV)) break;
-    double s[NV];
-    for (int i = 0; i < NV; i++) s[i] = -grad[i];
+    double s[NV], snorm = 0;
+    for (int i = 0; i < NV; i++) s[i] = -S.grad[i];
     chol_solve(H, NV, s);
-    /* line search on phi(alpha) = f(a + alpha s) */
-    double Ms[NV], sMs = 0, sMdq = 0, Js[BBO_MAXCON * 3];
+    for (int i = 0; i < NV; i++) snorm += s[i] * s[i];
+    snorm = sqrt(snorm);
+    /* the line: Gauss quadratic and each contact's cone terms */
+    double Ms[NV], Js[BBO_MAXCON * 3], sMs = 0, sMdq = 0;
     for (int i = 0; i < NV; i++) { double t = 0; for (int j = 0; j < NV; j++) t += Mm[i * NV + j] * s[j]; Ms[i] = t; }
-    for (int i = 0; i < NV; i++) { sMs += s[i] * Ms[i]; sMdq += Ms[i] * dq[i]; }
+    for (int i = 0; i < NV; i++) { sMs += s[i] * Ms[i]; sMdq += s[i] * S.Mdq[i]; }
     for (int r = 0; r < nr; r++) { double t = 0; for (int d = 0; d < NV; d++) t += e->J[r][d] * s[d]; Js[r] = t; }
-    double d0 = 0, alpha;
-    double jt[BBO_MAXCON * 3], ft[BBO_MAXCON * 3];
-    static __thread LsTerm lt[BBO_MAXCON];
-    const int exact = (g_flags & 2048) != 0;
-    for (int r = 0; r < nr; r++) d0 -= force[r] * Js[r];
-    d0 += sMdq;
-    if (d0 >= 0) break; /* not a descent direction: converged to roundoff */
-    if (exact) { /* the exact search of earlier rounds: Newton/bisection on phi' to g_lstol */
-      double lo = 0, hi = -1, Ht[BBO_MAXCON * 9];
-      alpha = 1;
-      for (int ls = 0; ls < g_lsmax; ls++) {
-        for (int r = 0; r < nr; r++) jt[r] = jar[r] + alpha * Js[r];
-        total_cost(e, jt, ft, Ht);
-        double d1 = sMdq + alpha * sMs, d2 = sMs;
-        for (int c = 0; c < e->nc; c++) {
-          for (int p = 0; p < 3; p++) {
-            d1 -= ft[3 * c + p] * Js[3 * c + p];
-            for (int q = 0; q < 3; q++) d2 += Js[3 * c + p] * Ht[9 * c + 3 * p + q] * Js[3 * c + q];
-          }
-        }
-        if (fabs(d1) <= g_lstol * fabs(d0)) break;
-        if (d1 < 0) lo = alpha; else hi = alpha;
-        double an = alpha - d1 / d2;
-        if (hi < 0) { if (an <= lo) an = 2 * alpha; }
-        else if (!(an > lo && an < hi)) an = 0.5 * (lo + hi);
-        if (hi >= 0 && hi - lo <= 1e-16 * hi) break;
-        alpha = an;
-      }
-    } else {
-      /* MuJoCo stops its line search at |phi'| <= ls_tolerance |phi'(0)| within
-       * ls_iterations; its search path is not restated (parity unpinned).  The
-       * oracle runs the kernel's 1-D search (bb_solve.h LineSearch: safeguarded
-       * Newton / Illinois false position, steps stopped at contact kinks) to that
-       * criterion, so that the Newton iterates, and with them MuJoCo's
-       * improvement stop below, are the kernel's up to roundoff */
-      for (int c = 0; c < e->nc; c++)
-        ls_prep(&lt[c], jar + 3 * c, Js + 3 * c, e->mu[c], e->fr[c][0], e->fr[c][1], e->D + 3 * c,
-                e->D[3 * c] / (e->mu[c] * e->mu[c] * (1 + e->mu[c] * e->mu[c])));
-      LineSearch L;
-      lsr_init(&L, d0);
-      int ok = 0;
-      for (int ls = 1; ls <= g_lsmax; ls++) {
-        double d1p = 0, d2p = 0, dmp = 0;
-        for (int c = 0; c < e->nc; c++) ls_eval(&lt[c], L.alpha, &d1p, &d2p, &dmp);
-        const double d1 = sMdq + L.alpha * sMs + d1p;
-        if (fabs(d1) <= g_lstol * fabs(d0)) { ok = 1; break; }
-        const double dmag = fabs(sMdq) + fabs(L.alpha * sMs) + dmp;
-        if (fabs(d1) <= 32 * DBL_EPSILON * dmag) { ok = 1; break; }
-        if (d1 != d1) break;
-        lsr_update(&L, d1, sMs + d2p);
-        const int up = L.alpha > L.prev;
-        double kn = -1;
-        for (int c = 0; c < e->nc; c++)
-          if (lsr_crosses(&L, lt[c].kink) && (kn < 0 || (up ? lt[c].kink < kn : lt[c].kink > kn))) kn = lt[c].kink;
-        if (kn > 0) lsr_snap(&L, kn);
-      }
-      if (!ok) L.alpha = lsr_fallback(&L);
-      alpha = L.alpha;
-      if (!(alpha > 0)) break;
-    }
-    if (g_flags & 256) fprintf(stderr, "   alpha %.6e d0 %.3e\n", alpha, d0);
-    /* the cost change of the step: Gauss term alpha s'M(a - a0) + alpha^2 s'Ms / 2
-     * (closed form on the line) plus the constraint cost at a + alpha s minus at a */
-    double dcost = alpha * (sMdq + 0.5 * alpha * sMs);
-    if (exact) {
-      for (int r = 0; r < nr; r++) jt[r] = jar[r] + alpha * Js[r];
-      dcost += total_cost(e, jt, ft, NULL) - ccost;
-    } else { /* per contact, as the kernel sums it (phi_c(alpha) - phi_c(0), bb_team16.h solve16) */
-      double dc = 0;
-      for (int c = 0; c < e->nc; c++) dc += ls_cost(&lt[c], alpha) - ls_cost(&lt[c], 0);
-      dcost += dc;
-    }
-    double snorm = 0, anorm = 0;
-    for (int i = 0; i < NV; i++) { a[i] += alpha * s[i]; snorm += (alpha * s[i]) * (alpha * s[i]); anorm += a[i] * a[i]; }
-    /* roundoff floor: the step no longer moves qacc */
-    if (sqrt(snorm) <= 1e-15 * (1 + sqrt(anorm))) { it++; break; }
-    /* MuJoCo's improvement stop: scale * (oldcost - cost) < opt.tolerance after the
-     * iteration (mj_solPrimal, engine_solver.c, MuJoCo 99490163 as pinned by the
-     * reference, Readme.md:101-103): the Newton solve ends when either the scaled
-     * cost decrease or the scaled gradient falls below the tolerance */
-    if (-scale * dcost < g_tol) { it++; break; }
+    for (int c = 0; c < e->nc; c++)
+      cone_line_prep(&cl[c], S.jar + 3 * c, Js + 3 * c, e->mu[c], e->fr[c][0], e->fr[c][1], e->D + 3 * c);
+    PrimalLine L;
+    L.nc = e->nc; L.cl = cl;
+    L.q0 = S.cost - total_cost(e, S.jar, S.force, NULL);  /* the Gauss part of the cost */
+    L.q1 = sMdq; L.q2 = 0.5 * sMs;
+    const double alpha = primal_search(&L, snorm, scale);
+    if (g_flags & 256) fprintf(stderr, "   alpha %.6e evals %d\n", alpha, L.evals);
+    if (alpha == 0) break;  /* no improvement */
+    for (int i = 0; i < NV; i++) a[i] += alpha * s[i];
+    const double oldcost = S.cost;
+    primal_update(e, Mm, a0, a, &S);
+    double gn = 0;
+    for (int i = 0; i < NV; i++) gn += S.grad[i] * S.grad[i];
+    if (scale * (oldcost - S.cost) < g_tol || scale * sqrt(gn) < g_tol) { it++; break; }
   }
   return it;
+}
+
+/* mj_fwdConstraint's warm start for the primal solvers: qacc_warmstart if its
+ * total cost (Gauss + constraint) is not above the constraint cost of qacc_smooth
+ * (whose Gauss cost is 0), else qacc_smooth [MJ] */
+static void warmstart_choice(const Efc* e, const double* Mm, const double* a0, const double* warm, double* a) {
+  static __thread PrimalState S;
+  primal_update(e, Mm, a0, warm, &S);
+  const double cw = S.cost;
+  primal_update(e, Mm, a0, a0, &S);
+  memcpy(a, cw > S.cost ? a0 : warm, NV * sizeof(double));
 }
 
 /* -------------------------------------------------------------- forward */
@@ -1555,8 +1565,9 @@ static void forward_impl(const double* qpos, const double* qvel, const double* c
   int niter = 0;
   if (nc == 0) memcpy(a, a0, sizeof a);
   else {
-    if (warm_io) memcpy(a, warm_io, sizeof a); else memcpy(a, a0, sizeof a);
-    for (int i = 0; i < NV; i++) if (!isfinite(a[i])) { memcpy(a, a0, sizeof a); break; }
+    int finite = warm_io != NULL;
+    for (int i = 0; finite && i < NV; i++) finite = isfinite(warm_io[i]);
+    if (finite) warmstart_choice(&E, w->M, a0, warm_io, a); else memcpy(a, a0, sizeof a);
     BBO_PHASE(3);
     niter = newton(&E, w->M, a0, a, 1.0 / (m->meaninertia * NV));
   }
@@ -1581,6 +1592,13 @@ static void forward_impl(const double* qpos, const double* qvel, const double* c
       out->con_body2[c] = con[c].body2;
       out->con_body1[c] = con[c].body1;
     }
+    /* efc_force of each contact (contact frame: normal, then the two tangents) at the solution */
+    {
+      static __thread double jar[BBO_MAXCON * 3], frc[BBO_MAXCON * 3];
+      for (int r = 0; r < 3 * nc; r++) { double s = -E.aref[r]; for (int d = 0; d < NV; d++) s += E.J[r][d] * a[d]; jar[r] = s; }
+      total_cost(&E, jar, frc, NULL);
+      memcpy(out->con_force, frc, 3 * nc * sizeof(double));
+    }
     double ek = 0;
     for (int i = 0; i < NV; i++) for (int j = 0; j < NV; j++) ek += 0.5 * qvel[i] * w->M[i * NV + j] * qvel[j];
     double ep = 0;
@@ -1594,6 +1612,39 @@ void bbo_forward(const double* qpos, const double* qvel, const double* ctrl, con
   double w[NV];
   if (warm) memcpy(w, warm, sizeof w);
   forward_impl(qpos, qvel, ctrl, warm ? w : NULL, hfield, size_z, out);
+}
+
+/* Momentum of the bodies (invariant tests): per tree the spatial
+ * momentum sum_b cinert_b cvel_b about the tree's subtree COM (cvel_b = sum of the
+ * chain's cdof qvel), moved to the system COM.  Hinge armature is joint-space
+ * inertia invariant under a rigid motion of the whole, so these bodies' momenta are
+ * what gravity-free, contact-free, undamped motion conserves. */
+void bbo_momentum(const double* qpos, const double* qvel, double* out) {
+  compile_model();
+  Model* m = &M_;
+  static __thread Work W_;
+  Work* w = &W_;
+  kinematics_all(qpos, w->xpos, w->xquat, w->xmat, w->xipos, w->xI, w->xanchor, w->xaxis);
+  build_M(w->xmat, w->xpos, w->xipos, w->xI, w->xanchor, w->xaxis, w->scom, w->cinert, w->cdof, w->M);
+  double h[2][6] = {{0}}, mt = 0, c[3] = {0, 0, 0};
+  for (int b = 1; b < NB; b++) {
+    double cv[6] = {0, 0, 0, 0, 0, 0};
+    for (int d = 0; d < NV; d++)
+      if (dof_in_chain(d, b)) for (int j = 0; j < 6; j++) cv[j] += w->cdof[d][j] * qvel[d];
+    const int t = b == 7;
+    for (int i = 0; i < 6; i++) { double s = 0; for (int j = 0; j < 6; j++) s += w->cinert[b][6 * i + j] * cv[j]; h[t][i] += s; }
+    mt += m->mass[b];
+    for (int i = 0; i < 3; i++) c[i] += m->mass[b] * w->xipos[b][i];
+  }
+  for (int i = 0; i < 3; i++) c[i] /= mt;
+  double L[3] = {0, 0, 0}, P[3] = {0, 0, 0};
+  for (int t = 0; t < 2; t++) {
+    double r[3], x[3];
+    v3sub(r, w->scom[t == 0 ? 1 : 7], c);
+    v3cross(x, r, h[t] + 3);
+    for (int i = 0; i < 3; i++) { L[i] += h[t][i] + x[i]; P[i] += h[t][3 + i]; }
+  }
+  v3copy(out, P); v3copy(out + 3, L); v3copy(out + 6, c);
 }
 
 /* mj_integratePos */
@@ -1620,6 +1671,19 @@ static void reset_data(double* qpos, double* qvel, double* warm, double* ctrl) {
   memset(qvel, 0, NV * sizeof(double));
   if (warm) memset(warm, 0, NV * sizeof(double));
   ctrl[0] = ctrl[1] = ctrl[2] = 0;
+}
+
+/* BBO_RKMK: replace the free joints' body angular velocities in x (dofs 3..6, 12..15)
+ * by dexp^-1_{-theta}(w) for the stage's rotation vectors theta[0..3) (base), [3..6) (ball) */
+static void rkmk_rates(double* x, const double* theta) {
+  for (int t = 0; t < 2; t++) {
+    double* w = x + (t ? 9 : 0) + 3;
+    const double* th = theta + 3 * t;
+    double c1[3], c2[3];
+    v3cross(c1, th, w);
+    v3cross(c2, th, c1);
+    for (int i = 0; i < 3; i++) w[i] += 0.5 * c1[i] + c2[i] / 12.0;
+  }
 }
 
 /* mj_step with integrator RK4: mj_checkPos, mj_checkVel, mj_forward,
@@ -1649,15 +1713,28 @@ int bbo_mj_step(double* qpos, double* qvel, double* warm, const double* ctrl_in,
   }
   memcpy(X[0], v0, sizeof v0);
   memcpy(F[0], o->qacc, sizeof F[0]);
+  /* BBO_RKMK (test-only): the free joints' rotation rates of stage j become
+   * dexp^-1_{-theta_j}(w_j) = w + theta x w / 2 + theta x (theta x w) / 12, theta_j
+   * the stage's rotation vector from the step's start orientation (q_j = q0 exp(theta_j)) */
+  const int rkmk = (g_flags & BBO_RKMK) != 0;
+  double th[4][6];
+  memset(th, 0, sizeof th);
+  if (rkmk) rkmk_rates(X[0], th[0]);
   for (int i = 1; i < 4; i++) {
     double dxv[NV], dxa[NV], q[NQ], v[NV];
     for (int d = 0; d < NV; d++) { dxv[d] = A[i - 1] * X[i - 1][d]; dxa[d] = A[i - 1] * F[i - 1][d]; }
+    if (rkmk)
+      for (int t = 0; t < 2; t++)
+        for (int c = 0; c < 3; c++) {
+          th[i][3 * t + c] = h * dxv[(t ? 9 : 0) + 3 + c];
+        }
     memcpy(q, q0, sizeof q);
     integrate_pos(q, dxv, h);
     for (int d = 0; d < NV; d++) v[d] = v0[d] + h * dxa[d];
     forward_impl(q, v, ctrl, warm, hfield, size_z, o);
     memcpy(X[i], v, sizeof v);
     memcpy(F[i], o->qacc, sizeof F[i]);
+    if (rkmk) rkmk_rates(X[i], th[i]);
   }
   double dv[NV], da[NV];
   for (int d = 0; d < NV; d++) {

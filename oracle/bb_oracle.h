@@ -45,6 +45,11 @@ extern "C" {
 #define BBO_DISABLE_CONTACT 1
 #define BBO_DISABLE_GRAVITY 2
 #define BBO_DISABLE_DAMPING 4
+/* test-only: compose the free joints' rotations in RK4 as Runge-Kutta-Munthe-Kaas
+ * (stage rates dexp^-1 of the body angular velocity, relative to the step's start
+ * orientation) instead of MuJoCo's sum of the stages' body-frame angular velocities.
+ * Pins that the forward dynamics are consistent to 4th order (tests/test_oracle.py). */
+#define BBO_RKMK 8
 
 /* Per-forward diagnostic outputs (stage-level view of mjData). */
 typedef struct {
@@ -64,6 +69,7 @@ typedef struct {
   int ground_overflow;          /* bit 0: ball-hfield cap, bit 1: base-tree contact cap */
   int nbody;                    /* base-tree geom contacts (after the 3 wheel + nground ball contacts) */
   int con_body1[BBO_MAXCON];    /* 0 world (hfield), 7 ball */
+  double con_force[BBO_MAXCON * 3];  /* efc_force per contact: normal, tangent 1, tangent 2 (contact frame) */
 } bbo_forward_out;
 
 /* Env configuration mirroring BBotSimulation.__init__ (ballbot_env.py:157-231). */
@@ -84,7 +90,12 @@ int  bbo_get_flags(void);
 void bbo_set_solver(int maxiter, double tol);
 /* line search: at most ls_iterations evaluations, stop at |phi'| <= ls_tolerance |phi'(0)| */
 void bbo_set_linesearch(int ls_iterations, double ls_tolerance);
-void bbo_model_info(double* out);   /* masses, invweight0, meaninertia, qpos0 ... (see .c) */
+void bbo_model_info(double* out);
+/* opt.timestep (invariant tests: RK4 order; h <= 0 restores 0.002) */
+void bbo_set_timestep(double h);
+/* momentum of the bodies at (qpos, qvel): out[0..3) linear, out[3..6) angular about
+ * the system COM (world frame), out[6..9) the system COM */
+void bbo_momentum(const double* qpos, const double* qvel, double* out);   /* masses, invweight0, meaninertia, qpos0 ... (see .c) */
 
 /* mj_forward at (qpos, qvel) with ctrl; warm = qacc_warmstart (may be NULL). */
 void bbo_forward(const double* qpos, const double* qvel, const double* ctrl,

@@ -23,9 +23,10 @@ struct Counts {
   unsigned long long add, mul, div, sqrt, trans, cmp;
 };
 constexpr int NPH = 5;  // bb_oracle.c BBO_PHASE: kinematics/mass/bias, collision, assembly, solver, RK4/glue
-static Counts ph[NPH];
-static Counts g;        // the phase being counted (copied back at every phase switch)
-static int cur = 4;
+// per thread: bbo_count_flops_replay runs on several host threads at once (tools/flops.py)
+static thread_local Counts ph[NPH];
+static thread_local Counts g;        // the phase being counted (copied back at every phase switch)
+static thread_local int cur = 4;
 inline void phase(int k) {
   Counts& a = ph[cur];
   a.add += g.add; a.mul += g.mul; a.div += g.div; a.sqrt += g.sqrt; a.trans += g.trans; a.cmp += g.cmp;
@@ -176,6 +177,76 @@ long long bbo_count_flops(int n_envs, int n_burn, int n_steps, const float* hfie
   g_lsmax = lsmax0;
   g_lstol = lstol0;
   free(q); free(v); free(w); free(sc);
+  return steps;
+}
+
+// Warm-up for threaded use: the model compiles once, outside the worker threads.
+void bbo_count_prepare(void) {
+  compile_model();
+  g_maxiter = 100;  // MuJoCo defaults: iterations, tolerance, ls_iterations, ls_tolerance
+  g_tol = 1e-8;
+  g_lsmax = 50;
+  g_lstol = 0.01;
+}
+
+// The bench's timed mix, replayed: n_envs envs from their states at the start of the timed window
+// (q[n][17], v[n][15], w[n][15], step counters sc[n]; updated in place) step n_steps times with
+// the window's own actions (actions[t][n][3]), auto-resetting onto the env's next terrain draw:
+// env e starts on table[terr[e * max_ep]] and its k-th reset moves to table[terr[e * max_ep + k]]
+// (the last one repeats past max_ep; *overrun counts such resets), each table slot a float32
+// [293 * 293] heightfield with its init offset offsets[slot], vertical scale size_z.  Thread-safe
+// (thread-local counters) after bbo_count_prepare().  out[30] = per env-step sums over this call
+// (not means) of {add/sub, mul, div, sqrt, transcendental, comparisons} per phase; returns the
+// env-steps run.
+long long bbo_count_flops_replay(int n_envs, int n_steps, double* q, double* v, double* w, int* sc,
+                                 const float* actions, const float* table, const double* offsets, const int* terr,
+                                 int max_ep, double size_z, double* out, int* overrun) {
+  bbo_env_cfg cfg;
+  memset(&cfg, 0, sizeof cfg);
+  cfg.max_ep_steps = 4000;
+  cfg.max_allowed_tilt = 20.0;
+  cfg.max_wheel_velocity = 10.0;
+  cfg.reward_scale = 0.01f;
+  cfg.action_reg_coef = -0.0001f;
+  cfg.survival_bonus = 0.02f;
+  cfg.target_dir[0] = 0.0f;
+  cfg.target_dir[1] = 1.0f;
+  const size_t HF = (size_t)BBO_HF_N * BBO_HF_N;
+  FD* Q = (FD*)calloc((size_t)n_envs * NQ, sizeof(FD));
+  FD* V = (FD*)calloc((size_t)n_envs * NV, sizeof(FD));
+  FD* W = (FD*)calloc((size_t)n_envs * NV, sizeof(FD));
+  int* ep = (int*)calloc((size_t)n_envs, sizeof(int));
+  for (size_t i = 0; i < (size_t)n_envs * NQ; i++) Q[i] = FD(q[i]);
+  for (size_t i = 0; i < (size_t)n_envs * NV; i++) { V[i] = FD(v[i]); W[i] = FD(w[i]); }
+  fc::g = fc::Counts{};
+  for (auto& c : fc::ph) c = fc::Counts{};
+  fc::cur = 4;
+  long long steps = 0;
+  for (int e = 0; e < n_envs; e++)
+    for (int t = 0; t < n_steps; t++) {
+      const int slot = terr[(size_t)e * max_ep + ep[e]];
+      const float* a = actions + ((size_t)t * n_envs + e) * 3;
+      float obs[15], r, p2[2];
+      const int f = bbo_env_step(&cfg, Q + e * NQ, V + e * NV, W + e * NV, sc + e, a, table + (size_t)slot * HF,
+                                 FD(size_z), obs, &r, p2, nullptr);
+      steps++;
+      if (f & 1) {  // auto-reset onto the env's next drawn terrain
+        if (ep[e] + 1 < max_ep) ep[e]++; else (*overrun)++;
+        const int ns = terr[(size_t)e * max_ep + ep[e]];
+        bbo_reset_state(FD(offsets[ns]), Q + e * NQ, V + e * NV, W + e * NV);
+        sc[e] = 0;
+      }
+    }
+  fc::phase(4);
+  for (int p = 0; p < fc::NPH; p++) {
+    const fc::Counts& c = fc::ph[p];
+    double* o = out + 6 * p;
+    o[0] = (double)c.add; o[1] = (double)c.mul; o[2] = (double)c.div; o[3] = (double)c.sqrt; o[4] = (double)c.trans;
+    o[5] = (double)c.cmp;
+  }
+  for (size_t i = 0; i < (size_t)n_envs * NQ; i++) q[i] = Q[i].v;
+  for (size_t i = 0; i < (size_t)n_envs * NV; i++) { v[i] = V[i].v; w[i] = W[i].v; }
+  free(Q); free(V); free(W); free(ep);
   return steps;
 }
 

@@ -7,6 +7,7 @@
 #include "bb_bodycon.h"
 #include "bb_model.h"
 #include "bb_step.h"
+#include "bb_pairmap.h"
 
 using namespace bb;
 
@@ -209,4 +210,6 @@ void hc_model(double* out) {
   out[8] = m.iw_base; out[9] = m.iw_cam[0]; out[10] = m.iw_cam[1];
   for (int i = 0; i < 3; i++) { out[11 + i] = m.stick_c[0][i]; out[14 + i] = m.stick_a[0][i]; out[17 + i] = m.stick_c[1][i]; out[20 + i] = m.stick_a[1][i]; }
 }
+// the relief pair's block -> (kind, index within kind) map (bb_pairmap.h)
+int hc_pair_kind_of(int b, int nf, int ns, int* wg) { return pair_kind_of(b, nf, ns, wg); }
 }

@@ -55,6 +55,7 @@ def lib():
         L.hc_body_jacobian_check.argtypes = [C.c_int, C.c_uint]
         L.hc_body_jacobian_check.restype = C.c_double
         L.hc_capsule_apart_check.argtypes = [C.c_int, C.c_uint, dp]
+        L.hc_pair_kind_of.argtypes = [C.c_int, C.c_int, C.c_int, ip]
         _lib = L
     return _lib
 
@@ -65,6 +66,13 @@ def _d(a):
 
 def _f(a):
     return None if a is None else a.ctypes.data_as(C.POINTER(C.c_float))
+
+
+def pair_kind_of(b, nf, ns):
+    """bb_pairmap.h: block b of the one-launch relief pair -> (kind 0 fast / 1 full / -1 idle, index)."""
+    wg = C.c_int(0)
+    k = lib().hc_pair_kind_of(int(b), int(nf), int(ns), C.byref(wg))
+    return k, wg.value
 
 
 def model():

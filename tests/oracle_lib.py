@@ -19,7 +19,7 @@ LIB_PATH = ORACLE_DIR / "_build" / "libbb_oracle.so"
 NQ, NV, NB, MAXCON = 17, 15, 8, 356  # MAXCON = 3 + BBO_MAXGROUND 50 + BBO_MAXBODY (3 + 6 x 50)
 HF_N = 293
 
-DISABLE_CONTACT, DISABLE_GRAVITY, DISABLE_DAMPING = 1, 2, 4
+DISABLE_CONTACT, DISABLE_GRAVITY, DISABLE_DAMPING, RKMK = 1, 2, 4, 8
 
 
 class ForwardOut(C.Structure):
@@ -44,6 +44,7 @@ class ForwardOut(C.Structure):
         ("ground_overflow", C.c_int),
         ("nbody", C.c_int),
         ("con_body1", C.c_int * MAXCON),
+        ("con_force", C.c_double * (MAXCON * 3)),
     ]
 
 
@@ -103,6 +104,8 @@ def lib():
         L.bbo_env_step_batch_mt.argtypes = L.bbo_env_step_batch.argtypes + [C.c_int]
         L.bbo_env_step_batch_mt.restype = C.c_int
         L.bbo_render_depth.argtypes = [dp, fp, C.c_double, C.c_int, C.c_int, C.c_int, fp]
+        L.bbo_set_timestep.argtypes = [C.c_double]
+        L.bbo_momentum.argtypes = [dp, dp, dp]
         _lib = L
     return _lib
 
@@ -144,6 +147,18 @@ def render_depth(qpos: np.ndarray, hfield: np.ndarray, cam: int, H: int = 64, W:
 
 def set_flags(flags: int) -> None:
     lib().bbo_set_flags(flags)
+
+
+def set_timestep(h: float = 0.002) -> None:
+    """opt.timestep of the oracle's mj_step (the RK4 convergence test)."""
+    lib().bbo_set_timestep(float(h))
+
+
+def momentum(qpos, qvel):
+    """(linear momentum, angular momentum about the system COM, system COM) of the bodies."""
+    out = np.zeros(9)
+    lib().bbo_momentum(_d(np.ascontiguousarray(qpos, np.float64)), _d(np.ascontiguousarray(qvel, np.float64)), _d(out))
+    return out[0:3], out[3:6], out[6:9]
 
 
 def set_solver(maxiter: int = 100, tol: float = 1e-12) -> None:

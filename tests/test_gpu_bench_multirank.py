@@ -42,3 +42,6 @@ def test_bench_two_ranks_over_gloo(terrain):
     assert line["value"] > 0 and line["steps"] == 20
     assert line["value"] == pytest.approx(1024 * 20 / (line["ms_per_step"] * 20 / 1e3), rel=1e-6)
     assert "env-sharded x2" in line["config"]["parallelism"]
+    # two ranks share the chip: each rank's persistent relief pair (perlin) must still have
+    # finished every launch without its budget firing (bench.py would have exited non-zero)
+    assert line["stats"]["pair_budget"] == 0 and line["status"] == "ok"

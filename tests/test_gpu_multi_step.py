@@ -160,16 +160,17 @@ def test_headline_form_k512_and_driver_window(terrain, route, monkeypatch):
     512 steps per launch): a burn-in of 400 steps and 300 warm-up steps (launches of 512 +
     188), then the timed 500 steps as one launch (bench.launch_chunks); and the driver's
     window, one 20-step launch after the burn-in.  Against one bb_step per step, bit for bit
-    (flat: 4096 envs, configs[1]; perlin: 1024 envs on per-env generators over the whole
-    seed space, route 0: the relief pair)."""
+    (flat: 4096 envs, configs[1]; perlin: 4096 envs, configs[2] at the bench's own size, env g
+    on np_random(1000 + g) over the whole seed space as bench.py seeds it, route 0: the relief
+    pair -- no launch of it may end on its budget)."""
     import sys
     from pathlib import Path
 
     sys.path.insert(0, str(Path(__file__).resolve().parents[1]))
     import bench
 
-    n = 4096 if terrain == "flat" else 1024
-    kw = {} if terrain == "flat" else {"n_terrains": None}
+    n = 4096
+    kw = {} if terrain == "flat" else {"n_terrains": None, "stream_seeds": [1000 + i for i in range(n)]}
     a, b = _pair(n, terrain, monkeypatch, route=route, **kw)
     g = torch.Generator(device="cuda:0").manual_seed(1234)
     PS = M = 512
@@ -184,8 +185,40 @@ def test_headline_form_k512_and_driver_window(terrain, route, monkeypatch):
         assert (x is None and y is None) or np.array_equal(x, y)
     sa, sb = a.stats(), b.stats()
     assert sa == sb, (sa, sb)
-    assert sa["resets"] > n // 2
+    assert sa["resets"] > n // 2 and sb["pair_budget"] == 0
+    if terrain == "perlin":
+        assert sa["slow_path"] > 0 and b.pair_counters()["steps_full"] > 0  # the pair's full loop ran
+    b.check()
     a.close(), b.close()
+
+
+def test_relief_pair_budget_expiry_is_loud(monkeypatch):
+    """A relief-pair launch that ends on its wall-clock budget must not pass silently.  With
+    BB_PAIR_BUDGET_MS=1 a team that waits 1 ms for an env (teams outnumber the 512 envs 8:1, so
+    most wait from the start) ends the launch: stats count it, check() raises, and every later
+    step -- bb_step, bb_step_multi -- refuses until a full reset() clears the fault."""
+    monkeypatch.setenv("BB_PAIR_BUDGET_MS", "1")  # read by bb_create
+    monkeypatch.setenv("BB_ROUTE", "0")
+    from ballbot_gym.envs import BallbotVecEnv
+
+    n = 512
+    env = BallbotVecEnv(n, device="cuda:0", seed=3, terrain_config={"type": "perlin", "config": {}},
+                        stream_seeds=[80 + i for i in range(n)])
+    g = torch.Generator(device="cuda:0").manual_seed(4)
+    acts = torch.rand(64, n, 3, generator=g, device="cuda:0") * 2 - 1
+    env.step_multi(acts)  # asynchronous: no error yet
+    with pytest.raises(RuntimeError, match="wall-clock budget"):
+        env.check()
+    assert env.stats()["pair_budget"] >= 1
+    with pytest.raises(RuntimeError, match="wall-clock budget"):
+        env.step(acts[0])
+    with pytest.raises(RuntimeError, match="wall-clock budget"):
+        env.step_multi(acts)
+    env.reset()  # a full reset gives every env a valid state: the fault clears on the device
+    env.check()
+    env.step(acts[0])
+    env.check()
+    env.close()
 
 
 @pytest.mark.parametrize("variant", [{"BB_PAIR_ONE": "0"}, {"BB_PAIR_SOLO": "64", "BB_PAIR_HEAVY": "100"},

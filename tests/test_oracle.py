@@ -11,8 +11,10 @@ G = 9.81
 @pytest.fixture(autouse=True)
 def _reset_flags(oracle):
     oracle.set_flags(0)
+    oracle.set_timestep(0.002)
     yield
     oracle.set_flags(0)
+    oracle.set_timestep(0.002)
 
 
 def test_model_constants(oracle):
@@ -88,6 +90,98 @@ def test_linear_momentum_conserved_without_gravity(oracle):
     p1, P1 = momentum()
     np.testing.assert_allclose(p1, p0, atol=1e-9)
     np.testing.assert_allclose(P1, P0, atol=1e-9)
+
+
+def _tumbling_state(oracle, seed=5):
+    """The robot in the air, base tilted 30 deg, tumbling (body rates ~6 rad/s) with the
+    wheels spinning (~30 rad/s): torque-free motion whose body-frame angular velocity varies."""
+    rng = np.random.default_rng(seed)
+    q, v, _ = oracle.reset_state(0.01)
+    t = np.radians(30)
+    q[3:7] = [np.cos(t / 2), *(np.sin(t / 2) * np.array([0.6, 0.8, 0.0]))]
+    v[:] = rng.normal(0, 1, 15)
+    v[3:6] = rng.normal(0, 6, 3)
+    v[6:9] = rng.normal(0, 30, 3)
+    return q, v
+
+
+def _rk4_errors(oracle, q0, v0, T=0.128, hs=(0.008, 0.004, 0.002, 0.001)):
+    def run(h):
+        oracle.set_timestep(h)
+        q, v, w = q0.copy(), v0.copy(), np.zeros(15)
+        for _ in range(int(round(T / h))):
+            oracle.mj_step(q, v, w, np.zeros(3))
+        return q
+    ref = run(hs[-1] / 64)
+    return np.array([np.abs(run(h) - ref).max() for h in hs])
+
+
+def test_rk4_convergence_order(oracle):
+    """SURVEY.md §8 C1, RK4 order in dt (contacts and damping off, gravity on).
+
+    With the free joints' rotations composed as Runge-Kutta-Munthe-Kaas (BBO_RKMK,
+    test-only) the qpos error after 0.128 s falls 16x per halving of dt: the forward
+    dynamics the integrator samples are consistent to 4th order.  MuJoCo's own
+    composition -- mj_RungeKutta sums the stages' BODY-frame angular velocities and
+    mj_integratePos applies q0 * exp(h * sum) -- drops the commutator of the varying
+    body rates and converges at 2nd order in the rotation: 4x per halving [MJ].  The
+    oracle, like MuJoCo and the kernel, steps with MuJoCo's composition."""
+    q0, v0 = _tumbling_state(oracle)
+    oracle.set_flags(oracle.DISABLE_CONTACT | oracle.DISABLE_DAMPING | oracle.RKMK)
+    e = _rk4_errors(oracle, q0, v0)
+    r = e[:-1] / e[1:]
+    assert np.all((r > 15.0) & (r < 17.0)), r
+    oracle.set_flags(oracle.DISABLE_CONTACT | oracle.DISABLE_DAMPING)
+    e = _rk4_errors(oracle, q0, v0)
+    r = e[:-1] / e[1:]
+    assert np.all((r > 3.8) & (r < 4.2)), r
+    assert e[2] < 1e-5  # at ballbot.xml's 2 ms: a few microns after 64 steps of tumbling
+
+
+def test_angular_momentum_conserved_without_gravity(oracle):
+    """with gravity and contacts off, the bodies' angular momentum about
+    the system COM is conserved -- the hinge damping and motor torques are internal, so it
+    holds with damping on too -- and the COM moves on a straight line.  RK4's rotation
+    error drifts it by < 1e-4 relative over 2 s at 2 ms, 4x less per halving of dt."""
+    q0, v0 = _tumbling_state(oracle, seed=6)
+    mtot = oracle.model_info()["mass"][1:].sum()
+    drift = []
+    for h, damping in ((0.002, False), (0.001, False), (0.002, True)):
+        oracle.set_flags(oracle.DISABLE_CONTACT | oracle.DISABLE_GRAVITY | (0 if damping else oracle.DISABLE_DAMPING))
+        oracle.set_timestep(h)
+        q, v, w = q0.copy(), v0.copy(), np.zeros(15)
+        P0, L0, c0 = oracle.momentum(q, v)
+        n = int(round(2.0 / h))
+        for _ in range(n):
+            oracle.mj_step(q, v, w, np.array([3.0, -2.0, 1.0]) if damping else np.zeros(3))
+        P1, L1, c1 = oracle.momentum(q, v)
+        drift.append(np.abs(L1 - L0).max() / np.linalg.norm(L0))
+        assert drift[-1] < 1e-4, (h, damping, drift[-1])
+        assert np.abs(P1 - P0).max() < 1e-4 * np.linalg.norm(P0)
+        np.testing.assert_allclose(c1, c0 + P0 / mtot * n * h, atol=1e-4)
+    assert 3.5 < drift[0] / drift[1] < 4.5, drift
+
+
+def test_static_ball_load_equals_weight(oracle):
+    """SURVEY.md §8 C1, static load: the ball alone at rest on flat ground (the base tree
+    lies on the ground 2 m away) -- the summed normal forces of its terrain contacts equal
+    m_ball g within 1%; so do the base tree's ground contacts with its own weight."""
+    hf = oracle.flat_hfield()
+    q, v, w = oracle.reset_state(0.01)
+    q[0:3] = [2.0, 0.0, 0.3]
+    q[10:13] = [0.0, 0.0, 0.14 + 0.09 + 0.001]  # ball centre 1 mm above the plane
+    for _ in range(2000):
+        oracle.mj_step(q, v, w, np.zeros(3), hf)
+    assert np.abs(v).max() < 0.01
+    fo = oracle.forward(q, v, np.zeros(3), w, hf)
+    m = oracle.model_info()["mass"]
+    ball = [k for k in range(fo.ncon) if fo.con_body1[k] == 0 and fo.con_body2[k] == 7]
+    base = [k for k in range(fo.ncon) if fo.con_body1[k] == 0 and 1 <= fo.con_body2[k] <= 6]
+    assert ball and base and fo.ncon == len(ball) + len(base)  # the ball-wheel pairs are apart
+    fb = sum(fo.con_force[3 * k] for k in ball)
+    ft = sum(fo.con_force[3 * k] for k in base)
+    assert abs(fb - m[7] * G) <= 0.01 * m[7] * G, (fb, m[7] * G)
+    assert abs(ft - m[1:7].sum() * G) <= 0.01 * m[1:7].sum() * G, (ft, m[1:7].sum() * G)
 
 
 def test_patched_contact_frame(oracle):
@@ -413,3 +507,32 @@ def test_flop_counter_counts_the_oracle_step():
     c = F.count(L, high, 2.0, 4, 6, burn_in=100)
     assert c["flops_by_phase"]["constraint_assembly"] < ph["constraint_assembly"]
     assert c["flops_per_env_step"] < 0.8 * a["flops_per_env_step"]
+
+
+def test_flop_replay_of_the_timed_mix():
+    """bench.py's FLOP count replays its timed window (tools/flops.py count_replay): the counts
+    do not depend on how the envs are split over host threads (thread-local counters), every
+    env-step is counted, and an env's resets walk its own terrain row (a row that ends sooner
+    than the resets repeats its last terrain and is reported)."""
+    import sys
+    from pathlib import Path
+
+    import oracle_lib as O
+
+    sys.path.insert(0, str(Path(__file__).resolve().parents[1] / "tools"))
+    import flops as F
+    from ballbot_gym.terrain import generate_hills_terrain
+
+    table = np.stack([O.flat_hfield(), generate_hills_terrain(293, seed=7).astype(np.float32)])
+    offs = np.array([O.init_offset(t) for t in table])
+    n, T = 12, 400
+    q = np.zeros((n, 17)); v = np.zeros((n, 15)); w = np.zeros((n, 15))
+    for e in range(n):
+        q[e], v[e], w[e] = O.reset_state(offs[e % 2])
+    acts = np.random.default_rng(0).uniform(-1.5, 1.5, (T, n, 3)).astype(np.float32)
+    terr = np.array([[e % 2] for e in range(n)], np.int32)  # one terrain each: every reset overruns the row
+    runs = [F.count_replay(q.copy(), v.copy(), w.copy(), np.zeros(n, np.int32), acts, table, offs, terr, 2.0,
+                           threads=t) for t in (1, 3)]
+    assert runs[0]["env_steps"] == runs[1]["env_steps"] == n * T
+    assert runs[0]["flops_per_env_step"] == runs[1]["flops_per_env_step"] > 1e5
+    assert runs[0]["terrain_overrun_resets"] == runs[1]["terrain_overrun_resets"] > 0  # large actions: resets

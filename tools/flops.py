@@ -30,13 +30,65 @@ KINDS = ("add_sub", "mul", "div", "sqrt", "transcendental", "compare")
 LIB = ROOT / "oracle" / "_build" / "libbb_flops.so"
 
 
+_L = None
+
+
 def lib():
+    global _L
+    if _L is not None:
+        return _L
     subprocess.run(["make", "-s", "-C", str(ROOT / "oracle")], check=True)
     L = C.CDLL(str(LIB))
+    dp, ip = C.POINTER(C.c_double), C.POINTER(C.c_int)
+    L.bbo_count_prepare.argtypes = []
+    L.bbo_count_flops_replay.argtypes = [C.c_int, C.c_int, dp, dp, dp, ip, C.POINTER(C.c_float), C.POINTER(C.c_float),
+                                         dp, ip, C.c_int, C.c_double, dp, ip]
+    L.bbo_count_flops_replay.restype = C.c_longlong
+    L.bbo_count_prepare()
+    _L = L
     L.bbo_count_flops.argtypes = [C.c_int, C.c_int, C.c_int, C.POINTER(C.c_float), C.c_double, C.c_double, C.c_double,
                                   C.c_uint, C.POINTER(C.c_double)]
     L.bbo_count_flops.restype = C.c_longlong
     return L
+
+
+def count_replay(q, v, w, sc, actions, table, offsets, terr, size_z, threads=8) -> dict:
+    """Algorithmic FLOPs of the bench's own timed mix: envs replayed from their states at the
+    start of the timed window with the window's actions ([T][n][3]) and their own next terrain
+    draws (terr[n][max_ep] rows into table[slots][293*293] / offsets[slots]), split over host
+    threads (oracle/flopcount.cpp bbo_count_flops_replay: thread-local counters)."""
+    from concurrent.futures import ThreadPoolExecutor
+
+    L = lib()
+    n = q.shape[0]
+    T = actions.shape[0]
+    table = np.ascontiguousarray(table, np.float32)
+    offsets = np.ascontiguousarray(offsets, np.float64)
+    chunks = [c for c in np.array_split(np.arange(n), max(1, min(threads, n))) if len(c)]
+
+    def work(idx):
+        qq = np.ascontiguousarray(q[idx], np.float64); vv = np.ascontiguousarray(v[idx], np.float64)
+        ww = np.ascontiguousarray(w[idx], np.float64); ss = np.ascontiguousarray(sc[idx], np.int32)
+        aa = np.ascontiguousarray(actions[:, idx], np.float32)
+        tt = np.ascontiguousarray(terr[idx], np.int32)
+        out = np.zeros(30)
+        over = C.c_int(0)
+        f, dp, ip = C.POINTER(C.c_float), C.POINTER(C.c_double), C.POINTER(C.c_int)
+        steps = L.bbo_count_flops_replay(len(idx), T, qq.ctypes.data_as(dp), vv.ctypes.data_as(dp),
+                                         ww.ctypes.data_as(dp), ss.ctypes.data_as(ip), aa.ctypes.data_as(f),
+                                         table.ctypes.data_as(f), offsets.ctypes.data_as(dp), tt.ctypes.data_as(ip),
+                                         tt.shape[1], float(size_z), out.ctypes.data_as(dp), C.byref(over))
+        return steps, out, over.value
+
+    t0 = time.perf_counter()
+    with ThreadPoolExecutor(len(chunks)) as ex:
+        res = list(ex.map(work, chunks))
+    steps = sum(r[0] for r in res)
+    a = sum(r[1] for r in res).reshape(5, 6) / max(steps, 1)
+    flop_phase = {p: float(a[i, :5].sum()) for i, p in enumerate(PHASES)}
+    return {"env_steps": int(steps), "seconds": round(time.perf_counter() - t0, 2), "threads": len(chunks),
+            "flops_per_env_step": float(a[:, :5].sum()), "flops_by_phase": flop_phase,
+            "terrain_overrun_resets": int(sum(r[2] for r in res))}
 
 
 def count(L, hf: np.ndarray, size_z: float, n_envs: int, n_steps: int, seed: int = 1, burn_in: int = 0) -> dict:

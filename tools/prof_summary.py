@@ -1,6 +1,6 @@
 """Summarise tools/profile.sh output into profiles/ (tracked).
 
-  python tools/prof_summary.py gpurun_out/prof_r01_fp64 profiles/r01_fp64 --timed 300
+  python tools/prof_summary.py gpurun_out/prof_r05_flat profiles/r05_flat --kernel multi --f64 --traffic
 
 Writes <dst>_kernel_stats.csv (rocprofv3 --stats, verbatim), <dst>_summary.json
 (average step_kernel duration over the timed dispatches, PMC per launch) and,
@@ -91,8 +91,9 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("src")
     ap.add_argument("dst")
-    ap.add_argument("--timed", type=int, default=300, help="timed step_kernel dispatches at the end of the trace run")
-    ap.add_argument("--pmc-last", type=int, default=20)
+    ap.add_argument("--timed", type=int, default=1, help="timed dispatches at the end of the trace run (bench.py's "
+                                                         "timed window is the last launch with --no-per-step)")
+    ap.add_argument("--pmc-last", type=int, default=1)
     ap.add_argument("--traffic", action="store_true")
     ap.add_argument("--kernel", default="fast", choices=["fast", "pred", "multi", "pair"])
     ap.add_argument("--f64", action="store_true", help="also summarise the FP64 VALU instruction pass (sq64)")
@@ -156,20 +157,22 @@ def main():
                           "fp64_tflops_upper_bound": fl / (out["avg_ms_rocprof"] * 1e-3) / 1e12}
     (Path(str(dst) + "_summary.json")).write_text(json.dumps(out, indent=1))
     print(json.dumps(out, indent=1))
-    if a.traffic:
+    if a.traffic:  # the entry bench.py reads for a line of exactly this launch shape (profile_entry)
         tj = dst.parent / "traffic.json"
         cur = json.loads(tj.read_text()) if tj.exists() else {}
-        prec = bench["config"]["precision"]
-        spl = bench["config"].get("steps_per_launch", 1) if a.kernel in ("multi", "pair") else 1
-        terrain = bench["config"].get("workload", "").split(", ")[1].split(" ")[0] if "workload" in bench["config"] else "flat"
-        key = (prec if spl == 1 else f"{prec}_multi{spl}") + ("" if terrain == "flat" else f"_{terrain}")
+        cfg = bench["config"]
+        prec, envs = cfg["precision"], cfg["envs_per_gpu"]
+        spl = cfg.get("steps_per_launch", 1) if a.kernel in ("multi", "pair") else 1
+        terrain = cfg.get("terrain") or cfg.get("workload", "").split(", ")[1].split(" ")[0]
+        key = f"{prec}_{terrain}_n{envs}_spl{spl:g}"
         cur[key] = {
-            "precision": prec, "envs": bench["config"]["envs_per_gpu"], "steps_per_launch": spl, "terrain": terrain,
+            "precision": prec, "envs": envs, "steps_per_launch": spl, "terrain": terrain,
             "bytes_per_launch": fetch_b + write_b, "fetch_raw_bytes_per_launch": f["FETCH_SIZE"] * 1024,
             "write_bytes_per_launch": write_b, "issue_frac": out["derived"]["issue_frac"],
+            "avg_ms_rocprof": out["avg_ms_rocprof"],
+            "fp64_flop_executed_per_launch": (out.get("pmc_f64") or {}).get("fp64_flop_upper_bound_per_launch"),
             "source": str(dst) + "_summary.json"}
         tj.write_text(json.dumps(cur, indent=1))
-
 
 if __name__ == "__main__":
     main()

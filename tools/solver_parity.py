@@ -1,0 +1,76 @@
+"""Kernel solver vs the MuJoCo-form oracle, teacher-forced, on the CPU.
+
+The host build of the product's per-env templates (tests/hostcheck: the kernel's
+forward, its Newton solve with its own line search, RK4, glue) and the oracle
+(MuJoCo's PrimalSearch, warm-start choice, improvement/gradient stop) step the
+same recorded pre-step states; reported per env-step are max |dqpos|, max
+|dqvel| and the share within the parity tests' stated fp64 tolerance (qpos 1e-9,
+qvel 1e-6).  The residual is where the two line searches end an iteration at
+different points and MuJoCo's improvement test then stops one Newton iteration
+apart.
+
+  python tools/solver_parity.py [--envs 64] [--steps 120] [--terrain flat|hills|both] [--out profiles/r05_solver_parity.json]
+"""
+import argparse
+import json
+import sys
+from pathlib import Path
+
+import numpy as np
+
+ROOT = Path(__file__).resolve().parents[1]
+for p in (ROOT / "tests", ROOT / "openballbot-rl_amd"):
+    sys.path.insert(0, str(p))
+
+import hostcheck_lib as HC  # noqa: E402
+import oracle_lib as O  # noqa: E402
+import traj  # noqa: E402
+
+
+def measure(hf, n_envs, n_steps, seed, size_z=2.0):
+    rec = traj.record(n_envs=n_envs, n_steps=n_steps, hfield=hf, size_z=size_z, seed=seed)
+    cfg = HC.default_cfg()
+    dq, dv = [], []
+    for t in range(n_steps):
+        for e in range(n_envs):
+            q, v, w = rec["qpos"][t][e].copy(), rec["qvel"][t][e].copy(), rec["warm"][t][e].copy()
+            st = np.array([rec["steps"][t][e]], np.int32)
+            HC.env_step(cfg, q, v, w, st, rec["action"][t][e], hf, size_z)
+            dq.append(float(np.abs(q - rec["qpos1"][t][e]).max()))
+            dv.append(float(np.abs(v - rec["qvel1"][t][e]).max()))
+    dq, dv = np.array(dq), np.array(dv)
+    ok = (dq <= 1e-9) & (dv <= 1e-6)
+    worst = np.argsort(-dv)[:5]
+    return {"env_steps": int(len(dq)), "within_q1e-9_v1e-6": float(ok.mean()), "outliers": int((~ok).sum()),
+            "qpos_max": float(dq.max()), "qvel_max": float(dv.max()),
+            "qpos_p50": float(np.median(dq)), "qvel_p50": float(np.median(dv)),
+            "qpos_p999": float(np.quantile(dq, 0.999)), "qvel_p999": float(np.quantile(dv, 0.999)),
+            "worst_qvel": [float(dv[i]) for i in worst]}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--envs", type=int, default=64)
+    ap.add_argument("--steps", type=int, default=120)
+    ap.add_argument("--terrain", default="both")
+    ap.add_argument("--out", default=None)
+    a = ap.parse_args()
+    O.build()
+    HC.build()
+    res = {}
+    if a.terrain in ("flat", "both"):
+        res["flat"] = measure(O.flat_hfield(), a.envs, a.steps, seed=3)
+        print("flat", json.dumps(res["flat"]), flush=True)
+    if a.terrain in ("hills", "both"):
+        from ballbot_gym.terrain import generate_hills_terrain
+
+        hf = generate_hills_terrain(293, seed=7).astype(np.float32)
+        res["hills"] = measure(hf, a.envs // 2, a.steps * 2 // 3, seed=5)
+        print("hills", json.dumps(res["hills"]), flush=True)
+    if a.out:
+        Path(a.out).write_text(json.dumps({"what": "hostcheck (kernel templates, host build) vs MuJoCo-form oracle, "
+                                                   "teacher-forced one step per recorded state", **res}, indent=1))
+
+
+if __name__ == "__main__":
+    main()
