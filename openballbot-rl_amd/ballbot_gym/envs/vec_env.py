@@ -109,6 +109,7 @@ class BallbotVecEnv:
         self._n_terrains_arg = n_terrains
         self._shared_stream = bool(shared_stream)
         self._pending_seeds: Optional[list] = None
+        self._graphs = 0  # HIP graphs captured over this handle (capture_step, the trainer's rollout graph)
         self._h = None
         if terrain_slots is not None:  # host-driven terrains (load_terrain + assign_terrain), e.g. BBotSimulation
             from .config import TerrainPlan, terrain_size_z
@@ -158,6 +159,12 @@ class BallbotVecEnv:
         p.n_terrains = len(plan.seeds)
         L = N.lib()
         if self._h is not None:
+            if self._graphs:
+                raise RuntimeError(
+                    f"{self._graphs} HIP graph(s) were captured over this env's handle, and the new terrain "
+                    "generators' draws are not in its bank: regenerating the bank needs a new handle, which "
+                    "those graphs would not follow (re-seed before capturing, or with a bank that covers the "
+                    "new draws, e.g. perlin's whole seed space)")
             L.bb_destroy(self._h)
             self._h = None
         h = C.c_void_p()
@@ -197,8 +204,9 @@ class BallbotVecEnv:
 
     def _reseed(self, stream_seeds) -> None:
         """Put env i on np_random(stream_seeds[i]) from its next reset on (its draw
-        counter restarts).  A bank that lacks the new generators' first draws is
-        regenerated, on a new handle: HIP graphs captured before this are invalid."""
+        counter restarts).  The generators are rewritten in place (bb_set_terrain_rng), so
+        HIP graphs captured before this draw from them at replay.  A bank that lacks the new
+        generators' first draws would need a new handle: refused once graphs exist."""
         from .config import stream_draws, terrain_plan
 
         plan = self.terrain_plan
@@ -295,6 +303,7 @@ class BallbotVecEnv:
         if self._reward_error:
             raise ValueError(self._reward_error)
         graph = torch.cuda.CUDAGraph()
+        self.note_graph_capture()
         side = torch.cuda.Stream(device=self.device)
         side.wait_stream(torch.cuda.current_stream(self.device))
         torch.cuda.synchronize(self.device)
@@ -302,6 +311,11 @@ class BallbotVecEnv:
             self._step_launch(actions)
         torch.cuda.synchronize(self.device)
         return graph
+
+    def note_graph_capture(self) -> None:
+        """Record that a HIP graph holding this env's handle exists (it lives as long as the env):
+        a re-seed that would need a new handle then raises instead of leaving the graph stale."""
+        self._graphs += 1
 
     def _step_launch(self, actions: torch.Tensor) -> None:
         N.check(N.lib().bb_step(self._h, _ptr(actions), _ptr(self.obs), _ptr(self.reward), _ptr(self.done),

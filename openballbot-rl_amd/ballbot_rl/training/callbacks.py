@@ -36,17 +36,19 @@ class EvalCallback:
         self.results: List[List[float]] = []
         self.ep_lengths: List[List[int]] = []
 
-    def due(self, first: int, last: int) -> Optional[int]:
-        """The multiple of eval_freq in vec-env steps [first, last], if any."""
-        k = last // self.eval_freq
-        return k * self.eval_freq if k * self.eval_freq >= first and k > 0 else None
+    def due(self, first: int, last: int) -> List[int]:
+        """Every multiple of eval_freq in vec-env steps [first, last]: SB3 calls _on_step at
+        every vec-env step, so with eval_freq < n_steps one rollout holds several evaluations."""
+        k0 = max(1, -(-first // self.eval_freq))
+        return [k * self.eval_freq for k in range(k0, last // self.eval_freq + 1)]
 
     def __call__(self, model, first: int, last: int) -> None:
+        for step in self.due(first, last):  # the rollout's fixed parameters, one evaluation per multiple
+            self._evaluate(model, step)
+
+    def _evaluate(self, model, step: int) -> None:
         from ballbot_rl.evaluation import evaluate_policy
 
-        step = self.due(first, last)
-        if step is None:
-            return
         r = evaluate_policy(model.policy, self.eval_env, n_eval_episodes=self.n_eval_episodes,
                             deterministic=self.deterministic)
         ts = step * self.n_total_envs  # SB3's num_timesteps at that step

@@ -487,6 +487,7 @@ class _RolloutGraph:
         flat, nflat = C.c_void_p(self.flat.data_ptr()), int(self.flat.numel())
         torch.cuda.synchronize(dev)
         _dbg(f"rollout graph: capture T={T} n={n} obs={obs.data_ptr():#x} flat={self.flat.data_ptr():#x}")
+        env.note_graph_capture()
         self.graph = torch.cuda.CUDAGraph()
         with torch.cuda.graph(self.graph):
             stream = C.c_void_p(torch.cuda.current_stream(dev).cuda_stream)

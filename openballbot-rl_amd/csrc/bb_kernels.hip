@@ -80,6 +80,15 @@ __device__ __forceinline__ EnvWork<T>& team_work(unsigned char* smem, int team) 
   return *reinterpret_cast<EnvWork<T>*>(smem + size_t(team) * work_stride<T>());
 }
 
+// the terrain-draw configuration (Dev.tsrc; one per handle, in device memory)
+struct TerrainSrc {
+  const int* tstream;         // [n_streams][tlen] bank slot of draw k (bb_set_terrain_stream); NULL: none
+  const int* env_stream;      // [n] stream of each env; NULL: stream 0
+  int tlen;
+  unsigned long long* rng;    // [5][n] per-env PCG64 (bb_set_terrain_rng): state hi/lo, inc hi/lo, 32-bit buffer
+  const int* seed_slot;       // [TERRAIN_SEEDS] bank slot holding each terrain seed (-1: not resident); NULL: slot == seed
+};
+
 struct Dev {
   int n;
   void* qpos;
@@ -89,11 +98,11 @@ struct Dev {
   int* terrain;
   int* pending_terrain;       // >= 0: terrain pinned by bb_assign_terrain; < 0: draw from the stream
   int* episodes;              // terrain-stream draws made by each env so far
-  const int* tstream;         // [n_streams][tlen] bank slot of draw k (bb_set_terrain_stream); NULL: none
-  const int* env_stream;      // [n] stream of each env; NULL: stream 0
-  int tlen;
-  unsigned long long* rng;    // [5][n] per-env PCG64 (bb_set_terrain_rng): state hi/lo, inc hi/lo, 32-bit buffer
-  const int* seed_slot;       // [TERRAIN_SEEDS] bank slot holding each terrain seed (-1: not resident); NULL: slot == seed
+  // Where a reset's terrain comes from: a device record that bb_set_terrain_rng /
+  // bb_set_terrain_stream rewrite in place.  Dev is captured by value in HIP graphs, so it holds
+  // only this record's address, which never changes: a graph captured before a re-seed draws
+  // from the new generators (or the new table) at replay.
+  const struct TerrainSrc* tsrc;
   int* tseed;                 // [n] terrain seed of each env's last device draw (-1: none)
   const float* bank;
   const float* size_z;
@@ -253,30 +262,32 @@ __device__ __forceinline__ int pcg64_terrain_seed(Pcg64& g) {
 __device__ __forceinline__ int next_terrain(const Dev& d, int e) {
   const int pin = d.pending_terrain[e];
   if (pin >= 0) return pin;
-  if (d.rng) {
+  const TerrainSrc src = *d.tsrc;
+  if (src.rng) {
     const size_t n = size_t(d.n);
-    Pcg64 g{ld_coh(d.rng + e), ld_coh(d.rng + n + e), ld_coh(d.rng + 2 * n + e), ld_coh(d.rng + 3 * n + e),
-            ld_coh(d.rng + 4 * n + e)};
+    unsigned long long* rng = src.rng;
+    Pcg64 g{ld_coh(rng + e), ld_coh(rng + n + e), ld_coh(rng + 2 * n + e), ld_coh(rng + 3 * n + e),
+            ld_coh(rng + 4 * n + e)};
     const int s = pcg64_terrain_seed(g);
-    st_coh(d.rng + e, g.sh); st_coh(d.rng + n + e, g.sl); st_coh(d.rng + 4 * n + e, g.buf);
+    st_coh(rng + e, g.sh); st_coh(rng + n + e, g.sl); st_coh(rng + 4 * n + e, g.buf);
     st_coh(d.episodes + e, ld_coh(d.episodes + e) + 1);
     st_coh(d.tseed + e, s);
-    int slot = d.seed_slot ? d.seed_slot[s] : s;
+    int slot = src.seed_slot ? src.seed_slot[s] : s;
     if (unsigned(slot) >= unsigned(d.n_terrains)) {
       atomicAdd(&d.stats[5], 1ull);
       slot = s % d.n_terrains;
     }
     return slot;
   }
-  if (!d.tstream) return 0;
+  if (!src.tstream) return 0;
   int k = ld_coh(d.episodes + e);
   st_coh(d.episodes + e, k + 1);
-  if (k >= d.tlen) {  // past the resident draws: reuse them (counted)
+  if (k >= src.tlen) {  // past the resident draws: reuse them (counted)
     atomicAdd(&d.stats[5], 1ull);
-    k %= d.tlen;
+    k %= src.tlen;
   }
-  const int st = d.env_stream ? d.env_stream[e] : 0;
-  return d.tstream[size_t(st) * d.tlen + k];
+  const int st = src.env_stream ? src.env_stream[e] : 0;
+  return src.tstream[size_t(st) * src.tlen + k];
 }
 
 template <typename T>
@@ -1741,6 +1752,8 @@ struct bb_handle {
   int n_streams = 0;
   unsigned long long* rng = nullptr;  // per-env PCG64 words [5][n] (bb_set_terrain_rng), allocated once
   int* seed_slot = nullptr;           // [TERRAIN_SEEDS], allocated once
+  TerrainSrc tsrc{};                  // host copy of the device record Dev.tsrc points at
+  TerrainSrc* tsrc_dev = nullptr;
   CamRig rig;  // depth cameras in the base body (bb_render_depth)
   void* scenes = nullptr;
   volatile int* fault_host = nullptr;  // Dev.fault's host side (hipHostMalloc, mapped)
@@ -2164,6 +2177,9 @@ int bb_create(int n_envs, int device, const bb_params* p, bb_handle** out) {
   HIPCHK(hipMalloc((void**)&d.episodes, sizeof(int) * n));
   HIPCHK(hipMalloc((void**)&d.tseed, sizeof(int) * n));
   HIPCHK(hipMemset(d.tseed, 0xFF, sizeof(int) * n));  // -1: no device draw yet
+  HIPCHK(hipMalloc((void**)&h->tsrc_dev, sizeof(TerrainSrc)));
+  HIPCHK(hipMemcpy(h->tsrc_dev, &h->tsrc, sizeof(TerrainSrc), hipMemcpyHostToDevice));  // no draws: terrain 0
+  d.tsrc = h->tsrc_dev;
   HIPCHK(hipMalloc((void**)&h->bank, sizeof(float) * nt * HF_N * HF_N));
   HIPCHK(hipMalloc((void**)&h->size_z, sizeof(float) * nt));
   HIPCHK(hipMalloc((void**)&h->offset, sizeof(float) * nt));
@@ -2268,7 +2284,7 @@ int bb_destroy(bb_handle* h) {
   (void)hipFree(h->d.body_spill); (void)hipFree(h->d.hand); (void)hipFree(h->d.perm); (void)hipFree(h->d.cost); (void)hipFree(h->d.ring); (void)hipFree(h->d.rctr);
   (void)hipFree(h->d.pair_busy); (void)hipFree(h->d.pair_env);
   (void)hipFree(h->tstream); (void)hipFree(h->env_stream); (void)hipFree(h->rng); (void)hipFree(h->seed_slot);
-  (void)hipFree(h->d.tseed);
+  (void)hipFree(h->d.tseed); (void)hipFree(h->tsrc_dev);
   (void)hipStreamDestroy(h->side); (void)hipEventDestroy(h->fork); (void)hipEventDestroy(h->join);
   for (hipEvent_t e : h->tev) (void)hipEventDestroy(e);
   (void)hipFree(h->scenes);
@@ -2705,6 +2721,12 @@ int bb_pair_env_times(bb_handle* h, uint64_t* out) {
   return 0;
 }
 
+// the handle's terrain-draw record to the device (setters run after a device sync)
+static int put_tsrc(bb_handle* h) {
+  HIPCHK(hipMemcpy(h->tsrc_dev, &h->tsrc, sizeof(TerrainSrc), hipMemcpyHostToDevice));
+  return 0;
+}
+
 int bb_set_terrain_stream(bb_handle* h, const int32_t* slots, int n_streams, int length, const int32_t* env_stream) {
   if (!h) return fail("bb_set_terrain_stream: NULL handle");
   if (n_streams < 0) return fail("bb_set_terrain_stream: n_streams must be >= 0 (got %d)", n_streams);
@@ -2712,8 +2734,8 @@ int bb_set_terrain_stream(bb_handle* h, const int32_t* slots, int n_streams, int
   HIPCHK(hipDeviceSynchronize());
   if (n_streams == 0) {
     h->n_streams = 0;
-    h->d.tstream = nullptr; h->d.env_stream = nullptr; h->d.tlen = 0;
-    return 0;
+    h->tsrc.tstream = nullptr; h->tsrc.env_stream = nullptr; h->tsrc.tlen = 0;
+    return put_tsrc(h);
   }
   if (!slots) return fail("bb_set_terrain_stream: NULL slots");
   if (length < 1) return fail("bb_set_terrain_stream: length must be >= 1 (got %d)", length);
@@ -2728,8 +2750,8 @@ int bb_set_terrain_stream(bb_handle* h, const int32_t* slots, int n_streams, int
   } else if (n_streams != 1) {
     return fail("bb_set_terrain_stream: %d streams need an env_stream map", n_streams);
   }
-  // refill in place while the table fits, so a graph captured before this call
-  // reads the new table; a larger table is a new allocation
+  // refill in place while the table fits; a larger table is a new allocation, whose address
+  // goes into the device record that graphs captured before this call read at replay
   if (cnt > h->tstream_cap) {
     (void)hipFree(h->tstream);
     h->tstream = nullptr;
@@ -2744,9 +2766,9 @@ int bb_set_terrain_stream(bb_handle* h, const int32_t* slots, int n_streams, int
   }
   HIPCHK(hipMemset(h->d.episodes, 0, sizeof(int) * h->n));  // the next reset takes draw 0
   h->n_streams = n_streams;
-  h->d.tstream = h->tstream; h->d.env_stream = env_stream ? h->env_stream : nullptr; h->d.tlen = length;
-  h->d.rng = nullptr;  // the table replaces any device generators
-  return 0;
+  h->tsrc.tstream = h->tstream; h->tsrc.env_stream = env_stream ? h->env_stream : nullptr; h->tsrc.tlen = length;
+  h->tsrc.rng = nullptr;  // the table replaces any device generators
+  return put_tsrc(h);
 }
 
 int bb_set_terrain_rng(bb_handle* h, const uint64_t* words, const int32_t* seed_slot) {
@@ -2754,8 +2776,8 @@ int bb_set_terrain_rng(bb_handle* h, const uint64_t* words, const int32_t* seed_
   HIPCHK(hipSetDevice(h->device));
   HIPCHK(hipDeviceSynchronize());
   if (!words) {
-    h->d.rng = nullptr;
-    return 0;
+    h->tsrc.rng = nullptr;
+    return put_tsrc(h);
   }
   if (seed_slot)
     for (int s = 0; s < TERRAIN_SEEDS; s++)
@@ -2779,9 +2801,9 @@ int bb_set_terrain_rng(bb_handle* h, const uint64_t* words, const int32_t* seed_
   }
   HIPCHK(hipMemset(h->d.episodes, 0, sizeof(int) * n));
   HIPCHK(hipMemset(h->d.tseed, 0xFF, sizeof(int) * n));
-  h->d.rng = h->rng;
-  h->d.seed_slot = seed_slot ? h->seed_slot : nullptr;
-  return 0;
+  h->tsrc.rng = h->rng;
+  h->tsrc.seed_slot = seed_slot ? h->seed_slot : nullptr;
+  return put_tsrc(h);
 }
 
 int bb_get_terrain_rng(bb_handle* h, uint64_t* words, int32_t* last_seed) {
@@ -2790,7 +2812,7 @@ int bb_get_terrain_rng(bb_handle* h, uint64_t* words, int32_t* last_seed) {
   HIPCHK(hipDeviceSynchronize());
   const size_t n = h->n;
   if (words) {
-    if (!h->d.rng) return fail("bb_get_terrain_rng: no device generators (bb_set_terrain_rng)");
+    if (!h->tsrc.rng) return fail("bb_get_terrain_rng: no device generators (bb_set_terrain_rng)");
     std::vector<unsigned long long> soa(5 * n);
     HIPCHK(hipMemcpy(soa.data(), h->rng, sizeof(unsigned long long) * 5 * n, hipMemcpyDeviceToHost));
     for (size_t e = 0; e < n; e++)

@@ -32,6 +32,8 @@ def _airborne(oracle, seed):
     q[0:3] = [0.0, 0.0, 2.0]
     q[10:13] = [1.5, 1.5, 2.0]
     v[:] = rng.normal(0, 1, 15)
+    v[0:3] = [0.1, -0.05, 0.2]    # both trees drift up and apart: no ground, no ball-base contact
+    v[9:12] = [0.3, 0.2, 0.25]
     v[3:6] = rng.normal(0, 6, 3)
     v[6:9] = rng.normal(0, 30, 3)
     return q, v

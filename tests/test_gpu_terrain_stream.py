@@ -277,3 +277,45 @@ def test_single_env_reset_seed_reseeds_every_time():
         seen.append(int(env.last_r_seed))
     assert seen == exp
     env.close()
+
+
+def test_captured_step_follows_reseed():
+    """A step captured as a HIP graph before env.seed(s) draws its later terrains from the new
+    generators np_random(s + i) at replay: bb_set_terrain_rng rewrites the device record that
+    the captured Dev points at, in place (the graph holds its address only).  A host-generated
+    bank whose new draws are not resident would need a new handle: refused while graphs exist."""
+    from ballbot_gym.envs import BallbotVecEnv
+    from ballbot_gym.envs.config import stream_draws
+
+    n = 256
+    kw = dict(device="cuda:0", seed=5, terrain_config={"type": "perlin", "config": {}}, max_ep_steps=40)
+    eager, graphed = BallbotVecEnv(n, **kw), BallbotVecEnv(n, **kw)
+    static_a = torch.zeros(n, 3, device="cuda:0")
+    graph = graphed.capture_step(static_a)
+    for e in (eager, graphed):
+        e.seed(77)
+        e.reset()
+    g = torch.Generator(device="cuda:0").manual_seed(3)
+    for t in range(130):  # 40-step episodes: every env resets at least three times after the re-seed
+        a = torch.rand(n, 3, generator=g, device="cuda:0") * 2 - 1
+        eager.step(a)
+        static_a.copy_(a)
+        graph.replay()
+    torch.cuda.synchronize()
+    for x, y in zip(eager.get_state(), graphed.get_state()):
+        np.testing.assert_array_equal(x, y)
+    w_e, s_e = eager.terrain_rng()
+    w_g, s_g = graphed.terrain_rng()
+    np.testing.assert_array_equal(w_e, w_g)
+    _, draws = graphed.env_terrain()
+    assert draws.min() >= 4
+    for i in range(0, n, 37):  # the last drawn seed is np_random(77 + i)'s draw number draws[i] - 1
+        assert s_g[i] == stream_draws(77 + i, int(draws[i]))[-1]
+    eager.close(), graphed.close()
+
+    env = BallbotVecEnv(64, device="cuda:0", seed=1, n_terrains=2, terrain_config={"type": "hills", "config": {}})
+    env.capture_step(torch.zeros(64, 3, device="cuda:0"))
+    env.seed(999)  # hills bank of 2 draws per generator: the new generators' draws are not resident
+    with pytest.raises(RuntimeError, match="HIP graph"):
+        env.reset()
+    env.close()

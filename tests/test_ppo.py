@@ -223,3 +223,19 @@ def test_eval_callback_sb3_timing_targets_and_npz(tmp_path):
     evals = [v for v in cols["eval/mean_reward"] if v is not None]
     np.testing.assert_allclose(evals, d["results"].mean(1), rtol=1e-9)
     assert (tmp_path / "best_model.safetensors").exists()
+
+
+def test_eval_callback_every_multiple_in_a_rollout(tmp_path):
+    """eval_freq below n_steps: SB3's EvalCallback fires at every multiple of eval_freq inside
+    one rollout (its _on_step runs per vec-env step), so a rollout of vec-steps [1, 8] with
+    eval_freq 3 holds evaluations at 3 and 6, then 9, 12, 15 in the next, one npz row each."""
+    from fake_env import FakeEnv
+    from ballbot_rl.training.callbacks import EvalCallback
+
+    cb = EvalCallback(FakeEnv(4, seed=2, ep_len=3), n_eval_episodes=4, eval_freq=3, n_total_envs=4,
+                      log_path=tmp_path / "results")
+    assert cb.due(1, 8) == [3, 6] and cb.due(9, 16) == [9, 12, 15] and cb.due(1, 2) == []
+    m = _ppo(FakeEnv(4, ep_len=5), n_steps=8, batch_size=16, log_dir=str(tmp_path))
+    m.learn(total_timesteps=4 * 8 * 2, rollout_callback=cb)
+    d = np.load(tmp_path / "results" / "evaluations.npz", allow_pickle=False)
+    assert d["timesteps"].tolist() == [12, 24, 36, 48, 60]
