@@ -66,4 +66,6 @@ for s in $STEPS; do
     *) echo "unknown step $s"; exit 2 ;;
   esac
 done
+# the summaries prof_summary wrote under profiles/ travel back with gpurun_out/ (copy them into profiles/ here)
+mkdir -p $O/profiles && cp profiles/traffic.json profiles/${TAG}_* $O/profiles/ 2>/dev/null
 echo SESSION_DONE
