@@ -56,7 +56,7 @@
 extern "C" {
 #endif
 
-#define BB_ABI_VERSION 17
+#define BB_ABI_VERSION 18
 #define BB_NQ 17
 #define BB_NV 15
 #define BB_OBS 15
@@ -216,6 +216,14 @@ typedef struct bb_ppo_mlp_args {
   double beta1, beta2, eps, weight_decay, max_grad_norm;
   float* workspace;
   int64_t workspace_bytes;
+  /* data-parallel update (ABI 18; update_mode="allreduce" over RCCL, ballbot_rl/training/ppo.py):
+   * phase 0 runs the whole minibatch; phase 1 stops after the flat gradient (grad, the log row,
+   * the counters); phase 2 runs only the clip + AdamW step over grad as it then is, its norm
+   * taken from grad itself (after the caller's all-reduce of it).  adv_stats (device float[2]:
+   * mean, 1 / (std + 1e-8)), when non-NULL, replaces the minibatch's own advantage
+   * normalisation -- the global minibatch's statistics, from the ranks' all-reduce. */
+  int32_t phase;
+  const float* adv_stats;
 } bb_ppo_mlp_args;
 int bb_ppo_mlp_workspace_bytes(int B, int64_t* bytes);
 int bb_ppo_mlp_step(const bb_ppo_mlp_args* args, void* stream);

@@ -74,6 +74,8 @@ class PPOMlpArgs(C.Structure):
     ] + [(name, C.c_double) for name in ("beta1", "beta2", "eps", "weight_decay", "max_grad_norm")] + [
         ("workspace", C.c_void_p),
         ("workspace_bytes", C.c_int64),
+        ("phase", C.c_int32),
+        ("adv_stats", C.c_void_p),
     ]
 
 
@@ -110,7 +112,7 @@ EXPORTS = [
     "bb_set_terrain_rng", "bb_get_terrain_rng", "bb_pair_counters", "bb_pair_env_times", "bb_check",
 ]
 
-ABI_VERSION = 17  # include/ballbot_mi355x.h BB_ABI_VERSION
+ABI_VERSION = 18  # include/ballbot_mi355x.h BB_ABI_VERSION
 
 _lib = None
 

@@ -26,10 +26,14 @@ rollout for episode statistics and one per minibatch for the KL early stop
 steps its own env shard; at the update boundary the rollout buffers are
 gathered to rank 0 over RCCL (gather_rollouts), rank 0 runs the update and
 broadcasts the new parameters (update_mode="gather", north_star's design).
-update_mode="allreduce" instead updates data-parallel: every rank takes its
-minibatches (batch_size / world rows each) from its own shard, the gradients
-are averaged with an RCCL all-reduce before the clip and AdamW step, and the
-KL early stop uses the ranks' mean approx_kl, so no rank waits for rank 0.
+update_mode="allreduce" -- the default on more than one rank -- instead updates
+data-parallel: every rank takes its minibatches (batch_size / world rows each)
+from its own shard, the advantages are normalised over the global minibatch, the
+gradients are averaged with an RCCL all-reduce before the clip and AdamW step,
+and the KL early stop uses the ranks' mean approx_kl, so no rank waits for rank
+0.  The all-reduces are nodes of the captured per-minibatch / per-epoch update
+graphs (with the fused minibatch split around them, bb_ppo_mlp_args.phase); the
+eager minibatch loop is the fallback (use_graphs=False, a short last minibatch).
 """
 from __future__ import annotations
 
@@ -242,8 +246,14 @@ class _UpdateGraphs:
 
     LOG_COLS = 6  # loss, pg, vf, ent, kl, clip_fraction
 
-    def __init__(self, ppo: "BatchedPPO", n: int):
-        dev, B = ppo.device, ppo.batch_size
+    def __init__(self, ppo: "BatchedPPO", n: int, B: Optional[int] = None):
+        dev = ppo.device
+        B = ppo.batch_size if B is None else int(B)
+        # data-parallel update (update_mode="allreduce"): each minibatch's graph also holds the
+        # ranks' all-reduces -- the global advantage statistics before the loss, the gradient
+        # between backward and the clip + AdamW step (RCCL collectives captured in the graph)
+        self.dp = ppo._dp
+        self.B = B
         self.n, self.nb = n, n // B
         self.data = {"obs": torch.zeros(n, 15, device=dev), "actions": torch.zeros(n, 3, device=dev),
                      "log_probs": torch.zeros(n, device=dev), "advantages": torch.zeros(n, device=dev),
@@ -256,6 +266,7 @@ class _UpdateGraphs:
         self.k = torch.zeros(1, dtype=torch.int64, device=dev)        # minibatch within the epoch
         self.row = torch.zeros(1, dtype=torch.int64, device=dev)      # log row within the update
         self.clip = torch.zeros((), device=dev)
+        self.adv_stats = torch.zeros(2, device=dev)  # dp: the global minibatch's mean, 1 / (std + 1e-8)
         self.log = torch.zeros(ppo.n_epochs * self.nb, self.LOG_COLS, device=dev)
         self.params = params = [p for p in ppo.policy.parameters() if p.requires_grad]
         # BatchNorm running statistics and num_batches_tracked of the (frozen) encoders: a
@@ -318,15 +329,17 @@ class _UpdateGraphs:
         cams = "depth" in d
         fd = ppo.policy.features_extractor.features_dim
         if cams:  # the minibatch's features (frozen encoders in train mode) land here, in minibatch order
-            self.feats = torch.zeros(ppo.batch_size, fd, device=ppo.device)
+            self.feats = torch.zeros(self.B, fd, device=ppo.device)
         a.obs = self.feats.data_ptr() if cams else d["obs"].data_ptr()
         a.obs_dim, a.obs_direct = int(fd), int(cams)
         a.actions, a.old_logp = d["actions"].data_ptr(), d["log_probs"].data_ptr()
         a.advantages, a.returns = d["advantages"].data_ptr(), d["returns"].data_ptr()
         a.perm, a.mb_counter, a.row_counter, a.log = (t.data_ptr() for t in (self.perm, self.k, self.row, self.log))
         a.clip, a.lr, a.step, a.coef = (t.data_ptr() for t in (self.clip, opt.lr, opt.step_t, opt.coef))
-        a.B = int(ppo.batch_size)
+        a.B = int(self.B)
         a.normalize_advantage = int(ppo.normalize_advantage)
+        dp_norm = self.dp and ppo.normalize_advantage
+        a.adv_stats = self.adv_stats.data_ptr() if dp_norm else None
         a.ent_coef, a.vf_coef = float(ppo.ent_coef), float(ppo.vf_coef)
         a.beta1, a.beta2, a.eps = opt.beta1, opt.beta2, opt.eps
         a.weight_decay, a.max_grad_norm = opt.weight_decay, opt.max_grad_norm
@@ -350,21 +363,51 @@ class _UpdateGraphs:
                         fused_encoder_forward(ext.extractors[key], d["depth"][:, c:c + 1], index=idx))
                 f[:, 53:56].copy_(o15[:, 12:15])            # vel
             stream = C.c_void_p(torch.cuda.current_stream(dev).cuda_stream)
+            if not self.dp:
+                a.phase = 0
+                N.check(lib.bb_ppo_mlp_step(C.byref(a), stream), "bb_ppo_mlp_step")
+                return
+            if dp_norm:
+                self._global_adv_stats(ppo)
+            a.phase = 1  # forward, loss, backward: the flat gradient, the log row, the counters
+            N.check(lib.bb_ppo_mlp_step(C.byref(a), stream), "bb_ppo_mlp_step")
+            ppo._allreduce(opt.grad)  # the ranks' mean gradient
+            opt.grad.div_(ppo.world)
+            a.phase = 2  # clip + AdamW over the mean gradient
             N.check(lib.bb_ppo_mlp_step(C.byref(a), stream), "bb_ppo_mlp_step")
 
         return mb_step
+
+    def _global_adv_stats(self, ppo: "BatchedPPO") -> None:
+        """The global minibatch's advantage mean and 1 / (std + 1e-8) into adv_stats (SB3's
+        normalisation over the union of the ranks' local minibatches: one all-reduce of count,
+        sum and sum of squares, fp64), read by the fused tile kernel (bb_ppo_mlp_args.adv_stats)."""
+        idx = self.perm.index_select(0, self.k).view(-1)
+        a64 = self.data["advantages"][idx].double()
+        t = torch.stack([torch.full((), float(a64.numel()), dtype=torch.float64, device=a64.device), a64.sum(),
+                         (a64 * a64).sum()])
+        ppo._allreduce(t)
+        mean = t[1] / t[0]
+        var = (t[2] - t[0] * mean * mean) / torch.clamp(t[0] - 1.0, min=1.0)
+        std = torch.sqrt(torch.clamp(var, min=0.0))
+        self.adv_stats.copy_(torch.stack([mean, 1.0 / (std + 1e-8)]).float())
 
     def _autograd_step(self, ppo: "BatchedPPO", params, opt):
         def mb_step():
             d = self.data
             idx = self.perm.index_select(0, self.k).view(-1)
+            adv, norm = d["advantages"][idx], None
+            if self.dp and ppo.normalize_advantage:  # the global minibatch's normalisation
+                adv, norm = ppo._global_normalized(adv), False
             loss, pg, vf, ent, kl, cf = ppo._loss(ppo._mb_obs(d, idx), d["actions"][idx], d["log_probs"][idx],
-                                                  d["advantages"][idx], d["returns"][idx], self.clip)
+                                                  adv, d["returns"][idx], self.clip, normalize=norm)
             self.log.index_copy_(0, self.row, torch.stack([loss.detach(), pg, vf, ent, kl, cf]).view(1, -1))
             for p in params:
                 if p.grad is not None:
                     p.grad.zero_()
             loss.backward()
+            if self.dp:  # the ranks' mean gradient before the clip and the step
+                ppo._allreduce_grads(params)
             if not getattr(opt, "clips_grad", False):
                 nn.utils.clip_grad_norm_(params, ppo.max_grad_norm)
             opt.step()
@@ -439,6 +482,9 @@ class _UpdateGraphs:
         _dbg("update: before replay")
         self._replay(total)
         _dbg("update: replayed")
+        if self.dp and ppo.world > 1:  # the global minibatches' terms: the ranks' mean (the KL stop reads it)
+            ppo._allreduce(self.log)
+            self.log.div_(ppo.world)
         log = self.log.cpu().numpy()
         if ppo.target_kl is not None:
             trip = np.nonzero(log[:, 4] > 1.5 * ppo.target_kl)[0]
@@ -534,7 +580,7 @@ class BatchedPPO:
                  logger: Optional[CSVLogger] = None, stats_window_size: int = 100,
                  gae_fn: Callable = gae_hip, policy: Optional[ActorCriticPolicy] = None,
                  use_graphs: Optional[bool] = None, frozen_encoder: Optional[nn.Module] = None,
-                 update_mode: str = "gather"):
+                 update_mode: Optional[str] = None):
         self.env = env
         self.device = torch.device(env.device)
         self.n_envs = int(env.num_envs)
@@ -548,6 +594,8 @@ class BatchedPPO:
         self.gae_fn = gae_fn
         self.rank = dist.get_rank() if dist.is_available() and dist.is_initialized() else 0
         self.world = dist.get_world_size() if dist.is_available() and dist.is_initialized() else 1
+        if update_mode is None:  # data-parallel on several ranks: no rank updates world x the samples
+            update_mode = "allreduce" if self.world > 1 else "gather"
         if update_mode not in ("gather", "allreduce"):
             raise ValueError(f"update_mode must be 'gather' or 'allreduce' (got {update_mode!r})")
         if update_mode == "allreduce" and self.world > 1 and int(batch_size) % self.world:
@@ -563,6 +611,9 @@ class BatchedPPO:
                                  f"has {self.n_envs}, the ranks range over [{int(-t[1])}, {int(t[0])}]): make "
                                  "num_envs divisible by the world size")
         self.update_mode = update_mode
+        # the data-parallel update; _force_dp runs it at world size 1 too (tests: its collectives
+        # are then the identity, so its graph is checked against the eager form on one GPU)
+        self._force_dp = False
         self._dp_adv_hook = None  # tests: called with each data-parallel minibatch's normalised advantages
         torch.manual_seed(int(seed))
         self.cameras = bool(getattr(env, "cameras", False))
@@ -847,28 +898,51 @@ class BatchedPPO:
             out[k] = None if g is None else g.reshape(-1, *v.shape[1:])
         return out if self.rank == 0 else None
 
-    def _graphs_for(self, n: int) -> Optional[_UpdateGraphs]:
-        if n < self.batch_size or n % self.batch_size:
+    def _graphs_for(self, n: int, bsz: Optional[int] = None) -> Optional[_UpdateGraphs]:
+        bsz = self.batch_size if bsz is None else int(bsz)
+        if n < bsz or n % bsz:
             return None
-        if self._graphs is None or self._graphs.n != n:
-            self._graphs = _UpdateGraphs(self, n)
+        if self._graphs is None or self._graphs.n != n or self._graphs.B != bsz or self._graphs.dp != self._dp:
+            self._graphs = _UpdateGraphs(self, n, bsz)
         return self._graphs
 
     def train(self) -> None:
-        if self.world > 1 and self.update_mode == "allreduce":
+        if self._dp:
             self._update(self.buf.flat(), dp=True)  # every rank, its own shard; parameters stay equal
-            for bf in self.policy.buffers():  # BatchNorm statistics (camera encoder) from rank 0
-                dist.broadcast(bf, src=0)
+            if self.world > 1:
+                for bf in self.policy.buffers():  # BatchNorm statistics (camera encoder) from rank 0
+                    dist.broadcast(bf, src=0)
             return
         data = self._gathered()
         if data is not None:
             self._update(data)
         self._sync_params()
 
+    @property
+    def _dp(self) -> bool:
+        return self.update_mode == "allreduce" and (self.world > 1 or self._force_dp)
+
+    def _allreduce(self, t: torch.Tensor) -> None:
+        """Sum t over the ranks in place (RCCL on the GPU; captured when inside a graph); the
+        identity on one rank."""
+        if self.world > 1:
+            dist.all_reduce(t)
+
+    def _allreduce_grads(self, params) -> None:
+        """Average the parameters' gradients over the ranks: one all-reduce of the flattened set."""
+        if self.world == 1:
+            return
+        gs = [p_.grad for p_ in params if p_.grad is not None]
+        fg = torch._utils._flatten_dense_tensors(gs)
+        dist.all_reduce(fg)
+        fg.div_(self.world)
+        for g_, f_ in zip(gs, torch._utils._unflatten_dense_tensors(fg, gs)):
+            g_.copy_(f_)
+
     def _allreduce_mean(self, ts) -> list:
         """The ranks' mean of several scalars, in ONE all-reduce."""
         t = torch.stack([x.detach().float().reshape(()) for x in ts])
-        dist.all_reduce(t)
+        self._allreduce(t)
         return list(t / self.world)
 
     def _global_normalized(self, adv: torch.Tensor) -> torch.Tensor:
@@ -876,12 +950,12 @@ class BatchedPPO:
         with the unbiased std, over the GLOBAL minibatch: the union of the ranks'
         local minibatches (one all-reduce of count, sum and sum of squares)."""
         a64 = adv.detach().double()
-        t = torch.stack([torch.tensor(float(a64.numel()), dtype=torch.float64, device=adv.device), a64.sum(),
+        t = torch.stack([torch.full((), float(a64.numel()), dtype=torch.float64, device=adv.device), a64.sum(),
                          (a64 * a64).sum()])
-        dist.all_reduce(t)
-        n, s1, s2 = float(t[0]), t[1], t[2]
+        self._allreduce(t)
+        n, s1, s2 = t[0], t[1], t[2]  # device scalars: no host sync (graph-capturable)
         mean = s1 / n
-        var = (s2 - n * mean * mean) / max(n - 1.0, 1.0)
+        var = (s2 - n * mean * mean) / torch.clamp(n - 1.0, min=1.0)
         std = torch.sqrt(torch.clamp(var, min=0.0))
         out = ((a64 - mean) / (std + 1e-8)).to(adv.dtype)
         if self._dp_adv_hook is not None:
@@ -935,8 +1009,11 @@ class BatchedPPO:
                 g["lr"].fill_(lr)
             else:
                 g["lr"] = lr
-        graphs = self._graphs_for(n) if self.use_graphs and not dp else None
         bsz = self.batch_size // self.world if dp else self.batch_size
+        # a data-parallel update captures its all-reduces in the graphs: RCCL ("nccl") collectives
+        # can be captured, gloo's (CPU) cannot -- the eager loop then runs them
+        dp_graph = not dp or self.world == 1 or dist.get_backend() == "nccl"
+        graphs = self._graphs_for(n, bsz) if self.use_graphs and dp_graph else None
         loss = torch.zeros((), device=self.device)
         ent_l, pg_l, vf_l, clip_f, kls = [], [], [], [], []
         if graphs is not None:
@@ -977,12 +1054,7 @@ class BatchedPPO:
                     self.optimizer.zero_grad(set_to_none=False)
                     loss.backward()
                     if dp:  # average the gradient over the ranks: one all-reduce (RCCL on the GPU)
-                        gs = [p_.grad for p_ in self.policy.parameters() if p_.grad is not None]
-                        fg = torch._utils._flatten_dense_tensors(gs)
-                        dist.all_reduce(fg)
-                        fg.div_(self.world)
-                        for g_, f_ in zip(gs, torch._utils._unflatten_dense_tensors(fg, gs)):
-                            g_.copy_(f_)
+                        self._allreduce_grads(self.policy.parameters())
                     if not getattr(self.optimizer, "clips_grad", False):
                         nn.utils.clip_grad_norm_(self.policy.parameters(), self.max_grad_norm)
                     self.optimizer.step()

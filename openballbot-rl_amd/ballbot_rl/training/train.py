@@ -80,7 +80,7 @@ def make_env(config: Dict[str, Any], num_envs: int, device, seed: int, precision
 
 
 def main(config: Dict[str, Any], seed: int, out: Optional[str] = None, total_timesteps: Optional[int] = None,
-         precision: str = "fp64", update_mode: str = "gather") -> BatchedPPO:
+         precision: str = "fp64", update_mode: Optional[str] = None) -> BatchedPPO:
     from ballbot_gym.distributed import env_shard, shard_stream_seeds
     from ballbot_rl.evaluation import evaluate_policy
 
@@ -161,8 +161,9 @@ def cli_main() -> None:
     ap.add_argument("--total-timesteps", type=float, default=None)
     ap.add_argument("--out", default=None)
     ap.add_argument("--precision", default="fp64", choices=["fp32", "fp64"])
-    ap.add_argument("--update-mode", default="gather", choices=["gather", "allreduce"],
-                    help="multi-GPU PPO update: gather the rollouts to rank 0 (north_star) or data-parallel")
+    ap.add_argument("--update-mode", default=None, choices=["gather", "allreduce"],
+                    help="multi-GPU PPO update: data-parallel all-reduce (the default on > 1 rank) or gather the "
+                         "rollouts to rank 0 (north_star)")
     args = ap.parse_args()
     cfg = load_training_config(str(Path(args.config).resolve()))
     seed = int(cfg.get("seed", 0))

@@ -2436,6 +2436,7 @@ int bb_ppo_mlp_step(const bb_ppo_mlp_args* a, void* stream) {
                   a->offsets[i], (long long)a->n_params);
   if ((reinterpret_cast<uintptr_t>(a->params) | reinterpret_cast<uintptr_t>(a->grad)) & 15)
     return fail("bb_ppo_mlp_step: params and grad must be 16-byte aligned");
+  if (a->phase < 0 || a->phase > 2) return fail("bb_ppo_mlp_step: phase must be 0, 1 or 2 (got %d)", a->phase);
   MlpStepArgs m;
   m.params = a->params; m.grad = a->grad; m.exp_avg = a->exp_avg; m.exp_avg_sq = a->exp_avg_sq;
   m.n_params = a->n_params;
@@ -2448,6 +2449,7 @@ int bb_ppo_mlp_step(const bb_ppo_mlp_args* a, void* stream) {
   m.B = a->B; m.normalize = a->normalize_advantage ? 1 : 0; m.in_dim = a->obs_dim; m.obs_direct = a->obs_direct ? 1 : 0; m.ent_coef = a->ent_coef; m.vf_coef = a->vf_coef;
   m.beta1 = a->beta1; m.beta2 = a->beta2; m.eps = a->eps; m.weight_decay = a->weight_decay;
   m.max_norm = a->max_grad_norm; m.ws = a->workspace; m.ws_bytes = a->workspace_bytes;
+  m.phase = a->phase; m.adv_stats = a->adv_stats;
   const int rc = launch_mlp_step(m, (hipStream_t)stream);
   if (rc) return fail("bb_ppo_mlp_step: launch failed (%d): %s", rc, hipGetErrorString(hipGetLastError()));
   return 0;

@@ -47,6 +47,12 @@ struct MlpStepArgs {
   double beta1, beta2, eps, weight_decay, max_norm;
   float* ws;
   long long ws_bytes;
+  // data-parallel update: phase 0 the whole minibatch, 1 up to the flat gradient (no optimiser
+  // step), 2 clip + AdamW over the gradient as it then is (after the ranks' all-reduce);
+  // adv_stats (device [2]: mean, 1 / (std + 1e-8)) replaces the minibatch's own advantage
+  // normalisation (the global minibatch's statistics), NULL: the minibatch's own
+  int phase = 0;
+  const float* adv_stats = nullptr;
 };
 
 // the rollout's policy step (SB3 ActorCriticPolicy.forward) for n obs rows

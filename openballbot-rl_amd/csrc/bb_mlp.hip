@@ -117,6 +117,7 @@ struct TileArgs {
   const long long* perm;
   const long long* mb_counter;
   const float* clip;
+  const float* adv_stats;  // TRAIN: external advantage normalisation [mean, 1/(std+1e-8)], or NULL
   int B, normalize;
   float vf_coef;
   Workspace w;
@@ -205,7 +206,10 @@ __global__ __launch_bounds__(T1) void mlp_tile_kernel(TileArgs p) {
   // advantage normalisation over the minibatch (torch.std: unbiased), one pass
   // over memory: each thread keeps its samples in registers
   float amean = 0.f, ainv = 1.f;
-  if (TRAIN && p.normalize && B > 1) {
+  if (TRAIN && p.normalize && B > 1 && p.adv_stats) {  // the global minibatch's (data-parallel update)
+    amean = p.adv_stats[0];
+    ainv = p.adv_stats[1];
+  } else if (TRAIN && p.normalize && B > 1) {
     constexpr int MAXPT = 32;  // B <= 16384 keeps every sample in registers
     float v[MAXPT];
     float s = 0.f;
@@ -610,13 +614,20 @@ int launch_mlp_step(const MlpStepArgs& A, hipStream_t s) {
   if (A.ws_bytes < mlp_workspace_bytes(B)) return -3;
   const Workspace w = carve(A.ws, B, nullptr);
   const int ntiles = B / ROWS, nch = n_chunks(B);
+  if (A.phase == 2) {  // clip + AdamW only: the clip norm from the (all-reduced) flat gradient itself
+    AdamWArgs o{A.params, A.grad, A.exp_avg, A.exp_avg_sq, A.n_params, A.lr, A.step, A.coef, A.beta1, A.beta2,
+                A.weight_decay, float(A.beta2), float(1.0 - A.beta1), float(1.0 - A.beta2), float(A.eps),
+                float(A.max_norm), nullptr, 0};
+    if (launch_adamw_clip(o, s)) return -1;
+    return hipGetLastError() == hipSuccess ? 0 : -1;
+  }
 
   TileArgs t;
   t.P = A.params;
   for (int i = 0; i < MLP_NSLOTS; i++) t.off[i] = A.off[i];
   t.obs = A.obs; t.actions = A.actions; t.old_logp = A.old_logp; t.adv = A.adv; t.returns = A.returns;
   t.perm = A.perm; t.mb_counter = A.mb_counter; t.clip = A.clip;
-  t.B = B; t.normalize = A.normalize; t.vf_coef = A.vf_coef; t.w = w;
+  t.B = B; t.normalize = A.normalize; t.vf_coef = A.vf_coef; t.w = w; t.adv_stats = A.adv_stats;
   t.n = 0; t.noise = nullptr; t.obs_copy = t.act_out = t.act_clipped = t.values_out = t.logp_out = nullptr;
   t.obs_direct = A.obs_direct;
   if (A.in_dim == 15)
@@ -662,6 +673,7 @@ int launch_mlp_step(const MlpStepArgs& A, hipStream_t s) {
   const int nred = (total + 255) / 256;
   if (nred > 4096) return -4;
   hipLaunchKernelGGL(mlp_reduce_kernel, dim3(nred), dim3(256), 0, s, r);
+  if (A.phase == 1) return hipGetLastError() == hipSuccess ? 0 : -1;  // the caller reduces the gradient first
 
   AdamWArgs o{A.params, A.grad, A.exp_avg, A.exp_avg_sq, A.n_params, A.lr, A.step, A.coef, A.beta1, A.beta2,
               A.weight_decay, float(A.beta2), float(1.0 - A.beta1), float(1.0 - A.beta2), float(A.eps),

@@ -59,7 +59,7 @@ def test_gloo_world2_gather_and_max():
     assert seed0 == (None, [5, 6, 7, 8, 9])  # shared stream on request; per-env generators from the global id
 
 
-def _ppo_worker(rank, world, port, q):
+def _ppo_worker(rank, world, port, q, mode="gather"):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world))
     dist.init_process_group("gloo", rank=rank, world_size=world)
     from fake_env import FakeEnv
@@ -67,10 +67,10 @@ def _ppo_worker(rank, world, port, q):
 
     torch.manual_seed(100 + rank)  # different local init: the broadcast must align them
     env = FakeEnv(8, seed=rank, ep_len=4)
-    m = _ppo(env, n_steps=4, batch_size=16, n_epochs=1)
+    m = _ppo(env, n_steps=4, batch_size=16, n_epochs=1, **({} if mode == "default" else {"update_mode": mode}))
     m.learn(total_timesteps=2 * 8 * 4 * world)
     vec = torch.nn.utils.parameters_to_vector(m.policy.parameters()).detach()
-    q.put((rank, m.num_timesteps, m._n_updates, vec.numpy(), len(m.ep_info_buffer)))
+    q.put((rank, m.num_timesteps, m._n_updates, vec.numpy(), len(m.ep_info_buffer), m.update_mode))
     dist.destroy_process_group()
 
 
@@ -87,11 +87,30 @@ def test_gloo_world2_ppo_update_boundary():
     for p in procs:
         p.join(timeout=60)
         assert p.exitcode == 0
-    (_, t0, u0, v0, e0), (_, t1, u1, v1, e1) = res
+    (_, t0, u0, v0, e0, _), (_, t1, u1, v1, e1, _) = res
     assert t0 == t1 == 2 * 8 * 4 * 2        # timesteps count every rank's envs
     assert u0 == 2 and u1 == 0             # SB3 counts epochs: 1 epoch x 2 iterations, on rank 0 only
     assert (v0 == v1).all()
     assert e0 == e1 > 0                    # episode stats gathered from both ranks
+
+
+def test_gloo_world2_default_update_is_data_parallel():
+    """With more than one rank and no update_mode given, every rank updates on its own shard
+    (update_mode="allreduce"): both count the update's epochs, and the parameters stay equal."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_ppo_worker, args=(r, 2, port, q, "default")) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = sorted([q.get(timeout=180) for _ in range(2)], key=lambda x: x[0])
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    (_, t0, u0, v0, e0, m0), (_, t1, u1, v1, e1, m1) = res
+    assert m0 == m1 == "allreduce"
+    assert t0 == t1 == 2 * 8 * 4 * 2 and u0 == u1 == 2
+    assert np.allclose(v0, v1, rtol=0, atol=1e-6)
 
 
 def _dp_worker(rank, world, port, q, target_kl):

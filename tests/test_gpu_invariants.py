@@ -85,17 +85,24 @@ def test_gpu_rk4_matches_oracle_and_converges(oracle):
 
 
 def test_gpu_angular_momentum_conserved_without_gravity(oracle):
+    """Gravity off (BB_DSBL_GRAVITY), airborne: the bodies' angular momentum about the system COM
+    is conserved up to RK4's rotation error, which falls 4x per halving of dt (2 s at 2 ms and
+    at 1 ms), and the COM moves on a straight line.  The kernel's trajectory is the oracle's."""
     q0, v0 = _airborne(oracle, 6)
-    n = 1000  # 2 s at 2 ms
-    qg, vg = _gpu_run(q0, v0, n, disable=64)  # BB_DSBL_GRAVITY; damping on (internal torques)
-    qo, vo = _oracle_run(oracle, q0, v0, n, 0.002, oracle.DISABLE_CONTACT | oracle.DISABLE_GRAVITY)
-    assert np.abs(qg - qo).max() < 1e-8 and np.abs(vg - vo).max() < 1e-6
     P0, L0, c0 = oracle.momentum(q0, v0)
-    P1, L1, c1 = oracle.momentum(qg, vg)
-    assert np.abs(L1 - L0).max() < 1e-4 * np.linalg.norm(L0), (L0, L1)
-    assert np.abs(P1 - P0).max() < 1e-4 * np.linalg.norm(P0)
     mtot = oracle.model_info()["mass"][1:].sum()
-    np.testing.assert_allclose(c1, c0 + P0 / mtot * n * 0.002, atol=1e-4)
+    drift = []
+    for h in (0.002, 0.001):
+        n = int(round(2.0 / h))
+        qg, vg = _gpu_run(q0, v0, n, h=h, disable=64)  # damping on: internal torques
+        if h == 0.002:
+            qo, vo = _oracle_run(oracle, q0, v0, n, h, oracle.DISABLE_CONTACT | oracle.DISABLE_GRAVITY)
+            assert np.abs(qg - qo).max() < 1e-8 and np.abs(vg - vo).max() < 1e-6
+        P1, L1, c1 = oracle.momentum(qg, vg)
+        drift.append(np.abs(L1 - L0).max() / np.linalg.norm(L0))
+        assert np.abs(P1 - P0).max() < 1e-3 * np.linalg.norm(P0)
+        np.testing.assert_allclose(c1, c0 + P0 / mtot * 2.0, atol=1e-4)
+    assert drift[0] < 5e-4 and 3.5 < drift[0] / drift[1] < 4.5, drift
     # the switch acts on the kernel: with gravity on, the ball falls g t^2 / 2 further in 0.2 s
     qa, _ = _gpu_run(q0, v0, 100)
     qb, _ = _gpu_run(q0, v0, 100, disable=64)

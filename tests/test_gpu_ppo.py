@@ -736,3 +736,39 @@ def test_data_parallel_update_on_gpu_ranks():
         assert p.exitcode == 0
     (_, v0, u0, l0), (_, v1, u1, l1) = res
     assert (v0 == v1).all() and u0 == u1 == 4 and l0 == l1 and np.isfinite(l0)
+
+
+@pytest.mark.parametrize("fused", ["1", "0"])
+def test_data_parallel_update_graph_on_one_rank(fused, monkeypatch):
+    """update_mode="allreduce" through the captured update graphs (the form RCCL ranks run: the
+    global advantage statistics and the gradient all-reduce are graph nodes; the fused minibatch
+    splits around them, bb_ppo_mlp_args.phase 1 / 2 with adv_stats).  At world size 1 the
+    collectives are the identity, so the graph must equal the eager data-parallel loop, and the
+    split fused minibatch the unsplit one, to the fp32 reduction-order tolerance.  The RCCL
+    capture itself needs a multi-GPU node: unmeasured on hardware."""
+    from ballbot_rl.training.logger import CSVLogger
+    from ballbot_rl.training.ppo import BatchedPPO
+
+    monkeypatch.setenv("BB_PPO_FUSED", fused)
+    models = []
+    for dp, graphs in ((True, True), (True, False), (False, True)):
+        m = BatchedPPO(_gpu_fake(), n_steps=16, batch_size=512, n_epochs=3, learning_rate=3e-4, target_kl=None,
+                       normalize_advantage=True, seed=4, use_graphs=graphs, update_mode="allreduce",
+                       logger=CSVLogger(None, stdout=False))
+        m._force_dp = dp
+        m.collect_rollouts()
+        models.append(m)
+    d0 = models[0].buf.flat()
+    for m in models:
+        m.shuffle_gen.manual_seed(99)
+        m._update({k: v.clone() for k, v in d0.items()}, dp=m._dp)
+    g = models[0]._graphs
+    assert g is not None and g.dp and g.fused == (fused == "1") and models[1]._graphs is None
+    assert models[0]._n_updates == models[1]._n_updates == models[2]._n_updates == 3
+    for ref in models[1:]:
+        la, lb = models[0].logger.values, ref.logger.values
+        for k in ("train/policy_gradient_loss", "train/value_loss", "train/approx_kl", "train/clip_fraction"):
+            assert la[k] == pytest.approx(lb[k], rel=5e-3, abs=1e-6), k
+        for a, b in zip(models[0].policy.parameters(), ref.policy.parameters()):
+            diff = (a - b).abs()
+            assert float((diff > 1e-5).float().mean()) < 1e-2, float(diff.max())
