@@ -467,6 +467,17 @@ constexpr int F_PARKED = 1 << 17;  // internal: never in a done byte
 // launches), SC_TOUCHED counts the envs of the last launch that needed a full step
 constexpr int SC_ROUTE = 8, SC_TOUCHED = 10, ROUTE_PARK = 1;
 
+// stores of the step's output rows (obs, reward, done, terminal obs, pos2d): -DBB_OUT_NT makes
+// them nontemporal (a diagnostic A/B of the relief pair's output write-backs)
+template <typename V>
+__device__ __forceinline__ void out_st(V* p, V v) {
+#ifdef BB_OUT_NT
+  __builtin_nontemporal_store(v, p);
+#else
+  *p = v;
+#endif
+}
+
 template <typename T, bool HO = true, bool FULLONLY = false>
 __device__ __forceinline__ int team_step(const ModelT<T>& m, const EnvCfg& cfg, const Dev& d, int e, int& tid,
                                          T* q, T* v, T* w, int& step, T* bk, const float* a, EnvWork<T>& W, float* o,
@@ -513,9 +524,9 @@ __device__ __forceinline__ int team_step(const ModelT<T>& m, const EnvCfg& cfg, 
     cnt[3] += slow;
     if (tobs_row) {
 #pragma unroll
-      for (int i = 0; i < 15; i++) tobs_row[i] = o[i];
+      for (int i = 0; i < 15; i++) out_st(tobs_row + i, o[i]);
     }
-    if (p2_row) { p2_row[0] = p2[0]; p2_row[1] = p2[1]; }
+    if (p2_row) { out_st(p2_row, p2[0]); out_st(p2_row + 1, p2[1]); }
     if (reset) {
       tid = next_terrain(d, e);
       st_coh(d.terrain + e, tid);
@@ -1445,9 +1456,9 @@ __device__ __forceinline__ void pair_loop(const ModelT<T>& mg, const EnvCfg& cfg
         if (lead) {
           s_diag[team][1]++;
 #pragma unroll
-          for (int i = 0; i < 15; i++) obs[15 * row + i] = o[i];
-          rew[row] = r;
-          done[row] = uint8_t(fl);
+          for (int i = 0; i < 15; i++) out_st(obs + 15 * row + i, o[i]);
+          out_st(rew + row, r);
+          out_st(done + row, uint8_t(fl));
         }
         k++;
         held++;
