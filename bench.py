@@ -466,6 +466,10 @@ def main() -> None:
             roof["valu_fp64_executed"] = {"flop_per_launch_upper_bound": ex,
                                           "tflops_upper_bound": ex / (kern_ms * 1e-3) / 1e12,
                                           "executed_over_counted": ex / (fpe * envs_dom) if fpe else None}
+            act = prof.get("fp64_flop_active_lanes_per_launch")
+            if act:  # the FP64 FLOPs of the lanes that were active (SQ_INSTS_VALU_FLOPS_FP64)
+                roof["valu_fp64_executed"].update({"flop_per_launch_active_lanes": act,
+                                                   "active_over_counted": act / (fpe * envs_dom) if fpe else None})
         line = {
             "metric": f"env-steps/sec at {n} envs per GPU ({args.terrain} terrain, random actions)",
             "value": value,

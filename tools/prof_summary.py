@@ -155,6 +155,21 @@ def main():
         fl = 64 * (c64[n64[0]] + c64[n64[1]] + 2 * c64[n64[2]] + c64[n64[3]])
         out["pmc_f64"] = {**c64, "dispatches_averaged": n6, "fp64_flop_upper_bound_per_launch": fl,
                           "fp64_tflops_upper_bound": fl / (out["avg_ms_rocprof"] * 1e-3) / 1e12}
+    if (src / "lanes").exists():  # VALU lane occupancy
+        nl = ["SQ_INSTS_VALU_FLOPS_FP64", "SQ_INSTS_VALU_FLOPS_FP64_TRANS", "SQ_THREAD_CYCLES_VALU",
+              "SQ_ACTIVE_INST_VALU"]
+        cl, nn = counters(src / "lanes" / "run_counter_collection.csv", nl, a.pmc_last)
+        # THREAD_CYCLES_VALU / ACTIVE_INST_VALU is the mean number of active lanes per VALU
+        # instruction: 64.0 for torch's elementwise kernels and the perlin generator, 2.7 for a
+        # one-thread kernel in the same passes (calibration).  SQ_INSTS_VALU_FLOPS_FP64
+        # counts FLOPs per wave-instruction (1 add, 2 FMA), not per lane.
+        lanes = {**cl, "dispatches_averaged": nn,
+                 "valu_active_lanes": cl[nl[2]] / max(cl[nl[3]], 1.0)}
+        lanes["valu_active_lane_frac"] = lanes["valu_active_lanes"] / 64.0
+        if "pmc_f64" in out:  # the 64-lane bound scaled by the measured lane occupancy (all VALU alike)
+            lanes["fp64_flop_active_lanes_per_launch"] = (out["pmc_f64"]["fp64_flop_upper_bound_per_launch"]
+                                                          * lanes["valu_active_lane_frac"])
+        out["pmc_lanes"] = lanes
     (Path(str(dst) + "_summary.json")).write_text(json.dumps(out, indent=1))
     print(json.dumps(out, indent=1))
     if a.traffic:  # the entry bench.py reads for a line of exactly this launch shape (profile_entry)
@@ -171,6 +186,7 @@ def main():
             "write_bytes_per_launch": write_b, "issue_frac": out["derived"]["issue_frac"],
             "avg_ms_rocprof": out["avg_ms_rocprof"],
             "fp64_flop_executed_per_launch": (out.get("pmc_f64") or {}).get("fp64_flop_upper_bound_per_launch"),
+            "fp64_flop_active_lanes_per_launch": (out.get("pmc_lanes") or {}).get("fp64_flop_active_lanes_per_launch"),
             "source": str(dst) + "_summary.json"}
         tj.write_text(json.dumps(cur, indent=1))
 

@@ -10,6 +10,8 @@
 #   write  : --pmc WRITE_SIZE
 #   sq     : SQ instruction / wait counters
 #   sq64   : FP64 VALU instruction counters (F64=1)
+#   lanes  : SQ_INSTS_VALU_FLOPS_FP64(_TRANS) (FP64 FLOPs of the active lanes) and VALU thread-cycles
+#            against VALU busy cycles (LANES=1): how much of the 64-lane upper bound is masked lanes
 # Each pass is its own process (counters never combined with traces).
 #   TAG=r05 NAME=flat ARGS="--terrain flat" bash tools/profile.sh
 #   -> gpurun_out/prof_${TAG}_${NAME}/{trace,fetch,write,sq,sq64}; summarise with tools/prof_summary.py
@@ -31,5 +33,9 @@ timeout -s KILL 150 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INST
 if [ "${F64:-1}" = "1" ]; then
   timeout -s KILL 150 rocprofv3 --pmc SQ_INSTS_VALU_ADD_F64 SQ_INSTS_VALU_MUL_F64 SQ_INSTS_VALU_FMA_F64 SQ_INSTS_VALU_TRANS_F64 \
     --output-format csv -d $OUT/sq64 -o run -- python3 $B > $OUT/bench_sq64.json || exit $?
+fi
+if [ "${LANES:-1}" = "1" ]; then  # lane activity: FP64 FLOPs counted per active lane, VALU thread-cycles
+  timeout -s KILL 150 rocprofv3 --pmc SQ_INSTS_VALU_FLOPS_FP64 SQ_INSTS_VALU_FLOPS_FP64_TRANS SQ_THREAD_CYCLES_VALU SQ_ACTIVE_INST_VALU \
+    --output-format csv -d $OUT/lanes -o run -- python3 $B > $OUT/bench_lanes.json || exit $?
 fi
 echo "profile: $OUT"
