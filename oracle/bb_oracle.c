@@ -1567,7 +1567,9 @@ static void forward_impl(const double* qpos, const double* qvel, const double* c
   else {
     int finite = warm_io != NULL;
     for (int i = 0; finite && i < NV; i++) finite = isfinite(warm_io[i]);
-    if (finite) warmstart_choice(&E, w->M, a0, warm_io, a); else memcpy(a, a0, sizeof a);
+    if (finite && !(g_flags & BBO_WARM_ONLY)) warmstart_choice(&E, w->M, a0, warm_io, a);
+    else if (finite) memcpy(a, warm_io, sizeof a);  /* the kernel's start: always the warm start */
+    else memcpy(a, a0, sizeof a);
     BBO_PHASE(3);
     niter = newton(&E, w->M, a0, a, 1.0 / (m->meaninertia * NV));
   }

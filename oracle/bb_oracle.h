@@ -50,6 +50,9 @@ extern "C" {
  * orientation) instead of MuJoCo's sum of the stages' body-frame angular velocities.
  * Pins that the forward dynamics are consistent to 4th order (tests/test_oracle.py). */
 #define BBO_RKMK 8
+/* test-only: start every solve from qacc_warmstart, without MuJoCo's comparison against
+ * qacc_smooth (the kernel's start; DESIGN.md §4 measures the difference) */
+#define BBO_WARM_ONLY 16
 
 /* Per-forward diagnostic outputs (stage-level view of mjData). */
 typedef struct {

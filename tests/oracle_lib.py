@@ -19,7 +19,7 @@ LIB_PATH = ORACLE_DIR / "_build" / "libbb_oracle.so"
 NQ, NV, NB, MAXCON = 17, 15, 8, 356  # MAXCON = 3 + BBO_MAXGROUND 50 + BBO_MAXBODY (3 + 6 x 50)
 HF_N = 293
 
-DISABLE_CONTACT, DISABLE_GRAVITY, DISABLE_DAMPING, RKMK = 1, 2, 4, 8
+DISABLE_CONTACT, DISABLE_GRAVITY, DISABLE_DAMPING, RKMK, WARM_ONLY = 1, 2, 4, 8, 16
 
 
 class ForwardOut(C.Structure):

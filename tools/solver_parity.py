@@ -9,7 +9,8 @@ qvel 1e-6).  The residual is where the two line searches end an iteration at
 different points and MuJoCo's improvement test then stops one Newton iteration
 apart.
 
-  python tools/solver_parity.py [--envs 64] [--steps 120] [--terrain flat|hills|both] [--out profiles/r05_solver_parity.json]
+  python tools/solver_parity.py [--envs 64] [--steps 120] [--terrain flat|hills|both] [--warm-only]
+                                [--out profiles/r05_solver_parity.json]
 """
 import argparse
 import json
@@ -54,9 +55,13 @@ def main():
     ap.add_argument("--steps", type=int, default=120)
     ap.add_argument("--terrain", default="both")
     ap.add_argument("--out", default=None)
+    ap.add_argument("--warm-only", action="store_true",
+                    help="oracle starts every solve from qacc_warmstart, as the kernel does (no comparison "
+                         "against qacc_smooth): separates the warm-start choice from the line search")
     a = ap.parse_args()
     O.build()
     HC.build()
+    O.set_flags(O.WARM_ONLY if a.warm_only else 0)
     res = {}
     if a.terrain in ("flat", "both"):
         res["flat"] = measure(O.flat_hfield(), a.envs, a.steps, seed=3)
@@ -69,7 +74,9 @@ def main():
         print("hills", json.dumps(res["hills"]), flush=True)
     if a.out:
         Path(a.out).write_text(json.dumps({"what": "hostcheck (kernel templates, host build) vs MuJoCo-form oracle, "
-                                                   "teacher-forced one step per recorded state", **res}, indent=1))
+                                                   "teacher-forced one step per recorded state",
+                                        "oracle_warm_start": "qacc_warmstart always" if a.warm_only else "MuJoCo's choice",
+                                        **res}, indent=1))
 
 
 if __name__ == "__main__":
