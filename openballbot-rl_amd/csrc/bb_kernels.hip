@@ -468,7 +468,12 @@ constexpr int F_PARKED = 1 << 17;  // internal: never in a done byte
 constexpr int SC_ROUTE = 8, SC_TOUCHED = 10, ROUTE_PARK = 1;
 
 // stores of the step's output rows (obs, reward, done, terminal obs, pos2d): -DBB_OUT_NT makes
-// them nontemporal (a diagnostic A/B of the relief pair's output write-backs)
+// them nontemporal, -DBB_OUT_SKIP=mask drops some of them in the relief pair (1 obs, 2 reward,
+// 4 done, 8 terminal obs, 16 pos2d): diagnostics of the pair's output write-backs,
+// never in the product build
+#ifndef BB_OUT_SKIP
+#define BB_OUT_SKIP 0
+#endif
 template <typename V>
 __device__ __forceinline__ void out_st(V* p, V v) {
 #ifdef BB_OUT_NT
@@ -522,11 +527,11 @@ __device__ __forceinline__ int team_step(const ModelT<T>& m, const EnvCfg& cfg, 
   const bool reset = auto_reset && (fl & F_TERMINATED);
   if (lead) {
     cnt[3] += slow;
-    if (tobs_row) {
+    if (tobs_row && !(BB_OUT_SKIP & 8)) {
 #pragma unroll
       for (int i = 0; i < 15; i++) out_st(tobs_row + i, o[i]);
     }
-    if (p2_row) { out_st(p2_row, p2[0]); out_st(p2_row + 1, p2[1]); }
+    if (p2_row && !(BB_OUT_SKIP & 16)) { out_st(p2_row, p2[0]); out_st(p2_row + 1, p2[1]); }
     if (reset) {
       tid = next_terrain(d, e);
       st_coh(d.terrain + e, tid);
@@ -1455,10 +1460,12 @@ __device__ __forceinline__ void pair_loop(const ModelT<T>& mg, const EnvCfg& cfg
       } else {
         if (lead) {
           s_diag[team][1]++;
+          if (!(BB_OUT_SKIP & 1)) {
 #pragma unroll
-          for (int i = 0; i < 15; i++) out_st(obs + 15 * row + i, o[i]);
-          out_st(rew + row, r);
-          out_st(done + row, uint8_t(fl));
+            for (int i = 0; i < 15; i++) out_st(obs + 15 * row + i, o[i]);
+          }
+          if (!(BB_OUT_SKIP & 2)) out_st(rew + row, r);
+          if (!(BB_OUT_SKIP & 4)) out_st(done + row, uint8_t(fl));
         }
         k++;
         held++;
