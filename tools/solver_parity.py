@@ -42,7 +42,23 @@ def measure(hf, n_envs, n_steps, seed, size_z=2.0):
     dq, dv = np.array(dq), np.array(dv)
     ok = (dq <= 1e-9) & (dv <= 1e-6)
     worst = np.argsort(-dv)[:5]
+    # each outlier's pre-state stepped again by the oracle with the kernel's start (qacc_warmstart,
+    # no comparison against qacc_smooth): how far the kernel is from THAT oracle step
+    attrib = []
+    for i in np.flatnonzero(~ok):
+        t, e = divmod(int(i), n_envs)
+        q, v, w = rec["qpos"][t][e].copy(), rec["qvel"][t][e].copy(), rec["warm"][t][e].copy()
+        qk, vk, wk = q.copy(), v.copy(), w.copy()
+        HC.env_step(cfg, qk, vk, wk, np.array([rec["steps"][t][e]], np.int32), rec["action"][t][e], hf, size_z)
+        flags = O.lib().bbo_get_flags() if hasattr(O.lib(), "bbo_get_flags") else None
+        O.set_flags(O.WARM_ONLY)
+        O.env_step(O.default_cfg(), q, v, w, np.array([rec["steps"][t][e]], np.int32), rec["action"][t][e], hf, size_z)
+        O.set_flags(0 if flags is None else flags)
+        attrib.append({"t": t, "env": e, "qvel_vs_oracle": float(dv[i]),
+                       "qvel_vs_warm_start_oracle": float(np.abs(vk - v).max()),
+                       "qpos_vs_warm_start_oracle": float(np.abs(qk - q).max())})
     return {"env_steps": int(len(dq)), "within_q1e-9_v1e-6": float(ok.mean()), "outliers": int((~ok).sum()),
+            "outlier_attribution": attrib,
             "qpos_max": float(dq.max()), "qvel_max": float(dv.max()),
             "qpos_p50": float(np.median(dq)), "qvel_p50": float(np.median(dv)),
             "qpos_p999": float(np.quantile(dq, 0.999)), "qvel_p999": float(np.quantile(dv, 0.999)),
