@@ -490,6 +490,7 @@ class _UpdateGraphs:
             trip = np.nonzero(log[:, 4] > 1.5 * ppo.target_kl)[0]
             if len(trip):
                 r = int(trip[0])
+                ppo.kl_stops += 1  # an update that replays: restore + r minibatches again
                 self._restore(ppo.optimizer, snap)
                 self._replay(r)            # the steps before the tripping minibatch
                 self._stats_forward(ppo, r)  # ... and its own forward (BatchNorm statistics)
@@ -614,6 +615,7 @@ class BatchedPPO:
         # the data-parallel update; _force_dp runs it at world size 1 too (tests: its collectives
         # are then the identity, so its graph is checked against the eager form on one GPU)
         self._force_dp = False
+        self.kl_stops = 0  # updates the KL early stop ended (diagnostic: each replays part of the update)
         self._dp_adv_hook = None  # tests: called with each data-parallel minibatch's normalised advantages
         torch.manual_seed(int(seed))
         self.cameras = bool(getattr(env, "cameras", False))

@@ -78,17 +78,18 @@ def main():
                    normalize_advantage=False, weight_decay=0.01, seed=a.seed,
                    logger=CSVLogger(a.out, stdout=False), frozen_encoder=frozen)
     t_roll = t_upd = 0.0
+    roll_times, upd_times = [], []
     orig_collect, orig_train = m.collect_rollouts, m.train
 
     def collect():
         nonlocal t_roll
         torch.cuda.synchronize(); t = time.perf_counter()
-        orig_collect(); torch.cuda.synchronize(); t_roll += time.perf_counter() - t
+        orig_collect(); torch.cuda.synchronize(); roll_times.append(time.perf_counter() - t); t_roll += roll_times[-1]
 
     def train():
         nonlocal t_upd
         torch.cuda.synchronize(); t = time.perf_counter()
-        orig_train(); torch.cuda.synchronize(); t_upd += time.perf_counter() - t
+        orig_train(); torch.cuda.synchronize(); upd_times.append(time.perf_counter() - t); t_upd += upd_times[-1]
 
     m.collect_rollouts, m.train = collect, train
     iters = [0]
@@ -122,6 +123,8 @@ def main():
            "unit": "env-steps/s", "timesteps": m.num_timesteps, "iterations": iters[0], "wall_s": el,
            "rollout_s": t_roll, "update_s": t_upd, "eval_s": t_eval[0],
            "rollout_env_steps_per_s": m.num_timesteps / max(t_roll, 1e-9),
+           "rollout_times_s": [round(x, 4) for x in roll_times], "update_times_s": [round(x, 4) for x in upd_times],
+           "kl_stops": getattr(m, "kl_stops", None),
            "config": {"envs": a.envs, "n_steps": a.n_steps, "batch_size": a.batch, "n_epochs": a.epochs,
                       "terrain": a.terrain, "precision": a.precision, "cameras": a.cameras,
                       "frozen_encoder": frozen is not None, "encoder_pretrain_s": pre_s},
