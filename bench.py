@@ -12,6 +12,7 @@ Prints ONE JSON line (rank 0).
 from __future__ import annotations
 
 import argparse
+import gc
 import json
 import os
 import platform
@@ -336,17 +337,23 @@ def main() -> None:
             dist.barrier()
         torch.cuda.synchronize()
         ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        ev0.record(), ev1.record()  # torch creates an event at its first record: not inside the window
         env.time_kernel(len(chunks(args.steps, m)) if m else args.steps)  # HIP events around each launch, on its stream
         st0 = env.stats()
+        gc.disable()  # no garbage-collector pass inside the window (it would land between launches)
+        torch.cuda.synchronize()
         t0 = time.perf_counter()
         ev0.record()
+        t_ev = time.perf_counter() - t0
         run(args.steps, m)
+        enq = time.perf_counter() - t0  # host time to enqueue the timed launches
         ev1.record()
         torch.cuda.synchronize()
         if world > 1:
             dist.barrier()
         torch.cuda.synchronize()
         elapsed = time.perf_counter() - t0
+        gc.enable()
         step_ms = ev0.elapsed_time(ev1) / args.steps  # whole step sequence per step, torch's stream
         st1 = env.stats()
         if graph is not None:  # graph replays carry no per-kernel events: time eager steps of the same kernels
@@ -355,12 +362,15 @@ def main() -> None:
                 env.step_async_raw(pool[i % PS])
             torch.cuda.synchronize()
         ktimes, kern_n = env.kernel_times()  # fast (or multi-step), predicted-full (side stream), hand-over full
+        timed.enqueue_ms = enq * 1e3
+        timed.event_record_ms = t_ev * 1e3
         return max_over_ranks(elapsed, device=dev), step_ms, ktimes, kern_n, st0, st1
 
     run(args.burn_in + args.warmup, M)
     # the CPU leg's FLOP count replays the timed window's own mix: snapshot it before the window
     mix = mix_snapshot(env, pool, args.steps) if (world == 1 and not args.no_cpu_baseline) else None
     elapsed, step_ms, ktimes, kern_n, st0, st1 = timed(M)
+    enqueue_ms = {"all": timed.enqueue_ms, "torch_event_record": timed.event_record_ms}  # (timed() runs again below)
     pair = env.pair_counters() if (M and env.relief) else None  # the last timed launch (relief pair)
     if pair is not None and pair["claims_fast"] + pair["claims_full"] > 0:
         import numpy as np
@@ -451,6 +461,7 @@ def main() -> None:
             "kernel": kernel, "kernel_ms": kern_ms, "envs_per_launch": envs_dom, "steps_per_launch": spl,
             "kernel_ms_all": ktimes, "full_kernel_envs_per_step": full_per_step,
             "kernel_launches_timed": kern_n, "step_ms_hip_events": step_ms,
+            "host_enqueue_ms": enqueue_ms,
             "flops": fl,
             # the secondary roof, as BASELINE.json asks: algorithmic HBM bytes per launch over the
             # kernel's duration against the 8 TB/s peak

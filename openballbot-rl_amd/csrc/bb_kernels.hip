@@ -2879,6 +2879,10 @@ int bb_time_kernel(bb_handle* h, int max_launches) {
   h->tev.assign(6 * (size_t)max_launches, nullptr);
   h->tpred.assign((size_t)max_launches, 0);
   for (hipEvent_t& e : h->tev) HIPCHK(hipEventCreate(&e));
+  // record each once now: the runtime sets an event up at its first record, which would
+  // otherwise land inside the caller's timed window, between its launches
+  for (hipEvent_t& e : h->tev) HIPCHK(hipEventRecord(e, nullptr));
+  HIPCHK(hipDeviceSynchronize());
   h->tcap = max_launches;
   h->tn = 0;
   return 0;
