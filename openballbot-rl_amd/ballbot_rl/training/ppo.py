@@ -783,12 +783,12 @@ class BatchedPPO:
         T, n = self.n_steps, self.n_envs
         if self._last_obs is None:
             self._last_obs, _ = env.reset()
-        # the whole rollout as one bb_rollout launch on flat banks; on relief banks the per-step
-        # rollout measured faster (perlin PPO, shared terrain stream: 5.13 M rollout env-steps/s
-        # against 4.78 M with bb_rollout's work queue).  BB_FUSED_ROLLOUT=1/0 forces either.
+        # the whole rollout as one bb_rollout launch (on relief banks the relief pair with the
+        # policy in it): 4096 perlin envs on per-env generators, 64-step rollouts, 67 ms per
+        # rollout against 81 ms for the per-step graph below (tools/archive/r5_pair_rollout.sh).
+        # BB_FUSED_ROLLOUT=0 forces the per-step form.
         fr = os.environ.get("BB_FUSED_ROLLOUT", "auto")
-        if (hasattr(env, "run_rollout") and getattr(env, "_host_reward", None) is None and fr != "0"
-                and (fr == "1" or not getattr(env, "relief", True))):
+        if hasattr(env, "run_rollout") and getattr(env, "_host_reward", None) is None and fr != "0":
             return self._collect_rollout_kernel(slots)
         if (self.use_graphs and hasattr(env, "step_flags") and getattr(env, "_host_reward", None) is None
                 and hasattr(env, "obs") and os.environ.get("BB_ROLLOUT_GRAPH", "1") != "0"):

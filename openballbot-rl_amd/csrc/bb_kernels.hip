@@ -1361,15 +1361,30 @@ __device__ __forceinline__ void ring_push(const Dev& d, int kind, int e) {
   st_coh(d.ring + size_t(r) * d.ring_len + (unsigned(t) % unsigned(d.ring_len)), ring_entry(t, e));
 }
 
+// A rollout's per-env carry between steps (ROLL): the observation the policy sees next, the
+// episode-start flag and the Monitor's running return and length.  In LDS while a team holds
+// the env; in RolloutDev's [n] arrays (device-coherent) between holds and at the ends.
+struct RollCarry {
+  float o[16];
+  double ret;
+  long long len;
+  int start;
+};
+
 // one team loop of the relief pair (FULL: the full launch's; wg: this workgroup's index among
-// its kind's working workgroups; the caller checked the gate and the active count)
-template <typename T, bool FULL>
+// its kind's working workgroups; the caller checked the gate and the active count).  ROLL: a
+// PPO rollout (bb_rollout) instead of bb_step_multi's open-loop actions -- per step the team
+// runs the policy on the env's observation (team_policy), samples and clips the action, steps,
+// and keeps the rollout buffer and the Monitor's episode statistics (rollout_kernel's body);
+// K is the rollout length, act and the [K][n] outputs are unused.
+template <typename T, bool FULL, bool ROLL>
 __device__ __forceinline__ void pair_loop(const ModelT<T>& mg, const EnvCfg& cfg, const Dev& d, const float* __restrict__ act,
                                           int K, float* __restrict__ obs, float* __restrict__ rew,
                                           uint8_t* __restrict__ done, float* __restrict__ tobs,
                                           float* __restrict__ pos2d, int auto_reset, int seg,
                                           unsigned long long budget, const int* __restrict__ gate, int wg,
-                                          unsigned char* smem, ModelT<T>& ms, unsigned (*s_cnt)[8], int (*s_diag)[3]) {
+                                          unsigned char* smem, ModelT<T>& ms, unsigned (*s_cnt)[8], int (*s_diag)[3],
+                                          const RolloutDev& ro, RollCarry* s_roll) {
   int* sc = d.slow_count;
   if (threadIdx.x == 0) ms = mg;
   if (threadIdx.x < 32) s_cnt[threadIdx.x >> 3][threadIdx.x & 7] = 0u;
@@ -1440,6 +1455,15 @@ __device__ __forceinline__ void pair_loop(const ModelT<T>& mg, const EnvCfg& cfg
         held = 0;
         held_busy = 0;
         if (lead) { W.bspill = body_spill_of<T>(d, e); s_diag[team][0]++; }
+        if constexpr (ROLL) {  // the env's rollout carry
+          RollCarry& c = s_roll[team];
+          if (tm.tl < 15) c.o[tm.tl] = ld_coh(ro.obs + 15 * size_t(e) + tm.tl);
+          if (lead) {
+            c.start = int(ld_coh(ro.last_starts + e));
+            c.ret = ld_coh(ro.ep_ret + e);
+            c.len = ld_coh(ro.ep_len + e);
+          }
+        }
         team_sync();
       }
     }
@@ -1447,8 +1471,42 @@ __device__ __forceinline__ void pair_loop(const ModelT<T>& mg, const EnvCfg& cfg
     if (e >= 0) {
       const unsigned long long c0 = clock64();
       const size_t row = size_t(k) * n + e;
-      const float* ak = act + 3 * row;
-      const float a[3] = {ak[0], ak[1], ak[2]};
+      float a[3];
+      if constexpr (ROLL) {
+        // SB3 policy step on the carried observation (rollout_kernel's arithmetic); a step the
+        // fast path hands over is redone by the full loop from the same observation and noise,
+        // so its buffer rows are rewritten with the same values
+        RollCarry& c = s_roll[team];
+        float* pol = reinterpret_cast<float*>(W.g);  // x[16], hA[128], hB[128]: contact stores, dead between steps
+        team_sync();
+        if (tm.tl < 15) pol[tm.tl] = c.o[tm.tl];
+        team_sync();
+        float mu[3] = {0.f, 0.f, 0.f}, val = 0.f;
+        team_policy(ro.P, ro.off, pol, pol + 16, pol + 144, tm, mu, val);
+        const float* ls = ro.P + ro.off[MLP_LS];
+        constexpr float HL2PI = 0.91893853320467274f;
+        float araw[3], lp = 0.f;
+#pragma unroll
+        for (int j = 0; j < 3; j++) {
+          const float ls_j = ls[j];
+          araw[j] = __fadd_rn(mu[j], __fmul_rn(ro.noise[3 * row + j], expf(ls_j)));
+          const float z = __fmul_rn(__fsub_rn(araw[j], mu[j]), expf(-ls_j));
+          lp += -0.5f * z * z - ls_j - 0.5f * (2.f * HL2PI);
+          a[j] = fminf(fmaxf(araw[j], -1.f), 1.f);
+        }
+        if (lead) {
+#pragma unroll
+          for (int i = 0; i < 15; i++) ro.b_obs[15 * row + i] = c.o[i];
+#pragma unroll
+          for (int j = 0; j < 3; j++) ro.b_act[3 * row + j] = araw[j];
+          ro.b_val[row] = val;
+          ro.b_logp[row] = lp;
+          ro.b_starts[row] = uint8_t(c.start);
+        }
+      } else {
+        const float* ak = act + 3 * row;
+        a[0] = ak[0]; a[1] = ak[1]; a[2] = ak[2];
+      }
       float o[15], r;
       const int fl = team_step<T, FULL, FULL>(m, cfg, d, e, tid, W.qn, W.vn, W.wn, step, bk, a, W, o, r,
                                                tobs ? tobs + 15 * row : nullptr, pos2d ? pos2d + 2 * row : nullptr,
@@ -1457,6 +1515,24 @@ __device__ __forceinline__ void pair_loop(const ModelT<T>& mg, const EnvCfg& cfg
       if (!FULL && (fl & F_PARKED)) {  // the fast path handed the step over: the full launch redoes it
         next = 1;
         if (lead) s_diag[team][2]++;
+      } else if constexpr (ROLL) {  // collect_rollouts + Monitor bookkeeping (bb_rollout_track)
+        RollCarry& c = s_roll[team];
+        const bool dn = (fl & F_TERMINATED) != 0;
+        if (lead) {
+          s_diag[team][1]++;
+          const double ret = c.ret + double(r);
+          const long long len = c.len + 1;
+          ro.b_rew[row] = r;
+          ro.ep_r[row] = dn ? ret : __builtin_nan("");
+          ro.ep_l[row] = dn ? len : 0;
+          c.ret = dn ? 0.0 : ret;
+          c.len = dn ? 0 : len;
+          c.start = dn ? 1 : 0;
+        }
+        if (tm.tl < 15) c.o[tm.tl] = o[tm.tl];
+        k++;
+        held++;
+        if (k < K) next = predict_env<T>(m, d, tid, W.qn, W.vn, tm.tl, team_shift_of(TEAM)) ? 1 : 0;
       } else {
         if (lead) {
           s_diag[team][1]++;
@@ -1480,6 +1556,15 @@ __device__ __forceinline__ void pair_loop(const ModelT<T>& mg, const EnvCfg& cfg
           T* hr = reinterpret_cast<T*>(d.hand) + size_t(e) * HAND;
           for (int i = tm.tl; i < HAND - 1; i += TEAM) st_coh(hr + i, W.qn[i]);
           if (lead) st_coh(hr + HAND - 1, T(step));
+        }
+        if constexpr (ROLL) {  // the carry, for the next holder (or the caller, after the last step)
+          const RollCarry& c = s_roll[team];
+          if (tm.tl < 15) st_coh(ro.obs + 15 * size_t(e) + tm.tl, c.o[tm.tl]);
+          if (lead) {
+            st_coh(ro.last_starts + e, uint8_t(c.start));
+            st_coh(ro.ep_ret + e, c.ret);
+            st_coh(ro.ep_len + e, c.len);
+          }
         }
         if (lead) {
           if (k >= K) store_state<T, true>(d, e, W.qn, W.vn, W.wn, step);
@@ -1527,19 +1612,21 @@ __global__ __launch_bounds__(64) void relief_pair_kernel(ModelT<T> mg, EnvCfg cf
   __shared__ ModelT<T> ms;
   __shared__ unsigned s_cnt[WAVE / TEAM][8];
   __shared__ int s_diag[WAVE / TEAM][3];  // claims, completed steps, fast-path hand-overs
-  pair_loop<T, FULL>(mg, cfg, d, act, K, obs, rew, done, tobs, pos2d, auto_reset, seg, budget, gate, int(blockIdx.x), smem,
-                     ms, s_cnt, s_diag);
+  pair_loop<T, FULL, false>(mg, cfg, d, act, K, obs, rew, done, tobs, pos2d, auto_reset, seg, budget, gate,
+                            int(blockIdx.x), smem, ms, s_cnt, s_diag, RolloutDev{}, nullptr);
 }
 
 // the pair as ONE launch: SC_ACTIVE[0] workgroups run the fast loop and SC_ACTIVE[1] the full
 // loop, interleaved by groups of NXCD blocks (pair_kind_of); the two loops are disjoint regions
-// of the kernel, so it keeps the larger one's registers, not their union
-template <typename T>
+// of the kernel, so it keeps the larger one's registers, not their union.  ROLL: a rollout
+// (bb_rollout on relief banks; ro), K = ro.T
+template <typename T, bool ROLL>
 __global__ __launch_bounds__(64) void relief_pair1_kernel(ModelT<T> mg, EnvCfg cfg, Dev d, const float* __restrict__ act,
                                                           int K, float* __restrict__ obs, float* __restrict__ rew,
                                                           uint8_t* __restrict__ done, float* __restrict__ tobs,
                                                           float* __restrict__ pos2d, int auto_reset, int seg,
-                                                          unsigned long long budget, const int* __restrict__ gate) {
+                                                          unsigned long long budget, const int* __restrict__ gate,
+                                                          RolloutDev ro) {
   if (gate && *gate == ROUTE_PARK) return;
   int wg = 0;
   const int kind = pair_kind_of(int(blockIdx.x), d.slow_count[SC_ACTIVE], d.slow_count[SC_ACTIVE + 1], &wg);
@@ -1548,12 +1635,13 @@ __global__ __launch_bounds__(64) void relief_pair1_kernel(ModelT<T> mg, EnvCfg c
   __shared__ ModelT<T> ms;
   __shared__ unsigned s_cnt[WAVE / TEAM][8];
   __shared__ int s_diag[WAVE / TEAM][3];
+  __shared__ RollCarry s_roll[ROLL ? WAVE / TEAM : 1];
   if (kind == 0)
-    pair_loop<T, false>(mg, cfg, d, act, K, obs, rew, done, tobs, pos2d, auto_reset, seg, budget, gate, wg, smem, ms,
-                        s_cnt, s_diag);
+    pair_loop<T, false, ROLL>(mg, cfg, d, act, K, obs, rew, done, tobs, pos2d, auto_reset, seg, budget, gate, wg, smem,
+                              ms, s_cnt, s_diag, ro, s_roll);
   else
-    pair_loop<T, true>(mg, cfg, d, act, K, obs, rew, done, tobs, pos2d, auto_reset, seg, budget, gate, wg, smem, ms,
-                       s_cnt, s_diag);
+    pair_loop<T, true, ROLL>(mg, cfg, d, act, K, obs, rew, done, tobs, pos2d, auto_reset, seg, budget, gate, wg, smem,
+                             ms, s_cnt, s_diag, ro, s_roll);
 }
 
 // before the pair: every env's first route (predict_kernel's test) into the
@@ -1781,6 +1869,12 @@ template <typename T> const ModelT<T>& model_of(const bb_handle* h);
 template <> inline const ModelT<float>& model_of<float>(const bb_handle* h) { return h->mf; }
 template <> inline const ModelT<double>& model_of<double>(const bb_handle* h) { return h->md; }
 
+// bb_pair.hip's launch of the relief pair (declared again, with its comment, below)
+extern "C" __attribute__((visibility("hidden"))) int bb_pair_launch_tu(bb_handle* h, int fp64, const float* a, int K,
+                                                                      float* o, float* r, uint8_t* dn, float* t,
+                                                                      float* p2, int ar, hipStream_t s,
+                                                                      const int* gate, const void* ro);
+
 namespace {
 // init height offset (ballbot_env.py:546-563), incl. cell_size = size/nrows
 float init_offset(const float* hf, float size_z) {
@@ -1880,7 +1974,12 @@ int launch_rollout(bb_handle* h, const RolloutDev& ro, hipStream_t s) {
   const int epw = h->epw;
   const int blocks = (h->n + epw - 1) / epw;
   const int route = h->route >= 0 ? h->route : (h->n_relief == 0 ? 1 : 0);
-  if (route == 0 && h->team == 16 && h->multi_queue) {  // relief banks: the work queue with the policy in it
+  if (route == 0 && h->team == 16 && h->multi_queue && h->pair && h->pair_one) {
+    // relief banks: the relief pair with the policy in it (pair_loop<.., ROLL>)
+    if (bb_pair_launch_tu(h, sizeof(T) == 8, nullptr, ro.T, nullptr, nullptr, nullptr, nullptr, nullptr, 1, s, nullptr,
+                          &ro))
+      return fail("bb_rollout: relief pair launch failed");
+  } else if (route == 0 && h->team == 16 && h->multi_queue) {  // relief banks: the work queue with the policy in it
     const Dev dq = balanced_dev(h, s);
     hipLaunchKernelGGL((relief_multi_kernel<T, true>), dim3((h->n + QENV - 1) / QENV), dim3(64 * QW),
                        relief_lds_bytes<T>(), s, model_of<T>(h), h->cfg, dq, (const float*)nullptr, ro.T,
@@ -1903,16 +2002,20 @@ int launch_rollout(bb_handle* h, const RolloutDev& ro, hipStream_t s) {
 // then the split adaptation.  gate: the adaptive route's flag (NULL: always run)
 template <typename T>
 int launch_pair(bb_handle* h, const float* a, int K, float* o, float* r, uint8_t* dn, float* t, float* p2, int ar,
-                hipStream_t s, const int* gate) {
+                hipStream_t s, const int* gate, const RolloutDev* ro) {
   const ModelT<T>& m = model_of<T>(h);
   const size_t plb = multi_lds_bytes<T>(4);
   hipLaunchKernelGGL(pair_clear_kernel, dim3(64), dim3(256), 0, s, h->d, gate);
   hipLaunchKernelGGL(pair_init_kernel<T>, dim3((h->n + WAVE / 16 - 1) / (WAVE / 16)), dim3(WAVE), 0, s, m, h->d, gate,
                      h->pair_heavy_pct);
   hipLaunchKernelGGL(pair_rings_kernel, dim3(1), dim3(64), 0, s, h->d, gate);
-  if (h->pair_one) {
-    hipLaunchKernelGGL(relief_pair1_kernel<T>, dim3(h->pair_cap), dim3(WAVE), plb, s, m, h->cfg, h->d, a, K, o, r, dn, t,
-                       p2, ar, h->pair_seg, h->pair_budget, gate);
+  if (ro) {  // a rollout: the one-launch form (launch_rollout only comes here with pair_one)
+    hipLaunchKernelGGL((relief_pair1_kernel<T, true>), dim3(h->pair_cap), dim3(WAVE), plb, s, m, h->cfg, h->d,
+                       (const float*)nullptr, ro->T, (float*)nullptr, (float*)nullptr, (uint8_t*)nullptr,
+                       (float*)nullptr, (float*)nullptr, 1, h->pair_seg, h->pair_budget, gate, *ro);
+  } else if (h->pair_one) {
+    hipLaunchKernelGGL((relief_pair1_kernel<T, false>), dim3(h->pair_cap), dim3(WAVE), plb, s, m, h->cfg, h->d, a, K, o,
+                       r, dn, t, p2, ar, h->pair_seg, h->pair_budget, gate, RolloutDev{});
   } else {
     HIPCHK(hipEventRecord(h->fork, s));
     HIPCHK(hipStreamWaitEvent(h->side, h->fork, 0));
@@ -1941,7 +2044,7 @@ int launch_pair(bb_handle* h, const float* a, int K, float* o, float* r, uint8_t
 extern "C" __attribute__((visibility("hidden"))) int bb_pair_launch_tu(bb_handle* h, int fp64, const float* a, int K,
                                                                       float* o, float* r, uint8_t* dn, float* t,
                                                                       float* p2, int ar, hipStream_t s,
-                                                                      const int* gate);
+                                                                      const int* gate, const void* ro);
 // Once per handle, in the unit whose pair kernels are the ones launched: their dynamic-LDS
 // limit, and how many one-wave workgroups of relief_pair1_kernel<T> a CU holds at once
 // (*per_cu; the persistent pair's grid is sized from it, bb_create).
@@ -1950,24 +2053,27 @@ extern "C" __attribute__((visibility("hidden"))) int bb_pair_setup_tu(int fp64, 
 template <typename T>
 int pair_setup(int* per_cu) {  // -> a hipError_t (this unit's error text is not the C-ABI's)
   const size_t plb = multi_lds_bytes<T>(4);
-  const void* ks[3] = {(const void*)relief_pair1_kernel<T>, (const void*)relief_pair_kernel<T, false>,
-                       (const void*)relief_pair_kernel<T, true>};
+  const void* ks[4] = {(const void*)relief_pair1_kernel<T, false>, (const void*)relief_pair_kernel<T, false>,
+                       (const void*)relief_pair_kernel<T, true>, (const void*)relief_pair1_kernel<T, true>};
   for (const void* k : ks) {
     const hipError_t e = hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, int(plb));
     if (e != hipSuccess) return int(e);
   }
-  int nb = 0;
-  const hipError_t e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, ks[0], WAVE, plb);
-  *per_cu = nb;
+  // the grid is sized for both one-launch forms (step_multi's and the rollout's)
+  int nb = 0, nr = 0;
+  hipError_t e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, ks[0], WAVE, plb);
+  if (e == hipSuccess) e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&nr, ks[3], WAVE, plb);
+  *per_cu = nb < nr ? nb : nr;
   return int(e);
 }
 extern "C" __attribute__((visibility("hidden"))) int bb_pair_setup_tu(int fp64, int* per_cu) {
   return fp64 ? pair_setup<double>(per_cu) : pair_setup<float>(per_cu);
 }
 extern "C" __attribute__((visibility("hidden"))) int bb_pair_launch_tu(bb_handle* h, int fp64, const float* a, int K, float* o, float* r, uint8_t* dn,
-                                 float* t, float* p2, int ar, hipStream_t s, const int* gate) {
-  return fp64 ? launch_pair<double>(h, a, K, o, r, dn, t, p2, ar, s, gate)
-              : launch_pair<float>(h, a, K, o, r, dn, t, p2, ar, s, gate);
+                                 float* t, float* p2, int ar, hipStream_t s, const int* gate, const void* ro) {
+  const RolloutDev* rd = static_cast<const RolloutDev*>(ro);
+  return fp64 ? launch_pair<double>(h, a, K, o, r, dn, t, p2, ar, s, gate, rd)
+              : launch_pair<float>(h, a, K, o, r, dn, t, p2, ar, s, gate, rd);
 }
 #endif
 
@@ -1976,7 +2082,7 @@ namespace {
 template <typename T>
 int pair_entry(bb_handle* h, const float* a, int K, float* o, float* r, uint8_t* dn, float* t, float* p2, int ar,
                hipStream_t s, const int* gate) {
-  if (bb_pair_launch_tu(h, sizeof(T) == 8, a, K, o, r, dn, t, p2, ar, s, gate))
+  if (bb_pair_launch_tu(h, sizeof(T) == 8, a, K, o, r, dn, t, p2, ar, s, gate, nullptr))
     return fail("bb_step_multi: relief pair launch failed");
   return 0;
 }

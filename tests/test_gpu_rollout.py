@@ -67,17 +67,22 @@ def test_rollout_policy_matches_mlp_act():
     env.close()
 
 
-@pytest.mark.parametrize("terrain,route,park", [("flat", "1", "1"), ("perlin", "1", "1"), ("perlin", "1", "0"),
-                                               ("perlin", "0", "1")])
-def test_rollout_steps_replay_bit_exact(terrain, route, park, monkeypatch):
+@pytest.mark.parametrize("terrain,route,park,pair,n_envs", [("flat", "1", "1", "1", 1024), ("perlin", "1", "1", "1", 256),
+                                                           ("perlin", "1", "0", "1", 256), ("perlin", "0", "1", "1", 256),
+                                                           ("perlin", "0", "1", "0", 256),
+                                                           ("perlin", "0", "1", "1", 4096)])
+def test_rollout_steps_replay_bit_exact(terrain, route, park, pair, n_envs, monkeypatch):
     """The kernel's env steps == bb_step on the kernel's own clipped actions.  Route 1 (fast
     path, hand-over): rollout_kernel, hand-overs parked for a finish launch (BB_MULTI_PARK=1)
-    or inline (0); route 0 on perlin (predictor): the relief work queue with the policy in it."""
+    or inline (0); route 0 on perlin (predictor): the relief pair with the policy in it
+    (relief_pair1_kernel<T, true>, the default), or the relief work queue (BB_RELIEF_PAIR=0);
+    the pair also at PPO's size, 4096 envs on per-env generators."""
     monkeypatch.setenv("BB_ROUTE", route)
     monkeypatch.setenv("BB_MULTI_PARK", park)
-    n, T = (1024, 64) if terrain == "flat" else (256, 96)
+    monkeypatch.setenv("BB_RELIEF_PAIR", pair)
+    n, T = (n_envs, 64) if terrain == "flat" else (n_envs, 96)
     kw = {"max_ep_steps": 30} if terrain == "flat" else {"n_terrains": None, "max_ep_steps": 200,
-                                                          "stream_seeds": [70 + i for i in range(256)]}
+                                                          "stream_seeds": [70 + i for i in range(n)]}
     a, b = _env(n, terrain, **kw), _env(n, terrain, **kw)
     m, slots = _ppo(a, T)
     m._last_obs = a.obs
