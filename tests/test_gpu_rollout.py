@@ -123,6 +123,29 @@ def test_rollout_steps_replay_bit_exact(terrain, route, park, pair, n_envs, monk
     a.close(), b.close()
 
 
+def test_pair_rollout_budget_expiry_is_loud(monkeypatch):
+    """The relief pair's rollout form ends on its wall-clock budget loudly, as bb_step_multi's does
+    (test_gpu_multi_step.py): with BB_PAIR_BUDGET_MS=1 most of the 8x surplus teams wait out the
+    budget, check() raises, the next rollout refuses, and a full reset() clears the fault."""
+    monkeypatch.setenv("BB_PAIR_BUDGET_MS", "1")  # read by bb_create
+    monkeypatch.setenv("BB_ROUTE", "0")
+    monkeypatch.setenv("BB_RELIEF_PAIR", "1")
+    n = 512
+    env = _env(n, "perlin", n_terrains=None, stream_seeds=[90 + i for i in range(n)])
+    m, slots = _ppo(env, 32)
+    m._last_obs = env.obs
+    m._last_starts.fill_(1)
+    m._collect_rollout_kernel(slots)  # asynchronous: no error yet
+    with pytest.raises(RuntimeError, match="wall-clock budget"):
+        env.check()
+    assert env.stats()["pair_budget"] >= 1
+    with pytest.raises(RuntimeError, match="wall-clock budget"):
+        m._collect_rollout_kernel(slots)
+    env.reset()
+    env.check()
+    env.close()
+
+
 def test_learn_with_the_rollout_kernel(monkeypatch):
     """BatchedPPO.learn rolls out with bb_rollout by default: finite losses, episodes logged."""
     monkeypatch.delenv("BB_FUSED_ROLLOUT", raising=False)
