@@ -253,6 +253,34 @@ __attribute__((noinline)) __device__ ApartOut<T> capsule_prism_apart_call(T p00,
 }
 #endif
 
+#ifdef BB_PHASE_CLOCKS
+// (diagnostic) which way capsule_prism goes: 0 the face early-out, 1 the intersecting segment's
+// SAT, 2 the separated segment's distance (capsule_prism_apart); the same tests, in its order
+template <typename T>
+BB_HD int capsule_prism_path(const Seg<T>& g, const PrismG<T>& P) {
+  T p0[3], p1[3];
+  seg_ends(g, p0, p1);
+  T dir[3] = {p1[0] - p0[0], p1[1] - p0[1], p1[2] - p0[2]};
+  for (int f = 0; f < 5; f++) {
+    const T d0 = dot3(P.pn[f], p0) - P.pd[f], d1 = dot3(P.pn[f], p1) - P.pd[f];
+    if (d0 >= g.r && d1 >= g.r) return 0;
+  }
+  T t0 = 0, t1 = 1;
+  bool inter = true;
+  for (int f = 0; f < 5; f++) {
+    const T a0 = dot3(P.pn[f], p0) - P.pd[f], ad = dot3(P.pn[f], dir);
+    if (fabs(ad) < T(1e-30)) {
+      if (a0 > 0) inter = false;
+    } else {
+      const T t = -a0 / ad;
+      if (ad > 0) t1 = minT(t1, t); else t0 = maxT(t0, t);
+    }
+  }
+  if (t0 > t1) inter = false;
+  return inter ? 1 : 2;
+}
+#endif
+
 // capsule vs prism; normal from prism to capsule.  Returns 1 on contact.
 template <typename T>
 BB_HD bool capsule_prism(const Seg<T>& g, const PrismG<T>& P, T& dist, T* n, T* pos) {

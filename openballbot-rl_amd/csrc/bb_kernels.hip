@@ -44,11 +44,8 @@
 using namespace bb;
 
 #ifdef BB_PHASE_CLOCKS
-#ifdef BB_PAIR_TU
-namespace bb { static __device__ unsigned long long bb_phase_cycles[100]; }  // (not read back)
-#else
+// (in bb_pair.hip the name is bb_phase_cycles_pair, renamed there: not read back)
 namespace bb { __device__ unsigned long long bb_phase_cycles[100]; }
-#endif
 #endif
 
 namespace {

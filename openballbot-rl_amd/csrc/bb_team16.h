@@ -1079,6 +1079,10 @@ __device__ int collide_body_team(const ModelT<T>& m, const Kin<T>& k, const floa
         bool hit = false;
         T dist = 0, n[3] = {0, 0, 1}, pos[3] = {0, 0, 0};
         int b2 = 0;
+#if defined(BB_PHASE_CLOCKS) && defined(__HIP_DEVICE_COMPILE__)
+        int sat_path = -1;
+        const unsigned long long sat_c0 = clock64();
+#endif
         if (base + tl < nc) {
           const int code = cand[base + tl];
           const int gi = code >> 26, rr = (code >> 13) & 0x1FFF, p = code & 0x1FFF;
@@ -1095,9 +1099,32 @@ __device__ int collide_body_team(const ModelT<T>& m, const Kin<T>& k, const floa
             asm volatile("" :: "v"(d2), "v"(n2[0]), "v"(p2[0]), "v"(int(h2)) : "memory");
           }
 #endif
+#if defined(BB_PHASE_CLOCKS) && defined(__HIP_DEVICE_COMPILE__)
+          sat_path = gi == 0 ? 3 : capsule_prism_path(g, Pr);
+#endif
           hit = gi == 0 ? cylinder_prism(g, Pr, dist, n, pos) : capsule_prism(g, Pr, dist, n, pos);
           b2 = gi + 1;  // body ids: tower 1, sticks 2-3, wheels 4-6
         }
+#if defined(BB_PHASE_CLOCKS) && defined(__HIP_DEVICE_COMPILE__)
+        {  // SAT rounds: lanes per path, and the rounds each path ran in (the wave runs every path any lane takes)
+          const int sh = team_shift_of(L);
+          auto lanes = [&](bool c) { return __popc(unsigned(__ballot(c) >> sh) & 0xFFFFu); };
+          const int nl = lanes(sat_path >= 0), ncy = lanes(sat_path == 3), neo = lanes(sat_path == 0),
+                    nin = lanes(sat_path == 1), nap = lanes(sat_path == 2), nah = lanes(sat_path == 2 && hit);
+          if (tl == 0) {
+            atomicAdd(&bb_phase_cycles[90], 1ull);
+            atomicAdd(&bb_phase_cycles[91], (unsigned long long)nl);
+            atomicAdd(&bb_phase_cycles[92], (unsigned long long)ncy);
+            atomicAdd(&bb_phase_cycles[93], (unsigned long long)neo);
+            atomicAdd(&bb_phase_cycles[94], (unsigned long long)nin);
+            atomicAdd(&bb_phase_cycles[95], (unsigned long long)nap);
+            atomicAdd(&bb_phase_cycles[96], (unsigned long long)nah);
+            atomicAdd(&bb_phase_cycles[97], (unsigned long long)(nap > 0));
+            atomicAdd(&bb_phase_cycles[98], (unsigned long long)(nin + ncy > 0));
+            atomicAdd(&bb_phase_cycles[99], clock64() - sat_c0);
+          }
+        }
+#endif
         // per-pair cap: a hit is kept while its pair has fewer than MAXPAIR
         // (candidates of one pair sit in consecutive lanes, in prism order)
         bool keep = hit;

@@ -25,7 +25,11 @@ def main():
     ap.add_argument("--warmup", type=int, default=300)
     ap.add_argument("--build", action="store_true")
     ap.add_argument("--terrain", default="flat")
+    ap.add_argument("--lib", default=None, help="a prebuilt -DBB_PHASE_CLOCKS library (e.g. under tools/variants)")
     a = ap.parse_args()
+    global LIB
+    if a.lib:
+        LIB = Path(a.lib)
     from ballbot_gym import _native
     if a.build or not LIB.exists():
         LIB.parent.mkdir(parents=True, exist_ok=True)
@@ -85,6 +89,16 @@ def main():
                                       "body_contacts_per_step": out[50 + b] / max(out[40 + b], 1),
                                       "max_body_contacts_per_step": out[70 + b],
                                       "newton_iters_per_step": out[60 + b] / max(out[40 + b], 1)} for b in range(10)]
+    if out[90]:  # the full kernel's exact-SAT rounds (slots 90-99): lanes per path, rounds per path
+        r = out[90]
+        res["sat_rounds"] = {"rounds": r, "rounds_per_full_forward": r / max(out[12], 1),
+                             "lanes_per_round": out[91] / r,
+                             "lanes": {"cylinder": out[92], "capsule_face_early_out": out[93],
+                                       "capsule_intersecting": out[94], "capsule_apart": out[95],
+                                       "capsule_apart_hits": out[96]},
+                             "rounds_running_apart": out[97] / r, "rounds_running_cylinder_or_intersecting": out[98] / r,
+                             "cycles_per_round": out[99] / r,
+                             "cycles_per_full_forward": out[99] / max(out[12], 1)}
     print(json.dumps(res, indent=1))
 
 
