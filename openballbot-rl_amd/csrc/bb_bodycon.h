@@ -198,8 +198,13 @@ BB_HD inline bool capsule_prism_apart(const Seg<T>& g, const PrismG<T>& P, const
     }
   }
   const int E[9][2] = {{0, 1}, {1, 2}, {2, 0}, {3, 4}, {4, 5}, {5, 3}, {0, 3}, {1, 4}, {2, 5}};
+  // the bottom edges (3-5) are at least the segment's height above the prism's bottom away: when
+  // that is >= r they cannot make a contact, and when a contact exists they are not the closest
+  // feature -- skipping them changes no result (a capsule near the surface is far above it)
+  const bool bottom = minT(p0[2], p1[2]) - P.V[3][2] < g.r;
 #pragma unroll
   for (int e = 0; e < 9; e++) {
+    if (e >= 3 && e <= 5 && !bottom) continue;
     T cp[3], cq[3];
     const T d2 = seg_seg2(p0, p1, P.V[E[e][0]], P.V[E[e][1]], cp, cq);
     if (d2 < best2) {
