@@ -252,7 +252,10 @@ int bb_ppo_mlp_act(const float* params_dev, const int32_t* offsets, int64_t n_pa
  * team, in another summation order than bb_ppo_mlp_act's MFMA tiles (equal to
  * fp32 rounding); the env step is bb_step_multi's (bit-identical to bb_step's
  * serial route for the same clipped actions).  Built-in rewards only (not
- * BB_REWARD_NONE).  One launch; graph-capturable. */
+ * BB_REWARD_NONE).  One launch; graph-capturable.  On relief banks it runs as
+ * bb_step_multi's relief pair (persistent, with the policy inside): a launch
+ * that ends on the pair's wall-clock budget raises the handle's sticky fault
+ * (bb_check), as bb_step_multi does. */
 typedef struct bb_rollout_args {
   const float* params;      /* flat fp32 policy parameters, bb_ppo_mlp_act's slots, except that the eight
                                trunk weight matrices (slots 0-3, 8-11) are stored input-major (W^T,
