@@ -67,11 +67,11 @@ def test_rollout_policy_matches_mlp_act():
     env.close()
 
 
-@pytest.mark.parametrize("terrain,route,park,pair,n_envs", [("flat", "1", "1", "1", 1024), ("perlin", "1", "1", "1", 256),
-                                                           ("perlin", "1", "0", "1", 256), ("perlin", "0", "1", "1", 256),
-                                                           ("perlin", "0", "1", "0", 256),
-                                                           ("perlin", "0", "1", "1", 4096)])
-def test_rollout_steps_replay_bit_exact(terrain, route, park, pair, n_envs, monkeypatch):
+@pytest.mark.parametrize("terrain,route,park,pair,n_envs,precision", [
+    ("flat", "1", "1", "1", 1024, "fp64"), ("perlin", "1", "1", "1", 256, "fp64"), ("perlin", "1", "0", "1", 256, "fp64"),
+    ("perlin", "0", "1", "1", 256, "fp64"), ("perlin", "0", "1", "0", 256, "fp64"), ("perlin", "0", "1", "1", 4096, "fp64"),
+    ("perlin", "0", "1", "1", 256, "fp32")])
+def test_rollout_steps_replay_bit_exact(terrain, route, park, pair, n_envs, precision, monkeypatch):
     """The kernel's env steps == bb_step on the kernel's own clipped actions.  Route 1 (fast
     path, hand-over): rollout_kernel, hand-overs parked for a finish launch (BB_MULTI_PARK=1)
     or inline (0); route 0 on perlin (predictor): the relief pair with the policy in it
@@ -83,6 +83,7 @@ def test_rollout_steps_replay_bit_exact(terrain, route, park, pair, n_envs, monk
     n, T = (n_envs, 64) if terrain == "flat" else (n_envs, 96)
     kw = {"max_ep_steps": 30} if terrain == "flat" else {"n_terrains": None, "max_ep_steps": 200,
                                                           "stream_seeds": [70 + i for i in range(n)]}
+    kw["precision"] = precision
     a, b = _env(n, terrain, **kw), _env(n, terrain, **kw)
     m, slots = _ppo(a, T)
     m._last_obs = a.obs
