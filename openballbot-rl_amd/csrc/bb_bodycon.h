@@ -313,6 +313,14 @@ BB_HD bool capsule_prism(const Seg<T>& g, const PrismG<T>& P, T& dist, T* n, T* 
   if (t0 > t1) inter = false;
   if (!inter) {
 #if defined(__HIP_DEVICE_COMPILE__) && !defined(BB_CAPSULE_INLINE)
+#ifdef BB_EXP_DUP_APART  // timing experiment (tools/lib_bench): the separated-segment distance twice
+    {
+      const ApartOut<T> o2 = capsule_prism_apart_call(p0[0], p0[1], p0[2], p1[0], p1[1], p1[2], g.r, P.V[0][0],
+                                                      P.V[0][1], P.V[0][2], P.V[1][0], P.V[1][1], P.V[1][2],
+                                                      P.V[2][0], P.V[2][1], P.V[2][2], P.V[3][2]);
+      asm volatile("" :: "v"(o2.dist), "v"(o2.n[0]), "v"(o2.pos[0]) : "memory");
+    }
+#endif
     const ApartOut<T> o = capsule_prism_apart_call(p0[0], p0[1], p0[2], p1[0], p1[1], p1[2], g.r, P.V[0][0], P.V[0][1],
                                                    P.V[0][2], P.V[1][0], P.V[1][1], P.V[1][2], P.V[2][0], P.V[2][1],
                                                    P.V[2][2], P.V[3][2]);
@@ -401,9 +409,15 @@ BB_HD bool cylinder_prism(const Seg<T>& g, const PrismG<T>& P, T& dist, T* n, T*
     if (dm <= 0) sep = true;
     if (dm < bestd) { bestd = dm; bn[0] = -ax[0]; bn[1] = -ax[1]; bn[2] = -ax[2]; }
   };
+  // a separating axis decides the result (no contact) whatever the later axes give: leave at
+  // the first group that finds one (the face normals, most often the top face's, for a tower
+  // above the terrain), so most non-touching candidates skip the other eleven axes
+  test(P.pn[0]);  // the top face first: it separates most non-touching candidates by itself
+  if (sep) return false;
 #pragma unroll
-  for (int f = 0; f < 5; f++) test(P.pn[f]);
+  for (int f = 1; f < 5; f++) test(P.pn[f]);
   test(g.a);
+  if (sep) return false;
 #pragma unroll
   for (int k = 0; k < 4; k++) {
     T e[3] = {0, 0, 1};
@@ -413,6 +427,7 @@ BB_HD bool cylinder_prism(const Seg<T>& g, const PrismG<T>& P, T& dist, T* n, T*
     const T xl = sqrt(dot3(x, x));
     if (xl > T(1e-12) * (sqrt(dot3(e, e)) + T(1e-30))) { x[0] /= xl; x[1] /= xl; x[2] /= xl; test(x); }
   }
+  if (sep) return false;
 #pragma unroll
   for (int v = 0; v < 6; v++) {
     T d[3] = {P.V[v][0] - g.c[0], P.V[v][1] - g.c[1], P.V[v][2] - g.c[2]};
@@ -448,6 +463,22 @@ BB_HD bool cylinder_prism(const Seg<T>& g, const PrismG<T>& P, T& dist, T* n, T*
   for (int k = 0; k < 3; k++) pos[k] = sp[k] - n[k] * (dist * T(0.5));
   return true;
 }
+
+#if defined(__HIP_DEVICE_COMPILE__) && defined(BB_EXP_DUP_CYL)
+// timing experiment: cylinder_prism from scalars, as a call (bb_team16.h BB_EXP_DUP_CYL)
+template <typename T>
+__attribute__((noinline)) __device__ T cylinder_prism_dup_call(T c0, T c1, T c2, T a0, T a1, T a2, T hh, T r, T v00,
+                                                             T v01, T v02, T v10, T v11, T v12, T v20, T v21, T v22,
+                                                             T zb) {
+  const T Tp[3][3] = {{v00, v01, v02}, {v10, v11, v12}, {v20, v21, v22}};
+  PrismG<T> P;
+  prism_build(P, Tp, zb);
+  Seg<T> g;
+  g.c[0] = c0; g.c[1] = c1; g.c[2] = c2; g.a[0] = a0; g.a[1] = a1; g.a[2] = a2; g.hh = hh; g.r = r;
+  T d = 0, n[3], pos[3];
+  return cylinder_prism(g, P, d, n, pos) ? d : T(1e30);
+}
+#endif
 
 // sphere (geom1) vs cylinder (geom2); normal from sphere to cylinder
 template <typename T>

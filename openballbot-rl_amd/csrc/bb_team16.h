@@ -1102,6 +1102,15 @@ __device__ int collide_body_team(const ModelT<T>& m, const Kin<T>& k, const floa
 #if defined(BB_PHASE_CLOCKS) && defined(__HIP_DEVICE_COMPILE__)
           sat_path = gi == 0 ? 3 : capsule_prism_path(g, Pr);
 #endif
+#ifdef BB_EXP_DUP_CYL  // timing experiment: the tower's cylinder SAT once more, as a call (an inlined copy
+                       // spills the pair's registers and measures the spills)
+          if (gi == 0) {
+            const T d2 = cylinder_prism_dup_call(g.c[0], g.c[1], g.c[2], g.a[0], g.a[1], g.a[2], g.hh, g.r, V[0][0],
+                                                 V[0][1], V[0][2], V[1][0], V[1][1], V[1][2], V[2][0], V[2][1],
+                                                 V[2][2], -zb);
+            asm volatile("" :: "v"(d2) : "memory");
+          }
+#endif
           hit = gi == 0 ? cylinder_prism(g, Pr, dist, n, pos) : capsule_prism(g, Pr, dist, n, pos);
           b2 = gi + 1;  // body ids: tower 1, sticks 2-3, wheels 4-6
         }
