@@ -1032,11 +1032,23 @@ __device__ __forceinline__ bool predict_env(const ModelT<T>& m, const Dev& d, in
 #endif
     const int nc = cmax - cmin, total = (rmax - rmin) * nc;
     bool hit = false;
+    // cell i's four heights; the next cell's are loaded while this one is tested
+    auto cellz = [&](int i, float (&z)[4]) {
+      if (i < total) {
+        const int r = rmin + i / nc, c = cmin + i % nc;
+        z[0] = hf[r * HF_N + c]; z[1] = hf[(r + 1) * HF_N + c];
+        z[2] = hf[r * HF_N + c + 1]; z[3] = hf[(r + 1) * HF_N + c + 1];
+      }
+    };
+    float znext[4] = {0.f, 0.f, 0.f, 0.f};
+    cellz(tl, znext);
     for (int i = tl; i < total && !hit; i += PL) {  // cell i of the sub-grid, row-major
+      const float zc[4] = {znext[0], znext[1], znext[2], znext[3]};
+      cellz(i + PL, znext);
       const int r = rmin + i / nc, c = cmin + i % nc;
       const T x0 = dx * c - sx, x1 = dx * (c + 1) - sx, y0 = dy * r - sy, y1 = dy * (r + 1) - sy;
-      const T z00 = T(hf[r * HF_N + c]) * size_z, z10 = T(hf[(r + 1) * HF_N + c]) * size_z;
-      const T z01 = T(hf[r * HF_N + c + 1]) * size_z, z11 = T(hf[(r + 1) * HF_N + c + 1]) * size_z;
+      const T z00 = T(zc[0]) * size_z, z10 = T(zc[1]) * size_z;
+      const T z01 = T(zc[2]) * size_z, z11 = T(zc[3]) * size_z;
       if (maxT(maxT(z00, z10), maxT(z01, z11)) < lo) continue;
       const T A[3][3] = {{x0, y0, z00}, {x0, y1, z10}, {x1, y0, z01}};
       const T B[3][3] = {{x0, y1, z10}, {x1, y0, z01}, {x1, y1, z11}};

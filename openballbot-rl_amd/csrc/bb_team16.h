@@ -834,10 +834,26 @@ __device__ __forceinline__ int collide_team(const ModelT<T>& m, const Kin<T>& k,
   (void)v;
   const int team_shift = team_shift_of(L);
   int ng = 0;
+  // the heights of prism P's three top vertices; the next round's are loaded while this round
+  // is tested, so a round does not wait for its loads (one wave per SIMD hides no latency)
+  auto heights = [&](int P, float (&h)[3]) {
+    if (P < total) {
+      const int rr = rmin + P / np, p = P % np;
+#pragma unroll
+      for (int t = 0; t < 3; t++) {
+        const int vt = p + t;
+        h[t] = hf[(rr + (vt & 1)) * HF_N + cmin + (vt >> 1)];
+      }
+    }
+  };
+  float hnext[3] = {0.f, 0.f, 0.f};
+  heights(tl, hnext);
   for (int base = 0; base < total; base += L) {
     const int P = base + tl;
     bool hit = false;
     T nn[3] = {0, 0, 1}, dist = 0;
+    const float hcur[3] = {hnext[0], hnext[1], hnext[2]};
+    heights(P + L, hnext);
     if (P < total) {
       const int rr = rmin + P / np, p = P % np;
       T V[3][3];
@@ -846,7 +862,8 @@ __device__ __forceinline__ int collide_team(const ModelT<T>& m, const Kin<T>& k,
         const int vt = p + t, cc = cmin + (vt >> 1), ri = rr + (vt & 1);
         V[t][0] = dx * cc - sx;
         V[t][1] = dy * ri - sy;
-        V[t][2] = T(hf[ri * HF_N + cc]) * size_z;
+        V[t][2] = T(hcur[t]) * size_z;
+        (void)ri; (void)cc;
       }
       if (!(V[0][2] < zmin && V[1][2] < zmin && V[2][2] < zmin)) {
         const T bx0 = minT(V[0][0], minT(V[1][0], V[2][0])), bx1 = maxT(V[0][0], maxT(V[1][0], V[2][0]));
@@ -1186,14 +1203,35 @@ __device__ int collide_body_team(const ModelT<T>& m, const Kin<T>& k, const floa
         asm volatile("" :: "s"(bal) : "memory");
       }
 #endif
+      // the next round's vertex heights are loaded while this round is tested (as collide_team)
+      auto heights = [&](int P, float (&h)[3]) {
+        if (P < total) {
+          const int rr = rmin + P / np, p = 2 * cmin + P % np;
+#pragma unroll
+          for (int t = 0; t < 3; t++) {
+            const int vt = p + t;
+            h[t] = hf[(rr + (vt & 1)) * HF_N + (vt >> 1)];
+          }
+        }
+      };
+      float hnext[3] = {0.f, 0.f, 0.f};
+      heights(tl, hnext);
       for (int base = 0; base < total; base += L) {
         const int P = base + tl;
         bool cand_hit = false;
         int code = 0;
+        const float hcur[3] = {hnext[0], hnext[1], hnext[2]};
+        heights(P + L, hnext);
         if (P < total) {
           const int rr = rmin + P / np, p = 2 * cmin + P % np;
           T V[3][3];
-          vertices(rr, p, V);
+#pragma unroll
+          for (int t = 0; t < 3; t++) {  // vertices(rr, p, V), with the prefetched heights
+            const int vt = p + t;
+            V[t][0] = dx * (vt >> 1) - sx;
+            V[t][1] = dy * (rr + (vt & 1)) - sy;
+            V[t][2] = T(hcur[t]) * size_z;
+          }
           cand_hit = !(V[0][2] < lo[2] && V[1][2] < lo[2] && V[2][2] < lo[2]) && prism_may_hit(gr, V);
           code = (gi << 26) | (rr << 13) | p;
         }
