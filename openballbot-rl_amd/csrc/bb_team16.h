@@ -372,6 +372,11 @@ __device__ int solve16(const ModelT<T>& m, EnvWork<T>& W, int ng, int nb, T* a, 
   for (; it < m.maxiter; it++) {
     team_sync();
     PH_TOP
+    // the lane index as the sweeps see it, redefined each iteration: otherwise the compiler hoists
+    // the fifteen (lane == j) masks out of the Newton loop, keeps them in SGPR pairs and spills
+    // them to VGPR lanes, and every use costs two v_readlane and a hazard wait (flat -1.2%)
+    int tlx = tl;
+    asm volatile("" : "+v"(tlx));
     // ---- (1) contact pass, contact-parallel (c = tl, tl + 16, ...): the
     // wheels' cone force f and Hessian C (3x3, packed) into LDS for the row
     // owners; ball-terrain contacts add ball-block gradient and C-weighted J'J
@@ -678,7 +683,7 @@ __device__ int solve16(const ModelT<T>& m, EnvWork<T>& W, int ng, int nb, T* a, 
       team_sync();
     }
 #endif
-    chol_solve_rows(h, diag, gi, s, sown, tl, &W.u.hes.cj[0][0][0]);  // cj is dead after the Hessian
+    chol_solve_rows(h, diag, gi, s, sown, tlx, &W.u.hes.cj[0][0][0]);  // cj is dead after the Hessian
     T d0 = tsum(sown * gi);
     bool fin = true;
 #pragma unroll
