@@ -27,6 +27,10 @@ for _p in (ROOT / "openballbot-rl_amd", ROOT / "tests"):
 
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
 FP64_VECTOR_PEAK_TFLOPS = 78.6  # MI355X spec: half the 157.3 TF FP32 vector rate (MI355X_MICROARCH.md)
+# the yardstick of roofline.achieved: the oracle's op count (oracle/flopcount.cpp) of MuJoCo's solver
+# as restated since round 5 (PrimalSearch line search, warm-start choice); rounds before 5 counted
+# the kernel-borrowed search (825,731 FLOP per flat env-step in round 4 against 942,434 now)
+FLOP_BASIS = "oracle-PrimalSearch-r5"
 
 
 def algorithmic_bytes(precision: str, steps_per_launch: float = 1, relief: bool = False) -> float:
@@ -268,7 +272,10 @@ def main() -> None:
     # one-GPU box; the driver's multi-GPU runs use RCCL ("nccl"), one GPU per rank
     backend = os.environ.get("BB_BENCH_BACKEND", "nccl")
     gpu = local % max(torch.cuda.device_count(), 1) if backend != "nccl" else local
-    if world > 1:
+    # BB_BENCH_FORCE_PG=1: the process group (and its barriers / max-over-ranks all-reduce) at
+    # world size 1 too -- runs the RCCL path of the driver's multi-GPU line on a one-GPU box
+    use_pg = world > 1 or os.environ.get("BB_BENCH_FORCE_PG", "0") == "1"
+    if use_pg:
         os.environ.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
         torch.cuda.set_device(gpu)
         if backend == "nccl":
@@ -333,7 +340,7 @@ def main() -> None:
     def timed(m):
         """args.steps steps, m per launch, bracketed by barrier + synchronize; the MAX over ranks."""
         torch.cuda.synchronize()
-        if world > 1:
+        if use_pg:
             dist.barrier()
         torch.cuda.synchronize()
         ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
@@ -349,7 +356,7 @@ def main() -> None:
         enq = time.perf_counter() - t0  # host time to enqueue the timed launches
         ev1.record()
         torch.cuda.synchronize()
-        if world > 1:
+        if use_pg:
             dist.barrier()
         torch.cuda.synchronize()
         elapsed = time.perf_counter() - t0
@@ -446,6 +453,8 @@ def main() -> None:
                 fl = {"error": repr(e)}
         if fl is None or "error" in fl:
             fl = committed_flops(args.terrain) or fl
+        if fl and "error" not in fl:
+            fl.setdefault("basis", FLOP_BASIS)
         fpe = (fl or {}).get("flops_per_env_step")
         tf = fpe * envs_dom / (kern_ms * 1e-3) / 1e12 if fpe else None
         roof = {
@@ -481,6 +490,9 @@ def main() -> None:
             if act:  # the FP64 FLOPs of the lanes that were active (SQ_INSTS_VALU_FLOPS_FP64)
                 roof["valu_fp64_executed"].update({"flop_per_launch_active_lanes": act,
                                                    "active_over_counted": act / (fpe * envs_dom) if fpe else None})
+                # the hardware's view on the same peak: the executed FP64 of the active lanes (same-shape
+                # profile) over this run's kernel time -- independent of the FLOP-count basis
+                roof["frac_executed"] = act / (kern_ms * 1e-3) / 1e12 / FP64_VECTOR_PEAK_TFLOPS
         line = {
             "metric": f"env-steps/sec at {n} envs per GPU ({args.terrain} terrain, random actions)",
             "value": value,
@@ -505,6 +517,7 @@ def main() -> None:
                        "multi_step": M, "steps_per_launch": spl,
                        "envs_per_gpu": n, "total_envs": n * world, "precision": args.precision,
                        "parallelism": f"env-sharded x{world} (no collective on the step path)",
+                       "process_group": dist.get_backend() if use_pg else None,
                        "launch": launch},
             "roofline": roof,
             "stats": stats,
@@ -531,7 +544,7 @@ def main() -> None:
                                                               fields_desc=desc)
         print(json.dumps(line), flush=True)
     env.close()
-    if world > 1:
+    if use_pg:
         dist.destroy_process_group()
 
 

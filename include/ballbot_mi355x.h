@@ -56,7 +56,7 @@
 extern "C" {
 #endif
 
-#define BB_ABI_VERSION 18
+#define BB_ABI_VERSION 19
 #define BB_NQ 17
 #define BB_NV 15
 #define BB_OBS 15
@@ -68,7 +68,7 @@ extern "C" {
 #define BB_DONE_DIVERGED 4 /* MuJoCo's divergence reset ran inside this step (informational) */
 #define BB_DONE_OVERFLOW 8
 #define BB_NSTATS 8
-#define BB_NPAIR 16
+#define BB_NPAIR 19
 
 /* reward kinds (built-in reward plugins, ballbot_gym/rewards) */
 #define BB_REWARD_DIRECTIONAL 0 /* rewards/directional.py:33-54 */
@@ -364,7 +364,9 @@ int bb_get_terrain_rng(bb_handle* h, uint64_t* words_host, int32_t* last_seed_ho
 /* current bank slot and number of stream draws of every env (host int32[n] each, may be NULL) */
 int bb_get_env_terrain(bb_handle* h, int32_t* terrain_host, int32_t* draws_host);
 
-/* reset envs where mask_dev[i] != 0 (mask NULL = all); writes reset obs */
+/* reset envs where mask_dev[i] != 0 (mask NULL = all); writes reset obs.  A full reset (mask
+ * NULL) clears the sticky fault of bb_check: when the fault is set it waits for `stream` so that
+ * a bb_step* call straight after it steps (asynchronous, and capturable, otherwise). */
 int bb_reset(bb_handle* h, const uint8_t* mask_dev, float* obs_dev, void* stream);
 
 /* one env.step for all envs.  actions_dev float[n][3]; obs_dev float[n][15];
@@ -419,7 +421,8 @@ int bb_get_stats(bb_handle* h, int64_t* out, int n);
  * n (<= BB_NPAIR) of [team-cycles stepping (fast, full), idle loop passes (fast, full), working
  * workgroups of the next launch (fast, full), env claims (fast, full), completed env-steps (fast,
  * full), fast-path hand-overs to the full launch, team lifetimes in shader cycles (fast, full), team
- * lifetimes in wall-clock ticks (fast, full), envs marked heavy for the solo waves].  No
+ * lifetimes in wall-clock ticks (fast, full), envs marked heavy for the solo waves, the ring length,
+ * appends to the least-used fast ring and to the least-used full ring (laps = appends / length)].  No
  * reference counterpart (tools/). */
 int bb_pair_counters(bb_handle* h, int64_t* out, int n);
 /* per env, the last relief-pair launch (waits for the device): out[0:n] shader cycles its steps

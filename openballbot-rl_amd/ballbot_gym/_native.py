@@ -112,7 +112,7 @@ EXPORTS = [
     "bb_set_terrain_rng", "bb_get_terrain_rng", "bb_pair_counters", "bb_pair_env_times", "bb_check",
 ]
 
-ABI_VERSION = 18  # include/ballbot_mi355x.h BB_ABI_VERSION
+ABI_VERSION = 19  # include/ballbot_mi355x.h BB_ABI_VERSION
 
 _lib = None
 

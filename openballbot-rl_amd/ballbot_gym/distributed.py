@@ -42,8 +42,11 @@ def shard_stream_seeds(seed: int, first_env: int, count: int, per_env: bool = Tr
 
 
 def max_over_ranks(value: float, device=None) -> float:
-    """All-reduce MAX of a scalar (elapsed time); identity without a process group."""
-    if not (dist.is_available() and dist.is_initialized()) or dist.get_world_size() == 1:
+    """All-reduce MAX of a scalar (elapsed time); identity without a process group (an RCCL
+    group of one rank still runs the all-reduce: the driver's multi-GPU path, rehearsed)."""
+    if not (dist.is_available() and dist.is_initialized()):
+        return float(value)
+    if dist.get_world_size() == 1 and dist.get_backend() != "nccl":
         return float(value)
     if dist.get_backend() == "gloo":  # host tensors on gloo (rehearsals sharing one GPU)
         device = None

@@ -549,7 +549,7 @@ class BallbotVecEnv:
         """Diagnostics of the last relief-pair launch of step_multi (bb_pair_counters; waits for the device)."""
         keys = ("busy_fast", "busy_full", "idle_fast", "idle_full", "active_fast", "active_full", "claims_fast",
                 "claims_full", "steps_fast", "steps_full", "handovers", "life_cycles_fast", "life_cycles_full",
-                "life_wall_fast", "life_wall_full", "heavy")
+                "life_wall_fast", "life_wall_full", "heavy", "ring_len", "ring_pushes_min_fast", "ring_pushes_min_full")
         out = (C.c_int64 * len(keys))()
         N.check(N.lib().bb_pair_counters(self._h, out, len(keys)), "bb_pair_counters")
         return dict(zip(keys, out))

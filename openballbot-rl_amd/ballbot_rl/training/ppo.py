@@ -25,9 +25,8 @@ rollout for episode statistics and one per minibatch for the KL early stop
 (SB3's semantics need it).  Multi-GPU: each rank
 steps its own env shard; at the update boundary the rollout buffers are
 gathered to rank 0 over RCCL (gather_rollouts), rank 0 runs the update and
-broadcasts the new parameters (update_mode="gather", north_star's design).
-update_mode="allreduce" -- the default on more than one rank -- instead updates
-data-parallel: every rank takes its minibatches (batch_size / world rows each)
+broadcasts the new parameters (update_mode="gather", north_star's design and
+the default).  update_mode="allreduce" instead updates data-parallel: every rank takes its minibatches (batch_size / world rows each)
 from its own shard, the advantages are normalised over the global minibatch, the
 gradients are averaged with an RCCL all-reduce before the clip and AdamW step,
 and the KL early stop uses the ranks' mean approx_kl, so no rank waits for rank
@@ -170,12 +169,14 @@ def policy_obs(obs15: torch.Tensor, depth: Optional[torch.Tensor] = None,
     return d
 
 
-def fused_mlp_slots(ppo: "BatchedPPO", update: bool = True):
+def fused_mlp_slots(ppo: "BatchedPPO", update: bool = True, B: Optional[int] = None):
     """Flat-buffer offsets of the 21 tensors bb_ppo_mlp_step reads, or None when
     the policy/optimiser is not the reference's MLP on FlatAdamW (pi = vf =
     [128]*4 LeakyReLU(0.01) over the 15-d proprio obs, or the 56-d features of
     the camera policy with fused frozen encoders; 3-d action head);
-    update=True also needs a batch size bb_ppo_mlp_step takes.
+    update=True also needs a minibatch bb_ppo_mlp_step takes: B rows (default
+    ppo.batch_size; the data-parallel update passes its local batch_size / world),
+    a multiple of 256 in [256, 16384] -- else the autograd graph step runs.
     BB_PPO_FUSED=0 disables the fused update and rollout step (A/B runs)."""
     import os
 
@@ -186,8 +187,10 @@ def fused_mlp_slots(ppo: "BatchedPPO", update: bool = True):
     opt, pol = ppo.optimizer, ppo.policy
     if not isinstance(opt, FlatAdamW):
         return None
-    if update and (ppo.batch_size % 256 or ppo.batch_size > 16384):
-        return None
+    if update:  # the LOCAL minibatch bb_ppo_mlp_step runs: batch_size / world rows when data-parallel
+        B = int(ppo.batch_size if B is None else B)
+        if B < 256 or B % 256 or B > 16384:
+            return None
 
     ext = pol.features_extractor
     fd = ext.features_dim
@@ -278,7 +281,7 @@ class _UpdateGraphs:
         st_snap = {id(p): {k: v.clone() for k, v in opt.state[p].items()} for p in params if p in opt.state}
         b_snap = [b.detach().clone() for b in self.buffers]
 
-        slots = fused_mlp_slots(ppo)
+        slots = fused_mlp_slots(ppo, B=B)
         self.fused = slots is not None
         if self.fused:
             mb_step = self._fused_step(ppo, slots)
@@ -482,7 +485,7 @@ class _UpdateGraphs:
         _dbg("update: before replay")
         self._replay(total)
         _dbg("update: replayed")
-        if self.dp and ppo.world > 1:  # the global minibatches' terms: the ranks' mean (the KL stop reads it)
+        if self.dp and ppo._collective:  # the global minibatches' terms: the ranks' mean (the KL stop reads it)
             ppo._allreduce(self.log)
             self.log.div_(ppo.world)
         log = self.log.cpu().numpy()
@@ -595,8 +598,11 @@ class BatchedPPO:
         self.gae_fn = gae_fn
         self.rank = dist.get_rank() if dist.is_available() and dist.is_initialized() else 0
         self.world = dist.get_world_size() if dist.is_available() and dist.is_initialized() else 1
-        if update_mode is None:  # data-parallel on several ranks: no rank updates world x the samples
-            update_mode = "allreduce" if self.world > 1 else "gather"
+        # RCCL process group (backend "nccl"): the collectives run even at world size 1, so a one-GPU
+        # run executes the same captured all-reduce nodes as the multi-GPU one
+        self._rccl = bool(dist.is_available() and dist.is_initialized() and dist.get_backend() == "nccl")
+        if update_mode is None:  # north_star's design: rollouts gathered to rank 0 at the update boundary
+            update_mode = "gather"
         if update_mode not in ("gather", "allreduce"):
             raise ValueError(f"update_mode must be 'gather' or 'allreduce' (got {update_mode!r})")
         if update_mode == "allreduce" and self.world > 1 and int(batch_size) % self.world:
@@ -746,8 +752,10 @@ class BatchedPPO:
         if self._last_obs.data_ptr() != obs_io.data_ptr():
             obs_io.copy_(self._last_obs)
         noise = torch.randn(T, n, 3, generator=self.gen, device=dev)
-        ep_r = torch.empty(T, n, dtype=torch.float64, device=dev)
-        ep_l = torch.empty(T, n, dtype=torch.int64, device=dev)
+        # "no episode ended" in every row before the launch: a relief-pair rollout that ends on
+        # its budget leaves rows unwritten, and those must not read as finished episodes
+        ep_r = torch.full((T, n), float("nan"), dtype=torch.float64, device=dev)
+        ep_l = torch.zeros(T, n, dtype=torch.int64, device=dev)
         # bb_rollout reads the trunk weights input-major (W^T): a transposed copy per rollout
         flat = self.optimizer.flat
         if getattr(self, "_pol_t", None) is None or self._pol_t.numel() != flat.numel():
@@ -768,6 +776,8 @@ class BatchedPPO:
         a.buf_log_prob, a.buf_rewards, a.buf_starts = b.log_probs.data_ptr(), b.rewards.data_ptr(), b.starts.data_ptr()
         a.ep_r_out, a.ep_l_out = ep_r.data_ptr(), ep_l.data_ptr()
         env.run_rollout(a)
+        if getattr(env, "relief", False):  # the relief pair's budget fault, before GAE and the update
+            env.check()                    # read the buffer (the rollout's host sync comes next anyway)
         self._last_obs = obs_io
         return ep_r, ep_l
 
@@ -922,17 +932,22 @@ class BatchedPPO:
 
     @property
     def _dp(self) -> bool:
-        return self.update_mode == "allreduce" and (self.world > 1 or self._force_dp)
+        return self.update_mode == "allreduce" and (self._collective or self._force_dp)
+
+    @property
+    def _collective(self) -> bool:
+        """The update's collectives execute: several ranks, or an RCCL group of any size."""
+        return self.world > 1 or self._rccl
 
     def _allreduce(self, t: torch.Tensor) -> None:
         """Sum t over the ranks in place (RCCL on the GPU; captured when inside a graph); the
-        identity on one rank."""
-        if self.world > 1:
+        identity on one rank without an RCCL group."""
+        if self._collective:
             dist.all_reduce(t)
 
     def _allreduce_grads(self, params) -> None:
         """Average the parameters' gradients over the ranks: one all-reduce of the flattened set."""
-        if self.world == 1:
+        if not self._collective:
             return
         gs = [p_.grad for p_ in params if p_.grad is not None]
         fg = torch._utils._flatten_dense_tensors(gs)

@@ -28,6 +28,8 @@
 #include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
+#include <algorithm>
+#include <climits>
 #include <vector>
 
 #include "../../include/ballbot_mi355x.h"
@@ -2331,7 +2333,14 @@ int bb_create(int n_envs, int device, const bb_params* p, bb_handle** out) {
   HIPCHK(hipMalloc((void**)&d.perm, sizeof(int) * n));
   // per ring: an XCD label's envs (32-env blocks) + its resident teams, with margin (the solo ring
   // holds at most SC_SOLO envs)
-  d.ring_len = (n + 255) / 256 * 32 + WAVE / TEAM * ((h->pair_cap + NXCD - 1) / NXCD) + 64;
+  {
+    const int ring_min = (n + 255) / 256 * 32 + WAVE / TEAM * ((h->pair_cap + NXCD - 1) / NXCD) + 1;
+    d.ring_len = ring_min + 63;
+    // BB_RING_LEN (tests): a shorter ring, never below the bound above (envs + resident teams of
+    // one XCD label + 1), so that the rings wrap more laps per launch at the bound itself
+    const char* rl = getenv("BB_RING_LEN");
+    if (rl && atoi(rl) > 0) d.ring_len = atoi(rl) < ring_min ? ring_min : atoi(rl);
+  }
   HIPCHK(hipMalloc((void**)&d.ring, sizeof(unsigned long long) * NRINGS * size_t(d.ring_len)));
   HIPCHK(hipMalloc((void**)&d.rctr, sizeof(int) * 2 * NRINGS));
   HIPCHK(hipMalloc((void**)&d.pair_busy, sizeof(unsigned long long) * 6));
@@ -2687,6 +2696,14 @@ int bb_reset(bb_handle* h, const uint8_t* mask, float* obs, void* stream) {
   else
     hipLaunchKernelGGL(reset_kernel<float>, dim3(blocks), dim3(WAVE), 0, (hipStream_t)stream, h->mf, h->d, mask, obs);
   HIPCHK(hipGetLastError());
+  // A full reset clears a budget fault. reset_kernel clears the device word in stream order, but
+  // bb_step* read the host side as soon as they are called: with a fault set, wait for the reset
+  // so that reset-then-step works without a bb_check in between (no wait when no fault is set,
+  // so a captured or asynchronous full reset stays asynchronous).
+  if (!mask && *h->fault_host) {
+    HIPCHK(hipStreamSynchronize((hipStream_t)stream));
+    *h->fault_host = 0;
+  }
   return 0;
 }
 
@@ -2840,10 +2857,14 @@ int bb_pair_counters(bb_handle* h, int64_t* out, int n) {
   unsigned long long busy[6];
   HIPCHK(hipMemcpy(sc, h->d.slow_count, sizeof sc, hipMemcpyDeviceToHost));
   HIPCHK(hipMemcpy(busy, h->d.pair_busy, sizeof busy, hipMemcpyDeviceToHost));
+  int rc[2 * NRINGS];
+  HIPCHK(hipMemcpy(rc, h->d.rctr, sizeof rc, hipMemcpyDeviceToHost));
+  int push_min[2] = {INT_MAX, INT_MAX};  // appends to the least-used fast / full ring of the launch
+  for (int r = 0; r < 2 * NXCD; r++) push_min[r / NXCD] = std::min(push_min[r / NXCD], rc[2 * r + 1]);
   const int64_t v[BB_NPAIR] = {(int64_t)busy[0], (int64_t)busy[1], sc[SC_IDLE], sc[SC_IDLE + 1], sc[SC_ACTIVE],
                                sc[SC_ACTIVE + 1], sc[SC_CLAIMS], sc[SC_CLAIMS + 1], sc[SC_STEPS], sc[SC_STEPS + 1],
                                sc[SC_PARKED], (int64_t)busy[2], (int64_t)busy[3], (int64_t)busy[4],
-                               (int64_t)busy[5], sc[SC_HEAVY_LAST]};
+                               (int64_t)busy[5], sc[SC_HEAVY_LAST], h->d.ring_len, push_min[0], push_min[1]};
   for (int i = 0; i < n; i++) out[i] = v[i];
   return 0;
 }

@@ -94,9 +94,10 @@ def test_gloo_world2_ppo_update_boundary():
     assert e0 == e1 > 0                    # episode stats gathered from both ranks
 
 
-def test_gloo_world2_default_update_is_data_parallel():
-    """With more than one rank and no update_mode given, every rank updates on its own shard
-    (update_mode="allreduce"): both count the update's epochs, and the parameters stay equal."""
+def test_gloo_world2_default_update_is_gather():
+    """With more than one rank and no update_mode given, the update is north_star's gather
+    (rollouts to rank 0, one update there, parameters broadcast); the data-parallel update is
+    opt-in (update_mode="allreduce")."""
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
@@ -108,9 +109,9 @@ def test_gloo_world2_default_update_is_data_parallel():
         p.join(timeout=60)
         assert p.exitcode == 0
     (_, t0, u0, v0, e0, m0), (_, t1, u1, v1, e1, m1) = res
-    assert m0 == m1 == "allreduce"
-    assert t0 == t1 == 2 * 8 * 4 * 2 and u0 == u1 == 2
-    assert np.allclose(v0, v1, rtol=0, atol=1e-6)
+    assert m0 == m1 == "gather"
+    assert t0 == t1 == 2 * 8 * 4 * 2 and u0 == 2 and u1 == 0
+    assert (v0 == v1).all()
 
 
 def _dp_worker(rank, world, port, q, target_kl):

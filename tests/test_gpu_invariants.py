@@ -7,8 +7,9 @@ kernel to physics rather than to the oracle alone:
   and its error against a fine-step reference falls 4x per halving of h -- the
   2nd-order rotation composition MuJoCo's mj_RungeKutta has for tumbling free
   bodies (tests/test_oracle.py::test_rk4_convergence_order; 16x with RKMK);
-- angular momentum about the system COM and straight-line COM motion with
-  gravity off (BB_DSBL_GRAVITY), airborne (no contacts);
+- angular and linear momentum about the system COM and straight-line COM motion
+  with gravity off (BB_DSBL_GRAVITY), airborne (no contacts): both drift at RK4's
+  2nd-order rotation error, checked by their 4x fall per halving of dt;
 - static load: the ball alone at rest on the plane -- the kernel's forward has
   zero vertical ball acceleration there (its contact forces carry m_ball g) and
   its rest state is the oracle's, where the oracle's summed normal force is m g.
@@ -91,7 +92,7 @@ def test_gpu_angular_momentum_conserved_without_gravity(oracle):
     q0, v0 = _airborne(oracle, 6)
     P0, L0, c0 = oracle.momentum(q0, v0)
     mtot = oracle.model_info()["mass"][1:].sum()
-    drift = []
+    drift, pdrift = [], []
     for h in (0.002, 0.001):
         n = int(round(2.0 / h))
         qg, vg = _gpu_run(q0, v0, n, h=h, disable=64)  # damping on: internal torques
@@ -100,9 +101,13 @@ def test_gpu_angular_momentum_conserved_without_gravity(oracle):
             assert np.abs(qg - qo).max() < 1e-8 and np.abs(vg - vo).max() < 1e-6
         P1, L1, c1 = oracle.momentum(qg, vg)
         drift.append(np.abs(L1 - L0).max() / np.linalg.norm(L0))
-        assert np.abs(P1 - P0).max() < 1e-3 * np.linalg.norm(P0)
+        pdrift.append(np.abs(P1 - P0).max() / np.linalg.norm(P0))
         np.testing.assert_allclose(c1, c0 + P0 / mtot * 2.0, atol=1e-4)
     assert drift[0] < 5e-4 and 3.5 < drift[0] / drift[1] < 4.5, drift
+    # linear momentum: P is a nonlinear function of the orientations (COM offsets), so RK4 in
+    # MuJoCo's coordinates conserves it only up to the same 2nd-order rotation composition:
+    # the oracle gives 4.46e-4, 1.11e-4, 2.79e-5, 6.97e-6 at 4, 2, 1, 0.5 ms (4.00x per halving)
+    assert pdrift[0] < 2e-4 and 3.5 < pdrift[0] / pdrift[1] < 4.5, pdrift
     # the switch acts on the kernel: with gravity on, the ball falls g t^2 / 2 further in 0.2 s
     qa, _ = _gpu_run(q0, v0, 100)
     qb, _ = _gpu_run(q0, v0, 100, disable=64)

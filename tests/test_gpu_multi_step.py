@@ -214,9 +214,8 @@ def test_relief_pair_budget_expiry_is_loud(monkeypatch):
         env.step(acts[0])
     with pytest.raises(RuntimeError, match="wall-clock budget"):
         env.step_multi(acts)
-    env.reset()  # a full reset gives every env a valid state: the fault clears on the device
-    env.check()
-    env.step(acts[0])
+    env.reset()  # a full reset gives every env a valid state: bb_reset waits for it and clears the fault
+    env.step(acts[0])  # straight after the reset, no check() in between
     env.check()
     env.close()
 

@@ -3,13 +3,14 @@
 Teacher-forced: every env starts each step from the oracle's state, so the
 comparison measures one mj_step + glue, not chaotic drift.
 
-fp64 kernel (the default): qpos 1e-9, qvel 1e-6, obs 1e-6, reward 1e-7 for at least
-99.9% of env-steps, and every env-step within qvel 1e-4.  The oracle restates MuJoCo's
-solver (PrimalSearch line search, improvement-or-gradient stop at 1e-8); the kernel keeps
-its own line search.  Where the two searches end an iteration at different points, the
-improvement test can stop one Newton iteration apart: tools/solver_parity.py (host build
-of the kernel templates) finds that in 1 of 81,920 teacher-forced env-steps, at qvel
-1.0e-5 / qpos 5e-9 (profiles/r05_solver_parity.json).
+fp64 kernel (the default): qpos 1e-9, qvel 1e-6, obs 1e-6, reward 1e-7 for every
+env-step but at most ONE per test, and every env-step within qvel 2e-5.  The oracle
+restates MuJoCo's solver (PrimalSearch line search, improvement-or-gradient stop at 1e-8);
+the kernel keeps its own line search.  Where the two searches end an iteration at
+different points, the improvement test can stop one Newton iteration apart:
+tools/solver_parity.py (host build of the kernel templates) finds that in 1 of 81,920
+teacher-forced env-steps, at qvel 1.0e-5 / qpos 5e-9 (profiles/r05_solver_parity.json).
+Each test prints its worst errors and outlier count (DESIGN §4 keeps the measured ones).
 
 fp32 kernel: qpos 1e-5, qvel 1e-3, obs 1e-4, reward 1e-6 for
 at least 99.9% of env-steps; the rest must stay below qvel 1e-2.  Residual
@@ -24,7 +25,7 @@ torch = pytest.importorskip("torch")
 pytestmark = pytest.mark.gpu
 
 TOL = {"fp32": dict(q=1e-5, v=1e-3, obs=1e-4, r=1e-6, frac=0.999, vmax=1e-2),
-       "fp64": dict(q=1e-9, v=1e-6, obs=1e-6, r=1e-7, frac=0.999, vmax=1e-4)}
+       "fp64": dict(q=1e-9, v=1e-6, obs=1e-6, r=1e-7, max_bad=1, vmax=2e-5)}
 
 
 @pytest.fixture(scope="module")
@@ -74,8 +75,12 @@ def _teacher_forced(env, rec, tol):
         gflags = info["done_flags"].cpu().numpy() & 3
         mism = np.nonzero((gflags != (rec["flags"][t] & 3)) & ok)[0]
         assert len(mism) == 0, f"step {t}: termination flags differ for envs {mism}"
-    frac = 1.0 - bad / total
-    assert frac >= tol["frac"], f"only {frac:.4%} of env-steps within tolerance ({worst})"
+    print(f"\nteacher-forced: {total} env-steps, {bad} outside tolerance, worst {worst}")
+    if "max_bad" in tol:
+        assert bad <= tol["max_bad"], f"{bad} of {total} env-steps outside tolerance ({worst})"
+    else:
+        frac = 1.0 - bad / total
+        assert frac >= tol["frac"], f"only {frac:.4%} of env-steps within tolerance ({worst})"
     return worst
 
 

@@ -1,0 +1,112 @@
+"""The relief pair (bb_step_multi on relief banks) on its own terms.
+
+1. Teacher-forced parity of the pair ITSELF against the fp64 oracle on 256 perlin
+   envs, each on its own terrain draws: every step is one bb_step_multi launch of
+   the pair from the GPU's own pre-step state, and the oracle takes the same step
+   from the same state on the env's terrain (BallbotVecEnv.hfield of its bank
+   slot).  The tolerance is test_gpu_parity's fp64 one: qpos 1e-9, qvel 1e-6, obs
+   1e-6, reward 1e-7 for all env-steps but at most one, qvel <= 2e-5 everywhere.
+   Reference: ballbot_gym/envs/ballbot_env.py:854-1036 (the step), :912 (mj_step),
+   ballbot_gym/terrain/perlin.py:8-74 (the terrain).
+2. Ring reuse across laps: the ticket rings at their minimum length (BB_RING_LEN
+   clamps to envs + resident teams of one XCD label + 1) with one step per hold
+   (BB_PAIR_SEG=1: an append per env-step) wrap many laps per launch; bit-exact
+   against one bb_step per step.
+"""
+import numpy as np
+import pytest
+
+torch = pytest.importorskip("torch")
+pytestmark = pytest.mark.gpu
+
+TOL = dict(q=1e-9, v=1e-6, obs=1e-6, r=1e-7, max_bad=1, vmax=2e-5)
+
+
+def test_relief_pair_teacher_forced_vs_oracle(oracle, monkeypatch):
+    monkeypatch.setenv("BB_ROUTE", "0")  # read by bb_create: relief banks always take the pair
+    from ballbot_gym.envs import BallbotVecEnv
+
+    n = 256
+    env = BallbotVecEnv(n, device="cuda:0", seed=3, terrain_config={"type": "perlin", "config": {}},
+                        n_terrains=None, stream_seeds=[300 + i for i in range(n)])
+    size_z = float(env.terrain_plan.size_z)
+    g = torch.Generator(device="cuda:0").manual_seed(11)
+    # burn-in through the pair: the robots drop onto their terrains, balance, fall, topple
+    for _ in range(5):
+        env.step_multi(torch.rand(32, n, 3, generator=g, device="cuda:0") * 2 - 1)
+    cfg = oracle.default_cfg()
+    fields = {}
+    bad = total = full_steps = 0
+    worst = dict(q=0.0, v=0.0, obs=0.0, r=0.0)
+    s0 = env.stats()
+    for t in range(48):
+        q, v, w, sc = env.get_state()
+        slots, _ = env.env_terrain()
+        acts = torch.rand(1, n, 3, generator=g, device="cuda:0") * 2 - 1
+        out = env.step_multi(acts)  # ONE pair launch of one step
+        q1, v1, _, _ = env.get_state()
+        pc = env.pair_counters()
+        full_steps += pc["steps_full"]
+        a_h = acts[0].cpu().numpy()
+        obs, rew, fl = out["obs"][0].cpu().numpy(), out["reward"][0].cpu().numpy(), out["done"][0].cpu().numpy()
+        tobs = out["terminal_obs"][0].cpu().numpy()
+        for e in range(n):
+            sl = int(slots[e])
+            if sl not in fields:
+                fields[sl] = env.hfield(sl)
+            qe, ve, we, se = q[e].copy(), v[e].copy(), w[e].copy(), np.array([sc[e]], np.int32)
+            o, r, f, _, _ = oracle.env_step(cfg, qe, ve, we, se, a_h[e], fields[sl], size_z)
+            assert (int(fl[e]) & 3) == (int(f) & 3), (t, e, int(fl[e]), int(f))
+            if f & 1:  # terminated: the GPU auto-reset it (terminal obs carries the step's obs)
+                eo = float(np.abs(tobs[e] - o).max())
+                worst["obs"] = max(worst["obs"], eo)
+                continue
+            eq, ev = float(np.abs(q1[e] - qe).max()), float(np.abs(v1[e] - ve).max())
+            eo, er = float(np.abs(obs[e] - o).max()), abs(float(rew[e]) - r)
+            total += 1
+            bad += not (eq <= TOL["q"] and ev <= TOL["v"] and eo <= TOL["obs"] and er <= TOL["r"])
+            for k, x in (("q", eq), ("v", ev), ("obs", eo), ("r", er)):
+                worst[k] = max(worst[k], x)
+            assert ev <= TOL["vmax"], (t, e, ev)
+    st = env.stats()
+    env.check()
+    env.close()
+    print(f"\nrelief pair teacher-forced: {total} env-steps on {len(fields)} perlin terrains, {bad} outside "
+          f"tolerance, worst {worst}, full-loop steps {full_steps}, slow path {st['slow_path'] - s0['slow_path']}")
+    assert bad <= TOL["max_bad"], (bad, total, worst)
+    assert total >= 48 * n // 2 and len(fields) >= n // 2
+    assert full_steps > 0 and st["slow_path"] > s0["slow_path"]  # the pair's full loop stepped envs
+    assert st["pair_budget"] == 0
+
+
+def test_relief_pair_rings_wrap_laps_at_minimum_length(monkeypatch):
+    """BB_RING_LEN=1 (clamped to the minimum), BB_PAIR_SEG=1: every ring wraps laps within each
+    launch; all outputs, states, counters and terrain draws equal one bb_step per step."""
+    from test_gpu_multi_step import _chunked_equal, _pair
+
+    monkeypatch.setenv("BB_RING_LEN", "1")
+    monkeypatch.setenv("BB_PAIR_SEG", "1")
+    n = 512
+    a, b = _pair(n, "perlin", monkeypatch, route="0", n_terrains=None, stream_seeds=[700 + i for i in range(n)])
+    g = torch.Generator(device="cuda:0").manual_seed(9)
+    pool = torch.rand(512, n, 3, generator=g, device="cuda:0") * 2 - 1
+    laps = []
+    for k in (512, 512):
+        _chunked_equal(a, b, pool, [k])
+        pc = b.pair_counters()
+        laps.append((pc["ring_len"], pc["ring_pushes_min_fast"] / pc["ring_len"],
+                     pc["ring_pushes_min_full"] / pc["ring_len"]))
+    for x, y in zip(a.get_state(), b.get_state()):
+        np.testing.assert_array_equal(x, y)
+    for x, y in zip(a.terrain_rng(), b.terrain_rng()):
+        assert (x is None and y is None) or np.array_equal(x, y)
+    sa, sb = a.stats(), b.stats()
+    assert sa == sb, (sa, sb)
+    b.check()
+    print(f"\nring length, laps of the least-used fast / full ring per launch: {laps}")
+    ring_len = laps[0][0]
+    # the minimum: 512 envs -> 64 per label, + 4 teams x the resident workgroups of one label + 1
+    assert ring_len < 64 + 4 * 128 + 64
+    assert all(f >= 3.0 for _, f, _ in laps), laps
+    assert all(u >= 3.0 for _, _, u in laps), laps
+    a.close(), b.close()
