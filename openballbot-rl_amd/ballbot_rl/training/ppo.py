@@ -313,6 +313,20 @@ class _UpdateGraphs:
         self._restore(opt, [p_snap, {i: st_snap.get(id(p)) for i, p in enumerate(params)}, b_snap])
         _dbg(f"update graphs built (fused={self.fused}, epoch graph={self.graph_epoch is not None})")
 
+    def prime(self, ppo: "BatchedPPO") -> None:
+        """Replay each captured graph once on the static zero data and restore the parameters,
+        AdamW state and BatchNorm statistics: a graph's first replay uploads it (~50 ms for the
+        update's graphs), which would otherwise land in the first update of learn()."""
+        opt = ppo.optimizer
+        snap = self._snapshot(opt)
+        for g in (self.graph, self.graph_epoch):
+            if g is not None:
+                self.k.zero_(); self.row.zero_()
+                g.replay()
+        torch.cuda.synchronize(ppo.device)
+        self._restore(opt, snap)
+        self.k.zero_(); self.row.zero_(); self.log.zero_()
+
     def _fused_step(self, ppo: "BatchedPPO", slots):
         """bb_ppo_mlp_step: the whole minibatch (forward, loss, backward, clip,
         AdamW) in five HIP launches; it advances k and row itself."""
@@ -1091,6 +1105,47 @@ class BatchedPPO:
         L.record("train/n_updates", self._n_updates)
         L.record("train/clip_range", clip)
         L.record("train/learning_rate", lr)
+
+    def warm_up(self) -> "BatchedPPO":
+        """Build, before learn(), what its first iteration would otherwise build inside the run:
+        the update graphs of this trainer's update shape (_UpdateGraphs: two warm-up minibatches,
+        the captures and one replay of each graph on static zero data, after which the
+        parameters, AdamW state and BatchNorm statistics are restored; the first BLAS call of the
+        bootstrap value; the first device randperm and reductions of the update, on a throwaway
+        generator).  The training trajectory is unchanged
+        (tests/test_gpu_ppo.py::test_warm_up_keeps_the_trajectory).  SB3 builds its model in the
+        constructor (_setup_model); this is the same kind of setup, kept out of the constructor so
+        that a trainer that never learns does not pay for it."""
+        if self.device.type != "cuda" or not self.use_graphs:
+            return self
+        n_local = self.n_envs * self.n_steps
+        was_training = self.policy.training
+        self.policy.train()  # _update captures in train mode (BatchNorm of the camera encoders)
+        g = None
+        if self._dp:
+            if self.world == 1 or dist.get_backend() == "nccl":
+                g = self._graphs_for(n_local, self.batch_size // self.world)
+        elif self.rank == 0:
+            g = self._graphs_for(n_local * self.world)
+        if g is not None:
+            g.prime(self)
+        # the rollout's bootstrap value is a torch forward: its first GEMM initialises the BLAS
+        # library (~0.2 s), so run one here
+        self.policy.eval()
+        with torch.no_grad():
+            o = torch.zeros(self.n_envs, 15, device=self.device)
+            self.policy.predict_values(policy_obs(o, self.env.depth, self.env.rel_ts) if self.cameras else o)
+            # the update's first calls of torch kernels outside the graphs: the minibatch shuffle
+            # (a device randperm of the update's rows: a sort) and explained_variance's reductions,
+            # on a throwaway generator so that shuffle_gen's stream is untouched
+            n_upd = n_local if self._dp else n_local * self.world
+            torch.randperm(n_upd, generator=torch.Generator(device=self.device).manual_seed(0), device=self.device)
+            explained_variance(torch.zeros(n_upd, device=self.device),
+                               torch.arange(n_upd, dtype=torch.float32, device=self.device))
+            float(torch.exp(self.policy.log_std.detach()).mean())  # train/std's elementwise kernels
+        self.policy.train(was_training)
+        torch.cuda.synchronize(self.device)
+        return self
 
     # ------------------------------------------------------------------ learn
     def learn(self, total_timesteps: int, callback: Optional[Callable[["BatchedPPO"], bool]] = None,

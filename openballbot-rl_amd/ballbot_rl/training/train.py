@@ -136,6 +136,7 @@ def main(config: Dict[str, Any], seed: int, out: Optional[str] = None, total_tim
                        **ppo_kwargs(config))
     if config.get("resume"):
         model.load_policy(config["resume"])
+    model.warm_up()  # the update graphs and first library calls, before the run (SB3's _setup_model)
     eval_freq = int(eval_cfg.get("freq", 5000))
     on_rollout = None
     if rank == 0 and eval_env is not None:

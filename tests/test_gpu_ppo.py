@@ -772,3 +772,32 @@ def test_data_parallel_update_graph_on_one_rank(fused, monkeypatch):
         for a, b in zip(models[0].policy.parameters(), ref.policy.parameters()):
             diff = (a - b).abs()
             assert float((diff > 1e-5).float().mean()) < 1e-2, float(diff.max())
+
+
+@pytest.mark.parametrize("terrain", ["flat", "perlin"])
+def test_warm_up_keeps_the_trajectory(terrain):
+    """BatchedPPO.warm_up (update graphs captured and primed on zero data, BLAS initialised) before
+    learn() leaves the training trajectory as it was: the same parameters and logs after three
+    iterations as a trainer that builds its graphs inside its first update."""
+    from ballbot_gym.envs import BallbotVecEnv
+    from ballbot_rl.training.logger import CSVLogger
+    from ballbot_rl.training.ppo import BatchedPPO
+
+    kw = {} if terrain == "flat" else {"n_terrains": None}
+    res = []
+    for warm in (False, True):
+        env = BallbotVecEnv(512, device="cuda:0", seed=21, terrain_config={"type": terrain, "config": {}}, **kw)
+        m = BatchedPPO(env, n_steps=16, batch_size=2048, n_epochs=2, ent_coef=0.001, clip_range=0.015, vf_coef=2.0,
+                       target_kl=0.3, seed=6, logger=CSVLogger(None, stdout=False))
+        if warm:
+            m.warm_up()
+            assert m._graphs is not None and m._graphs.fused
+        m.learn(total_timesteps=512 * 16 * 3)
+        vec = torch.nn.utils.parameters_to_vector(m.policy.parameters()).detach().cpu().numpy()
+        res.append((vec, dict(m.logger.values), m._n_updates, len(m.ep_info_buffer)))
+        env.close()
+    (v0, l0, u0, e0), (v1, l1, u1, e1) = res
+    assert u0 == u1 == 6 and e0 == e1
+    np.testing.assert_allclose(v0, v1, rtol=0, atol=1e-6)
+    for k in ("train/value_loss", "train/policy_gradient_loss", "train/approx_kl"):
+        assert l0[k] == pytest.approx(l1[k], rel=1e-5, abs=1e-8), k

@@ -91,6 +91,9 @@ def main():
         torch.cuda.synchronize(); t = time.perf_counter()
         orig_train(); torch.cuda.synchronize(); upd_times.append(time.perf_counter() - t); t_upd += upd_times[-1]
 
+    t_setup = time.perf_counter()
+    m.warm_up()  # graphs captured and primed, BLAS initialised: setup, reported apart from the run
+    setup_s = time.perf_counter() - t_setup
     m.collect_rollouts, m.train = collect, train
     iters = [0]
 
@@ -121,7 +124,8 @@ def main():
     el = time.perf_counter() - t0
     out = {"metric": "PPO env-steps/sec (rollout + GAE + update)", "value": m.num_timesteps / el,
            "unit": "env-steps/s", "timesteps": m.num_timesteps, "iterations": iters[0], "wall_s": el,
-           "rollout_s": t_roll, "update_s": t_upd, "eval_s": t_eval[0],
+           "rollout_s": t_roll, "update_s": t_upd, "eval_s": t_eval[0], "setup_s": setup_s,
+           "value_including_setup": m.num_timesteps / (el + setup_s),
            "rollout_env_steps_per_s": m.num_timesteps / max(t_roll, 1e-9),
            "rollout_times_s": [round(x, 4) for x in roll_times], "update_times_s": [round(x, 4) for x in upd_times],
            "kl_stops": getattr(m, "kl_stops", None),
