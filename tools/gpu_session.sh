@@ -15,6 +15,8 @@
 #                    own command, summarised into profiles/${TAG}_* by tools/prof_summary.py, with
 #                    profiles/traffic.json updated for the bench line's roofline.traffic.
 #   prof_driver      the same for the driver's 20-step flat launch (its own traffic entry).
+#   ppo_flat ppo_perlin
+#                    tools/bench_ppo.py: PPO end to end, flat 10M and perlin 5M steps (4096 x 64).
 # Run the prof_* steps BEFORE the bench steps: a line reads the traffic entry of its own shape.
 # Output: gpurun_out/$TAG/ (bench lines as <step>.json, logs as <step>.log).
 set -o pipefail
@@ -63,6 +65,10 @@ for s in $STEPS; do
       prof prof_perlin pair BB_PAIR_BUDGET_MS=3000 NAME=perlin ARGS="--terrain perlin"
       python tools/prof_summary.py gpurun_out/prof_${TAG}_perlin profiles/${TAG}_perlin_pair --kernel pair --f64 --traffic > $O/sum_perlin.log 2>&1 || { tail $O/sum_perlin.log; exit 1; }
       tail -3 $O/sum_perlin.log ;;
+    ppo_flat)   timeout -k 10 240 python -u tools/bench_ppo.py --timesteps 10e6 --out $O/ppo_flat > $O/ppo_flat.json 2> $O/ppo_flat.log || { tail -20 $O/ppo_flat.log; exit 1; }
+                python -c "import json;d=json.load(open('$O/ppo_flat.json'));print('ppo_flat', round(d['value']/1e6,3), 'M end to end, setup', round(d['setup_s'],3), 's')" ;;
+    ppo_perlin) timeout -k 10 240 python -u tools/bench_ppo.py --timesteps 5e6 --terrain perlin --out $O/ppo_perlin > $O/ppo_perlin.json 2> $O/ppo_perlin.log || { tail -20 $O/ppo_perlin.log; exit 1; }
+                python -c "import json;d=json.load(open('$O/ppo_perlin.json'));print('ppo_perlin', round(d['value']/1e6,3), 'M end to end, setup', round(d['setup_s'],3), 's')" ;;
     *) echo "unknown step $s"; exit 2 ;;
   esac
 done
