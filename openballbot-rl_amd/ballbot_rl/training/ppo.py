@@ -298,15 +298,20 @@ class _UpdateGraphs:
         for p in params:  # backward allocates the grads inside the graph pool (static addresses)
             p.grad = None
         self.k.zero_(); self.row.zero_()
+        # thread-local capture: with RCCL collectives in the graph, the process group's watchdog
+        # thread polls the events of the warm-up's (eager) collectives while this thread captures;
+        # under the default global mode that poll invalidates the capture (hipErrorStreamCapture-
+        # Invalidated, seen on one GPU with an RCCL group in round 6, tests/test_gpu_rccl.py)
+        mode = "thread_local"
         self.graph = torch.cuda.CUDAGraph()
-        with torch.cuda.graph(self.graph):
+        with torch.cuda.graph(self.graph, capture_error_mode=mode):
             mb_step()
         # the fused proprio minibatch advances its own device counters, so a whole epoch
         # (nb minibatches) is one graph as well: one host launch per epoch instead of nb
         self.graph_epoch = None
         if self.fused and "depth" not in self.data and self.nb > 1:
             self.graph_epoch = torch.cuda.CUDAGraph()
-            with torch.cuda.graph(self.graph_epoch):
+            with torch.cuda.graph(self.graph_epoch, capture_error_mode=mode):
                 for _ in range(self.nb):
                     mb_step()
         torch.cuda.synchronize(dev)

@@ -127,7 +127,9 @@ def test_rollout_steps_replay_bit_exact(terrain, route, park, pair, n_envs, prec
 def test_pair_rollout_budget_expiry_is_loud(monkeypatch):
     """The relief pair's rollout form ends on its wall-clock budget loudly, as bb_step_multi's does
     (test_gpu_multi_step.py): with BB_PAIR_BUDGET_MS=1 most of the 8x surplus teams wait out the
-    budget, check() raises, the next rollout refuses, and a full reset() clears the fault."""
+    budget: the rollout itself raises (on relief banks _collect_rollout_kernel checks the fault
+    before GAE and the update can read the buffer), check() raises, the next rollout
+    refuses, and a full reset() clears the fault."""
     monkeypatch.setenv("BB_PAIR_BUDGET_MS", "1")  # read by bb_create
     monkeypatch.setenv("BB_ROUTE", "0")
     monkeypatch.setenv("BB_RELIEF_PAIR", "1")
@@ -136,7 +138,8 @@ def test_pair_rollout_budget_expiry_is_loud(monkeypatch):
     m, slots = _ppo(env, 32)
     m._last_obs = env.obs
     m._last_starts.fill_(1)
-    m._collect_rollout_kernel(slots)  # asynchronous: no error yet
+    with pytest.raises(RuntimeError, match="wall-clock budget"):
+        m._collect_rollout_kernel(slots)  # the rollout's own check
     with pytest.raises(RuntimeError, match="wall-clock budget"):
         env.check()
     assert env.stats()["pair_budget"] >= 1
