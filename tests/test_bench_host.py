@@ -50,3 +50,21 @@ def test_launch_chunks_driver_window_is_one_launch():
     # the driver's --steps 20 --warmup 5: one 20-step launch
     assert bench.launch_chunks(20, 256, 256) == [20]
     assert bench.launch_chunks(500, 256, 256) == [256, 244]
+
+
+def test_committed_flops_and_profiles_name_their_basis():
+    """Lines without the CPU leg (N > 1 ranks, --no-cpu-baseline) take the committed FLOP count of
+    their terrain, on the same yardstick as the live count (bench.FLOP_BASIS); the same-shape
+    profiles that roofline.traffic / frac_executed read exist for the driver's and the bench's
+    flat launches and the perlin pair."""
+    import json
+
+    for t in ("flat", "perlin"):
+        fl = bench.committed_flops(t)
+        assert fl and fl["flops_per_env_step"] > 0 and fl["basis"] == bench.FLOP_BASIS
+    tab = bench.ROOT / "profiles" / "traffic.json"
+    for shape in (("flat", 20.0), ("flat", 500.0), ("perlin", 500.0)):
+        e = bench.profile_entry(tab, "fp64", shape[0], 4096, shape[1])
+        assert e.get("fp64_flop_active_lanes_per_launch", 0) > 0 and e.get("bytes_per_launch", 0) > 0, shape
+        assert (bench.ROOT / e["source"]).exists(), e["source"]
+    assert json.loads((bench.ROOT / "profiles" / "flops.json").read_text())
