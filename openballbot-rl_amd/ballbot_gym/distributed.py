@@ -61,6 +61,13 @@ def gather_rollouts(buf: torch.Tensor, dst: int = 0):
     if not (dist.is_available() and dist.is_initialized()) or dist.get_world_size() == 1:
         return buf
     world = dist.get_world_size()
-    parts = [torch.empty_like(buf) for _ in range(world)] if dist.get_rank() == dst else None
-    dist.gather(buf.contiguous(), parts, dst=dst)
-    return torch.cat(parts, dim=1) if parts is not None else None
+    # gloo gathers host tensors only: device buffers (ranks sharing a GPU over gloo, the one-GPU
+    # rehearsal of the RCCL path) go through host memory; RCCL gathers them in place
+    host = dist.get_backend() == "gloo" and buf.device.type != "cpu"
+    src = buf.detach().cpu() if host else buf.contiguous()
+    parts = [torch.empty_like(src) for _ in range(world)] if dist.get_rank() == dst else None
+    dist.gather(src.contiguous(), parts, dst=dst)
+    if parts is None:
+        return None
+    out = torch.cat(parts, dim=1)
+    return out.to(buf.device) if host else out

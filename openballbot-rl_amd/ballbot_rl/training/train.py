@@ -87,11 +87,19 @@ def main(config: Dict[str, Any], seed: int, out: Optional[str] = None, total_tim
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    # BB_TRAIN_BACKEND=gloo: ranks sharing the box's GPUs over gloo (a one-GPU rehearsal of the
+    # multi-GPU run, as bench.py's BB_BENCH_BACKEND); the multi-GPU default is RCCL ("nccl"), one
+    # GPU per rank
+    backend = os.environ.get("BB_TRAIN_BACKEND", "nccl")
+    gpu = local if backend == "nccl" else local % max(torch.cuda.device_count(), 1)
     if world > 1 and not dist.is_initialized():
         os.environ.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
-        torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
-    dev = torch.device("cuda", local)
+        torch.cuda.set_device(gpu)
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device("cuda", gpu))
+        else:
+            dist.init_process_group(backend)
+    dev = torch.device("cuda", gpu)
     n_total = int(config["num_envs"])
     first, n_local = env_shard(n_total, rank, world)
     # training env g draws its terrains from np_random(seed + g): PPO(seed=seed) seeds the
@@ -163,8 +171,8 @@ def cli_main() -> None:
     ap.add_argument("--out", default=None)
     ap.add_argument("--precision", default="fp64", choices=["fp32", "fp64"])
     ap.add_argument("--update-mode", default=None, choices=["gather", "allreduce"],
-                    help="multi-GPU PPO update: data-parallel all-reduce (the default on > 1 rank) or gather the "
-                         "rollouts to rank 0 (north_star)")
+                    help="multi-GPU PPO update: gather the rollouts to rank 0 (north_star; the default) or the "
+                         "data-parallel all-reduce")
     args = ap.parse_args()
     cfg = load_training_config(str(Path(args.config).resolve()))
     seed = int(cfg.get("seed", 0))

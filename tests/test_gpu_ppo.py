@@ -693,7 +693,7 @@ def test_update_graph_build_keeps_encoder_statistics(monkeypatch):
     env.close()
 
 
-def _dp_gpu_worker(rank, world, port, q):
+def _dp_gpu_worker(rank, world, port, q, mode="allreduce"):
     import os
 
     import torch.distributed as dist
@@ -706,11 +706,12 @@ def _dp_gpu_worker(rank, world, port, q):
 
     torch.manual_seed(10 + rank)
     env = BallbotVecEnv(256, device="cuda:0", seed=3 + rank, max_ep_steps=40)
-    m = BatchedPPO(env, n_steps=16, batch_size=1024, n_epochs=2, seed=5, update_mode="allreduce",
+    m = BatchedPPO(env, n_steps=16, batch_size=1024, n_epochs=2, seed=5, update_mode=mode,
                    logger=CSVLogger(None, stdout=False))
+    m.warm_up()
     m.learn(total_timesteps=256 * 16 * world * 2)
     vec = torch.nn.utils.parameters_to_vector(m.policy.parameters()).detach().cpu()
-    q.put((rank, vec.numpy(), m._n_updates, float(m.logger.values["train/value_loss"])))
+    q.put((rank, vec.numpy(), m._n_updates, float(m.logger.values.get("train/value_loss", float("nan")))))
     env.close()
     dist.destroy_process_group()
 
@@ -736,6 +737,31 @@ def test_data_parallel_update_on_gpu_ranks():
         assert p.exitcode == 0
     (_, v0, u0, l0), (_, v1, u1, l1) = res
     assert (v0 == v1).all() and u0 == u1 == 4 and l0 == l1 and np.isfinite(l0)
+
+
+def test_gather_update_on_gpu_ranks():
+    """The multi-rank default, update_mode="gather", with the GPU env on two ranks sharing the GPU
+    over gloo: the rollouts (device buffers; gloo gathers them through host memory) reach rank 0,
+    which updates and broadcasts -- both ranks end with the same parameters, rank 0 counts the
+    epochs.  warm_up() builds rank 0's update graphs for the gathered size before learn()."""
+    import socket
+
+    import torch.multiprocessing as mp
+
+    with socket.socket() as s_:
+        s_.bind(("127.0.0.1", 0))
+        port = s_.getsockname()[1]
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    procs = [ctx.Process(target=_dp_gpu_worker, args=(r, 2, port, q, "gather")) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = sorted([q.get(timeout=240) for _ in range(2)], key=lambda x: x[0])
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    (_, v0, u0, l0), (_, v1, u1, l1) = res
+    assert (v0 == v1).all() and u0 == 4 and u1 == 0 and np.isfinite(l0)
 
 
 @pytest.mark.parametrize("fused", ["1", "0"])
