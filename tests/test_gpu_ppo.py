@@ -800,29 +800,38 @@ def test_data_parallel_update_graph_on_one_rank(fused, monkeypatch):
             assert float((diff > 1e-5).float().mean()) < 1e-2, float(diff.max())
 
 
-@pytest.mark.parametrize("terrain", ["flat", "perlin"])
+@pytest.mark.parametrize("terrain", ["flat", "perlin", "cameras"])
 def test_warm_up_keeps_the_trajectory(terrain):
     """BatchedPPO.warm_up (update graphs captured and primed on zero data, BLAS initialised) before
     learn() leaves the training trajectory as it was: the same parameters and logs after three
     iterations as a trainer that builds its graphs inside its first update."""
+    import copy
+
     from ballbot_gym.envs import BallbotVecEnv
     from ballbot_rl.training.logger import CSVLogger
     from ballbot_rl.training.ppo import BatchedPPO
 
-    kw = {} if terrain == "flat" else {"n_terrains": None}
+    cams = terrain == "cameras"  # the camera policy with a frozen encoder: BatchNorm statistics restored too
+    kw = {"n_terrains": None} if terrain == "perlin" else {}
+    enc = _random_frozen_encoder(7) if cams else None  # ONE encoder (its conv weights come from torch's RNG)
     res = []
     for warm in (False, True):
-        env = BallbotVecEnv(512, device="cuda:0", seed=21, terrain_config={"type": terrain, "config": {}}, **kw)
+        env = BallbotVecEnv(512, device="cuda:0", seed=21, disable_cameras=not cams,
+                            terrain_config={"type": "flat" if cams else terrain, "config": {}}, **kw)
+        extra = {"frozen_encoder": copy.deepcopy(enc)} if cams else {}
         m = BatchedPPO(env, n_steps=16, batch_size=2048, n_epochs=2, ent_coef=0.001, clip_range=0.015, vf_coef=2.0,
-                       target_kl=0.3, seed=6, logger=CSVLogger(None, stdout=False))
+                       target_kl=0.3, seed=6, logger=CSVLogger(None, stdout=False), **extra)
         if warm:
             m.warm_up()
             assert m._graphs is not None and m._graphs.fused
         m.learn(total_timesteps=512 * 16 * 3)
         vec = torch.nn.utils.parameters_to_vector(m.policy.parameters()).detach().cpu().numpy()
-        res.append((vec, dict(m.logger.values), m._n_updates, len(m.ep_info_buffer)))
+        bufs = [b.detach().cpu().numpy().astype(np.float64).ravel() for b in m.policy.buffers()]
+        res.append((vec, dict(m.logger.values), m._n_updates, len(m.ep_info_buffer), bufs))
         env.close()
-    (v0, l0, u0, e0), (v1, l1, u1, e1) = res
+    (v0, l0, u0, e0, b0), (v1, l1, u1, e1, b1) = res
+    for x, y in zip(b0, b1):  # BatchNorm running statistics of the frozen encoders (cameras)
+        np.testing.assert_allclose(x, y, rtol=0, atol=1e-6)
     assert u0 == u1 == 6 and e0 == e1
     np.testing.assert_allclose(v0, v1, rtol=0, atol=1e-6)
     for k in ("train/value_loss", "train/policy_gradient_loss", "train/approx_kl"):
