@@ -391,6 +391,8 @@ def main() -> None:
         pair["env_finish_ms_before_last"] = {q: float(np.percentile(f, p)) for q, p in (("p0", 0), ("p10", 10),
                                                                                        ("p50", 50), ("p90", 90))}
         pair["corr_cycles_finish"] = float(np.corrcoef(c, f)[0, 1])
+        # the launch is its slowest env's chain: how far the slowest env is from the median one
+        pair["chain_p100_over_p50"] = pair["env_mcycles"]["p100"] / max(pair["env_mcycles"]["p50"], 1e-9)
     per_step = None
     if M and not args.no_per_step:  # the same steps with one bb_step launch per step (what a closed-loop rollout uses)
         run(args.warmup, 0)
@@ -478,6 +480,12 @@ def main() -> None:
                     "algorithmic_bytes_per_env_step": algorithmic_bytes(args.precision, spl, env.relief),
                     "traffic_bytes_per_env_step": (prof["bytes_per_launch"] / envs_dom
                                                    if prof.get("bytes_per_launch") else None),
+                    # HBM writes per env-step (same-shape profile) against the 133 B of outputs the
+                    # step stores (obs 60, reward 4, done 1, terminal obs 60, pos2d 8)
+                    "write_bytes_per_env_step": (prof["write_bytes_per_launch"] / envs_dom
+                                                 if prof.get("write_bytes_per_launch") else None),
+                    "write_over_outputs": (prof["write_bytes_per_launch"] / envs_dom / 133.0
+                                           if prof.get("write_bytes_per_launch") else None),
                     "note": "algorithmic I/O: state once per launch of the line's steps, action and all five "
                             "outputs every step" + (", 7x7 hfield vertices per step" if env.relief else "")},
         }
