@@ -22,13 +22,27 @@ pytestmark = pytest.mark.gpu
 TOL = dict(q=1e-9, v=1e-6, obs=1e-6, r=1e-7, max_bad=1, vmax=2e-5)
 
 
-def test_relief_pair_teacher_forced_vs_oracle(oracle, monkeypatch):
+# fp32: test_gpu_parity's fraction bound (qpos 1e-5 / qvel 1e-3 on >= 99.9% of env-steps) and no
+# outlier bound: on perlin's contact states 11 of 12,221 teacher-forced env-steps are off by up to
+# qvel 0.8 / qpos 5e-4 (round 6), where a wheel's drive-direction row makes the Newton Hessian
+# ~1e10-ill-conditioned for float; fp64, the default, holds qvel 2e-5 everywhere
+TOL32 = dict(q=1e-5, v=1e-3, obs=1e-4, r=1e-6, frac=0.999, vmax=None)
+
+
+@pytest.mark.parametrize("terrain,precision", [("perlin", "fp64"), ("hills", "fp64"), ("perlin", "fp32")])
+def test_relief_pair_teacher_forced_vs_oracle(oracle, terrain, precision, monkeypatch):
+    """perlin: per-env generators over the whole seed bank; hills: one shared generator over an
+    8-draw bank (the numpy generator on the host); fp32: the pair's float build against the fp64
+    oracle at the fp32 fraction bound (qpos 1e-5 / qvel 1e-3 on >= 99.9% of env-steps)."""
     monkeypatch.setenv("BB_ROUTE", "0")  # read by bb_create: relief banks always take the pair
     from ballbot_gym.envs import BallbotVecEnv
 
     n = 256
-    env = BallbotVecEnv(n, device="cuda:0", seed=3, terrain_config={"type": "perlin", "config": {}},
-                        n_terrains=None, stream_seeds=[300 + i for i in range(n)])
+    tol = TOL if precision == "fp64" else TOL32
+    kw = (dict(n_terrains=None, stream_seeds=[300 + i for i in range(n)]) if terrain == "perlin"
+          else dict(n_terrains=8, shared_stream=True))
+    env = BallbotVecEnv(n, device="cuda:0", seed=3, terrain_config={"type": terrain, "config": {}},
+                        precision=precision, **kw)
     size_z = float(env.terrain_plan.size_z)
     g = torch.Generator(device="cuda:0").manual_seed(11)
     # burn-in through the pair: the robots drop onto their terrains, balance, fall, topple
@@ -36,7 +50,7 @@ def test_relief_pair_teacher_forced_vs_oracle(oracle, monkeypatch):
         env.step_multi(torch.rand(32, n, 3, generator=g, device="cuda:0") * 2 - 1)
     cfg = oracle.default_cfg()
     fields = {}
-    bad = total = full_steps = 0
+    bad = total = full_steps = big = 0
     worst = dict(q=0.0, v=0.0, obs=0.0, r=0.0)
     s0 = env.stats()
     for t in range(48):
@@ -64,18 +78,26 @@ def test_relief_pair_teacher_forced_vs_oracle(oracle, monkeypatch):
             eq, ev = float(np.abs(q1[e] - qe).max()), float(np.abs(v1[e] - ve).max())
             eo, er = float(np.abs(obs[e] - o).max()), abs(float(rew[e]) - r)
             total += 1
-            bad += not (eq <= TOL["q"] and ev <= TOL["v"] and eo <= TOL["obs"] and er <= TOL["r"])
+            bad += not (eq <= tol["q"] and ev <= tol["v"] and eo <= tol["obs"] and er <= tol["r"])
             for k, x in (("q", eq), ("v", ev), ("obs", eo), ("r", er)):
                 worst[k] = max(worst[k], x)
-            assert ev <= TOL["vmax"], (t, e, ev)
+            big += ev > tol["v"] * 10
+            assert tol["vmax"] is None or ev <= tol["vmax"], (t, e, ev)
     st = env.stats()
     env.check()
     env.close()
-    print(f"\nrelief pair teacher-forced: {total} env-steps on {len(fields)} perlin terrains, {bad} outside "
-          f"tolerance, worst {worst}, full-loop steps {full_steps}, slow path {st['slow_path'] - s0['slow_path']}")
-    assert bad <= TOL["max_bad"], (bad, total, worst)
-    assert total >= 48 * n // 2 and len(fields) >= n // 2
-    assert full_steps > 0 and st["slow_path"] > s0["slow_path"]  # the pair's full loop stepped envs
+    print(f"\nrelief pair teacher-forced ({terrain}, {precision}): {total} env-steps on {len(fields)} terrains, {bad} "
+          f"outside tolerance ({big} beyond 10x qvel), worst {worst}, full-loop steps {full_steps}, slow path "
+          f"{st['slow_path'] - s0['slow_path']}")
+    if "max_bad" in tol:
+        assert bad <= tol["max_bad"], (bad, total, worst)
+    else:
+        assert bad <= (1.0 - tol["frac"]) * total, (bad, total, worst)
+    assert total >= 48 * n // 2
+    if terrain == "perlin":
+        assert len(fields) >= n // 2
+    if terrain == "perlin":  # rough terrain: the pair's full loop stepped envs (hills: rarely, robots stay central)
+        assert full_steps > 0 and st["slow_path"] > s0["slow_path"]
     assert st["pair_budget"] == 0
 
 
