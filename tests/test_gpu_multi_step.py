@@ -251,3 +251,21 @@ def test_multi_step_rejects_bad_shapes():
     with pytest.raises(ValueError):
         env.step_multi(torch.zeros(64, 3, device="cuda:0"))
     env.close()
+
+
+@pytest.mark.parametrize("n", [1, 3, 17, 65])
+@pytest.mark.parametrize("terrain,route", [("flat", "1"), ("perlin", "0")])
+def test_ragged_env_counts(n, terrain, route, monkeypatch):
+    """Env counts that fill no wave, workgroup or XCD label evenly (1: the reference's single env;
+    3, 17, 65: partial teams, partial 32-env output blocks, labels without envs -- on perlin the
+    relief pair's rings of the empty labels must still drain): bb_step_multi equals one bb_step
+    per step bit for bit, with auto-resets."""
+    kw = {"max_ep_steps": 20} if terrain == "flat" else {"n_terrains": None, "max_ep_steps": 60,
+                                                         "stream_seeds": [40 + i for i in range(n)]}
+    a, b = _pair(n, terrain, monkeypatch, route=route, **kw)
+    g = torch.Generator(device="cuda:0").manual_seed(3 + n)
+    actions = torch.rand(96, n, 3, generator=g, device="cuda:0") * 4 - 2
+    st = _compare_runs(a, b, actions, 32)
+    assert st["resets"] >= 1 and st["pair_budget"] == 0
+    b.check()
+    a.close(), b.close()
